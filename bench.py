@@ -1,0 +1,168 @@
+#!/usr/bin/env python
+"""North-star benchmark: ResNet-50 training images/sec on MI355X (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W [--batch 256] [--impl dtf|torch]
+
+For N > 1 run under ``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N``
+(one process per GPU, RCCL over xGMI).  Each rank trains on its own synthetic ImageNet-shaped
+batch (weak scaling: per-GPU batch fixed); the timed region is exactly K full training steps
+(forward, backward, overlapped bucketed all-reduce, fused SGD-momentum update) bracketed by a
+barrier + device synchronize on both sides; the MAX elapsed time over ranks is reported.
+
+``--impl dtf``   (default) this framework: hand-written HIP kernels, MirroredStrategy.
+``--impl torch`` the stock PyTorch-ROCm comparator (MIOpen convs, DDP) on the same data.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec (whole node) ResNet-50 synthetic ImageNet at 1/2/4/8 MI355X"
+BASELINE_VALUE = None   # the reference publishes no ResNet-50 number
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    p.add_argument("--impl", choices=("dtf", "torch"), default="dtf")
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--bucket-mb", type=float, default=64)
+    p.add_argument("--profile-steps", type=int, default=0)
+    return p.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build_dtf(args, dev):
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.models import resnet50
+    from distributedtensorflow_amd.optimizers import MomentumOptimizer
+    from distributedtensorflow_amd.parallel import MirroredStrategy
+    from distributedtensorflow_amd.train import get_or_create_global_step
+
+    strategy = MirroredStrategy(bucket_mb=args.bucket_mb)
+    with strategy.scope():
+        model = resnet50()
+        model.train()
+        opt = MomentumOptimizer(args.lr, momentum=0.9, weight_decay=1e-4)
+        gstep = get_or_create_global_step()
+        opt.build(list(model.parameters()))
+
+    def step(images, labels):
+        logits = model(images)
+        loss = ops.sparse_softmax_cross_entropy(logits, labels)
+        opt.minimize(loss, global_step=gstep)
+        return loss
+
+    return step, strategy
+
+
+def build_torch(args, dev):
+    from distributedtensorflow_amd.utils.torch_baseline import TorchResNet50
+    model = TorchResNet50().to(dev).to(memory_format=torch.channels_last)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
+                                                          bucket_cap_mb=args.bucket_mb)
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=1e-4,
+                          foreach=True)
+    lossf = torch.nn.CrossEntropyLoss()
+
+    def step(images, labels):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(images)
+            loss = lossf(out.float(), labels)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    return step, None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1 and not dist.is_initialized():
+        from distributedtensorflow_amd.parallel import init_process_group_from_env
+        init_process_group_from_env("nccl")
+    torch.backends.cudnn.benchmark = True
+
+    B, S = args.batch, args.image_size
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    if args.impl == "dtf":
+        step, _ = build_dtf(args, dev)
+        images = torch.randn(B, S, S, 3, device=dev, generator=g).to(torch.bfloat16)  # NHWC
+    else:
+        step, _ = build_torch(args, dev)
+        images = torch.randn(B, 3, S, S, device=dev, generator=g).contiguous(
+            memory_format=torch.channels_last)
+    labels = torch.randint(0, 1000, (B,), device=dev, generator=g)
+
+    def sync():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    t0 = time.time()
+    for i in range(args.warmup):
+        loss = step(images, labels)
+    sync()
+    log(f"warmup {args.warmup} steps in {time.time() - t0:.1f}s, loss={float(loss):.4f}")
+
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(images, labels)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss)
+    ms = elapsed / args.steps * 1000
+    ips = B * world * args.steps / elapsed
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": round(ips, 2), "unit": "images/sec",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": (round(ips / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+            "dtype": "bf16", "data": "synthetic (random NHWC 224x224x3 images, random labels; "
+                                      "random-init weights)",
+            "config": {"model": "resnet50", "global_batch": B * world, "per_gpu_batch": B,
+                       "seq_len": None, "image_size": S, "parallelism": f"dp{world}",
+                       "impl": args.impl, "optimizer": "momentum0.9+wd1e-4",
+                       "final_loss": round(final_loss, 4)},
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,306 @@
+// Fused BatchNorm (+residual add) (+ReLU), NHWC bf16 activations, fp32 statistics.
+//
+// ResNet-50 runs BN after every conv.  The channel axis is innermost (NHWC),
+// so one row of M = N*H*W rows holds all C channels contiguously: each lane owns 8 channels
+// (one 16-B load) and a block sweeps a contiguous chunk of rows.  Per-channel reductions
+// cross workgroups (and therefore XCDs, whose L2s are not coherent), so they are done the
+// placement-independent way: per-block partial slabs written with plain stores, combined by a
+// SEPARATE finalize launch (the kernel boundary is the release/acquire; cdna_hip_programming.md
+// §5 "combine in the NEXT kernel's prologue").  Partial combination is in fp64.
+//
+// Forward (training):  stats -> finalize(mean, invstd, scale, shift, moving averages) -> apply
+// Backward:            reduce(sum dz, sum dz*xhat) -> finalize(dgamma, dbeta, coefs) -> apply
+//   with dz = dy * (y > 0) when ReLU was fused, and dx = A*dz + B*x + C per channel.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+// rows handled by one block: big enough to amortise the partial slab, small enough to give
+// >= ~1024 blocks on ResNet-50's large layers (M = 256*112*112 = 3.2M rows).
+inline int stats_grid(long M, int C, int* rows_per_block) {
+  const int tpr = C / 8;                        // threads per row
+  const int rpi = kThreads / tpr;               // rows per block iteration
+  long target_blocks = 1024;
+  long rpb = (M + target_blocks - 1) / target_blocks;
+  rpb = ((rpb + rpi - 1) / rpi) * rpi;
+  if (rpb < rpi) rpb = rpi;
+  *rows_per_block = (int)rpb;
+  return (int)((M + rpb - 1) / rpb);
+}
+
+// MODE 0: forward stats   acc0 += x,           acc1 += x*x
+// MODE 1: backward reduce acc0 += dz,          acc1 += dz*(x-mean)*invstd
+template <int MODE>
+__global__ void __launch_bounds__(kThreads)
+bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                 const bf16_t* __restrict__ y, const float* __restrict__ mean,
+                 const float* __restrict__ invstd, long M, int C, int rows_per_block, int relu,
+                 float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float red[];   // [rpi][2][C]
+  const int tpr = C >> 3;
+  const int rpi = kThreads / tpr;
+  const int tid = threadIdx.x;
+  const int cg = tid % tpr, ro = tid / tpr;
+  const bool active = ro < rpi;
+  float a0[8], a1[8], mu[8], is[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { a0[i] = 0.f; a1[i] = 0.f; }
+  if (MODE == 1 && active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { mu[i] = mean[cg * 8 + i]; is[i] = invstd[cg * 8 + i]; }
+  }
+  const long m0 = (long)blockIdx.x * rows_per_block;
+  long m1 = m0 + rows_per_block;
+  if (m1 > M) m1 = M;
+  if (active) {
+    for (long m = m0 + ro; m < m1; m += rpi) {
+      const long off = m * C + cg * 8;
+      float xv[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
+      if (MODE == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { a0[i] += xv[i]; a1[i] += xv[i] * xv[i]; }
+      } else {
+        float g[8];
+        unpack8(*reinterpret_cast<const uint4*>(dy + off), g);
+        if (relu) {
+          float yv[8];
+          unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { a0[i] += g[i]; a1[i] += g[i] * (xv[i] - mu[i]) * is[i]; }
+      }
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[(ro * 2 + 0) * C + cg * 8 + i] = a0[i];
+      red[(ro * 2 + 1) * C + cg * 8 + i] = a1[i];
+    }
+  }
+  __syncthreads();
+  // tree-free final sum: thread t reduces channel-slot t over the rpi row groups
+  for (int idx = tid; idx < 2 * C; idx += kThreads) {
+    const int which = idx / C, c = idx % C;
+    float s = 0.f;
+    for (int r = 0; r < rpi; ++r) s += red[(r * 2 + which) * C + c];
+    partial[((long)blockIdx.x * 2 + which) * C + c] = s;
+  }
+}
+
+__global__ void bn_fwd_finalize_kernel(const float* __restrict__ partial, int G, int C, long M,
+                                       const float* __restrict__ gamma,
+                                       const float* __restrict__ beta,
+                                       float* __restrict__ run_mean, float* __restrict__ run_var,
+                                       float momentum, float eps, float* __restrict__ mean,
+                                       float* __restrict__ invstd, float* __restrict__ scale,
+                                       float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, ss = 0.0;
+  for (int g = 0; g < G; ++g) {
+    s += partial[((long)g * 2 + 0) * C + c];
+    ss += partial[((long)g * 2 + 1) * C + c];
+  }
+  const double mu = s / (double)M;
+  double var = ss / (double)M - mu * mu;
+  if (var < 0) var = 0;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  mean[c] = (float)mu;
+  invstd[c] = is;
+  const float sc = gamma[c] * is;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mu * sc;
+  if (run_mean) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    run_mean[c] = run_mean[c] * momentum + (float)mu * (1.f - momentum);
+    run_var[c] = run_var[c] * momentum + (float)unb * (1.f - momentum);
+  }
+}
+
+__global__ void bn_infer_finalize_kernel(int C, const float* __restrict__ gamma,
+                                         const float* __restrict__ beta,
+                                         const float* __restrict__ run_mean,
+                                         const float* __restrict__ run_var, float eps,
+                                         float* __restrict__ mean, float* __restrict__ invstd,
+                                         float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = rsqrtf(run_var[c] + eps);
+  mean[c] = run_mean[c];
+  invstd[c] = is;
+  scale[c] = gamma[c] * is;
+  shift[c] = beta[c] - run_mean[c] * gamma[c] * is;
+}
+
+__global__ void __launch_bounds__(kThreads)
+bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                bf16_t* __restrict__ y, const float* __restrict__ scale,
+                const float* __restrict__ shift, long nvec, int C, int relu) {
+  const int tpr = C >> 3;
+  for (long v = (long)blockIdx.x * kThreads + threadIdx.x; v < nvec;
+       v += (long)gridDim.x * kThreads) {
+    const int cg = (int)(v % tpr);
+    float xv[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[v], xv);
+    const float4 s0 = reinterpret_cast<const float4*>(scale)[cg * 2];
+    const float4 s1 = reinterpret_cast<const float4*>(scale)[cg * 2 + 1];
+    const float4 h0 = reinterpret_cast<const float4*>(shift)[cg * 2];
+    const float4 h1 = reinterpret_cast<const float4*>(shift)[cg * 2 + 1];
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = xv[i] * sc[i] + sh[i];
+    if (res) {
+      float r[8];
+      unpack8(reinterpret_cast<const uint4*>(res)[v], r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] += r[i];
+    }
+    if (relu) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = fmaxf(o[i], 0.f);
+    }
+    reinterpret_cast<uint4*>(y)[v] = pack8(o);
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int G, int C, long M,
+                                       const float* __restrict__ gamma,
+                                       const float* __restrict__ mean,
+                                       const float* __restrict__ invstd,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ coefA, float* __restrict__ coefB,
+                                       float* __restrict__ coefC, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sdz = 0.0, sdzx = 0.0;
+  for (int g = 0; g < G; ++g) {
+    sdz += partial[((long)g * 2 + 0) * C + c];
+    sdzx += partial[((long)g * 2 + 1) * C + c];
+  }
+  const float db = (float)sdz, dg = (float)sdzx;
+  if (accumulate) { dgamma[c] += dg; dbeta[c] += db; }
+  else { dgamma[c] = dg; dbeta[c] = db; }
+  const float is = invstd[c];
+  const float k = gamma[c] * is;
+  const float invM = 1.f / (float)M;
+  const float B = -k * is * dg * invM;
+  coefA[c] = k;
+  coefB[c] = B;
+  coefC[c] = -k * db * invM - B * mean[c];
+}
+
+__global__ void __launch_bounds__(kThreads)
+bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                    const bf16_t* __restrict__ x, const float* __restrict__ cA,
+                    const float* __restrict__ cB, const float* __restrict__ cC,
+                    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long nvec, int C,
+                    int relu) {
+  const int tpr = C >> 3;
+  for (long v = (long)blockIdx.x * kThreads + threadIdx.x; v < nvec;
+       v += (long)gridDim.x * kThreads) {
+    const int cg = (int)(v % tpr);
+    float g[8], xv[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[v], g);
+    if (relu) {
+      float yv[8];
+      unpack8(reinterpret_cast<const uint4*>(y)[v], yv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+    }
+    if (dres) reinterpret_cast<uint4*>(dres)[v] = pack8(g);
+    unpack8(reinterpret_cast<const uint4*>(x)[v], xv);
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = cg * 8 + i;
+      o[i] = cA[c] * g[i] + cB[c] * xv[i] + cC[c];
+    }
+    reinterpret_cast<uint4*>(dx)[v] = pack8(o);
+  }
+}
+
+inline int ew_grid(long nvec) {
+  long g = (nvec + kThreads - 1) / kThreads;
+  if (g > 256 * 16) g = 256 * 16;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers (host)
+int dtf_bn_partial_blocks(long M, int C) {
+  int rpb;
+  return stats_grid(M, C, &rpb);
+}
+
+void dtf_bn_fwd_stats(const bf16_t* x, long M, int C, float* partial, hipStream_t st) {
+  int rpb;
+  const int G = stats_grid(M, C, &rpb);
+  const int rpi = kThreads / (C / 8);
+  const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
+  hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(G), dim3(kThreads), lds, st, x, nullptr, nullptr,
+                     nullptr, nullptr, M, C, rpb, 0, partial);
+}
+
+void dtf_bn_fwd_finalize(const float* partial, long M, int C, const float* gamma,
+                         const float* beta, float* run_mean, float* run_var, float momentum,
+                         float eps, float* mean, float* invstd, float* scale, float* shift,
+                         hipStream_t st) {
+  int rpb;
+  const int G = stats_grid(M, C, &rpb);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, partial, G,
+                     C, M, gamma, beta, run_mean, run_var, momentum, eps, mean, invstd, scale,
+                     shift);
+}
+
+void dtf_bn_infer_finalize(int C, const float* gamma, const float* beta, const float* run_mean,
+                           const float* run_var, float eps, float* mean, float* invstd,
+                           float* scale, float* shift, hipStream_t st) {
+  hipLaunchKernelGGL(bn_infer_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma,
+                     beta, run_mean, run_var, eps, mean, invstd, scale, shift);
+}
+
+void dtf_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* scale,
+                  const float* shift, long M, int C, int relu, hipStream_t st) {
+  const long nvec = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(kThreads), 0, st, x, res, y, scale,
+                     shift, nvec, C, relu);
+}
+
+void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
+                       const float* invstd, long M, int C, int relu, float* partial,
+                       hipStream_t st) {
+  int rpb;
+  const int G = stats_grid(M, C, &rpb);
+  const int rpi = kThreads / (C / 8);
+  const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
+  hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(G), dim3(kThreads), lds, st, x, dy, y, mean, invstd,
+                     M, C, rpb, relu, partial);
+}
+
+void dtf_bn_bwd_finalize(const float* partial, long M, int C, const float* gamma,
+                         const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                         float* coefA, float* coefB, float* coefC, int accumulate,
+                         hipStream_t st) {
+  int rpb;
+  const int G = stats_grid(M, C, &rpb);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, partial, G, C,
+                     M, gamma, mean, invstd, dgamma, dbeta, coefA, coefB, coefC, accumulate);
+}
+
+void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* cA,
+                      const float* cB, const float* cC, bf16_t* dx, bf16_t* dres, long M, int C,
+                      int relu, hipStream_t st) {
+  const long nvec = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(kThreads), 0, st, dy, y, x, cA,
+                     cB, cC, dx, dres, nvec, C, relu);
+}

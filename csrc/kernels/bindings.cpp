@@ -1,0 +1,222 @@
+// pybind11 module `_dtf_hip`: thin launch entry points for the HIP kernels.
+// Arguments are raw device addresses (tensor.data_ptr()) and the hipStream_t of the caller's
+// current torch stream, so every launch is ordered on torch's stream (and captured into a
+// hipGraph when torch is capturing).  Shape validation lives in distributedtensorflow_amd/ops/native.py;
+// the launchers re-check the invariants their kernels index with.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace py = pybind11;
+
+#define DTF_MAX_TAPS 64
+struct TapTable { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
+struct TapTableW { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
+struct ConvGeom { int N, H, W, C, P, Q, sh, sw, Kout, Kpad, Ho, Wo, osh, osw, oh0, ow0; };
+struct WgradGeom { int N, H, W, C, P, Q, sh, sw, Kout, ldw; long m_per_split; };
+
+// ---- launchers defined in the .hip translation units
+int dtf_bn_partial_blocks(long M, int C);
+void dtf_bn_fwd_stats(const bf16_t*, long, int, float*, hipStream_t);
+void dtf_bn_fwd_finalize(const float*, long, int, const float*, const float*, float*, float*,
+                         float, float, float*, float*, float*, float*, hipStream_t);
+void dtf_bn_infer_finalize(int, const float*, const float*, const float*, const float*, float,
+                           float*, float*, float*, float*, hipStream_t);
+void dtf_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, const float*, const float*, long, int,
+                  int, hipStream_t);
+void dtf_bn_bwd_reduce(const bf16_t*, const bf16_t*, const bf16_t*, const float*, const float*,
+                       long, int, int, float*, hipStream_t);
+void dtf_bn_bwd_finalize(const float*, long, int, const float*, const float*, const float*,
+                         float*, float*, float*, float*, float*, int, hipStream_t);
+void dtf_bn_bwd_apply(const bf16_t*, const bf16_t*, const bf16_t*, const float*, const float*,
+                      const float*, bf16_t*, bf16_t*, long, int, int, hipStream_t);
+void dtf_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int,
+                     int, int, int, int, hipStream_t);
+void dtf_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int,
+                     int, int, int, int, int, hipStream_t);
+void dtf_gap_fwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
+void dtf_gap_bwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
+void dtf_softmax_xent(const float*, const void*, int, int, int, float*, float*, float,
+                      hipStream_t);
+void dtf_sgd_momentum(float*, const float*, float*, bf16_t*, long, const float*, float, float,
+                      float, int, int*, hipStream_t);
+void dtf_adam(float*, const float*, float*, float*, bf16_t*, long, const float*, float, float,
+              float, float, float, int*, hipStream_t);
+void dtf_adagrad(float*, const float*, float*, bf16_t*, long, const float*, float, int*,
+                 hipStream_t);
+void dtf_lamb(float*, float*, float*, float*, bf16_t*, const void*, int, const float*,
+              const float*, float, float, float, const float*, float, float*, int*, hipStream_t);
+int dtf_lamb_chunk_bytes();
+void dtf_sumsq(const float*, long, float*, hipStream_t);
+void dtf_cast_f32_bf16(const float*, bf16_t*, long, hipStream_t);
+void dtf_conv_igemm(const bf16_t*, const bf16_t*, bf16_t*, const ConvGeom&, const TapTable&, int,
+                    hipStream_t);
+void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, WgradGeom, const TapTableW&,
+                    hipStream_t);
+int dtf_conv_wgrad_splits(long, int, int);
+
+template <typename T>
+static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename TT>
+static TT make_taps(const std::vector<int>& dh, const std::vector<int>& dw) {
+  if (dh.size() != dw.size() || dh.empty() || dh.size() > DTF_MAX_TAPS)
+    throw std::runtime_error("bad tap table");
+  TT t{};
+  t.n = (int)dh.size();
+  for (size_t i = 0; i < dh.size(); ++i) { t.dh[i] = dh[i]; t.dw[i] = dw[i]; }
+  return t;
+}
+
+PYBIND11_MODULE(_dtf_hip, m) {
+  m.doc() = "distributedtensorflow_amd HIP/CDNA4 kernels (gfx950)";
+
+  m.def("bn_partial_blocks", &dtf_bn_partial_blocks);
+  m.def("bn_fwd_stats", [](uintptr_t x, long M, int C, uintptr_t part, uintptr_t st) {
+    dtf_bn_fwd_stats(P<const bf16_t>(x), M, C, P<float>(part), S(st));
+    check_launch("bn_fwd_stats");
+  });
+  m.def("bn_fwd_finalize", [](uintptr_t part, long M, int C, uintptr_t gamma, uintptr_t beta,
+                              uintptr_t rm, uintptr_t rv, float mom, float eps, uintptr_t mean,
+                              uintptr_t invstd, uintptr_t scale, uintptr_t shift, uintptr_t st) {
+    dtf_bn_fwd_finalize(P<const float>(part), M, C, P<const float>(gamma), P<const float>(beta),
+                        P<float>(rm), P<float>(rv), mom, eps, P<float>(mean), P<float>(invstd),
+                        P<float>(scale), P<float>(shift), S(st));
+    check_launch("bn_fwd_finalize");
+  });
+  m.def("bn_infer_finalize", [](int C, uintptr_t gamma, uintptr_t beta, uintptr_t rm,
+                                uintptr_t rv, float eps, uintptr_t mean, uintptr_t invstd,
+                                uintptr_t scale, uintptr_t shift, uintptr_t st) {
+    dtf_bn_infer_finalize(C, P<const float>(gamma), P<const float>(beta), P<const float>(rm),
+                          P<const float>(rv), eps, P<float>(mean), P<float>(invstd),
+                          P<float>(scale), P<float>(shift), S(st));
+    check_launch("bn_infer_finalize");
+  });
+  m.def("bn_apply", [](uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t scale, uintptr_t shift,
+                       long M, int C, int relu, uintptr_t st) {
+    dtf_bn_apply(P<const bf16_t>(x), P<const bf16_t>(res), P<bf16_t>(y), P<const float>(scale),
+                 P<const float>(shift), M, C, relu, S(st));
+    check_launch("bn_apply");
+  });
+  m.def("bn_bwd_reduce", [](uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t mean,
+                            uintptr_t invstd, long M, int C, int relu, uintptr_t part,
+                            uintptr_t st) {
+    dtf_bn_bwd_reduce(P<const bf16_t>(dy), P<const bf16_t>(y), P<const bf16_t>(x),
+                      P<const float>(mean), P<const float>(invstd), M, C, relu, P<float>(part),
+                      S(st));
+    check_launch("bn_bwd_reduce");
+  });
+  m.def("bn_bwd_finalize", [](uintptr_t part, long M, int C, uintptr_t gamma, uintptr_t mean,
+                              uintptr_t invstd, uintptr_t dg, uintptr_t db, uintptr_t a,
+                              uintptr_t b, uintptr_t c, int accumulate, uintptr_t st) {
+    dtf_bn_bwd_finalize(P<const float>(part), M, C, P<const float>(gamma), P<const float>(mean),
+                        P<const float>(invstd), P<float>(dg), P<float>(db), P<float>(a),
+                        P<float>(b), P<float>(c), accumulate, S(st));
+    check_launch("bn_bwd_finalize");
+  });
+  m.def("bn_bwd_apply", [](uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t a, uintptr_t b,
+                           uintptr_t c, uintptr_t dx, uintptr_t dres, long M, int C, int relu,
+                           uintptr_t st) {
+    dtf_bn_bwd_apply(P<const bf16_t>(dy), P<const bf16_t>(y), P<const bf16_t>(x),
+                     P<const float>(a), P<const float>(b), P<const float>(c), P<bf16_t>(dx),
+                     P<bf16_t>(dres), M, C, relu, S(st));
+    check_launch("bn_bwd_apply");
+  });
+  m.def("maxpool_fwd", [](uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W, int C,
+                          int Pp, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
+                          uintptr_t st) {
+    dtf_maxpool_fwd(P<const bf16_t>(x), P<bf16_t>(y), P<uint8_t>(arg), N, H, W, C, Pp, Q, kh, kw,
+                    sh, sw, ph, pw, S(st));
+    check_launch("maxpool_fwd");
+  });
+  m.def("maxpool_bwd", [](uintptr_t dy, uintptr_t arg, uintptr_t dx, int N, int H, int W, int C,
+                          int Pp, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
+                          uintptr_t st) {
+    dtf_maxpool_bwd(P<const bf16_t>(dy), P<const uint8_t>(arg), P<bf16_t>(dx), N, H, W, C, Pp, Q,
+                    kh, kw, sh, sw, ph, pw, S(st));
+    check_launch("maxpool_bwd");
+  });
+  m.def("gap_fwd", [](uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t st) {
+    dtf_gap_fwd(P<const bf16_t>(x), P<bf16_t>(y), N, HW, C, S(st));
+    check_launch("gap_fwd");
+  });
+  m.def("gap_bwd", [](uintptr_t dy, uintptr_t dx, int N, int HW, int C, uintptr_t st) {
+    dtf_gap_bwd(P<const bf16_t>(dy), P<bf16_t>(dx), N, HW, C, S(st));
+    check_launch("gap_bwd");
+  });
+  m.def("softmax_xent", [](uintptr_t logits, uintptr_t labels, int label_bytes, int B, int V,
+                           uintptr_t loss_rows, uintptr_t grad, float gscale, uintptr_t st) {
+    dtf_softmax_xent(P<const float>(logits), P<const void>(labels), label_bytes, B, V,
+                     P<float>(loss_rows), P<float>(grad), gscale, S(st));
+    check_launch("softmax_xent");
+  });
+  m.def("sgd_momentum", [](uintptr_t p, uintptr_t g, uintptr_t a, uintptr_t shadow, long n,
+                           uintptr_t lr, float mom, float wd, float gscale, int nesterov,
+                           uintptr_t nonfinite, uintptr_t st) {
+    dtf_sgd_momentum(P<float>(p), P<const float>(g), P<float>(a), P<bf16_t>(shadow), n,
+                     P<const float>(lr), mom, wd, gscale, nesterov, P<int>(nonfinite), S(st));
+    check_launch("sgd_momentum");
+  });
+  m.def("adam", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t shadow, long n,
+                   uintptr_t lr_t, float b1, float b2, float eps, float wd, float gscale,
+                   uintptr_t nonfinite, uintptr_t st) {
+    dtf_adam(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), P<bf16_t>(shadow), n,
+             P<const float>(lr_t), b1, b2, eps, wd, gscale, P<int>(nonfinite), S(st));
+    check_launch("adam");
+  });
+  m.def("adagrad", [](uintptr_t p, uintptr_t g, uintptr_t acc, uintptr_t shadow, long n,
+                      uintptr_t lr, float gscale, uintptr_t nonfinite, uintptr_t st) {
+    dtf_adagrad(P<float>(p), P<const float>(g), P<float>(acc), P<bf16_t>(shadow), n,
+                P<const float>(lr), gscale, P<int>(nonfinite), S(st));
+    check_launch("adagrad");
+  });
+  m.def("lamb", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t shadow,
+                   uintptr_t chunks, int nchunks, uintptr_t hyper, uintptr_t lr, float b1,
+                   float b2, float eps, uintptr_t wd_seg, float gscale, uintptr_t norms,
+                   uintptr_t nonfinite, uintptr_t st) {
+    dtf_lamb(P<float>(p), P<float>(g), P<float>(mm), P<float>(v), P<bf16_t>(shadow),
+             P<const void>(chunks), nchunks, P<const float>(hyper), P<const float>(lr), b1, b2,
+             eps, P<const float>(wd_seg), gscale, P<float>(norms), P<int>(nonfinite), S(st));
+    check_launch("lamb");
+  });
+  m.def("lamb_chunk_bytes", &dtf_lamb_chunk_bytes);
+  m.def("sumsq", [](uintptr_t x, long n, uintptr_t out, uintptr_t st) {
+    dtf_sumsq(P<const float>(x), n, P<float>(out), S(st));
+    check_launch("sumsq");
+  });
+  m.def("cast_f32_bf16", [](uintptr_t x, uintptr_t y, long n, uintptr_t st) {
+    dtf_cast_f32_bf16(P<const float>(x), P<bf16_t>(y), n, S(st));
+    check_launch("cast_f32_bf16");
+  });
+  m.def("conv_igemm", [](uintptr_t x, uintptr_t w, uintptr_t y, std::vector<int> geom,
+                         std::vector<int> dh, std::vector<int> dw, int bk, uintptr_t st) {
+    if (geom.size() != 16) throw std::runtime_error("conv_igemm: geom needs 16 ints");
+    ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
+               geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15]};
+    dtf_conv_igemm(P<const bf16_t>(x), P<const bf16_t>(w), P<bf16_t>(y), g,
+                   make_taps<TapTable>(dh, dw), bk, S(st));
+    check_launch("conv_igemm");
+  });
+  m.def("conv_wgrad", [](uintptr_t x, uintptr_t dy, uintptr_t dw_out, std::vector<int> geom,
+                         std::vector<int> dh, std::vector<int> dw, uintptr_t st) {
+    if (geom.size() != 10) throw std::runtime_error("conv_wgrad: geom needs 10 ints");
+    WgradGeom g{geom[0], geom[1], geom[2], geom[3], geom[4], geom[5], geom[6], geom[7], geom[8],
+                geom[9], 0};
+    dtf_conv_wgrad(P<const bf16_t>(x), P<const bf16_t>(dy), P<float>(dw_out), g,
+                   make_taps<TapTableW>(dh, dw), S(st));
+    check_launch("conv_wgrad");
+  });
+  m.def("conv_wgrad_splits", &dtf_conv_wgrad_splits);
+}

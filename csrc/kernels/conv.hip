@@ -1,0 +1,283 @@
+// Implicit-GEMM convolution on MFMA (gfx950), NHWC bf16, fp32 accumulate.
+//
+//   Y[m, k] = sum_{t, c} X[n(m), h(m,t), w(m,t), c] * Wt[k, t*C + c]
+//
+// "Tap table" formulation: an output grid (N, P, Q) and a list of T taps (dh_t, dw_t); output
+// pixel (n,p,q) reads input pixel (p*sh + dh_t, q*sw + dw_t) for tap t (zero outside the image)
+// and is stored at Y[n, p*osh + oh0, q*osw + ow0, :] of an [N, Ho, Wo, Kout] tensor.
+//   * forward:              taps = {(r - pad_h, s - pad_w)}, (osh,osw,oh0,ow0) = (1,1,0,0)
+//   * data-grad, stride 1:  forward conv of dY with the spatially flipped, C<->K transposed
+//                           filter and taps {(pad_h - r', ...)}
+//   * data-grad, stride s:  one launch per output phase class (a, b) in [0,s)^2 with the taps
+//                           that hit that class; osh = osw = s, (oh0, ow0) = (a, b)
+// so one MFMA kernel serves SURVEY.md K3/K5/N-K1 forward and dgrad.
+//
+// Tiling (cdna_hip_programming.md §5, "step-3"-style 2-stage pipeline):
+//   block = 256 threads = 4 waves in WAVES_M x WAVES_N, wave tile 64x64 built from 4x4
+//   v_mfma_f32_16x16x32_bf16 tiles (16x16x32 holds a higher clock than 32x32x16 under load:
+//   MI355X_MICROARCH.md "DVFS give-back" (7)).
+//   K-step BK = 64 (C % 64 == 0) or 32 (C % 32 == 0); each (row, tap) supplies BK contiguous
+//   channels = one 128-B / 64-B line per output row, loaded 16 B per lane.
+//   Register staging with the T14 split: next tile's global loads are issued before the MFMAs
+//   of the current tile and written to the other LDS buffer after them; one barrier per K-step.
+//   LDS rows are XOR-swizzled by 16-B chunk so ds_read_b128 fragment reads of 16 different rows
+//   are conflict-free (T2).
+//   Epilogue: accumulators -> bf16 -> LDS -> 16-B coalesced global stores (T21 in spirit).
+//   Tile order: XCD-aware bijective remap of the block id, N-tile fastest so blocks sharing an
+//   A panel run on the same XCD's L2 (T1).
+//   GENERIC=true: per-element gather for C % 32 != 0 (stem 7x7x3, MNIST conv 5x5x1).
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+
+#define DTF_MAX_TAPS 64
+
+struct TapTable {
+  int n;
+  int dh[DTF_MAX_TAPS];
+  int dw[DTF_MAX_TAPS];
+};
+
+struct ConvGeom {
+  int N, H, W, C;        // input
+  int P, Q;              // output grid of this launch
+  int sh, sw;            // input stride
+  int Kout;              // output channels (GEMM N)
+  int Kpad;              // filter row stride (T*C rounded up to BK)
+  int Ho, Wo;            // output tensor spatial dims
+  int osh, osw, oh0, ow0;// output placement
+};
+
+namespace {
+
+constexpr int kThreads = 256;
+
+template <int BK>
+DTF_DEV int swz_chunk(int row, int chunk) {
+  constexpr int CPR = BK / 8;           // 16-B chunks per row
+  constexpr int RPB = 16 / CPR;         // rows per 256-B bank row
+  return chunk ^ ((row / RPB) % CPR);
+}
+
+template <int WAVES_M, int WAVES_N, int BK, bool GENERIC>
+__global__ void __launch_bounds__(kThreads, 2)
+conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+                  bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps) {
+  constexpr int BM = 64 * WAVES_M, BN = 64 * WAVES_N;
+  constexpr int CPR = BK / 8;                            // chunks per row
+  constexpr int A_CHUNKS = BM * CPR / kThreads;          // 16-B loads per thread for A
+  constexpr int B_CHUNKS = BN * CPR / kThreads;
+  constexpr int ROWS_PER_PASS = kThreads / CPR;
+  constexpr int STAGE_ELEMS = (BM + BN) * BK;            // bf16 elements per LDS stage
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+
+  const long M = (long)g.N * g.P * g.Q;
+  const int tiles_n = (g.Kout + BN - 1) / BN;
+  const int tiles_m = (int)((M + BM - 1) / BM);
+  const int nwg = tiles_n * tiles_m;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+
+  const int K = taps.n * g.C;
+  const int nk = (K + BK - 1) / BK;
+
+  // ---- per-thread A rows: decode (n, p, q) once
+  const int chunk = tid % CPR;
+  int a_nbase[A_CHUNKS], a_h[A_CHUNKS], a_w[A_CHUNKS];
+  bool a_ok[A_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < A_CHUNKS; ++i) {
+    const long m = m0 + tid / CPR + i * ROWS_PER_PASS;
+    a_ok[i] = m < M;
+    const long mm = a_ok[i] ? m : 0;
+    const int q = (int)(mm % g.Q);
+    const long t = mm / g.Q;
+    const int p = (int)(t % g.P);
+    const int n = (int)(t / g.P);
+    a_nbase[i] = n;
+    a_h[i] = p * g.sh;
+    a_w[i] = q * g.sw;
+  }
+
+  uint4 ra[A_CHUNKS], rb[B_CHUNKS];
+
+  auto load_stage = [&](int kt) {
+    const int k0 = kt * BK;
+    if constexpr (!GENERIC) {
+      const int t = k0 / g.C;
+      const int c0 = k0 - t * g.C + chunk * 8;
+      const int dh = taps.dh[t], dw = taps.dw[t];
+#pragma unroll
+      for (int i = 0; i < A_CHUNKS; ++i) {
+        const int h = a_h[i] + dh, w = a_w[i] + dw;
+        if (a_ok[i] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W) {
+          const long off = (((long)a_nbase[i] * g.H + h) * g.W + w) * g.C + c0;
+          ra[i] = *reinterpret_cast<const uint4*>(X + off);
+        } else {
+          ra[i] = make_uint4(0, 0, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_CHUNKS; ++i) {
+        uint32_t wv[4];
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          uint32_t pair = 0;
+#pragma unroll
+          for (int e1 = 0; e1 < 2; ++e1) {
+            const int k = k0 + chunk * 8 + e2 * 2 + e1;
+            uint32_t v = 0;
+            if (k < K && a_ok[i]) {
+              const int t = k / g.C, c = k - t * g.C;
+              const int h = a_h[i] + taps.dh[t], w = a_w[i] + taps.dw[t];
+              if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
+                v = X[(((long)a_nbase[i] * g.H + h) * g.W + w) * g.C + c];
+            }
+            pair |= v << (16 * e1);
+          }
+          wv[e2] = pair;
+        }
+        ra[i] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_CHUNKS; ++i) {
+      const int nrow = n0 + tid / CPR + i * ROWS_PER_PASS;
+      if (nrow < g.Kout)
+        rb[i] = *reinterpret_cast<const uint4*>(Wt + (long)nrow * g.Kpad + k0 + chunk * 8);
+      else
+        rb[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  auto store_stage = [&](int buf) {
+    bf16_t* sa = lds + buf * STAGE_ELEMS;
+    bf16_t* sb = sa + BM * BK;
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) {
+      const int r = tid / CPR + i * ROWS_PER_PASS;
+      *reinterpret_cast<uint4*>(sa + r * BK + swz_chunk<BK>(r, chunk) * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CHUNKS; ++i) {
+      const int r = tid / CPR + i * ROWS_PER_PASS;
+      *reinterpret_cast<uint4*>(sb + r * BK + swz_chunk<BK>(r, chunk) * 8) = rb[i];
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+
+  const int frow = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_stage(kt + 1);
+    const bf16_t* sa = lds + cur * STAGE_ELEMS;
+    const bf16_t* sb = sa + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8_t af[4], bfr[4];
+      const int ch = ks * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + frow;
+        af[i] = *reinterpret_cast<const bf16x8_t*>(sa + r * BK + swz_chunk<BK>(r, ch) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wn * 64 + j * 16 + frow;
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + swz_chunk<BK>(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_stage(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: acc -> bf16 LDS tile [BM][BN + 8] -> coalesced 16-B stores
+  constexpr int LDC = BN + 8;
+  bf16_t* st = lds;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + i * 16 + fq * 4 + r;
+        const int col = wn * 64 + j * 16 + frow;
+        st[row * LDC + col] = f2bf(acc[i][j][r]);
+      }
+  __syncthreads();
+  constexpr int OCPR = BN / 8;                 // 16-B chunks per output row
+  constexpr int OROWS = kThreads / OCPR;
+  const int oc = tid % OCPR;
+  const bool col_ok = n0 + oc * 8 < g.Kout;
+  for (int r = tid / OCPR; r < BM; r += OROWS) {
+    const long m = m0 + r;
+    if (m >= M || !col_ok) continue;
+    const int q = (int)(m % g.Q);
+    const long t = m / g.Q;
+    const int p = (int)(t % g.P);
+    const int n = (int)(t / g.P);
+    const int ho = p * g.osh + g.oh0, wo = q * g.osw + g.ow0;
+    const long off = (((long)n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8;
+    *reinterpret_cast<uint4*>(Y + off) = *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
+  }
+}
+
+template <int WM, int WN, int BK, bool GEN>
+void launch_cfg(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
+                const TapTable& taps, hipStream_t st) {
+  constexpr int BM = 64 * WM, BN = 64 * WN;
+  const long M = (long)g.N * g.P * g.Q;
+  const long tiles = ((M + BM - 1) / BM) * ((g.Kout + BN - 1) / BN);
+  const size_t stage = (size_t)(BM + BN) * BK * sizeof(bf16_t) * 2;
+  const size_t epi = (size_t)BM * (BN + 8) * sizeof(bf16_t);
+  const size_t lds = stage > epi ? stage : epi;
+  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN>), dim3((unsigned)tiles), dim3(kThreads),
+                     lds, st, X, Wt, Y, g, taps);
+}
+
+}  // namespace
+
+// Host launcher.  Caller guarantees: Kout % 8 == 0, Kpad % BK == 0 (filter rows zero-padded),
+// 16-B aligned tensors, taps.n <= DTF_MAX_TAPS.
+void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
+                    const TapTable& taps, int bk, hipStream_t st) {
+  if (taps.n <= 0 || taps.n > DTF_MAX_TAPS) throw std::runtime_error("conv: bad tap count");
+  if (g.Kout % 8) throw std::runtime_error("conv: Kout % 8 != 0");
+  const bool generic = (g.C % 32) != 0;
+  const bool narrow = g.Kout <= 64;        // 256 x 64 tile for 64-wide layers
+  if (generic) {
+    if (g.Kpad % 32) throw std::runtime_error("conv: Kpad % 32 != 0");
+    if (narrow) launch_cfg<4, 1, 32, true>(X, Wt, Y, g, taps, st);
+    else launch_cfg<2, 2, 32, true>(X, Wt, Y, g, taps, st);
+    return;
+  }
+  if (bk == 64 && g.C % 64 == 0) {
+    if (narrow) launch_cfg<4, 1, 64, false>(X, Wt, Y, g, taps, st);
+    else launch_cfg<2, 2, 64, false>(X, Wt, Y, g, taps, st);
+  } else {
+    if (narrow) launch_cfg<4, 1, 32, false>(X, Wt, Y, g, taps, st);
+    else launch_cfg<2, 2, 32, false>(X, Wt, Y, g, taps, st);
+  }
+}

@@ -1,0 +1,161 @@
+// Max-pool (any k/stride/pad, NHWC) forward with stored window-argmax, gather-form backward
+// (no atomics: each input pixel sums the <= ceil(k/s)^2 outputs whose argmax selected it),
+// and global average pool forward/backward.  SURVEY.md K4/K4b/K6 (MNIST 2x2/2) and N-K3
+// (ResNet-50 3x3/2 pad 1, 7x7 global average).  8 channels (16 B) per lane.
+#include "common.h"
+
+namespace {
+constexpr int kT = 256;
+
+__global__ void __launch_bounds__(kT)
+maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                   uint8_t* __restrict__ arg, int N, int H, int W, int C, int P, int Q, int kh,
+                   int kw, int sh, int sw, int ph, int pw) {
+  const int cv = C >> 3;
+  const long total = (long)N * P * Q * cv;
+  for (long i = (long)blockIdx.x * kT + threadIdx.x; i < total; i += (long)gridDim.x * kT) {
+    const int cg = (int)(i % cv);
+    long t = i / cv;
+    const int q = (int)(t % Q); t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int r = 0; r < kh; ++r) {
+      const int h = p * sh - ph + r;
+      if (h < 0 || h >= H) continue;
+      for (int s = 0; s < kw; ++s) {
+        const int w = q * sw - pw + s;
+        if (w < 0 || w >= W) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * H + h) * W + w) * C + cg * 8), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > best[j]) { best[j] = v[j]; bi[j] = (uint8_t)(r * kw + s); }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+    uint2 a;
+    a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    reinterpret_cast<uint2*>(arg)[i] = a;
+  }
+}
+
+__global__ void __launch_bounds__(kT)
+maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                   bf16_t* __restrict__ dx, int N, int H, int W, int C, int P, int Q, int kh,
+                   int kw, int sh, int sw, int ph, int pw) {
+  const int cv = C >> 3;
+  const long total = (long)N * H * W * cv;
+  for (long i = (long)blockIdx.x * kT + threadIdx.x; i < total; i += (long)gridDim.x * kT) {
+    const int cg = (int)(i % cv);
+    long t = i / cv;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    // outputs p with p*sh - ph <= h <= p*sh - ph + kh - 1
+    int p0 = h + ph - kh + 1;
+    p0 = p0 <= 0 ? 0 : (p0 + sh - 1) / sh;
+    int p1 = (h + ph) / sh;
+    if (p1 > P - 1) p1 = P - 1;
+    int q0 = w + pw - kw + 1;
+    q0 = q0 <= 0 ? 0 : (q0 + sw - 1) / sw;
+    int q1 = (w + pw) / sw;
+    if (q1 > Q - 1) q1 = Q - 1;
+    for (int p = p0; p <= p1; ++p) {
+      const int r = h - (p * sh - ph);
+      for (int q = q0; q <= q1; ++q) {
+        const int s = w - (q * sw - pw);
+        const uint8_t me = (uint8_t)(r * kw + s);
+        const long o = (((long)n * P + p) * Q + q) * cv + cg;
+        float g[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[o], g);
+        const uint2 a = reinterpret_cast<const uint2*>(arg)[o];
+        const uint32_t aw[2] = {a.x, a.y};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((aw[j >> 2] >> ((j & 3) * 8)) & 0xff) == me) acc[j] += g[j];
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(acc);
+  }
+}
+
+// global average pool: one lane = 8 channels of one image, loops over H*W rows.
+__global__ void __launch_bounds__(kT)
+gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N, int HW, int C) {
+  const int cv = C >> 3;
+  const long total = (long)N * cv;
+  const long i = (long)blockIdx.x * kT + threadIdx.x;
+  if (i >= total) return;
+  const int cg = (int)(i % cv);
+  const int n = (int)(i / cv);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const bf16_t* base = x + (long)n * HW * C + cg * 8;
+  for (int r = 0; r < HW; ++r) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(base + (long)r * C), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  reinterpret_cast<uint4*>(y)[i] = pack8(acc);
+}
+
+__global__ void __launch_bounds__(kT)
+gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N, int HW, int C) {
+  const int cv = C >> 3;
+  const long total = (long)N * HW * cv;
+  const float inv = 1.f / (float)HW;
+  for (long i = (long)blockIdx.x * kT + threadIdx.x; i < total; i += (long)gridDim.x * kT) {
+    const int cg = (int)(i % cv);
+    const int n = (int)(i / ((long)HW * cv));
+    float g[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[(long)n * cv + cg], g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] *= inv;
+    reinterpret_cast<uint4*>(dx)[i] = pack8(g);
+  }
+}
+
+inline int grid_for(long n) {
+  long g = (n + kT - 1) / kT;
+  if (g > 4096) g = 4096;
+  return (int)(g < 1 ? 1 : g);
+}
+}  // namespace
+
+void dtf_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* arg, int N, int H, int W, int C,
+                     int P, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)N * P * Q * (C / 8))), dim3(kT), 0,
+                     st, x, y, arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+}
+
+void dtf_maxpool_bwd(const bf16_t* dy, const uint8_t* arg, bf16_t* dx, int N, int H, int W,
+                     int C, int P, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(kT), 0,
+                     st, dy, arg, dx, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+}
+
+void dtf_gap_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st) {
+  const long total = (long)N * (C / 8);
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3((int)((total + kT - 1) / kT)), dim3(kT), 0, st, x, y, N,
+                     HW, C);
+}
+
+void dtf_gap_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st) {
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(kT), 0, st, dy,
+                     dx, N, HW, C);
+}

@@ -1,0 +1,94 @@
+"""ResNet-50 v1.5 (stride on the 3x3 conv), NHWC / bf16 compute, fp32 master weights.
+
+North-star model (BASELINE.json configs 2-4).  Not present in the
+reference, which only trains MNIST models (``run_mnist_distributed.py:46-70``); the layer
+naming follows tf.keras.applications.ResNet50 so checkpoints carry familiar keys
+(``conv2_block1_1_conv/kernel``, ``conv2_block1_1_bn/gamma`` ...).
+
+Every conv is bias-free and followed by a fused BatchNorm(+residual)(+ReLU) op, so a
+bottleneck block is 3-4 conv launches + 3-4 fused BN launches forward.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .layers import BatchNormalization, Conv2D, Dense, Layer, name_scope
+
+
+class ConvBN(nn.Module):
+    def __init__(self, cin, cout, k, stride, name, bn_momentum, bn_eps, zero_gamma=False):
+        super().__init__()
+        self.conv = Conv2D(cin, cout, k, strides=stride, padding=(k - 1) // 2, use_bias=False,
+                           name=f"{name}_conv", init="he")
+        self.bn = BatchNormalization(cout, bn_momentum, bn_eps, name=f"{name}_bn",
+                                     gamma_init=0.0 if zero_gamma else 1.0)
+
+    def forward(self, x, relu=True, residual=None):
+        y = ops.conv2d(x, self.conv.kernel, self.conv.strides, self.conv.padding)
+        return self.bn(y, relu=relu, residual=residual)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride, name, bn_momentum, bn_eps, zero_gamma=False):
+        super().__init__()
+        cout = width * self.expansion
+        self.has_proj = stride != 1 or cin != cout
+        if self.has_proj:
+            self.proj = ConvBN(cin, cout, 1, stride, f"{name}_0", bn_momentum, bn_eps)
+        self.c1 = ConvBN(cin, width, 1, 1, f"{name}_1", bn_momentum, bn_eps)
+        self.c2 = ConvBN(width, width, 3, stride, f"{name}_2", bn_momentum, bn_eps)
+        self.c3 = ConvBN(width, cout, 1, 1, f"{name}_3", bn_momentum, bn_eps, zero_gamma)
+
+    def forward(self, x):
+        sc = self.proj(x, relu=False) if self.has_proj else x
+        y = self.c1(x)
+        y = self.c2(y)
+        return self.c3(y, relu=True, residual=sc)
+
+
+class ResNet(Layer):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, in_channels=3,
+                 bn_momentum=0.997, bn_eps=1e-5, zero_init_residual=False):
+        super().__init__()
+        with name_scope():
+            self.stem = ConvBN(in_channels, 64, 7, 2, "conv1", bn_momentum, bn_eps)
+            blocks = []
+            cin = 64
+            for si, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
+                for bi in range(n):
+                    stride = 2 if (bi == 0 and si > 0) else 1
+                    blocks.append(Bottleneck(cin, width, stride, f"conv{si + 2}_block{bi + 1}",
+                                             bn_momentum, bn_eps, zero_init_residual))
+                    cin = width * 4
+            self.blocks = nn.ModuleList(blocks)
+            self.fc = Dense(cin, num_classes, name="predictions")
+            nn.init.normal_(self.fc.kernel.data, 0.0, 0.01)
+
+    def forward(self, x):
+        """x: [N, 224, 224, 3] NHWC (compute dtype) -> logits [N, classes] fp32."""
+        y = self.stem(x)
+        y = ops.max_pool2d(y, 3, 2, 1)
+        for b in self.blocks:
+            y = b(y)
+        y = ops.global_avg_pool(y)
+        return self.fc(y).float()
+
+
+def resnet50(num_classes=1000, **kw) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes, **kw)
+
+
+def resnet101(num_classes=1000, **kw) -> ResNet:
+    return ResNet((3, 4, 23, 3), num_classes, **kw)
+
+
+def resnet152(num_classes=1000, **kw) -> ResNet:
+    return ResNet((3, 8, 36, 3), num_classes, **kw)
+
+
+def num_params(model: nn.Module) -> int:
+    return sum(p.numel() for p in model.parameters())

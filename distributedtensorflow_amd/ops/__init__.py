@@ -1,0 +1,120 @@
+"""Op layer: NHWC / bf16 ops backed by hand-written HIP (gfx950) kernels.
+
+Dispatch rule (no multi-backend indirection on the GPU):
+  * CUDA (HIP) tensors  -> :mod:`.native` (our HIP kernels).  If the compiled extension is
+    missing this RAISES; it never silently falls back to PyTorch.
+  * CPU tensors         -> :mod:`.reference` (PyTorch CPU), the OneDevice("/cpu:0") path.
+  * ``set_backend("reference")`` forces the PyTorch path everywhere.  It exists for the
+    stock-PyTorch comparator in ``bench.py --impl torch`` and for numerics tests.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import reference
+
+_BACKEND = os.environ.get("DTF_OPS_BACKEND", "auto")   # auto | native | reference
+
+
+def set_backend(name: str):
+    global _BACKEND
+    if name not in ("auto", "native", "reference"):
+        raise ValueError(name)
+    _BACKEND = name
+
+
+def get_backend() -> str:
+    return _BACKEND
+
+
+def _use_native(t: torch.Tensor) -> bool:
+    if _BACKEND == "reference":
+        return False
+    if _BACKEND == "native":
+        return True
+    return t.is_cuda
+
+
+def _native():
+    from . import native
+    return native
+
+
+def conv2d(x, w, stride=1, padding=0):
+    if _use_native(x):
+        return _native().conv2d(x, w, stride, padding)
+    return reference.conv2d(x, w, stride, padding)
+
+
+def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True,
+               momentum=0.997, eps=1e-5, relu=False, residual=None):
+    if _use_native(x):
+        return _native().batch_norm(x, gamma, beta, running_mean, running_var, training,
+                                    momentum, eps, relu, residual)
+    return reference.batch_norm(x, gamma, beta, running_mean, running_var, training,
+                                momentum, eps, relu, residual)
+
+
+def relu(x):
+    if _use_native(x):
+        return _native().relu(x)
+    return reference.relu(x)
+
+
+def max_pool2d(x, kernel=2, stride=2, padding=0):
+    if _use_native(x):
+        return _native().max_pool2d(x, kernel, stride, padding)
+    return reference.max_pool2d(x, kernel, stride, padding)
+
+
+def global_avg_pool(x):
+    if _use_native(x):
+        return _native().global_avg_pool(x)
+    return reference.global_avg_pool(x)
+
+
+def dense(x, w, b=None, relu=False):
+    if _use_native(x):
+        return _native().dense(x, w, b, relu)
+    return reference.dense(x, w, b, relu)
+
+
+def sparse_softmax_cross_entropy(logits, labels):
+    if _use_native(logits):
+        return _native().sparse_softmax_cross_entropy(logits, labels)
+    return reference.sparse_softmax_cross_entropy(logits, labels)
+
+
+def softmax_cross_entropy_clipped_sum(logits, onehot):
+    return reference.softmax_cross_entropy_clipped_sum(logits, onehot)
+
+
+def layer_norm(x, gamma, beta, eps=1e-12):
+    if _use_native(x):
+        return _native().layer_norm(x, gamma, beta, eps)
+    return reference.layer_norm(x, gamma, beta, eps)
+
+
+def gelu(x):
+    if _use_native(x):
+        return _native().gelu(x)
+    return reference.gelu(x)
+
+
+def attention(q, k, v, mask=None, scale=None):
+    if _use_native(q):
+        return _native().attention(q, k, v, mask, scale)
+    return reference.attention(q, k, v, mask, scale)
+
+
+def dropout(x, p, training=True):
+    return reference.dropout(x, p, training)
+
+
+__all__ = [
+    "set_backend", "get_backend", "conv2d", "batch_norm", "relu", "max_pool2d",
+    "global_avg_pool", "dense", "sparse_softmax_cross_entropy",
+    "softmax_cross_entropy_clipped_sum", "layer_norm", "gelu", "attention", "dropout",
+]

@@ -1,0 +1,405 @@
+"""Autograd wrappers around the HIP/CDNA4 kernels in ``csrc/kernels`` (module ``_dtf_hip``).
+
+Every function here launches OUR kernels on the caller's current torch stream; there is no
+PyTorch fallback: if the extension is missing this module raises at import (a GPU box without
+the built ``.so`` must fail loudly, not silently run eager PyTorch).
+
+Precision contract (mixed precision, TF-style "float32 variables, bf16 compute"):
+  * activations bf16 NHWC;
+  * weights: fp32 master parameters; kernels consume the bf16 shadow the optimizer maintains
+    (``param._dtf_shadow``) or a cast made on the fly;
+  * weight gradients are produced directly in fp32 (MFMA fp32 accumulate, no bf16 round trip).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .reference import resolve_padding
+
+try:
+    from .._lib import _dtf_hip as _K  # noqa: N812
+except ImportError as e:  # pragma: no cover - exercised on boxes without a build
+    raise ImportError(
+        "distributedtensorflow_amd HIP extension (_lib/_dtf_hip*.so) is not built; run "
+        "`python -m distributedtensorflow_amd._build` (hipcc --offload-arch=gfx950). "
+        f"Original error: {e}") from e
+
+_BF16 = torch.bfloat16
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    s = getattr(w, "_dtf_shadow", None)
+    if s is not None and s.dtype == _BF16:
+        return s
+    return w.detach().to(_BF16)
+
+
+def _check_cuda_bf16(*ts):
+    for t in ts:
+        if t is not None and (not t.is_cuda or t.dtype != _BF16):
+            raise TypeError(f"native op expects CUDA bf16 tensors, got {t.dtype} on {t.device}")
+
+
+# ----------------------------------------------------------------------------- convolution
+
+def _conv_geom_fwd(x, K, R, S, stride, padding):
+    n, h, w, c = x.shape
+    sh, sw = _pair(stride)
+    pt, pb, pl, pr = resolve_padding(padding, h, w, R, S, stride)
+    P = (h + pt + pb - R) // sh + 1
+    Q = (w + pl + pr - S) // sw + 1
+    return n, h, w, c, P, Q, sh, sw, pt, pl
+
+
+def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0):
+    """wmat: [K, T*C] bf16 (rows zero-padded here to a multiple of 32 for the gather path)."""
+    n, h, w, c = x.shape
+    dh = [t[0] for t in taps]
+    dw = [t[1] for t in taps]
+    kdim = len(taps) * c
+    kpad = -(-kdim // 32) * 32
+    if kpad != kdim:
+        padded = torch.zeros(K, kpad, device=x.device, dtype=_BF16)
+        padded[:, :kdim] = wmat
+        wmat = padded
+    geom = [n, h, w, c, P, Q, sh, sw, K, kpad, Ho, Wo, osh, osw, oh0, ow0]
+    _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st())
+
+
+def conv2d_forward(x, w_bf16, stride, padding):
+    """x [N,H,W,C] bf16, w [K,R,S,C] bf16 -> y [N,P,Q,K]."""
+    K, R, S, C = w_bf16.shape
+    n, h, wd, c, P, Q, sh, sw, pt, pl = _conv_geom_fwd(x, K, R, S, stride, padding)
+    assert c == C, (x.shape, w_bf16.shape)
+    taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
+    y = torch.empty(n, P, Q, K, device=x.device, dtype=_BF16)
+    _launch_fwd(x, w_bf16.reshape(K, R * S * C), K, taps, P, Q, sh, sw, y, P, Q)
+    return y
+
+
+def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding):
+    """dX of conv2d via per-phase-class tap tables (see csrc/kernels/conv.hip header)."""
+    K, R, S, C = w_bf16.shape
+    n, h, wd, c = x_shape
+    sh, sw = _pair(stride)
+    pt, pb, pl, pr = resolve_padding(padding, h, wd, R, S, stride)
+    dx = None
+    wflat = w_bf16.reshape(K, R * S, C)
+    need_zero = False
+    launches = []
+    for a in range(sh):
+        for b in range(sw):
+            Pc = (h - a + sh - 1) // sh
+            Qc = (wd - b + sw - 1) // sw
+            if Pc <= 0 or Qc <= 0:
+                continue
+            taps, idx = [], []
+            for r in range(R):
+                if (a + pt - r) % sh:
+                    continue
+                for s in range(S):
+                    if (b + pl - s) % sw:
+                        continue
+                    taps.append(((a + pt - r) // sh, (b + pl - s) // sw))
+                    idx.append(r * S + s)
+            if not taps:
+                need_zero = True
+                continue
+            launches.append((a, b, Pc, Qc, taps, idx))
+    dx = (torch.zeros if need_zero else torch.empty)(n, h, wd, C, device=dy.device, dtype=_BF16)
+    dyc = dy.contiguous()
+    for a, b, Pc, Qc, taps, idx in launches:
+        if len(idx) == R * S and sh == 1 and sw == 1:
+            sel = wflat
+        else:
+            sel = wflat[:, torch.tensor(idx, device=dy.device), :]
+        wd_mat = sel.permute(2, 1, 0).contiguous()           # [C, T, K]
+        _launch_fwd(dyc, wd_mat.reshape(C, -1), C, taps, Pc, Qc, 1, 1, dx, h, wd, sh, sw, a, b)
+    return dx
+
+
+def conv2d_wgrad(x, dy, w_shape, stride, padding):
+    K, R, S, C = w_shape
+    n, h, wd, c = x.shape
+    sh, sw = _pair(stride)
+    pt, pb, pl, pr = resolve_padding(padding, h, wd, R, S, stride)
+    _, P, Q, _ = dy.shape
+    taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
+    dW = torch.zeros(K, R * S * C, device=x.device, dtype=torch.float32)
+    geom = [n, h, wd, c, P, Q, sh, sw, K, R * S * C]
+    _K.conv_wgrad(x.data_ptr(), dy.contiguous().data_ptr(), dW.data_ptr(), geom,
+                  [t[0] for t in taps], [t[1] for t in taps], _st())
+    return dW.reshape(K, R, S, C)
+
+
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w_master, stride, padding):
+        xb = x.contiguous()
+        wb = _bf16_weight(w_master)
+        ctx.save_for_backward(xb, wb)
+        ctx.stride, ctx.padding = stride, padding
+        ctx.w_dtype = w_master.dtype
+        return conv2d_forward(xb, wb, stride, padding)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb = ctx.saved_tensors
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if xb.shape[-1] % 8:
+                raise NotImplementedError("native conv2d dgrad needs C % 8 == 0 (input-layer "
+                                          "convs never need it)")
+            dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding)
+        if ctx.needs_input_grad[1]:
+            dw = conv2d_wgrad(xb, dy, wb.shape, ctx.stride, ctx.padding).to(ctx.w_dtype)
+        return dx, dw, None, None
+
+
+def conv2d(x, w, stride=1, padding=0):
+    _check_cuda_bf16(x)
+    K, R, S, C = w.shape
+    if K % 8 or (C % 8 and C > 8) or R * S > 64:
+        raise ValueError(f"native conv2d: unsupported filter {tuple(w.shape)}")
+    return _Conv2d.apply(x, w, stride, padding)
+
+
+# ----------------------------------------------------------------------------- batch norm
+
+class _BatchNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu,
+                residual):
+        x = x.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        dev = x.device
+        stats = torch.empty(4, C, device=dev, dtype=torch.float32)  # mean, invstd, scale, shift
+        mean, invstd, scale, shift = stats[0], stats[1], stats[2], stats[3]
+        st = _st()
+        g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
+        if training:
+            G = _K.bn_partial_blocks(M, C)
+            part = torch.empty(G, 2, C, device=dev, dtype=torch.float32)
+            _K.bn_fwd_stats(x.data_ptr(), M, C, part.data_ptr(), st)
+            _K.bn_fwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), b32.data_ptr(),
+                               _p(running_mean), _p(running_var), float(momentum), float(eps),
+                               mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
+                               shift.data_ptr(), st)
+        else:
+            _K.bn_infer_finalize(C, g32.data_ptr(), b32.data_ptr(), running_mean.data_ptr(),
+                                 running_var.data_ptr(), float(eps), mean.data_ptr(),
+                                 invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), st)
+        res = residual.contiguous() if residual is not None else None
+        y = torch.empty_like(x)
+        _K.bn_apply(x.data_ptr(), _p(res), y.data_ptr(), scale.data_ptr(), shift.data_ptr(), M, C,
+                    int(relu), st)
+        ctx.save_for_backward(x, y, g32, stats)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.gdt, ctx.bdt = gamma.dtype, beta.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, g32, stats = ctx.saved_tensors
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        dev = x.device
+        st = _st()
+        mean, invstd = stats[0], stats[1]
+        G = _K.bn_partial_blocks(M, C)
+        part = torch.empty(G, 2, C, device=dev, dtype=torch.float32)
+        _K.bn_bwd_reduce(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr(),
+                         invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st)
+        gb = torch.empty(5, C, device=dev, dtype=torch.float32)  # dgamma dbeta A B C
+        _K.bn_bwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), mean.data_ptr(),
+                           invstd.data_ptr(), gb[0].data_ptr(), gb[1].data_ptr(),
+                           gb[2].data_ptr(), gb[3].data_ptr(), gb[4].data_ptr(), 0, st)
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        _K.bn_bwd_apply(dy.data_ptr(), y.data_ptr(), x.data_ptr(), gb[2].data_ptr(),
+                        gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
+                        int(ctx.relu), st)
+        return (dx, gb[0].to(ctx.gdt), gb[1].to(ctx.bdt), None, None, None, None, None, None,
+                dres)
+
+
+def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True,
+               momentum=0.997, eps=1e-5, relu=False, residual=None):
+    _check_cuda_bf16(x, residual)
+    C = x.shape[-1]
+    if C % 8 or C > 2048:
+        raise ValueError(f"native batch_norm: unsupported channel count {C}")
+    if residual is not None and residual.shape != x.shape:
+        raise ValueError("residual shape mismatch")
+    return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps,
+                            relu, residual)
+
+
+# ----------------------------------------------------------------------------- ReLU (standalone)
+
+def relu(x):
+    return torch.relu(x)   # folded into conv/BN epilogues on the hot path
+
+
+# ----------------------------------------------------------------------------- pooling
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kernel, stride, padding):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        kh, kw = _pair(kernel)
+        sh, sw = _pair(stride)
+        pt, pb, pl, pr = resolve_padding(padding, h, w, kh, kw, stride)
+        P = (h + pt + pb - kh) // sh + 1
+        Q = (w + pl + pr - kw) // sw + 1
+        y = torch.empty(n, P, Q, c, device=x.device, dtype=x.dtype)
+        arg = torch.empty(n, P, Q, c, device=x.device, dtype=torch.uint8)
+        _K.maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), n, h, w, c, P, Q, kh, kw, sh,
+                       sw, pt, pl, _st())
+        ctx.save_for_backward(arg)
+        ctx.geom = (n, h, w, c, P, Q, kh, kw, sh, sw, pt, pl)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        n, h, w, c, P, Q, kh, kw, sh, sw, pt, pl = ctx.geom
+        dx = torch.empty(n, h, w, c, device=dy.device, dtype=dy.dtype)
+        _K.maxpool_bwd(dy.contiguous().data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, P,
+                       Q, kh, kw, sh, sw, pt, pl, _st())
+        return dx, None, None, None
+
+
+def max_pool2d(x, kernel=2, stride=2, padding=0):
+    _check_cuda_bf16(x)
+    if x.shape[-1] % 8:
+        raise ValueError("native max_pool2d needs C % 8 == 0")
+    kh, kw = _pair(kernel)
+    if kh * kw > 255:
+        raise ValueError("pool window too large")
+    return _MaxPool.apply(x, kernel, stride, padding)
+
+
+class _GAP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        y = torch.empty(n, c, device=x.device, dtype=x.dtype)
+        _K.gap_fwd(x.data_ptr(), y.data_ptr(), n, h * w, c, _st())
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, c = ctx.shape
+        dx = torch.empty(ctx.shape, device=dy.device, dtype=dy.dtype)
+        _K.gap_bwd(dy.contiguous().data_ptr(), dx.data_ptr(), n, h * w, c, _st())
+        return dx
+
+
+def global_avg_pool(x):
+    _check_cuda_bf16(x)
+    if x.shape[-1] % 8:
+        raise ValueError("native global_avg_pool needs C % 8 == 0")
+    return _GAP.apply(x)
+
+
+# ----------------------------------------------------------------------------- dense (library GEMM)
+
+def dense(x, w, b=None, relu=False):
+    """Plain GEMM -> hipBLASLt via torch.matmul (a *library* GEMM per the design rules);
+    the bias and ReLU stay fused in the same addmm epilogue."""
+    wb = _bf16_weight(w) if w.dtype != x.dtype else w
+    if w.requires_grad and wb is not w:
+        wb = _MasterCast.apply(w, wb)
+    y = torch.nn.functional.linear(x, wb, None if b is None else b.to(x.dtype))
+    return torch.relu(y) if relu else y
+
+
+class _MasterCast(torch.autograd.Function):
+    """Use the bf16 shadow forward; route the gradient to the fp32 master in fp32."""
+
+    @staticmethod
+    def forward(ctx, master, shadow):
+        ctx.dt = master.dtype
+        return shadow
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dt), None
+
+
+# ----------------------------------------------------------------------------- loss
+
+class _SoftmaxXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        lg = logits.detach().float().contiguous()
+        B, V = lg.shape
+        lab = labels.contiguous()
+        if lab.dtype not in (torch.int64, torch.int32):
+            lab = lab.long()
+        rows = torch.empty(B, device=lg.device, dtype=torch.float32)
+        grad = torch.empty_like(lg)
+        _K.softmax_xent(lg.data_ptr(), lab.data_ptr(), lab.element_size(), B, V, rows.data_ptr(),
+                        grad.data_ptr(), 1.0 / B, _st())
+        ctx.save_for_backward(grad)
+        ctx.ldt = logits.dtype
+        return rows.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return (grad * g).to(ctx.ldt), None
+
+
+def sparse_softmax_cross_entropy(logits, labels):
+    if logits.dim() != 2:
+        raise ValueError("logits must be [B, V]")
+    return _SoftmaxXent.apply(logits, labels)
+
+
+# ----------------------------------------------------------------------------- transformer ops
+# (LayerNorm / GELU / attention for BERT live in .native_nlp to keep this file focused)
+
+def layer_norm(x, gamma, beta, eps=1e-12):
+    from . import native_nlp
+    return native_nlp.layer_norm(x, gamma, beta, eps)
+
+
+def gelu(x):
+    from . import native_nlp
+    return native_nlp.gelu(x)
+
+
+def attention(q, k, v, mask=None, scale=None):
+    from . import native_nlp
+    return native_nlp.attention(q, k, v, mask, scale)
+
+
+def kernels():
+    """The loaded extension module (for optimizers / strategies)."""
+    return _K
+
+
+def extension_path():
+    return os.path.abspath(_K.__file__)

@@ -1,0 +1,353 @@
+"""tf.distribute-style strategies, MI355X-native: one process per GPU, RCCL over xGMI.
+
+BASELINE.json configs 1-5 name OneDevice / Mirrored / MultiWorkerMirrored /
+ParameterServer strategies (none exist in the reference, which does TF1 between-graph PS
+replication — ``run_mnist_distributed.py:104-161``).  Design:
+
+* Every replica is its own OS process bound to one GPU (``LOCAL_RANK``); "in-graph" multi-GPU
+  replication is deliberately not used — on MI355X one process per GPU with RCCL is the
+  idiomatic (and fastest) layout.  ``MirroredStrategy`` over the 8 GPUs of a node and
+  ``MultiWorkerMirroredStrategy`` across nodes are therefore the same engine; they differ only
+  in how the cluster is discovered (env/torchrun vs ``TF_CONFIG``/``config.json``).
+* Variables are created on the replica's device inside ``strategy.scope()`` (default device),
+  then made identical by ONE broadcast of the optimizer's flat master buffer from rank 0.
+* Gradients: the optimizer's flat fp32 gradient buffer is cut into contiguous buckets (sized for
+  xGMI: a ring all-reduce is per-link bound, so few large buckets — default 64 MB — beat many
+  small ones).  A post-accumulate hook counts each bucket's variables; the moment a bucket is
+  complete its all-reduce is launched asynchronously on RCCL's stream while autograd keeps
+  producing earlier-layer gradients on the compute stream (backward/communication overlap).
+  The 1/N averaging is folded into the fused optimizer kernel's gradient scale.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+import threading
+
+import torch
+import torch.distributed as dist
+
+_tls = threading.local()
+_default_strategy = None
+
+
+class ReduceOp:
+    SUM = "sum"
+    MEAN = "mean"
+    MAX = "max"
+    MIN = "min"
+
+
+def _torch_op(op):
+    return {ReduceOp.SUM: dist.ReduceOp.SUM, ReduceOp.MEAN: dist.ReduceOp.SUM,
+            ReduceOp.MAX: dist.ReduceOp.MAX, ReduceOp.MIN: dist.ReduceOp.MIN}[op]
+
+
+def get_strategy():
+    s = getattr(_tls, "strategy", None)
+    if s is not None:
+        return s
+    global _default_strategy
+    if _default_strategy is None:
+        _default_strategy = _DefaultStrategy()
+    return _default_strategy
+
+
+def has_strategy():
+    return getattr(_tls, "strategy", None) is not None
+
+
+# ----------------------------------------------------------------------------- gradient reducers
+
+class _NullReducer:
+    def __init__(self, space=None):
+        self.space = space
+
+    def begin_step(self):
+        pass
+
+    def finish(self):
+        pass
+
+    def grad_scale(self):
+        return 1.0
+
+
+class BucketedAllReduce:
+    """Overlapped bucketed all-reduce of a FlatSpace's gradient buffer."""
+
+    def __init__(self, space, group=None, bucket_bytes=64 << 20, first_bucket_bytes=4 << 20,
+                 average=True, compress_bf16=False):
+        self.space = space
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.average = average
+        self.compress = compress_bf16
+        # buckets over the decayed region in flat order (== reverse creation order), then one
+        # bucket for the small non-decayed tail (BN gamma/beta, biases)
+        ranges = []
+        order, offs = space.order, space.offsets
+        cur_start, cur_bytes, members = None, 0, []
+        limit = first_bucket_bytes
+        for i, (v, o) in enumerate(zip(order, offs)):
+            if o >= space.decay_end and space.decay_end < space.numel:
+                break
+            if cur_start is None:
+                cur_start = o
+            members.append(i)
+            end = offs[i + 1] if i + 1 < len(offs) else space.numel
+            cur_bytes = (end - cur_start) * 4
+            if cur_bytes >= limit:
+                ranges.append((cur_start, end, members))
+                cur_start, members, limit = None, [], bucket_bytes
+        if members:
+            ranges.append((cur_start, space.decay_end, members))
+        tail = [i for i, o in enumerate(offs) if o >= space.decay_end and space.decay_end < space.numel]
+        if tail:
+            ranges.append((space.decay_end, space.numel, tail))
+        self.buckets = ranges
+        self.var_bucket = {}
+        for b, (_, _, mem) in enumerate(ranges):
+            for i in mem:
+                self.var_bucket[i] = b
+        self.pending = [0] * len(ranges)
+        self.works = []
+        self.launched = [False] * len(ranges)
+        self._hooks = []
+        for i, v in enumerate(order):
+            self._hooks.append(v.register_post_accumulate_grad_hook(self._make_hook(i)))
+
+    def _make_hook(self, i):
+        def hook(_p):
+            b = self.var_bucket[i]
+            self.pending[b] -= 1
+            if self.pending[b] == 0:
+                self._launch(b)
+        return hook
+
+    def _launch(self, b):
+        if self.launched[b]:
+            return
+        self.launched[b] = True
+        s, e, _ = self.buckets[b]
+        view = self.space.grad[s:e]
+        if self.compress:
+            tmp = view.to(torch.bfloat16)
+            w = dist.all_reduce(tmp, group=self.group, async_op=True)
+            self.works.append((w, view, tmp))
+        else:
+            self.works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+
+    def begin_step(self):
+        self.pending = [len(m) for (_, _, m) in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.works = []
+
+    def finish(self):
+        # buckets whose variables received no gradient this step still have to be reduced
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        for w, view, tmp in self.works:
+            w.wait()
+            if view is not None:
+                view.copy_(tmp)
+        self.works = []
+
+    def grad_scale(self):
+        return 1.0 / self.world if self.average else 1.0
+
+
+# ----------------------------------------------------------------------------- strategies
+
+class Strategy:
+    """Base: ``scope()``, ``run()``, ``reduce()``, ``experimental_distribute_dataset()``."""
+
+    def __init__(self, device=None):
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self._prev = None
+
+    # -- replica topology
+    @property
+    def num_replicas_in_sync(self) -> int:
+        return 1
+
+    @property
+    def replica_id(self) -> int:
+        return 0
+
+    @property
+    def is_chief(self) -> bool:
+        return self.replica_id == 0
+
+    # -- context
+    @contextlib.contextmanager
+    def scope(self):
+        prev = getattr(_tls, "strategy", None)
+        _tls.strategy = self
+        prev_dev = torch.get_default_device()
+        torch.set_default_device(self.device)
+        try:
+            yield self
+        finally:
+            torch.set_default_device(prev_dev)
+            _tls.strategy = prev
+
+    def run(self, fn, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        with self.scope():
+            return fn(*args, **kwargs)
+
+    def reduce(self, op, value, axis=None):
+        if axis is not None:
+            value = value.sum(axis) if op in (ReduceOp.SUM, ReduceOp.MEAN) else value
+        return value
+
+    def experimental_distribute_dataset(self, dataset):
+        return dataset.shard(self.num_replicas_in_sync, self.replica_id) \
+            if hasattr(dataset, "shard") and self.num_replicas_in_sync > 1 else dataset
+
+    # -- variable sync hooks used by optimizers / checkpoints
+    def make_gradient_reducer(self, space):
+        return _NullReducer(space)
+
+    def broadcast_space(self, space):
+        pass
+
+    def broadcast_tensors(self, tensors, src=0):
+        pass
+
+    def all_reduce_(self, t, op=ReduceOp.SUM):
+        return t
+
+    def barrier(self):
+        pass
+
+
+class _DefaultStrategy(Strategy):
+    def __init__(self):
+        super().__init__("cpu")
+
+    @contextlib.contextmanager
+    def scope(self):
+        yield self
+
+
+class OneDeviceStrategy(Strategy):
+    """Single device, no communication.  ``OneDeviceStrategy("/cpu:0")`` is BASELINE config 1."""
+
+    def __init__(self, device="/gpu:0"):
+        super().__init__(_parse_device(device))
+
+
+def _parse_device(d):
+    if isinstance(d, torch.device):
+        return d
+    d = str(d).lower().strip("/")
+    if d.startswith("cpu"):
+        return torch.device("cpu")
+    if d.startswith("gpu") or d.startswith("device:gpu"):
+        idx = int(d.split(":")[-1]) if ":" in d else 0
+        return torch.device("cuda", idx)
+    return torch.device(d)
+
+
+def init_process_group_from_env(backend=None, timeout_s=600):
+    """Initialise torch.distributed from torchrun-style env (RANK/WORLD_SIZE/MASTER_*)."""
+    import datetime
+    if dist.is_initialized():
+        return
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    kw = {}
+    if backend == "nccl":
+        kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+
+
+class MirroredStrategy(Strategy):
+    """Synchronous data parallelism: replicated variables, all-reduced gradients (RCCL).
+
+    One process per GPU; ``devices`` (TF signature) is accepted for API compatibility but the
+    replica set is the torch.distributed world of this node.  With ``WORLD_SIZE`` unset it
+    runs single-replica on ``cuda:LOCAL_RANK``.
+    """
+
+    def __init__(self, devices=None, cross_device_ops=None, bucket_mb=64, first_bucket_mb=4,
+                 compress_bf16=False, backend=None):
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+            dev = torch.device("cuda", local)
+        else:
+            dev = torch.device("cpu")
+        super().__init__(dev)
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.first_bucket_bytes = int(first_bucket_mb * (1 << 20))
+        self.compress_bf16 = compress_bf16
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            init_process_group_from_env(backend)
+        self._dist = dist.is_initialized() and dist.get_world_size() > 1
+
+    @property
+    def num_replicas_in_sync(self):
+        return dist.get_world_size() if self._dist else 1
+
+    @property
+    def replica_id(self):
+        return dist.get_rank() if self._dist else 0
+
+    def make_gradient_reducer(self, space):
+        if not self._dist:
+            return _NullReducer(space)
+        return BucketedAllReduce(space, None, self.bucket_bytes, self.first_bucket_bytes,
+                                 compress_bf16=self.compress_bf16)
+
+    def broadcast_space(self, space):
+        if self._dist:
+            dist.broadcast(space.master, 0)
+            space.refresh_shadow()
+
+    def broadcast_tensors(self, tensors, src=0):
+        if self._dist:
+            for t in tensors:
+                dist.broadcast(t, src)
+
+    def reduce(self, op, value, axis=None):
+        value = super().reduce(op, value, axis)
+        if not self._dist:
+            return value
+        t = value.detach().clone() if isinstance(value, torch.Tensor) else torch.tensor(
+            float(value), device=self.device)
+        dist.all_reduce(t, _torch_op(op))
+        if op == ReduceOp.MEAN:
+            t /= self.num_replicas_in_sync
+        return t
+
+    def all_reduce_(self, t, op=ReduceOp.SUM):
+        if self._dist:
+            dist.all_reduce(t, _torch_op(op))
+            if op == ReduceOp.MEAN:
+                t /= self.num_replicas_in_sync
+        return t
+
+    def barrier(self):
+        if self._dist:
+            dist.barrier()
+
+
+class MultiWorkerMirroredStrategy(MirroredStrategy):
+    """Same engine as MirroredStrategy; cluster from ``TF_CONFIG`` / config.json when torchrun
+    env is absent (one process per GPU on every worker host)."""
+
+    def __init__(self, cluster_resolver=None, communication=None, **kw):
+        if "WORLD_SIZE" not in os.environ and (cluster_resolver is not None or
+                                               "TF_CONFIG" in os.environ):
+            from ..cluster import resolver as _res
+            _res.export_torch_env(cluster_resolver)
+        super().__init__(**kw)

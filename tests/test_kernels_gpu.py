@@ -1,0 +1,146 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op.
+
+Shapes cover the reference's MNIST CNN and ResNet-50's distinct conv
+geometries (N-K1..N-K5) at reduced batch.  Inputs are asymmetric random data (never symmetric
+operands: a transposed MFMA C-write would pass a symmetric test — guide §3).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def _native():
+    from distributedtensorflow_amd.ops import native
+    return native
+
+
+def _ref():
+    from distributedtensorflow_amd.ops import reference
+    return reference
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+CONV_CASES = [
+    # (N, H, W, C, K, R, stride, pad)
+    (2, 28, 28, 1, 32, 5, 1, "same"),      # MNIST conv1 (generic gather path)
+    (2, 14, 14, 32, 64, 5, 1, "same"),     # MNIST conv2 (BK=32)
+    (2, 56, 56, 64, 64, 1, 1, 0),          # bottleneck 1x1
+    (2, 56, 56, 64, 64, 3, 1, 1),          # bottleneck 3x3
+    (2, 56, 56, 64, 256, 1, 1, 0),         # expand 1x1
+    (2, 56, 56, 128, 128, 3, 2, 1),        # strided 3x3 (stage transition)
+    (2, 56, 56, 256, 512, 1, 2, 0),        # projection 1x1 stride 2
+    (2, 14, 14, 1024, 256, 1, 1, 0),
+    (2, 7, 7, 512, 512, 3, 1, 1),
+    (2, 224, 224, 3, 64, 7, 2, 3),         # stem 7x7/2 (generic)
+    (3, 9, 11, 64, 72, 3, 2, 1),           # odd sizes, Kout not a multiple of 64
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case):
+    N, H, W, C, K, R, stride, pad = case
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K, R, R, C, device=dev) / (R * R * C) ** 0.5)
+    nat = _native()
+    ref = _ref()
+    xr = x.float().requires_grad_(True)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = ref.conv2d(xr, wr, stride, pad)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+
+    xn = x.clone().requires_grad_(C % 8 == 0)   # input-layer convs need no data grad
+    wn = w.clone().requires_grad_(True)
+    yn = nat.conv2d(xn, wn, stride, pad)
+    assert yn.shape == yr.shape
+    assert _rel(yn, yr) < 1e-2, _rel(yn, yr)
+    yn.backward(g.to(torch.bfloat16))
+    if C % 8 == 0:
+        assert _rel(xn.grad, xr.grad) < 2e-2, _rel(xn.grad, xr.grad)
+    assert _rel(wn.grad, wr.grad) < 2e-2, _rel(wn.grad, wr.grad)
+
+
+@pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, True, True), (512, False, False),
+                                        (2048, True, True), (32, True, False)])
+def test_batch_norm(C, relu, res):
+    torch.manual_seed(1)
+    x = (torch.randn(4, 7, 9, C, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    r = torch.randn_like(x) if res else None
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev)
+    rm1, rv1 = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    nat, ref = _native(), _ref()
+    xr = x.float().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    yr = ref.batch_norm(xr, gr, br, rm1, rv1, True, 0.9, 1e-5, relu, rr)
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    xn = x.clone().requires_grad_(True)
+    gn, bn = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    rn = r.clone().requires_grad_(True) if res else None
+    yn = nat.batch_norm(xn, gn, bn, rm2, rv2, True, 0.9, 1e-5, relu, rn)
+    assert _rel(yn, yr) < 1e-2
+    assert torch.allclose(rm1, rm2, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(rv1, rv2, atol=1e-3, rtol=1e-3)
+    yn.backward(dy.to(torch.bfloat16))
+    assert _rel(xn.grad, xr.grad) < 2e-2
+    assert _rel(gn.grad, gr.grad) < 1e-2
+    assert _rel(bn.grad, br.grad) < 1e-2
+    if res:
+        assert _rel(rn.grad, rr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((2, 112, 112, 64), 3, 2, 1), ((4, 28, 28, 32), 2, 2, 0),
+                                         ((2, 14, 14, 64), 2, 2, 0)])
+def test_max_pool(shape, k, s, p):
+    torch.manual_seed(2)
+    x = torch.randn(*shape, device=dev).to(torch.bfloat16)
+    nat, ref = _native(), _ref()
+    xr = x.float().requires_grad_(True)
+    yr = ref.max_pool2d(xr, k, s, p)
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    xn = x.clone().requires_grad_(True)
+    yn = nat.max_pool2d(xn, k, s, p)
+    assert torch.equal(yn.float(), yr.detach())
+    yn.backward(dy.to(torch.bfloat16))
+    assert _rel(xn.grad, xr.grad) < 1e-2
+
+
+def test_global_avg_pool():
+    x = torch.randn(8, 7, 7, 2048, device=dev).to(torch.bfloat16)
+    nat, ref = _native(), _ref()
+    xr = x.float().requires_grad_(True)
+    yr = ref.global_avg_pool(xr)
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    xn = x.clone().requires_grad_(True)
+    yn = nat.global_avg_pool(xn)
+    assert _rel(yn, yr) < 1e-2
+    yn.backward(dy.to(torch.bfloat16))
+    assert _rel(xn.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("B,V", [(128, 10), (256, 1000), (7, 30522)])
+def test_softmax_xent(B, V):
+    logits = torch.randn(B, V, device=dev) * 3
+    labels = torch.randint(0, V, (B,), device=dev)
+    nat, ref = _native(), _ref()
+    lr = logits.clone().requires_grad_(True)
+    l1 = ref.sparse_softmax_cross_entropy(lr, labels)
+    l1.backward()
+    ln = logits.clone().requires_grad_(True)
+    l2 = nat.sparse_softmax_cross_entropy(ln, labels)
+    l2.backward()
+    assert abs(l1.item() - l2.item()) < 1e-4 * max(1, abs(l1.item()))
+    assert _rel(ln.grad, lr.grad) < 1e-5
