@@ -19,7 +19,7 @@ namespace py = pybind11;
 struct TapTable { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
 struct TapTableW { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
 struct ConvGeom { int N, H, W, C, P, Q, sh, sw, Kout, Kpad, Ho, Wo, osh, osw, oh0, ow0; };
-struct WgradGeom { int N, H, W, C, P, Q, sh, sw, Kout, ldw; long m_per_split; };
+struct WgradGeom { int N, H, W, C, P, Q, sh, sw, Kout, ldw; long m_per_split; long slab; };
 
 // ---- launchers defined in the .hip translation units
 int dtf_bn_partial_blocks(long M, int C);
@@ -57,9 +57,11 @@ void dtf_sumsq(const float*, long, float*, hipStream_t);
 void dtf_cast_f32_bf16(const float*, bf16_t*, long, hipStream_t);
 void dtf_conv_igemm(const bf16_t*, const bf16_t*, bf16_t*, const ConvGeom&, const TapTable&, int,
                     hipStream_t);
-void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, WgradGeom, const TapTableW&,
-                    hipStream_t);
-int dtf_conv_wgrad_splits(long, int, int);
+void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, const TapTableW&,
+                    int, int, hipStream_t);
+int dtf_conv_wgrad_splits(long, int, int, long);
+void dtf_lds_probe(int, int, int*, int, hipStream_t);
+int dtf_max_dynamic_lds(int);
 
 template <typename T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
@@ -209,14 +211,21 @@ PYBIND11_MODULE(_dtf_hip, m) {
                    make_taps<TapTable>(dh, dw), bk, S(st));
     check_launch("conv_igemm");
   });
-  m.def("conv_wgrad", [](uintptr_t x, uintptr_t dy, uintptr_t dw_out, std::vector<int> geom,
-                         std::vector<int> dh, std::vector<int> dw, uintptr_t st) {
+  m.def("conv_wgrad", [](uintptr_t x, uintptr_t dy, uintptr_t dw_out, uintptr_t ws,
+                         std::vector<int> geom, std::vector<int> dh, std::vector<int> dw,
+                         int splits, uintptr_t st, int tr_mode) {
     if (geom.size() != 10) throw std::runtime_error("conv_wgrad: geom needs 10 ints");
     WgradGeom g{geom[0], geom[1], geom[2], geom[3], geom[4], geom[5], geom[6], geom[7], geom[8],
-                geom[9], 0};
-    dtf_conv_wgrad(P<const bf16_t>(x), P<const bf16_t>(dy), P<float>(dw_out), g,
-                   make_taps<TapTableW>(dh, dw), S(st));
+                geom[9], 0, 0};
+    dtf_conv_wgrad(P<const bf16_t>(x), P<const bf16_t>(dy), P<float>(dw_out), P<float>(ws), g,
+                   make_taps<TapTableW>(dh, dw), splits, tr_mode, S(st));
     check_launch("conv_wgrad");
-  });
+  }, py::arg("x"), py::arg("dy"), py::arg("dw_out"), py::arg("ws"), py::arg("geom"),
+     py::arg("dh"), py::arg("dw"), py::arg("splits"), py::arg("stream"), py::arg("tr_mode") = 1);
   m.def("conv_wgrad_splits", &dtf_conv_wgrad_splits);
+  m.def("lds_probe", [](int bytes, int blocks, uintptr_t errors, int spin, uintptr_t st) {
+    dtf_lds_probe(bytes, blocks, P<int>(errors), spin, S(st));
+    check_launch("lds_probe");
+  });
+  m.def("max_dynamic_lds", &dtf_max_dynamic_lds);
 }

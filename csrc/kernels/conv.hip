@@ -6,26 +6,30 @@
 // pixel (n,p,q) reads input pixel (p*sh + dh_t, q*sw + dw_t) for tap t (zero outside the image)
 // and is stored at Y[n, p*osh + oh0, q*osw + ow0, :] of an [N, Ho, Wo, Kout] tensor.
 //   * forward:              taps = {(r - pad_h, s - pad_w)}, (osh,osw,oh0,ow0) = (1,1,0,0)
-//   * data-grad, stride 1:  forward conv of dY with the spatially flipped, C<->K transposed
-//                           filter and taps {(pad_h - r', ...)}
+//   * data-grad, stride 1:  forward conv of dY with the C<->K transposed filter and
+//                           taps {(pad_h - r, pad_w - s)}
 //   * data-grad, stride s:  one launch per output phase class (a, b) in [0,s)^2 with the taps
 //                           that hit that class; osh = osw = s, (oh0, ow0) = (a, b)
 // so one MFMA kernel serves SURVEY.md K3/K5/N-K1 forward and dgrad.
 //
-// Tiling (cdna_hip_programming.md §5, "step-3"-style 2-stage pipeline):
+// Tiling (cdna_hip_programming.md §5, 2-stage pipeline):
 //   block = 256 threads = 4 waves in WAVES_M x WAVES_N, wave tile 64x64 built from 4x4
 //   v_mfma_f32_16x16x32_bf16 tiles (16x16x32 holds a higher clock than 32x32x16 under load:
 //   MI355X_MICROARCH.md "DVFS give-back" (7)).
 //   K-step BK = 64 (C % 64 == 0) or 32 (C % 32 == 0); each (row, tap) supplies BK contiguous
 //   channels = one 128-B / 64-B line per output row, loaded 16 B per lane.
+//   Loads are raw BUFFER loads (guide §5.5 T8): the per-lane byte offset of a padding tap is set
+//   out of range, so the hardware range check returns zeros — zero padding with no branches.
 //   Register staging with the T14 split: next tile's global loads are issued before the MFMAs
 //   of the current tile and written to the other LDS buffer after them; one barrier per K-step.
 //   LDS rows are XOR-swizzled by 16-B chunk so ds_read_b128 fragment reads of 16 different rows
 //   are conflict-free (T2).
-//   Epilogue: accumulators -> bf16 -> LDS -> 16-B coalesced global stores (T21 in spirit).
+//   Epilogue: accumulators -> bf16 -> LDS -> 16-B coalesced global stores.
 //   Tile order: XCD-aware bijective remap of the block id, N-tile fastest so blocks sharing an
 //   A panel run on the same XCD's L2 (T1).
 //   GENERIC=true: per-element gather for C % 32 != 0 (stem 7x7x3, MNIST conv 5x5x1).
+//   The tap table arrives as a kernel argument; it is only ever read with wave-uniform indices
+//   (scalar loads) — per-lane indices go through a copy in LDS.
 #include <stdexcept>
 #include <string>
 
@@ -52,12 +56,23 @@ struct ConvGeom {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr uint32_t kOOB = 0xFFFFFFF0u;   // byte offset the buffer range check always rejects
 
 template <int BK>
 DTF_DEV int swz_chunk(int row, int chunk) {
   constexpr int CPR = BK / 8;           // 16-B chunks per row
   constexpr int RPB = 16 / CPR;         // rows per 256-B bank row
   return chunk ^ ((row / RPB) % CPR);
+}
+
+DTF_DEV __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+DTF_DEV uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+DTF_DEV uint32_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
 }
 
 template <int WAVES_M, int WAVES_N, int BK, bool GENERIC>
@@ -71,38 +86,45 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   constexpr int ROWS_PER_PASS = kThreads / CPR;
   constexpr int STAGE_ELEMS = (BM + BN) * BK;            // bf16 elements per LDS stage
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  int* lds_taps = reinterpret_cast<int*>(lds + 2 * STAGE_ELEMS);   // [2][DTF_MAX_TAPS]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
 
-  const long M = (long)g.N * g.P * g.Q;
+  const int M = g.N * g.P * g.Q;
   const int tiles_n = (g.Kout + BN - 1) / BN;
-  const int tiles_m = (int)((M + BM - 1) / BM);
+  const int tiles_m = (M + BM - 1) / BM;
   const int nwg = tiles_n * tiles_m;
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const long m0 = (long)tm * BM;
+  const int m0 = tm * BM;
   const int n0 = tn * BN;
 
   const int K = taps.n * g.C;
   const int nk = (K + BK - 1) / BK;
+  const auto rx = rsrc(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
+  const auto rw = rsrc(Wt, (uint32_t)g.Kout * g.Kpad * 2u);
 
-  // ---- per-thread A rows: decode (n, p, q) once
+  if constexpr (GENERIC) {
+    if (tid == 0)
+      for (int t = 0; t < taps.n; ++t) { lds_taps[t] = taps.dh[t]; lds_taps[DTF_MAX_TAPS + t] = taps.dw[t]; }
+  }
+
+  // ---- per-thread A rows: decode (n, p, q) once (32-bit; host guarantees M < 2^31)
   const int chunk = tid % CPR;
-  int a_nbase[A_CHUNKS], a_h[A_CHUNKS], a_w[A_CHUNKS];
-  bool a_ok[A_CHUNKS];
+  int a_pix[A_CHUNKS], a_h[A_CHUNKS], a_w[A_CHUNKS];
 #pragma unroll
   for (int i = 0; i < A_CHUNKS; ++i) {
-    const long m = m0 + tid / CPR + i * ROWS_PER_PASS;
-    a_ok[i] = m < M;
-    const long mm = a_ok[i] ? m : 0;
-    const int q = (int)(mm % g.Q);
-    const long t = mm / g.Q;
-    const int p = (int)(t % g.P);
-    const int n = (int)(t / g.P);
-    a_nbase[i] = n;
-    a_h[i] = p * g.sh;
+    const int m = m0 + tid / CPR + i * ROWS_PER_PASS;
+    const bool ok = m < M;
+    const int mm = ok ? m : 0;
+    const int q = mm % g.Q;
+    const int t = mm / g.Q;
+    const int p = t % g.P;
+    const int n = t / g.P;
+    a_pix[i] = n * g.H * g.W;                 // image base pixel
+    a_h[i] = ok ? p * g.sh : -(1 << 24);      // invalid rows fail every bounds test
     a_w[i] = q * g.sw;
   }
 
@@ -111,18 +133,15 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   auto load_stage = [&](int kt) {
     const int k0 = kt * BK;
     if constexpr (!GENERIC) {
-      const int t = k0 / g.C;
+      const int t = __builtin_amdgcn_readfirstlane(k0 / g.C);
       const int c0 = k0 - t * g.C + chunk * 8;
-      const int dh = taps.dh[t], dw = taps.dw[t];
+      const int dh = taps.dh[t], dw = taps.dw[t];          // uniform index: scalar loads
 #pragma unroll
       for (int i = 0; i < A_CHUNKS; ++i) {
         const int h = a_h[i] + dh, w = a_w[i] + dw;
-        if (a_ok[i] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W) {
-          const long off = (((long)a_nbase[i] * g.H + h) * g.W + w) * g.C + c0;
-          ra[i] = *reinterpret_cast<const uint4*>(X + off);
-        } else {
-          ra[i] = make_uint4(0, 0, 0, 0);
-        }
+        const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+        const uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * g.W + w) * g.C + c0) * 2) : kOOB;
+        ra[i] = bload16(rx, off);
       }
     } else {
 #pragma unroll
@@ -134,14 +153,12 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
 #pragma unroll
           for (int e1 = 0; e1 < 2; ++e1) {
             const int k = k0 + chunk * 8 + e2 * 2 + e1;
-            uint32_t v = 0;
-            if (k < K && a_ok[i]) {
-              const int t = k / g.C, c = k - t * g.C;
-              const int h = a_h[i] + taps.dh[t], w = a_w[i] + taps.dw[t];
-              if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
-                v = X[(((long)a_nbase[i] * g.H + h) * g.W + w) * g.C + c];
-            }
-            pair |= v << (16 * e1);
+            const int t = k / g.C, c = k - t * g.C;
+            const int tt = t < taps.n ? t : 0;
+            const int h = a_h[i] + lds_taps[tt], w = a_w[i] + lds_taps[DTF_MAX_TAPS + tt];
+            const bool ok = k < K && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+            const uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * g.W + w) * g.C + c) * 2) : kOOB;
+            pair |= bload2(rx, off) << (16 * e1);
           }
           wv[e2] = pair;
         }
@@ -151,10 +168,8 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
 #pragma unroll
     for (int i = 0; i < B_CHUNKS; ++i) {
       const int nrow = n0 + tid / CPR + i * ROWS_PER_PASS;
-      if (nrow < g.Kout)
-        rb[i] = *reinterpret_cast<const uint4*>(Wt + (long)nrow * g.Kpad + k0 + chunk * 8);
-      else
-        rb[i] = make_uint4(0, 0, 0, 0);
+      const uint32_t off = nrow < g.Kout ? (uint32_t)((nrow * g.Kpad + k0 + chunk * 8) * 2) : kOOB;
+      rb[i] = bload16(rw, off);
     }
   };
 
@@ -179,6 +194,7 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (GENERIC) __syncthreads();   // tap table visible before the first gather
   load_stage(0);
   store_stage(0);
   __syncthreads();
@@ -214,6 +230,10 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   }
 
   // ---- epilogue: acc -> bf16 LDS tile [BM][BN + 8] -> coalesced 16-B stores
+  // (explicit wait states between the MFMA chain and the first consumer of its results)
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
   constexpr int LDC = BN + 8;
   bf16_t* st = lds;
 #pragma unroll
@@ -232,12 +252,12 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   const int oc = tid % OCPR;
   const bool col_ok = n0 + oc * 8 < g.Kout;
   for (int r = tid / OCPR; r < BM; r += OROWS) {
-    const long m = m0 + r;
+    const int m = m0 + r;
     if (m >= M || !col_ok) continue;
-    const int q = (int)(m % g.Q);
-    const long t = m / g.Q;
-    const int p = (int)(t % g.P);
-    const int n = (int)(t / g.P);
+    const int q = m % g.Q;
+    const int t = m / g.Q;
+    const int p = t % g.P;
+    const int n = t / g.P;
     const int ho = p * g.osh + g.oh0, wo = q * g.osw + g.ow0;
     const long off = (((long)n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8;
     *reinterpret_cast<uint4*>(Y + off) = *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
@@ -250,7 +270,7 @@ void launch_cfg(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
   constexpr int BM = 64 * WM, BN = 64 * WN;
   const long M = (long)g.N * g.P * g.Q;
   const long tiles = ((M + BM - 1) / BM) * ((g.Kout + BN - 1) / BN);
-  const size_t stage = (size_t)(BM + BN) * BK * sizeof(bf16_t) * 2;
+  const size_t stage = (size_t)(BM + BN) * BK * sizeof(bf16_t) * 2 + 2 * DTF_MAX_TAPS * sizeof(int);
   const size_t epi = (size_t)BM * (BN + 8) * sizeof(bf16_t);
   const size_t lds = stage > epi ? stage : epi;
   hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN>), dim3((unsigned)tiles), dim3(kThreads),
@@ -265,6 +285,10 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
                     const TapTable& taps, int bk, hipStream_t st) {
   if (taps.n <= 0 || taps.n > DTF_MAX_TAPS) throw std::runtime_error("conv: bad tap count");
   if (g.Kout % 8) throw std::runtime_error("conv: Kout % 8 != 0");
+  const double xbytes = 2.0 * g.N * g.H * g.W * g.C, wbytes = 2.0 * g.Kout * g.Kpad;
+  const double m = (double)g.N * g.P * g.Q;
+  if (xbytes >= 2147483647.0 || wbytes >= 2147483647.0 || m >= 2147483647.0)
+    throw std::runtime_error("conv: tensor too large for 32-bit buffer offsets");
   const bool generic = (g.C % 32) != 0;
   const bool narrow = g.Kout <= 64;        // 256 x 64 tile for 64-wide layers
   if (generic) {

@@ -30,6 +30,7 @@ struct WgradGeom {
   int Kout;
   int ldw;          // dW row stride (>= T*C)
   long m_per_split; // reduction pixels per split (multiple of BKM)
+  long slab;        // floats per split slab (Kout * ldw)
 };
 
 namespace {
@@ -37,23 +38,36 @@ constexpr int kThreads = 256;
 constexpr int BM = 128, BN = 128, BKM = 64;
 constexpr int LDA = BM + 16;   // padded LDS row (elements): 288 B rows = 8-bank shift per row
 constexpr int LDB = BN + 16;
-// rows r and r+8 are read by the two 16-lane groups of one 32-lane half of a transposed read:
-// shift rows with bit 3 set by 128 B (32 banks) so the half's 8 rows cover all 64 banks.
-DTF_DEV int roff(int r, int ld) { return r * ld + ((r >> 3) & 1) * 64; }
-constexpr int OPER_A = BKM * LDA + 64;
-constexpr int OPER_B = BKM * LDB + 64;
+// rows r and r+8 are read by the two 16-lane groups of one 32-lane half of a transposed read;
+// with a 288-B pitch they land on the same banks, so rows with bit 3 set store their two 128-B
+// column halves swapped (a permutation within the row: element (r, c) lives at column
+// c ^ 64): the half's 8 rows then cover all 64 banks.
+DTF_DEV int lidx(int r, int c, int ld) { return r * ld + (c ^ (((r >> 3) & 1) << 6)); }
+constexpr int OPER_A = BKM * LDA;
+constexpr int OPER_B = BKM * LDB;
 
 typedef __attribute__((ext_vector_type(4))) short s4_t;
 typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+constexpr uint32_t kOOB = 0xFFFFFFF0u;   // byte offset the buffer range check always rejects
+
+DTF_DEV __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+DTF_DEV uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+DTF_DEV uint32_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+}
 
 DTF_DEV s4_t tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(p));
 }
 
-template <bool GENERIC>
+template <bool GENERIC, bool TR>
 __global__ void __launch_bounds__(kThreads, 2)
 conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
-                  float* __restrict__ dW, const WgradGeom g, const TapTableW taps) {
+                  float* __restrict__ dW, const WgradGeom g, const TapTableW taps, int mode) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr int STAGE = OPER_A + OPER_B;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -65,46 +79,51 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
   const int split = blockIdx.x / (tiles_m * tiles_n);
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int k0 = tm * BM, j0 = tn * BN;
-  const long M = (long)g.N * g.P * g.Q;
-  const long ms = (long)split * g.m_per_split;
-  long me = ms + g.m_per_split;
+  const int M = g.N * g.P * g.Q;               // host guarantees < 2^31
+  const int ms = split * (int)g.m_per_split;
+  int me = ms + (int)g.m_per_split;
   if (me > M) me = M;
-  const int nk = (int)((me - ms + BKM - 1) / BKM);
+  const int nk = (me - ms + BKM - 1) / BKM;
 
   // thread -> (row, chunk) for staging: 16 chunks of 8 channels per 128-wide row
   const int cc = tid & 15;
   const int rr = tid >> 4;         // 0..15, rows rr + 16*i
   uint4 ra[4], rb[4];
 
+  // tap table -> LDS with wave-uniform (scalar) kernel-argument reads only; per-lane lookups
+  // then come from LDS (never per-lane vector loads from the kernarg segment)
+  int* lds_taps = reinterpret_cast<int*>(lds + 2 * STAGE);   // [2][DTF_MAX_TAPS]
+  if (tid == 0)
+    for (int t = 0; t < taps.n; ++t) { lds_taps[t] = taps.dh[t]; lds_taps[DTF_MAX_TAPS + t] = taps.dw[t]; }
+  __syncthreads();
+
   // per-chunk tap / channel for the B (X) gather (fixed across K-steps)
   const int jc = j0 + cc * 8;
-  int bt = 0, bc = 0;
-  if (!GENERIC && jc < TC) { bt = jc / g.C; bc = jc - bt * g.C; }
-  const int bdh = (!GENERIC && jc < TC) ? taps.dh[bt] : 0;
-  const int bdw = (!GENERIC && jc < TC) ? taps.dw[bt] : 0;
+  const bool b_col_ok = jc < TC;
+  const int bt = b_col_ok ? jc / g.C : 0;
+  const int bc = jc - bt * g.C;
+  const int bdh = lds_taps[bt], bdw = lds_taps[DTF_MAX_TAPS + bt];
   const bool a_col_ok = (k0 + cc * 8) < g.Kout;
+  const auto rx = rsrc(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
+  const auto ry = rsrc(dY, (uint32_t)M * g.Kout * 2u);
+  const int HW = g.H * g.W;
 
+  // branch-free loads: padding / out-of-range lanes get an out-of-range buffer offset -> zeros
   auto load_stage = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const long m = ms + (long)kt * BKM + rr + 16 * i;
+      const int m = ms + kt * BKM + rr + 16 * i;
       const bool mok = m < me;
-      // A: dY row m, channels k0 + cc*8
-      if (mok && a_col_ok)
-        ra[i] = *reinterpret_cast<const uint4*>(dY + m * g.Kout + k0 + cc * 8);
-      else
-        ra[i] = make_uint4(0, 0, 0, 0);
-      const long mm = mok ? m : 0;
-      const int q = (int)(mm % g.Q);
-      const long t = mm / g.Q;
-      const int p = (int)(t % g.P);
-      const int n = (int)(t / g.P);
+      ra[i] = bload16(ry, (mok && a_col_ok) ? (uint32_t)((m * g.Kout + k0 + cc * 8) * 2) : kOOB);
+      const int mm = mok ? m : 0;
+      const int q = mm % g.Q;
+      const int t = mm / g.Q;
+      const int p = t % g.P;
+      const int n = t / g.P;
       if constexpr (!GENERIC) {
         const int h = p * g.sh + bdh, w = q * g.sw + bdw;
-        if (mok && jc < TC && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
-          rb[i] = *reinterpret_cast<const uint4*>(X + (((long)n * g.H + h) * g.W + w) * g.C + bc);
-        else
-          rb[i] = make_uint4(0, 0, 0, 0);
+        const bool ok = mok && b_col_ok && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+        rb[i] = bload16(rx, ok ? (uint32_t)(((n * HW + h * g.W + w) * g.C + bc) * 2) : kOOB);
       } else {
         uint32_t wv[4];
 #pragma unroll
@@ -113,14 +132,12 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
 #pragma unroll
           for (int e1 = 0; e1 < 2; ++e1) {
             const int j = jc + e2 * 2 + e1;
-            uint32_t v = 0;
-            if (mok && j < TC) {
-              const int tt = j / g.C, c = j - tt * g.C;
-              const int h = p * g.sh + taps.dh[tt], w = q * g.sw + taps.dw[tt];
-              if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
-                v = X[(((long)n * g.H + h) * g.W + w) * g.C + c];
-            }
-            pair |= v << (16 * e1);
+            const int tt = j < TC ? j / g.C : 0;
+            const int c = j - tt * g.C;
+            const int h = p * g.sh + lds_taps[tt], w = q * g.sw + lds_taps[DTF_MAX_TAPS + tt];
+            const bool ok = mok && j < TC && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+            pair |= bload2(rx, ok ? (uint32_t)(((n * HW + h * g.W + w) * g.C + c) * 2) : kOOB)
+                    << (16 * e1);
           }
           wv[e2] = pair;
         }
@@ -133,8 +150,8 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
     bf16_t* sb = sa + OPER_A;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<uint4*>(sa + roff(rr + 16 * i, LDA) + cc * 8) = ra[i];
-      *reinterpret_cast<uint4*>(sb + roff(rr + 16 * i, LDB) + cc * 8) = rb[i];
+      *reinterpret_cast<uint4*>(sa + lidx(rr + 16 * i, cc * 8, LDA)) = ra[i];
+      *reinterpret_cast<uint4*>(sb + lidx(rr + 16 * i, cc * 8, LDB)) = rb[i];
     }
   };
 
@@ -153,7 +170,7 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
   const int li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = mode == 2 ? 0 : (kt & 1);
     if (kt + 1 < nk) load_stage(kt + 1);
     const bf16_t* sa = lds + cur * STAGE;
     const bf16_t* sb = sa + OPER_A;
@@ -162,17 +179,29 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
       bf16x8_t af[4], bfr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int r0 = 32 * ks + 8 * gq + tq, c0 = wm * 64 + 16 * i + 4 * tp;
-        const s4_t lo = tr_read(sa + roff(r0, LDA) + c0);
-        const s4_t hi = tr_read(sa + roff(r0 + 4, LDA) + c0);
-        af[i] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if constexpr (TR) {
+          const int r0 = 32 * ks + 8 * gq + tq, c0 = wm * 64 + 16 * i + 4 * tp;
+          const s4_t lo = tr_read(sa + lidx(r0, c0, LDA));
+          const s4_t hi = tr_read(sa + lidx(r0 + 4, c0, LDA));
+          af[i] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        } else {
+          const int c = wm * 64 + 16 * i + li;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) af[i][e] = (short)sa[lidx(32 * ks + 8 * gq + e, c, LDA)];
+        }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int r0 = 32 * ks + 8 * gq + tq, c0 = wn * 64 + 16 * j + 4 * tp;
-        const s4_t lo = tr_read(sb + roff(r0, LDB) + c0);
-        const s4_t hi = tr_read(sb + roff(r0 + 4, LDB) + c0);
-        bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if constexpr (TR) {
+          const int r0 = 32 * ks + 8 * gq + tq, c0 = wn * 64 + 16 * j + 4 * tp;
+          const s4_t lo = tr_read(sb + lidx(r0, c0, LDB));
+          const s4_t hi = tr_read(sb + lidx(r0 + 4, c0, LDB));
+          bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        } else {
+          const int c = wn * 64 + 16 * j + li;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[j][e] = (short)sb[lidx(32 * ks + 8 * gq + e, c, LDB)];
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -180,53 +209,109 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_stage(cur ^ 1);
+    if (mode >= 1) __syncthreads();
+    if (kt + 1 < nk) store_stage(mode == 2 ? 0 : (cur ^ 1));
     __syncthreads();
   }
-  // epilogue: fp32 atomic add (split-K) — rows = k, cols = j
+  // epilogue: this split's fp32 partial tile goes into its own slab (split s writes
+  // dW + s * slab); a separate launch sums the slabs in split order -> deterministic, no atomics.
+  // The accumulators are staged through LDS by VALU moves (never consumed directly as memory-op
+  // data right behind the MFMA chain) after explicit wait states, then stored row-coalesced.
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr int LDO = BN + 4;                       // fp32 tile [BM][BN+4] = 66 KB
+  float* so = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = j0 + wn * 64 + 16 * j + li;
-      if (col >= TC) continue;
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = k0 + wm * 64 + 16 * i + 4 * gq + r;
-        if (row < g.Kout) atomicAdd(dW + (long)row * g.ldw + col, acc[i][j][r]);
+        const float v = acc[i][j][r] + 0.0f;
+        so[(wm * 64 + 16 * i + 4 * gq + r) * LDO + wn * 64 + 16 * j + li] = v;
       }
+  __syncthreads();
+  float* out = dW + (long)split * g.slab;
+  for (int idx = tid; idx < BM * BN; idx += kThreads) {
+    const int r = idx / BN, c = idx % BN;
+    const int row = k0 + r, col = j0 + c;
+    if (row < g.Kout && col < TC) out[(long)row * g.ldw + col] = so[r * LDO + c];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n, long slab,
+                   int nsplit) {
+  const long n4 = n >> 2;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 s = reinterpret_cast<const float4*>(ws)[i];
+    for (int k = 1; k < nsplit; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(ws + k * slab)[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
+  for (long i = n4 * 4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float s = ws[i];
+    for (int k = 1; k < nsplit; ++k) s += ws[k * slab + i];
+    out[i] = s;
+  }
 }
 }  // namespace
 
-int dtf_conv_wgrad_splits(long M, int Kout, int TC) {
+// Number of reduction splits: aim for ~1024 blocks (4 per CU), keep >= 4 K-steps per split and
+// the fp32 slab workspace (splits x Kout x TC) under `ws_cap` floats.
+int dtf_conv_wgrad_splits(long M, int Kout, int TC, long ws_cap) {
   const long tiles = (long)((Kout + BM - 1) / BM) * ((TC + BN - 1) / BN);
-  long splits = (1024 + tiles - 1) / tiles;              // ~4 blocks per CU in flight
-  const long max_splits = (M + 4 * BKM - 1) / (4 * BKM);  // >= 4 K-steps per split
+  long splits = (1024 + tiles - 1) / tiles;
+  const long max_splits = (M + 4 * BKM - 1) / (4 * BKM);
   if (splits > max_splits) splits = max_splits;
+  const long cap = ws_cap / ((long)Kout * TC);
+  if (splits > cap) splits = cap;
   if (splits < 1) splits = 1;
-  return (int)splits;
+  // normalise so that every split gets work (M rounded to BKM multiples)
+  long mps = (M + splits - 1) / splits;
+  mps = ((mps + BKM - 1) / BKM) * BKM;
+  return (int)((M + mps - 1) / mps);
 }
 
-// dW must be zero-filled by the caller (atomic accumulation).
-void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, WgradGeom g,
-                    const TapTableW& taps, hipStream_t st) {
+// splits == 1: dW written directly.  splits > 1: `ws` holds splits x Kout x ldw floats; the
+// slabs are summed (in split order) into dW by a second launch.
+void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, WgradGeom g,
+                    const TapTableW& taps, int splits, int tr_mode, hipStream_t st) {
   if (taps.n <= 0 || taps.n > DTF_MAX_TAPS) throw std::runtime_error("wgrad: bad tap count");
   if (g.Kout % 8) throw std::runtime_error("wgrad: Kout % 8 != 0");
+  if (splits < 1 || (splits > 1 && !ws)) throw std::runtime_error("wgrad: bad split workspace");
+  if (2.0 * g.N * g.H * g.W * g.C >= 2147483647.0 || 2.0 * g.N * g.P * g.Q * g.Kout >= 2147483647.0)
+    throw std::runtime_error("wgrad: tensor too large for 32-bit buffer offsets");
   const long M = (long)g.N * g.P * g.Q;
   const int TC = taps.n * g.C;
-  const int splits = dtf_conv_wgrad_splits(M, g.Kout, TC);
   long mps = (M + splits - 1) / splits;
   mps = ((mps + BKM - 1) / BKM) * BKM;
   g.m_per_split = mps;
+  g.slab = (long)g.Kout * g.ldw;
   const int nsplit = (int)((M + mps - 1) / mps);
+  if (nsplit != splits) throw std::runtime_error("wgrad: split plan mismatch");
+  float* target = splits > 1 ? ws : dW;
   const long tiles = (long)((g.Kout + BM - 1) / BM) * ((TC + BN - 1) / BN);
-  const size_t lds = (size_t)2 * (OPER_A + OPER_B) * sizeof(bf16_t);
+  const size_t lds = (size_t)2 * (OPER_A + OPER_B) * sizeof(bf16_t) + 2 * DTF_MAX_TAPS * sizeof(int);
   const bool generic = (g.C % 8) != 0;
-  if (generic)
-    hipLaunchKernelGGL(conv_wgrad_kernel<true>, dim3((unsigned)(tiles * nsplit)), dim3(kThreads),
-                       lds, st, X, dY, dW, g, taps);
-  else
-    hipLaunchKernelGGL(conv_wgrad_kernel<false>, dim3((unsigned)(tiles * nsplit)), dim3(kThreads),
-                       lds, st, X, dY, dW, g, taps);
+  const dim3 grid((unsigned)(tiles * nsplit));
+  if (!(tr_mode & 1)) {  // debug path: element-wise LDS reads instead of ds_read_b64_tr_b16
+    if (generic) hipLaunchKernelGGL((conv_wgrad_kernel<true, false>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<false, false>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
+  } else if (generic) {
+    hipLaunchKernelGGL((conv_wgrad_kernel<true, true>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
+  } else {
+    hipLaunchKernelGGL((conv_wgrad_kernel<false, true>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
+  }
+  if (splits > 1) {
+    const long n = g.slab;
+    long blocks = (n / 4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ws, dW, n,
+                       g.slab, nsplit);
+  }
 }

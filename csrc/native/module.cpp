@@ -1,0 +1,169 @@
+// pybind11 module `_dtf_native`: host runtime of distributedtensorflow_amd.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+
+#include "bundle.h"
+#include "crc32c.h"
+#include "data.h"
+#include "records.h"
+
+namespace py = pybind11;
+using namespace dtf;
+
+static py::bytes to_bytes(const std::string& s) { return py::bytes(s); }
+
+template <typename T>
+static py::array_t<T> vec_to_array(std::vector<T>&& v, std::vector<py::ssize_t> shape) {
+  auto* heap = new std::vector<T>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete static_cast<std::vector<T>*>(p); });
+  return py::array_t<T>(shape, heap->data(), owner);
+}
+
+PYBIND11_MODULE(_dtf_native, m) {
+  m.doc() = "distributedtensorflow_amd host runtime (crc32c, TFRecord/tfevents, TF-V2 tensor "
+            "bundle, idx reader, prefetching batcher)";
+
+  m.def("crc32c", [](py::bytes b, uint32_t init) {
+    std::string s = b;
+    return crc32c_extend(init, s.data(), s.size());
+  }, py::arg("data"), py::arg("init") = 0);
+  m.def("masked_crc32c", [](py::bytes b) {
+    std::string s = b;
+    return crc_mask(crc32c(s.data(), s.size()));
+  });
+  m.def("mask", &crc_mask);
+  m.def("unmask", &crc_unmask);
+
+  py::class_<RecordWriter>(m, "RecordWriter")
+      .def(py::init<const std::string&, bool>(), py::arg("path"), py::arg("append") = false)
+      .def("write", [](RecordWriter& w, py::bytes b) { w.write(std::string(b)); })
+      .def("flush", &RecordWriter::flush)
+      .def("close", &RecordWriter::close)
+      .def_property_readonly("path", &RecordWriter::path);
+
+  py::class_<RecordReader>(m, "RecordReader")
+      .def(py::init<const std::string&>())
+      .def("next", [](RecordReader& r) -> py::object {
+        std::string s;
+        if (!r.next(&s)) return py::none();
+        return py::bytes(s);
+      });
+
+  m.def("encode_scalar_event", [](double wall, int64_t step,
+                                  std::vector<std::pair<std::string, float>> kv) {
+    return to_bytes(encode_scalar_event(wall, step, kv));
+  });
+  m.def("encode_histogram_event", [](double wall, int64_t step, const std::string& tag,
+                                     std::vector<double> values, int nbuckets) {
+    return to_bytes(encode_histogram_event(wall, step, tag, values, nbuckets));
+  });
+  m.def("parse_event", [](py::bytes b) {
+    ParsedEvent e = parse_event(std::string(b));
+    py::dict d;
+    d["wall_time"] = e.wall_time;
+    d["step"] = e.step;
+    d["file_version"] = e.file_version;
+    py::list sc;
+    for (auto& kv : e.scalars) sc.append(py::make_tuple(kv.first, kv.second));
+    d["scalars"] = sc;
+    py::list hs;
+    for (auto& kv : e.histograms) hs.append(py::make_tuple(kv.first, kv.second.first, kv.second.second));
+    d["histograms"] = hs;
+    return d;
+  });
+
+  py::class_<EventsWriter>(m, "EventsWriter")
+      .def(py::init<const std::string&, const std::string&>(), py::arg("prefix"),
+           py::arg("suffix") = "")
+      .def("write_event", [](EventsWriter& w, py::bytes b) { w.write_event(std::string(b)); })
+      .def("flush", &EventsWriter::flush)
+      .def("close", &EventsWriter::close)
+      .def_property_readonly("path", &EventsWriter::path);
+
+  py::class_<BundleWriter>(m, "BundleWriter")
+      .def(py::init<const std::string&, int>(), py::arg("prefix"), py::arg("num_shards") = 1)
+      .def("add", [](BundleWriter& w, const std::string& name, int dtype,
+                     std::vector<int64_t> shape, py::buffer buf, int shard) {
+        py::buffer_info info = buf.request();
+        py::ssize_t expect = info.itemsize;
+        for (py::ssize_t i = info.ndim - 1; i >= 0; --i) {   // require C-contiguous input
+          if (info.shape[i] > 1 && info.strides[i] != expect)
+            throw std::runtime_error("BundleWriter.add expects a C-contiguous buffer");
+          expect *= info.shape[i];
+        }
+        w.add(name, dtype, shape, info.ptr, (size_t)(info.size * info.itemsize), shard);
+      }, py::arg("name"), py::arg("dtype"), py::arg("shape"), py::arg("data"),
+         py::arg("shard") = 0)
+      .def("finish", &BundleWriter::finish);
+
+  py::class_<BundleReader>(m, "BundleReader")
+      .def(py::init<const std::string&>())
+      .def("keys", &BundleReader::keys)
+      .def("num_shards", &BundleReader::num_shards)
+      .def("entry", [](BundleReader& r, const std::string& name) {
+        const BundleEntry& e = r.entry(name);
+        py::dict d;
+        d["dtype"] = e.dtype;
+        d["shape"] = e.shape;
+        d["shard_id"] = e.shard_id;
+        d["offset"] = e.offset;
+        d["size"] = e.size;
+        d["crc32c"] = e.crc32c;
+        return d;
+      })
+      .def("read", [](BundleReader& r, const std::string& name) { return py::bytes(r.read(name)); });
+
+  m.def("read_idx", [](const std::string& path) {
+    IdxFile f = read_idx(path);
+    std::vector<py::ssize_t> shape(f.dims.begin(), f.dims.end());
+    return py::make_tuple(f.magic, vec_to_array<uint8_t>(std::move(f.data), shape));
+  });
+  m.def("write_idx", [](const std::string& path, py::array_t<uint8_t, py::array::c_style> a) {
+    std::vector<uint32_t> dims;
+    for (py::ssize_t i = 0; i < a.ndim(); ++i) dims.push_back((uint32_t)a.shape(i));
+    write_idx(path, dims, a.data());
+  });
+
+  py::class_<BatchPrefetcher>(m, "BatchPrefetcher")
+      .def(py::init([](py::array_t<uint8_t, py::array::c_style> images,
+                       py::object labels, int batch, bool shuffle, uint64_t seed, int threads,
+                       int depth, float scale, bool drop_remainder, int64_t shard_index,
+                       int64_t num_shards) {
+             const int64_t n = images.shape(0);
+             const int64_t dim = images.size() / std::max<int64_t>(n, 1);
+             const int64_t* lab = nullptr;
+             py::array_t<int64_t, py::array::c_style | py::array::forcecast> la;
+             if (!labels.is_none()) {
+               la = labels.cast<py::array_t<int64_t, py::array::c_style | py::array::forcecast>>();
+               if (la.size() != n) throw std::runtime_error("labels/images length mismatch");
+               lab = la.data();
+             }
+             auto* p = new BatchPrefetcher(images.data(), lab, n, dim, batch, shuffle, seed,
+                                           threads, depth, scale, drop_remainder, shard_index,
+                                           num_shards);
+             return std::unique_ptr<BatchPrefetcher>(p);
+           }),
+           py::arg("images"), py::arg("labels"), py::arg("batch"), py::arg("shuffle") = false,
+           py::arg("seed") = 0, py::arg("threads") = 2, py::arg("depth") = 4,
+           py::arg("scale") = 1.0f / 255.0f, py::arg("drop_remainder") = true,
+           py::arg("shard_index") = 0, py::arg("num_shards") = 1,
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("next", [](BatchPrefetcher& p, int64_t dim) {
+        std::vector<float> x;
+        std::vector<int32_t> y;
+        int rows;
+        {
+          py::gil_scoped_release nogil;
+          rows = p.next(&x, &y);
+        }
+        x.resize((size_t)rows * dim);
+        y.resize(rows);
+        return py::make_tuple(vec_to_array<float>(std::move(x), {rows, (py::ssize_t)dim}),
+                              vec_to_array<int32_t>(std::move(y), {rows}));
+      })
+      .def("epoch", &BatchPrefetcher::epoch)
+      .def("stop", &BatchPrefetcher::stop);
+}

@@ -132,17 +132,25 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding):
     return dx
 
 
+_WGRAD_WS_CAP = 32 << 20   # floats of split-K slab workspace per call (128 MB)
+
+
 def conv2d_wgrad(x, dy, w_shape, stride, padding):
+    """dW [K,R,S,C] fp32 via the MFMA wgrad kernel; deterministic split-K slab reduction."""
     K, R, S, C = w_shape
     n, h, wd, c = x.shape
     sh, sw = _pair(stride)
     pt, pb, pl, pr = resolve_padding(padding, h, wd, R, S, stride)
     _, P, Q, _ = dy.shape
     taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
-    dW = torch.zeros(K, R * S * C, device=x.device, dtype=torch.float32)
-    geom = [n, h, wd, c, P, Q, sh, sw, K, R * S * C]
-    _K.conv_wgrad(x.data_ptr(), dy.contiguous().data_ptr(), dW.data_ptr(), geom,
-                  [t[0] for t in taps], [t[1] for t in taps], _st())
+    tc = R * S * C
+    splits = _K.conv_wgrad_splits(n * P * Q, K, tc, _WGRAD_WS_CAP)
+    dW = torch.empty(K, tc, device=x.device, dtype=torch.float32)
+    ws = (torch.empty(splits * K * tc, device=x.device, dtype=torch.float32)
+          if splits > 1 else None)
+    geom = [n, h, wd, c, P, Q, sh, sw, K, tc]
+    _K.conv_wgrad(x.data_ptr(), dy.contiguous().data_ptr(), dW.data_ptr(), _p(ws), geom,
+                  [t[0] for t in taps], [t[1] for t in taps], splits, _st())
     return dW.reshape(K, R, S, C)
 
 
