@@ -93,20 +93,42 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
   }
 }
 
-__global__ void bn_fwd_finalize_kernel(const float* __restrict__ partial, int G, int C, long M,
-                                       const float* __restrict__ gamma,
-                                       const float* __restrict__ beta,
-                                       float* __restrict__ run_mean, float* __restrict__ run_var,
-                                       float momentum, float eps, float* __restrict__ mean,
-                                       float* __restrict__ invstd, float* __restrict__ scale,
-                                       float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Combine the per-block partial slabs: one block = 32 channels x 8 partial slots; each slot sums
+// every 8th partial row (coalesced 128-B reads) in fp64, slots are combined in a fixed order
+// (deterministic).  Returns true in the slot-0 lane that owns channel c.
+DTF_DEV bool combine_partials(const float* __restrict__ partial, int G, int C, double* a,
+                              double* b, int* c_out) {
+  __shared__ double red[2][8][32];
+  const int cl = threadIdx.x & 31, slot = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
   double s = 0.0, ss = 0.0;
-  for (int g = 0; g < G; ++g) {
-    s += partial[((long)g * 2 + 0) * C + c];
-    ss += partial[((long)g * 2 + 1) * C + c];
-  }
+  if (c < C)
+    for (int g = slot; g < G; g += 8) {
+      s += partial[((long)g * 2 + 0) * C + c];
+      ss += partial[((long)g * 2 + 1) * C + c];
+    }
+  red[0][slot][cl] = s;
+  red[1][slot][cl] = ss;
+  __syncthreads();
+  if (slot != 0 || c >= C) return false;
+  s = 0.0;
+  ss = 0.0;
+  for (int k = 0; k < 8; ++k) { s += red[0][k][cl]; ss += red[1][k][cl]; }
+  *a = s;
+  *b = ss;
+  *c_out = c;
+  return true;
+}
+
+__global__ void __launch_bounds__(256)
+bn_fwd_finalize_kernel(const float* __restrict__ partial, int G, int C, long M,
+                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                       float* __restrict__ run_mean, float* __restrict__ run_var, float momentum,
+                       float eps, float* __restrict__ mean, float* __restrict__ invstd,
+                       float* __restrict__ scale, float* __restrict__ shift) {
+  double s, ss;
+  int c;
+  if (!combine_partials(partial, G, C, &s, &ss, &c)) return;
   const double mu = s / (double)M;
   double var = ss / (double)M - mu * mu;
   if (var < 0) var = 0;
@@ -171,20 +193,15 @@ bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int G, int C, long M,
-                                       const float* __restrict__ gamma,
-                                       const float* __restrict__ mean,
-                                       const float* __restrict__ invstd,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ coefA, float* __restrict__ coefB,
-                                       float* __restrict__ coefC, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double sdz = 0.0, sdzx = 0.0;
-  for (int g = 0; g < G; ++g) {
-    sdz += partial[((long)g * 2 + 0) * C + c];
-    sdzx += partial[((long)g * 2 + 1) * C + c];
-  }
+__global__ void __launch_bounds__(256)
+bn_bwd_finalize_kernel(const float* __restrict__ partial, int G, int C, long M,
+                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                       const float* __restrict__ invstd, float* __restrict__ dgamma,
+                       float* __restrict__ dbeta, float* __restrict__ coefA,
+                       float* __restrict__ coefB, float* __restrict__ coefC, int accumulate) {
+  double sdz, sdzx;
+  int c;
+  if (!combine_partials(partial, G, C, &sdz, &sdzx, &c)) return;
   const float db = (float)sdz, dg = (float)sdzx;
   if (accumulate) { dgamma[c] += dg; dbeta[c] += db; }
   else { dgamma[c] = dg; dbeta[c] = db; }
@@ -257,7 +274,7 @@ void dtf_bn_fwd_finalize(const float* partial, long M, int C, const float* gamma
                          hipStream_t st) {
   int rpb;
   const int G = stats_grid(M, C, &rpb);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, partial, G,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, partial, G,
                      C, M, gamma, beta, run_mean, run_var, momentum, eps, mean, invstd, scale,
                      shift);
 }
@@ -293,7 +310,7 @@ void dtf_bn_bwd_finalize(const float* partial, long M, int C, const float* gamma
                          hipStream_t st) {
   int rpb;
   const int G = stats_grid(M, C, &rpb);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, partial, G, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, partial, G, C,
                      M, gamma, mean, invstd, dgamma, dbeta, coefA, coefB, coefC, accumulate);
 }
 

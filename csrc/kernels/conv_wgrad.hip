@@ -240,22 +240,29 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
   }
 }
 
+// Deterministic slab sum: block = 64 float4 columns x 4 split groups; group q sums splits
+// q, q+4, ... in order, the 4 group partials are added in a fixed order through LDS.
 __global__ void __launch_bounds__(256)
 slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n, long slab,
                    int nsplit) {
+  __shared__ float4 red[4][64];
+  const int col = threadIdx.x & 63, q = threadIdx.x >> 6;
   const long n4 = n >> 2;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    float4 s = reinterpret_cast<const float4*>(ws)[i];
-    for (int k = 1; k < nsplit; ++k) {
+  const long i = (long)blockIdx.x * 64 + col;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4)
+    for (int k = q; k < nsplit; k += 4) {
       const float4 v = reinterpret_cast<const float4*>(ws + k * slab)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    reinterpret_cast<float4*>(out)[i] = s;
-  }
-  for (long i = n4 * 4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    float s = ws[i];
-    for (int k = 1; k < nsplit; ++k) s += ws[k * slab + i];
-    out[i] = s;
+  red[q][col] = s;
+  __syncthreads();
+  if (q == 0 && i < n4) {
+    float4 t = red[0][col];
+    for (int k = 1; k < 4; ++k) {
+      t.x += red[k][col].x; t.y += red[k][col].y; t.z += red[k][col].z; t.w += red[k][col].w;
+    }
+    reinterpret_cast<float4*>(out)[i] = t;
   }
 }
 }  // namespace
@@ -307,11 +314,9 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
     hipLaunchKernelGGL((conv_wgrad_kernel<false, true>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
   }
   if (splits > 1) {
-    const long n = g.slab;
-    long blocks = (n / 4 + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ws, dW, n,
-                       g.slab, nsplit);
+    // slab = Kout * ldw floats, Kout % 8 == 0 -> slab % 4 == 0 (float4 path covers it)
+    const long n4 = g.slab / 4;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, ws,
+                       dW, g.slab, g.slab, nsplit);
   }
 }
