@@ -1,0 +1,97 @@
+"""Local cluster launcher: start every task of a PS/worker cluster as its own process.
+
+The reference starts each task by hand (``python run_mnist_distributed.py --job_name=ps
+--task_index=0`` on every host; README).  ``launch_local`` does the same on one host: it writes a
+``config.json`` (127.0.0.1, free ports), spawns ``num_ps`` PS and ``num_workers`` worker
+processes of ``script``, streams their logs to files, waits for the workers, and makes sure the
+PS processes exit (they return from ``join()`` when all workers stopped; anything still alive
+after ``grace_s`` is terminated by PID — never by pattern).
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+
+def free_ports(n):
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def write_config(path, num_ps, num_workers):
+    ports = free_ports(num_ps + num_workers)
+    cfg = {"ps": {f"ps:{i}": f"127.0.0.1:{ports[i]}" for i in range(num_ps)},
+           "workers": {f"worker:{i}": f"127.0.0.1:{ports[num_ps + i]}"
+                       for i in range(num_workers)}}
+    with open(path, "w") as f:
+        json.dump(cfg, f, indent=2)
+    return cfg
+
+
+def launch_local(script, num_ps=1, num_workers=2, workdir=None, extra_args=(), env=None,
+                 timeout_s=600, grace_s=30, gpus_per_host=None):
+    workdir = workdir or os.getcwd()
+    os.makedirs(workdir, exist_ok=True)
+    cfg_path = os.path.join(workdir, "config.json")
+    write_config(cfg_path, num_ps, num_workers)
+    base_env = dict(os.environ)
+    base_env.update(env or {})
+    procs = []
+    for job, n in (("ps", num_ps), ("worker", num_workers)):
+        for i in range(n):
+            e = dict(base_env)
+            if job == "ps":
+                e["HIP_VISIBLE_DEVICES"] = e.get("DTF_PS_VISIBLE_DEVICES", "")
+            elif gpus_per_host:
+                e["LOCAL_RANK"] = str(i % gpus_per_host)
+            log = open(os.path.join(workdir, f"{job}{i}.log"), "w")
+            cmd = [sys.executable, script, f"--job_name={job}", f"--task_index={i}",
+                   f"--config={cfg_path}", *extra_args]
+            p = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, env=e, cwd=workdir)
+            procs.append((job, i, p, log))
+    t0 = time.time()
+    rc = {}
+    try:
+        for job, i, p, log in procs:
+            if job != "worker":
+                continue
+            left = max(1.0, timeout_s - (time.time() - t0))
+            rc[(job, i)] = p.wait(timeout=left)
+        for job, i, p, log in procs:
+            if job == "ps":
+                try:
+                    rc[(job, i)] = p.wait(timeout=grace_s)
+                except subprocess.TimeoutExpired:
+                    p.terminate()
+                    rc[(job, i)] = p.wait(timeout=10)
+    finally:
+        for job, i, p, log in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+            log.close()
+    return rc, {f"{j}{i}": os.path.join(workdir, f"{j}{i}.log") for j, i, _, _ in procs}
+
+
+if __name__ == "__main__":
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("script")
+    ap.add_argument("--num_ps", type=int, default=1)
+    ap.add_argument("--num_workers", type=int, default=2)
+    ap.add_argument("--workdir", default=None)
+    a, rest = ap.parse_known_args()
+    codes, logs = launch_local(a.script, a.num_ps, a.num_workers, a.workdir, rest)
+    print(json.dumps({"exit_codes": {f"{k[0]}{k[1]}": v for k, v in codes.items()},
+                      "logs": logs}, indent=2))

@@ -1,0 +1,8 @@
+"""Input pipelines: tf.data-style Dataset, MNIST idx (offline synthetic fallback), synthetic
+ImageNet / MLM generators for benchmarks."""
+from . import mnist
+from .dataset import Dataset, Iterator, NativeBatchDataset
+from .synthetic import SyntheticImageNet, SyntheticMLM
+
+__all__ = ["mnist", "Dataset", "Iterator", "NativeBatchDataset", "SyntheticImageNet",
+           "SyntheticMLM"]

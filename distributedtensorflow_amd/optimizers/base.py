@@ -154,10 +154,20 @@ class Optimizer:
     def apply_gradients(self, grads_and_vars=None, global_step=None):
         assert self.space is not None, "call build()/compute_gradients() first"
         self.iterations += 1
+        if getattr(self._reducer, "applies_update", False):
+            # parameter-server strategies: the PS owning the variables applies the update
+            step = self._reducer.apply_remote(self)
+            if global_step is not None and step is not None:
+                global_step.assign(step) if hasattr(global_step, "assign") else None
+            return step
         self._apply(self._reducer.grad_scale())
         if global_step is not None:
             gs.increment(global_step)
         return None
+
+    def get_config(self) -> dict:
+        """Serializable description (shipped to parameter-server tasks)."""
+        raise NotImplementedError
 
     def minimize(self, loss, global_step=None, var_list=None):
         """backward -> (cross-replica reduce, overlapped) -> fused update -> global_step += 1."""
@@ -167,11 +177,25 @@ class Optimizer:
         return self.apply_gradients(None, global_step)
 
     # ------------------------------------------------------------------ update
-    def _apply(self, gscale):
-        if self.space.device.type == "cuda":
-            self._apply_native(gscale)
-        else:
-            self._apply_reference(gscale)
+    def _apply(self, gscale, rng=None):
+        """Run the update over the whole flat buffer, or only over ``rng = (start, end)`` (the
+        slice a parameter-server shard owns)."""
+        self._range = rng
+        try:
+            if self.space.device.type == "cuda":
+                self._apply_native(gscale)
+            else:
+                self._apply_reference(gscale)
+        finally:
+            self._range = None
+
+    def _regions(self):
+        regs = self.space.regions()
+        rng = getattr(self, "_range", None)
+        if rng is None:
+            return regs
+        lo, hi = rng
+        return [(max(s, lo), min(e, hi), d) for s, e, d in regs if min(e, hi) > max(s, lo)]
 
     def nonfinite_flag(self):
         return bool(self._nonfinite.item()) if self._nonfinite is not None else False

@@ -35,10 +35,14 @@ class GradientDescentOptimizer(Optimizer):
     def _build_slots(self):
         self._dummy = self.space.new_slot()
 
+    def get_config(self):
+        return {"type": "sgd", "learning_rate": self.learning_rate(),
+                "weight_decay": self.weight_decay}
+
     def _apply_native(self, gscale):
         self._lr_dev[0].fill_(self.learning_rate())
         K, sp = _K(), self.space
-        for s, e, dec in sp.regions():
+        for s, e, dec in self._regions():
             K.sgd_momentum(sp.master.data_ptr() + 4 * s, sp.grad.data_ptr() + 4 * s,
                            self._dummy.data_ptr() + 4 * s, _sh(sp, s), e - s,
                            self._lr_dev.data_ptr(), 0.0, self.weight_decay if dec else 0.0,
@@ -48,7 +52,7 @@ class GradientDescentOptimizer(Optimizer):
         lr = self.learning_rate()
         sp = self.space
         with torch.no_grad():
-            for s, e, dec in sp.regions():
+            for s, e, dec in self._regions():
                 g = sp.grad[s:e] * gscale + (self.weight_decay if dec else 0.0) * sp.master[s:e]
                 sp.master[s:e].sub_(lr * g)
 
@@ -69,10 +73,15 @@ class MomentumOptimizer(Optimizer):
     def _build_slots(self):
         self.slots = [FlatSlot("Momentum", self.space.new_slot())]
 
+    def get_config(self):
+        return {"type": "momentum", "learning_rate": self.learning_rate(),
+                "momentum": self.momentum, "use_nesterov": self.use_nesterov,
+                "weight_decay": self.weight_decay}
+
     def _apply_native(self, gscale):
         self._lr_dev[0].fill_(self.learning_rate())
         K, sp, a = _K(), self.space, self.slots[0].buf
-        for s, e, dec in sp.regions():
+        for s, e, dec in self._regions():
             K.sgd_momentum(sp.master.data_ptr() + 4 * s, sp.grad.data_ptr() + 4 * s,
                            a.data_ptr() + 4 * s, _sh(sp, s), e - s, self._lr_dev.data_ptr(),
                            float(self.momentum), self.weight_decay if dec else 0.0, gscale,
@@ -82,7 +91,7 @@ class MomentumOptimizer(Optimizer):
         lr, mu = self.learning_rate(), self.momentum
         sp, a = self.space, self.slots[0].buf
         with torch.no_grad():
-            for s, e, dec in sp.regions():
+            for s, e, dec in self._regions():
                 g = sp.grad[s:e] * gscale + (self.weight_decay if dec else 0.0) * sp.master[s:e]
                 a[s:e].mul_(mu).add_(g)
                 step = g + mu * a[s:e] if self.use_nesterov else a[s:e]
@@ -107,6 +116,10 @@ class AdamOptimizer(Optimizer):
         self.slots = [FlatSlot("Adam", self.space.new_slot()),
                       FlatSlot("Adam_1", self.space.new_slot())]
 
+    def get_config(self):
+        return {"type": "adam", "learning_rate": self.learning_rate(), "beta1": self.beta1,
+                "beta2": self.beta2, "epsilon": self.epsilon}
+
     def lr_t(self):
         return tf_adam_lr_t(self.learning_rate(), self.beta1, self.beta2, self.iterations)
 
@@ -114,7 +127,7 @@ class AdamOptimizer(Optimizer):
         self._lr_dev[0].fill_(self.lr_t())
         K, sp = _K(), self.space
         m, v = self.slots[0].buf, self.slots[1].buf
-        for s, e, dec in sp.regions():
+        for s, e, dec in self._regions():
             K.adam(sp.master.data_ptr() + 4 * s, sp.grad.data_ptr() + 4 * s, m.data_ptr() + 4 * s,
                    v.data_ptr() + 4 * s, _sh(sp, s), e - s, self._lr_dev.data_ptr(),
                    float(self.beta1), float(self.beta2), float(self.epsilon),
@@ -126,10 +139,13 @@ class AdamOptimizer(Optimizer):
         m, v = self.slots[0].buf, self.slots[1].buf
         b1, b2 = self.beta1, self.beta2
         with torch.no_grad():
-            g = sp.grad * gscale
-            m.mul_(b1).add_((1 - b1) * g)
-            v.mul_(b2).add_((1 - b2) * g * g)
-            sp.master.sub_(lr_t * m / (v.sqrt() + self.epsilon))
+            for s, e, dec in self._regions():
+                g = sp.grad[s:e] * gscale
+                p = sp.master[s:e]
+                m[s:e].mul_(b1).add_((1 - b1) * g)
+                v[s:e].mul_(b2).add_((1 - b2) * g * g)
+                wd = self.weight_decay if dec else 0.0
+                p.sub_(lr_t * m[s:e] / (v[s:e].sqrt() + self.epsilon) + lr_t * wd * p)
 
     def non_slot_variables(self):
         # TF1 keeps the bias-correction powers as variables beta1_power / beta2_power
@@ -150,19 +166,26 @@ class AdagradOptimizer(Optimizer):
     def _build_slots(self):
         self.slots = [FlatSlot("Adagrad", self.space.new_slot(self.initial_accumulator_value))]
 
+    def get_config(self):
+        return {"type": "adagrad", "learning_rate": self.learning_rate(),
+                "initial_accumulator_value": self.initial_accumulator_value}
+
     def _apply_native(self, gscale):
         self._lr_dev[0].fill_(self.learning_rate())
         K, sp, acc = _K(), self.space, self.slots[0].buf
-        K.adagrad(sp.master.data_ptr(), sp.grad.data_ptr(), acc.data_ptr(), _sh(sp, 0), sp.numel,
-                  self._lr_dev.data_ptr(), gscale, self._nonfinite.data_ptr(), _st())
+        for s, e, _ in self._regions():
+            K.adagrad(sp.master.data_ptr() + 4 * s, sp.grad.data_ptr() + 4 * s,
+                      acc.data_ptr() + 4 * s, _sh(sp, s), e - s, self._lr_dev.data_ptr(), gscale,
+                      self._nonfinite.data_ptr(), _st())
 
     def _apply_reference(self, gscale):
         lr = self.learning_rate()
         sp, acc = self.space, self.slots[0].buf
         with torch.no_grad():
-            g = sp.grad * gscale
-            acc.add_(g * g)
-            sp.master.sub_(lr * g * acc.rsqrt())
+            for s, e, _ in self._regions():
+                g = sp.grad[s:e] * gscale
+                acc[s:e].add_(g * g)
+                sp.master[s:e].sub_(lr * g * acc[s:e].rsqrt())
 
 
 class LAMBOptimizer(Optimizer):

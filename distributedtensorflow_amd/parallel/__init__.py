@@ -1,8 +1,11 @@
 """Distribution strategies and communication (RCCL over xGMI, one process per GPU)."""
+from .ps_service import PSClient, ParameterServerService, assign_shards
+from .ps_strategy import CentralStorageStrategy, ParameterServerStrategy
 from .strategy import (BucketedAllReduce, MirroredStrategy, MultiWorkerMirroredStrategy,
                        OneDeviceStrategy, ReduceOp, Strategy, get_strategy, has_strategy,
                        init_process_group_from_env)
 
-__all__ = ["BucketedAllReduce", "MirroredStrategy", "MultiWorkerMirroredStrategy",
-           "OneDeviceStrategy", "ReduceOp", "Strategy", "get_strategy", "has_strategy",
-           "init_process_group_from_env"]
+__all__ = ["PSClient", "ParameterServerService", "assign_shards", "CentralStorageStrategy",
+           "ParameterServerStrategy", "BucketedAllReduce", "MirroredStrategy",
+           "MultiWorkerMirroredStrategy", "OneDeviceStrategy", "ReduceOp", "Strategy",
+           "get_strategy", "has_strategy", "init_process_group_from_env"]

@@ -1,0 +1,340 @@
+"""``MonitoredTrainingSession`` / ``Supervisor`` for eager step functions.
+
+Reference: ``run_mnist_distributed.py:118-161`` (MTS + StopAtStepHook, chief logs every step),
+``templates/00_mnist_replica.py:193-240`` (Supervisor, prepare_or_wait_for_session),
+``templates/00_between…:40-52`` (MTS with checkpoint_dir).  SURVEY R14/R16/R17, T12.
+
+A "train op" is a Python callable performing one training step (forward, backward, optimizer
+update through the active strategy).  ``run(fetches)`` accepts a callable, a list/tuple/dict of
+callables, :class:`~.global_step.GlobalStep` objects (resolved after the step), or strings naming
+keys of the dict returned by the first callable — so the reference's
+``mon_sess.run([train_op, loss, global_step])`` becomes ``run([train_op, "loss", global_step])``.
+
+Session creation follows TF1: the chief restores the latest checkpoint in ``checkpoint_dir`` (or
+initialises) and, under a between-graph ParameterServerStrategy, ships the variables to the PS;
+non-chief workers wait for the chief (``recovery_wait_secs`` polling is implicit in the PS
+rendezvous).  Recoverable failures during ``run`` (a dropped RCCL/gloo peer, an injected fault)
+re-create the session from the latest checkpoint up to ``max_recovery_attempts`` times.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+
+from . import global_step as gs_mod
+from .checkpoint import Saver, latest_checkpoint
+from .hooks import (CheckpointSaverHook, InjectedFault, SessionRunContext, SessionRunValues,
+                    StepCounterHook, SummarySaverHook)
+
+
+class ConfigProto:
+    """``tf.ConfigProto`` subset (``run_mnist_distributed.py:122-124``,
+    ``templates/00_mnist_replica.py:213-217``).  Thread counts are applied to torch's CPU pools."""
+
+    def __init__(self, allow_soft_placement=True, log_device_placement=False,
+                 intra_op_parallelism_threads=0, inter_op_parallelism_threads=0,
+                 device_filters=None, gpu_options=None, **kw):
+        self.allow_soft_placement = allow_soft_placement
+        self.log_device_placement = log_device_placement
+        self.intra_op_parallelism_threads = intra_op_parallelism_threads
+        self.inter_op_parallelism_threads = inter_op_parallelism_threads
+        self.device_filters = list(device_filters or [])
+        self.gpu_options = gpu_options
+        self.extra = kw
+
+    def apply(self):
+        if self.intra_op_parallelism_threads:
+            torch.set_num_threads(int(self.intra_op_parallelism_threads))
+        if self.inter_op_parallelism_threads:
+            try:
+                torch.set_num_interop_threads(int(self.inter_op_parallelism_threads))
+            except RuntimeError:
+                pass   # can only be set once per process
+
+
+RunConfig = ConfigProto
+
+
+class Scaffold:
+    def __init__(self, model=None, optimizer=None, global_step=None, saver=None, init_fn=None):
+        self.model, self.optimizer, self.global_step = model, optimizer, global_step
+        self.saver, self.init_fn = saver, init_fn
+
+    def finalize(self):
+        if self.global_step is None:
+            self.global_step = gs_mod.get_or_create_global_step()
+        if self.saver is None and (self.model is not None or self.optimizer is not None):
+            self.saver = Saver(model=self.model, optimizer=self.optimizer,
+                               global_step=self.global_step)
+        return self
+
+
+class _Session:
+    """The object hooks see (``run_context.session``)."""
+
+    def __init__(self, scaffold, strategy, is_chief, checkpoint_dir, summary_writer):
+        self.scaffold = scaffold
+        self.strategy = strategy
+        self.is_chief = is_chief
+        self.checkpoint_dir = checkpoint_dir
+        self.summary_writer = summary_writer
+        self.last_results = None
+
+    @property
+    def global_step(self):
+        return self.scaffold.global_step
+
+    @property
+    def saver(self):
+        return self.scaffold.saver
+
+    def save_checkpoint(self, path, step, saver=None):
+        saver = saver or self.saver
+        values = None
+        client = getattr(self.strategy, "ps_client", None)
+        if client is not None and client.params is not None:
+            gstep, values, slots = client.get_state()
+            for sname, per in slots.items():
+                for vname, t in per.items():
+                    values[f"{vname}/{sname}"] = t
+            self.global_step.assign(gstep)
+        return saver.save(None, path, global_step=step, values=values)
+
+    def run(self, fetches, feed_dict=None):
+        return _execute(fetches, feed_dict, self)
+
+
+def _execute(fetches, feed_dict, session):
+    first_result = {}
+
+    def ev(f):
+        nonlocal first_result
+        if isinstance(f, gs_mod.GlobalStep):
+            return None   # resolved after all callables ran
+        if callable(f):
+            r = f(**feed_dict) if feed_dict else f()
+            if isinstance(r, dict) and not first_result:
+                first_result = r
+            return r
+        return f
+
+    def resolve(f, v):
+        if isinstance(f, gs_mod.GlobalStep):
+            return f.value()
+        if isinstance(f, str):
+            r = first_result.get(f)
+            return float(r) if isinstance(r, torch.Tensor) and r.numel() == 1 else r
+        return v
+
+    if isinstance(fetches, (list, tuple)):
+        vals = [ev(f) if not isinstance(f, str) else None for f in fetches]
+        out = [resolve(f, v) for f, v in zip(fetches, vals)]
+        return type(fetches)(out) if isinstance(fetches, tuple) else out
+    if isinstance(fetches, dict):
+        vals = {k: (ev(f) if not isinstance(f, str) else None) for k, f in fetches.items()}
+        return {k: resolve(f, vals[k]) for k, f in fetches.items()}
+    return resolve(fetches, ev(fetches))
+
+
+class MonitoredTrainingSession:
+    RECOVERABLE = (InjectedFault, ConnectionError, TimeoutError)
+
+    def __init__(self, master="", is_chief=True, checkpoint_dir=None, scaffold=None, hooks=None,
+                 chief_only_hooks=None, save_checkpoint_secs=600, save_summaries_steps=100,
+                 save_summaries_secs=None, config=None, stop_grace_period_secs=120,
+                 log_step_count_steps=100, max_wait_secs=7200, save_checkpoint_steps=None,
+                 summary_dir=None, model=None, optimizer=None, global_step=None, strategy=None,
+                 max_recovery_attempts=3):
+        from ..parallel.strategy import get_strategy
+        self.master = master
+        self.is_chief = is_chief
+        self.checkpoint_dir = checkpoint_dir
+        self.scaffold = (scaffold or Scaffold(model, optimizer, global_step)).finalize()
+        self.strategy = strategy or get_strategy()
+        self.config = config
+        self.max_recovery_attempts = max_recovery_attempts
+        self.hooks = list(hooks or [])
+        self._writer = None
+        if is_chief:
+            self.hooks += list(chief_only_hooks or [])
+            sdir = summary_dir or checkpoint_dir
+            if sdir:
+                from ..summary.events import EventFileWriter
+                self._writer = EventFileWriter(sdir)
+            if checkpoint_dir and (save_checkpoint_secs or save_checkpoint_steps):
+                self.hooks.append(CheckpointSaverHook(checkpoint_dir, save_checkpoint_secs
+                                                      if not save_checkpoint_steps else None,
+                                                      save_checkpoint_steps))
+            if sdir and log_step_count_steps:
+                self.hooks.append(StepCounterHook(every_n_steps=log_step_count_steps))
+            if sdir and (save_summaries_steps or save_summaries_secs):
+                self.hooks.append(SummarySaverHook(save_summaries_steps, save_summaries_secs))
+        self._session = None
+        self._should_stop = False
+        self._closed = False
+        self._create()
+
+    # -- creation / recovery
+    def _create(self):
+        if self.config is not None and hasattr(self.config, "apply"):
+            self.config.apply()
+        sc = self.scaffold
+        restored = False
+        if self.is_chief and self.checkpoint_dir and sc.saver is not None:
+            ckpt = latest_checkpoint(self.checkpoint_dir)
+            if ckpt:
+                sc.saver.restore(None, ckpt, strict=False)
+                restored = True
+        if sc.init_fn is not None and not restored:
+            sc.init_fn(self)
+        if sc.optimizer is not None and hasattr(self.strategy, "register_with_ps"):
+            self.strategy.register_with_ps(sc.optimizer, sc.global_step.value())
+            client = getattr(self.strategy, "ps_client", None)
+            if client is not None:
+                sc.global_step.assign(client.global_step)
+        self._session = _Session(sc, self.strategy, self.is_chief, self.checkpoint_dir,
+                                 self._writer)
+        for h in self.hooks:
+            h.begin()
+        for h in self.hooks:
+            h.after_create_session(self._session, None)
+
+    def _recover(self):
+        ckpt = latest_checkpoint(self.checkpoint_dir) if self.checkpoint_dir else None
+        if ckpt and self.scaffold.saver is not None:
+            self.scaffold.saver.restore(None, ckpt, strict=False)
+            client = getattr(self.strategy, "ps_client", None)
+            if client is not None and self.is_chief:
+                client.set_state(self.scaffold.global_step.value())
+
+    # -- public API
+    @property
+    def global_step(self):
+        return self.scaffold.global_step
+
+    def should_stop(self):
+        return self._should_stop or self._closed
+
+    def run(self, fetches, feed_dict=None, options=None, run_metadata=None):
+        attempts = 0
+        while True:
+            ctx = SessionRunContext(fetches, self._session)
+            for h in self.hooks:
+                h.before_run(ctx)
+            if ctx.stop_requested:
+                self._should_stop = True
+                return None
+            try:
+                results = _execute(fetches, feed_dict, self._session)
+                break
+            except self.RECOVERABLE:
+                attempts += 1
+                if attempts > self.max_recovery_attempts:
+                    raise
+                self._recover()
+        self._session.last_results = results
+        rv = SessionRunValues(results)
+        for h in self.hooks:
+            h.after_run(ctx, rv)
+        if ctx.stop_requested:
+            self._should_stop = True
+        return results
+
+    def run_step_fn(self, step_fn):
+        return self.run(step_fn)
+
+    def close(self):
+        if self._closed:
+            return
+        try:
+            for h in self.hooks:
+                h.end(self._session)
+        finally:
+            self._closed = True
+            client = getattr(self.strategy, "ps_client", None)
+            if client is not None and client.params is not None:
+                client.stop()
+            if self._writer is not None:
+                self._writer.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        if exc_type is None or issubclass(exc_type, StopIteration):
+            self.close()
+            return exc_type is not None
+        self._closed = True
+        client = getattr(self.strategy, "ps_client", None)
+        if client is not None and client.params is not None:
+            client.stop()
+        return False
+
+
+class Supervisor:
+    """``tf.train.Supervisor`` compat (``templates/00_mnist_replica.py:193-235``): chief
+    initialises (``init_op`` callable) / restores from ``logdir``; others wait; the returned
+    session supports ``run``."""
+
+    def __init__(self, is_chief=True, logdir=None, init_op=None, local_init_op=None,
+                 ready_for_local_init_op=None, recovery_wait_secs=1, global_step=None,
+                 saver=None, model=None, optimizer=None, save_model_secs=600,
+                 summary_writer=None, strategy=None):
+        self.is_chief = is_chief
+        self.logdir = logdir
+        self.init_op = init_op
+        self.local_init_op = local_init_op
+        self.recovery_wait_secs = recovery_wait_secs
+        self.global_step = global_step or gs_mod.get_or_create_global_step()
+        self.model, self.optimizer, self.strategy = model, optimizer, strategy
+        self.saver = saver
+        self.save_model_secs = save_model_secs
+        self._mts = None
+
+    def prepare_or_wait_for_session(self, master="", config=None, wait_for_checkpoint=False,
+                                    max_wait_secs=7200, start_standard_services=True):
+        scaffold = Scaffold(self.model, self.optimizer, self.global_step, self.saver,
+                            init_fn=(lambda s: self.init_op()) if callable(self.init_op) else None)
+        self._mts = MonitoredTrainingSession(
+            master, self.is_chief, self.logdir, scaffold, config=config,
+            save_checkpoint_secs=self.save_model_secs if self.logdir else None,
+            save_summaries_steps=None, log_step_count_steps=None, strategy=self.strategy)
+        if callable(self.local_init_op):
+            self.local_init_op()
+        return self._mts
+
+    def managed_session(self, master="", config=None):
+        sess = self.prepare_or_wait_for_session(master, config)
+        return sess
+
+    def start_queue_runners(self, sess=None, queue_runners=None):
+        return []
+
+    def should_stop(self):
+        return self._mts.should_stop() if self._mts else False
+
+    def stop(self, threads=None, close_summary_writer=True):
+        if self._mts is not None:
+            self._mts.close()
+
+    def request_stop(self, ex=None):
+        if self._mts is not None:
+            self._mts._should_stop = True
+
+
+def wait_for_new_checkpoint(checkpoint_dir, last_checkpoint=None, seconds_to_sleep=1,
+                            timeout=None):
+    t0 = time.time()
+    while True:
+        ck = latest_checkpoint(checkpoint_dir)
+        if ck and ck != last_checkpoint:
+            return ck
+        if timeout is not None and time.time() - t0 > timeout:
+            return None
+        time.sleep(seconds_to_sleep)
+
+
+def default_checkpoint_dir():
+    return os.path.join("/tmp", "train_logs")
