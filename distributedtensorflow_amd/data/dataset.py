@@ -155,6 +155,7 @@ class Dataset:
             q: queue.Queue = queue.Queue(maxsize=size)
             stop = threading.Event()
             done = object()
+            error = []
 
             def producer():
                 try:
@@ -167,6 +168,8 @@ class Dataset:
                                 continue
                         if stop.is_set():
                             return
+                except BaseException as exc:     # re-raised in the consumer, like tf.data
+                    error.append(exc)
                 finally:
                     while not stop.is_set():
                         try:
@@ -180,6 +183,8 @@ class Dataset:
                 while True:
                     e = q.get()
                     if e is done:
+                        if error:
+                            raise error[0]
                         return
                     yield e
             finally:

@@ -27,7 +27,7 @@ def write_bundle(prefix: str, tensors: dict, num_shards: int = 1, shard_of=None)
                 w.add(name, DT_BFLOAT16, list(t.shape), raw, shard_of(name) if shard_of else 0)
                 continue
             arr = t.numpy()
-        arr = np.ascontiguousarray(arr)
+        arr = np.asarray(arr, order="C")          # (ascontiguousarray would promote 0-d to [1])
         if arr.dtype not in _NP2TF:
             raise TypeError(f"unsupported dtype {arr.dtype} for {name}")
         w.add(name, _NP2TF[arr.dtype], list(arr.shape), arr.reshape(-1) if arr.ndim else

@@ -157,8 +157,11 @@ class Optimizer:
         if getattr(self._reducer, "applies_update", False):
             # parameter-server strategies: the PS owning the variables applies the update
             step = self._reducer.apply_remote(self)
-            if global_step is not None and step is not None:
-                global_step.assign(step) if hasattr(global_step, "assign") else None
+            if global_step is not None:
+                if step is None:                 # colocated owners: a local synchronous step
+                    gs.increment(global_step)
+                elif hasattr(global_step, "assign"):
+                    global_step.assign(step)     # the PS's authoritative global step
             return step
         self._apply(self._reducer.grad_scale())
         if global_step is not None:

@@ -199,6 +199,10 @@ class LAMBOptimizer(Optimizer):
         super().__init__(learning_rate, name, weight_decay=weight_decay, **kw)
         self.beta1, self.beta2, self.epsilon, self.chunk = beta1, beta2, epsilon, chunk
 
+    def get_config(self):
+        return {"type": "lamb", "learning_rate": self.learning_rate(), "beta1": self.beta1,
+                "beta2": self.beta2, "epsilon": self.epsilon, "weight_decay": self.weight_decay}
+
     def _build_slots(self):
         sp = self.space
         self.slots = [FlatSlot("m", sp.new_slot()), FlatSlot("v", sp.new_slot())]
@@ -211,15 +215,25 @@ class LAMBOptimizer(Optimizer):
             for c in range(0, n, self.chunk):
                 rows.append((seg, min(self.chunk, n - c), o + c))
         self._nseg = len(sp.order)
-        self._nchunks = len(rows)
-        tbl = torch.zeros(len(rows), 4, dtype=torch.int32)
-        for i, (seg, ln, st) in enumerate(rows):
-            tbl[i, 0], tbl[i, 1] = seg, ln
-            tbl[i, 2], tbl[i, 3] = st & 0xFFFFFFFF if st < 2 ** 31 else st - 2 ** 32, st >> 32
-        self._chunks = tbl.to(sp.device)
+        self._rows = rows
+        self._tables = {}
         self._wd_seg = torch.tensor(wd, dtype=torch.float32, device=sp.device)
         self._norms = torch.zeros(2 * self._nseg, dtype=torch.float32, device=sp.device)
         self._hyper = torch.zeros(4, dtype=torch.float32, device=sp.device)
+
+    def _chunk_table(self):
+        """Chunk table for the whole space, or for the variables inside ``self._range`` (a
+        colocated parameter-server shard; shard ranges fall on variable boundaries)."""
+        key = getattr(self, "_range", None)
+        if key not in self._tables:
+            lo, hi = key if key is not None else (0, self.space.numel)
+            rows = [r for r in self._rows if lo <= r[2] < hi]
+            tbl = torch.zeros(max(1, len(rows)), 4, dtype=torch.int32)
+            for i, (seg, ln, st) in enumerate(rows):
+                tbl[i, 0], tbl[i, 1] = seg, ln
+                tbl[i, 2], tbl[i, 3] = st & 0xFFFFFFFF if st < 2 ** 31 else st - 2 ** 32, st >> 32
+            self._tables[key] = (tbl.to(self.space.device), len(rows))
+        return self._tables[key]
 
     def _apply_native(self, gscale):
         t = self.iterations
@@ -228,8 +242,11 @@ class LAMBOptimizer(Optimizer):
         self._lr_dev[0].fill_(self.learning_rate())
         self._norms.zero_()
         sp, m, v = self.space, self.slots[0].buf, self.slots[1].buf
+        chunks, nchunks = self._chunk_table()
+        if nchunks == 0:
+            return
         _K().lamb(sp.master.data_ptr(), sp.grad.data_ptr(), m.data_ptr(), v.data_ptr(),
-                  _sh(sp, 0), self._chunks.data_ptr(), self._nchunks, self._hyper.data_ptr(),
+                  _sh(sp, 0), chunks.data_ptr(), nchunks, self._hyper.data_ptr(),
                   self._lr_dev.data_ptr(), float(self.beta1), float(self.beta2),
                   float(self.epsilon), self._wd_seg.data_ptr(), gscale, self._norms.data_ptr(),
                   self._nonfinite.data_ptr(), _st())
@@ -239,8 +256,11 @@ class LAMBOptimizer(Optimizer):
         lr = self.learning_rate()
         sp, m, v = self.space, self.slots[0].buf, self.slots[1].buf
         b1, b2 = self.beta1, self.beta2
+        lo, hi = getattr(self, "_range", None) or (0, sp.numel)
         with torch.no_grad():
             for var, o in zip(sp.order, sp.offsets):
+                if not lo <= o < hi:
+                    continue
                 n = var.numel()
                 g = sp.grad[o:o + n] * gscale
                 mm, vv, p = m[o:o + n], v[o:o + n], sp.master[o:o + n]

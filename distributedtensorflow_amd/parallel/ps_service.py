@@ -87,7 +87,7 @@ def assign_shards(sizes, num_ps, policy="balanced"):
 class _Shard:
     def __init__(self, spec, values, device):
         from ..optimizers import (AdagradOptimizer, AdamOptimizer, GradientDescentOptimizer,
-                                  MomentumOptimizer)
+                                  LAMBOptimizer, MomentumOptimizer)
         self.names = spec["names"]
         self.shapes = [tuple(s) for s in spec["shapes"]]
         self.numel = int(values.numel())
@@ -95,7 +95,7 @@ class _Shard:
         opt = dict(spec["optimizer"])
         kind = opt.pop("type")
         cls = {"adam": AdamOptimizer, "adagrad": AdagradOptimizer, "momentum": MomentumOptimizer,
-               "sgd": GradientDescentOptimizer}[kind]
+               "sgd": GradientDescentOptimizer, "lamb": LAMBOptimizer}[kind]
         self.params = [torch.nn.Parameter(t.clone().to(device)) for t in
                        _split(values, self.shapes)]
         for p, n in zip(self.params, self.names):

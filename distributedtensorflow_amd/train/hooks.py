@@ -176,7 +176,10 @@ class LoggingTensorHook(SessionRunHook):
 
     def after_run(self, run_context, run_values):
         if self.timer.should_trigger(self.iter):
-            vals = {k: (float(v()) if callable(v) else float(v)) for k, v in self.tensors.items()}
+            named = _step_values(run_context, run_values)
+            vals = {k: (float(v()) if callable(v) else
+                        float(named[v]) if isinstance(v, str) else float(v))
+                    for k, v in self.tensors.items()}
             line = self._fmt(vals)
             self.lines.append(line)
             print(line, flush=True)
@@ -197,11 +200,8 @@ class SummarySaverHook(SessionRunHook):
         if not self.timer.should_trigger(step):
             return
         self.timer.update(step)
-        res = run_values.results
-        vals = {}
-        if isinstance(res, dict):
-            vals = {k: float(v) for k, v in res.items()
-                    if (self.scalars is None or k in self.scalars) and _is_number(v)}
+        vals = {k: float(v) for k, v in _step_values(run_context, run_values).items()
+                if (self.scalars is None or k in self.scalars) and _is_number(v)}
         w = self.writer or run_context.session.summary_writer
         if vals and w is not None:
             w.add_scalars(vals, step)
@@ -212,8 +212,10 @@ class NanTensorHook(SessionRunHook):
         self.loss, self.fail = loss_tensor, fail_on_nan_loss
 
     def after_run(self, run_context, run_values):
-        res = run_values.results
-        v = res.get("loss") if isinstance(res, dict) else (self.loss() if callable(self.loss) else None)
+        if callable(self.loss):
+            v = self.loss()
+        else:
+            v = _step_values(run_context, run_values).get(self.loss or "loss")
         if v is not None and not math.isfinite(float(v)):
             if self.fail:
                 raise FloatingPointError("NaN loss during training.")
@@ -248,6 +250,16 @@ class FaultInjectionHook(SessionRunHook):
 
 class InjectedFault(RuntimeError):
     pass
+
+
+def _step_values(run_context, run_values):
+    """Named values of the step: the dict returned by the train-op callable (whatever shape the
+    fetch structure had), else the run results themselves when they are a dict."""
+    named = getattr(run_context.session, "last_named", None)
+    if named:
+        return named
+    res = run_values.results
+    return res if isinstance(res, dict) else {}
 
 
 def _is_number(v):

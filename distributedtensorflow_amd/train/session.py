@@ -125,17 +125,21 @@ def _execute(fetches, feed_dict, session):
             return f.value()
         if isinstance(f, str):
             r = first_result.get(f)
-            return float(r) if isinstance(r, torch.Tensor) and r.numel() == 1 else r
+            return float(r.detach()) if isinstance(r, torch.Tensor) and r.numel() == 1 else r
         return v
 
     if isinstance(fetches, (list, tuple)):
         vals = [ev(f) if not isinstance(f, str) else None for f in fetches]
         out = [resolve(f, v) for f, v in zip(fetches, vals)]
-        return type(fetches)(out) if isinstance(fetches, tuple) else out
-    if isinstance(fetches, dict):
+        out = type(fetches)(out) if isinstance(fetches, tuple) else out
+    elif isinstance(fetches, dict):
         vals = {k: (ev(f) if not isinstance(f, str) else None) for k, f in fetches.items()}
-        return {k: resolve(f, vals[k]) for k, f in fetches.items()}
-    return resolve(fetches, ev(fetches))
+        out = {k: resolve(f, vals[k]) for k, f in fetches.items()}
+    else:
+        out = resolve(fetches, ev(fetches))
+    if session is not None:
+        session.last_named = first_result   # what hooks (summaries, NaN check, logging) see
+    return out
 
 
 class MonitoredTrainingSession:
@@ -228,16 +232,18 @@ class MonitoredTrainingSession:
                 return None
             try:
                 results = _execute(fetches, feed_dict, self._session)
+                self._session.last_results = results
+                rv = SessionRunValues(results)
+                for h in self.hooks:
+                    h.after_run(ctx, rv)
                 break
             except self.RECOVERABLE:
+                # the step (or a hook observing it) failed: roll back to the latest checkpoint
+                # and run the step again, like TF's _RecoverableSession
                 attempts += 1
                 if attempts > self.max_recovery_attempts:
                     raise
                 self._recover()
-        self._session.last_results = results
-        rv = SessionRunValues(results)
-        for h in self.hooks:
-            h.after_run(ctx, rv)
         if ctx.stop_requested:
             self._should_stop = True
         return results

@@ -1,0 +1,69 @@
+"""One rank of a multi-process CPU (gloo) data-parallel run, launched by tests/test_distributed.py
+exactly like torchrun would (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the env).
+
+    python dist_worker.py <strategy> <out_dir> [key=value ...]
+
+Each rank initialises its model with a DIFFERENT seed (the strategy must broadcast rank 0's
+variables), trains on its own shard of a fixed global batch, and saves its final variables and
+global step to ``out_dir/rank<r>.pt`` for the test to compare against a single-process run.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def global_batch(step, n=16):
+    g = torch.Generator().manual_seed(1000 + step)
+    return torch.rand(n, 784, generator=g), torch.randint(0, 10, (n,), generator=g)
+
+
+def make_optimizer(name):
+    from distributedtensorflow_amd.optimizers import AdamOptimizer, MomentumOptimizer
+    return AdamOptimizer(1e-3) if name == "adam" else MomentumOptimizer(0.05, 0.9)
+
+
+def main():
+    kind, out = sys.argv[1], sys.argv[2]
+    kw = dict(a.split("=", 1) for a in sys.argv[3:])
+    steps = int(kw.get("steps", 3))
+    import distributedtensorflow_amd as dtf
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.models import MnistCNN
+    from distributedtensorflow_amd.parallel import (MirroredStrategy, MultiWorkerMirroredStrategy,
+                                                    ParameterServerStrategy)
+    if kind == "mirrored":
+        strat = MirroredStrategy(bucket_mb=float(kw.get("bucket_mb", 64)),
+                                 first_bucket_mb=float(kw.get("bucket_mb", 4)),
+                                 compress_bf16=kw.get("bf16", "0") == "1")
+    elif kind == "multiworker":
+        strat = MultiWorkerMirroredStrategy()
+    elif kind == "colocated_ps":
+        strat = ParameterServerStrategy(num_ps=int(kw.get("num_ps", 1)))
+    else:
+        raise SystemExit(f"unknown strategy {kind}")
+    rank, world = strat.replica_id, strat.num_replicas_in_sync
+    torch.manual_seed(17 + 101 * rank)
+    with strat.scope():
+        model = MnistCNN()
+        opt = make_optimizer(kw.get("opt", "momentum"))
+        gstep = dtf.train.get_or_create_global_step()
+        opt.build(list(model.parameters()))
+        per = 16 // world
+        for step in range(steps):
+            x, y = global_batch(step)
+            x, y = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
+            loss = ops.sparse_softmax_cross_entropy(model(x), y)
+            opt.minimize(loss, global_step=gstep)
+        mean_loss = float(strat.reduce(dtf.distribute.ReduceOp.MEAN, loss.detach()))
+    torch.save({"state": {k: v.detach().clone() for k, v in model.state_dict().items()},
+                "global_step": gstep.value(), "world": world, "mean_loss": mean_loss},
+               os.path.join(out, f"rank{rank}.pt"))
+    strat.barrier()
+
+
+if __name__ == "__main__":
+    main()

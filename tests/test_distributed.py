@@ -1,0 +1,155 @@
+"""Multi-process data parallelism on CPU (gloo), the way the driver runs it on GPUs (one process
+per rank, torchrun env).  SURVEY.md §4: replicas must stay bit-identical and match a
+single-process run on the concatenated batch; parameter-server clusters (reference
+``run_mnist_distributed.py``: 1 PS + 2 workers, async and SyncReplicas) must train and exit."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+import dist_worker  # noqa: E402
+
+from distributedtensorflow_amd.cluster.launcher import free_ports, launch_local  # noqa: E402
+
+
+def _launch(kind, world, tmp_path, *args, extra_env=None, timeout=240):
+    port = free_ports(1)[0]
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="2",
+                   PYTHONPATH=ROOT)
+        env.update(extra_env(r) if extra_env else {})
+        if extra_env:
+            for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+                if k in extra_env(r) and extra_env(r)[k] is None:
+                    env.pop(k)
+            env = {k: v for k, v in env.items() if v is not None}
+        log = open(tmp_path / f"{kind}{r}.log", "w")
+        procs.append((subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"),
+                                        kind, str(tmp_path), *args], env=env, stdout=log,
+                                       stderr=subprocess.STDOUT), log))
+    try:
+        for p, _ in procs:
+            p.wait(timeout=timeout)
+    finally:
+        for p, log in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+            log.close()
+    for r, (p, _) in enumerate(procs):
+        assert p.returncode == 0, open(tmp_path / f"{kind}{r}.log").read()[-3000:]
+    return [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+
+
+def _single_process(opt="momentum", steps=3):
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.models import MnistCNN
+    from distributedtensorflow_amd.parallel import OneDeviceStrategy
+    from distributedtensorflow_amd.train import global_step as gs_mod
+    gs_mod.reset_global_step()
+    torch.manual_seed(17)
+    strat = OneDeviceStrategy("cpu")
+    with strat.scope():
+        model = MnistCNN()
+        o = dist_worker.make_optimizer(opt)
+        o.build(list(model.parameters()))
+        for step in range(steps):
+            x, y = dist_worker.global_batch(step)
+            o.minimize(ops.sparse_softmax_cross_entropy(model(x), y))
+    return {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+
+def _assert_replicas(results, ref, atol=2e-6, steps=3):
+    for r in results[1:]:
+        for k in ref:
+            assert torch.equal(r["state"][k], results[0]["state"][k]), f"replicas diverged at {k}"
+    for k in ref:
+        torch.testing.assert_close(results[0]["state"][k], ref[k], atol=atol, rtol=1e-5)
+    assert all(r["global_step"] == steps for r in results)
+
+
+@pytest.mark.parametrize("args", [(), ("bucket_mb=0.05",)], ids=["default_buckets", "many_buckets"])
+def test_mirrored_two_ranks_matches_single_process(tmp_path, args):
+    res = _launch("mirrored", 2, tmp_path, *args)
+    _assert_replicas(res, _single_process())
+    assert res[0]["mean_loss"] == res[1]["mean_loss"]
+
+
+def test_mirrored_bf16_gradient_compression(tmp_path):
+    res = _launch("mirrored", 2, tmp_path, "bf16=1", "opt=adam")
+    ref = _single_process("adam")
+    for k in ref:
+        assert torch.equal(res[0]["state"][k], res[1]["state"][k])
+        torch.testing.assert_close(res[0]["state"][k], ref[k], atol=5e-3, rtol=0)
+
+
+def test_multiworker_from_tf_config(tmp_path):
+    ports = free_ports(2)
+    cluster = {"worker": [f"127.0.0.1:{p}" for p in ports]}
+
+    def env(r):
+        return {"TF_CONFIG": json.dumps({"cluster": cluster, "task": {"type": "worker",
+                                                                      "index": r}}),
+                "RANK": None, "WORLD_SIZE": None, "LOCAL_RANK": None, "MASTER_ADDR": None,
+                "MASTER_PORT": None}
+    res = _launch("multiworker", 2, tmp_path, extra_env=env)
+    _assert_replicas(res, _single_process())
+
+
+@pytest.mark.parametrize("num_ps", [1, 2])
+def test_colocated_parameter_server_sync(tmp_path, num_ps):
+    res = _launch("colocated_ps", 2, tmp_path, f"num_ps={num_ps}", "opt=adam")
+    _assert_replicas(res, _single_process("adam"), atol=2e-5)   # Adam normalises fp noise
+
+
+# ----------------------------------------------------------------------------- between-graph PS
+@pytest.fixture(scope="module")
+def mnist_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("mnist")
+    from distributedtensorflow_amd.data import mnist
+    mnist.load_arrays(str(d), "train")          # writes the offline synthetic stand-in once
+    return str(d)
+
+
+def _ps_run(tmp_path, mnist_dir, num_ps, num_workers, steps, *flags):
+    codes, logs = launch_local(os.path.join(ROOT, "run_mnist_distributed.py"), num_ps,
+                               num_workers, str(tmp_path),
+                               [f"--max_steps={steps}", f"--data_dir={mnist_dir}",
+                                f"--log_dir={tmp_path}/tb", "--batch_size=32", *flags],
+                               env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2"}, timeout_s=300)
+    text = {k: open(v).read() for k, v in logs.items()}
+    assert all(c == 0 for c in codes.values()), {k: t[-2000:] for k, t in text.items()}
+    return text
+
+
+def test_between_graph_async_ps(tmp_path, mnist_dir):
+    text = _ps_run(tmp_path, mnist_dir, 1, 2, 30)
+    chief = text["worker0"]
+    lines = re.findall(r"Worker \(0\): loss = ([0-9.]+) \(global step: (\d+)\)", chief)
+    assert lines, chief[-2000:]
+    steps = [int(s) for _, s in lines]
+    assert steps == sorted(steps) and steps[-1] >= 30
+    assert float(lines[-1][0]) < float(lines[0][0])
+    assert "Close Parameter Server" in text["ps0"]
+    from distributedtensorflow_amd.summary.events import read_scalars
+    tb = [os.path.join(dp, ) for dp, _, fs in os.walk(tmp_path / "tb") if fs]
+    assert tb and "Loss" in read_scalars(tb[0])
+
+
+def test_between_graph_sync_replicas_two_ps(tmp_path, mnist_dir):
+    text = _ps_run(tmp_path, mnist_dir, 2, 2, 12, "--sync_replicas")
+    lines = re.findall(r"global step: (\d+)\)", text["worker0"])
+    steps = [int(s) for s in lines]
+    # synchronous aggregation: every applied update consumed both workers' gradients, so the
+    # chief sees each global step at most once and the run ends at max_steps
+    assert len(set(steps)) == len(steps) and steps[-1] >= 12
+    assert "Close Parameter Server" in text["ps0"] and "Close Parameter Server" in text["ps1"]
