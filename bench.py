@@ -41,7 +41,15 @@ def parse():
     p.add_argument("--lr", type=float, default=0.1)
     p.add_argument("--bucket-mb", type=float, default=64)
     p.add_argument("--profile-steps", type=int, default=0)
-    return p.parse_args()
+    p.add_argument("--model", choices=("resnet50", "bert_base"), default="resnet50",
+                   help="resnet50: the headline metric; bert_base: BASELINE config 5 "
+                        "(MLM, LAMB, MultiWorkerMirroredStrategy) in tokens/sec")
+    p.add_argument("--seq-len", type=int, default=128)
+    p.add_argument("--max-predictions", type=int, default=20)
+    args = p.parse_args()
+    if args.model == "bert_base" and args.batch == 256 and "--batch" not in sys.argv:
+        args.batch = 128
+    return args
 
 
 def log(*a):
@@ -67,6 +75,31 @@ def build_dtf(args, dev):
     def step(images, labels):
         logits = model(images)
         loss = ops.sparse_softmax_cross_entropy(logits, labels)
+        opt.minimize(loss, global_step=gstep)
+        return loss
+
+    return step, strategy
+
+
+def build_bert(args, dev):
+    """BERT-base MLM pre-training step: MultiWorkerMirroredStrategy + fused LAMB."""
+    from distributedtensorflow_amd.models.bert import bert_base
+    from distributedtensorflow_amd.optimizers import LAMBOptimizer
+    from distributedtensorflow_amd.optimizers.optimizers import polynomial_decay
+    from distributedtensorflow_amd.parallel import MultiWorkerMirroredStrategy
+    from distributedtensorflow_amd.train import get_or_create_global_step
+
+    strategy = MultiWorkerMirroredStrategy(bucket_mb=args.bucket_mb)
+    with strategy.scope():
+        model = bert_base()
+        model.train()
+        opt = LAMBOptimizer(polynomial_decay(args.lr, 10000, warmup_steps=100),
+                            weight_decay=0.01)
+        gstep = get_or_create_global_step()
+        opt.build(list(model.parameters()))
+
+    def step(batch):
+        loss = model(*batch)
         opt.minimize(loss, global_step=gstep)
         return loss
 
@@ -112,14 +145,28 @@ def main():
     B, S = args.batch, args.image_size
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    if args.impl == "dtf":
+    if args.model == "bert_base":
+        from distributedtensorflow_amd.data.synthetic import SyntheticMLM
+        if args.lr == 0.1 and "--lr" not in sys.argv:
+            args.lr = 1e-3
+        bert_step, _ = build_bert(args, dev)
+        d = next(iter(SyntheticMLM(B, args.seq_len, max_predictions=args.max_predictions,
+                                   device=dev, seed=1234 + rank)))
+        batch = (d["input_ids"], d["segment_ids"], d["input_mask"], d["masked_lm_positions"],
+                 d["masked_lm_ids"], torch.ones_like(d["masked_lm_ids"], dtype=torch.float32))
+
+        def step(_images, _labels):
+            return bert_step(batch)
+        images = labels = None
+    elif args.impl == "dtf":
         step, _ = build_dtf(args, dev)
         images = torch.randn(B, S, S, 3, device=dev, generator=g).to(torch.bfloat16)  # NHWC
     else:
         step, _ = build_torch(args, dev)
         images = torch.randn(B, 3, S, S, device=dev, generator=g).contiguous(
             memory_format=torch.channels_last)
-    labels = torch.randint(0, 1000, (B,), device=dev, generator=g)
+    if labels is not None or args.model != "bert_base":
+        labels = torch.randint(0, 1000, (B,), device=dev, generator=g)
 
     def sync():
         if world > 1:
@@ -145,7 +192,24 @@ def main():
     final_loss = float(loss)
     ms = elapsed / args.steps * 1000
     ips = B * world * args.steps / elapsed
-    if rank == 0:
+    if rank == 0 and args.model == "bert_base":
+        from distributedtensorflow_amd.models.bert import BertConfig, mlm_flops_per_token
+        tps = ips * args.seq_len
+        fpt = mlm_flops_per_token(BertConfig(), args.seq_len, args.max_predictions)
+        rec = {
+            "metric": "tokens/sec (whole node) BERT-base MLM pre-training", "value": round(tps, 1),
+            "unit": "tokens/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random token ids, 15% masked positions; random-init weights)",
+            "config": {"model": "bert_base", "global_batch": B * world, "per_gpu_batch": B,
+                       "seq_len": args.seq_len, "max_predictions": args.max_predictions,
+                       "parallelism": f"dp{world}", "optimizer": "lamb+wd0.01",
+                       "dropout": 0.1, "tflops_per_gpu": round(tps * fpt / world / 1e12, 1),
+                       "final_loss": round(final_loss, 4)},
+        }
+        print(json.dumps(rec), flush=True)
+    elif rank == 0:
         rec = {
             "metric": METRIC, "value": round(ips, 2), "unit": "images/sec",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

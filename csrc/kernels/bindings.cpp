@@ -62,6 +62,27 @@ void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, con
 int dtf_conv_wgrad_splits(long, int, int, long);
 void dtf_lds_probe(int, int, int*, int, hipStream_t);
 int dtf_max_dynamic_lds(int);
+// transformer kernels (nlp.hip)
+void dtf_ln_fwd(const bf16_t*, const float*, const bf16_t*, const float*, const float*, bf16_t*,
+                bf16_t*, float*, float*, int, int, float, float, uint32_t, float, uint32_t,
+                const int64_t*, const int64_t*, const bf16_t*, const bf16_t*, const bf16_t*, int,
+                hipStream_t);
+int dtf_ln_bwd_blocks(int);
+void dtf_ln_bwd(const bf16_t*, const bf16_t*, const float*, const float*, const float*, bf16_t*,
+                bf16_t*, float*, float*, float*, float*, int, int, float, uint32_t, float,
+                uint32_t, hipStream_t);
+void dtf_bias_gelu_fwd(const bf16_t*, const float*, bf16_t*, long, int, hipStream_t);
+int dtf_bias_gelu_bwd_blocks(int);
+void dtf_bias_gelu_bwd(const bf16_t*, const bf16_t*, const float*, bf16_t*, float*, float*, int,
+                       int, hipStream_t);
+void dtf_attn_fwd(const bf16_t*, const float*, bf16_t*, float*, int, int, int, float, float,
+                  uint32_t, hipStream_t);
+void dtf_attn_bwd(const bf16_t*, const float*, const bf16_t*, const bf16_t*, const float*, float*,
+                  bf16_t*, int, int, int, float, float, uint32_t, hipStream_t);
+void dtf_segment_sum(const int64_t*, const int64_t*, const bf16_t*, float*, int, int,
+                     hipStream_t);
+void dtf_mlm_xent(const bf16_t*, const int64_t*, const float*, const float*, int, int, float*,
+                  bf16_t*, hipStream_t);
 
 template <typename T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
@@ -228,4 +249,67 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("lds_probe");
   });
   m.def("max_dynamic_lds", &dtf_max_dynamic_lds);
+
+  // ---- transformer (BERT) kernels
+  m.def("ln_fwd", [](uintptr_t a, uintptr_t bias, uintptr_t res, uintptr_t gamma, uintptr_t beta,
+                     uintptr_t y, uintptr_t s, uintptr_t mean, uintptr_t rstd, int M, int H,
+                     float eps, float p_pre, uint32_t seed_pre, float p_post, uint32_t seed_post,
+                     uintptr_t ids, uintptr_t tt, uintptr_t word, uintptr_t pos, uintptr_t type,
+                     int S_, uintptr_t st) {
+    dtf_ln_fwd(P<const bf16_t>(a), P<const float>(bias), P<const bf16_t>(res),
+               P<const float>(gamma), P<const float>(beta), P<bf16_t>(y), P<bf16_t>(s),
+               P<float>(mean), P<float>(rstd), M, H, eps, p_pre, seed_pre, p_post, seed_post,
+               P<const int64_t>(ids), P<const int64_t>(tt), P<const bf16_t>(word),
+               P<const bf16_t>(pos), P<const bf16_t>(type), S_, S(st));
+    check_launch("ln_fwd");
+  });
+  m.def("ln_bwd_blocks", &dtf_ln_bwd_blocks);
+  m.def("ln_bwd", [](uintptr_t dy, uintptr_t s, uintptr_t mean, uintptr_t rstd, uintptr_t gamma,
+                     uintptr_t ds, uintptr_t da, uintptr_t part, uintptr_t dgamma,
+                     uintptr_t dbeta, uintptr_t dbias, int M, int H, float p_pre,
+                     uint32_t seed_pre, float p_post, uint32_t seed_post, uintptr_t st) {
+    dtf_ln_bwd(P<const bf16_t>(dy), P<const bf16_t>(s), P<const float>(mean),
+               P<const float>(rstd), P<const float>(gamma), P<bf16_t>(ds), P<bf16_t>(da),
+               P<float>(part), P<float>(dgamma), P<float>(dbeta), P<float>(dbias), M, H, p_pre,
+               seed_pre, p_post, seed_post, S(st));
+    check_launch("ln_bwd");
+  });
+  m.def("bias_gelu_fwd", [](uintptr_t a, uintptr_t bias, uintptr_t y, long M, int N,
+                            uintptr_t st) {
+    dtf_bias_gelu_fwd(P<const bf16_t>(a), P<const float>(bias), P<bf16_t>(y), M, N, S(st));
+    check_launch("bias_gelu_fwd");
+  });
+  m.def("bias_gelu_bwd_blocks", &dtf_bias_gelu_bwd_blocks);
+  m.def("bias_gelu_bwd", [](uintptr_t dy, uintptr_t a, uintptr_t bias, uintptr_t da,
+                            uintptr_t part, uintptr_t dbias, int M, int N, uintptr_t st) {
+    dtf_bias_gelu_bwd(P<const bf16_t>(dy), P<const bf16_t>(a), P<const float>(bias),
+                      P<bf16_t>(da), P<float>(part), P<float>(dbias), M, N, S(st));
+    check_launch("bias_gelu_bwd");
+  });
+  m.def("attn_fwd", [](uintptr_t qkv, uintptr_t mask, uintptr_t out, uintptr_t lse, int B, int S_,
+                       int H, float scale, float p, uint32_t seed, uintptr_t st) {
+    dtf_attn_fwd(P<const bf16_t>(qkv), P<const float>(mask), P<bf16_t>(out), P<float>(lse), B,
+                 S_, H, scale, p, seed, S(st));
+    check_launch("attn_fwd");
+  });
+  m.def("attn_bwd", [](uintptr_t qkv, uintptr_t mask, uintptr_t out, uintptr_t dout,
+                       uintptr_t lse, uintptr_t delta, uintptr_t dqkv, int B, int S_, int H,
+                       float scale, float p, uint32_t seed, uintptr_t st) {
+    dtf_attn_bwd(P<const bf16_t>(qkv), P<const float>(mask), P<const bf16_t>(out),
+                 P<const bf16_t>(dout), P<const float>(lse), P<float>(delta), P<bf16_t>(dqkv), B,
+                 S_, H, scale, p, seed, S(st));
+    check_launch("attn_bwd");
+  });
+  m.def("segment_sum", [](uintptr_t sorted_ids, uintptr_t perm, uintptr_t src, uintptr_t out,
+                          int T, int H, uintptr_t st) {
+    dtf_segment_sum(P<const int64_t>(sorted_ids), P<const int64_t>(perm), P<const bf16_t>(src),
+                    P<float>(out), T, H, S(st));
+    check_launch("segment_sum");
+  });
+  m.def("mlm_xent", [](uintptr_t logits, uintptr_t labels, uintptr_t weights, uintptr_t denom,
+                       int N, int V, uintptr_t loss_rows, uintptr_t grad, uintptr_t st) {
+    dtf_mlm_xent(P<const bf16_t>(logits), P<const int64_t>(labels), P<const float>(weights),
+                 P<const float>(denom), N, V, P<float>(loss_rows), P<bf16_t>(grad), S(st));
+    check_launch("mlm_xent");
+  });
 }

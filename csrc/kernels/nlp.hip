@@ -1,0 +1,807 @@
+// Transformer (BERT-base MLM, BASELINE.json config 5) kernels for gfx950: SURVEY.md N-K7/N-K8.
+//
+//  * LayerNorm forward/backward with the surrounding elementwise work fused in:
+//      s = dropout(a + bias) + residual ;  y = dropout_post(LN(s))
+//    (encoder sub-layers use the pre-dropout + residual form, the embeddings the post-dropout
+//    form).  One wave per row, every lane owns NV 4-element chunks (H = 256*NV); backward
+//    emits dx plus deterministic per-block partial sums of dgamma / dbeta / dbias that a
+//    column-reduction kernel folds in fixed order (no atomics).
+//  * bias + GELU (tanh form of google-research/bert modeling.py) forward / backward with the
+//    bias gradient reduced in the same pass.
+//  * Flash-style attention for head_dim 64 on v_mfma_f32_16x16x32_bf16, reading Q/K/V straight
+//    out of the fused [T, 3*H*64] QKV GEMM output (no transposes) and writing [T, H*64]:
+//      fwd  : per 16-query wave, S^T = K.Q^T so every lane owns ONE query column -> the online
+//             softmax max/sum is lane-local except one xor-16/xor-32 exchange; P^T goes from the
+//             accumulator straight into the B operand of O^T = V^T.P^T (keys permuted
+//             consistently in both operands), V^T is read with ds_read_b64_tr_b16.
+//      bwd  : two deterministic kernels (no dQ atomics): dK/dV per 16-key wave sweeping all
+//             queries, dQ per 16-query wave sweeping all keys; P is recomputed from the saved
+//             log2-domain LSE; delta = rowsum(dO*O) comes from a small prep kernel.
+//    Attention dropout uses a counter-based hash of (seed, b, h, q, k) so the backward
+//    regenerates the mask instead of storing it.
+//  * Embedding gather+sum+LN forward, deterministic segment-sum backward for the word table.
+//  * MLM cross-entropy over bf16 logits with per-prediction weights (loss = sum(w*nll)/sum(w)).
+#include "common.h"
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+DTF_DEV uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+// keep with probability 1 - thr/2^32 (thr == 0: dropout off)
+DTF_DEV bool keep_elem(uint32_t seed, uint32_t idx, uint32_t thr) {
+  return fmix32(idx * 0x9E3779B1u + seed) >= thr;
+}
+
+DTF_DEV void load4(const bf16_t* p, float* f) {
+  const uint2 v = *(const uint2*)p;
+  f[0] = __builtin_bit_cast(float, v.x << 16);
+  f[1] = __builtin_bit_cast(float, v.x & 0xffff0000u);
+  f[2] = __builtin_bit_cast(float, v.y << 16);
+  f[3] = __builtin_bit_cast(float, v.y & 0xffff0000u);
+}
+DTF_DEV void store4(bf16_t* p, const float* f) {
+  uint2 v;
+  v.x = pack2(f[0], f[1]);
+  v.y = pack2(f[2], f[3]);
+  *(uint2*)p = v;
+}
+DTF_DEV float round_bf(float x) { return bf2f(f2bf(x)); }
+
+struct LnArgs {
+  const bf16_t* a;        // [M, H] main input
+  const float* bias;      // [H] or null (added to a before the pre-dropout)
+  const bf16_t* res;      // [M, H] or null
+  const float* gamma;
+  const float* beta;
+  bf16_t* y;              // [M, H] output
+  bf16_t* s;              // [M, H] saved LN input (null: not saved; then s == a)
+  float* mean;
+  float* rstd;
+  // embedding mode (a == null): s = word[ids] + pos[row % S] + type[tt]
+  const int64_t* ids;
+  const int64_t* tt;
+  const bf16_t* word;
+  const bf16_t* pos;
+  const bf16_t* type;
+  int M, S;
+  float eps;
+  uint32_t seed_pre, thr_pre;
+  uint32_t seed_post, thr_post;
+  float inv_keep_pre, inv_keep_post;
+};
+
+template <int NV>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const LnArgs g) {
+  constexpr int H = NV * 256;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= g.M) return;
+  const long base = (long)row * H;
+  float v[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int col = (i * 64 + lane) * 4;
+    if (g.a) {
+      load4(g.a + base + col, v[i]);
+      if (g.bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[i][e] += g.bias[col + e];
+      }
+      if (g.thr_pre) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[i][e] = keep_elem(g.seed_pre, (uint32_t)(base + col + e), g.thr_pre)
+                        ? v[i][e] * g.inv_keep_pre : 0.f;
+      }
+      if (g.res) {
+        float r[4];
+        load4(g.res + base + col, r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[i][e] += r[e];
+      }
+    } else {
+      float w[4], p[4], t[4];
+      load4(g.word + g.ids[row] * (long)H + col, w);
+      load4(g.pos + (long)(row % g.S) * H + col, p);
+      load4(g.type + (g.tt ? g.tt[row] : 0) * (long)H + col, t);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[i][e] = w[e] + p[e] + t[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[i][e] = round_bf(v[i][e]);   // stats of exactly what is saved
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sum += v[i][e];
+  const float mean = wave_sum(sum) * (1.f / H);
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[i][e] - mean;
+      sq += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(sq) * (1.f / H) + g.eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int col = (i * 64 + lane) * 4;
+    if (g.s) store4(g.s + base + col, v[i]);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = (v[i][e] - mean) * rstd * g.gamma[col + e] + g.beta[col + e];
+      if (g.thr_post)
+        o[e] = keep_elem(g.seed_post, (uint32_t)(base + col + e), g.thr_post)
+                   ? o[e] * g.inv_keep_post : 0.f;
+    }
+    store4(g.y + base + col, o);
+  }
+  if (lane == 0) {
+    g.mean[row] = mean;
+    g.rstd[row] = rstd;
+  }
+}
+
+struct LnBwdArgs {
+  const bf16_t* dy;       // [M, H]
+  const bf16_t* s;        // saved LN input
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  bf16_t* ds;             // [M, H] d(LN input) (= d residual)
+  bf16_t* da;             // [M, H] d(a) when a pre-dropout was applied (else null: da == ds)
+  float* part_g;          // [nblk, H]
+  float* part_b;          // [nblk, H]
+  float* part_bias;       // [nblk, H] or null
+  int M, rows_per_block;
+  uint32_t seed_pre, thr_pre, seed_post, thr_post;
+  float inv_keep_pre, inv_keep_post;
+};
+
+template <int NV>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs g) {
+  constexpr int H = NV * 256;
+  __shared__ float red[4][H];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float ag[NV][4], ab[NV][4], abias[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ag[i][e] = ab[i][e] = abias[i][e] = 0.f;
+  const int r0 = blockIdx.x * g.rows_per_block;
+  const int r1 = min(g.M, r0 + g.rows_per_block);
+  for (int row = r0 + wave; row < r1; row += 4) {
+    const long base = (long)row * H;
+    const float mean = g.mean[row], rstd = g.rstd[row];
+    float dy[NV][4], xh[NV][4], gy[NV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = (i * 64 + lane) * 4;
+      float sv[4];
+      load4(g.dy + base + col, dy[i]);
+      load4(g.s + base + col, sv);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (g.thr_post)
+          dy[i][e] = keep_elem(g.seed_post, (uint32_t)(base + col + e), g.thr_post)
+                         ? dy[i][e] * g.inv_keep_post : 0.f;
+        xh[i][e] = (sv[e] - mean) * rstd;
+        gy[i][e] = dy[i][e] * g.gamma[col + e];
+        s1 += gy[i][e];
+        s2 += gy[i][e] * xh[i][e];
+      }
+    }
+    s1 = wave_sum(s1) * (1.f / H);
+    s2 = wave_sum(s2) * (1.f / H);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int col = (i * 64 + lane) * 4;
+      float dx[4], da[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dx[e] = rstd * (gy[i][e] - s1 - xh[i][e] * s2);
+        ag[i][e] += dy[i][e] * xh[i][e];
+        ab[i][e] += dy[i][e];
+        if (g.thr_pre)
+          da[e] = keep_elem(g.seed_pre, (uint32_t)(base + col + e), g.thr_pre)
+                      ? dx[e] * g.inv_keep_pre : 0.f;
+        else
+          da[e] = dx[e];
+        abias[i][e] += da[e];
+      }
+      store4(g.ds + base + col, dx);
+      if (g.da) store4(g.da + base + col, da);
+    }
+  }
+  // fixed-order block reduction of the three column partials
+  float* outs[3] = {g.part_g, g.part_b, g.part_bias};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (!outs[k]) continue;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        red[wave][(i * 64 + lane) * 4 + e] = k == 0 ? ag[i][e] : (k == 1 ? ab[i][e] : abias[i][e]);
+    __syncthreads();
+    for (int c = threadIdx.x; c < H; c += 256)
+      outs[k][(long)blockIdx.x * H + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+  }
+}
+
+// out[c] (+)= sum_p part[p, c] in fixed order
+__global__ void __launch_bounds__(256)
+col_sum_kernel(const float* __restrict__ part, int P, int N, float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(long)p * N + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ----------------------------------------------------------------------------- bias + GELU
+constexpr float kGeluK0 = 0.7978845608028654f;   // sqrt(2/pi)
+constexpr float kGeluK1 = 0.044715f;
+
+DTF_DEV float gelu_f(float x) {
+  const float t = tanhf(kGeluK0 * (x + kGeluK1 * x * x * x));
+  return 0.5f * x * (1.f + t);
+}
+DTF_DEV float gelu_grad(float x) {
+  const float t = tanhf(kGeluK0 * (x + kGeluK1 * x * x * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluK0 * (1.f + 3.f * kGeluK1 * x * x);
+}
+
+__global__ void __launch_bounds__(256)
+bias_gelu_fwd_kernel(const bf16_t* __restrict__ a, const float* __restrict__ bias,
+                     bf16_t* __restrict__ y, long n8, int N) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const int col = (int)((i * 8) % N);
+  float f[8];
+  unpack8(((const uint4*)a)[i], f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = gelu_f(f[e] + (bias ? bias[col + e] : 0.f));
+  ((uint4*)y)[i] = pack8(f);
+}
+
+// block = (row tile of R rows) x (all columns); thread owns column vectors cv = tid + 256*j
+__global__ void __launch_bounds__(256)
+bias_gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ a,
+                     const float* __restrict__ bias, bf16_t* __restrict__ da,
+                     float* __restrict__ part, int M, int N, int R) {
+  const int nv = N / 8;
+  const int r0 = blockIdx.x * R, r1 = min(M, r0 + R);
+  for (int cv = threadIdx.x; cv < nv; cv += 256) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float bb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bb[e] = bias ? bias[cv * 8 + e] : 0.f;
+    for (int r = r0; r < r1; ++r) {
+      const long off = (long)r * nv + cv;
+      float fd[8], fa[8];
+      unpack8(((const uint4*)dy)[off], fd);
+      unpack8(((const uint4*)a)[off], fa);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        fd[e] *= gelu_grad(fa[e] + bb[e]);
+        acc[e] += fd[e];
+      }
+      ((uint4*)da)[off] = pack8(fd);
+    }
+    if (part) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part[(long)blockIdx.x * N + cv * 8 + e] = acc[e];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- attention
+constexpr int AD = 64;    // head dim
+constexpr int ALD = 72;   // LDS row pitch in elements (144 B: 16-B aligned rows, spread banks)
+
+typedef __attribute__((ext_vector_type(4))) short s4_t;
+typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+
+struct AttnGeom {
+  int B, S, H, ld;        // ld = row pitch of the qkv / dqkv buffers (3*H*64)
+  float scale;            // softmax scale (1/sqrt(64))
+  uint32_t seed, thr;     // attention-probability dropout
+  float inv_keep;
+};
+
+DTF_DEV bf16x8_t lds_row8(const bf16_t* base, int row, int col) {
+  return *(const bf16x8_t*)(base + row * ALD + col);
+}
+// 8 keys x one column for an MFMA operand whose k index is the key permutation
+//   j < 4 : key row0 + 4g + j,   j >= 4 : key row0 + 16 + 4g + (j - 4)
+// read with ds_read_b64_tr_b16 (lane 4q+p of each 16-lane group addresses row q, cols 4p..4p+3)
+DTF_DEV bf16x8_t lds_tr8(const bf16_t* base, int row0, int col0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const bf16_t* p = base + (row0 + 4 * g + (i >> 2)) * ALD + col0 + 4 * (i & 3);
+  const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(p));
+  const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(p + 16 * ALD));
+  return (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+DTF_DEV bf16x8_t pack_frag(const f32x4_t& x0, const f32x4_t& x1) {
+  return (bf16x8_t){(short)f2bf(x0[0]), (short)f2bf(x0[1]), (short)f2bf(x0[2]), (short)f2bf(x0[3]),
+                    (short)f2bf(x1[0]), (short)f2bf(x1[1]), (short)f2bf(x1[2]), (short)f2bf(x1[3])};
+}
+DTF_DEV f32x4_t mfma(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// Explicit wait states between an MFMA chain and the first VALU / accvgpr read of its result.
+// Measured need: with a (uniform) branch between the last MFMA and the read, hipcc's hazard
+// recognizer only padded the fall-through path, and the taken path read the accumulator ~1
+// instruction after a 16x16x32 MFMA issued (wrong dQ whenever dropout was off).  Fencing the
+// scheduler on both sides keeps every consumer behind the nops.
+DTF_DEV void mfma_fence() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+DTF_DEV void store4_scaled(bf16_t* p, const f32x4_t& v, float s) {
+  const float f[4] = {v[0] * s, v[1] * s, v[2] * s, v[3] * s};
+  store4(p, f);
+}
+
+// cooperative 64-row x 64-col loads of two operands (256 threads, 4 x 16 B each)
+DTF_DEV void load_two_tiles(bf16_t* d0, const bf16_t* s0, long ld0, bf16_t* d1, const bf16_t* s1,
+                            long ld1, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = tid + 256 * i;
+    const int sel = v >> 9, row = (v >> 3) & 63, cc = (v & 7) * 8;
+    const uint4 x = sel ? *(const uint4*)(s1 + row * ld1 + cc) : *(const uint4*)(s0 + row * ld0 + cc);
+    *(uint4*)((sel ? d1 : d0) + row * ALD + cc) = x;
+  }
+}
+
+template <bool DROP>
+__global__ void __launch_bounds__(256)
+attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                bf16_t* __restrict__ out, float* __restrict__ lse, const AttnGeom g) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[64 * ALD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[64 * ALD];
+  __shared__ float Ms[64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = lane >> 4, li = lane & 15;
+  const int h = blockIdx.y, b = blockIdx.z, S = g.S, H = g.H;
+  const long tok0 = (long)b * S;
+  const int q = blockIdx.x * 64 + w * 16 + li;
+  const bf16_t* qrow = qkv + (tok0 + q) * g.ld + h * AD;
+  const bf16x8_t bq0 = *(const bf16x8_t*)(qrow + 8 * gq);
+  const bf16x8_t bq1 = *(const bf16x8_t*)(qrow + 32 + 8 * gq);
+  const float c = g.scale * kLog2e;
+  const uint32_t kbase = (uint32_t)((((long)b * H + h) * S + q) * S);
+  float m = -INFINITY, l = 0.f;
+  f32x4_t acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  for (int kc = 0; kc < S; kc += 64) {
+    __syncthreads();
+    load_two_tiles(Ks, qkv + (tok0 + kc) * g.ld + (H + h) * AD, g.ld,
+                   Vs, qkv + (tok0 + kc) * g.ld + (2 * H + h) * AD, g.ld, tid);
+    if (tid < 64) Ms[tid] = mask ? mask[tok0 + kc + tid] * kLog2e : 0.f;
+    __syncthreads();
+    f32x4_t s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      s[t] = mfma(lds_row8(Ks, 16 * t + li, 8 * gq), bq0, s[t]);
+      s[t] = mfma(lds_row8(Ks, 16 * t + li, 32 + 8 * gq), bq1, s[t]);
+    }
+    mfma_fence();
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[t][r] = s[t][r] * c + Ms[16 * t + 4 * gq + r];
+        mloc = fmaxf(mloc, s[t][r]);
+      }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float mnew = fmaxf(m, mloc);
+    const float alpha = exp2f(m - mnew);
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] *= alpha;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[t][r] - mnew);
+        l += p;
+        if (DROP)
+          s[t][r] = keep_elem(g.seed, kbase + kc + 16 * t + 4 * gq + r, g.thr) ? p * g.inv_keep
+                                                                               : 0.f;
+        else
+          s[t][r] = p;
+      }
+    const bf16x8_t bp0 = pack_frag(s[0], s[1]);
+    const bf16x8_t bp1 = pack_frag(s[2], s[3]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      acc[dt] = mfma(lds_tr8(Vs, 0, 16 * dt, lane), bp0, acc[dt]);
+      acc[dt] = mfma(lds_tr8(Vs, 32, 16 * dt, lane), bp1, acc[dt]);
+    }
+    m = mnew;
+  }
+  mfma_fence();
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  bf16_t* orow = out + (tok0 + q) * (long)(H * AD) + h * AD;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) store4_scaled(orow + 16 * dt + 4 * gq, acc[dt], inv);
+  if (gq == 0) lse[((long)b * H + h) * S + q] = m + log2f(l);
+}
+
+// delta[b,h,s] = sum_d O * dO  (one thread per (token, head))
+__global__ void __launch_bounds__(256)
+attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
+                  float* __restrict__ delta, int B, int S, int H) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * S * H) return;
+  const long tok = i / H;
+  const int h = (int)(i % H);
+  const uint4* o = (const uint4*)(O + tok * H * AD + h * AD);
+  const uint4* d = (const uint4*)(dO + tok * H * AD + h * AD);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < AD / 8; ++k) {
+    float a[8], c[8];
+    unpack8(o[k], a);
+    unpack8(d[k], c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += a[e] * c[e];
+  }
+  const long b = tok / S, sq = tok % S;
+  delta[(b * H + h) * S + sq] = s;
+}
+
+template <bool DROP>
+__global__ void __launch_bounds__(256)
+attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                    const bf16_t* __restrict__ dO, const float* __restrict__ lse,
+                    const float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom g) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[64 * ALD];
+  __shared__ __attribute__((aligned(16))) bf16_t Os[64 * ALD];
+  __shared__ float Ls[64], Ds[64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = lane >> 4, li = lane & 15;
+  const int h = blockIdx.y, b = blockIdx.z, S = g.S, H = g.H;
+  const long tok0 = (long)b * S;
+  const int k = blockIdx.x * 64 + w * 16 + li;            // this lane's key
+  const bf16_t* krow = qkv + (tok0 + k) * g.ld + (H + h) * AD;
+  const bf16_t* vrow = qkv + (tok0 + k) * g.ld + (2 * H + h) * AD;
+  const bf16x8_t bk0 = *(const bf16x8_t*)(krow + 8 * gq), bk1 = *(const bf16x8_t*)(krow + 32 + 8 * gq);
+  const bf16x8_t bv0 = *(const bf16x8_t*)(vrow + 8 * gq), bv1 = *(const bf16x8_t*)(vrow + 32 + 8 * gq);
+  const float mk = mask ? mask[tok0 + k] * kLog2e : 0.f;
+  const float c = g.scale * kLog2e;
+  const long bh = (long)b * H + h;
+  f32x4_t dv[4], dk[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dv[dt] = dk[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  for (int qc = 0; qc < S; qc += 64) {
+    __syncthreads();
+    load_two_tiles(Qs, qkv + (tok0 + qc) * g.ld + h * AD, g.ld,
+                   Os, dO + (tok0 + qc) * (long)(H * AD) + h * AD, H * AD, tid);
+    if (tid < 64) {
+      Ls[tid] = lse[bh * S + qc + tid];
+      Ds[tid] = delta[bh * S + qc + tid];
+    }
+    __syncthreads();
+    f32x4_t P[4], dS[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      f32x4_t s = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dp = s;
+      s = mfma(lds_row8(Qs, 16 * qt + li, 8 * gq), bk0, s);
+      s = mfma(lds_row8(Qs, 16 * qt + li, 32 + 8 * gq), bk1, s);
+      dp = mfma(lds_row8(Os, 16 * qt + li, 8 * gq), bv0, dp);
+      dp = mfma(lds_row8(Os, 16 * qt + li, 32 + 8 * gq), bv1, dp);
+      mfma_fence();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = 16 * qt + 4 * gq + r;
+        const float p = exp2f(s[r] * c + mk - Ls[qq]);
+        if (DROP) {
+          const bool kp = keep_elem(g.seed, (uint32_t)((bh * S + qc + qq) * S + k), g.thr);
+          P[qt][r] = kp ? p * g.inv_keep : 0.f;
+          dS[qt][r] = p * ((kp ? dp[r] * g.inv_keep : 0.f) - Ds[qq]);
+        } else {
+          P[qt][r] = p;
+          dS[qt][r] = p * (dp[r] - Ds[qq]);
+        }
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t bP = pack_frag(P[2 * ks], P[2 * ks + 1]);
+      const bf16x8_t bS = pack_frag(dS[2 * ks], dS[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma(lds_tr8(Os, 32 * ks, 16 * dt, lane), bP, dv[dt]);
+        dk[dt] = mfma(lds_tr8(Qs, 32 * ks, 16 * dt, lane), bS, dk[dt]);
+      }
+    }
+  }
+  // dV^T / dK^T accumulators: column = this lane's key, rows d = 16dt + 4gq + r
+  mfma_fence();
+  bf16_t* dkrow = dqkv + (tok0 + k) * g.ld + (H + h) * AD;
+  bf16_t* dvrow = dqkv + (tok0 + k) * g.ld + (2 * H + h) * AD;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    store4_scaled(dkrow + 16 * dt + 4 * gq, dk[dt], g.scale);
+    store4_scaled(dvrow + 16 * dt + 4 * gq, dv[dt], 1.f);
+  }
+}
+
+template <bool DROP>
+__global__ void __launch_bounds__(256)
+attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                   const bf16_t* __restrict__ dO, const float* __restrict__ lse,
+                   const float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom g) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[64 * ALD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[64 * ALD];
+  __shared__ float Ms[64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = lane >> 4, li = lane & 15;
+  const int h = blockIdx.y, b = blockIdx.z, S = g.S, H = g.H;
+  const long tok0 = (long)b * S;
+  const int q = blockIdx.x * 64 + w * 16 + li;
+  const bf16_t* qrow = qkv + (tok0 + q) * g.ld + h * AD;
+  const bf16_t* orow = dO + (tok0 + q) * (long)(H * AD) + h * AD;
+  const bf16x8_t bq0 = *(const bf16x8_t*)(qrow + 8 * gq), bq1 = *(const bf16x8_t*)(qrow + 32 + 8 * gq);
+  const bf16x8_t bo0 = *(const bf16x8_t*)(orow + 8 * gq), bo1 = *(const bf16x8_t*)(orow + 32 + 8 * gq);
+  const long bh = (long)b * H + h;
+  const float lq = lse[bh * S + q], dl = delta[bh * S + q];
+  const float c = g.scale * kLog2e;
+  const uint32_t kbase = (uint32_t)((bh * S + q) * S);
+  f32x4_t dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  for (int kc = 0; kc < S; kc += 64) {
+    __syncthreads();
+    load_two_tiles(Ks, qkv + (tok0 + kc) * g.ld + (H + h) * AD, g.ld,
+                   Vs, qkv + (tok0 + kc) * g.ld + (2 * H + h) * AD, g.ld, tid);
+    if (tid < 64) Ms[tid] = mask ? mask[tok0 + kc + tid] * kLog2e : 0.f;
+    __syncthreads();
+    f32x4_t dS[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4_t s = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dp = s;
+      s = mfma(lds_row8(Ks, 16 * t + li, 8 * gq), bq0, s);
+      s = mfma(lds_row8(Ks, 16 * t + li, 32 + 8 * gq), bq1, s);
+      dp = mfma(lds_row8(Vs, 16 * t + li, 8 * gq), bo0, dp);
+      dp = mfma(lds_row8(Vs, 16 * t + li, 32 + 8 * gq), bo1, dp);
+      mfma_fence();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * t + 4 * gq + r;
+        const float p = exp2f(s[r] * c + Ms[key] - lq);
+        float dpu = dp[r];
+        if (DROP) dpu = keep_elem(g.seed, kbase + kc + key, g.thr) ? dpu * g.inv_keep : 0.f;
+        dS[t][r] = p * (dpu - dl);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t bS = pack_frag(dS[2 * ks], dS[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma(lds_tr8(Ks, 32 * ks, 16 * dt, lane), bS, dq[dt]);
+    }
+  }
+  mfma_fence();
+  bf16_t* dqrow = dqkv + (tok0 + q) * g.ld + h * AD;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) store4_scaled(dqrow + 16 * dt + 4 * gq, dq[dt], g.scale);
+}
+
+// ----------------------------------------------------------------------------- embeddings
+// out[ids_sorted[i]] = sum over the run of equal ids of src[perm[j]]  (one wave per run start)
+__global__ void __launch_bounds__(256)
+segment_sum_kernel(const int64_t* __restrict__ sorted_ids, const int64_t* __restrict__ perm,
+                   const bf16_t* __restrict__ src, float* __restrict__ out, int T, int H) {
+  const int i = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (i >= T) return;
+  const int64_t id = sorted_ids[i];
+  if (i > 0 && sorted_ids[i - 1] == id) return;
+  for (int c0 = lane * 4; c0 < H; c0 += 256) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j = i; j < T && sorted_ids[j] == id; ++j) {
+      float v[4];
+      load4(src + perm[j] * (long)H + c0, v);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += v[e];
+    }
+    float* o = out + id * (long)H + c0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] += acc[e];
+  }
+}
+
+// ----------------------------------------------------------------------------- MLM loss
+// rows: loss_rows[i] = w_i * (lse - logit[label]) / denom ; grad = w_i * (softmax - onehot) / denom
+__global__ void __launch_bounds__(256)
+mlm_xent_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ labels,
+                const float* __restrict__ weights, const float* __restrict__ denom, int N, int V,
+                float* __restrict__ loss_rows, bf16_t* __restrict__ grad) {
+  const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= N) return;
+  const bf16_t* x = logits + (long)row * V;
+  float mx = -INFINITY, s = 0.f;
+  for (int i = lane; i < V; i += 64) {
+    const float v = bf2f(x[i]);
+    if (v > mx) {
+      s = s * __expf(mx - v) + 1.f;
+      mx = v;
+    } else {
+      s += __expf(v - mx);
+    }
+  }
+  // combine (max, sum) pairs across the wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(mx, om);
+    s = (mx == -INFINITY ? 0.f : s * __expf(mx - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    mx = nm;
+  }
+  const float lse = mx + __logf(s);
+  const int lab = (int)labels[row];
+  const float wsc = weights ? weights[row] / fmaxf(denom[0], 1e-5f) : 1.f / fmaxf(denom[0], 1e-5f);
+  if (lane == 0) loss_rows[row] = wsc * (lse - bf2f(x[lab]));
+  if (grad) {
+    bf16_t* gr = grad + (long)row * V;
+    for (int i = lane; i < V; i += 64) {
+      const float p = __expf(bf2f(x[i]) - lse);
+      gr[i] = f2bf(wsc * (p - (i == lab ? 1.f : 0.f)));
+    }
+  }
+}
+
+}  // namespace
+
+// ============================================================================= launchers
+
+static uint32_t drop_thr(float p) {
+  if (p <= 0.f) return 0u;
+  const double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+}
+
+void dtf_ln_fwd(const bf16_t* a, const float* bias, const bf16_t* res, const float* gamma,
+                const float* beta, bf16_t* y, bf16_t* s, float* mean, float* rstd, int M, int H,
+                float eps, float p_pre, uint32_t seed_pre, float p_post, uint32_t seed_post,
+                const int64_t* ids, const int64_t* tt, const bf16_t* word, const bf16_t* pos,
+                const bf16_t* type, int S, hipStream_t st) {
+  if (H % 256 != 0 || H > 1024) throw std::runtime_error("ln_fwd: H must be 256/512/768/1024");
+  LnArgs g{a, bias, res, gamma, beta, y, s, mean, rstd, ids, tt, word, pos, type, M, S, eps,
+           seed_pre, drop_thr(p_pre), seed_post, drop_thr(p_post),
+           p_pre > 0.f ? 1.f / (1.f - p_pre) : 1.f, p_post > 0.f ? 1.f / (1.f - p_post) : 1.f};
+  const dim3 grid((M + 3) / 4), block(256);
+  switch (H / 256) {
+    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, block, 0, st, g); break;
+    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, block, 0, st, g); break;
+    case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, block, 0, st, g); break;
+    default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, block, 0, st, g); break;
+  }
+}
+
+int dtf_ln_bwd_blocks(int M) { return (M + 31) / 32; }
+
+void dtf_ln_bwd(const bf16_t* dy, const bf16_t* s, const float* mean, const float* rstd,
+                const float* gamma, bf16_t* ds, bf16_t* da, float* part, float* dgamma,
+                float* dbeta, float* dbias, int M, int H, float p_pre, uint32_t seed_pre,
+                float p_post, uint32_t seed_post, hipStream_t st) {
+  if (H % 256 != 0 || H > 1024) throw std::runtime_error("ln_bwd: H must be 256/512/768/1024");
+  const int nblk = dtf_ln_bwd_blocks(M);
+  float* pg = part;
+  float* pb = part + (long)nblk * H;
+  float* pbias = dbias ? part + 2L * nblk * H : nullptr;
+  LnBwdArgs g{dy, s, mean, rstd, gamma, ds, da, pg, pb, pbias, M, 32,
+              seed_pre, drop_thr(p_pre), seed_post, drop_thr(p_post),
+              p_pre > 0.f ? 1.f / (1.f - p_pre) : 1.f, p_post > 0.f ? 1.f / (1.f - p_post) : 1.f};
+  const dim3 grid(nblk), block(256);
+  switch (H / 256) {
+    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, st, g); break;
+    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, st, g); break;
+    case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, st, g); break;
+    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, block, 0, st, g); break;
+  }
+  const dim3 cg((H + 255) / 256);
+  hipLaunchKernelGGL(col_sum_kernel, cg, block, 0, st, pg, nblk, H, dgamma, 0);
+  hipLaunchKernelGGL(col_sum_kernel, cg, block, 0, st, pb, nblk, H, dbeta, 0);
+  if (dbias) hipLaunchKernelGGL(col_sum_kernel, cg, block, 0, st, pbias, nblk, H, dbias, 0);
+}
+
+void dtf_bias_gelu_fwd(const bf16_t* a, const float* bias, bf16_t* y, long M, int N,
+                       hipStream_t st) {
+  if (N % 8) throw std::runtime_error("bias_gelu: N % 8 != 0");
+  const long n8 = M * N / 8;
+  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st,
+                     a, bias, y, n8, N);
+}
+
+int dtf_bias_gelu_bwd_blocks(int M) { return (M + 15) / 16; }
+
+void dtf_bias_gelu_bwd(const bf16_t* dy, const bf16_t* a, const float* bias, bf16_t* da,
+                       float* part, float* dbias, int M, int N, hipStream_t st) {
+  if (N % 8) throw std::runtime_error("bias_gelu: N % 8 != 0");
+  const int nblk = dtf_bias_gelu_bwd_blocks(M);
+  hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3(nblk), dim3(256), 0, st, dy, a, bias, da,
+                     dbias ? part : nullptr, M, N, 16);
+  if (dbias)
+    hipLaunchKernelGGL(col_sum_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part, nblk, N,
+                       dbias, 0);
+}
+
+static AttnGeom attn_geom(int B, int S, int H, float scale, float p, uint32_t seed) {
+  if (S % 64) throw std::runtime_error("attention: seq_len must be a multiple of 64");
+  if ((long)B * H * S * S > 0xFFFFFFFFL && p > 0.f)
+    throw std::runtime_error("attention dropout index space exceeds 32 bits");
+  return AttnGeom{B, S, H, 3 * H * AD, scale, seed, drop_thr(p), p > 0.f ? 1.f / (1.f - p) : 1.f};
+}
+
+void dtf_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int B, int S,
+                  int H, float scale, float p, uint32_t seed, hipStream_t st) {
+  const AttnGeom g = attn_geom(B, S, H, scale, p, seed);
+  if (g.thr)
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3(S / 64, H, B), dim3(256), 0, st, qkv, mask,
+                       out, lse, g);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3(S / 64, H, B), dim3(256), 0, st, qkv, mask,
+                       out, lse, g);
+}
+
+void dtf_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* out, const bf16_t* dout,
+                  const float* lse, float* delta, bf16_t* dqkv, int B, int S, int H, float scale,
+                  float p, uint32_t seed, hipStream_t st) {
+  const AttnGeom g = attn_geom(B, S, H, scale, p, seed);
+  const long n = (long)B * S * H;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out,
+                     dout, delta, B, S, H);
+  const dim3 grid(S / 64, H, B);
+  if (g.thr) {
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<true>, grid, dim3(256), 0, st, qkv, mask, dout, lse,
+                       delta, dqkv, g);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid, dim3(256), 0, st, qkv, mask, dout, lse,
+                       delta, dqkv, g);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<false>, grid, dim3(256), 0, st, qkv, mask, dout, lse,
+                       delta, dqkv, g);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid, dim3(256), 0, st, qkv, mask, dout, lse,
+                       delta, dqkv, g);
+  }
+}
+
+void dtf_segment_sum(const int64_t* sorted_ids, const int64_t* perm, const bf16_t* src,
+                     float* out, int T, int H, hipStream_t st) {
+  if (H % 4) throw std::runtime_error("segment_sum: H % 4 != 0");
+  hipLaunchKernelGGL(segment_sum_kernel, dim3((T * 64 + 255) / 256), dim3(256), 0, st, sorted_ids,
+                     perm, src, out, T, H);
+}
+
+void dtf_mlm_xent(const bf16_t* logits, const int64_t* labels, const float* weights,
+                  const float* denom, int N, int V, float* loss_rows, bf16_t* grad,
+                  hipStream_t st) {
+  hipLaunchKernelGGL(mlm_xent_kernel, dim3((N * 64 + 255) / 256), dim3(256), 0, st, logits,
+                     labels, weights, denom, N, V, loss_rows, grad);
+}

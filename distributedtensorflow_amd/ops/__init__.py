@@ -113,8 +113,51 @@ def dropout(x, p, training=True):
     return reference.dropout(x, p, training)
 
 
+def _nlp():
+    from . import native_nlp
+    return native_nlp
+
+
+def bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p=0.0, training=True, eps=1e-12):
+    """LN(dropout(a + bias) + residual): the BERT sub-layer output, one fused kernel."""
+    if _use_native(a):
+        return _nlp().bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p, training, eps)
+    return reference.bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p, training, eps)
+
+
+def embedding_layer_norm(ids, token_type_ids, word, pos, typ, gamma, beta, p=0.0, training=True,
+                         eps=1e-12, dtype=None):
+    """dropout(LN(word[ids] + pos + type[tt])) -> [B*S, H]."""
+    if _use_native(word):
+        return _nlp().embedding_layer_norm(ids, token_type_ids, word, pos, typ, gamma, beta, p,
+                                           training, eps)
+    return reference.embedding_layer_norm(ids, token_type_ids, word, pos, typ, gamma, beta, p,
+                                          training, eps, dtype=dtype)
+
+
+def bias_gelu(a, bias=None):
+    if _use_native(a):
+        return _nlp().bias_gelu(a, bias)
+    return reference.bias_gelu(a, bias)
+
+
+def attention_qkv(qkv, mask, batch, seq_len, heads, p=0.0, training=True, scale=None):
+    """Multi-head self-attention straight from the fused QKV projection output."""
+    if _use_native(qkv):
+        return _nlp().attention_qkv(qkv, mask, batch, seq_len, heads, p, training, scale)
+    return reference.attention_qkv(qkv, mask, batch, seq_len, heads, p, training, scale)
+
+
+def mlm_loss(logits, labels, weights=None):
+    if _use_native(logits):
+        return _nlp().mlm_loss(logits, labels, weights)
+    return reference.mlm_loss(logits, labels, weights)
+
+
 __all__ = [
     "set_backend", "get_backend", "conv2d", "batch_norm", "relu", "max_pool2d",
     "global_avg_pool", "dense", "sparse_softmax_cross_entropy",
     "softmax_cross_entropy_clipped_sum", "layer_norm", "gelu", "attention", "dropout",
+    "bias_dropout_add_layer_norm", "embedding_layer_norm", "bias_gelu", "attention_qkv",
+    "mlm_loss",
 ]

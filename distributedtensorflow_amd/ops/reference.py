@@ -149,3 +149,128 @@ def attention(q, k, v, mask=None, scale=None):
 
 def dropout(x, p, training=True):
     return F.dropout(x, p, training)
+
+
+# ----------------------------------------------------------------------------- transformer ops
+# Bit-exact twins of csrc/kernels/nlp.hip (same hash-based dropout masks), used as the CPU path
+# and as the oracle of the GPU numerics tests.
+
+_M32 = 0xFFFFFFFF
+
+
+def _fmix32(h):
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _M32
+    return h ^ (h >> 16)
+
+
+def drop_threshold(p):
+    import numpy as np
+    if p <= 0:
+        return 0
+    t = float(np.float32(p)) * 4294967296.0
+    return 4294967295 if t >= 4294967295.0 else int(t)
+
+
+def keep_mask(seed, idx, p):
+    """keep(idx) of the kernels: fmix32(idx * 0x9E3779B1 + seed) >= p * 2^32 (uint32 math)."""
+    idx = idx.to(torch.int64) & _M32
+    h = _fmix32((idx * 0x9E3779B1 + int(seed)) & _M32)
+    return h >= drop_threshold(p)
+
+
+def _drop(x, p, seed, idx):
+    if p <= 0:
+        return x
+    return torch.where(keep_mask(seed, idx, p), x / (1.0 - float(torch.tensor(p, dtype=torch.float32))), torch.zeros_like(x))
+
+
+def _rows_cols_idx(M, H, device):
+    return torch.arange(M * H, device=device, dtype=torch.int64).view(M, H)
+
+
+def _next_seed(p):
+    return int(torch.randint(0, 2 ** 31 - 1, (1,), device="cpu").item()) if p > 0 else 0
+
+
+def _round_st(t, dtype):
+    """Round the forward value to ``dtype`` (what the kernels store) while the gradient passes
+    through in full precision (the kernels accumulate gradients in fp32)."""
+    if dtype == t.dtype:
+        return t
+    return t + (t.to(dtype).to(t.dtype) - t).detach()
+
+
+def _ln(s, gamma, beta, eps):
+    mean = s.mean(-1, keepdim=True)
+    var = s.var(-1, unbiased=False, keepdim=True)
+    return (s - mean) * torch.rsqrt(var + eps) * gamma.float() + beta.float()
+
+
+def bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p=0.0, training=True, eps=1e-12,
+                                seed=None):
+    p = p if training else 0.0
+    H = a.shape[-1]
+    s = a.float().reshape(-1, H)
+    if bias is not None:
+        s = s + bias.float()
+    if p > 0:
+        seed = _next_seed(p) if seed is None else seed
+        s = _drop(s, p, seed, _rows_cols_idx(s.shape[0], H, s.device))
+    if residual is not None:
+        s = s + residual.float().reshape(-1, H)
+    s = _round_st(s, a.dtype)
+    return _ln(s, gamma, beta, eps).to(a.dtype).view(a.shape)
+
+
+def embedding_layer_norm(ids, token_type_ids, word, pos, typ, gamma, beta, p=0.0, training=True,
+                         eps=1e-12, seed=None, dtype=None):
+    p = p if training else 0.0
+    B, S = ids.shape
+    H = word.shape[1]
+    dtype = dtype or word.dtype
+    tt = token_type_ids if token_type_ids is not None else torch.zeros_like(ids)
+    w32, p32, t32 = (_round_st(t.float(), dtype) for t in (word, pos, typ))
+    s = (w32[ids] + p32[:S].unsqueeze(0) + t32[tt]).reshape(B * S, H)
+    s = _round_st(s, dtype)
+    y = _ln(s, gamma, beta, eps)
+    if p > 0:
+        seed = _next_seed(p) if seed is None else seed
+        y = _drop(y, p, seed, _rows_cols_idx(B * S, H, y.device))
+    return y.to(dtype)
+
+
+def bias_gelu(a, bias=None):
+    x = a.float() + (bias.float() if bias is not None else 0.0)
+    return F.gelu(x, approximate="tanh").to(a.dtype)
+
+
+def attention_qkv(qkv, mask, batch, seq_len, heads, p=0.0, training=True, scale=None, seed=None):
+    """qkv [B*S, 3*H*D] (all q heads | all k heads | all v heads) -> [B*S, H*D]."""
+    p = p if training else 0.0
+    B, S, Hh = batch, seq_len, heads
+    D = qkv.shape[-1] // (3 * Hh)
+    scale = D ** -0.5 if scale is None else scale
+    x = qkv.float().view(B, S, 3, Hh, D)
+    q, k, v = (x[:, :, i].permute(0, 2, 1, 3) for i in range(3))     # [B, H, S, D]
+    s = torch.matmul(q, k.transpose(-1, -2)) * scale
+    if mask is not None:
+        s = s + mask.float().view(B, 1, 1, S)
+    prob = torch.softmax(s, dim=-1)
+    if p > 0:
+        seed = _next_seed(p) if seed is None else seed
+        idx = torch.arange(B * Hh * S * S, device=qkv.device, dtype=torch.int64).view(B, Hh, S, S)
+        prob = _drop(prob, p, seed, idx)
+    o = torch.matmul(prob, v)                                         # [B, H, S, D]
+    return o.permute(0, 2, 1, 3).reshape(B * S, Hh * D).to(qkv.dtype)
+
+
+def mlm_loss(logits, labels, weights=None):
+    """sum_i w_i * nll_i / sum_i w_i  (google-research/bert run_pretraining.py)."""
+    nll = F.cross_entropy(logits.float(), labels.reshape(-1).long(), reduction="none")
+    if weights is None:
+        return nll.mean()
+    w = weights.reshape(-1).float()
+    return (w * nll).sum() / w.sum().clamp_min(1e-5)

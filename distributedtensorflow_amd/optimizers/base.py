@@ -208,7 +208,13 @@ class Optimizer:
         out = {}
         for slot in self.slots:
             for v in self.space.order:
-                out[f"{v._dtf_name}/{slot.name}"] = self.space.view_of(slot.buf, v)
+                view = self.space.view_of(slot.buf, v)
+                splits = getattr(v, "_dtf_splits", None)   # fused variables (e.g. BERT Q|K|V)
+                if splits:
+                    for name, s, e in splits:
+                        out[f"{name}/{slot.name}"] = view[s:e]
+                else:
+                    out[f"{v._dtf_name}/{slot.name}"] = view
         return out
 
     def non_slot_variables(self):

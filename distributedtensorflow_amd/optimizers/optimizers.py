@@ -192,7 +192,7 @@ class LAMBOptimizer(Optimizer):
     """LAMB (layer-wise adaptive moments, You et al. 2019) for BERT pre-training
     (BASELINE.json config 5): per-variable trust ratio |p|/|u|."""
 
-    slot_names = ("m", "v")
+    slot_names = ("adam_m", "adam_v")     # google-research/bert optimization.py slot names
 
     def __init__(self, learning_rate, beta1=0.9, beta2=0.999, epsilon=1e-6, weight_decay=0.01,
                  name="LAMB", chunk=4096, **kw):
@@ -205,7 +205,7 @@ class LAMBOptimizer(Optimizer):
 
     def _build_slots(self):
         sp = self.space
-        self.slots = [FlatSlot("m", sp.new_slot()), FlatSlot("v", sp.new_slot())]
+        self.slots = [FlatSlot("adam_m", sp.new_slot()), FlatSlot("adam_v", sp.new_slot())]
         # chunk table {seg:int32, len:int32, start:int64} — one block per chunk
         rows = []
         wd = []

@@ -1,0 +1,257 @@
+"""BERT-base MLM path (BASELINE config 5): model structure / TF names on CPU, and the HIP
+transformer kernels (csrc/kernels/nlp.hip) against fp32 PyTorch references of the same op —
+including bit-identical hash dropout masks, so dropout-on numerics are compared exactly."""
+import pytest
+import torch
+
+from distributedtensorflow_amd import ops
+from distributedtensorflow_amd.models import collect_variables
+from distributedtensorflow_amd.models.bert import BertConfig, BertForPreTraining, bert_base
+from distributedtensorflow_amd.models.resnet import num_params
+from distributedtensorflow_amd.ops import reference as R
+from distributedtensorflow_amd.optimizers import LAMBOptimizer
+from distributedtensorflow_amd.parallel import OneDeviceStrategy
+
+TINY = dict(vocab_size=1000, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+            intermediate_size=512, max_position_embeddings=128)
+
+
+def _batch(B=4, S=64, P=10, V=1000, device="cpu", seed=0):
+    g = torch.Generator().manual_seed(seed)
+    cpu = dict(device="cpu")
+    ids = torch.randint(0, V, (B, S), generator=g, **cpu)
+    tt = (torch.arange(S, **cpu) >= S // 2).long().expand(B, S).contiguous()
+    am = torch.ones(B, S, **cpu)
+    am[1, S - 9:] = 0
+    pos = torch.randint(0, S - 10, (B, P), generator=g, **cpu)
+    lab = torch.randint(0, V, (B, P), generator=g, **cpu)
+    w = torch.ones(B, P, **cpu)
+    w[:, P - 2:] = 0
+    return [t.to(device) for t in (ids, tt, am, pos, lab, w)]
+
+
+# ----------------------------------------------------------------------------- CPU
+def test_bert_base_size_and_tf_names():
+    m = bert_base()
+    names = [n for n, _, _ in collect_variables(m)]
+    for n in ("bert/embeddings/word_embeddings", "bert/embeddings/LayerNorm/gamma",
+              "bert/encoder/layer_0/attention/self/query/kernel",
+              "bert/encoder/layer_11/attention/self/value/bias",
+              "bert/encoder/layer_5/intermediate/dense/kernel",
+              "bert/encoder/layer_5/output/LayerNorm/beta",
+              "cls/predictions/transform/dense/kernel", "cls/predictions/output_bias"):
+        assert n in names, n
+    assert not any("qkv" in n for n in names)
+    total = sum(t.numel() for _, t, _ in collect_variables(m))
+    assert total == num_params(m)
+
+
+def test_bert_param_count_exact():
+    cfg = BertConfig()
+    H, I, V, L = 768, 3072, 30522, 12
+    per_layer = 4 * (H * H + H) + 2 * 2 * H + (H * I + I) + (I * H + H)
+    emb = (V + 512 + 2) * H + 2 * H
+    head = H * H + H + 2 * H + V
+    assert num_params(BertForPreTraining(cfg)) == emb + L * per_layer + head
+
+
+def test_bert_tiny_trains_with_lamb_cpu():
+    torch.manual_seed(0)
+    m = BertForPreTraining(BertConfig(**TINY, hidden_dropout_prob=0.0,
+                                      attention_probs_dropout_prob=0.0))
+    batch = _batch()
+    with OneDeviceStrategy("cpu").scope():
+        opt = LAMBOptimizer(5e-3)
+        first = None
+        for _ in range(15):
+            loss = m(*batch)
+            opt.minimize(loss)
+            first = first if first is not None else loss.item()
+    assert loss.item() < first - 0.3
+
+
+def test_qkv_split_checkpoint_roundtrip(tmp_path):
+    from distributedtensorflow_amd.train import Saver, list_variables, load_variable
+    torch.manual_seed(0)
+    m = BertForPreTraining(BertConfig(**TINY))
+    with OneDeviceStrategy("cpu").scope():
+        opt = LAMBOptimizer(1e-3)
+        opt.minimize(m(*_batch()))
+    p = Saver(model=m, optimizer=opt).save(None, str(tmp_path / "bert.ckpt"))
+    names = dict(list_variables(p))
+    assert names["bert/encoder/layer_1/attention/self/key/kernel"] == [256, 256]
+    assert "bert/encoder/layer_1/attention/self/key/kernel/adam_m" in names
+    qk = m.layers[1].qkv_kernel.detach()
+    torch.testing.assert_close(
+        torch.from_numpy(load_variable(p, "bert/encoder/layer_1/attention/self/key/kernel")),
+        qk[256:512].t())
+    m2 = BertForPreTraining(BertConfig(**TINY))
+    Saver(model=m2).restore(None, p)
+    torch.testing.assert_close(m2.layers[1].qkv_kernel, m.layers[1].qkv_kernel)
+
+
+def test_keep_mask_rate_and_determinism():
+    idx = torch.arange(200_000)
+    k = R.keep_mask(1234, idx, 0.1)
+    assert abs(k.float().mean().item() - 0.9) < 0.005
+    assert torch.equal(k, R.keep_mask(1234, idx, 0.1))
+    assert not torch.equal(k, R.keep_mask(1235, idx, 0.1))
+
+
+def test_reference_attention_matches_naive():
+    torch.manual_seed(0)
+    B, S, H, D = 2, 16, 3, 64
+    qkv = torch.randn(B * S, 3 * H * D)
+    mask = torch.zeros(B, S)
+    mask[0, 10:] = -10000.0
+    out = R.attention_qkv(qkv, mask, B, S, H)
+    x = qkv.view(B, S, 3, H, D)
+    for b in range(B):
+        for h in range(H):
+            q, k, v = x[b, :, 0, h], x[b, :, 1, h], x[b, :, 2, h]
+            p = torch.softmax(q @ k.t() / 8.0 + mask[b], -1)
+            torch.testing.assert_close(out.view(B, S, H, D)[b, :, h], p @ v, atol=1e-5, rtol=1e-5)
+
+
+# ----------------------------------------------------------------------------- GPU kernels
+def _leaf(t, dtype=torch.bfloat16):
+    return t.to("cuda", dtype).detach().requires_grad_(True)
+
+
+def _grads_of(fn, inputs, dy):
+    for t in inputs:
+        if t is not None:
+            t.grad = None
+    y = fn()
+    y.backward(dy)
+    return y.detach().float(), [None if t is None else t.grad.detach().float() for t in inputs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("H", [768, 1024])
+def test_fused_layer_norm_gpu(p, H):
+    torch.manual_seed(0)
+    M = 300
+    a32, r32 = torch.randn(M, H), torch.randn(M, H)
+    bias = torch.randn(H) * 0.1
+    gamma, beta = 1 + 0.1 * torch.randn(H), 0.1 * torch.randn(H)
+    dy = torch.randn(M, H)
+    # native
+    a, r = _leaf(a32), _leaf(r32)
+    b, g, be = (_leaf(t, torch.float32) for t in (bias, gamma, beta))
+    torch.manual_seed(7)
+    y, (da, dr, db, dg, dbe) = _grads_of(
+        lambda: ops.bias_dropout_add_layer_norm(a, b, r, g, be, p, True),
+        [a, r, b, g, be], dy.cuda().bfloat16())
+    # fp32 reference on the same bf16-rounded inputs and the same dropout seed
+    a_, r_ = (t.bfloat16().float().requires_grad_(True) for t in (a32, r32))
+    b_, g_, be_ = (t.clone().requires_grad_(True) for t in (bias, gamma, beta))
+    torch.manual_seed(7)
+    y_, (da_, dr_, db_, dg_, dbe_) = _grads_of(
+        lambda: R.bias_dropout_add_layer_norm(a_, b_, r_, g_, be_, p, True),
+        [a_, r_, b_, g_, be_], dy.bfloat16().float())
+    torch.testing.assert_close(y.cpu(), y_, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(da.cpu(), da_, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(dr.cpu(), dr_, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(db.cpu(), db_, atol=0.3, rtol=2e-2)
+    torch.testing.assert_close(dg.cpu(), dg_, atol=0.3, rtol=2e-2)
+    torch.testing.assert_close(dbe.cpu(), dbe_, atol=0.3, rtol=2e-2)
+
+
+@pytest.mark.gpu
+def test_embedding_layer_norm_gpu():
+    torch.manual_seed(0)
+    V, P, T, H, B, S = 500, 128, 2, 768, 3, 128
+    word, pos, typ = torch.randn(V, H) * 0.02, torch.randn(P, H) * 0.02, torch.randn(T, H) * 0.02
+    gamma, beta = 1 + 0.1 * torch.randn(H), 0.1 * torch.randn(H)
+    ids = torch.randint(0, 50, (B, S))          # many repeats -> exercises the segment sum
+    tt = torch.randint(0, 2, (B, S))
+    dy = torch.randn(B * S, H)
+    leaves = [_leaf(t, torch.float32) for t in (word, pos, typ, gamma, beta)]
+    torch.manual_seed(3)
+    y, gr = _grads_of(lambda: ops.embedding_layer_norm(ids.cuda(), tt.cuda(), *leaves, p=0.1),
+                      leaves, dy.cuda().bfloat16())
+    leaves_ = [t.clone().requires_grad_(True) for t in (word, pos, typ, gamma, beta)]
+    torch.manual_seed(3)
+    y_, gr_ = _grads_of(lambda: R.embedding_layer_norm(ids, tt, *leaves_, p=0.1,
+                                                       dtype=torch.bfloat16).float(),
+                        leaves_, dy.bfloat16().float())
+    torch.testing.assert_close(y.cpu(), y_, atol=3e-2, rtol=2e-2)
+    # d(LN input) is stored in bf16 (|ds| ~ 30 here: rstd of 0.02-scale tables) and then summed
+    # over up to ~10 rows per id, so allow bf16-of-the-summands absolute error
+    for a, b in zip(gr, gr_):
+        torch.testing.assert_close(a.cpu(), b, atol=0.02 * b.abs().max().item(), rtol=3e-2)
+
+
+@pytest.mark.gpu
+def test_bias_gelu_gpu():
+    torch.manual_seed(0)
+    M, N = 257, 3072
+    a32, bias, dy = torch.randn(M, N) * 2, torch.randn(N), torch.randn(M, N)
+    a, b = _leaf(a32), _leaf(bias, torch.float32)
+    y, (da, db) = _grads_of(lambda: ops.bias_gelu(a, b), [a, b], dy.cuda().bfloat16())
+    a_, b_ = a32.bfloat16().float().requires_grad_(True), bias.clone().requires_grad_(True)
+    y_, (da_, db_) = _grads_of(lambda: R.bias_gelu(a_, b_), [a_, b_], dy.bfloat16().float())
+    torch.testing.assert_close(y.cpu(), y_, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(da.cpu(), da_, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(db.cpu(), db_, atol=0.2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,S,H,p,masked", [(2, 128, 2, 0.0, True), (2, 128, 3, 0.1, True),
+                                            (1, 512, 2, 0.0, False), (1, 64, 1, 0.1, False)])
+def test_attention_gpu(B, S, H, p, masked):
+    torch.manual_seed(0)
+    D = 64
+    qkv32 = torch.randn(B * S, 3 * H * D)
+    mask = torch.zeros(B, S)
+    if masked:
+        mask[0, S - 37:] = -10000.0
+    dy = torch.randn(B * S, H * D)
+    x = _leaf(qkv32)
+    torch.manual_seed(11)
+    y, (dx,) = _grads_of(lambda: ops.attention_qkv(x, mask.cuda() if masked else None, B, S, H,
+                                                   p, True), [x], dy.cuda().bfloat16())
+    x_ = qkv32.bfloat16().float().requires_grad_(True)
+    torch.manual_seed(11)
+    y_, (dx_,) = _grads_of(lambda: R.attention_qkv(x_, mask if masked else None, B, S, H, p,
+                                                   True), [x_], dy.bfloat16().float())
+    torch.testing.assert_close(y.cpu(), y_, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(dx.cpu(), dx_, atol=5e-2, rtol=5e-2)
+
+
+@pytest.mark.gpu
+def test_mlm_loss_gpu():
+    torch.manual_seed(0)
+    N, V = 80, 30522
+    lg32 = torch.randn(N, V) * 3
+    lab = torch.randint(0, V, (N,))
+    w = (torch.rand(N) > 0.2).float()
+    lg = _leaf(lg32)
+    loss, (dl,) = _grads_of(lambda: ops.mlm_loss(lg, lab.cuda(), w.cuda()), [lg], None)
+    lg_ = lg32.bfloat16().float().requires_grad_(True)
+    loss_, (dl_,) = _grads_of(lambda: R.mlm_loss(lg_, lab, w), [lg_], None)
+    torch.testing.assert_close(loss.cpu(), loss_, atol=1e-3, rtol=1e-4)
+    torch.testing.assert_close(dl.cpu(), dl_, atol=1e-4, rtol=2e-2)
+
+
+@pytest.mark.gpu
+def test_bert_tiny_gpu_matches_cpu_and_trains():
+    torch.manual_seed(0)
+    cfg = BertConfig(**TINY, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    m_cpu = BertForPreTraining(cfg)
+    m_gpu = BertForPreTraining(cfg)
+    m_gpu.load_state_dict(m_cpu.state_dict())
+    m_gpu.cuda()
+    batch = _batch()
+    ref = m_cpu(*batch).item()
+    with OneDeviceStrategy("cuda").scope():
+        loss = m_gpu(*[t.cuda() for t in batch])
+        assert abs(loss.item() - ref) < 0.05 * abs(ref)
+        opt = LAMBOptimizer(5e-3)
+        first = loss.item()
+        for _ in range(15):
+            loss = m_gpu(*[t.cuda() for t in _batch()])
+            opt.minimize(loss)
+    assert loss.item() < first - 0.3

@@ -23,7 +23,7 @@ def _params(device, seed=0):
     names = ["dense/kernel", "dense/bias", "conv2d/kernel", "bn/gamma"]
     ps = []
     for s, n in zip(shapes, names):
-        p = torch.nn.Parameter(torch.randn(s, generator=g).to(device))
+        p = torch.nn.Parameter(torch.randn(s, generator=g, device="cpu").to(device))
         p._dtf_name = n
         ps.append(p)
     return ps
@@ -31,7 +31,7 @@ def _params(device, seed=0):
 
 def _grads(ps, step):
     g = torch.Generator().manual_seed(100 + step)
-    return [torch.randn(p.shape, generator=g) for p in ps]
+    return [torch.randn(p.shape, generator=g, device="cpu") for p in ps]
 
 
 def _run(opt, device, steps=4):
