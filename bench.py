@@ -68,7 +68,11 @@ def build_dtf(args, dev):
     with strategy.scope():
         model = resnet50()
         model.train()
-        opt = MomentumOptimizer(args.lr, momentum=0.9, weight_decay=1e-4)
+        # Goyal et al. recipe: lr 0.1 x (global batch / 256) after a linear warm-up
+        from distributedtensorflow_amd.optimizers.optimizers import cosine_decay
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        lr = cosine_decay(args.lr * args.batch * world / 256, 90 * 5000, warmup_steps=500)
+        opt = MomentumOptimizer(lr, momentum=0.9, weight_decay=1e-4)
         gstep = get_or_create_global_step()
         opt.build(list(model.parameters()))
 
@@ -165,7 +169,7 @@ def main():
         step, _ = build_torch(args, dev)
         images = torch.randn(B, 3, S, S, device=dev, generator=g).contiguous(
             memory_format=torch.channels_last)
-    if labels is not None or args.model != "bert_base":
+    if args.model != "bert_base":
         labels = torch.randint(0, 1000, (B,), device=dev, generator=g)
 
     def sync():
@@ -219,7 +223,7 @@ def main():
                                       "random-init weights)",
             "config": {"model": "resnet50", "global_batch": B * world, "per_gpu_batch": B,
                        "seq_len": None, "image_size": S, "parallelism": f"dp{world}",
-                       "impl": args.impl, "optimizer": "momentum0.9+wd1e-4",
+                       "impl": args.impl, "optimizer": "momentum0.9+wd1e-4, lr 0.1*B/256 warmup500+cosine",
                        "final_loss": round(final_loss, 4)},
         }
         print(json.dumps(rec), flush=True)

@@ -93,27 +93,54 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
   }
 }
 
-// Combine the per-block partial slabs: one block = 32 channels x 8 partial slots; each slot sums
-// every 8th partial row (coalesced 128-B reads) in fp64, slots are combined in a fixed order
-// (deterministic).  Returns true in the slot-0 lane that owns channel c.
-DTF_DEV bool combine_partials(const float* __restrict__ partial, int G, int C, double* a,
-                              double* b, int* c_out) {
+// Two-level fixed-order combine of the G per-block partial slabs (G ~ 1024).  A single
+// 32-channel-per-block pass left small-C layers with 2-8 latency-bound blocks (38 us per BN
+// call in the r1_v0 profile); stage 1 splits the G rows into S slices over a 2-D grid of
+// (C/32) x S blocks, stage 2 (inside the finalize kernels, one thread per channel) adds the S
+// fp64 slice sums in order.  Deterministic and placement-independent (kernel boundary = the
+// release/acquire between the stages).
+inline int combine_slices(int G, int C) {
+  const int groups = (C + 31) / 32;
+  int S = 512 / groups;
+  if (S > 64) S = 64;
+  if (S > G / 8) S = G / 8;
+  return S < 1 ? 1 : S;
+}
+
+__global__ void __launch_bounds__(256)
+bn_combine_kernel(const float* __restrict__ partial, int G, int C, int S,
+                  double* __restrict__ level2) {
   __shared__ double red[2][8][32];
   const int cl = threadIdx.x & 31, slot = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
+  const int j = blockIdx.y;
+  const int g0 = (int)((long)j * G / S), g1 = (int)((long)(j + 1) * G / S);
   double s = 0.0, ss = 0.0;
   if (c < C)
-    for (int g = slot; g < G; g += 8) {
+    for (int g = g0 + slot; g < g1; g += 8) {
       s += partial[((long)g * 2 + 0) * C + c];
       ss += partial[((long)g * 2 + 1) * C + c];
     }
   red[0][slot][cl] = s;
   red[1][slot][cl] = ss;
   __syncthreads();
-  if (slot != 0 || c >= C) return false;
+  if (slot != 0 || c >= C) return;
   s = 0.0;
   ss = 0.0;
   for (int k = 0; k < 8; ++k) { s += red[0][k][cl]; ss += red[1][k][cl]; }
+  level2[((long)j * 2 + 0) * C + c] = s;
+  level2[((long)j * 2 + 1) * C + c] = ss;
+}
+
+DTF_DEV bool combine_partials(const double* __restrict__ level2, int S, int C, double* a,
+                              double* b, int* c_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return false;
+  double s = 0.0, ss = 0.0;
+  for (int j = 0; j < S; ++j) {
+    s += level2[((long)j * 2 + 0) * C + c];
+    ss += level2[((long)j * 2 + 1) * C + c];
+  }
   *a = s;
   *b = ss;
   *c_out = c;
@@ -121,14 +148,14 @@ DTF_DEV bool combine_partials(const float* __restrict__ partial, int G, int C, d
 }
 
 __global__ void __launch_bounds__(256)
-bn_fwd_finalize_kernel(const float* __restrict__ partial, int G, int C, long M,
+bn_fwd_finalize_kernel(const double* __restrict__ level2, int S, int C, long M,
                        const float* __restrict__ gamma, const float* __restrict__ beta,
                        float* __restrict__ run_mean, float* __restrict__ run_var, float momentum,
                        float eps, float* __restrict__ mean, float* __restrict__ invstd,
                        float* __restrict__ scale, float* __restrict__ shift) {
   double s, ss;
   int c;
-  if (!combine_partials(partial, G, C, &s, &ss, &c)) return;
+  if (!combine_partials(level2, S, C, &s, &ss, &c)) return;
   const double mu = s / (double)M;
   double var = ss / (double)M - mu * mu;
   if (var < 0) var = 0;
@@ -194,14 +221,14 @@ bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
 }
 
 __global__ void __launch_bounds__(256)
-bn_bwd_finalize_kernel(const float* __restrict__ partial, int G, int C, long M,
+bn_bwd_finalize_kernel(const double* __restrict__ level2, int S, int C, long M,
                        const float* __restrict__ gamma, const float* __restrict__ mean,
                        const float* __restrict__ invstd, float* __restrict__ dgamma,
                        float* __restrict__ dbeta, float* __restrict__ coefA,
                        float* __restrict__ coefB, float* __restrict__ coefC, int accumulate) {
   double sdz, sdzx;
   int c;
-  if (!combine_partials(partial, G, C, &sdz, &sdzx, &c)) return;
+  if (!combine_partials(level2, S, C, &sdz, &sdzx, &c)) return;
   const float db = (float)sdz, dg = (float)sdzx;
   if (accumulate) { dgamma[c] += dg; dbeta[c] += db; }
   else { dgamma[c] = dg; dbeta[c] = db; }
@@ -274,9 +301,20 @@ void dtf_bn_fwd_finalize(const float* partial, long M, int C, const float* gamma
                          hipStream_t st) {
   int rpb;
   const int G = stats_grid(M, C, &rpb);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, partial, G,
+  const int S = combine_slices(G, C);
+  double* level2 = reinterpret_cast<double*>(const_cast<float*>(partial) + (long)G * 2 * C);
+  hipLaunchKernelGGL(bn_combine_kernel, dim3((C + 31) / 32, S), dim3(256), 0, st, partial, G, C,
+                     S, level2);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, level2, S,
                      C, M, gamma, beta, run_mean, run_var, momentum, eps, mean, invstd, scale,
                      shift);
+}
+
+// floats of workspace a stats/reduce + finalize pair needs: G partial slabs + S fp64 slices
+long dtf_bn_workspace_floats(long M, int C) {
+  int rpb;
+  const int G = stats_grid(M, C, &rpb);
+  return (long)G * 2 * C + 2L * combine_slices(G, C) * 2 * C;
 }
 
 void dtf_bn_infer_finalize(int C, const float* gamma, const float* beta, const float* run_mean,
@@ -310,8 +348,12 @@ void dtf_bn_bwd_finalize(const float* partial, long M, int C, const float* gamma
                          hipStream_t st) {
   int rpb;
   const int G = stats_grid(M, C, &rpb);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, partial, G, C,
-                     M, gamma, mean, invstd, dgamma, dbeta, coefA, coefB, coefC, accumulate);
+  const int S = combine_slices(G, C);
+  double* level2 = reinterpret_cast<double*>(const_cast<float*>(partial) + (long)G * 2 * C);
+  hipLaunchKernelGGL(bn_combine_kernel, dim3((C + 31) / 32, S), dim3(256), 0, st, partial, G, C,
+                     S, level2);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, level2, S,
+                     C, M, gamma, mean, invstd, dgamma, dbeta, coefA, coefB, coefC, accumulate);
 }
 
 void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* cA,

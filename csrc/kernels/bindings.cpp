@@ -23,6 +23,7 @@ struct WgradGeom { int N, H, W, C, P, Q, sh, sw, Kout, ldw; long m_per_split; lo
 
 // ---- launchers defined in the .hip translation units
 int dtf_bn_partial_blocks(long M, int C);
+long dtf_bn_workspace_floats(long M, int C);
 void dtf_bn_fwd_stats(const bf16_t*, long, int, float*, hipStream_t);
 void dtf_bn_fwd_finalize(const float*, long, int, const float*, const float*, float*, float*,
                          float, float, float*, float*, float*, float*, hipStream_t);
@@ -58,7 +59,8 @@ void dtf_cast_f32_bf16(const float*, bf16_t*, long, hipStream_t);
 void dtf_conv_igemm(const bf16_t*, const bf16_t*, bf16_t*, const ConvGeom&, const TapTable&, int,
                     hipStream_t);
 void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, const TapTableW&,
-                    int, int, hipStream_t);
+                    int, int, int, hipStream_t);
+
 int dtf_conv_wgrad_splits(long, int, int, long);
 void dtf_lds_probe(int, int, int*, int, hipStream_t);
 int dtf_max_dynamic_lds(int);
@@ -107,6 +109,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.doc() = "distributedtensorflow_amd HIP/CDNA4 kernels (gfx950)";
 
   m.def("bn_partial_blocks", &dtf_bn_partial_blocks);
+  m.def("bn_workspace_floats", &dtf_bn_workspace_floats);
   m.def("bn_fwd_stats", [](uintptr_t x, long M, int C, uintptr_t part, uintptr_t st) {
     dtf_bn_fwd_stats(P<const bf16_t>(x), M, C, P<float>(part), S(st));
     check_launch("bn_fwd_stats");
@@ -234,15 +237,16 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("conv_wgrad", [](uintptr_t x, uintptr_t dy, uintptr_t dw_out, uintptr_t ws,
                          std::vector<int> geom, std::vector<int> dh, std::vector<int> dw,
-                         int splits, uintptr_t st, int tr_mode) {
+                         int splits, uintptr_t st, int tr_mode, int accumulate) {
     if (geom.size() != 10) throw std::runtime_error("conv_wgrad: geom needs 10 ints");
     WgradGeom g{geom[0], geom[1], geom[2], geom[3], geom[4], geom[5], geom[6], geom[7], geom[8],
                 geom[9], 0, 0};
     dtf_conv_wgrad(P<const bf16_t>(x), P<const bf16_t>(dy), P<float>(dw_out), P<float>(ws), g,
-                   make_taps<TapTableW>(dh, dw), splits, tr_mode, S(st));
+                   make_taps<TapTableW>(dh, dw), splits, tr_mode, accumulate, S(st));
     check_launch("conv_wgrad");
   }, py::arg("x"), py::arg("dy"), py::arg("dw_out"), py::arg("ws"), py::arg("geom"),
-     py::arg("dh"), py::arg("dw"), py::arg("splits"), py::arg("stream"), py::arg("tr_mode") = 1);
+     py::arg("dh"), py::arg("dw"), py::arg("splits"), py::arg("stream"), py::arg("tr_mode") = 1,
+     py::arg("accumulate") = 0);
   m.def("conv_wgrad_splits", &dtf_conv_wgrad_splits);
   m.def("lds_probe", [](int bytes, int blocks, uintptr_t errors, int spin, uintptr_t st) {
     dtf_lds_probe(bytes, blocks, P<int>(errors), spin, S(st));

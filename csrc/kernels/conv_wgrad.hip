@@ -244,7 +244,7 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
 // q, q+4, ... in order, the 4 group partials are added in a fixed order through LDS.
 __global__ void __launch_bounds__(256)
 slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n, long slab,
-                   int nsplit) {
+                   int nsplit, int accumulate) {
   __shared__ float4 red[4][64];
   const int col = threadIdx.x & 63, q = threadIdx.x >> 6;
   const long n4 = n >> 2;
@@ -261,6 +261,10 @@ slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n
     float4 t = red[0][col];
     for (int k = 1; k < 4; ++k) {
       t.x += red[k][col].x; t.y += red[k][col].y; t.z += red[k][col].z; t.w += red[k][col].w;
+    }
+    if (accumulate) {   // gradient written straight into the optimizer's flat fp32 grad buffer
+      const float4 o = reinterpret_cast<const float4*>(out)[i];
+      t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
     }
     reinterpret_cast<float4*>(out)[i] = t;
   }
@@ -283,13 +287,16 @@ int dtf_conv_wgrad_splits(long M, int Kout, int TC, long ws_cap) {
   return (int)((M + mps - 1) / mps);
 }
 
-// splits == 1: dW written directly.  splits > 1: `ws` holds splits x Kout x ldw floats; the
-// slabs are summed (in split order) into dW by a second launch.
+// splits == 1 (and not accumulating): dW written directly.  Otherwise `ws` holds splits x Kout x
+// ldw floats; the slabs are summed (in split order) into dW by a second launch, which adds the
+// existing dW last when `accumulate` (direct writes into the flat gradient buffer).
 void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, WgradGeom g,
-                    const TapTableW& taps, int splits, int tr_mode, hipStream_t st) {
+                    const TapTableW& taps, int splits, int tr_mode, int accumulate,
+                    hipStream_t st) {
   if (taps.n <= 0 || taps.n > DTF_MAX_TAPS) throw std::runtime_error("wgrad: bad tap count");
   if (g.Kout % 8) throw std::runtime_error("wgrad: Kout % 8 != 0");
-  if (splits < 1 || (splits > 1 && !ws)) throw std::runtime_error("wgrad: bad split workspace");
+  const bool via_ws = splits > 1 || accumulate;
+  if (splits < 1 || (via_ws && !ws)) throw std::runtime_error("wgrad: bad split workspace");
   if (2.0 * g.N * g.H * g.W * g.C >= 2147483647.0 || 2.0 * g.N * g.P * g.Q * g.Kout >= 2147483647.0)
     throw std::runtime_error("wgrad: tensor too large for 32-bit buffer offsets");
   const long M = (long)g.N * g.P * g.Q;
@@ -300,7 +307,7 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   g.slab = (long)g.Kout * g.ldw;
   const int nsplit = (int)((M + mps - 1) / mps);
   if (nsplit != splits) throw std::runtime_error("wgrad: split plan mismatch");
-  float* target = splits > 1 ? ws : dW;
+  float* target = via_ws ? ws : dW;
   const long tiles = (long)((g.Kout + BM - 1) / BM) * ((TC + BN - 1) / BN);
   const size_t lds = (size_t)2 * (OPER_A + OPER_B) * sizeof(bf16_t) + 2 * DTF_MAX_TAPS * sizeof(int);
   const bool generic = (g.C % 8) != 0;
@@ -313,10 +320,10 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   } else {
     hipLaunchKernelGGL((conv_wgrad_kernel<false, true>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
   }
-  if (splits > 1) {
+  if (via_ws) {
     // slab = Kout * ldw floats, Kout % 8 == 0 -> slab % 4 == 0 (float4 path covers it)
     const long n4 = g.slab / 4;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, ws,
-                       dW, g.slab, g.slab, nsplit);
+                       dW, g.slab, g.slab, nsplit, accumulate);
   }
 }

@@ -48,6 +48,31 @@ def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
     return w.detach().to(_BF16)
 
 
+_DIRECT_GRAD = os.environ.get("DTF_DIRECT_GRAD", "1") == "1"
+
+
+def _direct_grad(p):
+    """The fp32 flat-buffer gradient view of parameter ``p`` when our kernels may accumulate into
+    it directly (saving autograd's separate ``grad += g`` launch per parameter), else None.
+
+    After writing, the op calls :func:`_grad_ready` so gradient-bucketing strategies see the
+    same "this parameter's gradient is complete" event AccumulateGrad would have raised.  Valid
+    for parameters consumed once per step (convs / BN in ResNet); set DTF_DIRECT_GRAD=0 to route
+    everything through autograd (e.g. for weights shared across several calls)."""
+    if not _DIRECT_GRAD or p is None or not getattr(p, "_dtf_flat", False):
+        return None
+    g = p.grad
+    if g is None or g.dtype != torch.float32 or not g.is_contiguous():
+        return None
+    return g
+
+
+def _grad_ready(p):
+    cb = getattr(p, "_dtf_grad_ready", None)
+    if cb is not None:
+        cb()
+
+
 def _check_cuda_bf16(*ts):
     for t in ts:
         if t is not None and (not t.is_cuda or t.dtype != _BF16):
@@ -135,8 +160,9 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding):
 _WGRAD_WS_CAP = 32 << 20   # floats of split-K slab workspace per call (128 MB)
 
 
-def conv2d_wgrad(x, dy, w_shape, stride, padding):
-    """dW [K,R,S,C] fp32 via the MFMA wgrad kernel; deterministic split-K slab reduction."""
+def conv2d_wgrad(x, dy, w_shape, stride, padding, out=None):
+    """dW [K,R,S,C] fp32 via the MFMA wgrad kernel; deterministic split-K slab reduction.
+    With ``out`` (a contiguous fp32 [K,R,S,C] buffer) the result is ADDED into it."""
     K, R, S, C = w_shape
     n, h, wd, c = x.shape
     sh, sw = _pair(stride)
@@ -145,12 +171,13 @@ def conv2d_wgrad(x, dy, w_shape, stride, padding):
     taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
     tc = R * S * C
     splits = _K.conv_wgrad_splits(n * P * Q, K, tc, _WGRAD_WS_CAP)
-    dW = torch.empty(K, tc, device=x.device, dtype=torch.float32)
+    acc = out is not None
+    dW = out if acc else torch.empty(K, tc, device=x.device, dtype=torch.float32)
     ws = (torch.empty(splits * K * tc, device=x.device, dtype=torch.float32)
-          if splits > 1 else None)
+          if splits > 1 or acc else None)
     geom = [n, h, wd, c, P, Q, sh, sw, K, tc]
     _K.conv_wgrad(x.data_ptr(), dy.contiguous().data_ptr(), dW.data_ptr(), _p(ws), geom,
-                  [t[0] for t in taps], [t[1] for t in taps], splits, _st())
+                  [t[0] for t in taps], [t[1] for t in taps], splits, _st(), 1, int(acc))
     return dW.reshape(K, R, S, C)
 
 
@@ -162,19 +189,27 @@ class _Conv2d(torch.autograd.Function):
         ctx.save_for_backward(xb, wb)
         ctx.stride, ctx.padding = stride, padding
         ctx.w_dtype = w_master.dtype
+        ctx.w_param = w_master
         return conv2d_forward(xb, wb, stride, padding)
 
     @staticmethod
     def backward(ctx, dy):
         xb, wb = ctx.saved_tensors
         dx = dw = None
+        if ctx.needs_input_grad[1]:
+            # weight gradient first: it only depends on dy, so the bucketed all-reduce of this
+            # layer can start while dgrad still runs
+            target = _direct_grad(ctx.w_param)
+            if target is not None:
+                conv2d_wgrad(xb, dy, wb.shape, ctx.stride, ctx.padding, out=target)
+                _grad_ready(ctx.w_param)
+            else:
+                dw = conv2d_wgrad(xb, dy, wb.shape, ctx.stride, ctx.padding).to(ctx.w_dtype)
         if ctx.needs_input_grad[0]:
             if xb.shape[-1] % 8:
                 raise NotImplementedError("native conv2d dgrad needs C % 8 == 0 (input-layer "
                                           "convs never need it)")
             dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding)
-        if ctx.needs_input_grad[1]:
-            dw = conv2d_wgrad(xb, dy, wb.shape, ctx.stride, ctx.padding).to(ctx.w_dtype)
         return dx, dw, None, None
 
 
@@ -201,8 +236,7 @@ class _BatchNorm(torch.autograd.Function):
         st = _st()
         g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
         if training:
-            G = _K.bn_partial_blocks(M, C)
-            part = torch.empty(G, 2, C, device=dev, dtype=torch.float32)
+            part = torch.empty(_K.bn_workspace_floats(M, C), device=dev, dtype=torch.float32)
             _K.bn_fwd_stats(x.data_ptr(), M, C, part.data_ptr(), st)
             _K.bn_fwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), b32.data_ptr(),
                                _p(running_mean), _p(running_var), float(momentum), float(eps),
@@ -220,6 +254,7 @@ class _BatchNorm(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.gdt, ctx.bdt = gamma.dtype, beta.dtype
+        ctx.params = (gamma, beta)
         return y
 
     @staticmethod
@@ -231,19 +266,27 @@ class _BatchNorm(torch.autograd.Function):
         dev = x.device
         st = _st()
         mean, invstd = stats[0], stats[1]
-        G = _K.bn_partial_blocks(M, C)
-        part = torch.empty(G, 2, C, device=dev, dtype=torch.float32)
+        part = torch.empty(_K.bn_workspace_floats(M, C), device=dev, dtype=torch.float32)
         _K.bn_bwd_reduce(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr(),
                          invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st)
         gb = torch.empty(5, C, device=dev, dtype=torch.float32)  # dgamma dbeta A B C
+        tg, tb = (_direct_grad(p) for p in ctx.params)
+        direct = tg is not None and tb is not None
+        dg_ptr, db_ptr = ((tg.data_ptr(), tb.data_ptr()) if direct
+                          else (gb[0].data_ptr(), gb[1].data_ptr()))
         _K.bn_bwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), mean.data_ptr(),
-                           invstd.data_ptr(), gb[0].data_ptr(), gb[1].data_ptr(),
-                           gb[2].data_ptr(), gb[3].data_ptr(), gb[4].data_ptr(), 0, st)
+                           invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(), gb[3].data_ptr(),
+                           gb[4].data_ptr(), int(direct), st)
+        if direct:
+            for p in ctx.params:
+                _grad_ready(p)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
         _K.bn_bwd_apply(dy.data_ptr(), y.data_ptr(), x.data_ptr(), gb[2].data_ptr(),
                         gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
                         int(ctx.relu), st)
+        if direct:
+            return dx, None, None, None, None, None, None, None, None, dres
         return (dx, gb[0].to(ctx.gdt), gb[1].to(ctx.bdt), None, None, None, None, None, None,
                 dres)
 

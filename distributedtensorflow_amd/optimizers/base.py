@@ -62,6 +62,8 @@ class FlatSpace:
                 self.master[o:o + n].copy_(v.detach().reshape(-1).float())
                 v.data = self.master[o:o + n].view(v.shape)
                 v.grad = self.grad[o:o + n].view(v.shape)
+                v._dtf_flat = True           # kernels may accumulate into v.grad directly
+                v._dtf_grad_ready = None     # set by gradient-bucketing reducers
                 if self.shadow is not None:
                     s = self.shadow[o:o + n].view(v.shape)
                     s.copy_(v.data)

@@ -115,7 +115,11 @@ class BucketedAllReduce:
         self.launched = [False] * len(ranges)
         self._hooks = []
         for i, v in enumerate(order):
-            self._hooks.append(v.register_post_accumulate_grad_hook(self._make_hook(i)))
+            hook = self._make_hook(i)
+            self._hooks.append(v.register_post_accumulate_grad_hook(hook))
+            # ops that write their gradient straight into the flat buffer (ops/native.py
+            # _direct_grad) raise the same readiness event themselves
+            v._dtf_grad_ready = (lambda h=hook, p=v: h(p))
 
     def _make_hook(self, i):
         def hook(_p):

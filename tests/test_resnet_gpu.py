@@ -1,0 +1,99 @@
+"""ResNet-50 end to end on the GPU: the native op graph against the PyTorch reference graph on
+the same weights, and the direct-to-flat-buffer gradient path against plain autograd
+accumulation (must be bit-identical)."""
+import copy
+
+import pytest
+import torch
+
+from distributedtensorflow_amd import ops
+from distributedtensorflow_amd.models import resnet50
+from distributedtensorflow_amd.ops import native
+from distributedtensorflow_amd.optimizers import MomentumOptimizer
+from distributedtensorflow_amd.parallel import OneDeviceStrategy
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(n=4, s=64):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(n, s, s, 3, generator=g, device="cpu")
+    y = torch.randint(0, 1000, (n,), generator=g, device="cpu")
+    return x.cuda().bfloat16(), y.cuda()
+
+
+def _grads(model, direct):
+    prev = native._DIRECT_GRAD
+    native._DIRECT_GRAD = direct
+    try:
+        with OneDeviceStrategy("cuda").scope():
+            opt = MomentumOptimizer(0.1, 0.9)
+            x, y = _inputs()
+            loss = ops.sparse_softmax_cross_entropy(model(x), y)
+            opt.compute_gradients(loss, list(model.parameters()))
+            torch.cuda.synchronize()
+            return loss.item(), opt.space.grad.clone()
+    finally:
+        native._DIRECT_GRAD = prev
+
+
+def test_direct_grad_path_bit_identical():
+    torch.manual_seed(0)
+    base = resnet50().cuda()
+    a = copy.deepcopy(base)
+    b = copy.deepcopy(base)
+    la, ga = _grads(a, True)
+    lb, gb = _grads(b, False)
+    assert la == lb
+    assert torch.equal(ga, gb)
+    assert ga.abs().sum() > 0
+
+
+def test_resnet50_eval_native_matches_reference_graph():
+    """Whole-network inference forward, native bf16 kernels vs the fp32 PyTorch reference."""
+    torch.manual_seed(0)
+    m = resnet50().cuda().eval()
+    x, _ = _inputs()
+    with torch.no_grad():
+        nat = m(x).float()
+        ops.set_backend("reference")
+        try:
+            ref = m(x.float()).float()
+        finally:
+            ops.set_backend("auto")
+    rel = ((nat - ref).norm() / ref.norm()).item()
+    assert rel < 0.05, rel
+
+
+def test_resnet50_train_first_stage_matches_reference():
+    """Training-mode (batch-statistics BN) forward through the stem and stage 1.
+
+    Deeper outputs are not compared: a random-init BN ResNet is chaotic — feeding the fp32
+    reference graph the bf16-ROUNDED input (0.17% change) already moves the final block by 23%
+    (tools/debug_resnet_layers.py), so end-to-end agreement is not a kernel-accuracy test."""
+    torch.manual_seed(0)
+    m = resnet50().cuda().train()
+    x, _ = _inputs(n=16, s=96)
+    outs = {}
+
+    def grab(tag):
+        def hook(mod, i, o):
+            outs.setdefault(tag, []).append(o.detach().float())
+        return hook
+    hs = [b.register_forward_hook(grab(k)) for k, b in
+          [("stem", m.stem)] + [(f"b{i}", m.blocks[i]) for i in range(3)]]
+    rm = [b.clone() for b in m.buffers()]
+    with torch.no_grad():
+        m(x)
+        for b, r in zip(m.buffers(), rm):
+            b.copy_(r)
+        ops.set_backend("reference")
+        try:
+            m(x.float())
+        finally:
+            ops.set_backend("auto")
+    for h in hs:
+        h.remove()
+    for tag, (nat, ref) in outs.items():
+        rel = ((nat - ref).norm() / ref.norm()).item()
+        assert rel < 0.03, (tag, rel)

@@ -17,5 +17,5 @@ prof() {  # name, args...
   rm -rf "/tmp/prof_$name"
   return $rc
 }
-prof dtf --steps 5 --warmup 3 ${DTF_BENCH_ARGS} || exit $?
+prof "${PROF_NAME:-dtf}" --steps 5 --warmup 3 ${DTF_BENCH_ARGS} || exit $?
 [ -n "$SKIP_TORCH" ] || prof torch --impl torch --steps 5 --warmup 3
