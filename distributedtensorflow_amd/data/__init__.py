@@ -2,7 +2,8 @@
 ImageNet / MLM generators for benchmarks."""
 from . import mnist
 from .dataset import Dataset, Iterator, NativeBatchDataset
+from .device import DeviceArrayDataset
 from .synthetic import SyntheticImageNet, SyntheticMLM
 
-__all__ = ["mnist", "Dataset", "Iterator", "NativeBatchDataset", "SyntheticImageNet",
-           "SyntheticMLM"]
+__all__ = ["mnist", "Dataset", "DeviceArrayDataset", "Iterator", "NativeBatchDataset",
+           "SyntheticImageNet", "SyntheticMLM"]
