@@ -35,7 +35,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    p.add_argument("--batch", type=int, default=None,
+                   help="per-GPU batch (default 512 for ResNet-50: 288 GB HBM per MI355X; "
+                        "128 sequences for BERT)")
     p.add_argument("--impl", choices=("dtf", "torch"), default="dtf")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--lr", type=float, default=0.1)
@@ -47,8 +49,8 @@ def parse():
     p.add_argument("--seq-len", type=int, default=128)
     p.add_argument("--max-predictions", type=int, default=20)
     args = p.parse_args()
-    if args.model == "bert_base" and args.batch == 256 and "--batch" not in sys.argv:
-        args.batch = 128
+    if args.batch is None:
+        args.batch = 128 if args.model == "bert_base" else 512
     return args
 
 

@@ -101,8 +101,8 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
 // release/acquire between the stages).
 inline int combine_slices(int G, int C) {
   const int groups = (C + 31) / 32;
-  int S = 512 / groups;
-  if (S > 64) S = 64;
+  int S = 256 / groups;
+  if (S > 16) S = 16;        // stage 2 reads S values per channel serially: keep it short
   if (S > G / 8) S = G / 8;
   return S < 1 ? 1 : S;
 }
@@ -116,11 +116,14 @@ bn_combine_kernel(const float* __restrict__ partial, int G, int C, int S,
   const int j = blockIdx.y;
   const int g0 = (int)((long)j * G / S), g1 = (int)((long)(j + 1) * G / S);
   double s = 0.0, ss = 0.0;
-  if (c < C)
+  if (c < C) {
+    // loads of 8 rows issued back to back before their (fixed-order) adds
+#pragma unroll 8
     for (int g = g0 + slot; g < g1; g += 8) {
       s += partial[((long)g * 2 + 0) * C + c];
       ss += partial[((long)g * 2 + 1) * C + c];
     }
+  }
   red[0][slot][cl] = s;
   red[1][slot][cl] = ss;
   __syncthreads();
@@ -137,6 +140,7 @@ DTF_DEV bool combine_partials(const double* __restrict__ level2, int S, int C, d
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return false;
   double s = 0.0, ss = 0.0;
+#pragma unroll 16
   for (int j = 0; j < S; ++j) {
     s += level2[((long)j * 2 + 0) * C + c];
     ss += level2[((long)j * 2 + 1) * C + c];

@@ -27,7 +27,9 @@
 //   Epilogue: accumulators -> bf16 -> LDS -> 16-B coalesced global stores.
 //   Tile order: XCD-aware bijective remap of the block id, N-tile fastest so blocks sharing an
 //   A panel run on the same XCD's L2 (T1).
-//   GENERIC=true: per-element gather for C % 32 != 0 (stem 7x7x3, MNIST conv 5x5x1).
+//   GATHER (template): 0 = each K-step lies inside one tap (C % BK == 0: every ResNet body conv);
+//   2 = per-16-B-chunk taps from an LDS copy of the table (C % 8 == 0: the stem / MNIST conv1 after
+//   their input channels are zero-padded to 8 by the host); 1 = per-element gather (any C).
 //   The tap table arrives as a kernel argument; it is only ever read with wave-uniform indices
 //   (scalar loads) — per-lane indices go through a copy in LDS.
 #include <stdexcept>
@@ -75,7 +77,7 @@ DTF_DEV uint32_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
 }
 
-template <int WAVES_M, int WAVES_N, int BK, bool GENERIC>
+template <int WAVES_M, int WAVES_N, int BK, int GATHER>
 __global__ void __launch_bounds__(kThreads, 2)
 conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                   bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps) {
@@ -106,7 +108,7 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   const auto rx = rsrc(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
   const auto rw = rsrc(Wt, (uint32_t)g.Kout * g.Kpad * 2u);
 
-  if constexpr (GENERIC) {
+  if constexpr (GATHER != 0) {
     if (tid == 0)
       for (int t = 0; t < taps.n; ++t) { lds_taps[t] = taps.dh[t]; lds_taps[DTF_MAX_TAPS + t] = taps.dw[t]; }
   }
@@ -132,7 +134,7 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
 
   auto load_stage = [&](int kt) {
     const int k0 = kt * BK;
-    if constexpr (!GENERIC) {
+    if constexpr (GATHER == 0) {
       const int t = __builtin_amdgcn_readfirstlane(k0 / g.C);
       const int c0 = k0 - t * g.C + chunk * 8;
       const int dh = taps.dh[t], dw = taps.dw[t];          // uniform index: scalar loads
@@ -142,6 +144,17 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
         const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
         const uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * g.W + w) * g.C + c0) * 2) : kOOB;
         ra[i] = bload16(rx, off);
+      }
+    } else if constexpr (GATHER == 2) {
+      const int k = k0 + chunk * 8;                   // 8 channels of one tap per 16-B chunk
+      const int t = k / g.C, c = k - t * g.C;
+      const int tt = k < K ? t : 0;
+      const int dh = lds_taps[tt], dw = lds_taps[DTF_MAX_TAPS + tt];
+#pragma unroll
+      for (int i = 0; i < A_CHUNKS; ++i) {
+        const int h = a_h[i] + dh, w = a_w[i] + dw;
+        const bool ok = k < K && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+        ra[i] = bload16(rx, ok ? (uint32_t)(((a_pix[i] + h * g.W + w) * g.C + c) * 2) : kOOB);
       }
     } else {
 #pragma unroll
@@ -194,7 +207,7 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (GENERIC) __syncthreads();   // tap table visible before the first gather
+  if constexpr (GATHER != 0) __syncthreads();   // tap table visible before the first gather
   load_stage(0);
   store_stage(0);
   __syncthreads();
@@ -264,7 +277,7 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   }
 }
 
-template <int WM, int WN, int BK, bool GEN>
+template <int WM, int WN, int BK, int GEN>
 void launch_cfg(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
                 const TapTable& taps, hipStream_t st) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -289,19 +302,23 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
   const double m = (double)g.N * g.P * g.Q;
   if (xbytes >= 2147483647.0 || wbytes >= 2147483647.0 || m >= 2147483647.0)
     throw std::runtime_error("conv: tensor too large for 32-bit buffer offsets");
-  const bool generic = (g.C % 32) != 0;
   const bool narrow = g.Kout <= 64;        // 256 x 64 tile for 64-wide layers
-  if (generic) {
+  if (g.C % 32 != 0) {
     if (g.Kpad % 32) throw std::runtime_error("conv: Kpad % 32 != 0");
-    if (narrow) launch_cfg<4, 1, 32, true>(X, Wt, Y, g, taps, st);
-    else launch_cfg<2, 2, 32, true>(X, Wt, Y, g, taps, st);
+    if (g.C % 8 == 0) {                    // chunk gather (stem / MNIST conv1, C padded to 8)
+      if (narrow) launch_cfg<4, 1, 32, 2>(X, Wt, Y, g, taps, st);
+      else launch_cfg<2, 2, 32, 2>(X, Wt, Y, g, taps, st);
+    } else {
+      if (narrow) launch_cfg<4, 1, 32, 1>(X, Wt, Y, g, taps, st);
+      else launch_cfg<2, 2, 32, 1>(X, Wt, Y, g, taps, st);
+    }
     return;
   }
   if (bk == 64 && g.C % 64 == 0) {
-    if (narrow) launch_cfg<4, 1, 64, false>(X, Wt, Y, g, taps, st);
-    else launch_cfg<2, 2, 64, false>(X, Wt, Y, g, taps, st);
+    if (narrow) launch_cfg<4, 1, 64, 0>(X, Wt, Y, g, taps, st);
+    else launch_cfg<2, 2, 64, 0>(X, Wt, Y, g, taps, st);
   } else {
-    if (narrow) launch_cfg<4, 1, 32, false>(X, Wt, Y, g, taps, st);
-    else launch_cfg<2, 2, 32, false>(X, Wt, Y, g, taps, st);
+    if (narrow) launch_cfg<4, 1, 32, 0>(X, Wt, Y, g, taps, st);
+    else launch_cfg<2, 2, 32, 0>(X, Wt, Y, g, taps, st);
   }
 }

@@ -57,15 +57,32 @@ def test_conv_fwd_dgrad_wgrad(case):
     g = torch.randn_like(yr)
     yr.backward(g)
 
-    xn = x.clone().requires_grad_(C % 8 == 0)   # input-layer convs need no data grad
+    xn = x.clone().requires_grad_(True)         # C % 8 != 0: channels zero-padded to 8
     wn = w.clone().requires_grad_(True)
     yn = nat.conv2d(xn, wn, stride, pad)
     assert yn.shape == yr.shape
     assert _rel(yn, yr) < 1e-2, _rel(yn, yr)
     yn.backward(g.to(torch.bfloat16))
-    if C % 8 == 0:
-        assert _rel(xn.grad, xr.grad) < 2e-2, _rel(xn.grad, xr.grad)
+    assert _rel(xn.grad, xr.grad) < 2e-2, _rel(xn.grad, xr.grad)
     assert _rel(wn.grad, wr.grad) < 2e-2, _rel(wn.grad, wr.grad)
+
+
+@pytest.mark.parametrize("case", [(2, 28, 28, 1, 32, 5, 1, "same"), (2, 64, 64, 3, 64, 7, 2, 3)])
+def test_conv_element_gather_paths(case):
+    """The per-element gather kernels (fwd GATHER=1, wgrad GENERIC) on unpadded C=1 / C=3."""
+    N, H, W, C, K, R, stride, pad = case
+    torch.manual_seed(1)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K, R, R, C, device=dev) / (R * R * C) ** 0.5).to(torch.bfloat16)
+    nat, ref = _native(), _ref()
+    y = nat.conv2d_forward(x, w, stride, pad)
+    yr = ref.conv2d(x.float(), w.float(), stride, pad)
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(yr)
+    dw = nat.conv2d_wgrad(x, dy.to(torch.bfloat16), w.shape, stride, pad)
+    wr = w.float().requires_grad_(True)
+    ref.conv2d(x.float(), wr, stride, pad).backward(dy.to(torch.bfloat16).float())
+    assert _rel(dw, wr.grad) < 2e-2
 
 
 @pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, True, True), (512, False, False),

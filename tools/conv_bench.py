@@ -1,0 +1,103 @@
+"""Per-shape roofline table for the ResNet-50 (batch 256) convolutions: our fwd / dgrad / wgrad
+kernels timed with HIP events, reported as TFLOP/s, GB/s (compulsory bytes) and the fraction
+of the binding roof (2.5 PF/s bf16 dense, ~5 TB/s achievable HBM).
+
+    python tools/conv_bench.py [--batch 256] [--iters 20]
+"""
+import argparse
+import collections
+import json
+
+import torch
+
+from distributedtensorflow_amd.ops import native
+
+PEAK_TF = 2500.0
+PEAK_BW = 5.0e12   # achievable HBM3E (~8 TB/s theoretical)
+
+
+def resnet50_convs(B):
+    """(name, H, W, C, K, R, stride, pad, count) of every conv (v1.5: stride on the 3x3)."""
+    out = [("stem", 224, 224, 3, 64, 7, 2, 3, 1)]
+    cin, res = 64, 56
+    for si, (n, w) in enumerate(zip((3, 4, 6, 3), (64, 128, 256, 512))):
+        for bi in range(n):
+            s = 2 if (bi == 0 and si > 0) else 1
+            out.append((f"s{si}b{bi}c1", res, res, cin, w, 1, 1, 0, 1))
+            out.append((f"s{si}b{bi}c2", res, res, w, w, 3, s, 1, 1))
+            res2 = res // s
+            out.append((f"s{si}b{bi}c3", res2, res2, w, 4 * w, 1, 1, 0, 1))
+            if bi == 0:
+                out.append((f"s{si}b{bi}proj", res, res, cin, 4 * w, 1, s, 0, 1))
+            cin, res = 4 * w, res2
+    # merge identical shapes
+    agg = collections.OrderedDict()
+    for name, H, W, C, K, R, s, p, c in out:
+        key = (H, W, C, K, R, s, p)
+        if key in agg:
+            agg[key][1] += c
+        else:
+            agg[key] = [name, c]
+    return [(v[0], *k, v[1]) for k, v in agg.items()]
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default=None, help="comma list of layer names to run")
+    ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
+    args = ap.parse_args()
+    only = set(args.only.split(",")) if args.only else None
+    kinds = set(args.kinds.split(","))
+    B = args.batch
+    rows, tot = [], collections.Counter()
+    for name, H, W, C, K, R, s, p, cnt in resnet50_convs(B):
+        if only and name not in only:
+            continue
+        C = -(-C // 8) * 8          # the op zero-pads C=3 (stem) to 8 channels
+        x = torch.randn(B, H, W, C, device="cuda").bfloat16()
+        w = (torch.randn(K, R, R, C, device="cuda") * 0.05).bfloat16()
+        y = native.conv2d_forward(x, w, s, p)
+        P, Q = y.shape[1], y.shape[2]
+        dy = torch.randn_like(y)
+        flops = 2.0 * B * P * Q * K * R * R * C
+        xb, yb, wb = x.numel() * 2, y.numel() * 2, w.numel() * 2
+        cases = [("fwd", lambda: native.conv2d_forward(x, w, s, p), xb + yb + wb)]
+        if C % 8 == 0:
+            cases.append(("dgrad", lambda: native.conv2d_dgrad(dy, w, x.shape, s, p),
+                          xb + yb + wb))
+        cases.append(("wgrad", lambda: native.conv2d_wgrad(x, dy, w.shape, s, p),
+                      xb + yb + 2 * wb))
+        for kind, fn, nbytes in cases:
+            if kind not in kinds:
+                continue
+            t = timeit(fn, args.iters)
+            tf = flops / t / 1e12
+            bw = nbytes / t
+            roof = max(flops / (PEAK_TF * 1e12), nbytes / PEAK_BW)
+            rows.append({"layer": name, "kind": kind, "shape": f"{H}x{W}x{C}->{K} r{R} s{s}",
+                         "count": cnt, "us": round(t * 1e6, 1), "tflops": round(tf, 1),
+                         "GBps": round(bw / 1e9), "roof_frac": round(roof / t, 3)})
+            tot[kind] += t * cnt
+            tot["roof_" + kind] += roof * cnt
+    for r in rows:
+        print(json.dumps(r), flush=True)
+    summ = {k: round(v * 1e3, 3) for k, v in tot.items()}
+    print(json.dumps({"total_ms": summ}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
