@@ -10,7 +10,11 @@
 //
 // Forward (training):  stats -> finalize(mean, invstd, scale, shift, moving averages) -> apply
 // Backward:            reduce(sum dz, sum dz*xhat) -> finalize(dgamma, dbeta, coefs) -> apply
-//   with dz = dy * (y > 0) when ReLU was fused, and dx = A*dz + B*x + C per channel.
+//   with dz = dy * (y > 0) when ReLU was fused, and dx = A*dz + B*x + C per channel.  Without a
+//   residual the mask is recomputed from x (fmaf(x, scale, shift) > 0, the forward's exact
+//   expression), so the backward never reads y (-2 B/element in both backward passes).
+#include <stdexcept>
+
 #include "common.h"
 
 namespace {
@@ -37,19 +41,27 @@ __global__ void __launch_bounds__(kThreads)
 bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                  const bf16_t* __restrict__ y, const float* __restrict__ mean,
                  const float* __restrict__ invstd, long M, int C, int rows_per_block, int relu,
-                 float* __restrict__ partial) {
+                 float* __restrict__ partial, const float* __restrict__ fsc,
+                 const float* __restrict__ fsh) {
   extern __shared__ __attribute__((aligned(16))) float red[];   // [rpi][2][C]
   const int tpr = C >> 3;
   const int rpi = kThreads / tpr;
   const int tid = threadIdx.x;
   const int cg = tid % tpr, ro = tid / tpr;
   const bool active = ro < rpi;
-  float a0[8], a1[8], mu[8], is[8];
+  float a0[8], a1[8], mu[8], is[8], ksc[8], ksh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { a0[i] = 0.f; a1[i] = 0.f; }
+  // ReLU mask source: the saved output y, or (y == null) recomputed from x with the forward's
+  // scale/shift -- the same fmaf as bn_apply, so the sign (= the mask) is bit-identical
+  const bool mask_x = MODE == 1 && relu && y == nullptr;
   if (MODE == 1 && active) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) { mu[i] = mean[cg * 8 + i]; is[i] = invstd[cg * 8 + i]; }
+    if (mask_x) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { ksc[i] = fsc[cg * 8 + i]; ksh[i] = fsh[cg * 8 + i]; }
+    }
   }
   const long m0 = (long)blockIdx.x * rows_per_block;
   long m1 = m0 + rows_per_block;
@@ -65,7 +77,10 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
       } else {
         float g[8];
         unpack8(*reinterpret_cast<const uint4*>(dy + off), g);
-        if (relu) {
+        if (mask_x) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) g[i] = __builtin_fmaf(xv[i], ksc[i], ksh[i]) > 0.f ? g[i] : 0.f;
+        } else if (relu) {
           float yv[8];
           unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
 #pragma unroll
@@ -209,7 +224,7 @@ bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
     const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
     float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = xv[i] * sc[i] + sh[i];
+    for (int i = 0; i < 8; ++i) o[i] = __builtin_fmaf(xv[i], sc[i], sh[i]);
     if (res) {
       float r[8];
       unpack8(reinterpret_cast<const uint4*>(res)[v], r);
@@ -250,21 +265,26 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                     const bf16_t* __restrict__ x, const float* __restrict__ cA,
                     const float* __restrict__ cB, const float* __restrict__ cC,
                     bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long nvec, int C,
-                    int relu) {
+                    int relu, const float* __restrict__ fsc, const float* __restrict__ fsh) {
   const int tpr = C >> 3;
+  const bool mask_x = relu && y == nullptr;
   for (long v = (long)blockIdx.x * kThreads + threadIdx.x; v < nvec;
        v += (long)gridDim.x * kThreads) {
     const int cg = (int)(v % tpr);
     float g[8], xv[8];
     unpack8(reinterpret_cast<const uint4*>(dy)[v], g);
-    if (relu) {
+    unpack8(reinterpret_cast<const uint4*>(x)[v], xv);
+    if (mask_x) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        g[i] = __builtin_fmaf(xv[i], fsc[cg * 8 + i], fsh[cg * 8 + i]) > 0.f ? g[i] : 0.f;
+    } else if (relu) {
       float yv[8];
       unpack8(reinterpret_cast<const uint4*>(y)[v], yv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
     }
     if (dres) reinterpret_cast<uint4*>(dres)[v] = pack8(g);
-    unpack8(reinterpret_cast<const uint4*>(x)[v], xv);
     float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -296,15 +316,13 @@ void dtf_bn_fwd_stats(const bf16_t* x, long M, int C, float* partial, hipStream_
   const int rpi = kThreads / (C / 8);
   const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
   hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(G), dim3(kThreads), lds, st, x, nullptr, nullptr,
-                     nullptr, nullptr, M, C, rpb, 0, partial);
+                     nullptr, nullptr, M, C, rpb, 0, partial, nullptr, nullptr);
 }
 
-void dtf_bn_fwd_finalize(const float* partial, long M, int C, const float* gamma,
-                         const float* beta, float* run_mean, float* run_var, float momentum,
-                         float eps, float* mean, float* invstd, float* scale, float* shift,
-                         hipStream_t st) {
-  int rpb;
-  const int G = stats_grid(M, C, &rpb);
+void dtf_bn_fwd_finalize_g(const float* partial, int G, long M, int C, const float* gamma,
+                           const float* beta, float* run_mean, float* run_var, float momentum,
+                           float eps, float* mean, float* invstd, float* scale, float* shift,
+                           hipStream_t st) {
   const int S = combine_slices(G, C);
   double* level2 = reinterpret_cast<double*>(const_cast<float*>(partial) + (long)G * 2 * C);
   hipLaunchKernelGGL(bn_combine_kernel, dim3((C + 31) / 32, S), dim3(256), 0, st, partial, G, C,
@@ -314,11 +332,25 @@ void dtf_bn_fwd_finalize(const float* partial, long M, int C, const float* gamma
                      shift);
 }
 
+void dtf_bn_fwd_finalize(const float* partial, long M, int C, const float* gamma,
+                         const float* beta, float* run_mean, float* run_var, float momentum,
+                         float eps, float* mean, float* invstd, float* scale, float* shift,
+                         hipStream_t st) {
+  int rpb;
+  const int G = stats_grid(M, C, &rpb);
+  dtf_bn_fwd_finalize_g(partial, G, M, C, gamma, beta, run_mean, run_var, momentum, eps, mean,
+                        invstd, scale, shift, st);
+}
+
+// floats of workspace for G partial slabs + the fp64 combine slices
+long dtf_bn_workspace_floats_g(int G, int C) {
+  return (long)G * 2 * C + 2L * combine_slices(G, C) * 2 * C;
+}
+
 // floats of workspace a stats/reduce + finalize pair needs: G partial slabs + S fp64 slices
 long dtf_bn_workspace_floats(long M, int C) {
   int rpb;
-  const int G = stats_grid(M, C, &rpb);
-  return (long)G * 2 * C + 2L * combine_slices(G, C) * 2 * C;
+  return dtf_bn_workspace_floats_g(stats_grid(M, C, &rpb), C);
 }
 
 void dtf_bn_infer_finalize(int C, const float* gamma, const float* beta, const float* run_mean,
@@ -337,13 +369,14 @@ void dtf_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* sc
 
 void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
                        const float* invstd, long M, int C, int relu, float* partial,
-                       hipStream_t st) {
+                       const float* fsc, const float* fsh, hipStream_t st) {
+  if (relu && !y && !(fsc && fsh)) throw std::runtime_error("bn_bwd: relu mask needs y or scale/shift");
   int rpb;
   const int G = stats_grid(M, C, &rpb);
   const int rpi = kThreads / (C / 8);
   const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
   hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(G), dim3(kThreads), lds, st, x, dy, y, mean, invstd,
-                     M, C, rpb, relu, partial);
+                     M, C, rpb, relu, partial, fsc, fsh);
 }
 
 void dtf_bn_bwd_finalize(const float* partial, long M, int C, const float* gamma,
@@ -362,8 +395,9 @@ void dtf_bn_bwd_finalize(const float* partial, long M, int C, const float* gamma
 
 void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* cA,
                       const float* cB, const float* cC, bf16_t* dx, bf16_t* dres, long M, int C,
-                      int relu, hipStream_t st) {
+                      int relu, const float* fsc, const float* fsh, hipStream_t st) {
+  if (relu && !y && !(fsc && fsh)) throw std::runtime_error("bn_bwd: relu mask needs y or scale/shift");
   const long nvec = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(kThreads), 0, st, dy, y, x, cA,
-                     cB, cC, dx, dres, nvec, C, relu);
+                     cB, cC, dx, dres, nvec, C, relu, fsc, fsh);
 }

@@ -27,16 +27,21 @@ long dtf_bn_workspace_floats(long M, int C);
 void dtf_bn_fwd_stats(const bf16_t*, long, int, float*, hipStream_t);
 void dtf_bn_fwd_finalize(const float*, long, int, const float*, const float*, float*, float*,
                          float, float, float*, float*, float*, float*, hipStream_t);
+void dtf_bn_fwd_finalize_g(const float*, int, long, int, const float*, const float*, float*,
+                           float*, float, float, float*, float*, float*, float*, hipStream_t);
+long dtf_bn_workspace_floats_g(int, int);
+int dtf_conv_stats_rows(long, int);
 void dtf_bn_infer_finalize(int, const float*, const float*, const float*, const float*, float,
                            float*, float*, float*, float*, hipStream_t);
 void dtf_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, const float*, const float*, long, int,
                   int, hipStream_t);
 void dtf_bn_bwd_reduce(const bf16_t*, const bf16_t*, const bf16_t*, const float*, const float*,
-                       long, int, int, float*, hipStream_t);
+                       long, int, int, float*, const float*, const float*, hipStream_t);
 void dtf_bn_bwd_finalize(const float*, long, int, const float*, const float*, const float*,
                          float*, float*, float*, float*, float*, int, hipStream_t);
 void dtf_bn_bwd_apply(const bf16_t*, const bf16_t*, const bf16_t*, const float*, const float*,
-                      const float*, bf16_t*, bf16_t*, long, int, int, hipStream_t);
+                      const float*, bf16_t*, bf16_t*, long, int, int, const float*, const float*,
+                      hipStream_t);
 void dtf_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int,
                      int, int, int, int, hipStream_t);
 void dtf_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int,
@@ -57,7 +62,7 @@ int dtf_lamb_chunk_bytes();
 void dtf_sumsq(const float*, long, float*, hipStream_t);
 void dtf_cast_f32_bf16(const float*, bf16_t*, long, hipStream_t);
 void dtf_conv_igemm(const bf16_t*, const bf16_t*, bf16_t*, const ConvGeom&, const TapTable&, int,
-                    hipStream_t);
+                    float*, hipStream_t);
 void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, const TapTableW&,
                     int, int, int, hipStream_t);
 
@@ -110,6 +115,18 @@ PYBIND11_MODULE(_dtf_hip, m) {
 
   m.def("bn_partial_blocks", &dtf_bn_partial_blocks);
   m.def("bn_workspace_floats", &dtf_bn_workspace_floats);
+  m.def("bn_workspace_floats_g", &dtf_bn_workspace_floats_g);
+  m.def("conv_stats_rows", &dtf_conv_stats_rows);
+  m.def("bn_fwd_finalize_g", [](uintptr_t part, int G, long M, int C, uintptr_t gamma,
+                                uintptr_t beta, uintptr_t rm, uintptr_t rv, float mom, float eps,
+                                uintptr_t mean, uintptr_t invstd, uintptr_t scale, uintptr_t shift,
+                                uintptr_t st) {
+    dtf_bn_fwd_finalize_g(P<const float>(part), G, M, C, P<const float>(gamma),
+                          P<const float>(beta), P<float>(rm), P<float>(rv), mom, eps,
+                          P<float>(mean), P<float>(invstd), P<float>(scale), P<float>(shift),
+                          S(st));
+    check_launch("bn_fwd_finalize_g");
+  });
   m.def("bn_fwd_stats", [](uintptr_t x, long M, int C, uintptr_t part, uintptr_t st) {
     dtf_bn_fwd_stats(P<const bf16_t>(x), M, C, P<float>(part), S(st));
     check_launch("bn_fwd_stats");
@@ -138,12 +155,14 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("bn_bwd_reduce", [](uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t mean,
                             uintptr_t invstd, long M, int C, int relu, uintptr_t part,
-                            uintptr_t st) {
+                            uintptr_t st, uintptr_t fsc, uintptr_t fsh) {
     dtf_bn_bwd_reduce(P<const bf16_t>(dy), P<const bf16_t>(y), P<const bf16_t>(x),
                       P<const float>(mean), P<const float>(invstd), M, C, relu, P<float>(part),
-                      S(st));
+                      P<const float>(fsc), P<const float>(fsh), S(st));
     check_launch("bn_bwd_reduce");
-  });
+  }, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("M"),
+     py::arg("C"), py::arg("relu"), py::arg("part"), py::arg("stream"), py::arg("scale") = 0,
+     py::arg("shift") = 0);
   m.def("bn_bwd_finalize", [](uintptr_t part, long M, int C, uintptr_t gamma, uintptr_t mean,
                               uintptr_t invstd, uintptr_t dg, uintptr_t db, uintptr_t a,
                               uintptr_t b, uintptr_t c, int accumulate, uintptr_t st) {
@@ -154,12 +173,14 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("bn_bwd_apply", [](uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t a, uintptr_t b,
                            uintptr_t c, uintptr_t dx, uintptr_t dres, long M, int C, int relu,
-                           uintptr_t st) {
+                           uintptr_t st, uintptr_t fsc, uintptr_t fsh) {
     dtf_bn_bwd_apply(P<const bf16_t>(dy), P<const bf16_t>(y), P<const bf16_t>(x),
                      P<const float>(a), P<const float>(b), P<const float>(c), P<bf16_t>(dx),
-                     P<bf16_t>(dres), M, C, relu, S(st));
+                     P<bf16_t>(dres), M, C, relu, P<const float>(fsc), P<const float>(fsh), S(st));
     check_launch("bn_bwd_apply");
-  });
+  }, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("a"), py::arg("b"), py::arg("c"),
+     py::arg("dx"), py::arg("dres"), py::arg("M"), py::arg("C"), py::arg("relu"),
+     py::arg("stream"), py::arg("scale") = 0, py::arg("shift") = 0);
   m.def("maxpool_fwd", [](uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W, int C,
                           int Pp, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
                           uintptr_t st) {
@@ -227,14 +248,16 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("cast_f32_bf16");
   });
   m.def("conv_igemm", [](uintptr_t x, uintptr_t w, uintptr_t y, std::vector<int> geom,
-                         std::vector<int> dh, std::vector<int> dw, int bk, uintptr_t st) {
+                         std::vector<int> dh, std::vector<int> dw, int bk, uintptr_t st,
+                         uintptr_t stats) {
     if (geom.size() != 16) throw std::runtime_error("conv_igemm: geom needs 16 ints");
     ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
                geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15]};
     dtf_conv_igemm(P<const bf16_t>(x), P<const bf16_t>(w), P<bf16_t>(y), g,
-                   make_taps<TapTable>(dh, dw), bk, S(st));
+                   make_taps<TapTable>(dh, dw), bk, P<float>(stats), S(st));
     check_launch("conv_igemm");
-  });
+  }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("dh"), py::arg("dw"),
+     py::arg("bk"), py::arg("stream"), py::arg("stats") = 0);
   m.def("conv_wgrad", [](uintptr_t x, uintptr_t dy, uintptr_t dw_out, uintptr_t ws,
                          std::vector<int> geom, std::vector<int> dh, std::vector<int> dw,
                          int splits, uintptr_t st, int tr_mode, int accumulate) {

@@ -80,7 +80,8 @@ DTF_DEV uint32_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 template <int WAVES_M, int WAVES_N, int BK, int GATHER>
 __global__ void __launch_bounds__(kThreads, 2)
 conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
-                  bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps) {
+                  bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
+                  float* __restrict__ stats) {
   constexpr int BM = 64 * WAVES_M, BN = 64 * WAVES_N;
   constexpr int CPR = BK / 8;                            // chunks per row
   constexpr int A_CHUNKS = BM * CPR / kThreads;          // 16-B loads per thread for A
@@ -275,27 +276,62 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     const long off = (((long)n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8;
     *reinterpret_cast<uint4*>(Y + off) = *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
   }
+  if (stats) {
+    // Fused BatchNorm statistics (training forward): per output channel, sum and sum of
+    // squares of this tile's bf16-ROUNDED outputs (exactly what the BN will normalise), written
+    // as row `tm` of a [tiles_m][2][Kout] partial slab that the BN finalize combines in a fixed
+    // order -- replaces a full re-read of the conv output by a separate stats kernel.
+    constexpr int GROUPS = kThreads / BN;          // row groups per column
+    constexpr int RPG = BM / GROUPS;
+    float* red = reinterpret_cast<float*>(st + BM * LDC);   // [GROUPS][2][BN], past the tile
+    const int col = tid % BN, grp = tid / BN;
+    float s1 = 0.f, s2 = 0.f;
+    const int rend = min(RPG * (grp + 1), M - m0);
+    for (int r = RPG * grp; r < rend; ++r) {
+      const float v = bf2f(st[r * LDC + col]);
+      s1 += v;
+      s2 += v * v;
+    }
+    red[(grp * 2 + 0) * BN + col] = s1;
+    red[(grp * 2 + 1) * BN + col] = s2;
+    __syncthreads();
+    if (grp == 0 && n0 + col < g.Kout) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) { a += red[(k * 2 + 0) * BN + col]; b += red[(k * 2 + 1) * BN + col]; }
+      stats[((long)tm * 2 + 0) * g.Kout + n0 + col] = a;
+      stats[((long)tm * 2 + 1) * g.Kout + n0 + col] = b;
+    }
+  }
 }
 
 template <int WM, int WN, int BK, int GEN>
 void launch_cfg(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
-                const TapTable& taps, hipStream_t st) {
+                const TapTable& taps, float* stats, hipStream_t st) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   const long M = (long)g.N * g.P * g.Q;
   const long tiles = ((M + BM - 1) / BM) * ((g.Kout + BN - 1) / BN);
   const size_t stage = (size_t)(BM + BN) * BK * sizeof(bf16_t) * 2 + 2 * DTF_MAX_TAPS * sizeof(int);
-  const size_t epi = (size_t)BM * (BN + 8) * sizeof(bf16_t);
+  const size_t epi = (size_t)BM * (BN + 8) * sizeof(bf16_t) +
+                    (size_t)2 * kThreads * sizeof(float);          // + stats reduction scratch
   const size_t lds = stage > epi ? stage : epi;
   hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN>), dim3((unsigned)tiles), dim3(kThreads),
-                     lds, st, X, Wt, Y, g, taps);
+                     lds, st, X, Wt, Y, g, taps, stats);
 }
 
 }  // namespace
 
 // Host launcher.  Caller guarantees: Kout % 8 == 0, Kpad % BK == 0 (filter rows zero-padded),
 // 16-B aligned tensors, taps.n <= DTF_MAX_TAPS.
+// Rows of the BN-statistics slab a forward launch writes (= its M tiles), for the caller's
+// workspace sizing; must mirror the tile choice in dtf_conv_igemm.
+int dtf_conv_stats_rows(long M, int Kout) {
+  const int BM = Kout <= 64 ? 256 : 128;
+  return (int)((M + BM - 1) / BM);
+}
+
 void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
-                    const TapTable& taps, int bk, hipStream_t st) {
+                    const TapTable& taps, int bk, float* stats, hipStream_t st) {
   if (taps.n <= 0 || taps.n > DTF_MAX_TAPS) throw std::runtime_error("conv: bad tap count");
   if (g.Kout % 8) throw std::runtime_error("conv: Kout % 8 != 0");
   const double xbytes = 2.0 * g.N * g.H * g.W * g.C, wbytes = 2.0 * g.Kout * g.Kpad;
@@ -306,19 +342,19 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
   if (g.C % 32 != 0) {
     if (g.Kpad % 32) throw std::runtime_error("conv: Kpad % 32 != 0");
     if (g.C % 8 == 0) {                    // chunk gather (stem / MNIST conv1, C padded to 8)
-      if (narrow) launch_cfg<4, 1, 32, 2>(X, Wt, Y, g, taps, st);
-      else launch_cfg<2, 2, 32, 2>(X, Wt, Y, g, taps, st);
+      if (narrow) launch_cfg<4, 1, 32, 2>(X, Wt, Y, g, taps, stats, st);
+      else launch_cfg<2, 2, 32, 2>(X, Wt, Y, g, taps, stats, st);
     } else {
-      if (narrow) launch_cfg<4, 1, 32, 1>(X, Wt, Y, g, taps, st);
-      else launch_cfg<2, 2, 32, 1>(X, Wt, Y, g, taps, st);
+      if (narrow) launch_cfg<4, 1, 32, 1>(X, Wt, Y, g, taps, stats, st);
+      else launch_cfg<2, 2, 32, 1>(X, Wt, Y, g, taps, stats, st);
     }
     return;
   }
   if (bk == 64 && g.C % 64 == 0) {
-    if (narrow) launch_cfg<4, 1, 64, 0>(X, Wt, Y, g, taps, st);
-    else launch_cfg<2, 2, 64, 0>(X, Wt, Y, g, taps, st);
+    if (narrow) launch_cfg<4, 1, 64, 0>(X, Wt, Y, g, taps, stats, st);
+    else launch_cfg<2, 2, 64, 0>(X, Wt, Y, g, taps, stats, st);
   } else {
-    if (narrow) launch_cfg<4, 1, 32, 0>(X, Wt, Y, g, taps, st);
-    else launch_cfg<2, 2, 32, 0>(X, Wt, Y, g, taps, st);
+    if (narrow) launch_cfg<4, 1, 32, 0>(X, Wt, Y, g, taps, stats, st);
+    else launch_cfg<2, 2, 32, 0>(X, Wt, Y, g, taps, stats, st);
   }
 }

@@ -26,7 +26,8 @@ class ConvBN(nn.Module):
                                      gamma_init=0.0 if zero_gamma else 1.0)
 
     def forward(self, x, relu=True, residual=None):
-        y = ops.conv2d(x, self.conv.kernel, self.conv.strides, self.conv.padding)
+        y = ops.conv2d(x, self.conv.kernel, self.conv.strides, self.conv.padding,
+                       bn_stats=self.bn.training)
         return self.bn(y, relu=relu, residual=residual)
 
 

@@ -42,9 +42,11 @@ def _native():
     return native
 
 
-def conv2d(x, w, stride=1, padding=0):
+def conv2d(x, w, stride=1, padding=0, bn_stats=False):
+    """``bn_stats``: a training-mode batch_norm consumes the result (native path fuses the BN
+    statistics into the conv epilogue; ignored by the reference path)."""
     if _use_native(x):
-        return _native().conv2d(x, w, stride, padding)
+        return _native().conv2d(x, w, stride, padding, bn_stats)
     return reference.conv2d(x, w, stride, padding)
 
 

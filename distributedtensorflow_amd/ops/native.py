@@ -90,7 +90,8 @@ def _conv_geom_fwd(x, K, R, S, stride, padding):
     return n, h, w, c, P, Q, sh, sw, pt, pl
 
 
-def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0):
+def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
+                stats=None):
     """wmat: [K, T*C] bf16 (rows zero-padded here to a multiple of 32 for the gather path)."""
     n, h, w, c = x.shape
     dh = [t[0] for t in taps]
@@ -102,17 +103,19 @@ def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0
         padded[:, :kdim] = wmat
         wmat = padded
     geom = [n, h, w, c, P, Q, sh, sw, K, kpad, Ho, Wo, osh, osw, oh0, ow0]
-    _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st())
+    _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
+                  _p(stats))
 
 
-def conv2d_forward(x, w_bf16, stride, padding):
-    """x [N,H,W,C] bf16, w [K,R,S,C] bf16 -> y [N,P,Q,K]."""
+def conv2d_forward(x, w_bf16, stride, padding, stats=None):
+    """x [N,H,W,C] bf16, w [K,R,S,C] bf16 -> y [N,P,Q,K].  ``stats``: fp32 workspace that also
+    receives the per-M-tile BatchNorm partial sums of y (see conv2d(bn_stats=True))."""
     K, R, S, C = w_bf16.shape
     n, h, wd, c, P, Q, sh, sw, pt, pl = _conv_geom_fwd(x, K, R, S, stride, padding)
     assert c == C, (x.shape, w_bf16.shape)
     taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
     y = torch.empty(n, P, Q, K, device=x.device, dtype=_BF16)
-    _launch_fwd(x, w_bf16.reshape(K, R * S * C), K, taps, P, Q, sh, sw, y, P, Q)
+    _launch_fwd(x, w_bf16.reshape(K, R * S * C), K, taps, P, Q, sh, sw, y, P, Q, stats=stats)
     return y
 
 
@@ -190,7 +193,7 @@ def _pad_c8(t):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w_master, stride, padding):
+    def forward(ctx, x, w_master, stride, padding, stats=None):
         xb = x.contiguous()
         wb = _bf16_weight(w_master)
         ctx.c_orig = xb.shape[-1]
@@ -202,7 +205,7 @@ class _Conv2d(torch.autograd.Function):
         ctx.stride, ctx.padding = stride, padding
         ctx.w_dtype = w_master.dtype
         ctx.w_param = w_master
-        return conv2d_forward(xb, wb, stride, padding)
+        return conv2d_forward(xb, wb, stride, padding, stats)
 
     @staticmethod
     def backward(ctx, dy):
@@ -231,15 +234,26 @@ class _Conv2d(torch.autograd.Function):
             dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding)
             if padded:
                 dx = dx[..., :C].contiguous()
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
-def conv2d(x, w, stride=1, padding=0):
+def conv2d(x, w, stride=1, padding=0, bn_stats=False):
+    """NHWC conv.  ``bn_stats=True`` (a training-mode BatchNorm consumes the output): the conv
+    epilogue also emits the BN partial sums, attached to the output as ``_dtf_bn_part`` and picked
+    up by :func:`batch_norm`, which then skips its own statistics pass over the tensor."""
     _check_cuda_bf16(x)
     K, R, S, C = w.shape
     if K % 8 or R * S > 64:
         raise ValueError(f"native conv2d: unsupported filter {tuple(w.shape)}")
-    return _Conv2d.apply(x, w, stride, padding)
+    if not bn_stats:
+        return _Conv2d.apply(x, w, stride, padding, None)
+    n, h, wd, c, P, Q, sh, sw, pt, pl = _conv_geom_fwd(x, K, R, S, stride, padding)
+    M = n * P * Q
+    G = _K.conv_stats_rows(M, K)
+    part = torch.empty(_K.bn_workspace_floats_g(G, K), device=x.device, dtype=torch.float32)
+    y = _Conv2d.apply(x, w, stride, padding, part)
+    y._dtf_bn_part = (part, G, M, K)
+    return y
 
 
 # ----------------------------------------------------------------------------- batch norm
@@ -256,7 +270,15 @@ class _BatchNorm(torch.autograd.Function):
         mean, invstd, scale, shift = stats[0], stats[1], stats[2], stats[3]
         st = _st()
         g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
-        if training:
+        fused = getattr(x, "_dtf_bn_part", None)
+        if training and fused is not None and fused[2:] == (M, C):
+            # statistics already produced by the producing conv's epilogue
+            part, G = fused[0], fused[1]
+            _K.bn_fwd_finalize_g(part.data_ptr(), G, M, C, g32.data_ptr(), b32.data_ptr(),
+                                 _p(running_mean), _p(running_var), float(momentum), float(eps),
+                                 mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
+                                 shift.data_ptr(), st)
+        elif training:
             part = torch.empty(_K.bn_workspace_floats(M, C), device=dev, dtype=torch.float32)
             _K.bn_fwd_stats(x.data_ptr(), M, C, part.data_ptr(), st)
             _K.bn_fwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), b32.data_ptr(),
@@ -288,8 +310,14 @@ class _BatchNorm(torch.autograd.Function):
         st = _st()
         mean, invstd = stats[0], stats[1]
         part = torch.empty(_K.bn_workspace_floats(M, C), device=dev, dtype=torch.float32)
-        _K.bn_bwd_reduce(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr(),
-                         invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st)
+        # ReLU mask: from the saved output when a residual was added before the ReLU, else
+        # recomputed from x with the forward's scale/shift (saves reading y in both passes)
+        mask_x = ctx.relu and not ctx.has_res
+        y_ptr = 0 if mask_x else y.data_ptr()
+        sc_ptr, sh_ptr = (stats[2].data_ptr(), stats[3].data_ptr()) if mask_x else (0, 0)
+        _K.bn_bwd_reduce(dy.data_ptr(), y_ptr, x.data_ptr(), mean.data_ptr(),
+                         invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st,
+                         sc_ptr, sh_ptr)
         gb = torch.empty(5, C, device=dev, dtype=torch.float32)  # dgamma dbeta A B C
         tg, tb = (_direct_grad(p) for p in ctx.params)
         direct = tg is not None and tb is not None
@@ -303,9 +331,9 @@ class _BatchNorm(torch.autograd.Function):
                 _grad_ready(p)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
-        _K.bn_bwd_apply(dy.data_ptr(), y.data_ptr(), x.data_ptr(), gb[2].data_ptr(),
+        _K.bn_bwd_apply(dy.data_ptr(), y_ptr, x.data_ptr(), gb[2].data_ptr(),
                         gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
-                        int(ctx.relu), st)
+                        int(ctx.relu), st, sc_ptr, sh_ptr)
         if direct:
             return dx, None, None, None, None, None, None, None, None, dres
         return (dx, gb[0].to(ctx.gdt), gb[1].to(ctx.bdt), None, None, None, None, None, None,

@@ -97,3 +97,28 @@ def test_resnet50_train_first_stage_matches_reference():
     for tag, (nat, ref) in outs.items():
         rel = ((nat - ref).norm() / ref.norm()).item()
         assert rel < 0.03, (tag, rel)
+
+
+@pytest.mark.parametrize("shape", [(4, 56, 56, 64, 64, 1), (4, 28, 28, 128, 256, 3),
+                                   (3, 9, 11, 64, 72, 3)])
+def test_conv_epilogue_bn_stats_match_separate_pass(shape):
+    """conv2d(bn_stats=True) + batch_norm (statistics from the conv epilogue) == the separate
+    statistics kernel path: outputs, batch stats and moving averages."""
+    N, H, W, C, K, R = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    w = torch.randn(K, R, R, C, device="cuda") / (R * R * C) ** 0.5
+    gamma = torch.rand(K, device="cuda") + 0.5
+    beta = torch.randn(K, device="cuda") * 0.1
+    outs = []
+    for fused in (True, False):
+        rm, rv = torch.zeros(K, device="cuda"), torch.ones(K, device="cuda")
+        y = native.conv2d(x, w, 1, (R - 1) // 2, bn_stats=fused)
+        assert hasattr(y, "_dtf_bn_part") == fused
+        z = native.batch_norm(y, gamma, beta, rm, rv, True, 0.9, 1e-5, relu=True)
+        outs.append((y.float(), z.float(), rm, rv))
+    (y1, z1, m1, v1), (y2, z2, m2, v2) = outs
+    assert torch.equal(y1, y2)
+    torch.testing.assert_close(z1, z2, atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(m1, m2, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(v1, v2, atol=1e-5, rtol=1e-4)

@@ -3,6 +3,7 @@
 # ResNet-50 conv shapes; keeps only the counter CSV + a per-kernel summary.
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
+export PYTHONPATH="$R${PYTHONPATH:+:$PYTHONPATH}"
 OUT="$R/gpurun_out/pmc"
 mkdir -p "$OUT"
 cd /tmp || exit 1
