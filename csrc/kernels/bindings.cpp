@@ -18,7 +18,7 @@ namespace py = pybind11;
 #define DTF_MAX_TAPS 64
 struct TapTable { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
 struct TapTableW { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
-struct ConvGeom { int N, H, W, C, P, Q, sh, sw, Kout, Kpad, Ho, Wo, osh, osw, oh0, ow0; };
+struct ConvGeom { int N, H, W, C, P, Q, sh, sw, Kout, Kpad, Ho, Wo, osh, osw, oh0, ow0, acc; };
 struct WgradGeom { int N, H, W, C, P, Q, sh, sw, Kout, ldw; long m_per_split; long slab; };
 
 // ---- launchers defined in the .hip translation units
@@ -250,9 +250,11 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("conv_igemm", [](uintptr_t x, uintptr_t w, uintptr_t y, std::vector<int> geom,
                          std::vector<int> dh, std::vector<int> dw, int bk, uintptr_t st,
                          uintptr_t stats) {
-    if (geom.size() != 16) throw std::runtime_error("conv_igemm: geom needs 16 ints");
+    if (geom.size() != 16 && geom.size() != 17)
+      throw std::runtime_error("conv_igemm: geom needs 16 (+acc) ints");
     ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
-               geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15]};
+               geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15],
+               geom.size() == 17 ? geom[16] : 0};
     dtf_conv_igemm(P<const bf16_t>(x), P<const bf16_t>(w), P<bf16_t>(y), g,
                    make_taps<TapTable>(dh, dw), bk, P<float>(stats), S(st));
     check_launch("conv_igemm");

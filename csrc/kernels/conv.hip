@@ -53,6 +53,7 @@ struct ConvGeom {
   int Kpad;              // filter row stride (T*C rounded up to BK)
   int Ho, Wo;            // output tensor spatial dims
   int osh, osw, oh0, ow0;// output placement
+  int acc;               // 1: Y += result (dgrad accumulating onto a residual gradient)
 };
 
 namespace {
@@ -274,7 +275,16 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     const int n = t / g.P;
     const int ho = p * g.osh + g.oh0, wo = q * g.osw + g.ow0;
     const long off = (((long)n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8;
-    *reinterpret_cast<uint4*>(Y + off) = *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
+    uint4 v = *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
+    if (g.acc) {   // fused residual-gradient add: one extra 16-B read instead of an add kernel
+      float a[8], b[8];
+      unpack8(v, a);
+      unpack8(*reinterpret_cast<const uint4*>(Y + off), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+      v = pack8(a);
+    }
+    *reinterpret_cast<uint4*>(Y + off) = v;
   }
   if (stats) {
     // Fused BatchNorm statistics (training forward): per output channel, sum and sum of

@@ -171,9 +171,10 @@ class BatchNormalization(Layer):
         _tag(self.moving_variance, f"{self.name}/moving_variance")
         return out
 
-    def forward(self, x, relu=False, residual=None):
+    def forward(self, x, relu=False, residual=None, residual_to_conv=False):
         return ops.batch_norm(x, self.gamma, self.beta, self.moving_mean, self.moving_variance,
-                              self.training, self.momentum, self.epsilon, relu, residual)
+                              self.training, self.momentum, self.epsilon, relu, residual,
+                              residual_to_conv)
 
 
 class MaxPooling2D(Layer):

@@ -25,10 +25,10 @@ class ConvBN(nn.Module):
         self.bn = BatchNormalization(cout, bn_momentum, bn_eps, name=f"{name}_bn",
                                      gamma_init=0.0 if zero_gamma else 1.0)
 
-    def forward(self, x, relu=True, residual=None):
+    def forward(self, x, relu=True, residual=None, residual_to_conv=False):
         y = ops.conv2d(x, self.conv.kernel, self.conv.strides, self.conv.padding,
                        bn_stats=self.bn.training)
-        return self.bn(y, relu=relu, residual=residual)
+        return self.bn(y, relu=relu, residual=residual, residual_to_conv=residual_to_conv)
 
 
 class Bottleneck(nn.Module):
@@ -48,7 +48,8 @@ class Bottleneck(nn.Module):
         sc = self.proj(x, relu=False) if self.has_proj else x
         y = self.c1(x)
         y = self.c2(y)
-        return self.c3(y, relu=True, residual=sc)
+        # identity shortcut: c1 (1x1, stride 1) also reads x, so its dgrad absorbs d(residual)
+        return self.c3(y, relu=True, residual=sc, residual_to_conv=not self.has_proj)
 
 
 class ResNet(Layer):

@@ -51,10 +51,12 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False):
 
 
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True,
-               momentum=0.997, eps=1e-5, relu=False, residual=None):
+               momentum=0.997, eps=1e-5, relu=False, residual=None, residual_to_conv=False):
+    """``residual_to_conv``: the residual tensor is also the input of a stride-1 conv whose
+    data-gradient kernel will add d(residual) in its epilogue (native path; identity shortcuts)."""
     if _use_native(x):
         return _native().batch_norm(x, gamma, beta, running_mean, running_var, training,
-                                    momentum, eps, relu, residual)
+                                    momentum, eps, relu, residual, residual_to_conv)
     return reference.batch_norm(x, gamma, beta, running_mean, running_var, training,
                                 momentum, eps, relu, residual)
 

@@ -91,7 +91,7 @@ def _conv_geom_fwd(x, K, R, S, stride, padding):
 
 
 def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
-                stats=None):
+                stats=None, accumulate=False):
     """wmat: [K, T*C] bf16 (rows zero-padded here to a multiple of 32 for the gather path)."""
     n, h, w, c = x.shape
     dh = [t[0] for t in taps]
@@ -102,7 +102,7 @@ def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0
         padded = torch.zeros(K, kpad, device=x.device, dtype=_BF16)
         padded[:, :kdim] = wmat
         wmat = padded
-    geom = [n, h, w, c, P, Q, sh, sw, K, kpad, Ho, Wo, osh, osw, oh0, ow0]
+    geom = [n, h, w, c, P, Q, sh, sw, K, kpad, Ho, Wo, osh, osw, oh0, ow0, int(accumulate)]
     _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
                   _p(stats))
 
@@ -119,8 +119,9 @@ def conv2d_forward(x, w_bf16, stride, padding, stats=None):
     return y
 
 
-def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding):
-    """dX of conv2d via per-phase-class tap tables (see csrc/kernels/conv.hip header)."""
+def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None):
+    """dX of conv2d via per-phase-class tap tables (see csrc/kernels/conv.hip header).
+    ``out``: an existing bf16 gradient of x to ADD into (stride-1 convs only)."""
     K, R, S, C = w_bf16.shape
     n, h, wd, c = x_shape
     sh, sw = _pair(stride)
@@ -148,7 +149,11 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding):
                 need_zero = True
                 continue
             launches.append((a, b, Pc, Qc, taps, idx))
-    dx = (torch.zeros if need_zero else torch.empty)(n, h, wd, C, device=dy.device, dtype=_BF16)
+    acc = out is not None
+    if acc and (need_zero or len(launches) != 1):
+        raise ValueError("accumulating dgrad needs a single-phase (stride-1) conv")
+    dx = out if acc else (torch.zeros if need_zero else torch.empty)(
+        n, h, wd, C, device=dy.device, dtype=_BF16)
     dyc = dy.contiguous()
     for a, b, Pc, Qc, taps, idx in launches:
         if len(idx) == R * S and sh == 1 and sw == 1:
@@ -156,7 +161,8 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding):
         else:
             sel = wflat[:, torch.tensor(idx, device=dy.device), :]
         wd_mat = sel.permute(2, 1, 0).contiguous()           # [C, T, K]
-        _launch_fwd(dyc, wd_mat.reshape(C, -1), C, taps, Pc, Qc, 1, 1, dx, h, wd, sh, sw, a, b)
+        _launch_fwd(dyc, wd_mat.reshape(C, -1), C, taps, Pc, Qc, 1, 1, dx, h, wd, sh, sw, a, b,
+                    accumulate=acc)
     return dx
 
 
@@ -205,6 +211,7 @@ class _Conv2d(torch.autograd.Function):
         ctx.stride, ctx.padding = stride, padding
         ctx.w_dtype = w_master.dtype
         ctx.w_param = w_master
+        ctx.x_ref = x            # a residual BN may stash its residual gradient on x
         return conv2d_forward(xb, wb, stride, padding, stats)
 
     @staticmethod
@@ -231,9 +238,20 @@ class _Conv2d(torch.autograd.Function):
                 else:
                     dw = dw.to(ctx.w_dtype)
         if ctx.needs_input_grad[0]:
-            dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding)
-            if padded:
-                dx = dx[..., :C].contiguous()
+            pending = getattr(ctx.x_ref, "_dtf_pending_grad", None)
+            if pending is not None and not padded and _pair(ctx.stride) == (1, 1):
+                # identity shortcut: the block's final BN left d(residual) here; accumulate this
+                # conv's dgrad onto it in the epilogue instead of a separate bf16 add kernel
+                del ctx.x_ref._dtf_pending_grad
+                dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding, out=pending)
+            else:
+                dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding)
+                if padded:
+                    dx = dx[..., :C].contiguous()
+                if pending is not None:
+                    del ctx.x_ref._dtf_pending_grad
+                    dx = dx + pending
+        ctx.x_ref = None
         return dx, dw, None, None, None
 
 
@@ -258,10 +276,13 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False):
 
 # ----------------------------------------------------------------------------- batch norm
 
+_FUSE_RESIDUAL_GRAD = os.environ.get("DTF_FUSE_RESIDUAL_GRAD", "1") == "1"
+
+
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu,
-                residual):
+                residual, residual_to_conv=False):
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -298,6 +319,9 @@ class _BatchNorm(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.gdt, ctx.bdt = gamma.dtype, beta.dtype
         ctx.params = (gamma, beta)
+        # identity-shortcut blocks: hand d(residual) to the conv that also reads the residual
+        # tensor (it accumulates its dgrad onto it) instead of returning it to autograd
+        ctx.res_ref = residual if (residual_to_conv and _FUSE_RESIDUAL_GRAD) else None
         return y
 
     @staticmethod
@@ -334,14 +358,18 @@ class _BatchNorm(torch.autograd.Function):
         _K.bn_bwd_apply(dy.data_ptr(), y_ptr, x.data_ptr(), gb[2].data_ptr(),
                         gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
                         int(ctx.relu), st, sc_ptr, sh_ptr)
+        if dres is not None and ctx.res_ref is not None:
+            ctx.res_ref._dtf_pending_grad = dres
+            dres = None
+        ctx.res_ref = None
         if direct:
-            return dx, None, None, None, None, None, None, None, None, dres
+            return dx, None, None, None, None, None, None, None, None, dres, None
         return (dx, gb[0].to(ctx.gdt), gb[1].to(ctx.bdt), None, None, None, None, None, None,
-                dres)
+                dres, None)
 
 
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True,
-               momentum=0.997, eps=1e-5, relu=False, residual=None):
+               momentum=0.997, eps=1e-5, relu=False, residual=None, residual_to_conv=False):
     _check_cuda_bf16(x, residual)
     C = x.shape[-1]
     if C % 8 or C > 2048:
@@ -349,7 +377,7 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
     if residual is not None and residual.shape != x.shape:
         raise ValueError("residual shape mismatch")
     return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps,
-                            relu, residual)
+                            relu, residual, residual_to_conv)
 
 
 # ----------------------------------------------------------------------------- ReLU (standalone)

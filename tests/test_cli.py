@@ -85,3 +85,40 @@ def test_between_graph_cluster(tmp_path, data_dir):
     assert all(c == 0 for c in codes.values()), {k: t[-2000:] for k, t in text.items()}
     assert "Close Parameter Server" in text["ps0"]
     assert _result(text["worker0"])["global_step"] >= 12
+
+
+def _ports_args(n=3):
+    from distributedtensorflow_amd.cluster.launcher import free_ports
+    p = free_ports(n)
+    return [f"--ps_hosts=127.0.0.1:{p[0]}",
+            "--worker_hosts=" + ",".join(f"127.0.0.1:{x}" for x in p[1:])]
+
+
+def test_template_mnist_replica_sync(tmp_path, data_dir):
+    from distributedtensorflow_amd.cluster.launcher import launch_local
+    codes, logs = launch_local(os.path.join(ROOT, "templates", "mnist_replica.py"), 1, 2,
+                               str(tmp_path), _ports_args() + ["--train_steps=15",
+                                                               f"--data_dir={data_dir}",
+                                                               "--sync_replicas"],
+                               env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2"}, timeout_s=300)
+    text = {k: open(v).read() for k, v in logs.items()}
+    assert all(c == 0 for c in codes.values()), {k: t[-2000:] for k, t in text.items()}
+    for w in ("worker0", "worker1"):
+        assert "validation cross entropy" in text[w] and "Training elapsed time" in text[w]
+
+
+def test_template_between_graph_async_checkpoints(tmp_path, data_dir):
+    from distributedtensorflow_amd.cluster.launcher import launch_local
+    ck = str(tmp_path / "train_logs")
+    codes, logs = launch_local(os.path.join(ROOT, "templates", "between_graph_async_mnist.py"),
+                               1, 2, str(tmp_path), _ports_args() + [
+                                   "--train_steps=25", f"--data_dir={data_dir}",
+                                   f"--checkpoint_dir={ck}"],
+                               env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2"}, timeout_s=300)
+    text = {k: open(v).read() for k, v in logs.items()}
+    assert all(c == 0 for c in codes.values()), {k: t[-2000:] for k, t in text.items()}
+    from distributedtensorflow_amd.train import latest_checkpoint, load_variable
+    ckpt = latest_checkpoint(ck)
+    assert ckpt is not None
+    assert int(load_variable(ckpt, "global_step")) >= 25
+    assert load_variable(ckpt, "hid_w/Adagrad").shape == (784, 100)

@@ -22,9 +22,10 @@ def _inputs(n=4, s=64):
     return x.cuda().bfloat16(), y.cuda()
 
 
-def _grads(model, direct):
-    prev = native._DIRECT_GRAD
+def _grads(model, direct, fuse_res=True):
+    prev, prev_r = native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD
     native._DIRECT_GRAD = direct
+    native._FUSE_RESIDUAL_GRAD = fuse_res
     try:
         with OneDeviceStrategy("cuda").scope():
             opt = MomentumOptimizer(0.1, 0.9)
@@ -34,7 +35,7 @@ def _grads(model, direct):
             torch.cuda.synchronize()
             return loss.item(), opt.space.grad.clone()
     finally:
-        native._DIRECT_GRAD = prev
+        native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD = prev, prev_r
 
 
 def test_direct_grad_path_bit_identical():
@@ -122,3 +123,13 @@ def test_conv_epilogue_bn_stats_match_separate_pass(shape):
     torch.testing.assert_close(z1, z2, atol=2e-2, rtol=1e-2)
     torch.testing.assert_close(m1, m2, atol=1e-5, rtol=1e-4)
     torch.testing.assert_close(v1, v2, atol=1e-5, rtol=1e-4)
+
+
+def test_residual_grad_fusion_bit_identical():
+    """d(residual) accumulated in c1's dgrad epilogue == autograd's separate bf16 add."""
+    torch.manual_seed(0)
+    base = resnet50().cuda()
+    la, ga = _grads(copy.deepcopy(base), True, fuse_res=True)
+    lb, gb = _grads(copy.deepcopy(base), True, fuse_res=False)
+    assert la == lb
+    assert torch.equal(ga, gb)
