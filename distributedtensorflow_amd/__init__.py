@@ -13,7 +13,7 @@ with a tf.distribute-style strategy API.
 """
 __version__ = "0.1.0"
 
-from . import cluster, data, models, ops, optimizers, parallel, summary, train  # noqa: F401
+from . import cluster, data, models, ops, optimizers, parallel, profiler, summary, train  # noqa: F401
 from . import parallel as distribute  # tf.distribute-style alias
 from .summary import logger  # noqa: F401
 
@@ -24,5 +24,5 @@ for _n in ("AdamOptimizer", "AdagradOptimizer", "MomentumOptimizer", "GradientDe
 train.Server = cluster.Server
 train.ClusterSpec = cluster.ClusterSpec
 
-__all__ = ["cluster", "data", "models", "ops", "optimizers", "parallel", "distribute", "summary",
-           "train", "logger", "__version__"]
+__all__ = ["cluster", "data", "models", "ops", "optimizers", "parallel", "distribute", "profiler",
+           "summary", "train", "logger", "__version__"]

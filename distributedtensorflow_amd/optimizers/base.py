@@ -147,10 +147,13 @@ class Optimizer:
     def compute_gradients(self, loss, var_list=None):
         if self.space is None:
             self.build(var_list)
+        from .. import profiler
         self.space.zero_grad()
         self._reducer.begin_step()
-        loss.backward()
-        self._reducer.finish()
+        with profiler.maybe_phase("backward"):
+            loss.backward()
+        with profiler.maybe_phase("comm"):
+            self._reducer.finish()
         return [(v.grad, v) for v in self.space.order]
 
     def apply_gradients(self, grads_and_vars=None, global_step=None):
@@ -165,7 +168,9 @@ class Optimizer:
                 elif hasattr(global_step, "assign"):
                     global_step.assign(step)     # the PS's authoritative global step
             return step
-        self._apply(self._reducer.grad_scale())
+        from .. import profiler
+        with profiler.maybe_phase("optimizer"):
+            self._apply(self._reducer.grad_scale())
         if global_step is not None:
             gs.increment(global_step)
         return None

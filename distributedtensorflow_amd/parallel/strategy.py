@@ -267,6 +267,9 @@ def init_process_group_from_env(backend=None, timeout_s=600):
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
+    # RCCL watchdog: abort communicators whose collectives exceed the PG timeout instead of
+    # hanging (a dead peer then surfaces as an error the session layer can recover from)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     kw = {}
     if backend == "nccl":
         kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))

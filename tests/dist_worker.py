@@ -35,6 +35,8 @@ def main():
     from distributedtensorflow_amd.models import MnistCNN
     from distributedtensorflow_amd.parallel import (MirroredStrategy, MultiWorkerMirroredStrategy,
                                                     ParameterServerStrategy)
+    if kind == "heartbeat":
+        return heartbeat_probe(out)
     if kind == "mirrored":
         strat = MirroredStrategy(bucket_mb=float(kw.get("bucket_mb", 64)),
                                  first_bucket_mb=float(kw.get("bucket_mb", 4)),
@@ -59,10 +61,36 @@ def main():
             loss = ops.sparse_softmax_cross_entropy(model(x), y)
             opt.minimize(loss, global_step=gstep)
         mean_loss = float(strat.reduce(dtf.distribute.ReduceOp.MEAN, loss.detach()))
+        fps = dtf.distribute.check_replicas_consistent(opt)      # raises if replicas diverged
     torch.save({"state": {k: v.detach().clone() for k, v in model.state_dict().items()},
-                "global_step": gstep.value(), "world": world, "mean_loss": mean_loss},
+                "global_step": gstep.value(), "world": world, "mean_loss": mean_loss,
+                "fingerprints": fps},
                os.path.join(out, f"rank{rank}.pt"))
     strat.barrier()
+
+
+def heartbeat_probe(out):
+    """rank 1 stops beating (a hung / dead peer); rank 0 must notice it and no one else."""
+    import json
+    import time
+
+    from distributedtensorflow_amd.parallel import Heartbeat, init_process_group_from_env
+    init_process_group_from_env("gloo")
+    import torch.distributed as dist
+    rank = dist.get_rank()
+    hb = Heartbeat(interval_s=0.2, timeout_s=1.5).start()
+    dist.barrier()
+    if rank == 1:
+        hb.stop()                       # simulated failure: heartbeats stop, process stays
+        time.sleep(4.0)
+    else:
+        t0 = time.time()
+        while 1 not in hb.failed_peers and time.time() - t0 < 10:
+            time.sleep(0.1)
+        with open(os.path.join(out, "hb.json"), "w") as f:
+            json.dump({"failed": sorted(hb.failed_peers), "after_s": time.time() - t0}, f)
+        hb.stop()
+    dist.barrier()
 
 
 if __name__ == "__main__":

@@ -69,6 +69,7 @@ def _single_process(opt="momentum", steps=3):
 
 
 def _assert_replicas(results, ref, atol=2e-6, steps=3):
+    assert all(r["fingerprints"] == results[0]["fingerprints"] for r in results)
     for r in results[1:]:
         for k in ref:
             assert torch.equal(r["state"][k], results[0]["state"][k]), f"replicas diverged at {k}"
@@ -153,3 +154,18 @@ def test_between_graph_sync_replicas_two_ps(tmp_path, mnist_dir):
     # chief sees each global step at most once and the run ends at max_steps
     assert len(set(steps)) == len(steps) and steps[-1] >= 12
     assert "Close Parameter Server" in text["ps0"] and "Close Parameter Server" in text["ps1"]
+
+
+def test_heartbeat_detects_silent_peer(tmp_path):
+    port = free_ports(1)[0]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"),
+                                       "heartbeat", str(tmp_path)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = [p.communicate(timeout=120)[0].decode() for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    res = json.load(open(tmp_path / "hb.json"))
+    assert res["failed"] == [1] and res["after_s"] < 8
