@@ -41,7 +41,8 @@ def write_config(path, num_ps, num_workers):
 
 def launch_local(script, num_ps=1, num_workers=2, workdir=None, extra_args=(), env=None,
                  timeout_s=600, grace_s=30, gpus_per_host=None):
-    workdir = workdir or os.getcwd()
+    workdir = os.path.abspath(workdir or os.getcwd())
+    script = os.path.abspath(script)          # tasks run with cwd=workdir
     os.makedirs(workdir, exist_ok=True)
     cfg_path = os.path.join(workdir, "config.json")
     write_config(cfg_path, num_ps, num_workers)

@@ -71,16 +71,16 @@ def glorot_uniform_(t: torch.Tensor, fan_in: int, fan_out: int, gen=None):
 
 
 def truncated_normal_(t: torch.Tensor, stddev: float, gen=None):
-    """TF truncated_normal: resample beyond 2 stddev (here: clamp via rejection loop)."""
+    """TF truncated_normal: N(0, stddev) re-drawn outside +-2 stddev (vectorised inverse-CDF
+    sampling; O(numel), no rejection loop)."""
     with torch.no_grad():
-        t.normal_(0.0, stddev, generator=gen)
-        for _ in range(8):
-            bad = t.abs() > 2 * stddev
-            if not bool(bad.any()):
-                break
-            t[bad] = torch.empty(int(bad.sum()), dtype=t.dtype, device=t.device).normal_(
-                0.0, stddev, generator=gen)
-        t.clamp_(-2 * stddev, 2 * stddev)
+        if gen is None:
+            torch.nn.init.trunc_normal_(t, 0.0, stddev, -2 * stddev, 2 * stddev)
+        else:
+            lo, hi = 0.5 * (1 + math.erf(-2 / math.sqrt(2))), 0.5 * (1 + math.erf(2 / math.sqrt(2)))
+            u = torch.empty_like(t).uniform_(lo, hi, generator=gen)
+            t.copy_(torch.erfinv(2 * u - 1) * math.sqrt(2) * stddev)
+            t.clamp_(-2 * stddev, 2 * stddev)
     return t
 
 
