@@ -30,7 +30,8 @@ void dtf_bn_fwd_finalize(const float*, long, int, const float*, const float*, fl
 void dtf_bn_fwd_finalize_g(const float*, int, long, int, const float*, const float*, float*,
                            float*, float, float, float*, float*, float*, float*, hipStream_t);
 long dtf_bn_workspace_floats_g(int, int);
-int dtf_conv_stats_rows(long, int);
+int dtf_conv_stats_rows(long, int, int, int);
+void dtf_conv_set_dma_mode(int);
 void dtf_bn_infer_finalize(int, const float*, const float*, const float*, const float*, float,
                            float*, float*, float*, float*, hipStream_t);
 void dtf_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, const float*, const float*, long, int,
@@ -116,7 +117,9 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("bn_partial_blocks", &dtf_bn_partial_blocks);
   m.def("bn_workspace_floats", &dtf_bn_workspace_floats);
   m.def("bn_workspace_floats_g", &dtf_bn_workspace_floats_g);
-  m.def("conv_stats_rows", &dtf_conv_stats_rows);
+  m.def("conv_stats_rows", &dtf_conv_stats_rows, py::arg("M"), py::arg("Kout"), py::arg("C") = 0,
+        py::arg("taps") = 1);
+  m.def("conv_set_dma_mode", &dtf_conv_set_dma_mode);
   m.def("bn_fwd_finalize_g", [](uintptr_t part, int G, long M, int C, uintptr_t gamma,
                                 uintptr_t beta, uintptr_t rm, uintptr_t rv, float mom, float eps,
                                 uintptr_t mean, uintptr_t invstd, uintptr_t scale, uintptr_t shift,

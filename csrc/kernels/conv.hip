@@ -329,14 +329,262 @@ void launch_cfg(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
                      lds, st, X, Wt, Y, g, taps, stats);
 }
 
+// ---------------------------------------------------------------------------------------------
+// 8-wave LDS-DMA variant (GATHER 0, BK 64): 256 x 128 tile, waves 4 (M) x 2 (N) of 64 x 64,
+// THREE LDS stages filled by `buffer_load_dwordx4 ... lds` (no staging VGPRs, no ds_write pass),
+// loads issued two K-steps ahead (cdna_hip_programming.md §5 "glds vs register staging", 3-buffer
+// row: counted vmcnt + raw s_barrier, never __syncthreads() inside the loop).  One block per CU
+// (144 KB of LDS), 2 waves per SIMD.  The DMA writes each wave-instruction's 64 x 16 B
+// lane-linearly, so the XOR chunk swizzle of the fragment reads is applied on the SOURCE side:
+// LDS slot s of row r receives source chunk s ^ ((r >> 1) & 7).  Padding taps get an
+// out-of-range buffer offset -> the hardware range check delivers zeros.
+constexpr int kDmaThreads = 512;
+constexpr int kDmaBM = 256, kDmaBN = 128, kDmaBK = 64;
+constexpr int kDmaA = kDmaBM * kDmaBK;                    // A elements per stage
+constexpr int kDmaStage = (kDmaBM + kDmaBN) * kDmaBK;     // 24576 bf16 = 48 KB
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+
+// Buffer descriptor as a plain SGPR quad (for inline asm): base, stride 0, num_records = bytes.
+DTF_DEV i32x4_t rsrc_quad(const void* p, uint32_t bytes) {
+  const unsigned long long b = (unsigned long long)p;
+  return (i32x4_t){__builtin_amdgcn_readfirstlane((int)(uint32_t)b),
+                   __builtin_amdgcn_readfirstlane((int)((b >> 32) & 0xFFFFu)), (int)bytes,
+                   0x00020000};
+}
+DTF_DEV uint32_t lds_addr(const bf16_t* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(const lds_void_t*)p);
+}
+// One 1-KB LDS-DMA wave-instruction: lane l's 16 bytes at `voff` land at LDS byte lds + 16 l.
+// Issued as inline asm on purpose: the compiler then does not treat it as an LDS store and does
+// not insert its own (over-conservative) vmcnt waits in front of the fragment reads -- the
+// kernel waits with explicit counted vmcnt instead.  M0 is saved and restored around it.
+DTF_DEV void dma16(const i32x4_t& r, uint32_t lds, uint32_t voff) {
+  uint32_t save;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(save) : "s"(lds), "v"(voff), "s"(r) : "memory");
+}
+#define DTF_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+DTF_DEV void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__global__ void __launch_bounds__(kDmaThreads, 1)
+conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+                      bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
+                      float* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[3 * kDmaStage];
+  bf16_t* const s0 = lds;
+  bf16_t* const s1 = lds + kDmaStage;
+  bf16_t* const s2 = lds + 2 * kDmaStage;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int M = g.N * g.P * g.Q;
+  const int tiles_n = (g.Kout + kDmaBN - 1) / kDmaBN;
+  const int tiles_m = (M + kDmaBM - 1) / kDmaBM;
+  const int bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * kDmaBM, n0 = tn * kDmaBN;
+  const int nk = taps.n * g.C / kDmaBK;
+  const i32x4_t rx = rsrc_quad(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
+  const i32x4_t rw = rsrc_quad(Wt, (uint32_t)g.Kout * g.Kpad * 2u);
+  const uint32_t lds0 = lds_addr(lds);
+
+  // this wave fills row-groups (8 rows x 128 B = 1 KB) wave + 8j of each stage's 48 groups:
+  // j = 0..3 -> A rows, j = 4, 5 -> B rows.  Lane -> (row lrow of the group, LDS slot).
+  const int lrow = lane >> 3, slot = lane & 7;
+  int a_pix[4], a_h[4], a_w[4], a_ch[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * (wave + 8 * j) + lrow;
+    const int m = m0 + row;
+    const bool ok = m < M;
+    const int mm = ok ? m : 0;
+    const int q = mm % g.Q;
+    const int t = mm / g.Q;
+    const int p = t % g.P;
+    const int n = t / g.P;
+    a_pix[j] = n * g.H * g.W;
+    a_h[j] = ok ? p * g.sh : -(1 << 24);
+    a_w[j] = q * g.sw;
+    a_ch[j] = (slot ^ ((row >> 1) & 7)) * 8;
+  }
+  int b_off[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (wave + 8 * j) + lrow;
+    const int nrow = n0 + row;
+    b_off[j] = nrow < g.Kout ? nrow * g.Kpad + (slot ^ ((row >> 1) & 7)) * 8 : -1;
+  }
+
+  // K-step kt >= nk is issued too, with every lane out of range (no memory traffic): each step
+  // then has exactly 6 DMAs per wave in flight behind it, so the wait count is a constant
+  auto issue = [&](int kt, int stage) {
+    const bool live = kt < nk;
+    const int k0 = (live ? kt : 0) * kDmaBK;
+    const int t = __builtin_amdgcn_readfirstlane(k0 / g.C);
+    const int c0 = k0 - t * g.C;
+    const int dh = taps.dh[t], dw = taps.dw[t];
+    const uint32_t base = lds0 + (uint32_t)(stage * kDmaStage + wave * 512) * 2u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int h = a_h[j] + dh, w = a_w[j] + dw;
+      const bool ok = live && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const uint32_t off = ok ? (uint32_t)(((a_pix[j] + h * g.W + w) * g.C + c0 + a_ch[j]) * 2) : kOOB;
+      dma16(rx, base + j * 8 * 1024, off);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t off = (live && b_off[j] >= 0) ? (uint32_t)((b_off[j] + k0) * 2) : kOOB;
+      dma16(rw, base + kDmaA * 2 + j * 8 * 1024, off);
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fq = lane >> 4;
+  auto compute = [&](const bf16_t* sa) {
+    const bf16_t* sb = sa + kDmaA;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[4], bfr[4];
+      const int ch = ks * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + frow;
+        af[i] = *reinterpret_cast<const bf16x8_t*>(sa + r * kDmaBK + swz_chunk<kDmaBK>(r, ch) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wn * 64 + j * 16 + frow;
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sb + r * kDmaBK + swz_chunk<kDmaBK>(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  // step k: own DMAs of step k done (step k+1's 6 may still fly) -> barrier (every wave's step-k
+  // data landed AND every wave finished step k-1, freeing its stage) -> issue k+2 into that
+  // stage -> MFMAs on step k.
+  issue(0, 0);
+  issue(1, 1);
+  int cur = 0, nxt = 2;
+  for (int kt = 0; kt < nk; ++kt) {
+    DTF_WAIT_VM(6);
+    raw_barrier();
+    issue(kt + 2, nxt);
+    compute(lds + cur * kDmaStage);
+    cur = cur == 2 ? 0 : cur + 1;
+    nxt = nxt == 2 ? 0 : nxt + 1;
+  }
+
+  // ---- epilogue (as conv_igemm_kernel): rows 0..127 of the tile staged in s0, 128..255 in s1
+  DTF_WAIT_VM(0);
+  __syncthreads();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr int LDC = kDmaBN + 8;
+  {
+    bf16_t* st = wm < 2 ? s0 : s1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = (wm & 1) * 64 + i * 16 + fq * 4 + r;
+          const int col = wn * 64 + j * 16 + frow;
+          st[row * LDC + col] = f2bf(acc[i][j][r]);
+        }
+  }
+  __syncthreads();
+  constexpr int OCPR = kDmaBN / 8;
+  constexpr int OROWS = kDmaThreads / OCPR;
+  const int oc = tid % OCPR;
+  const bool col_ok = n0 + oc * 8 < g.Kout;
+  for (int r = tid / OCPR; r < kDmaBM; r += OROWS) {
+    const int m = m0 + r;
+    if (m >= M || !col_ok) continue;
+    const int q = m % g.Q;
+    const int t = m / g.Q;
+    const int p = t % g.P;
+    const int n = t / g.P;
+    const int ho = p * g.osh + g.oh0, wo = q * g.osw + g.ow0;
+    const long off = (((long)n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8;
+    const bf16_t* st = r < 128 ? s0 : s1;
+    uint4 v = *reinterpret_cast<const uint4*>(st + (r & 127) * LDC + oc * 8);
+    if (g.acc) {
+      float a[8], b[8];
+      unpack8(v, a);
+      unpack8(*reinterpret_cast<const uint4*>(Y + off), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+      v = pack8(a);
+    }
+    *reinterpret_cast<uint4*>(Y + off) = v;
+  }
+  if (stats) {   // fused BN partial sums, same contract as conv_igemm_kernel (row tm of the slab)
+    constexpr int GROUPS = kDmaThreads / kDmaBN;     // 4 groups of 64 rows
+    constexpr int RPG = kDmaBM / GROUPS;
+    float* red = reinterpret_cast<float*>(s2);
+    const int col = tid % kDmaBN, grp = tid / kDmaBN;
+    const bf16_t* st = grp < 2 ? s0 : s1;
+    float a1 = 0.f, a2 = 0.f;
+    const int rend = min(RPG * (grp + 1), M - m0);
+    for (int r = RPG * grp; r < rend; ++r) {
+      const float v = bf2f(st[(r & 127) * LDC + col]);
+      a1 += v;
+      a2 += v * v;
+    }
+    red[(grp * 2 + 0) * kDmaBN + col] = a1;
+    red[(grp * 2 + 1) * kDmaBN + col] = a2;
+    __syncthreads();
+    if (grp == 0 && n0 + col < g.Kout) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) { a += red[(k * 2 + 0) * kDmaBN + col]; b += red[(k * 2 + 1) * kDmaBN + col]; }
+      stats[((long)tm * 2 + 0) * g.Kout + n0 + col] = a;
+      stats[((long)tm * 2 + 1) * g.Kout + n0 + col] = b;
+    }
+  }
+}
+
 }  // namespace
 
 // Host launcher.  Caller guarantees: Kout % 8 == 0, Kpad % BK == 0 (filter rows zero-padded),
 // 16-B aligned tensors, taps.n <= DTF_MAX_TAPS.
 // Rows of the BN-statistics slab a forward launch writes (= its M tiles), for the caller's
 // workspace sizing; must mirror the tile choice in dtf_conv_igemm.
-int dtf_conv_stats_rows(long M, int Kout) {
-  const int BM = Kout <= 64 ? 256 : 128;
+// -1: automatic, 0: never the DMA kernel, 1: whenever legal (benchmarks / tests)
+static int g_conv_dma_mode = -1;
+void dtf_conv_set_dma_mode(int mode) { g_conv_dma_mode = mode; }
+
+// The 8-wave DMA kernel needs C % 64 == 0 (one tap per K-step) and 128-wide output tiles.
+// Measured (tools/conv_bench.py, batch 256, forced on vs off): it wins only on multi-tap convs
+// with C >= 256 (the 3x3 convs of stages 2-3: 1.05-1.11x); on 1x1 convs and C = 128 3x3 convs
+// the 2-blocks-per-CU register-staged kernel is 5-28 % faster, so auto mode picks it there.
+static bool use_dma_kernel(long M, int Kout, int C, int taps, int bk) {
+  if (g_conv_dma_mode == 0 || bk != 64 || C % 64 != 0 || Kout % 128 != 0) return false;
+  if (g_conv_dma_mode == 1) return true;
+  (void)M;
+  return taps > 1 && C >= 256;
+}
+
+int dtf_conv_stats_rows(long M, int Kout, int C, int taps) {
+  const int BM = use_dma_kernel(M, Kout, C, taps, 64) ? kDmaBM : (Kout <= 64 ? 256 : 128);
   return (int)((M + BM - 1) / BM);
 }
 
@@ -358,6 +606,12 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
       if (narrow) launch_cfg<4, 1, 32, 1>(X, Wt, Y, g, taps, stats, st);
       else launch_cfg<2, 2, 32, 1>(X, Wt, Y, g, taps, stats, st);
     }
+    return;
+  }
+  if (use_dma_kernel((long)m, g.Kout, g.C, taps.n, bk) && g.Kpad % 64 == 0) {
+    const long tiles = (((long)m + kDmaBM - 1) / kDmaBM) * (g.Kout / kDmaBN);
+    hipLaunchKernelGGL(conv_igemm_dma_kernel, dim3((unsigned)tiles), dim3(kDmaThreads), 0, st,
+                       X, Wt, Y, g, taps, stats);
     return;
   }
   if (bk == 64 && g.C % 64 == 0) {

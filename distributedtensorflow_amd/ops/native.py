@@ -267,7 +267,7 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False):
         return _Conv2d.apply(x, w, stride, padding, None)
     n, h, wd, c, P, Q, sh, sw, pt, pl = _conv_geom_fwd(x, K, R, S, stride, padding)
     M = n * P * Q
-    G = _K.conv_stats_rows(M, K)
+    G = _K.conv_stats_rows(M, K, c, R * S)
     part = torch.empty(_K.bn_workspace_floats_g(G, K), device=x.device, dtype=torch.float32)
     y = _Conv2d.apply(x, w, stride, padding, part)
     y._dtf_bn_part = (part, G, M, K)

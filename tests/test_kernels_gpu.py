@@ -67,6 +67,48 @@ def test_conv_fwd_dgrad_wgrad(case):
     assert _rel(wn.grad, wr.grad) < 2e-2, _rel(wn.grad, wr.grad)
 
 
+DMA_CASES = [
+    # shapes legal for the 8-wave LDS-DMA conv kernel (C % 64 == 0, Kout % 128 == 0) in fwd
+    # and/or dgrad; forced on with conv_set_dma_mode(1) and compared BIT-exactly with the
+    # register-staged kernel (same MFMA accumulation order per output element)
+    (2, 56, 56, 64, 256, 1, 1, 0),
+    (2, 56, 56, 128, 128, 3, 2, 1),
+    (2, 56, 56, 256, 512, 1, 2, 0),
+    (2, 14, 14, 1024, 256, 1, 1, 0),
+    (2, 7, 7, 512, 512, 3, 1, 1),
+    (3, 9, 11, 128, 384, 3, 1, 1),     # M not a multiple of 256, three N tiles, padding taps
+]
+
+
+@pytest.mark.parametrize("case", DMA_CASES)
+def test_conv_dma_kernel_bit_identical(case):
+    N, H, W, C, K, R, stride, pad = case
+    nat = _native()
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K, R, R, C, device=dev) / (R * R * C) ** 0.5)
+    g = None
+    outs = []
+    try:
+        for mode in (0, 1):
+            nat._K.conv_set_dma_mode(mode)
+            xn = x.clone().requires_grad_(True)
+            wn = w.clone().requires_grad_(True)
+            yn = nat.conv2d(xn, wn, stride, pad)
+            if g is None:
+                g = torch.randn(yn.shape, device=dev).to(torch.bfloat16)
+            yn.backward(g)
+            outs.append((yn.detach(), xn.grad, wn.grad))
+    finally:
+        nat._K.conv_set_dma_mode(-1)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    ref = _ref()
+    xr = x.float().requires_grad_(True)
+    yr = ref.conv2d(xr, w.detach().to(torch.bfloat16).float(), stride, pad)
+    assert _rel(outs[1][0], yr) < 1e-2
+
+
 @pytest.mark.parametrize("case", [(2, 28, 28, 1, 32, 5, 1, "same"), (2, 64, 64, 3, 64, 7, 2, 3)])
 def test_conv_element_gather_paths(case):
     """The per-element gather kernels (fwd GATHER=1, wgrad GENERIC) on unpadded C=1 / C=3."""

@@ -101,7 +101,7 @@ def test_resnet50_train_first_stage_matches_reference():
 
 
 @pytest.mark.parametrize("shape", [(4, 56, 56, 64, 64, 1), (4, 28, 28, 128, 256, 3),
-                                   (3, 9, 11, 64, 72, 3)])
+                                   (3, 9, 11, 64, 72, 3), (8, 14, 14, 256, 256, 3)])
 def test_conv_epilogue_bn_stats_match_separate_pass(shape):
     """conv2d(bn_stats=True) + batch_norm (statistics from the conv epilogue) == the separate
     statistics kernel path: outputs, batch stats and moving averages."""

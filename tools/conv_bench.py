@@ -59,7 +59,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None, help="comma list of layer names to run")
     ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
+    ap.add_argument("--dma", type=int, default=-1,
+                    help="conv kernel choice: -1 auto, 0 register-staged only, 1 LDS-DMA when legal")
     args = ap.parse_args()
+    native._K.conv_set_dma_mode(args.dma)
     only = set(args.only.split(",")) if args.only else None
     kinds = set(args.kinds.split(","))
     B = args.batch
