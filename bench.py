@@ -112,6 +112,45 @@ def build_bert(args, dev):
     return step, strategy
 
 
+def build_torch_bert(args, dev):
+    """Stock comparator for the BERT config: HuggingFace BertForPreTraining-style MLM (random init,
+    SDPA attention, bf16 autocast), fused torch AdamW (torch has no LAMB), DDP when distributed.
+    The MLM head runs on the gathered masked positions only, exactly like the dtf model."""
+    from transformers import BertConfig, BertForMaskedLM
+    cfg = BertConfig(vocab_size=30522, hidden_size=768, num_hidden_layers=12,
+                     num_attention_heads=12, intermediate_size=3072, max_position_embeddings=512,
+                     attn_implementation="sdpa")
+    hf = BertForMaskedLM(cfg).to(dev)
+
+    class MaskedOnly(torch.nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.m = m
+
+        def forward(self, ids, seg, mask, pos):
+            h = self.m.bert(input_ids=ids, token_type_ids=seg, attention_mask=mask).last_hidden_state
+            hm = torch.gather(h, 1, pos.unsqueeze(-1).expand(-1, -1, h.shape[-1]))
+            return self.m.cls(hm)
+
+    model = MaskedOnly(hf).train()
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
+                                                          bucket_cap_mb=args.bucket_mb)
+    opt = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=0.01, fused=True)
+
+    def step(batch):
+        ids, seg, mask, pos, lab, _w = batch
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = model(ids, seg, mask, pos)
+            loss = torch.nn.functional.cross_entropy(logits.float().flatten(0, 1), lab.flatten())
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    return step, None
+
+
 def build_torch(args, dev):
     from distributedtensorflow_amd.utils.torch_baseline import TorchResNet50
     model = TorchResNet50().to(dev).to(memory_format=torch.channels_last)
@@ -155,7 +194,7 @@ def main():
         from distributedtensorflow_amd.data.synthetic import SyntheticMLM
         if args.lr == 0.1 and "--lr" not in sys.argv:
             args.lr = 1e-3
-        bert_step, _ = build_bert(args, dev)
+        bert_step, _ = (build_bert if args.impl == "dtf" else build_torch_bert)(args, dev)
         d = next(iter(SyntheticMLM(B, args.seq_len, max_predictions=args.max_predictions,
                                    device=dev, seed=1234 + rank)))
         batch = (d["input_ids"], d["segment_ids"], d["input_mask"], d["masked_lm_positions"],
@@ -210,7 +249,8 @@ def main():
             "data": "synthetic (random token ids, 15% masked positions; random-init weights)",
             "config": {"model": "bert_base", "global_batch": B * world, "per_gpu_batch": B,
                        "seq_len": args.seq_len, "max_predictions": args.max_predictions,
-                       "parallelism": f"dp{world}", "optimizer": "lamb+wd0.01",
+                       "parallelism": f"dp{world}", "impl": args.impl,
+                       "optimizer": "lamb+wd0.01" if args.impl == "dtf" else "torch fused AdamW+wd0.01",
                        "dropout": 0.1, "tflops_per_gpu": round(tps * fpt / world / 1e12, 1),
                        "final_loss": round(final_loss, 4)},
         }
