@@ -250,9 +250,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs g) {
 // (A single pass of one thread per column serialised 512 dependent loads on 3 blocks: 130 us
 // per LayerNorm backward at BERT-base shape, 30 % of the step.)
 constexpr int kColSplits = 32;
+struct ColSumOut { float* p[3]; };
+
+// blockIdx.z = quantity q: its partial rows start at part + q * region, its level-1 workspace
+// right after them (P rows in)
 __global__ void __launch_bounds__(256)
-col_sum_split_kernel(const float* __restrict__ part, int P, int N, float* __restrict__ ws, int R) {
+col_sum_split_kernel(const float* __restrict__ part, long region, int P, int N, int R) {
   __shared__ float4 red[4][64];
+  const float* pq = part + blockIdx.z * region;
+  float* ws = const_cast<float*>(pq) + (long)P * N;
   const int c4 = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rg = threadIdx.x >> 6;
   const int r0 = blockIdx.y * R;
@@ -261,7 +267,7 @@ col_sum_split_kernel(const float* __restrict__ part, int P, int N, float* __rest
   if (c4 * 4 < N) {
 #pragma unroll 4
     for (int r = r0 + rg; r < r1; r += 4) {
-      const float4 v = reinterpret_cast<const float4*>(part + (long)r * N)[c4];
+      const float4 v = reinterpret_cast<const float4*>(pq + (long)r * N)[c4];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
   }
@@ -278,30 +284,41 @@ col_sum_split_kernel(const float* __restrict__ part, int P, int N, float* __rest
   }
 }
 
+// level 2: 64 float4 columns x 4 slice groups per block, fixed-order combine
 __global__ void __launch_bounds__(256)
-col_sum_final_kernel(const float* __restrict__ ws, int S, int N, float* __restrict__ out, int accumulate) {
-  const int c4 = blockIdx.x * 256 + threadIdx.x;
-  if (c4 * 4 >= N) return;
-  float4 t = reinterpret_cast<const float4*>(ws)[c4];
-  for (int k = 1; k < S; ++k) {
-    const float4 v = reinterpret_cast<const float4*>(ws + (long)k * N)[c4];
-    t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+col_sum_final_kernel(const float* __restrict__ part, long region, int P, int S, int N, ColSumOut outs) {
+  __shared__ float4 red[4][64];
+  const float* ws = part + blockIdx.z * region + (long)P * N;
+  const int c4 = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c4 * 4 < N)
+    for (int k = rg; k < S; k += 4) {
+      const float4 v = reinterpret_cast<const float4*>(ws + (long)k * N)[c4];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+  red[rg][threadIdx.x & 63] = t;
+  __syncthreads();
+  if (rg == 0 && c4 * 4 < N) {
+    float4 u = red[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 v = red[k][threadIdx.x];
+      u.x += v.x; u.y += v.y; u.z += v.z; u.w += v.w;
+    }
+    reinterpret_cast<float4*>(outs.p[blockIdx.z])[c4] = u;
   }
-  if (accumulate) {
-    const float4 o = reinterpret_cast<const float4*>(out)[c4];
-    t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
-  }
-  reinterpret_cast<float4*>(out)[c4] = t;
 }
 
-// part: [P][N] partial rows followed by kColSplits rows of level-1 workspace.
-void col_sum(const float* part, int P, int N, float* out, hipStream_t st) {
-  float* ws = const_cast<float*>(part) + (long)P * N;
+// part: nq quantities, each `region` floats apart: [P][N] partial rows then kColSplits rows of
+// workspace.  Two launches regardless of nq.
+void col_sum(const float* part, long region, int nq, int P, int N, ColSumOut outs, hipStream_t st) {
   int S = P / 16;
   S = S < 1 ? 1 : (S > kColSplits ? kColSplits : S);
   const int R = (P + S - 1) / S;
-  hipLaunchKernelGGL(col_sum_split_kernel, dim3((N / 4 + 63) / 64, S), dim3(256), 0, st, part, P, N, ws, R);
-  hipLaunchKernelGGL(col_sum_final_kernel, dim3((N / 4 + 255) / 256), dim3(256), 0, st, ws, S, N, out, 0);
+  const int gx = (N / 4 + 63) / 64;
+  hipLaunchKernelGGL(col_sum_split_kernel, dim3(gx, S, nq), dim3(256), 0, st, part, region, P, N, R);
+  hipLaunchKernelGGL(col_sum_final_kernel, dim3(gx, 1, nq), dim3(256), 0, st, part, region, P, S, N, outs);
 }
 
 // ----------------------------------------------------------------------------- bias + GELU
@@ -781,9 +798,7 @@ void dtf_ln_bwd(const bf16_t* dy, const bf16_t* s, const float* mean, const floa
     case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, st, g); break;
     default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, block, 0, st, g); break;
   }
-  col_sum(pg, nblk, H, dgamma, st);
-  col_sum(pb, nblk, H, dbeta, st);
-  if (dbias) col_sum(pbias, nblk, H, dbias, st);
+  col_sum(part, region, dbias ? 3 : 2, nblk, H, ColSumOut{{dgamma, dbeta, dbias}}, st);
 }
 
 void dtf_bias_gelu_fwd(const bf16_t* a, const float* bias, bf16_t* y, long M, int N,
@@ -803,7 +818,7 @@ void dtf_bias_gelu_bwd(const bf16_t* dy, const bf16_t* a, const float* bias, bf1
   const int nblk = bias_gelu_rows(M);
   hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3(nblk), dim3(256), 0, st, dy, a, bias, da,
                      dbias ? part : nullptr, M, N, 16);
-  if (dbias) col_sum(part, nblk, N, dbias, st);
+  if (dbias) col_sum(part, 0, 1, nblk, N, ColSumOut{{dbias, nullptr, nullptr}}, st);
 }
 
 static AttnGeom attn_geom(int B, int S, int H, float scale, float p, uint32_t seed) {

@@ -453,9 +453,76 @@ def global_avg_pool(x):
 
 # ----------------------------------------------------------------------------- dense (library GEMM)
 
+def _wgrad_splits(T, o, i):
+    """Token-axis split count for the dW = dY^T X GEMM: hipBLASLt tiles only the small o x i
+    output (36-144 tiles of 128 x 128 at BERT-base shapes) and leaves most CUs idle, so the
+    reduction is split into S batched slices and their fp32 partials summed.  Measured on MI355X
+    (tools/dense_wgrad_probe.py, T = 16384): 1.6-2.1x over the single GEMM."""
+    tiles = -(-o // 128) * -(-i // 128)
+    best = 1
+    for s in (2, 4, 8):
+        if T % s == 0 and T // s >= 1024 and tiles * s <= 1024:
+            best = s
+    return best
+
+
+class _Dense(torch.autograd.Function):
+    """y = x @ W^T (+ b) on hipBLASLt with the bf16 weight shadow; backward produces dW and db in
+    fp32 straight into the optimizer's flat gradient buffer (no bf16 dW, no cast/add kernels)."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, wb, b):
+        ctx.save_for_backward(x, wb)
+        ctx.w_param, ctx.b_param = w_master, b
+        ctx.has_b = b is not None
+        return torch.nn.functional.linear(x, wb, None if b is None else b.to(x.dtype))
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        o, i = wb.shape
+        x2, dy2 = x.reshape(-1, i), dy.reshape(-1, o)
+        T = x2.shape[0]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ wb).reshape(x.shape)
+        if ctx.needs_input_grad[1]:
+            target = _direct_grad(ctx.w_param)
+            S = _wgrad_splits(T, o, i)
+            if S == 1:
+                if target is not None:
+                    torch.addmm(target, dy2.t(), x2, out_dtype=torch.float32, out=target)
+                else:
+                    dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+            else:
+                part = torch.bmm(dy2.view(S, T // S, o).transpose(1, 2), x2.view(S, T // S, i),
+                                 out_dtype=torch.float32).sum(0)
+                if target is not None:
+                    target.add_(part)
+                else:
+                    dw = part
+            if target is not None:
+                _grad_ready(ctx.w_param)
+            elif ctx.w_param.dtype != torch.float32:
+                dw = dw.to(ctx.w_param.dtype)
+        if ctx.has_b and ctx.needs_input_grad[3]:
+            tb = _direct_grad(ctx.b_param)
+            s = torch.sum(dy2, 0, dtype=torch.float32)
+            if tb is not None:
+                tb.add_(s)
+                _grad_ready(ctx.b_param)
+            else:
+                db = s.to(ctx.b_param.dtype)
+        ctx.w_param = ctx.b_param = None
+        return dx, dw, None, db
+
+
 def dense(x, w, b=None, relu=False):
-    """Plain GEMM -> hipBLASLt via torch.matmul (a *library* GEMM per the design rules);
-    the bias and ReLU stay fused in the same addmm epilogue."""
+    """Plain GEMM -> hipBLASLt (a *library* GEMM per the design rules); the bias stays fused in
+    the GEMM epilogue.  Trainable fp32 masters go through :class:`_Dense` (fp32 dW/db)."""
+    if w.dtype == torch.float32 and x.dtype == _BF16 and w.requires_grad and x.is_cuda:
+        y = _Dense.apply(x, w, _bf16_weight(w), b)
+        return torch.relu(y) if relu else y
     wb = _bf16_weight(w) if w.dtype != x.dtype else w
     if w.requires_grad and wb is not w:
         wb = _MasterCast.apply(w, wb)

@@ -203,3 +203,31 @@ def test_softmax_xent(B, V):
     l2.backward()
     assert abs(l1.item() - l2.item()) < 1e-4 * max(1, abs(l1.item()))
     assert _rel(ln.grad, lr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("T,o,i", [(128, 1024, 3136), (16384, 768, 768), (8192, 3072, 768)])
+@pytest.mark.parametrize("direct", [False, True])
+def test_dense_fp32_weight_grads(T, o, i, direct):
+    """ops.dense backward: dW (split-K batched hipBLASLt, fp32) and db vs an fp32 reference; with
+    ``direct`` the gradients land in pre-existing fp32 .grad buffers flagged as flat."""
+    nat = _native()
+    torch.manual_seed(0)
+    x = torch.randn(T, i, device=dev).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(o, i, device=dev) / i ** 0.5).requires_grad_(True)
+    b = torch.randn(o, device=dev).requires_grad_(True)
+    if direct:
+        w.grad = torch.full_like(w, 0.5)
+        b.grad = torch.full_like(b, 0.25)
+        w._dtf_flat = b._dtf_flat = True
+    y = nat.dense(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float()
+    wr = w.detach().to(torch.bfloat16).float()
+    yr = xr @ wr.t() + b.detach().to(torch.bfloat16).float()
+    gf = g.float()
+    assert _rel(y, yr) < 1e-2
+    off_w, off_b = (0.5, 0.25) if direct else (0.0, 0.0)
+    assert _rel(w.grad - off_w, gf.t() @ xr) < 1e-3
+    assert _rel(b.grad - off_b, gf.sum(0)) < 1e-3
+    assert _rel(x.grad, gf @ wr) < 1e-2
