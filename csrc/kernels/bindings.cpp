@@ -81,6 +81,9 @@ void dtf_ln_bwd(const bf16_t*, const bf16_t*, const float*, const float*, const 
                 uint32_t, hipStream_t);
 void dtf_bias_gelu_fwd(const bf16_t*, const float*, bf16_t*, long, int, hipStream_t);
 int dtf_bias_gelu_bwd_blocks(int);
+int dtf_bf16_col_sum_ws_floats(int);
+void dtf_bf16_col_sum(const bf16_t*, int, int, float*, float*, int, hipStream_t);
+void dtf_slab_reduce(const float*, float*, long, int, int, hipStream_t);
 void dtf_bias_gelu_bwd(const bf16_t*, const bf16_t*, const float*, bf16_t*, float*, float*, int,
                        int, hipStream_t);
 void dtf_attn_fwd(const bf16_t*, const float*, bf16_t*, float*, int, int, int, float, float,
@@ -312,6 +315,15 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("bias_gelu_fwd");
   });
   m.def("bias_gelu_bwd_blocks", &dtf_bias_gelu_bwd_blocks);
+  m.def("bf16_col_sum_ws_floats", &dtf_bf16_col_sum_ws_floats);
+  m.def("bf16_col_sum", [](uintptr_t x, int T, int N, uintptr_t ws, uintptr_t out, int accumulate,
+                           uintptr_t stream) {
+    dtf_bf16_col_sum(P<const bf16_t>(x), T, N, P<float>(ws), P<float>(out), accumulate, S(stream));
+  });
+  m.def("slab_reduce", [](uintptr_t ws, uintptr_t out, long n, int nsplit, int accumulate,
+                          uintptr_t stream) {
+    dtf_slab_reduce(P<const float>(ws), P<float>(out), n, nsplit, accumulate, S(stream));
+  });
   m.def("bias_gelu_bwd", [](uintptr_t dy, uintptr_t a, uintptr_t bias, uintptr_t da,
                             uintptr_t part, uintptr_t dbias, int M, int N, uintptr_t st) {
     dtf_bias_gelu_bwd(P<const bf16_t>(dy), P<const bf16_t>(a), P<const float>(bias),

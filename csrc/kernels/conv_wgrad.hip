@@ -327,3 +327,13 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
                        dW, g.slab, g.slab, nsplit, accumulate);
   }
 }
+
+// Deterministic sum of `nsplit` contiguous fp32 slabs of n floats (n % 4 == 0) into `out`
+// (+= when accumulate): the split-K combine of the dense-layer weight-gradient GEMMs.
+void dtf_slab_reduce(const float* ws, float* out, long n, int nsplit, int accumulate, hipStream_t st) {
+  if (n % 4) throw std::runtime_error("slab_reduce: n % 4 != 0");
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, ws, out,
+                     n, n, nsplit, accumulate);
+}
+

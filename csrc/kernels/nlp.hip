@@ -286,7 +286,8 @@ col_sum_split_kernel(const float* __restrict__ part, long region, int P, int N, 
 
 // level 2: 64 float4 columns x 4 slice groups per block, fixed-order combine
 __global__ void __launch_bounds__(256)
-col_sum_final_kernel(const float* __restrict__ part, long region, int P, int S, int N, ColSumOut outs) {
+col_sum_final_kernel(const float* __restrict__ part, long region, int P, int S, int N, ColSumOut outs,
+                     int accumulate) {
   __shared__ float4 red[4][64];
   const float* ws = part + blockIdx.z * region + (long)P * N;
   const int c4 = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -306,7 +307,9 @@ col_sum_final_kernel(const float* __restrict__ part, long region, int P, int S, 
       const float4 v = red[k][threadIdx.x];
       u.x += v.x; u.y += v.y; u.z += v.z; u.w += v.w;
     }
-    reinterpret_cast<float4*>(outs.p[blockIdx.z])[c4] = u;
+    float4* o = reinterpret_cast<float4*>(outs.p[blockIdx.z]) + c4;
+    if (accumulate) { const float4 v = *o; u.x += v.x; u.y += v.y; u.z += v.z; u.w += v.w; }
+    *o = u;
   }
 }
 
@@ -318,28 +321,83 @@ void col_sum(const float* part, long region, int nq, int P, int N, ColSumOut out
   const int R = (P + S - 1) / S;
   const int gx = (N / 4 + 63) / 64;
   hipLaunchKernelGGL(col_sum_split_kernel, dim3(gx, S, nq), dim3(256), 0, st, part, region, P, N, R);
-  hipLaunchKernelGGL(col_sum_final_kernel, dim3(gx, 1, nq), dim3(256), 0, st, part, region, P, S, N, outs);
+  hipLaunchKernelGGL(col_sum_final_kernel, dim3(gx, 1, nq), dim3(256), 0, st, part, region, P, S, N, outs, 0);
 }
+
+// Column sums of a bf16 [T][N] matrix into fp32 (bias gradients of library-GEMM dense layers):
+// level 1 reads 16 B (8 columns) per lane, 4 row groups per block, grid (N/512, S slices) ->
+// ws[S][N]; level 2 = col_sum_final_kernel (optionally accumulating into `out`).
+__global__ void __launch_bounds__(256)
+bf16_col_sum_split_kernel(const bf16_t* __restrict__ x, int T, int N, float* __restrict__ ws, int R) {
+  __shared__ float red[4][64][9];
+  const int cv = blockIdx.x * 64 + (threadIdx.x & 63);      // 8-column vector index
+  const int rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * R, r1 = min(T, r0 + R);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cv * 8 < N) {
+    for (int r = r0 + rg; r < r1; r += 4) {
+      float f[8];
+      unpack8(reinterpret_cast<const uint4*>(x + (long)r * N)[cv], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += f[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rg][threadIdx.x & 63][e] = acc[e];
+  __syncthreads();
+  if (rg == 0 && cv * 8 < N) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = red[0][threadIdx.x][e];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) t += red[k][threadIdx.x][e];
+      ws[(long)blockIdx.y * N + cv * 8 + e] = t;
+    }
+  }
+}
+
+}  // namespace
+
+int dtf_bf16_col_sum_ws_floats(int N) { return kColSplits * N; }
+
+void dtf_bf16_col_sum(const bf16_t* x, int T, int N, float* ws, float* out, int accumulate,
+                      hipStream_t st) {
+  if (N % 8) throw std::runtime_error("bf16_col_sum: N % 8 != 0");
+  int S = T / 64;
+  S = S < 1 ? 1 : (S > kColSplits ? kColSplits : S);
+  const int R = (T + S - 1) / S;
+  hipLaunchKernelGGL(bf16_col_sum_split_kernel, dim3((N / 8 + 63) / 64, S), dim3(256), 0, st, x, T, N, ws, R);
+  hipLaunchKernelGGL(col_sum_final_kernel, dim3((N / 4 + 63) / 64, 1, 1), dim3(256), 0, st, ws, 0L, 0, S,
+                     N, ColSumOut{{out, nullptr, nullptr}}, accumulate);
+}
+
+namespace {
 
 // ----------------------------------------------------------------------------- bias + GELU
 constexpr float kGeluK0 = 0.7978845608028654f;   // sqrt(2/pi)
 constexpr float kGeluK1 = 0.044715f;
 
+// tanh(u) = 1 - 2 / (1 + e^{2u}) on v_exp_f32 / v_rcp_f32 (libm tanhf is a long branchy
+// sequence; the absolute error here is ~1e-7, far below the bf16 output rounding)
+DTF_DEV float tanh_fast(float u) {
+  const float e = __builtin_amdgcn_exp2f(u * 2.885390081777927f);   // 2 log2(e)
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
+}
 DTF_DEV float gelu_f(float x) {
-  const float t = tanhf(kGeluK0 * (x + kGeluK1 * x * x * x));
+  const float t = tanh_fast(kGeluK0 * (x + kGeluK1 * x * x * x));
   return 0.5f * x * (1.f + t);
 }
 DTF_DEV float gelu_grad(float x) {
-  const float t = tanhf(kGeluK0 * (x + kGeluK1 * x * x * x));
+  const float t = tanh_fast(kGeluK0 * (x + kGeluK1 * x * x * x));
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluK0 * (1.f + 3.f * kGeluK1 * x * x);
 }
 
 __global__ void __launch_bounds__(256)
 bias_gelu_fwd_kernel(const bf16_t* __restrict__ a, const float* __restrict__ bias,
                      bf16_t* __restrict__ y, long n8, int N) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int i = blockIdx.x * 256 + threadIdx.x;        // host guarantees n8 < 2^31
   if (i >= n8) return;
-  const int col = (int)((i * 8) % N);
+  const int col = (i % (N >> 3)) * 8;
   float f[8];
   unpack8(((const uint4*)a)[i], f);
 #pragma unroll
@@ -805,6 +863,7 @@ void dtf_bias_gelu_fwd(const bf16_t* a, const float* bias, bf16_t* y, long M, in
                        hipStream_t st) {
   if (N % 8) throw std::runtime_error("bias_gelu: N % 8 != 0");
   const long n8 = M * N / 8;
+  if (n8 >= 2147483647L) throw std::runtime_error("bias_gelu: tensor too large");
   hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st,
                      a, bias, y, n8, N);
 }

@@ -488,7 +488,7 @@ class _Dense(torch.autograd.Function):
             dx = (dy2 @ wb).reshape(x.shape)
         if ctx.needs_input_grad[1]:
             target = _direct_grad(ctx.w_param)
-            S = _wgrad_splits(T, o, i)
+            S = _wgrad_splits(T, o, i) if (o * i) % 4 == 0 and dy2.dtype == x2.dtype else 1
             if S == 1:
                 if target is not None:
                     torch.addmm(target, dy2.t(), x2, out_dtype=torch.float32, out=target)
@@ -496,23 +496,35 @@ class _Dense(torch.autograd.Function):
                     dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
             else:
                 part = torch.bmm(dy2.view(S, T // S, o).transpose(1, 2), x2.view(S, T // S, i),
-                                 out_dtype=torch.float32).sum(0)
-                if target is not None:
-                    target.add_(part)
-                else:
-                    dw = part
+                                 out_dtype=torch.float32)
+                out = target if target is not None else torch.empty(o, i, device=x.device,
+                                                                    dtype=torch.float32)
+                # deterministic in-order slab sum, fused with the += into the flat grad buffer
+                _K.slab_reduce(part.data_ptr(), out.data_ptr(), o * i, S, int(target is not None),
+                               _st())
+                if target is None:
+                    dw = out
             if target is not None:
                 _grad_ready(ctx.w_param)
             elif ctx.w_param.dtype != torch.float32:
                 dw = dw.to(ctx.w_param.dtype)
         if ctx.has_b and ctx.needs_input_grad[3]:
             tb = _direct_grad(ctx.b_param)
-            s = torch.sum(dy2, 0, dtype=torch.float32)
+            out = tb if tb is not None else torch.empty(o, device=x.device, dtype=torch.float32)
+            if dy2.dtype == _BF16 and o % 8 == 0:
+                dyc = dy2.contiguous()
+                ws = torch.empty(_K.bf16_col_sum_ws_floats(o), device=x.device,
+                                 dtype=torch.float32)
+                _K.bf16_col_sum(dyc.data_ptr(), T, o, ws.data_ptr(), out.data_ptr(),
+                                int(tb is not None), _st())
+            elif tb is not None:
+                out.add_(torch.sum(dy2, 0, dtype=torch.float32))
+            else:
+                out = torch.sum(dy2, 0, dtype=torch.float32)
             if tb is not None:
-                tb.add_(s)
                 _grad_ready(ctx.b_param)
             else:
-                db = s.to(ctx.b_param.dtype)
+                db = out.to(ctx.b_param.dtype)
         ctx.w_param = ctx.b_param = None
         return dx, dw, None, db
 
