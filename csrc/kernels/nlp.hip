@@ -765,6 +765,11 @@ segment_sum_kernel(const int64_t* __restrict__ sorted_ids, const int64_t* __rest
 
 // ----------------------------------------------------------------------------- MLM loss
 // rows: loss_rows[i] = w_i * (lse - logit[label]) / denom ; grad = w_i * (softmax - onehot) / denom
+// One wave per masked position; the row (V = 30522 bf16, rows only 4-B aligned) is swept in
+// 16-B chunks from the 16-B-aligned address below its start with raw buffer loads (range-checked:
+// the chunk before row 0 / past the last row reads zeros), elements outside the row masked.
+// Online (max, sum) with one rescale per 8 elements; the gradient pass stores whole 16-B chunks
+// inside the row and single elements at its two ends.
 __global__ void __launch_bounds__(256)
 mlm_xent_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ labels,
                 const float* __restrict__ weights, const float* __restrict__ denom, int N, int V,
@@ -772,18 +777,31 @@ mlm_xent_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ l
   const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (row >= N) return;
-  const bf16_t* x = logits + (long)row * V;
+  const auto rl = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(logits), (short)0,
+                                                    (int)((uint32_t)N * V * 2u), 0x00020000);
+  const uint32_t b0 = (uint32_t)row * V * 2u;
+  const uint32_t a0 = b0 & ~15u;
+  const int head = (int)(b0 - a0) >> 1;
+  const int nch = (head + V + 7) >> 3;
   float mx = -INFINITY, s = 0.f;
-  for (int i = lane; i < V; i += 64) {
-    const float v = bf2f(x[i]);
-    if (v > mx) {
-      s = s * __expf(mx - v) + 1.f;
-      mx = v;
-    } else {
-      s += __expf(v - mx);
+  for (int c = lane; c < nch; c += 64) {
+    const uint4 raw = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rl, a0 + c * 16u, 0, 0));
+    float f[8];
+    unpack8(raw, f);
+    const int e0 = c * 8 - head;
+    float m8 = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (e0 + k < 0 || e0 + k >= V) f[k] = -INFINITY;
+      m8 = fmaxf(m8, f[k]);
     }
+    const float nm = fmaxf(mx, m8);
+    float acc = mx == -INFINITY ? 0.f : s * __expf(mx - nm);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += __expf(f[k] - nm);   // exp(-inf) = 0 for masked slots
+    s = acc;
+    mx = nm;
   }
-  // combine (max, sum) pairs across the wave
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float om = __shfl_xor(mx, o, 64), os = __shfl_xor(s, o, 64);
@@ -793,13 +811,25 @@ mlm_xent_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ l
   }
   const float lse = mx + __logf(s);
   const int lab = (int)labels[row];
+  const bf16_t* x = logits + (long)row * V;
   const float wsc = weights ? weights[row] / fmaxf(denom[0], 1e-5f) : 1.f / fmaxf(denom[0], 1e-5f);
   if (lane == 0) loss_rows[row] = wsc * (lse - bf2f(x[lab]));
   if (grad) {
-    bf16_t* gr = grad + (long)row * V;
-    for (int i = lane; i < V; i += 64) {
-      const float p = __expf(bf2f(x[i]) - lse);
-      gr[i] = f2bf(wsc * (p - (i == lab ? 1.f : 0.f)));
+    bf16_t* gbase = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(grad) + a0);
+    for (int c = lane; c < nch; c += 64) {
+      const uint4 raw = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rl, a0 + c * 16u, 0, 0));
+      float f[8];
+      unpack8(raw, f);
+      const int e0 = c * 8 - head;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = wsc * (__expf(f[k] - lse) - (e0 + k == lab ? 1.f : 0.f));
+      if (e0 >= 0 && e0 + 8 <= V) {
+        reinterpret_cast<uint4*>(gbase)[c] = pack8(f);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (e0 + k >= 0 && e0 + k < V) gbase[c * 8 + k] = f2bf(f[k]);
+      }
     }
   }
 }
@@ -929,6 +959,7 @@ void dtf_segment_sum(const int64_t* sorted_ids, const int64_t* perm, const bf16_
 void dtf_mlm_xent(const bf16_t* logits, const int64_t* labels, const float* weights,
                   const float* denom, int N, int V, float* loss_rows, bf16_t* grad,
                   hipStream_t st) {
+  if ((double)N * V * 2.0 >= 2147483647.0) throw std::runtime_error("mlm_xent: logits too large");
   hipLaunchKernelGGL(mlm_xent_kernel, dim3((N * 64 + 255) / 256), dim3(256), 0, st, logits,
                      labels, weights, denom, N, V, loss_rows, grad);
 }

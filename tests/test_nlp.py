@@ -227,7 +227,9 @@ def test_mlm_loss_gpu():
     N, V = 80, 30522
     lg32 = torch.randn(N, V) * 3
     lab = torch.randint(0, V, (N,))
+    lab[0], lab[1], lab[2] = 0, V - 1, 7          # labels on the misaligned row ends
     w = (torch.rand(N) > 0.2).float()
+    w[:3] = 1.0
     lg = _leaf(lg32)
     loss, (dl,) = _grads_of(lambda: ops.mlm_loss(lg, lab.cuda(), w.cuda()), [lg], None)
     lg_ = lg32.bfloat16().float().requires_grad_(True)
