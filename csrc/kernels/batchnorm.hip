@@ -34,15 +34,50 @@ inline int stats_grid(long M, int C, int* rows_per_block) {
   return (int)((M + rpb - 1) / rpb);
 }
 
+// Row-sweep structure shared by the streaming kernels: lane (ro, cg) owns channel group cg
+// (8 channels = one 16-B vector) of rows ro, ro + rpi, ... and keeps that group's per-channel
+// coefficients in registers for the whole sweep.  Each trip issues the loads of kUnroll rows
+// back to back before any use (4-8 independent 16-B loads in flight per lane -- the r1 kernels had
+// one, and a 64-bit modulo per vector, and ran at ~4 TB/s).  All offsets are 32-bit vector
+// indices (host checks M*C/8 < 2^31).
+constexpr int kUnroll = 4;
+
+// ReLU mask source for the backward passes, in order of preference:
+//   mask (1 bit per element, written by the forward apply -- the residual BNs, 1/16 of y's bytes)
+//   fsc/fsh (recompute fmaf(x, scale, shift) > 0 from x -- BNs without a residual; free)
+//   y (the saved output)
+DTF_DEV void relu_mask8(float* g, const float* xv, uint32_t mbyte, uint4 yraw, int kind,
+                        const float* ksc, const float* ksh) {
+  if (kind == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = (mbyte >> i) & 1u ? g[i] : 0.f;
+  } else if (kind == 2) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = __builtin_fmaf(xv[i], ksc[i], ksh[i]) > 0.f ? g[i] : 0.f;
+  } else if (kind == 3) {
+    float yv[8];
+    unpack8(yraw, yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+  }
+}
+
+DTF_DEV void load8f(const float* __restrict__ p, int cg, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[cg * 2];
+  const float4 b = reinterpret_cast<const float4*>(p)[cg * 2 + 1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 // MODE 0: forward stats   acc0 += x,           acc1 += x*x
 // MODE 1: backward reduce acc0 += dz,          acc1 += dz*(x-mean)*invstd
+// mkind (MODE 1): 0 no ReLU, 1 bit mask, 2 recompute from x, 3 from y
 template <int MODE>
 __global__ void __launch_bounds__(kThreads)
 bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
-                 const bf16_t* __restrict__ y, const float* __restrict__ mean,
-                 const float* __restrict__ invstd, long M, int C, int rows_per_block, int relu,
-                 float* __restrict__ partial, const float* __restrict__ fsc,
-                 const float* __restrict__ fsh) {
+                 const bf16_t* __restrict__ y, const uint8_t* __restrict__ mask,
+                 const float* __restrict__ mean, const float* __restrict__ invstd, int M, int C,
+                 int rows_per_block, int mkind, float* __restrict__ partial,
+                 const float* __restrict__ fsc, const float* __restrict__ fsh) {
   extern __shared__ __attribute__((aligned(16))) float red[];   // [rpi][2][C]
   const int tpr = C >> 3;
   const int rpi = kThreads / tpr;
@@ -51,43 +86,47 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
   const bool active = ro < rpi;
   float a0[8], a1[8], mu[8], is[8], ksc[8], ksh[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { a0[i] = 0.f; a1[i] = 0.f; }
-  // ReLU mask source: the saved output y, or (y == null) recomputed from x with the forward's
-  // scale/shift -- the same fmaf as bn_apply, so the sign (= the mask) is bit-identical
-  const bool mask_x = MODE == 1 && relu && y == nullptr;
+  for (int i = 0; i < 8; ++i) { a0[i] = 0.f; a1[i] = 0.f; ksc[i] = 0.f; ksh[i] = 0.f; }
   if (MODE == 1 && active) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { mu[i] = mean[cg * 8 + i]; is[i] = invstd[cg * 8 + i]; }
-    if (mask_x) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { ksc[i] = fsc[cg * 8 + i]; ksh[i] = fsh[cg * 8 + i]; }
-    }
+    load8f(mean, cg, mu);
+    load8f(invstd, cg, is);
+    if (mkind == 2) { load8f(fsc, cg, ksc); load8f(fsh, cg, ksh); }
   }
-  const long m0 = (long)blockIdx.x * rows_per_block;
-  long m1 = m0 + rows_per_block;
-  if (m1 > M) m1 = M;
+  const int m0 = blockIdx.x * rows_per_block;
+  const int m1 = min(m0 + rows_per_block, M);
+  const uint4* X4 = reinterpret_cast<const uint4*>(x);
+  const uint4* D4 = reinterpret_cast<const uint4*>(dy);
+  const uint4* Y4 = reinterpret_cast<const uint4*>(y);
   if (active) {
-    for (long m = m0 + ro; m < m1; m += rpi) {
-      const long off = m * C + cg * 8;
-      float xv[8];
-      unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
-      if (MODE == 0) {
+    for (int m = m0 + ro; m < m1; m += rpi * kUnroll) {
+      uint4 xr[kUnroll], dr[kUnroll], yr[kUnroll];
+      uint32_t mb[kUnroll];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { a0[i] += xv[i]; a1[i] += xv[i] * xv[i]; }
-      } else {
-        float g[8];
-        unpack8(*reinterpret_cast<const uint4*>(dy + off), g);
-        if (mask_x) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) g[i] = __builtin_fmaf(xv[i], ksc[i], ksh[i]) > 0.f ? g[i] : 0.f;
-        } else if (relu) {
-          float yv[8];
-          unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+      for (int u = 0; u < kUnroll; ++u) {
+        const int r = m + u * rpi;
+        const uint32_t v = (uint32_t)r * tpr + cg;
+        const bool ok = r < m1;
+        xr[u] = ok ? X4[v] : make_uint4(0, 0, 0, 0);
+        if (MODE == 1) {
+          dr[u] = ok ? D4[v] : make_uint4(0, 0, 0, 0);
+          mb[u] = (ok && mkind == 1) ? (uint32_t)mask[v] : 0u;
+          yr[u] = (ok && mkind == 3) ? Y4[v] : make_uint4(0, 0, 0, 0);
         }
+      }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { a0[i] += g[i]; a1[i] += g[i] * (xv[i] - mu[i]) * is[i]; }
+      for (int u = 0; u < kUnroll; ++u) {
+        float xv[8];
+        unpack8(xr[u], xv);        // rows past m1 were loaded as zeros: they add nothing
+        if (MODE == 0) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { a0[i] += xv[i]; a1[i] += xv[i] * xv[i]; }
+        } else {
+          float g[8];
+          unpack8(dr[u], g);
+          relu_mask8(g, xv, mb[u], yr[u], mkind, ksc, ksh);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { a0[i] += g[i]; a1[i] += g[i] * (xv[i] - mu[i]) * is[i]; }
+        }
       }
     }
   }
@@ -206,36 +245,65 @@ __global__ void bn_infer_finalize_kernel(int C, const float* __restrict__ gamma,
   shift[c] = beta[c] - run_mean[c] * gamma[c] * is;
 }
 
+// y = [relu](x*scale + shift [+ res]); with `mask` also the ReLU bit mask (bit i of byte v =
+// element 8v+i > 0) the backward reads instead of y.
 __global__ void __launch_bounds__(kThreads)
 bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
-                bf16_t* __restrict__ y, const float* __restrict__ scale,
-                const float* __restrict__ shift, long nvec, int C, int relu) {
-  const int tpr = C >> 3;
-  for (long v = (long)blockIdx.x * kThreads + threadIdx.x; v < nvec;
-       v += (long)gridDim.x * kThreads) {
-    const int cg = (int)(v % tpr);
-    float xv[8];
-    unpack8(reinterpret_cast<const uint4*>(x)[v], xv);
-    const float4 s0 = reinterpret_cast<const float4*>(scale)[cg * 2];
-    const float4 s1 = reinterpret_cast<const float4*>(scale)[cg * 2 + 1];
-    const float4 h0 = reinterpret_cast<const float4*>(shift)[cg * 2];
-    const float4 h1 = reinterpret_cast<const float4*>(shift)[cg * 2 + 1];
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    float o[8];
+                bf16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                const float* __restrict__ scale, const float* __restrict__ shift, int M, int C,
+                int relu) {
+  const int tpr = C >> 3, rpi = kThreads / tpr;
+  const int cg = threadIdx.x % tpr, ro = threadIdx.x / tpr;
+  if (ro >= rpi) return;
+  float sc[8], sh[8];
+  load8f(scale, cg, sc);
+  load8f(shift, cg, sh);
+  const uint4* X4 = reinterpret_cast<const uint4*>(x);
+  const uint4* R4 = reinterpret_cast<const uint4*>(res);
+  uint4* Y4 = reinterpret_cast<uint4*>(y);
+  const int step = gridDim.x * rpi * kUnroll;
+  for (int m = blockIdx.x * rpi * kUnroll + ro; m < M; m += step) {
+    uint4 xr[kUnroll], rr[kUnroll];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = __builtin_fmaf(xv[i], sc[i], sh[i]);
-    if (res) {
-      float r[8];
-      unpack8(reinterpret_cast<const uint4*>(res)[v], r);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] += r[i];
+    for (int u = 0; u < kUnroll; ++u) {
+      const int r = m + u * rpi;
+      const uint32_t v = (uint32_t)r * tpr + cg;
+      if (r < M) {
+        xr[u] = X4[v];
+        if (res) rr[u] = R4[v];
+      }
     }
-    if (relu) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = fmaxf(o[i], 0.f);
+    for (int u = 0; u < kUnroll; ++u) {
+      const int r = m + u * rpi;
+      if (r >= M) break;
+      const uint32_t v = (uint32_t)r * tpr + cg;
+      float xv[8], o[8];
+      unpack8(xr[u], xv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = __builtin_fmaf(xv[i], sc[i], sh[i]);
+      if (res) {
+        float rv[8];
+        unpack8(rr[u], rv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] += rv[i];
+      }
+      if (relu) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = fmaxf(o[i], 0.f);
+      }
+      const uint4 packed = pack8(o);
+      Y4[v] = packed;
+      if (mask) {
+        // the mask is taken from the ROUNDED output, exactly what a y-based mask would see
+        float ov[8];
+        unpack8(packed, ov);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) bits |= (ov[i] > 0.f ? 1u : 0u) << i;
+        mask[v] = (uint8_t)bits;
+      }
     }
-    reinterpret_cast<uint4*>(y)[v] = pack8(o);
   }
 }
 
@@ -262,42 +330,76 @@ bn_bwd_finalize_kernel(const double* __restrict__ level2, int S, int C, long M,
 
 __global__ void __launch_bounds__(kThreads)
 bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
-                    const bf16_t* __restrict__ x, const float* __restrict__ cA,
-                    const float* __restrict__ cB, const float* __restrict__ cC,
-                    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long nvec, int C,
-                    int relu, const float* __restrict__ fsc, const float* __restrict__ fsh) {
-  const int tpr = C >> 3;
-  const bool mask_x = relu && y == nullptr;
-  for (long v = (long)blockIdx.x * kThreads + threadIdx.x; v < nvec;
-       v += (long)gridDim.x * kThreads) {
-    const int cg = (int)(v % tpr);
-    float g[8], xv[8];
-    unpack8(reinterpret_cast<const uint4*>(dy)[v], g);
-    unpack8(reinterpret_cast<const uint4*>(x)[v], xv);
-    if (mask_x) {
+                    const uint8_t* __restrict__ mask, const bf16_t* __restrict__ x,
+                    const float* __restrict__ cA, const float* __restrict__ cB,
+                    const float* __restrict__ cC, bf16_t* __restrict__ dx,
+                    bf16_t* __restrict__ dres, int M, int C, int mkind,
+                    const float* __restrict__ fsc, const float* __restrict__ fsh) {
+  const int tpr = C >> 3, rpi = kThreads / tpr;
+  const int cg = threadIdx.x % tpr, ro = threadIdx.x / tpr;
+  if (ro >= rpi) return;
+  float ka[8], kb[8], kc[8], ksc[8], ksh[8];
+  load8f(cA, cg, ka);
+  load8f(cB, cg, kb);
+  load8f(cC, cg, kc);
+  if (mkind == 2) { load8f(fsc, cg, ksc); load8f(fsh, cg, ksh); }
+  const uint4* D4 = reinterpret_cast<const uint4*>(dy);
+  const uint4* X4 = reinterpret_cast<const uint4*>(x);
+  const uint4* Y4 = reinterpret_cast<const uint4*>(y);
+  uint4* DX4 = reinterpret_cast<uint4*>(dx);
+  uint4* DR4 = reinterpret_cast<uint4*>(dres);
+  const int step = gridDim.x * rpi * kUnroll;
+  for (int m = blockIdx.x * rpi * kUnroll + ro; m < M; m += step) {
+    uint4 dr[kUnroll], xr[kUnroll], yr[kUnroll];
+    uint32_t mb[kUnroll];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        g[i] = __builtin_fmaf(xv[i], fsc[cg * 8 + i], fsh[cg * 8 + i]) > 0.f ? g[i] : 0.f;
-    } else if (relu) {
-      float yv[8];
-      unpack8(reinterpret_cast<const uint4*>(y)[v], yv);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+    for (int u = 0; u < kUnroll; ++u) {
+      const int r = m + u * rpi;
+      const uint32_t v = (uint32_t)r * tpr + cg;
+      if (r < M) {
+        dr[u] = D4[v];
+        xr[u] = X4[v];
+        if (mkind == 1) mb[u] = mask[v];
+        if (mkind == 3) yr[u] = Y4[v];
+      }
     }
-    if (dres) reinterpret_cast<uint4*>(dres)[v] = pack8(g);
-    float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = cg * 8 + i;
-      o[i] = cA[c] * g[i] + cB[c] * xv[i] + cC[c];
+    for (int u = 0; u < kUnroll; ++u) {
+      const int r = m + u * rpi;
+      if (r >= M) break;
+      const uint32_t v = (uint32_t)r * tpr + cg;
+      float g[8], xv[8], o[8];
+      unpack8(dr[u], g);
+      unpack8(xr[u], xv);
+      relu_mask8(g, xv, mkind == 1 ? mb[u] : 0u, mkind == 3 ? yr[u] : make_uint4(0, 0, 0, 0),
+                 mkind, ksc, ksh);
+      if (dres) DR4[v] = pack8(g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = ka[i] * g[i] + kb[i] * xv[i] + kc[i];
+      DX4[v] = pack8(o);
     }
-    reinterpret_cast<uint4*>(dx)[v] = pack8(o);
   }
 }
 
-inline int ew_grid(long nvec) {
-  long g = (nvec + kThreads - 1) / kThreads;
-  if (g > 256 * 16) g = 256 * 16;
+inline int mask_kind(int relu, const uint8_t* mask, const float* fsc, const float* fsh,
+                     const bf16_t* y) {
+  if (!relu) return 0;
+  if (mask) return 1;
+  if (fsc && fsh) return 2;
+  if (y) return 3;
+  throw std::runtime_error("bn_bwd: relu mask needs a bit mask, y or scale/shift");
+}
+
+inline void check_rows(long M, int C) {
+  if (C % 8 || C > 2048 || M * (long)(C / 8) >= 2147483647L)
+    throw std::runtime_error("batch_norm: unsupported shape (C % 8, C <= 2048, M*C/8 < 2^31)");
+}
+
+// blocks for a row sweep: enough for ~2 trips of kUnroll rows per lane on the big layers
+inline int sweep_grid(long M, int C) {
+  const int rpi = kThreads / (C / 8);
+  long g = (M + (long)rpi * kUnroll - 1) / ((long)rpi * kUnroll);
+  if (g > 256 * 8) g = 256 * 8;
   if (g < 1) g = 1;
   return (int)g;
 }
@@ -311,12 +413,13 @@ int dtf_bn_partial_blocks(long M, int C) {
 }
 
 void dtf_bn_fwd_stats(const bf16_t* x, long M, int C, float* partial, hipStream_t st) {
+  check_rows(M, C);
   int rpb;
   const int G = stats_grid(M, C, &rpb);
   const int rpi = kThreads / (C / 8);
   const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
   hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(G), dim3(kThreads), lds, st, x, nullptr, nullptr,
-                     nullptr, nullptr, M, C, rpb, 0, partial, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, (int)M, C, rpb, 0, partial, nullptr, nullptr);
 }
 
 void dtf_bn_fwd_finalize_g(const float* partial, int G, long M, int C, const float* gamma,
@@ -360,23 +463,25 @@ void dtf_bn_infer_finalize(int C, const float* gamma, const float* beta, const f
                      beta, run_mean, run_var, eps, mean, invstd, scale, shift);
 }
 
-void dtf_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* scale,
-                  const float* shift, long M, int C, int relu, hipStream_t st) {
-  const long nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(kThreads), 0, st, x, res, y, scale,
-                     shift, nvec, C, relu);
+void dtf_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, uint8_t* mask,
+                  const float* scale, const float* shift, long M, int C, int relu,
+                  hipStream_t st) {
+  check_rows(M, C);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, x, res, y,
+                     mask, scale, shift, (int)M, C, relu);
 }
 
-void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
-                       const float* invstd, long M, int C, int relu, float* partial,
-                       const float* fsc, const float* fsh, hipStream_t st) {
-  if (relu && !y && !(fsc && fsh)) throw std::runtime_error("bn_bwd: relu mask needs y or scale/shift");
+void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16_t* x,
+                       const float* mean, const float* invstd, long M, int C, int relu,
+                       float* partial, const float* fsc, const float* fsh, hipStream_t st) {
+  check_rows(M, C);
+  const int mk = mask_kind(relu, mask, fsc, fsh, y);
   int rpb;
   const int G = stats_grid(M, C, &rpb);
   const int rpi = kThreads / (C / 8);
   const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
-  hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(G), dim3(kThreads), lds, st, x, dy, y, mean, invstd,
-                     M, C, rpb, relu, partial, fsc, fsh);
+  hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(G), dim3(kThreads), lds, st, x, dy, y, mask, mean,
+                     invstd, (int)M, C, rpb, mk, partial, fsc, fsh);
 }
 
 void dtf_bn_bwd_finalize(const float* partial, long M, int C, const float* gamma,
@@ -393,11 +498,12 @@ void dtf_bn_bwd_finalize(const float* partial, long M, int C, const float* gamma
                      C, M, gamma, mean, invstd, dgamma, dbeta, coefA, coefB, coefC, accumulate);
 }
 
-void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* cA,
-                      const float* cB, const float* cC, bf16_t* dx, bf16_t* dres, long M, int C,
-                      int relu, const float* fsc, const float* fsh, hipStream_t st) {
-  if (relu && !y && !(fsc && fsh)) throw std::runtime_error("bn_bwd: relu mask needs y or scale/shift");
-  const long nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(kThreads), 0, st, dy, y, x, cA,
-                     cB, cC, dx, dres, nvec, C, relu, fsc, fsh);
+void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16_t* x,
+                      const float* cA, const float* cB, const float* cC, bf16_t* dx,
+                      bf16_t* dres, long M, int C, int relu, const float* fsc, const float* fsh,
+                      hipStream_t st) {
+  check_rows(M, C);
+  const int mk = mask_kind(relu, mask, fsc, fsh, y);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, dy, y,
+                     mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh);
 }

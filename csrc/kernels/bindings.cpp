@@ -34,15 +34,16 @@ int dtf_conv_stats_rows(long, int, int, int);
 void dtf_conv_set_dma_mode(int);
 void dtf_bn_infer_finalize(int, const float*, const float*, const float*, const float*, float,
                            float*, float*, float*, float*, hipStream_t);
-void dtf_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, const float*, const float*, long, int,
-                  int, hipStream_t);
-void dtf_bn_bwd_reduce(const bf16_t*, const bf16_t*, const bf16_t*, const float*, const float*,
-                       long, int, int, float*, const float*, const float*, hipStream_t);
+void dtf_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, uint8_t*, const float*, const float*,
+                  long, int, int, hipStream_t);
+void dtf_bn_bwd_reduce(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, const float*,
+                       const float*, long, int, int, float*, const float*, const float*,
+                       hipStream_t);
 void dtf_bn_bwd_finalize(const float*, long, int, const float*, const float*, const float*,
                          float*, float*, float*, float*, float*, int, hipStream_t);
-void dtf_bn_bwd_apply(const bf16_t*, const bf16_t*, const bf16_t*, const float*, const float*,
-                      const float*, bf16_t*, bf16_t*, long, int, int, const float*, const float*,
-                      hipStream_t);
+void dtf_bn_bwd_apply(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, const float*,
+                      const float*, const float*, bf16_t*, bf16_t*, long, int, int, const float*,
+                      const float*, hipStream_t);
 void dtf_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int,
                      int, int, int, int, hipStream_t);
 void dtf_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int,
@@ -68,6 +69,7 @@ void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, con
                     int, int, int, hipStream_t);
 
 int dtf_conv_wgrad_splits(long, int, int, long);
+void dtf_wgrad_set_dma_mode(int);
 void dtf_lds_probe(int, int, int*, int, hipStream_t);
 int dtf_max_dynamic_lds(int);
 // transformer kernels (nlp.hip)
@@ -154,21 +156,22 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("bn_infer_finalize");
   });
   m.def("bn_apply", [](uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t scale, uintptr_t shift,
-                       long M, int C, int relu, uintptr_t st) {
-    dtf_bn_apply(P<const bf16_t>(x), P<const bf16_t>(res), P<bf16_t>(y), P<const float>(scale),
-                 P<const float>(shift), M, C, relu, S(st));
+                       long M, int C, int relu, uintptr_t st, uintptr_t mask) {
+    dtf_bn_apply(P<const bf16_t>(x), P<const bf16_t>(res), P<bf16_t>(y), P<uint8_t>(mask),
+                 P<const float>(scale), P<const float>(shift), M, C, relu, S(st));
     check_launch("bn_apply");
-  });
+  }, py::arg("x"), py::arg("res"), py::arg("y"), py::arg("scale"), py::arg("shift"), py::arg("M"),
+     py::arg("C"), py::arg("relu"), py::arg("stream"), py::arg("mask") = 0);
   m.def("bn_bwd_reduce", [](uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t mean,
                             uintptr_t invstd, long M, int C, int relu, uintptr_t part,
-                            uintptr_t st, uintptr_t fsc, uintptr_t fsh) {
-    dtf_bn_bwd_reduce(P<const bf16_t>(dy), P<const bf16_t>(y), P<const bf16_t>(x),
-                      P<const float>(mean), P<const float>(invstd), M, C, relu, P<float>(part),
-                      P<const float>(fsc), P<const float>(fsh), S(st));
+                            uintptr_t st, uintptr_t fsc, uintptr_t fsh, uintptr_t mask) {
+    dtf_bn_bwd_reduce(P<const bf16_t>(dy), P<const bf16_t>(y), P<const uint8_t>(mask),
+                      P<const bf16_t>(x), P<const float>(mean), P<const float>(invstd), M, C, relu,
+                      P<float>(part), P<const float>(fsc), P<const float>(fsh), S(st));
     check_launch("bn_bwd_reduce");
   }, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("M"),
      py::arg("C"), py::arg("relu"), py::arg("part"), py::arg("stream"), py::arg("scale") = 0,
-     py::arg("shift") = 0);
+     py::arg("shift") = 0, py::arg("mask") = 0);
   m.def("bn_bwd_finalize", [](uintptr_t part, long M, int C, uintptr_t gamma, uintptr_t mean,
                               uintptr_t invstd, uintptr_t dg, uintptr_t db, uintptr_t a,
                               uintptr_t b, uintptr_t c, int accumulate, uintptr_t st) {
@@ -179,14 +182,15 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("bn_bwd_apply", [](uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t a, uintptr_t b,
                            uintptr_t c, uintptr_t dx, uintptr_t dres, long M, int C, int relu,
-                           uintptr_t st, uintptr_t fsc, uintptr_t fsh) {
-    dtf_bn_bwd_apply(P<const bf16_t>(dy), P<const bf16_t>(y), P<const bf16_t>(x),
-                     P<const float>(a), P<const float>(b), P<const float>(c), P<bf16_t>(dx),
-                     P<bf16_t>(dres), M, C, relu, P<const float>(fsc), P<const float>(fsh), S(st));
+                           uintptr_t st, uintptr_t fsc, uintptr_t fsh, uintptr_t mask) {
+    dtf_bn_bwd_apply(P<const bf16_t>(dy), P<const bf16_t>(y), P<const uint8_t>(mask),
+                     P<const bf16_t>(x), P<const float>(a), P<const float>(b), P<const float>(c),
+                     P<bf16_t>(dx), P<bf16_t>(dres), M, C, relu, P<const float>(fsc),
+                     P<const float>(fsh), S(st));
     check_launch("bn_bwd_apply");
   }, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("a"), py::arg("b"), py::arg("c"),
      py::arg("dx"), py::arg("dres"), py::arg("M"), py::arg("C"), py::arg("relu"),
-     py::arg("stream"), py::arg("scale") = 0, py::arg("shift") = 0);
+     py::arg("stream"), py::arg("scale") = 0, py::arg("shift") = 0, py::arg("mask") = 0);
   m.def("maxpool_fwd", [](uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W, int C,
                           int Pp, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
                           uintptr_t st) {
@@ -279,6 +283,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
      py::arg("dh"), py::arg("dw"), py::arg("splits"), py::arg("stream"), py::arg("tr_mode") = 1,
      py::arg("accumulate") = 0);
   m.def("conv_wgrad_splits", &dtf_conv_wgrad_splits);
+  m.def("wgrad_set_dma_mode", &dtf_wgrad_set_dma_mode);
   m.def("lds_probe", [](int bytes, int blocks, uintptr_t errors, int spin, uintptr_t st) {
     dtf_lds_probe(bytes, blocks, P<int>(errors), spin, S(st));
     check_launch("lds_probe");

@@ -63,6 +63,38 @@ DTF_DEV int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// ---- LDS-DMA (buffer_load_dwordx4 ... lds) helpers shared by the MFMA conv kernels
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+
+// Buffer descriptor as a plain SGPR quad (for inline asm): base, stride 0, num_records = bytes.
+DTF_DEV i32x4_t rsrc_quad(const void* p, uint32_t bytes) {
+  const unsigned long long b = (unsigned long long)p;
+  return (i32x4_t){__builtin_amdgcn_readfirstlane((int)(uint32_t)b),
+                   __builtin_amdgcn_readfirstlane((int)((b >> 32) & 0xFFFFu)), (int)bytes,
+                   0x00020000};
+}
+DTF_DEV uint32_t lds_addr(const bf16_t* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(const lds_void_t*)p);
+}
+// One 1-KB LDS-DMA wave-instruction: lane l's 16 bytes at `voff` land at LDS byte lds + 16 l.
+// Issued as inline asm on purpose: the compiler then does not treat it as an LDS store and does
+// not insert its own (over-conservative) vmcnt waits in front of the fragment reads -- the
+// kernel waits with explicit counted vmcnt instead.  M0 is saved and restored around it.
+DTF_DEV void dma16(const i32x4_t& r, uint32_t lds, uint32_t voff) {
+  uint32_t save;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(save) : "s"(lds), "v"(voff), "s"(r) : "memory");
+}
+#define DTF_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+DTF_DEV void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+
 #define HIP_CHECK(x)                                                               \
   do {                                                                             \
     hipError_t e_ = (x);                                                           \

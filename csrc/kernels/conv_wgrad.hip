@@ -240,6 +240,192 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA variant (C % 8 == 0, M < 2^24).  The r1 kernel above stages both operands through
+// VGPRs + ds_write_b128 into padded rows; at 2 blocks/CU that write pass (≈13 LDS cycles per
+// 1-KB wave-instruction) plus the transposed fragment reads exceeded the MFMA time per K-step
+// (profiles/r1_conv_roofline: 3x3 wgrad at 0.19-0.20 of the MFMA roof).  Here every 16-B piece
+// goes global -> LDS with `buffer_load_dwordx4 ... lds` (no staging VGPRs, ≈4 LDS cycles per
+// KB), double-buffered: the DMA of K-step k+1 is issued right after the barrier that publishes
+// K-step k, then the MFMAs of k run while it flies (cdna_hip_programming.md §5 "glds, 2 LDS
+// buffers, BK=64, vmcnt(0) + plain __syncthreads()").
+//
+// LDS image: unpadded pixel-major rows ([64 pixels][128 cols] per operand), 16-B chunks
+// XOR-swizzled per row so the ds_read_b64_tr_b16 fragment reads are conflict-free: a 32-lane
+// half of a transposed read touches rows {0-3, 8-11} (+32ks, +4) at one 32-B column pair, so
+// logical chunk c of row r lives in slot c ^ swz(r), swz(r) = 2 * ((r & 3) | ((r >> 3) & 1) << 2)
+// -> the 8 rows land on the 8 distinct 32-B bank groups of a 256-B bank row.  The DMA writes
+// lane-linearly, so the swizzle is applied on the SOURCE side (lane in slot s fetches chunk
+// s ^ swz(r)).  Pixel -> (n, p, q) uses an fp32 reciprocal divmod (exact for m < 2^24).
+constexpr int kWdStage = 2 * BKM * 128;      // bf16 elements per stage (A + B image)
+
+DTF_DEV int wswz(int r) { return (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
+DTF_DEV int lds_el(int r, int c) { return r * 128 + (((c >> 3) ^ wswz(r)) << 3) + (c & 7); }
+DTF_DEV void fdivmod(int m, int d, float inv, int& q, int& r) {
+  const int t = (int)((float)m * inv);
+  const int rem = m - t * d;
+  const int adj = rem < 0 ? -1 : (rem >= d ? 1 : 0);   // selects, no branches
+  q = t + adj;
+  r = rem - adj * d;
+}
+
+__global__ void __launch_bounds__(kThreads, 2)
+conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
+                      float* __restrict__ dW, const WgradGeom g, const TapTableW taps,
+                      float invQ, float invP) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int TC = taps.n * g.C;
+  const int tiles_m = (g.Kout + BM - 1) / BM;
+  const int tiles_n = (TC + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  // XCD-aware: consecutive logical ids (same split, neighbouring tiles -> the same pixel rows of
+  // X / dY) share an XCD's L2
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % ntiles;
+  const int split = bid / ntiles;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int k0 = tm * BM, j0 = tn * BN;
+  const int M = g.N * g.P * g.Q;
+  const int ms = split * (int)g.m_per_split;
+  const int me = min(ms + (int)g.m_per_split, M);
+  const int nk = (me - ms + BKM - 1) / BKM;
+  const i32x4_t rx = rsrc_quad(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
+  const i32x4_t ry = rsrc_quad(dY, (uint32_t)M * g.Kout * 2u);
+  const uint32_t lds0 = lds_addr(lds);
+  // tap table -> LDS (past the epilogue tile) so per-lane lookups never index the kernarg struct
+  int* lds_taps = reinterpret_cast<int*>(reinterpret_cast<float*>(lds) + BM * (BN + 4));
+  if (tid == 0)
+    for (int t = 0; t < taps.n; ++t) { lds_taps[t] = taps.dh[t]; lds_taps[DTF_MAX_TAPS + t] = taps.dw[t]; }
+  __syncthreads();
+
+  // DMA plan: per stage and operand 16 wave-instructions of 4 rows x 16 chunks; wave w issues
+  // instructions q = w + 4i (i < 4) of each operand -> rows 4q + (lane >> 4), LDS slot lane & 15.
+  // Per lane everything that does not change with the K-step is precomputed: the dY column and
+  // row offset, and the X tap offset / tap displacement of the chunk it fetches.
+  const int lrow = lane >> 4, slot = lane & 15;
+  int rowv[4], a_off[4], b_dh[4], b_dw[4], b_toff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * (wave + 4 * i) + lrow;
+    rowv[i] = r;
+    const int chunk = slot ^ wswz(r);
+    const int kc = k0 + chunk * 8;
+    a_off[i] = kc < g.Kout ? (r * g.Kout + kc) * 2 : -1;
+    const int jc = j0 + chunk * 8;
+    if (jc < TC) {
+      const int t = jc / g.C;
+      const int c = jc - t * g.C;
+      b_dh[i] = lds_taps[t];
+      b_dw[i] = lds_taps[DTF_MAX_TAPS + t];
+      b_toff[i] = ((b_dh[i] * g.W + b_dw[i]) * g.C + c) * 2;
+    } else {
+      b_dh[i] = 1 << 20;          // fails the bounds test -> zeros
+      b_dw[i] = 0;
+      b_toff[i] = 0;
+    }
+  }
+  const int HW = g.H * g.W;
+  const uint32_t a_step = (uint32_t)BKM * g.Kout * 2u;
+
+  // Each lane decodes ONE pixel of the K-step (row = lane); the 16 lanes that fetch a row's
+  // chunks get its decode by ds_bpermute -- 1 divmod pair per lane per step instead of 4.
+  auto issue = [&](int kt, int stage) {
+    const uint32_t base = lds0 + (uint32_t)(stage * kWdStage) * 2u;
+    const int mk = ms + kt * BKM;                     // wave-uniform first pixel of the step
+    const int live = me - mk;                         // rows < live are inside this split
+    const int mp = mk + lane;
+    int t, q, n, p;
+    fdivmod(mp < me ? mp : mk, g.Q, invQ, t, q);
+    fdivmod(t, g.P, invP, n, p);
+    const int hb = lane < live ? p * g.sh : 0x3FFF;   // an invalid row fails every bounds test
+    const int wb = q * g.sw;
+    const int pb = ((n * HW + hb * g.W + wb) * g.C) * 2;
+    const int hw = (hb << 16) | wb;
+    const uint32_t a_base = (uint32_t)mk * g.Kout * 2u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rowv[i];
+      const int hwr = __shfl(hw, r, 64);
+      const int pbr = __shfl(pb, r, 64);
+      const int h = (hwr >> 16) + b_dh[i], w = (hwr & 0xFFFF) + b_dw[i];
+      const bool bok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const uint32_t bo = bok ? (uint32_t)(pbr + b_toff[i]) : kOOB;
+      const uint32_t ao = (r < live && a_off[i] >= 0) ? a_base + (uint32_t)a_off[i] : kOOB;
+      const uint32_t inst = (uint32_t)(wave + 4 * i) * 1024u;
+      dma16(ry, base + inst, ao);
+      dma16(rx, base + (uint32_t)(BKM * 128 * 2) + inst, bo);
+    }
+    (void)a_step;
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int gq = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;
+  if (nk > 0) issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    DTF_WAIT_VM(0);            // this wave's DMAs of step kt landed ...
+    __syncthreads();           // ... and everyone's; everyone also finished reading step kt-1
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    const bf16_t* sa = lds + (kt & 1) * kWdStage;
+    const bf16_t* sb = sa + BKM * 128;
+#pragma unroll
+    for (int ks = 0; ks < BKM / 32; ++ks) {
+      bf16x8_t af[4], bfr[4];
+      const int r0 = 32 * ks + 8 * gq + tq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c0 = wm * 64 + 16 * i + 4 * tp;
+        const s4_t lo = tr_read(sa + lds_el(r0, c0));
+        const s4_t hi = tr_read(sa + lds_el(r0 + 4, c0));
+        af[i] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c0 = wn * 64 + 16 * j + 4 * tp;
+        const s4_t lo = tr_read(sb + lds_el(r0, c0));
+        const s4_t hi = tr_read(sb + lds_el(r0 + 4, c0));
+        bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  DTF_WAIT_VM(0);
+  __syncthreads();             // all fragment reads done before the epilogue reuses the LDS
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr int LDO = BN + 4;
+  float* so = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[i][j][r] + 0.0f;
+        so[(wm * 64 + 16 * i + 4 * gq + r) * LDO + wn * 64 + 16 * j + li] = v;
+      }
+  __syncthreads();
+  float* out = dW + (long)split * g.slab;
+  for (int idx = tid; idx < BM * BN; idx += kThreads) {
+    const int r = idx / BN, c = idx % BN;
+    const int row = k0 + r, col = j0 + c;
+    if (row < g.Kout && col < TC) out[(long)row * g.ldw + col] = so[r * LDO + c];
+  }
+}
+
 // Deterministic slab sum: block = 64 float4 columns x 4 split groups; group q sums splits
 // q, q+4, ... in order, the 4 group partials are added in a fixed order through LDS.
 __global__ void __launch_bounds__(256)
@@ -271,11 +457,17 @@ slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n
 }
 }  // namespace
 
+// -1 / 1: LDS-DMA kernel whenever legal (default), 0: the register-staged kernel (A/B tests)
+static int g_wgrad_dma_mode = -1;
+void dtf_wgrad_set_dma_mode(int mode) { g_wgrad_dma_mode = mode; }
+
 // Number of reduction splits: aim for ~1024 blocks (4 per CU), keep >= 4 K-steps per split and
 // the fp32 slab workspace (splits x Kout x TC) under `ws_cap` floats.
 int dtf_conv_wgrad_splits(long M, int Kout, int TC, long ws_cap) {
   const long tiles = (long)((Kout + BM - 1) / BM) * ((TC + BN - 1) / BN);
-  long splits = (1024 + tiles - 1) / tiles;
+  // never overshoot 1024 = exactly two rounds of 512 block slots (2 blocks x 256 CUs): one block
+  // past a round costs a whole extra round (29 splits x 36 tiles = 1044 blocks ran 3 rounds)
+  long splits = 1024 / tiles;
   const long max_splits = (M + 4 * BKM - 1) / (4 * BKM);
   if (splits > max_splits) splits = max_splits;
   const long cap = ws_cap / ((long)Kout * TC);
@@ -312,7 +504,15 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   const size_t lds = (size_t)2 * (OPER_A + OPER_B) * sizeof(bf16_t) + 2 * DTF_MAX_TAPS * sizeof(int);
   const bool generic = (g.C % 8) != 0;
   const dim3 grid((unsigned)(tiles * nsplit));
-  if (!(tr_mode & 1)) {  // debug path: element-wise LDS reads instead of ds_read_b64_tr_b16
+  const bool dma = g_wgrad_dma_mode != 0 && !generic && (tr_mode & 1) && M < (1L << 24) &&
+                   g.N * g.H * g.W < (1L << 24);
+  if (dma) {
+    const size_t lds_dma = (size_t)BM * (BN + 4) * sizeof(float) +   // epilogue tile >= 2 stages
+                           2 * DTF_MAX_TAPS * sizeof(int);
+    static_assert((size_t)BM * (BN + 4) * 4 >= (size_t)2 * kWdStage * 2, "LDS sizing");
+    hipLaunchKernelGGL(conv_wgrad_dma_kernel, grid, dim3(kThreads), lds_dma, st, X, dY, target, g,
+                       taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+  } else if (!(tr_mode & 1)) {  // debug path: element-wise LDS reads instead of ds_read_b64_tr_b16
     if (generic) hipLaunchKernelGGL((conv_wgrad_kernel<true, false>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
     else hipLaunchKernelGGL((conv_wgrad_kernel<false, false>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
   } else if (generic) {

@@ -25,10 +25,28 @@ class ConvBN(nn.Module):
         self.bn = BatchNormalization(cout, bn_momentum, bn_eps, name=f"{name}_bn",
                                      gamma_init=0.0 if zero_gamma else 1.0)
 
-    def forward(self, x, relu=True, residual=None, residual_to_conv=False):
+    def forward(self, x, relu=True, residual=None, residual_to_conv=False, grad_share=None):
         y = ops.conv2d(x, self.conv.kernel, self.conv.strides, self.conv.padding,
-                       bn_stats=self.bn.training)
+                       bn_stats=self.bn.training, grad_share=grad_share)
         return self.bn(y, relu=relu, residual=residual, residual_to_conv=residual_to_conv)
+
+
+class StemConvBN(ConvBN):
+    """7x7/2 stem.  On the native path the conv runs as a 4x4 stride-1 conv on the
+    space-to-depth image (ops.reference.space_to_depth_operands); the variable stays the TF
+    [7,7,3,64] kernel (checkpoint key conv1_conv/kernel) and its gradient flows back through the
+    rewrite."""
+
+    def forward(self, x, relu=True, residual=None, residual_to_conv=False, grad_share=None):
+        if not (ops._use_native(x) and self.conv.strides in (2, (2, 2)) and S2D_STEM):
+            return super().forward(x, relu, residual, residual_to_conv, grad_share)
+        from ..ops import reference
+        xs, ws = reference.space_to_depth_operands(x, self.conv.kernel, 2, self.conv.padding)
+        y = ops.conv2d(xs, ws, 1, 0, bn_stats=self.bn.training)
+        return self.bn(y, relu=relu)
+
+
+S2D_STEM = True
 
 
 class Bottleneck(nn.Module):
@@ -45,8 +63,10 @@ class Bottleneck(nn.Module):
         self.c3 = ConvBN(width, cout, 1, 1, f"{name}_3", bn_momentum, bn_eps, zero_gamma)
 
     def forward(self, x):
-        sc = self.proj(x, relu=False) if self.has_proj else x
-        y = self.c1(x)
+        # projection blocks: proj and c1 both read x -> one dgrad buffer, no autograd add
+        share = ops.GradShare(2) if self.has_proj else None
+        sc = self.proj(x, relu=False, grad_share=share) if self.has_proj else x
+        y = self.c1(x, grad_share=share)
         y = self.c2(y)
         # identity shortcut: c1 (1x1, stride 1) also reads x, so its dgrad absorbs d(residual)
         return self.c3(y, relu=True, residual=sc, residual_to_conv=not self.has_proj)
@@ -57,7 +77,7 @@ class ResNet(Layer):
                  bn_momentum=0.997, bn_eps=1e-5, zero_init_residual=False):
         super().__init__()
         with name_scope():
-            self.stem = ConvBN(in_channels, 64, 7, 2, "conv1", bn_momentum, bn_eps)
+            self.stem = StemConvBN(in_channels, 64, 7, 2, "conv1", bn_momentum, bn_eps)
             blocks = []
             cin = 64
             for si, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):

@@ -42,11 +42,24 @@ def _native():
     return native
 
 
-def conv2d(x, w, stride=1, padding=0, bn_stats=False):
+class GradShare:
+    """Marks the convs that read ONE input tensor (a projection block's x feeds both the 1x1
+    shortcut conv and c1): on the native path their data gradients accumulate into one buffer
+    in the dgrad epilogue instead of being summed by autograd with a separate add kernel.
+    Create one per forward call; ``n`` = number of convs sharing the input."""
+
+    def __init__(self, n: int):
+        self.n = n
+        self.left = n
+        self.buf = None
+
+
+def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
     """``bn_stats``: a training-mode batch_norm consumes the result (native path fuses the BN
-    statistics into the conv epilogue; ignored by the reference path)."""
+    statistics into the conv epilogue; ignored by the reference path).  ``grad_share``: a
+    :class:`GradShare` common to every conv reading ``x`` (native path only)."""
     if _use_native(x):
-        return _native().conv2d(x, w, stride, padding, bn_stats)
+        return _native().conv2d(x, w, stride, padding, bn_stats, grad_share)
     return reference.conv2d(x, w, stride, padding)
 
 
@@ -159,7 +172,7 @@ def mlm_loss(logits, labels, weights=None):
 
 
 __all__ = [
-    "set_backend", "get_backend", "conv2d", "batch_norm", "relu", "max_pool2d",
+    "set_backend", "get_backend", "GradShare", "conv2d", "batch_norm", "relu", "max_pool2d",
     "global_avg_pool", "dense", "sparse_softmax_cross_entropy",
     "softmax_cross_entropy_clipped_sum", "layer_norm", "gelu", "attention", "dropout",
     "bias_dropout_add_layer_norm", "embedding_layer_norm", "bias_gelu", "attention_qkv",

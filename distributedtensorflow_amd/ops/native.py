@@ -16,7 +16,7 @@ import os
 
 import torch
 
-from .reference import resolve_padding
+from .reference import resolve_padding, space_to_depth_operands  # noqa: F401
 
 try:
     from .._lib import _dtf_hip as _K  # noqa: N812
@@ -150,8 +150,8 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None):
                 continue
             launches.append((a, b, Pc, Qc, taps, idx))
     acc = out is not None
-    if acc and (need_zero or len(launches) != 1):
-        raise ValueError("accumulating dgrad needs a single-phase (stride-1) conv")
+    # accumulating: phases without taps contribute zero (nothing to add); the phase launches
+    # partition the output, so every element is read-modified-written at most once
     dx = out if acc else (torch.zeros if need_zero else torch.empty)(
         n, h, wd, C, device=dy.device, dtype=_BF16)
     dyc = dy.contiguous()
@@ -199,8 +199,9 @@ def _pad_c8(t):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w_master, stride, padding, stats=None):
+    def forward(ctx, x, w_master, stride, padding, stats=None, share=None):
         xb = x.contiguous()
+        ctx.share = share
         wb = _bf16_weight(w_master)
         ctx.c_orig = xb.shape[-1]
         if xb.shape[-1] % 8:
@@ -237,7 +238,16 @@ class _Conv2d(torch.autograd.Function):
                     dw = None
                 else:
                     dw = dw.to(ctx.w_dtype)
-        if ctx.needs_input_grad[0]:
+        share, ctx.share = ctx.share, None
+        if ctx.needs_input_grad[0] and share is not None and not padded:
+            # several convs read x: the first to run backward creates dx, the others add their
+            # dgrad onto it in the epilogue; only the last hands the sum to autograd
+            dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding, out=share.buf)
+            share.left -= 1
+            share.buf = dx if share.left > 0 else None
+            if share.left > 0:
+                dx = None
+        elif ctx.needs_input_grad[0]:
             pending = getattr(ctx.x_ref, "_dtf_pending_grad", None)
             if pending is not None and not padded and _pair(ctx.stride) == (1, 1):
                 # identity shortcut: the block's final BN left d(residual) here; accumulate this
@@ -252,10 +262,13 @@ class _Conv2d(torch.autograd.Function):
                     del ctx.x_ref._dtf_pending_grad
                     dx = dx + pending
         ctx.x_ref = None
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
-def conv2d(x, w, stride=1, padding=0, bn_stats=False):
+_SHARE_INPUT_GRAD = os.environ.get("DTF_SHARE_INPUT_GRAD", "1") == "1"
+
+
+def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
     """NHWC conv.  ``bn_stats=True`` (a training-mode BatchNorm consumes the output): the conv
     epilogue also emits the BN partial sums, attached to the output as ``_dtf_bn_part`` and picked
     up by :func:`batch_norm`, which then skips its own statistics pass over the tensor."""
@@ -263,13 +276,15 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False):
     K, R, S, C = w.shape
     if K % 8 or R * S > 64:
         raise ValueError(f"native conv2d: unsupported filter {tuple(w.shape)}")
+    if grad_share is not None and (x.shape[-1] % 8 or not _SHARE_INPUT_GRAD):
+        grad_share = None        # channel-padded convs produce their own (sliced) dx
     if not bn_stats:
-        return _Conv2d.apply(x, w, stride, padding, None)
+        return _Conv2d.apply(x, w, stride, padding, None, grad_share)
     n, h, wd, c, P, Q, sh, sw, pt, pl = _conv_geom_fwd(x, K, R, S, stride, padding)
     M = n * P * Q
     G = _K.conv_stats_rows(M, K, c, R * S)
     part = torch.empty(_K.bn_workspace_floats_g(G, K), device=x.device, dtype=torch.float32)
-    y = _Conv2d.apply(x, w, stride, padding, part)
+    y = _Conv2d.apply(x, w, stride, padding, part, grad_share)
     y._dtf_bn_part = (part, G, M, K)
     return y
 
@@ -312,9 +327,13 @@ class _BatchNorm(torch.autograd.Function):
                                  invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), st)
         res = residual.contiguous() if residual is not None else None
         y = torch.empty_like(x)
+        # residual + ReLU: the backward's ReLU mask cannot be recomputed from x alone, so the
+        # apply also writes it as 1 bit per element (1/16 of the bytes of y, read twice)
+        mask = (torch.empty(M * C // 8, device=dev, dtype=torch.uint8)
+                if relu and residual is not None else None)
         _K.bn_apply(x.data_ptr(), _p(res), y.data_ptr(), scale.data_ptr(), shift.data_ptr(), M, C,
-                    int(relu), st)
-        ctx.save_for_backward(x, y, g32, stats)
+                    int(relu), st, _p(mask))
+        ctx.save_for_backward(x, mask, g32, stats)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.gdt, ctx.bdt = gamma.dtype, beta.dtype
@@ -326,7 +345,7 @@ class _BatchNorm(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, g32, stats = ctx.saved_tensors
+        x, mask, g32, stats = ctx.saved_tensors
         dy = dy.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -334,14 +353,13 @@ class _BatchNorm(torch.autograd.Function):
         st = _st()
         mean, invstd = stats[0], stats[1]
         part = torch.empty(_K.bn_workspace_floats(M, C), device=dev, dtype=torch.float32)
-        # ReLU mask: from the saved output when a residual was added before the ReLU, else
-        # recomputed from x with the forward's scale/shift (saves reading y in both passes)
+        # ReLU mask: the forward's bit mask when a residual was added before the ReLU, else
+        # recomputed from x with the forward's scale/shift (neither pass reads y)
         mask_x = ctx.relu and not ctx.has_res
-        y_ptr = 0 if mask_x else y.data_ptr()
         sc_ptr, sh_ptr = (stats[2].data_ptr(), stats[3].data_ptr()) if mask_x else (0, 0)
-        _K.bn_bwd_reduce(dy.data_ptr(), y_ptr, x.data_ptr(), mean.data_ptr(),
+        _K.bn_bwd_reduce(dy.data_ptr(), 0, x.data_ptr(), mean.data_ptr(),
                          invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st,
-                         sc_ptr, sh_ptr)
+                         sc_ptr, sh_ptr, _p(mask))
         gb = torch.empty(5, C, device=dev, dtype=torch.float32)  # dgamma dbeta A B C
         tg, tb = (_direct_grad(p) for p in ctx.params)
         direct = tg is not None and tb is not None
@@ -355,9 +373,9 @@ class _BatchNorm(torch.autograd.Function):
                 _grad_ready(p)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
-        _K.bn_bwd_apply(dy.data_ptr(), y_ptr, x.data_ptr(), gb[2].data_ptr(),
+        _K.bn_bwd_apply(dy.data_ptr(), 0, x.data_ptr(), gb[2].data_ptr(),
                         gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
-                        int(ctx.relu), st, sc_ptr, sh_ptr)
+                        int(ctx.relu), st, sc_ptr, sh_ptr, _p(mask))
         if dres is not None and ctx.res_ref is not None:
             ctx.res_ref._dtf_pending_grad = dres
             dres = None

@@ -274,3 +274,32 @@ def mlm_loss(logits, labels, weights=None):
         return nll.mean()
     w = weights.reshape(-1).float()
     return (w * nll).sum() / w.sum().clamp_min(1e-5)
+
+
+def space_to_depth_operands(x, w, stride, pad):
+    """Rewrite a strided conv (the ResNet stem: 7x7 / 2, pad 3, C = 3) as a stride-1 VALID conv
+    on the space-to-depth input.  Output pixel p reads padded input rows s*p + r, r < R; with
+    r = s*i + a that is row p + i of the s2d image at sub-row a, so
+
+        x' [N, P + R' - 1, Q + S' - 1, s*s*C']  (C' = C zero-padded so s*s*C' % 8 == 0)
+        w' [K, R', S', s*s*C']                  (R' = ceil(R / s), taps past R are zero)
+
+    compute exactly the original conv.  For the stem: 16 taps x 16 channels = K 256 of which
+    147 are real (vs 49 taps x 8 padded channels = 392), and whole 32-B tap rows per pixel.
+    Both rewrites are differentiable torch views/pads (w' keeps autograd back to the master)."""
+    n, h, wd, c = x.shape
+    K, R, S, C = w.shape
+    s = stride
+    P = (h + 2 * pad - R) // s + 1
+    Q = (wd + 2 * pad - S) // s + 1
+    Rp, Sp = -(-R // s), -(-S // s)
+    cp = c
+    while (s * s * cp) % 8:
+        cp += 1
+    Hn, Wn = s * (P + Rp - 1), s * (Q + Sp - 1)
+    xp = torch.nn.functional.pad(x, (0, cp - c, pad, Wn - wd - pad, pad, Hn - h - pad))
+    xs = xp.view(n, Hn // s, s, Wn // s, s, cp).permute(0, 1, 3, 2, 4, 5).reshape(
+        n, Hn // s, Wn // s, s * s * cp)
+    wp = torch.nn.functional.pad(w, (0, cp - C, 0, s * Sp - S, 0, s * Rp - R))
+    ws = wp.view(K, Rp, s, Sp, s, cp).permute(0, 1, 3, 2, 4, 5).reshape(K, Rp, Sp, s * s * cp)
+    return xs.contiguous(), ws

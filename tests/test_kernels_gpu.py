@@ -109,6 +109,40 @@ def test_conv_dma_kernel_bit_identical(case):
     assert _rel(outs[1][0], yr) < 1e-2
 
 
+WGRAD_DMA_CASES = [
+    (2, 56, 56, 64, 64, 3, 1, 1),      # Kout 64 (half tile), 9 taps
+    (2, 28, 28, 128, 128, 3, 2, 1),    # stride 2, padding taps
+    (2, 14, 14, 1024, 256, 1, 1, 0),
+    (3, 9, 11, 128, 384, 3, 1, 1),     # M not a multiple of 64, TC not a multiple of 128
+    (2, 30, 30, 16, 64, 4, 1, 0),      # the space-to-depth stem shape (C 16, 16 taps)
+    (2, 17, 19, 8, 72, 7, 2, 3),       # C 8, 49 taps, Kout 72
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_DMA_CASES)
+def test_wgrad_dma_kernel_bit_identical(case):
+    """LDS-DMA wgrad kernel == the register-staged one (same fragment order -> same bits), and
+    both match the fp32 reference."""
+    N, H, W, C, K, R, stride, pad = case
+    nat, ref = _native(), _ref()
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, P, Q, K, device=dev).to(torch.bfloat16)
+    outs = []
+    try:
+        for mode in (0, 1):
+            nat._K.wgrad_set_dma_mode(mode)
+            outs.append(nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad))
+    finally:
+        nat._K.wgrad_set_dma_mode(-1)
+    assert torch.equal(outs[0], outs[1])
+    wr = torch.zeros(K, R, R, C, device=dev, requires_grad=True)
+    ref.conv2d(x.float(), wr, stride, pad).backward(dy.float())
+    assert _rel(outs[1], wr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("case", [(2, 28, 28, 1, 32, 5, 1, "same"), (2, 64, 64, 3, 64, 7, 2, 3)])
 def test_conv_element_gather_paths(case):
     """The per-element gather kernels (fwd GATHER=1, wgrad GENERIC) on unpadded C=1 / C=3."""
@@ -127,11 +161,14 @@ def test_conv_element_gather_paths(case):
     assert _rel(dw, wr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, True, True), (512, False, False),
-                                        (2048, True, True), (32, True, False)])
-def test_batch_norm(C, relu, res):
+@pytest.mark.parametrize("C,relu,res,shape", [
+    (64, True, False, (4, 7, 9)), (256, True, True, (4, 7, 9)), (512, False, False, (4, 7, 9)),
+    (2048, True, True, (4, 7, 9)), (32, True, False, (4, 7, 9)),
+    # many rows / ragged unroll tails / a channel count that does not divide the block
+    (64, True, True, (3, 37, 41)), (96, True, True, (2, 13, 17)), (128, True, False, (5, 29, 31))])
+def test_batch_norm(C, relu, res, shape):
     torch.manual_seed(1)
-    x = (torch.randn(4, 7, 9, C, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    x = (torch.randn(*shape, C, device=dev) * 2 + 0.5).to(torch.bfloat16)
     r = torch.randn_like(x) if res else None
     gamma = torch.rand(C, device=dev) + 0.5
     beta = torch.randn(C, device=dev)

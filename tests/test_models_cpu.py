@@ -133,3 +133,23 @@ def test_cnn_learns_synthetic_mnist():
             opt.minimize(loss)
             first = first if first is not None else loss.item()
     assert loss.item() < 0.5 * first
+
+
+def test_space_to_depth_stem_rewrite_is_exact():
+    """The stem's 7x7/2 conv == a 4x4/1 VALID conv on the space-to-depth image (forward and the
+    weight gradient mapped back through the rewrite), incl. odd sizes."""
+    from distributedtensorflow_amd.ops import reference as ref
+    torch.manual_seed(0)
+    for (h, w_, c, R, pad) in [(32, 32, 3, 7, 3), (17, 23, 3, 7, 3), (12, 10, 5, 3, 1)]:
+        x = torch.randn(2, h, w_, c, dtype=torch.float64)
+        w = torch.randn(6, R, R, c, dtype=torch.float64, requires_grad=True)
+        y0 = ref.conv2d(x, w, 2, pad)
+        g = torch.randn_like(y0)
+        (gw0,) = torch.autograd.grad((y0 * g).sum(), w)
+        xs, ws = ref.space_to_depth_operands(x, w, 2, pad)
+        assert xs.shape[-1] % 8 == 0 and ws.shape[1] == -(-R // 2)
+        y1 = ref.conv2d(xs, ws, 1, 0)
+        assert y1.shape == y0.shape
+        torch.testing.assert_close(y1, y0)
+        (gw1,) = torch.autograd.grad((y1 * g).sum(), w)
+        torch.testing.assert_close(gw1, gw0)

@@ -22,10 +22,11 @@ def _inputs(n=4, s=64):
     return x.cuda().bfloat16(), y.cuda()
 
 
-def _grads(model, direct, fuse_res=True):
-    prev, prev_r = native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD
+def _grads(model, direct, fuse_res=True, share=True):
+    prev, prev_r, prev_s = native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD, native._SHARE_INPUT_GRAD
     native._DIRECT_GRAD = direct
     native._FUSE_RESIDUAL_GRAD = fuse_res
+    native._SHARE_INPUT_GRAD = share
     try:
         with OneDeviceStrategy("cuda").scope():
             opt = MomentumOptimizer(0.1, 0.9)
@@ -36,6 +37,7 @@ def _grads(model, direct, fuse_res=True):
             return loss.item(), opt.space.grad.clone()
     finally:
         native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD = prev, prev_r
+        native._SHARE_INPUT_GRAD = prev_s
 
 
 def test_direct_grad_path_bit_identical():
@@ -131,5 +133,16 @@ def test_residual_grad_fusion_bit_identical():
     base = resnet50().cuda()
     la, ga = _grads(copy.deepcopy(base), True, fuse_res=True)
     lb, gb = _grads(copy.deepcopy(base), True, fuse_res=False)
+    assert la == lb
+    assert torch.equal(ga, gb)
+
+
+def test_shared_input_dgrad_bit_identical():
+    """Projection blocks: proj's and c1's dgrads accumulated into one buffer in the epilogue ==
+    autograd summing two separate dgrad tensors (round(round(a) + round(b)) either way)."""
+    torch.manual_seed(0)
+    base = resnet50().cuda()
+    la, ga = _grads(copy.deepcopy(base), True, share=True)
+    lb, gb = _grads(copy.deepcopy(base), True, share=False)
     assert la == lb
     assert torch.equal(ga, gb)

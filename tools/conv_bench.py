@@ -18,7 +18,9 @@ PEAK_BW = 5.0e12   # achievable HBM3E (~8 TB/s theoretical)
 
 def resnet50_convs(B):
     """(name, H, W, C, K, R, stride, pad, count) of every conv (v1.5: stride on the 3x3)."""
-    out = [("stem", 224, 224, 3, 64, 7, 2, 3, 1)]
+    # the stem runs as a 4x4/1 VALID conv on the 115x115x16 space-to-depth image
+    # (ops.reference.space_to_depth_operands); the original 7x7/2 form is kept for comparison
+    out = [("stem", 224, 224, 3, 64, 7, 2, 3, 0), ("stem_s2d", 115, 115, 16, 64, 4, 1, 0, 1)]
     cin, res = 64, 56
     for si, (n, w) in enumerate(zip((3, 4, 6, 3), (64, 128, 256, 512))):
         for bi in range(n):
