@@ -484,6 +484,18 @@ void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, c
                      invstd, (int)M, C, rpb, mk, partial, fsc, fsh);
 }
 
+void dtf_bn_bwd_finalize_g(const float* partial, int G, long M, int C, const float* gamma,
+                           const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                           float* coefA, float* coefB, float* coefC, int accumulate,
+                           hipStream_t st) {
+  const int S = combine_slices(G, C);
+  double* level2 = reinterpret_cast<double*>(const_cast<float*>(partial) + (long)G * 2 * C);
+  hipLaunchKernelGGL(bn_combine_kernel, dim3((C + 31) / 32, S), dim3(256), 0, st, partial, G, C,
+                     S, level2);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, level2, S,
+                     C, M, gamma, mean, invstd, dgamma, dbeta, coefA, coefB, coefC, accumulate);
+}
+
 void dtf_bn_bwd_finalize(const float* partial, long M, int C, const float* gamma,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta,
                          float* coefA, float* coefB, float* coefC, int accumulate,

@@ -19,6 +19,10 @@ namespace py = pybind11;
 struct TapTable { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
 struct TapTableW { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
 struct ConvGeom { int N, H, W, C, P, Q, sh, sw, Kout, Kpad, Ho, Wo, osh, osw, oh0, ow0, acc; };
+struct BnBwdEpi {
+  const bf16_t* x; const float* mean; const float* invstd; const float* fsc; const float* fsh;
+  const uint8_t* mask; float* part; int mkind; int row0;
+};
 struct WgradGeom { int N, H, W, C, P, Q, sh, sw, Kout, ldw; long m_per_split; long slab; };
 
 // ---- launchers defined in the .hip translation units
@@ -39,6 +43,8 @@ void dtf_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, uint8_t*, const float*,
 void dtf_bn_bwd_reduce(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, const float*,
                        const float*, long, int, int, float*, const float*, const float*,
                        hipStream_t);
+void dtf_bn_bwd_finalize_g(const float*, int, long, int, const float*, const float*, const float*,
+                           float*, float*, float*, float*, float*, int, hipStream_t);
 void dtf_bn_bwd_finalize(const float*, long, int, const float*, const float*, const float*,
                          float*, float*, float*, float*, float*, int, hipStream_t);
 void dtf_bn_bwd_apply(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, const float*,
@@ -64,7 +70,7 @@ int dtf_lamb_chunk_bytes();
 void dtf_sumsq(const float*, long, float*, hipStream_t);
 void dtf_cast_f32_bf16(const float*, bf16_t*, long, hipStream_t);
 void dtf_conv_igemm(const bf16_t*, const bf16_t*, bf16_t*, const ConvGeom&, const TapTable&, int,
-                    float*, hipStream_t);
+                    float*, const BnBwdEpi&, hipStream_t);
 void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, const TapTableW&,
                     int, int, int, hipStream_t);
 
@@ -259,17 +265,35 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("conv_igemm", [](uintptr_t x, uintptr_t w, uintptr_t y, std::vector<int> geom,
                          std::vector<int> dh, std::vector<int> dw, int bk, uintptr_t st,
-                         uintptr_t stats) {
+                         uintptr_t stats, std::vector<uintptr_t> bnb) {
     if (geom.size() != 16 && geom.size() != 17)
       throw std::runtime_error("conv_igemm: geom needs 16 (+acc) ints");
     ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
                geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15],
                geom.size() == 17 ? geom[16] : 0};
+    // bnb = [x, mean, invstd, fsc, fsh, mask, part, mkind, row0] (fused BN-backward sums) or []
+    BnBwdEpi e{};
+    if (!bnb.empty()) {
+      if (bnb.size() != 9) throw std::runtime_error("conv_igemm: bnb needs 9 entries");
+      e = BnBwdEpi{P<const bf16_t>(bnb[0]), P<const float>(bnb[1]), P<const float>(bnb[2]),
+                   P<const float>(bnb[3]), P<const float>(bnb[4]), P<const uint8_t>(bnb[5]),
+                   P<float>(bnb[6]), (int)bnb[7], (int)bnb[8]};
+    }
     dtf_conv_igemm(P<const bf16_t>(x), P<const bf16_t>(w), P<bf16_t>(y), g,
-                   make_taps<TapTable>(dh, dw), bk, P<float>(stats), S(st));
+                   make_taps<TapTable>(dh, dw), bk, P<float>(stats), e, S(st));
     check_launch("conv_igemm");
   }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("dh"), py::arg("dw"),
-     py::arg("bk"), py::arg("stream"), py::arg("stats") = 0);
+     py::arg("bk"), py::arg("stream"), py::arg("stats") = 0,
+     py::arg("bnb") = std::vector<uintptr_t>{});
+  m.def("bn_bwd_finalize_g", [](uintptr_t part, int G, long M, int C, uintptr_t gamma,
+                                uintptr_t mean, uintptr_t invstd, uintptr_t dg, uintptr_t db,
+                                uintptr_t a, uintptr_t b, uintptr_t c, int accumulate,
+                                uintptr_t st) {
+    dtf_bn_bwd_finalize_g(P<const float>(part), G, M, C, P<const float>(gamma),
+                          P<const float>(mean), P<const float>(invstd), P<float>(dg), P<float>(db),
+                          P<float>(a), P<float>(b), P<float>(c), accumulate, S(st));
+    check_launch("bn_bwd_finalize_g");
+  });
   m.def("conv_wgrad", [](uintptr_t x, uintptr_t dy, uintptr_t dw_out, uintptr_t ws,
                          std::vector<int> geom, std::vector<int> dh, std::vector<int> dw,
                          int splits, uintptr_t st, int tr_mode, int accumulate) {

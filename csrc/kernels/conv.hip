@@ -56,9 +56,94 @@ struct ConvGeom {
   int acc;               // 1: Y += result (dgrad accumulating onto a residual gradient)
 };
 
+// Fused BatchNorm-backward statistics in the DATA-GRADIENT epilogue: when this launch produces
+// dy of a training-mode BN's output (the BN sits right before this conv in the forward pass), the
+// epilogue also accumulates, per channel, sum(dz) and sum(dz * (x - mean) * invstd) with
+// dz = dy * relu_mask(x) -- exactly bn_reduce_kernel<1>'s sums, from the bf16-ROUNDED final dy
+// (after a fused residual accumulation) -- into row `row0 + tile` of a [rows][2][Kout] slab the
+// BN's finalize combines.  Saves the backward reduce pass its full re-read of dy.
+struct BnBwdEpi {
+  const bf16_t* x;          // BN input, same [N, Ho, Wo, Kout] layout as Y
+  const float* mean;
+  const float* invstd;
+  const float* fsc;         // forward scale / shift (mask recomputed from x, mkind 2)
+  const float* fsh;
+  const uint8_t* mask;      // ReLU bit mask (mkind 1)
+  float* part;              // null: off
+  int mkind;                // 0 no ReLU, 1 bit mask, 2 from x
+  int row0;
+};
+
 namespace {
 
 constexpr int kThreads = 256;
+
+DTF_DEV void load8(const float* __restrict__ p, int c, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p + c);
+  const float4 b = *reinterpret_cast<const float4*>(p + c + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// per-thread BN-backward partial sums of one 8-channel column chunk
+struct BnbAcc {
+  float s0[8], s1[8], mu[8], is[8], sc[8], sh[8];
+  DTF_DEV void init(const BnBwdEpi& e, int c, bool ok) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s0[i] = 0.f; s1[i] = 0.f; mu[i] = 0.f; is[i] = 0.f; sc[i] = 0.f; sh[i] = 0.f; }
+    if (!ok) return;
+    load8(e.mean, c, mu);
+    load8(e.invstd, c, is);
+    if (e.mkind == 2) { load8(e.fsc, c, sc); load8(e.fsh, c, sh); }
+  }
+  DTF_DEV void add(const BnBwdEpi& e, long off, const uint4& v) {
+    float g[8], xv[8];
+    unpack8(v, g);
+    unpack8(*reinterpret_cast<const uint4*>(e.x + off), xv);
+    if (e.mkind == 1) {
+      const uint32_t mb = e.mask[off >> 3];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = (mb >> i) & 1u ? g[i] : 0.f;
+    } else if (e.mkind == 2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = __builtin_fmaf(xv[i], sc[i], sh[i]) > 0.f ? g[i] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s0[i] += g[i]; s1[i] += g[i] * (xv[i] - mu[i]) * is[i]; }
+  }
+  // same, with x (and the mask byte) already in registers (prefetched before the LDS staging)
+  DTF_DEV void add_pre(const BnBwdEpi& e, const uint4& v, const uint4& xr, uint32_t mb) {
+    float g[8], xv[8];
+    unpack8(v, g);
+    unpack8(xr, xv);
+    if (e.mkind == 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = (mb >> i) & 1u ? g[i] : 0.f;
+    } else if (e.mkind == 2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = __builtin_fmaf(xv[i], sc[i], sh[i]) > 0.f ? g[i] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s0[i] += g[i]; s1[i] += g[i] * (xv[i] - mu[i]) * is[i]; }
+  }
+  // red: [orows][2][BN] floats; fixed-order column sums -> slab row
+  template <int BN, int NT>
+  DTF_DEV void flush(const BnBwdEpi& e, float* red, int orow, int oc, int orows, int tid, int tm,
+                     int n0, int Kout) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[(orow * 2 + 0) * BN + oc * 8 + i] = s0[i];
+      red[(orow * 2 + 1) * BN + oc * 8 + i] = s1[i];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < 2 * BN; idx += NT) {
+      const int which = idx / BN, col = idx % BN;
+      if (n0 + col >= Kout) continue;
+      float t = 0.f;
+      for (int k = 0; k < orows; ++k) t += red[(k * 2 + which) * BN + col];
+      e.part[((long)(e.row0 + tm) * 2 + which) * Kout + n0 + col] = t;
+    }
+  }
+};
 constexpr uint32_t kOOB = 0xFFFFFFF0u;   // byte offset the buffer range check always rejects
 
 template <int BK>
@@ -78,11 +163,11 @@ DTF_DEV uint32_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
 }
 
-template <int WAVES_M, int WAVES_N, int BK, int GATHER>
+template <int WAVES_M, int WAVES_N, int BK, int GATHER, bool BNB>
 __global__ void __launch_bounds__(kThreads, 2)
 conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                   bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
-                  float* __restrict__ stats) {
+                  float* __restrict__ stats, const BnBwdEpi bnb) {
   constexpr int BM = 64 * WAVES_M, BN = 64 * WAVES_N;
   constexpr int CPR = BK / 8;                            // chunks per row
   constexpr int A_CHUNKS = BM * CPR / kThreads;          // 16-B loads per thread for A
@@ -215,9 +300,46 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   __syncthreads();
 
   const int frow = lane & 15, fq = lane >> 4;
+  // Epilogue rows are decoded up front and, for the fused BN-backward sums, the BN input x (+ mask
+  // bytes) of every row this thread will store is loaded during the LAST K-step: those HBM reads
+  // overlap its MFMAs and the LDS staging instead of stalling the store loop.  The barriers from
+  // there to the store loop are raw s_barriers behind lgkmcnt(0) (a __syncthreads() would drain
+  // vmcnt, i.e. wait for the prefetch).
+  constexpr int OCPR = BN / 8;                 // 16-B chunks per output row
+  constexpr int OROWS = kThreads / OCPR;
+  constexpr int NR = BM / OROWS;               // rows per thread
+  const int oc = tid % OCPR;
+  const bool col_ok = n0 + oc * 8 < g.Kout;
+  // output element offset of this thread's k-th epilogue row (-1: none); int32 (host-checked)
+  auto row_off = [&](int k) -> int {
+    const int m = m0 + tid / OCPR + k * OROWS;
+    const int q = m % g.Q;
+    const int t = m / g.Q;
+    const int p = t % g.P;
+    const int n = t / g.P;
+    const int ho = p * g.osh + g.oh0, wo = q * g.osw + g.ow0;
+    return (m < M && col_ok) ? ((n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8 : -1;
+  };
+  int offs[NR];
+  uint4 xpre[BNB ? NR : 1];
+  uint32_t mpre[BNB ? (NR + 3) / 4 : 1];       // the rows' mask bytes, 4 per register
+  auto prefetch_epilogue = [&]() {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) offs[k] = row_off(k);
+#pragma unroll
+    for (int k = 0; k < (NR + 3) / 4; ++k) mpre[k] = 0u;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      xpre[k] = offs[k] >= 0 ? *reinterpret_cast<const uint4*>(bnb.x + offs[k]) : make_uint4(0, 0, 0, 0);
+      if (offs[k] >= 0 && bnb.mkind == 1) mpre[k >> 2] |= (uint32_t)bnb.mask[offs[k] >> 3] << (8 * (k & 3));
+    }
+  };
+  if constexpr (BNB) { if (nk == 0) prefetch_epilogue(); }
+
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) load_stage(kt + 1);
+    else if constexpr (BNB) prefetch_epilogue();
     const bf16_t* sa = lds + cur * STAGE_ELEMS;
     const bf16_t* sb = sa + BM * BK;
 #pragma unroll
@@ -240,11 +362,19 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_stage(cur ^ 1);
-    __syncthreads();
+    if (kt + 1 < nk) {
+      store_stage(cur ^ 1);
+      __syncthreads();
+    }
   }
+  if constexpr (!BNB) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) offs[k] = row_off(k);
+  }
+  // every wave is done reading the last stage before the staging below overwrites it
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
 
-  // ---- epilogue: acc -> bf16 LDS tile [BM][BN + 8] -> coalesced 16-B stores
   // (explicit wait states between the MFMA chain and the first consumer of its results)
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -261,20 +391,15 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
         const int col = wn * 64 + j * 16 + frow;
         st[row * LDC + col] = f2bf(acc[i][j][r]);
       }
-  __syncthreads();
-  constexpr int OCPR = BN / 8;                 // 16-B chunks per output row
-  constexpr int OROWS = kThreads / OCPR;
-  const int oc = tid % OCPR;
-  const bool col_ok = n0 + oc * 8 < g.Kout;
-  for (int r = tid / OCPR; r < BM; r += OROWS) {
-    const int m = m0 + r;
-    if (m >= M || !col_ok) continue;
-    const int q = m % g.Q;
-    const int t = m / g.Q;
-    const int p = t % g.P;
-    const int n = t / g.P;
-    const int ho = p * g.osh + g.oh0, wo = q * g.osw + g.ow0;
-    const long off = (((long)n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+  BnbAcc ba;
+  if constexpr (BNB) ba.init(bnb, n0 + oc * 8, col_ok);
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    if (offs[k] < 0) continue;
+    const int r = tid / OCPR + k * OROWS;
+    const long off = offs[k];
     uint4 v = *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
     if (g.acc) {   // fused residual-gradient add: one extra 16-B read instead of an add kernel
       float a[8], b[8];
@@ -285,7 +410,11 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
       v = pack8(a);
     }
     *reinterpret_cast<uint4*>(Y + off) = v;
+    if constexpr (BNB) ba.add_pre(bnb, v, xpre[k], (mpre[k >> 2] >> (8 * (k & 3))) & 0xFFu);
   }
+  if constexpr (BNB)
+    ba.template flush<BN, kThreads>(bnb, reinterpret_cast<float*>(st + BM * LDC), tid / OCPR, oc,
+                                    OROWS, tid, tm, n0, g.Kout);
   if (stats) {
     // Fused BatchNorm statistics (training forward): per output channel, sum and sum of
     // squares of this tile's bf16-ROUNDED outputs (exactly what the BN will normalise), written
@@ -317,16 +446,26 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
 
 template <int WM, int WN, int BK, int GEN>
 void launch_cfg(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
-                const TapTable& taps, float* stats, hipStream_t st) {
+                const TapTable& taps, float* stats, const BnBwdEpi& bnb, hipStream_t st) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int OROWS = kThreads / (BN / 8);
   const long M = (long)g.N * g.P * g.Q;
   const long tiles = ((M + BM - 1) / BM) * ((g.Kout + BN - 1) / BN);
   const size_t stage = (size_t)(BM + BN) * BK * sizeof(bf16_t) * 2 + 2 * DTF_MAX_TAPS * sizeof(int);
+  const size_t scratch = bnb.part ? (size_t)OROWS * 2 * BN : (size_t)2 * kThreads;
   const size_t epi = (size_t)BM * (BN + 8) * sizeof(bf16_t) +
-                    (size_t)2 * kThreads * sizeof(float);          // + stats reduction scratch
+                    scratch * sizeof(float);          // + stats / BN-backward reduction scratch
   const size_t lds = stage > epi ? stage : epi;
-  hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN>), dim3((unsigned)tiles), dim3(kThreads),
-                     lds, st, X, Wt, Y, g, taps, stats);
+  if (bnb.part) {
+    if constexpr (GEN == 0)
+      hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, true>), dim3((unsigned)tiles),
+                         dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
+    else
+      throw std::runtime_error("conv: fused BN-backward sums need a C % 32 == 0 dgrad");
+  } else {
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, false>), dim3((unsigned)tiles),
+                       dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -342,10 +481,11 @@ constexpr int kDmaThreads = 512;
 constexpr int kDmaBM = 256, kDmaBN = 128, kDmaBK = 64;
 constexpr int kDmaA = kDmaBM * kDmaBK;                    // A elements per stage
 constexpr int kDmaStage = (kDmaBM + kDmaBN) * kDmaBK;     // 24576 bf16 = 48 KB
+template <bool BNB>
 __global__ void __launch_bounds__(kDmaThreads, 1)
 conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                       bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
-                      float* __restrict__ stats) {
+                      float* __restrict__ stats, const BnBwdEpi bnb) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[3 * kDmaStage];
   bf16_t* const s0 = lds;
   bf16_t* const s1 = lds + kDmaStage;
@@ -461,8 +601,34 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
   }
 
   // ---- epilogue (as conv_igemm_kernel): rows 0..127 of the tile staged in s0, 128..255 in s1
-  DTF_WAIT_VM(0);
-  __syncthreads();
+  constexpr int OCPR = kDmaBN / 8;
+  constexpr int OROWS = kDmaThreads / OCPR;
+  constexpr int NR = kDmaBM / OROWS;
+  const int oc = tid % OCPR;
+  const bool col_ok = n0 + oc * 8 < g.Kout;
+  long offs[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const int m = m0 + tid / OCPR + k * OROWS;
+    const int q = m % g.Q;
+    const int t = m / g.Q;
+    const int p = t % g.P;
+    const int n = t / g.P;
+    const int ho = p * g.osh + g.oh0, wo = q * g.osw + g.ow0;
+    offs[k] = (m < M && col_ok) ? (((long)n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8 : -1;
+  }
+  uint4 xpre[BNB ? NR : 1];
+  uint32_t mpre[BNB ? NR : 1];
+  DTF_WAIT_VM(0);              // the trailing (out-of-range) DMAs still target the LDS stages
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+  if constexpr (BNB) {         // BN input rows in flight while the tile is staged
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      xpre[k] = offs[k] >= 0 ? *reinterpret_cast<const uint4*>(bnb.x + offs[k]) : make_uint4(0, 0, 0, 0);
+      mpre[k] = (offs[k] >= 0 && bnb.mkind == 1) ? (uint32_t)bnb.mask[offs[k] >> 3] : 0u;
+    }
+  }
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -480,20 +646,15 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
           st[row * LDC + col] = f2bf(acc[i][j][r]);
         }
   }
-  __syncthreads();
-  constexpr int OCPR = kDmaBN / 8;
-  constexpr int OROWS = kDmaThreads / OCPR;
-  const int oc = tid % OCPR;
-  const bool col_ok = n0 + oc * 8 < g.Kout;
-  for (int r = tid / OCPR; r < kDmaBM; r += OROWS) {
-    const int m = m0 + r;
-    if (m >= M || !col_ok) continue;
-    const int q = m % g.Q;
-    const int t = m / g.Q;
-    const int p = t % g.P;
-    const int n = t / g.P;
-    const int ho = p * g.osh + g.oh0, wo = q * g.osw + g.ow0;
-    const long off = (((long)n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+  BnbAcc ba;
+  if constexpr (BNB) ba.init(bnb, n0 + oc * 8, col_ok);
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    if (offs[k] < 0) continue;
+    const int r = tid / OCPR + k * OROWS;
+    const long off = offs[k];
     const bf16_t* st = r < 128 ? s0 : s1;
     uint4 v = *reinterpret_cast<const uint4*>(st + (r & 127) * LDC + oc * 8);
     if (g.acc) {
@@ -505,7 +666,11 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
       v = pack8(a);
     }
     *reinterpret_cast<uint4*>(Y + off) = v;
+    if constexpr (BNB) ba.add_pre(bnb, v, xpre[k], mpre[k]);
   }
+  if constexpr (BNB)   // [32][2][128] floats = 32 KB in the third stage buffer
+    ba.template flush<kDmaBN, kDmaThreads>(bnb, reinterpret_cast<float*>(s2), tid / OCPR, oc,
+                                           OROWS, tid, tm, n0, g.Kout);
   if (stats) {   // fused BN partial sums, same contract as conv_igemm_kernel (row tm of the slab)
     constexpr int GROUPS = kDmaThreads / kDmaBN;     // 4 groups of 64 rows
     constexpr int RPG = kDmaBM / GROUPS;
@@ -559,7 +724,13 @@ int dtf_conv_stats_rows(long M, int Kout, int C, int taps) {
 }
 
 void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
-                    const TapTable& taps, int bk, float* stats, hipStream_t st) {
+                    const TapTable& taps, int bk, float* stats, const BnBwdEpi& bnb,
+                    hipStream_t st) {
+  if (bnb.part && (double)g.N * g.Ho * g.Wo * g.Kout >= 2147483647.0)
+    throw std::runtime_error("conv: fused BN-backward epilogue needs a < 2^31-element output");
+  if (bnb.part && (stats || !bnb.x || !bnb.mean || !bnb.invstd ||
+                   (bnb.mkind == 1 && !bnb.mask) || (bnb.mkind == 2 && !(bnb.fsc && bnb.fsh))))
+    throw std::runtime_error("conv: bad fused BN-backward epilogue arguments");
   if (taps.n <= 0 || taps.n > DTF_MAX_TAPS) throw std::runtime_error("conv: bad tap count");
   if (g.Kout % 8) throw std::runtime_error("conv: Kout % 8 != 0");
   const double xbytes = 2.0 * g.N * g.H * g.W * g.C, wbytes = 2.0 * g.Kout * g.Kpad;
@@ -570,25 +741,29 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
   if (g.C % 32 != 0) {
     if (g.Kpad % 32) throw std::runtime_error("conv: Kpad % 32 != 0");
     if (g.C % 8 == 0) {                    // chunk gather (stem / MNIST conv1, C padded to 8)
-      if (narrow) launch_cfg<4, 1, 32, 2>(X, Wt, Y, g, taps, stats, st);
-      else launch_cfg<2, 2, 32, 2>(X, Wt, Y, g, taps, stats, st);
+      if (narrow) launch_cfg<4, 1, 32, 2>(X, Wt, Y, g, taps, stats, bnb, st);
+      else launch_cfg<2, 2, 32, 2>(X, Wt, Y, g, taps, stats, bnb, st);
     } else {
-      if (narrow) launch_cfg<4, 1, 32, 1>(X, Wt, Y, g, taps, stats, st);
-      else launch_cfg<2, 2, 32, 1>(X, Wt, Y, g, taps, stats, st);
+      if (narrow) launch_cfg<4, 1, 32, 1>(X, Wt, Y, g, taps, stats, bnb, st);
+      else launch_cfg<2, 2, 32, 1>(X, Wt, Y, g, taps, stats, bnb, st);
     }
     return;
   }
   if (use_dma_kernel((long)m, g.Kout, g.C, taps.n, bk) && g.Kpad % 64 == 0) {
     const long tiles = (((long)m + kDmaBM - 1) / kDmaBM) * (g.Kout / kDmaBN);
-    hipLaunchKernelGGL(conv_igemm_dma_kernel, dim3((unsigned)tiles), dim3(kDmaThreads), 0, st,
-                       X, Wt, Y, g, taps, stats);
+    if (bnb.part)
+      hipLaunchKernelGGL(conv_igemm_dma_kernel<true>, dim3((unsigned)tiles), dim3(kDmaThreads), 0,
+                         st, X, Wt, Y, g, taps, stats, bnb);
+    else
+      hipLaunchKernelGGL(conv_igemm_dma_kernel<false>, dim3((unsigned)tiles), dim3(kDmaThreads), 0,
+                         st, X, Wt, Y, g, taps, stats, bnb);
     return;
   }
   if (bk == 64 && g.C % 64 == 0) {
-    if (narrow) launch_cfg<4, 1, 64, 0>(X, Wt, Y, g, taps, stats, st);
-    else launch_cfg<2, 2, 64, 0>(X, Wt, Y, g, taps, stats, st);
+    if (narrow) launch_cfg<4, 1, 64, 0>(X, Wt, Y, g, taps, stats, bnb, st);
+    else launch_cfg<2, 2, 64, 0>(X, Wt, Y, g, taps, stats, bnb, st);
   } else {
-    if (narrow) launch_cfg<4, 1, 32, 0>(X, Wt, Y, g, taps, stats, st);
-    else launch_cfg<2, 2, 32, 0>(X, Wt, Y, g, taps, stats, st);
+    if (narrow) launch_cfg<4, 1, 32, 0>(X, Wt, Y, g, taps, stats, bnb, st);
+    else launch_cfg<2, 2, 32, 0>(X, Wt, Y, g, taps, stats, bnb, st);
   }
 }

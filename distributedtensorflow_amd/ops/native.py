@@ -91,7 +91,7 @@ def _conv_geom_fwd(x, K, R, S, stride, padding):
 
 
 def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
-                stats=None, accumulate=False):
+                stats=None, accumulate=False, bnb=()):
     """wmat: [K, T*C] bf16 (rows zero-padded here to a multiple of 32 for the gather path)."""
     n, h, w, c = x.shape
     dh = [t[0] for t in taps]
@@ -104,7 +104,7 @@ def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0
         wmat = padded
     geom = [n, h, w, c, P, Q, sh, sw, K, kpad, Ho, Wo, osh, osw, oh0, ow0, int(accumulate)]
     _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
-                  _p(stats))
+                  _p(stats), list(bnb))
 
 
 def conv2d_forward(x, w_bf16, stride, padding, stats=None):
@@ -119,9 +119,11 @@ def conv2d_forward(x, w_bf16, stride, padding, stats=None):
     return y
 
 
-def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None):
+def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None):
     """dX of conv2d via per-phase-class tap tables (see csrc/kernels/conv.hip header).
-    ``out``: an existing bf16 gradient of x to ADD into (stride-1 convs only)."""
+    ``out``: an existing bf16 gradient of x to ADD into.  ``bnb``: the BatchNorm whose output x
+    is (its ``_dtf_bnb`` record): the epilogue then also emits that BN's backward partial sums,
+    attached to the result as ``_dtf_bnb_part`` (see :class:`_BatchNorm`)."""
     K, R, S, C = w_bf16.shape
     n, h, wd, c = x_shape
     sh, sw = _pair(stride)
@@ -155,14 +157,31 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None):
     dx = out if acc else (torch.zeros if need_zero else torch.empty)(
         n, h, wd, C, device=dy.device, dtype=_BF16)
     dyc = dy.contiguous()
-    for a, b, Pc, Qc, taps, idx in launches:
+    part, row0 = None, 0
+    if bnb is not None:
+        xb, stats, mask, relu, has_res, tok = bnb
+        rows = [_K.conv_stats_rows(n * Pc * Qc, C, K, len(taps))
+                for (_, _, Pc, Qc, taps, _) in launches]
+        G = sum(rows)
+        part = torch.empty(_K.bn_workspace_floats_g(G, C), device=dy.device, dtype=torch.float32)
+        mkind = (1 if has_res else 2) if relu else 0
+        fsc, fsh = (stats[2].data_ptr(), stats[3].data_ptr()) if mkind == 2 else (0, 0)
+        base = [xb.data_ptr(), stats[0].data_ptr(), stats[1].data_ptr(), fsc, fsh,
+                _p(mask) if mkind == 1 else 0, part.data_ptr(), mkind]
+    for li, (a, b, Pc, Qc, taps, idx) in enumerate(launches):
         if len(idx) == R * S and sh == 1 and sw == 1:
             sel = wflat
         else:
             sel = wflat[:, torch.tensor(idx, device=dy.device), :]
         wd_mat = sel.permute(2, 1, 0).contiguous()           # [C, T, K]
+        extra = ()
+        if part is not None:
+            extra = base + [row0]
+            row0 += rows[li]
         _launch_fwd(dyc, wd_mat.reshape(C, -1), C, taps, Pc, Qc, 1, 1, dx, h, wd, sh, sw, a, b,
-                    accumulate=acc)
+                    accumulate=acc, bnb=extra)
+    if part is not None:
+        dx._dtf_bnb_part = (part, G, n * h * wd, C, tok)
     return dx
 
 
@@ -213,6 +232,8 @@ class _Conv2d(torch.autograd.Function):
         ctx.w_dtype = w_master.dtype
         ctx.w_param = w_master
         ctx.x_ref = x            # a residual BN may stash its residual gradient on x
+        bnb = getattr(x, "_dtf_bnb", None)
+        ctx.bnb = bnb if (_FUSE_BN_BWD and bnb is not None and xb is x) else None
         return conv2d_forward(xb, wb, stride, padding, stats)
 
     @staticmethod
@@ -242,7 +263,9 @@ class _Conv2d(torch.autograd.Function):
         if ctx.needs_input_grad[0] and share is not None and not padded:
             # several convs read x: the first to run backward creates dx, the others add their
             # dgrad onto it in the epilogue; only the last hands the sum to autograd
-            dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding, out=share.buf)
+            last = share.left == 1
+            dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding, out=share.buf,
+                              bnb=ctx.bnb if last else None)
             share.left -= 1
             share.buf = dx if share.left > 0 else None
             if share.left > 0:
@@ -253,19 +276,27 @@ class _Conv2d(torch.autograd.Function):
                 # identity shortcut: the block's final BN left d(residual) here; accumulate this
                 # conv's dgrad onto it in the epilogue instead of a separate bf16 add kernel
                 del ctx.x_ref._dtf_pending_grad
-                dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding, out=pending)
+                dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding, out=pending,
+                                  bnb=ctx.bnb)
             else:
-                dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding)
+                dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding,
+                                  bnb=ctx.bnb if pending is None and not padded else None)
                 if padded:
                     dx = dx[..., :C].contiguous()
                 if pending is not None:
                     del ctx.x_ref._dtf_pending_grad
                     dx = dx + pending
         ctx.x_ref = None
+        ctx.bnb = None
         return dx, dw, None, None, None, None
 
 
 _SHARE_INPUT_GRAD = os.environ.get("DTF_SHARE_INPUT_GRAD", "1") == "1"
+# BatchNorm backward sums fused into the consuming conv's dgrad epilogue.  Off by default:
+# measured on MI355X (ResNet-50 b512) the epilogue's extra read of the BN input costs the dgrad
+# kernels as much time (+3.8 ms/step) as the separate reduce pass it removes (-3.9 ms/step) --
+# the 1x1 dgrads are bandwidth-bound, and the streaming reduce runs at ~5.3 TB/s.
+_FUSE_BN_BWD = os.environ.get("DTF_FUSE_BN_BWD", "0") == "1"
 
 
 def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
@@ -336,6 +367,10 @@ class _BatchNorm(torch.autograd.Function):
         ctx.save_for_backward(x, mask, g32, stats)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        if training:
+            # a conv consuming y computes this BN's backward sums in its dgrad epilogue
+            ctx.bnb_token = object()
+            y._dtf_bnb = (x, stats, mask, relu, residual is not None, ctx.bnb_token)
         ctx.gdt, ctx.bdt = gamma.dtype, beta.dtype
         ctx.params = (gamma, beta)
         # identity-shortcut blocks: hand d(residual) to the conv that also reads the residual
@@ -352,22 +387,34 @@ class _BatchNorm(torch.autograd.Function):
         dev = x.device
         st = _st()
         mean, invstd = stats[0], stats[1]
-        part = torch.empty(_K.bn_workspace_floats(M, C), device=dev, dtype=torch.float32)
         # ReLU mask: the forward's bit mask when a residual was added before the ReLU, else
         # recomputed from x with the forward's scale/shift (neither pass reads y)
         mask_x = ctx.relu and not ctx.has_res
         sc_ptr, sh_ptr = (stats[2].data_ptr(), stats[3].data_ptr()) if mask_x else (0, 0)
-        _K.bn_bwd_reduce(dy.data_ptr(), 0, x.data_ptr(), mean.data_ptr(),
-                         invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st,
-                         sc_ptr, sh_ptr, _p(mask))
+        fused = getattr(dy, "_dtf_bnb_part", None)
+        tok = getattr(ctx, "bnb_token", None)
+        if fused is not None and tok is not None and fused[4] is tok and fused[2:4] == (M, C):
+            # sums already produced by the dgrad epilogue of the conv that consumed y
+            part, G = fused[0], fused[1]
+        else:
+            part, G = torch.empty(_K.bn_workspace_floats(M, C), device=dev,
+                                  dtype=torch.float32), None
+            _K.bn_bwd_reduce(dy.data_ptr(), 0, x.data_ptr(), mean.data_ptr(),
+                             invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st,
+                             sc_ptr, sh_ptr, _p(mask))
         gb = torch.empty(5, C, device=dev, dtype=torch.float32)  # dgamma dbeta A B C
         tg, tb = (_direct_grad(p) for p in ctx.params)
         direct = tg is not None and tb is not None
         dg_ptr, db_ptr = ((tg.data_ptr(), tb.data_ptr()) if direct
                           else (gb[0].data_ptr(), gb[1].data_ptr()))
-        _K.bn_bwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), mean.data_ptr(),
-                           invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(), gb[3].data_ptr(),
-                           gb[4].data_ptr(), int(direct), st)
+        if G is None:
+            _K.bn_bwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), mean.data_ptr(),
+                               invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
+                               gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
+        else:
+            _K.bn_bwd_finalize_g(part.data_ptr(), G, M, C, g32.data_ptr(), mean.data_ptr(),
+                                 invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
+                                 gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
         if direct:
             for p in ctx.params:
                 _grad_ready(p)
