@@ -46,6 +46,11 @@ def parse():
     p.add_argument("--model", choices=("resnet50", "bert_base"), default="resnet50",
                    help="resnet50: the headline metric; bert_base: BASELINE config 5 "
                         "(MLM, LAMB, MultiWorkerMirroredStrategy) in tokens/sec")
+    p.add_argument("--strategy", choices=("mirrored", "ps"), default="mirrored",
+                   help="mirrored: MirroredStrategy (bucketed RCCL all-reduce overlapped with "
+                        "backward); ps: BASELINE config 4, colocated synchronous "
+                        "ParameterServerStrategy (--num-ps owner ranks; 1 = '1 PS + N workers')")
+    p.add_argument("--num-ps", type=int, default=1)
     p.add_argument("--seq-len", type=int, default=128)
     p.add_argument("--max-predictions", type=int, default=20)
     args = p.parse_args()
@@ -66,7 +71,11 @@ def build_dtf(args, dev):
     from distributedtensorflow_amd.parallel import MirroredStrategy
     from distributedtensorflow_amd.train import get_or_create_global_step
 
-    strategy = MirroredStrategy(bucket_mb=args.bucket_mb)
+    if args.strategy == "ps":
+        from distributedtensorflow_amd.parallel import ParameterServerStrategy
+        strategy = ParameterServerStrategy(num_ps=args.num_ps)
+    else:
+        strategy = MirroredStrategy(bucket_mb=args.bucket_mb)
     with strategy.scope():
         model = resnet50()
         model.train()
@@ -264,7 +273,9 @@ def main():
             "dtype": "bf16", "data": "synthetic (random NHWC 224x224x3 images, random labels; "
                                       "random-init weights)",
             "config": {"model": "resnet50", "global_batch": B * world, "per_gpu_batch": B,
-                       "seq_len": None, "image_size": S, "parallelism": f"dp{world}",
+                       "seq_len": None, "image_size": S,
+                       "parallelism": (f"dp{world}" if args.strategy == "mirrored" else
+                                       f"ps{min(args.num_ps, world)}+dp{world}"),
                        "impl": args.impl, "optimizer": "momentum0.9+wd1e-4, lr 0.1*B/256 warmup500+cosine",
                        "final_loss": round(final_loss, 4)},
         }

@@ -91,9 +91,9 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const LnArgs g) {
     const int col = (i * 64 + lane) * 4;
     if (g.a) {
       load4(g.a + base + col, v[i]);
-      if (g.bias) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[i][e] += g.bias[col + e];
+      if (g.bias) {   // one 16-B load for the 4 columns (was 4 scalar loads)
+        const float4 b4 = *reinterpret_cast<const float4*>(g.bias + col);
+        v[i][0] += b4.x; v[i][1] += b4.y; v[i][2] += b4.z; v[i][3] += b4.w;
       }
       if (g.thr_pre) {
 #pragma unroll
@@ -138,9 +138,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const LnArgs g) {
     const int col = (i * 64 + lane) * 4;
     if (g.s) store4(g.s + base + col, v[i]);
     float o[4];
+    const float4 g4 = *reinterpret_cast<const float4*>(g.gamma + col);
+    const float4 be4 = *reinterpret_cast<const float4*>(g.beta + col);
+    const float gm[4] = {g4.x, g4.y, g4.z, g4.w}, bt[4] = {be4.x, be4.y, be4.z, be4.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      o[e] = (v[i][e] - mean) * rstd * g.gamma[col + e] + g.beta[col + e];
+      o[e] = (v[i][e] - mean) * rstd * gm[e] + bt[e];
       if (g.thr_post)
         o[e] = keep_elem(g.seed_post, (uint32_t)(base + col + e), g.thr_post)
                    ? o[e] * g.inv_keep_post : 0.f;
@@ -181,6 +184,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs g) {
     for (int e = 0; e < 4; ++e) ag[i][e] = ab[i][e] = abias[i][e] = 0.f;
   const int r0 = blockIdx.x * g.rows_per_block;
   const int r1 = min(g.M, r0 + g.rows_per_block);
+  float gm[NV][4];           // gamma of this lane's columns, loaded once (not per row)
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float4 g4 = *reinterpret_cast<const float4*>(g.gamma + (i * 64 + lane) * 4);
+    gm[i][0] = g4.x; gm[i][1] = g4.y; gm[i][2] = g4.z; gm[i][3] = g4.w;
+  }
   for (int row = r0 + wave; row < r1; row += 4) {
     const long base = (long)row * H;
     const float mean = g.mean[row], rstd = g.rstd[row];
@@ -198,7 +207,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs g) {
           dy[i][e] = keep_elem(g.seed_post, (uint32_t)(base + col + e), g.thr_post)
                          ? dy[i][e] * g.inv_keep_post : 0.f;
         xh[i][e] = (sv[e] - mean) * rstd;
-        gy[i][e] = dy[i][e] * g.gamma[col + e];
+        gy[i][e] = dy[i][e] * gm[i][e];
         s1 += gy[i][e];
         s2 += gy[i][e] * xh[i][e];
       }
@@ -392,17 +401,45 @@ DTF_DEV float gelu_grad(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluK0 * (1.f + 3.f * kGeluK1 * x * x);
 }
 
+// Row sweep (as bias_gelu_bwd_kernel): block = R rows x all columns, a thread owns column vectors
+// cv = tid + 256 j with the bias in registers and keeps 4 rows' 16-B loads in flight (the r1
+// one-vector-per-thread form did a 32-bit modulo and 8 scalar bias loads per vector and ran at
+// ~2.3 TB/s on the BERT FFN activation).
 __global__ void __launch_bounds__(256)
 bias_gelu_fwd_kernel(const bf16_t* __restrict__ a, const float* __restrict__ bias,
-                     bf16_t* __restrict__ y, long n8, int N) {
-  const int i = blockIdx.x * 256 + threadIdx.x;        // host guarantees n8 < 2^31
-  if (i >= n8) return;
-  const int col = (i % (N >> 3)) * 8;
-  float f[8];
-  unpack8(((const uint4*)a)[i], f);
+                     bf16_t* __restrict__ y, int M, int N, int R) {
+  constexpr int U = 4;
+  const int nv = N / 8;
+  const int r0 = blockIdx.x * R, r1 = min(M, r0 + R);
+  const uint4* A4 = reinterpret_cast<const uint4*>(a);
+  uint4* Y4 = reinterpret_cast<uint4*>(y);
+  for (int cv = threadIdx.x; cv < nv; cv += 256) {
+    float bb[8];
+    if (bias) {
+      const float4 b0 = reinterpret_cast<const float4*>(bias)[cv * 2];
+      const float4 b1 = reinterpret_cast<const float4*>(bias)[cv * 2 + 1];
+      bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+      bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+    } else {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) f[e] = gelu_f(f[e] + (bias ? bias[col + e] : 0.f));
-  ((uint4*)y)[i] = pack8(f);
+      for (int e = 0; e < 8; ++e) bb[e] = 0.f;
+    }
+    for (int r = r0; r < r1; r += U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (r + u < r1) v[u] = A4[(uint32_t)(r + u) * nv + cv];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (r + u >= r1) break;
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = gelu_f(f[e] + bb[e]);
+        Y4[(uint32_t)(r + u) * nv + cv] = pack8(f);
+      }
+    }
+  }
 }
 
 // block = (row tile of R rows) x (all columns); thread owns column vectors cv = tid + 256*j
@@ -894,8 +931,11 @@ void dtf_bias_gelu_fwd(const bf16_t* a, const float* bias, bf16_t* y, long M, in
   if (N % 8) throw std::runtime_error("bias_gelu: N % 8 != 0");
   const long n8 = M * N / 8;
   if (n8 >= 2147483647L) throw std::runtime_error("bias_gelu: tensor too large");
-  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st,
-                     a, bias, y, n8, N);
+  // ~1-2 blocks per CU-slot: R rows each (R a multiple of the 4-row unroll)
+  int R = (int)((M + 2047) / 2048);
+  R = ((R + 3) / 4) * 4;
+  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3((unsigned)((M + R - 1) / R)), dim3(256), 0, st,
+                     a, bias, y, (int)M, N, R);
 }
 
 static int bias_gelu_rows(int M) { return (M + 15) / 16; }

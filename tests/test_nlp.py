@@ -185,9 +185,9 @@ def test_embedding_layer_norm_gpu():
 
 
 @pytest.mark.gpu
-def test_bias_gelu_gpu():
+@pytest.mark.parametrize("M,N", [(257, 3072), (16390, 768)])
+def test_bias_gelu_gpu(M, N):
     torch.manual_seed(0)
-    M, N = 257, 3072
     a32, bias, dy = torch.randn(M, N) * 2, torch.randn(N), torch.randn(M, N)
     a, b = _leaf(a32), _leaf(bias, torch.float32)
     y, (da, db) = _grads_of(lambda: ops.bias_gelu(a, b), [a, b], dy.cuda().bfloat16())

@@ -17,6 +17,7 @@ for s in ${STEPS:-kernels bn bench prof}; do
     bert) timeout -k 10 300 python -u bench.py --model bert_base --steps 20 --warmup 5 > "$OUT/bench_bert.log" 2>&1 || exit $? ;;
     smoke) timeout -k 10 300 python -u __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1 || exit $? ;;
     prof) SKIP_TORCH=1 PROF_NAME=iter timeout -k 10 700 bash tools/prof_bench.sh || exit $? ;;
+    bertprof) SKIP_TORCH=1 PROF_NAME=bert DTF_BENCH_ARGS="--model bert_base" timeout -k 10 700 bash tools/prof_bench.sh || exit $? ;;
   esac
   echo "step $s ok"
 done
