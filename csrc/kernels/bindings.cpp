@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -23,6 +24,15 @@ struct BnBwdEpi {
   const bf16_t* x; const float* mean; const float* invstd; const float* fsc; const float* fsh;
   const uint8_t* mask; float* part; int mkind; int row0;
 };
+constexpr int kWtMaxJobs = 48;
+struct WtJobs {
+  const bf16_t* src[kWtMaxJobs];
+  bf16_t* dst[kWtMaxJobs];
+  int K[kWtMaxJobs], T[kWtMaxJobs], C[kWtMaxJobs];
+  int tile_end[kWtMaxJobs];
+  int n;
+};
+void dtf_filter_transpose(const WtJobs&, hipStream_t);
 struct WgradGeom { int N, H, W, C, P, Q, sh, sw, Kout, ldw; long m_per_split; long slab; };
 
 // ---- launchers defined in the .hip translation units
@@ -36,6 +46,7 @@ void dtf_bn_fwd_finalize_g(const float*, int, long, int, const float*, const flo
 long dtf_bn_workspace_floats_g(int, int);
 int dtf_conv_stats_rows(long, int, int, int);
 void dtf_conv_set_dma_mode(int);
+void dtf_conv_set_small_k(int);
 void dtf_bn_infer_finalize(int, const float*, const float*, const float*, const float*, float,
                            float*, float*, float*, float*, hipStream_t);
 void dtf_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, uint8_t*, const float*, const float*,
@@ -131,6 +142,31 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("conv_stats_rows", &dtf_conv_stats_rows, py::arg("M"), py::arg("Kout"), py::arg("C") = 0,
         py::arg("taps") = 1);
   m.def("conv_set_dma_mode", &dtf_conv_set_dma_mode);
+  m.def("filter_transpose", [](std::vector<uintptr_t> src, std::vector<uintptr_t> dst,
+                               std::vector<int> K, std::vector<int> T, std::vector<int> C,
+                               uintptr_t st) {
+    // [K][T][C] -> [C][T][K] for every job, kWtMaxJobs per launch
+    const size_t n = src.size();
+    if (dst.size() != n || K.size() != n || T.size() != n || C.size() != n)
+      throw std::runtime_error("filter_transpose: ragged job lists");
+    for (size_t b = 0; b < n; b += kWtMaxJobs) {
+      WtJobs j{};
+      int tiles = 0;
+      j.n = (int)std::min(n - b, (size_t)kWtMaxJobs);
+      for (int i = 0; i < j.n; ++i) {
+        const size_t q = b + i;
+        if (K[q] <= 0 || T[q] <= 0 || C[q] <= 0) throw std::runtime_error("filter_transpose: bad dims");
+        j.src[i] = P<const bf16_t>(src[q]);
+        j.dst[i] = P<bf16_t>(dst[q]);
+        j.K[i] = K[q]; j.T[i] = T[q]; j.C[i] = C[q];
+        tiles += T[q] * ((K[q] + 63) / 64) * ((C[q] + 63) / 64);
+        j.tile_end[i] = tiles;
+      }
+      dtf_filter_transpose(j, S(st));
+      check_launch("filter_transpose");
+    }
+  });
+  m.def("conv_set_small_k", &dtf_conv_set_small_k);
   m.def("bn_fwd_finalize_g", [](uintptr_t part, int G, long M, int C, uintptr_t gamma,
                                 uintptr_t beta, uintptr_t rm, uintptr_t rv, float mom, float eps,
                                 uintptr_t mean, uintptr_t invstd, uintptr_t scale, uintptr_t shift,

@@ -62,6 +62,10 @@ struct ConvGeom {
 // dz = dy * relu_mask(x) -- exactly bn_reduce_kernel<1>'s sums, from the bf16-ROUNDED final dy
 // (after a fused residual accumulation) -- into row `row0 + tile` of a [rows][2][Kout] slab the
 // BN's finalize combines.  Saves the backward reduce pass its full re-read of dy.
+// bit 0: one LDS stage when the whole reduction is one K-step; bit 1: BK 32 for 1x1 convs with
+// C <= 128 (see dtf_conv_igemm)
+static int g_small_k = 3;   // both on: measured -4..-6 % on the stage-1/2 1x1 convs (b512)
+
 struct BnBwdEpi {
   const bf16_t* x;          // BN input, same [N, Ho, Wo, Kout] layout as Y
   const float* mean;
@@ -451,7 +455,12 @@ void launch_cfg(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
   constexpr int OROWS = kThreads / (BN / 8);
   const long M = (long)g.N * g.P * g.Q;
   const long tiles = ((M + BM - 1) / BM) * ((g.Kout + BN - 1) / BN);
-  const size_t stage = (size_t)(BM + BN) * BK * sizeof(bf16_t) * 2 + 2 * DTF_MAX_TAPS * sizeof(int);
+  // one K-step (1x1 convs with C <= BK, the stage-1 layers): only stage 0 is ever filled, so size
+  // the LDS for one stage -> 3 blocks/CU (VGPR-bound) instead of 2 on these latency-bound shapes
+  const int nk = (taps.n * g.C + BK - 1) / BK;
+  const size_t stage = (size_t)(BM + BN) * BK * sizeof(bf16_t) *
+                           ((nk > 1 || GEN != 0 || !(g_small_k & 1)) ? 2 : 1) +
+                       2 * DTF_MAX_TAPS * sizeof(int);
   const size_t scratch = bnb.part ? (size_t)OROWS * 2 * BN : (size_t)2 * kThreads;
   const size_t epi = (size_t)BM * (BN + 8) * sizeof(bf16_t) +
                     scratch * sizeof(float);          // + stats / BN-backward reduction scratch
@@ -705,6 +714,7 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
 // workspace sizing; must mirror the tile choice in dtf_conv_igemm.
 // -1: automatic, 0: never the DMA kernel, 1: whenever legal (benchmarks / tests)
 static int g_conv_dma_mode = -1;
+void dtf_conv_set_small_k(int mode) { g_small_k = mode; }
 void dtf_conv_set_dma_mode(int mode) { g_conv_dma_mode = mode; }
 
 // The 8-wave DMA kernel needs C % 64 == 0 (one tap per K-step) and 128-wide output tiles.
@@ -759,6 +769,9 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
                          st, X, Wt, Y, g, taps, stats, bnb);
     return;
   }
+  // small-K 1x1 convs (one or two 64-deep K-steps: latency-bound blocks): optionally BK 32 with
+  // 16-KB stages -> more blocks per CU (g_small_k bit 1; A/B-measured by tools/conv_bench.py)
+  if ((g_small_k & 2) && taps.n == 1 && g.C <= 128) bk = 32;
   if (bk == 64 && g.C % 64 == 0) {
     if (narrow) launch_cfg<4, 1, 64, 0>(X, Wt, Y, g, taps, stats, bnb, st);
     else launch_cfg<2, 2, 64, 0>(X, Wt, Y, g, taps, stats, bnb, st);
@@ -766,4 +779,56 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
     if (narrow) launch_cfg<4, 1, 32, 0>(X, Wt, Y, g, taps, stats, bnb, st);
     else launch_cfg<2, 2, 32, 0>(X, Wt, Y, g, taps, stats, bnb, st);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Batched filter transpose for the data gradient: every conv's bf16 filter [K][T][C] -> [C][T][K]
+// (the dgrad GEMM's B operand) in ONE launch per step instead of one torch copy kernel per conv
+// (53 launches / ResNet-50 step).  Block = one 64 x 64 (k, c) tile of one tap of one filter,
+// staged through a padded LDS tile so both the reads (along c) and the writes (along k) are
+// coalesced.  Jobs are found by a scan of the (<= kWtMaxJobs) cumulative tile counts.
+constexpr int kWtMaxJobs = 48;
+struct WtJobs {
+  const bf16_t* src[kWtMaxJobs];
+  bf16_t* dst[kWtMaxJobs];
+  int K[kWtMaxJobs], T[kWtMaxJobs], C[kWtMaxJobs];
+  int tile_end[kWtMaxJobs];     // exclusive prefix sum of T * ceil(K/64) * ceil(C/64)
+  int n;
+};
+
+namespace {
+__global__ void __launch_bounds__(256) filter_transpose_kernel(const WtJobs jobs) {
+  __shared__ bf16_t tile[64][66];
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j < jobs.n - 1 && b >= jobs.tile_end[j]) ++j;     // wave-uniform scan
+  const int start = j ? jobs.tile_end[j - 1] : 0;
+  const int K = jobs.K[j], T = jobs.T[j], C = jobs.C[j];
+  const int tk = (K + 63) / 64, tc = (C + 63) / 64;
+  const int local = b - start;
+  const int t = local / (tk * tc);
+  const int rem = local % (tk * tc);
+  const int k0 = (rem / tc) * 64, c0 = (rem % tc) * 64;
+  const bf16_t* src = jobs.src[j];
+  bf16_t* dst = jobs.dst[j];
+  const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;   // 64 columns x 4 rows per pass
+#pragma unroll 4
+  for (int r = ly; r < 64; r += 4) {
+    const int k = k0 + r, c = c0 + lx;
+    tile[r][lx] = (k < K && c < C) ? src[((long)k * T + t) * C + c] : (bf16_t)0;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int r = ly; r < 64; r += 4) {
+    const int c = c0 + r, k = k0 + lx;
+    if (c < C && k < K) dst[((long)c * T + t) * K + k] = tile[lx][r];
+  }
+}
+}  // namespace
+
+void dtf_filter_transpose(const WtJobs& jobs, hipStream_t st) {
+  if (jobs.n <= 0) return;
+  if (jobs.n > kWtMaxJobs) throw std::runtime_error("filter_transpose: too many jobs");
+  hipLaunchKernelGGL(filter_transpose_kernel, dim3((unsigned)jobs.tile_end[jobs.n - 1]), dim3(256),
+                     0, st, jobs);
 }

@@ -119,6 +119,46 @@ def conv2d_forward(x, w_bf16, stride, padding, stats=None):
     return y
 
 
+# ---- batched dgrad filters: every conv forward registers its bf16 filter; the first data-gradient
+# of the step transposes ALL registered filters [K,T,C] -> [C,T,K] in one launch
+# (csrc/kernels/conv.hip filter_transpose_kernel) instead of one copy kernel per conv.  Keyed by
+# the shadow's data_ptr (the optimizer rewrites the shadow in place once per step, after backward);
+# a forward re-registration invalidates the previous step's copy.
+_WT_PENDING = {}
+_WT_CACHE = {}
+_BATCH_WT = os.environ.get("DTF_BATCH_FILTER_T", "1") == "1"
+
+
+def _register_dgrad_filter(wb):
+    if _BATCH_WT:
+        key = wb.data_ptr()
+        _WT_CACHE.pop(key, None)
+        _WT_PENDING[key] = wb
+
+
+def _dgrad_filter(wflat):
+    """[K, T, C] bf16 filter -> contiguous [C, T, K]."""
+    key = wflat.data_ptr()
+    t = _WT_CACHE.get(key)
+    if t is not None and t.shape == (wflat.shape[2], wflat.shape[1], wflat.shape[0]):
+        return t
+    if key in _WT_PENDING:
+        items = list(_WT_PENDING.values())
+        _WT_PENDING.clear()
+        _WT_CACHE.clear()            # bounded: only the current step's filters are kept
+        outs = [torch.empty(w.shape[3], w.shape[1] * w.shape[2], w.shape[0], device=w.device,
+                            dtype=_BF16) for w in items]
+        _K.filter_transpose([w.data_ptr() for w in items], [o.data_ptr() for o in outs],
+                            [w.shape[0] for w in items], [w.shape[1] * w.shape[2] for w in items],
+                            [w.shape[3] for w in items], _st())
+        for w, o in zip(items, outs):
+            _WT_CACHE[w.data_ptr()] = o
+        t = _WT_CACHE.get(key)
+        if t is not None and t.shape == (wflat.shape[2], wflat.shape[1], wflat.shape[0]):
+            return t
+    return wflat.permute(2, 1, 0).contiguous()
+
+
 def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None):
     """dX of conv2d via per-phase-class tap tables (see csrc/kernels/conv.hip header).
     ``out``: an existing bf16 gradient of x to ADD into.  ``bnb``: the BatchNorm whose output x
@@ -169,11 +209,11 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None):
         base = [xb.data_ptr(), stats[0].data_ptr(), stats[1].data_ptr(), fsc, fsh,
                 _p(mask) if mkind == 1 else 0, part.data_ptr(), mkind]
     for li, (a, b, Pc, Qc, taps, idx) in enumerate(launches):
-        if len(idx) == R * S and sh == 1 and sw == 1:
-            sel = wflat
+        if len(idx) == R * S:
+            wd_mat = _dgrad_filter(wflat)                      # [C, T, K]
         else:
             sel = wflat[:, torch.tensor(idx, device=dy.device), :]
-        wd_mat = sel.permute(2, 1, 0).contiguous()           # [C, T, K]
+            wd_mat = sel.permute(2, 1, 0).contiguous()
         extra = ()
         if part is not None:
             extra = base + [row0]
@@ -234,6 +274,8 @@ class _Conv2d(torch.autograd.Function):
         ctx.x_ref = x            # a residual BN may stash its residual gradient on x
         bnb = getattr(x, "_dtf_bnb", None)
         ctx.bnb = bnb if (_FUSE_BN_BWD and bnb is not None and xb is x) else None
+        if x.requires_grad and xb is x and wb.is_contiguous():
+            _register_dgrad_filter(wb)
         return conv2d_forward(xb, wb, stride, padding, stats)
 
     @staticmethod

@@ -279,3 +279,18 @@ def test_bf16_col_sum(T, N):
     nat._K.bf16_col_sum(x.data_ptr(), T, N, ws.data_ptr(), out.data_ptr(), 1,
                         torch.cuda.current_stream().cuda_stream)
     torch.testing.assert_close(out, x.float().sum(0) + 2.0, atol=1e-3, rtol=1e-4)
+
+
+def test_batched_filter_transpose():
+    """filter_transpose_kernel: [K,T,C] -> [C,T,K] for a batch of ragged filters (> 48 jobs ->
+    two launches), exactly equal to torch's permute."""
+    nat = _native()
+    torch.manual_seed(0)
+    shapes = [(64, 9, 64), (72, 1, 40), (256, 9, 128), (8, 49, 8), (2048, 1, 512)] * 11
+    ws = [torch.randn(k, t, c, device=dev).to(torch.bfloat16) for k, t, c in shapes]
+    outs = [torch.empty(c, t, k, device=dev, dtype=torch.bfloat16) for k, t, c in shapes]
+    nat._K.filter_transpose([w.data_ptr() for w in ws], [o.data_ptr() for o in outs],
+                            [s[0] for s in shapes], [s[1] for s in shapes], [s[2] for s in shapes],
+                            torch.cuda.current_stream().cuda_stream)
+    for w, o in zip(ws, outs):
+        assert torch.equal(o, w.permute(2, 1, 0))

@@ -63,8 +63,13 @@ def main():
     ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
     ap.add_argument("--dma", type=int, default=-1,
                     help="conv kernel choice: -1 auto, 0 register-staged only, 1 LDS-DMA when legal")
+    ap.add_argument("--small-k", type=int, default=None,
+                    help="conv_set_small_k bitmask (1: one LDS stage for single-K-step convs, "
+                         "2: BK 32 for 1x1 convs with C <= 128)")
     args = ap.parse_args()
     native._K.conv_set_dma_mode(args.dma)
+    if args.small_k is not None:
+        native._K.conv_set_small_k(args.small_k)
     only = set(args.only.split(",")) if args.only else None
     kinds = set(args.kinds.split(","))
     B = args.batch
