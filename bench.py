@@ -36,8 +36,10 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=None,
-                   help="per-GPU batch (default 512 for ResNet-50: 288 GB HBM per MI355X; "
-                        "128 sequences for BERT)")
+                   help="per-GPU batch (default 1024 for ResNet-50: 41 GB of the 288 GB HBM3E; "
+                        "measured sweep 512/640/768/1024/1280 -> 10.26k/10.57k/10.67k/10.85k/"
+                        "10.99k img/s: larger batches amortise launches and fill the 256 CUs "
+                        "with whole tile rounds; 128 sequences for BERT)")
     p.add_argument("--impl", choices=("dtf", "torch"), default="dtf")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--lr", type=float, default=0.1)
@@ -55,7 +57,7 @@ def parse():
     p.add_argument("--max-predictions", type=int, default=20)
     args = p.parse_args()
     if args.batch is None:
-        args.batch = 128 if args.model == "bert_base" else 512
+        args.batch = 128 if args.model == "bert_base" else 1024
     return args
 
 
@@ -277,7 +279,8 @@ def main():
                        "parallelism": (f"dp{world}" if args.strategy == "mirrored" else
                                        f"ps{min(args.num_ps, world)}+dp{world}"),
                        "impl": args.impl, "optimizer": "momentum0.9+wd1e-4, lr 0.1*B/256 warmup500+cosine",
-                       "final_loss": round(final_loss, 4)},
+                       "final_loss": round(final_loss, 4),
+                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1)},
         }
         print(json.dumps(rec), flush=True)
     if world > 1:
