@@ -45,11 +45,15 @@ class ConfigProto:
         self.extra = kw
 
     def apply(self):
+        # clamp to the CPUs this process may use (utils.cpu.usable_cpus): the reference passes
+        # os.cpu_count(), which on a shared many-core GPU host is far above the CPU quota
+        from ..utils.cpu import usable_cpus
+        cap = usable_cpus()
         if self.intra_op_parallelism_threads:
-            torch.set_num_threads(int(self.intra_op_parallelism_threads))
+            torch.set_num_threads(min(int(self.intra_op_parallelism_threads), cap))
         if self.inter_op_parallelism_threads:
             try:
-                torch.set_num_interop_threads(int(self.inter_op_parallelism_threads))
+                torch.set_num_interop_threads(min(int(self.inter_op_parallelism_threads), cap))
             except RuntimeError:
                 pass   # can only be set once per process
 

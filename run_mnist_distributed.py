@@ -98,6 +98,8 @@ def main():
     tf_config = ConfigProto(allow_soft_placement=True,
                             intra_op_parallelism_threads=os.cpu_count(),
                             inter_op_parallelism_threads=os.cpu_count())
+    import time
+    t_start, first_step = None, None
     with MonitoredTrainingSession(master=server.target, is_chief=is_chief,
                                   checkpoint_dir=FLAGS.checkpoint_dir, config=tf_config,
                                   hooks=hooks, model=model, optimizer=opt,
@@ -109,6 +111,8 @@ def main():
             logs = logger.TensorBoardOutputFormat(dir=log_directory)
             print("Logging to", log_directory, flush=True)
         while not mon_sess.should_stop():
+            if t_start is None:
+                t_start = time.time()
             if is_chief:
                 out = mon_sess.run([train_op, "loss", global_step])
                 if out is None:
@@ -121,6 +125,9 @@ def main():
                 mon_sess.run(train_op)
     if is_chief:
         logs.close()
+        if t_start is not None:
+            # reference template prints the same (templates/00_mnist_replica.py:265)
+            print("Training elapsed time: %.2f s" % (time.time() - t_start), flush=True)
     server.shutdown()
 
 

@@ -144,3 +144,20 @@ def test_tensorboard_writer_reference_signature(tmp_path):
     tb.close()
     sc = read_scalars(str(tmp_path))
     assert sc["Loss"] == [(5, 0.5), (6, 0.25)]
+
+
+def test_usable_cpus_clamps_thread_pools(monkeypatch):
+    """ConfigProto(intra_op_parallelism_threads=os.cpu_count()) (the reference's setting) must
+    not oversubscribe a CPU quota: threads are clamped to usable_cpus()."""
+    import torch
+
+    from distributedtensorflow_amd.train import ConfigProto
+    from distributedtensorflow_amd.utils.cpu import usable_cpus
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    assert usable_cpus() <= 2
+    prev = torch.get_num_threads()
+    try:
+        ConfigProto(intra_op_parallelism_threads=4096).apply()
+        assert torch.get_num_threads() <= 2
+    finally:
+        torch.set_num_threads(prev)
