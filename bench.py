@@ -191,6 +191,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # one process per GPU: split the CPU quota between the node's ranks (torch's default pool is
+    # sized by the whole machine and oversubscribes a shared host; see utils/cpu.py)
+    from distributedtensorflow_amd.utils.cpu import usable_cpus
+    per_node = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    torch.set_num_threads(max(1, usable_cpus() // max(per_node, 1)))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 and not dist.is_initialized():

@@ -85,7 +85,7 @@ void dtf_conv_igemm(const bf16_t*, const bf16_t*, bf16_t*, const ConvGeom&, cons
 void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, const TapTableW&,
                     int, int, int, hipStream_t);
 
-int dtf_conv_wgrad_splits(long, int, int, long);
+int dtf_conv_wgrad_splits(long, int, int, long, int);
 void dtf_wgrad_set_dma_mode(int);
 void dtf_lds_probe(int, int, int*, int, hipStream_t);
 int dtf_max_dynamic_lds(int);
@@ -342,7 +342,8 @@ PYBIND11_MODULE(_dtf_hip, m) {
   }, py::arg("x"), py::arg("dy"), py::arg("dw_out"), py::arg("ws"), py::arg("geom"),
      py::arg("dh"), py::arg("dw"), py::arg("splits"), py::arg("stream"), py::arg("tr_mode") = 1,
      py::arg("accumulate") = 0);
-  m.def("conv_wgrad_splits", &dtf_conv_wgrad_splits);
+  m.def("conv_wgrad_splits", &dtf_conv_wgrad_splits, py::arg("M"), py::arg("Kout"), py::arg("TC"),
+        py::arg("ws_cap"), py::arg("taps") = 1);
   m.def("wgrad_set_dma_mode", &dtf_wgrad_set_dma_mode);
   m.def("lds_probe", [](int bytes, int blocks, uintptr_t errors, int spin, uintptr_t st) {
     dtf_lds_probe(bytes, blocks, P<int>(errors), spin, S(st));

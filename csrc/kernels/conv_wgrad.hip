@@ -257,10 +257,19 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
 // -> the 8 rows land on the 8 distinct 32-B bank groups of a 256-B bank row.  The DMA writes
 // lane-linearly, so the swizzle is applied on the SOURCE side (lane in slot s fetches chunk
 // s ^ swz(r)).  Pixel -> (n, p, q) uses an fp32 reciprocal divmod (exact for m < 2^24).
-constexpr int kWdStage = 2 * BKM * 128;      // bf16 elements per stage (A + B image)
-
-DTF_DEV int wswz(int r) { return (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
-DTF_DEV int lds_el(int r, int c) { return r * 128 + (((c >> 3) ^ wswz(r)) << 3) + (c & 7); }
+// Row widths of the two images depend on the wave layout (WM x WN waves of 64 x 64): 128-wide
+// tiles (2 x 2, the default) give 256-B rows; the narrow layout for Kout <= 64 (1 x 4: 64 x 256
+// tile, no half-empty M tile) gives 128-B dY rows and 512-B X rows.  Conflict-free swizzles for
+// the tr-read half {rows 0-3, 8-11} x one 32-B column pair:
+//   256 / 512-B rows (bank-row aligned): slot = c ^ 2 * ((r & 3) | ((r >> 3) & 1) << 2)
+//   128-B rows (two rows per bank row):  slot = c ^ 2 * (((r >> 1) & 1) | ((r >> 3) & 1) << 1)
+template <int ROWB>
+DTF_DEV int wswz(int r) {
+  if constexpr (ROWB == 128) return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1;
+  else return (((r & 3) | (((r >> 3) & 1) << 2)) << 1);
+}
+template <int W>   // W = row width in elements
+DTF_DEV int lds_el(int r, int c) { return r * W + (((c >> 3) ^ wswz<W * 2>(r)) << 3) + (c & 7); }
 DTF_DEV void fdivmod(int m, int d, float inv, int& q, int& r) {
   const int t = (int)((float)m * inv);
   const int rem = m - t * d;
@@ -269,17 +278,31 @@ DTF_DEV void fdivmod(int m, int d, float inv, int& q, int& r) {
   r = rem - adj * d;
 }
 
+template <int WM, int WN>
+struct WdCfg {
+  static constexpr int BMw = 64 * WM, BNw = 64 * WN;          // dY cols (Kout), X cols (T*C)
+  static constexpr int RPI_A = 1024 / (BMw * 2), RPI_B = 1024 / (BNw * 2);   // rows / 1-KB DMA
+  static constexpr int IA = BKM / RPI_A / 4, IB = BKM / RPI_B / 4;           // DMAs per wave
+  static constexpr int STAGE = BKM * (BMw + BNw);                            // bf16 per stage
+  static constexpr int LDO = BNw + 4;
+  static constexpr size_t LDS = (size_t)(2 * STAGE * 2) > (size_t)(BMw * LDO * 4)
+                                    ? (size_t)(2 * STAGE * 2) : (size_t)(BMw * LDO * 4);
+};
+
+template <int WM, int WN>
 __global__ void __launch_bounds__(kThreads, 2)
 conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                       float* __restrict__ dW, const WgradGeom g, const TapTableW taps,
                       float invQ, float invP) {
+  using Cf = WdCfg<WM, WN>;
+  constexpr int BMw = Cf::BMw, BNw = Cf::BNw;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int TC = taps.n * g.C;
-  const int tiles_m = (g.Kout + BM - 1) / BM;
-  const int tiles_n = (TC + BN - 1) / BN;
+  const int tiles_m = (g.Kout + BMw - 1) / BMw;
+  const int tiles_n = (TC + BNw - 1) / BNw;
   const int ntiles = tiles_m * tiles_n;
   // XCD-aware: consecutive logical ids (same split, neighbouring tiles -> the same pixel rows of
   // X / dY) share an XCD's L2
@@ -287,7 +310,7 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
   const int tile = bid % ntiles;
   const int split = bid / ntiles;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
-  const int k0 = tm * BM, j0 = tn * BN;
+  const int k0 = tm * BMw, j0 = tn * BNw;
   const int M = g.N * g.P * g.Q;
   const int ms = split * (int)g.m_per_split;
   const int me = min(ms + (int)g.m_per_split, M);
@@ -295,25 +318,31 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
   const i32x4_t rx = rsrc_quad(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
   const i32x4_t ry = rsrc_quad(dY, (uint32_t)M * g.Kout * 2u);
   const uint32_t lds0 = lds_addr(lds);
-  // tap table -> LDS (past the epilogue tile) so per-lane lookups never index the kernarg struct
-  int* lds_taps = reinterpret_cast<int*>(reinterpret_cast<float*>(lds) + BM * (BN + 4));
+  // tap table -> LDS (read once below, before any DMA reuses the space) so per-lane lookups
+  // never index the kernarg struct
+  int* lds_taps = reinterpret_cast<int*>(lds);
   if (tid == 0)
     for (int t = 0; t < taps.n; ++t) { lds_taps[t] = taps.dh[t]; lds_taps[DTF_MAX_TAPS + t] = taps.dw[t]; }
   __syncthreads();
 
-  // DMA plan: per stage and operand 16 wave-instructions of 4 rows x 16 chunks; wave w issues
-  // instructions q = w + 4i (i < 4) of each operand -> rows 4q + (lane >> 4), LDS slot lane & 15.
-  // Per lane everything that does not change with the K-step is precomputed: the dY column and
-  // row offset, and the X tap offset / tap displacement of the chunk it fetches.
-  const int lrow = lane >> 4, slot = lane & 15;
-  int rowv[4], a_off[4], b_dh[4], b_dw[4], b_toff[4];
+  // DMA plan: per stage the dY image is 64 / RPI_A wave-instructions of RPI_A rows, the X image
+  // 64 / RPI_B; wave w issues instructions q = w + 4i of each.  Per lane everything that does not
+  // change with the K-step is precomputed: the dY column / row offset and the X tap offset and
+  // tap displacement of the chunk it fetches.
+  int rowa[Cf::IA], a_off[Cf::IA], rowb[Cf::IB], b_dh[Cf::IB], b_dw[Cf::IB], b_toff[Cf::IB];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 4 * (wave + 4 * i) + lrow;
-    rowv[i] = r;
-    const int chunk = slot ^ wswz(r);
+  for (int i = 0; i < Cf::IA; ++i) {
+    const int r = Cf::RPI_A * (wave + 4 * i) + lane / (BMw / 8);
+    rowa[i] = r;
+    const int chunk = (lane % (BMw / 8)) ^ wswz<BMw * 2>(r);
     const int kc = k0 + chunk * 8;
     a_off[i] = kc < g.Kout ? (r * g.Kout + kc) * 2 : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < Cf::IB; ++i) {
+    const int r = Cf::RPI_B * (wave + 4 * i) + lane / (BNw / 8);
+    rowb[i] = r;
+    const int chunk = (lane % (BNw / 8)) ^ wswz<BNw * 2>(r);
     const int jc = j0 + chunk * 8;
     if (jc < TC) {
       const int t = jc / g.C;
@@ -327,13 +356,13 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
       b_toff[i] = 0;
     }
   }
+  __syncthreads();                // the tap table is dead: stage 0 may now be filled
   const int HW = g.H * g.W;
-  const uint32_t a_step = (uint32_t)BKM * g.Kout * 2u;
 
-  // Each lane decodes ONE pixel of the K-step (row = lane); the 16 lanes that fetch a row's
-  // chunks get its decode by ds_bpermute -- 1 divmod pair per lane per step instead of 4.
+  // Each lane decodes ONE pixel of the K-step (row = lane); the lanes that fetch a row's chunks
+  // get its decode by ds_bpermute -- one divmod pair per lane per step.
   auto issue = [&](int kt, int stage) {
-    const uint32_t base = lds0 + (uint32_t)(stage * kWdStage) * 2u;
+    const uint32_t base = lds0 + (uint32_t)(stage * Cf::STAGE) * 2u;
     const int mk = ms + kt * BKM;                     // wave-uniform first pixel of the step
     const int live = me - mk;                         // rows < live are inside this split
     const int mp = mk + lane;
@@ -346,19 +375,21 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
     const int hw = (hb << 16) | wb;
     const uint32_t a_base = (uint32_t)mk * g.Kout * 2u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = rowv[i];
+    for (int i = 0; i < Cf::IA; ++i) {
+      const int r = rowa[i];
+      const uint32_t ao = (r < live && a_off[i] >= 0) ? a_base + (uint32_t)a_off[i] : kOOB;
+      dma16(ry, base + (uint32_t)(wave + 4 * i) * 1024u, ao);
+    }
+#pragma unroll
+    for (int i = 0; i < Cf::IB; ++i) {
+      const int r = rowb[i];
       const int hwr = __shfl(hw, r, 64);
       const int pbr = __shfl(pb, r, 64);
       const int h = (hwr >> 16) + b_dh[i], w = (hwr & 0xFFFF) + b_dw[i];
       const bool bok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
       const uint32_t bo = bok ? (uint32_t)(pbr + b_toff[i]) : kOOB;
-      const uint32_t ao = (r < live && a_off[i] >= 0) ? a_base + (uint32_t)a_off[i] : kOOB;
-      const uint32_t inst = (uint32_t)(wave + 4 * i) * 1024u;
-      dma16(ry, base + inst, ao);
-      dma16(rx, base + (uint32_t)(BKM * 128 * 2) + inst, bo);
+      dma16(rx, base + (uint32_t)(BKM * BMw * 2) + (uint32_t)(wave + 4 * i) * 1024u, bo);
     }
-    (void)a_step;
   };
 
   f32x4_t acc[4][4];
@@ -374,8 +405,8 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
     DTF_WAIT_VM(0);            // this wave's DMAs of step kt landed ...
     __syncthreads();           // ... and everyone's; everyone also finished reading step kt-1
     if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-    const bf16_t* sa = lds + (kt & 1) * kWdStage;
-    const bf16_t* sb = sa + BKM * 128;
+    const bf16_t* sa = lds + (kt & 1) * Cf::STAGE;
+    const bf16_t* sb = sa + BKM * BMw;
 #pragma unroll
     for (int ks = 0; ks < BKM / 32; ++ks) {
       bf16x8_t af[4], bfr[4];
@@ -383,15 +414,15 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c0 = wm * 64 + 16 * i + 4 * tp;
-        const s4_t lo = tr_read(sa + lds_el(r0, c0));
-        const s4_t hi = tr_read(sa + lds_el(r0 + 4, c0));
+        const s4_t lo = tr_read(sa + lds_el<BMw>(r0, c0));
+        const s4_t hi = tr_read(sa + lds_el<BMw>(r0 + 4, c0));
         af[i] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c0 = wn * 64 + 16 * j + 4 * tp;
-        const s4_t lo = tr_read(sb + lds_el(r0, c0));
-        const s4_t hi = tr_read(sb + lds_el(r0 + 4, c0));
+        const s4_t lo = tr_read(sb + lds_el<BNw>(r0, c0));
+        const s4_t hi = tr_read(sb + lds_el<BNw>(r0 + 4, c0));
         bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
@@ -406,7 +437,7 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  constexpr int LDO = BN + 4;
+  constexpr int LDO = Cf::LDO;
   float* so = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -419,8 +450,8 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
       }
   __syncthreads();
   float* out = dW + (long)split * g.slab;
-  for (int idx = tid; idx < BM * BN; idx += kThreads) {
-    const int r = idx / BN, c = idx % BN;
+  for (int idx = tid; idx < BMw * BNw; idx += kThreads) {
+    const int r = idx / BNw, c = idx % BNw;
     const int row = k0 + r, col = j0 + c;
     if (row < g.Kout && col < TC) out[(long)row * g.ldw + col] = so[r * LDO + c];
   }
@@ -460,11 +491,20 @@ slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n
 // -1 / 1: LDS-DMA kernel whenever legal (default), 0: the register-staged kernel (A/B tests)
 static int g_wgrad_dma_mode = -1;
 void dtf_wgrad_set_dma_mode(int mode) { g_wgrad_dma_mode = mode; }
+// 1 x 4 waves (64 x 256 tile) for multi-tap Kout <= 64 layers (stage-1 3x3, the stem): the 2 x 2
+// tile would leave half its MFMA rows empty.  Measured (tools/wgrad_ab.sh, b512): stem 611 ->
+// 493 us, 3x3 337 -> 288 us, but the bandwidth-bound 1x1 layers are 11-20 % slower with it, so
+// they keep 2 x 2.  Mode 2 disables it (A/B tests).
+static bool wgrad_narrow(int Kout, int taps) {
+  return g_wgrad_dma_mode != 2 && Kout <= 64 && taps > 1;
+}
 
 // Number of reduction splits: aim for ~1024 blocks (4 per CU), keep >= 4 K-steps per split and
 // the fp32 slab workspace (splits x Kout x TC) under `ws_cap` floats.
-int dtf_conv_wgrad_splits(long M, int Kout, int TC, long ws_cap) {
-  const long tiles = (long)((Kout + BM - 1) / BM) * ((TC + BN - 1) / BN);
+int dtf_conv_wgrad_splits(long M, int Kout, int TC, long ws_cap, int taps) {
+  const bool nar = wgrad_narrow(Kout, taps);
+  const int bm = nar ? 64 : BM, bn = nar ? 256 : BN;
+  const long tiles = (long)((Kout + bm - 1) / bm) * ((TC + bn - 1) / bn);
   // never overshoot 1024 = exactly two rounds of 512 block slots (2 blocks x 256 CUs): one block
   // past a round costs a whole extra round (29 splits x 36 tiles = 1044 blocks ran 3 rounds)
   long splits = 1024 / tiles;
@@ -500,18 +540,24 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   const int nsplit = (int)((M + mps - 1) / mps);
   if (nsplit != splits) throw std::runtime_error("wgrad: split plan mismatch");
   float* target = via_ws ? ws : dW;
-  const long tiles = (long)((g.Kout + BM - 1) / BM) * ((TC + BN - 1) / BN);
   const size_t lds = (size_t)2 * (OPER_A + OPER_B) * sizeof(bf16_t) + 2 * DTF_MAX_TAPS * sizeof(int);
   const bool generic = (g.C % 8) != 0;
-  const dim3 grid((unsigned)(tiles * nsplit));
   const bool dma = g_wgrad_dma_mode != 0 && !generic && (tr_mode & 1) && M < (1L << 24) &&
                    g.N * g.H * g.W < (1L << 24);
+  const bool narrow = dma && wgrad_narrow(g.Kout, taps.n);
+  const int bm = narrow ? 64 : BM, bn = narrow ? 256 : BN;
+  const long tiles = (long)((g.Kout + bm - 1) / bm) * ((TC + bn - 1) / bn);
+  const dim3 grid((unsigned)(tiles * nsplit));
   if (dma) {
-    const size_t lds_dma = (size_t)BM * (BN + 4) * sizeof(float) +   // epilogue tile >= 2 stages
-                           2 * DTF_MAX_TAPS * sizeof(int);
-    static_assert((size_t)BM * (BN + 4) * 4 >= (size_t)2 * kWdStage * 2, "LDS sizing");
-    hipLaunchKernelGGL(conv_wgrad_dma_kernel, grid, dim3(kThreads), lds_dma, st, X, dY, target, g,
-                       taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+    if (narrow) {
+      using Cf = WdCfg<1, 4>;
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<1, 4>), grid, dim3(kThreads), Cf::LDS, st, X, dY,
+                         target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+    } else {
+      using Cf = WdCfg<2, 2>;
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<2, 2>), grid, dim3(kThreads), Cf::LDS, st, X, dY,
+                         target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+    }
   } else if (!(tr_mode & 1)) {  // debug path: element-wise LDS reads instead of ds_read_b64_tr_b16
     if (generic) hipLaunchKernelGGL((conv_wgrad_kernel<true, false>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
     else hipLaunchKernelGGL((conv_wgrad_kernel<false, false>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);

@@ -28,6 +28,12 @@ except ImportError as e:  # pragma: no cover - exercised on boxes without a buil
 
 _BF16 = torch.bfloat16
 
+# kernel-variant switches for A/B runs on one box (defaults = the measured best)
+if os.environ.get("DTF_WGRAD_MODE"):
+    _K.wgrad_set_dma_mode(int(os.environ["DTF_WGRAD_MODE"]))
+if os.environ.get("DTF_CONV_SMALL_K"):
+    _K.conv_set_small_k(int(os.environ["DTF_CONV_SMALL_K"]))
+
 
 def _st():
     return torch.cuda.current_stream().cuda_stream
@@ -238,7 +244,7 @@ def conv2d_wgrad(x, dy, w_shape, stride, padding, out=None):
     _, P, Q, _ = dy.shape
     taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
     tc = R * S * C
-    splits = _K.conv_wgrad_splits(n * P * Q, K, tc, _WGRAD_WS_CAP)
+    splits = _K.conv_wgrad_splits(n * P * Q, K, tc, _WGRAD_WS_CAP, R * S)
     acc = out is not None
     dW = out if acc else torch.empty(K, tc, device=x.device, dtype=torch.float32)
     ws = (torch.empty(splits * K * tc, device=x.device, dtype=torch.float32)

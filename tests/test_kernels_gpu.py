@@ -132,12 +132,13 @@ def test_wgrad_dma_kernel_bit_identical(case):
     dy = torch.randn(N, P, Q, K, device=dev).to(torch.bfloat16)
     outs = []
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 2):     # register-staged, LDS-DMA (narrow for Kout <= 64), DMA 2x2
             nat._K.wgrad_set_dma_mode(mode)
             outs.append(nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad))
     finally:
         nat._K.wgrad_set_dma_mode(-1)
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])
     wr = torch.zeros(K, R, R, C, device=dev, requires_grad=True)
     ref.conv2d(x.float(), wr, stride, pad).backward(dy.float())
     assert _rel(outs[1], wr.grad) < 1e-2

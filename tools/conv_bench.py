@@ -66,8 +66,12 @@ def main():
     ap.add_argument("--small-k", type=int, default=None,
                     help="conv_set_small_k bitmask (1: one LDS stage for single-K-step convs, "
                          "2: BK 32 for 1x1 convs with C <= 128)")
+    ap.add_argument("--wgrad-mode", type=int, default=-1,
+                    help="wgrad_set_dma_mode: -1/1 LDS-DMA (narrow 1x4 for Kout <= 64), "
+                         "2 LDS-DMA 2x2 only, 0 register-staged")
     args = ap.parse_args()
     native._K.conv_set_dma_mode(args.dma)
+    native._K.wgrad_set_dma_mode(args.wgrad_mode)
     if args.small_k is not None:
         native._K.conv_set_small_k(args.small_k)
     only = set(args.only.split(",")) if args.only else None
