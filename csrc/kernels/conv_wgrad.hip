@@ -278,23 +278,25 @@ DTF_DEV void fdivmod(int m, int d, float inv, int& q, int& r) {
   r = rem - adj * d;
 }
 
-template <int WM, int WN>
+// BK pixels per K-step, NS LDS stages (NS - 1 K-steps of DMA in flight ahead of the MFMAs)
+template <int WM, int WN, int BK, int NS>
 struct WdCfg {
   static constexpr int BMw = 64 * WM, BNw = 64 * WN;          // dY cols (Kout), X cols (T*C)
   static constexpr int RPI_A = 1024 / (BMw * 2), RPI_B = 1024 / (BNw * 2);   // rows / 1-KB DMA
-  static constexpr int IA = BKM / RPI_A / 4, IB = BKM / RPI_B / 4;           // DMAs per wave
-  static constexpr int STAGE = BKM * (BMw + BNw);                            // bf16 per stage
+  static constexpr int IA = BK / RPI_A / 4, IB = BK / RPI_B / 4;             // DMAs per wave
+  static constexpr int STAGE = BK * (BMw + BNw);                             // bf16 per stage
   static constexpr int LDO = BNw + 4;
-  static constexpr size_t LDS = (size_t)(2 * STAGE * 2) > (size_t)(BMw * LDO * 4)
-                                    ? (size_t)(2 * STAGE * 2) : (size_t)(BMw * LDO * 4);
+  static constexpr size_t LDS = (size_t)(NS * STAGE * 2) > (size_t)(BMw * LDO * 4)
+                                    ? (size_t)(NS * STAGE * 2) : (size_t)(BMw * LDO * 4);
+  static_assert(IA >= 1 && IB >= 1 && BK % 32 == 0, "wgrad DMA plan");
 };
 
-template <int WM, int WN>
+template <int WM, int WN, int BK, int NS>
 __global__ void __launch_bounds__(kThreads, 2)
 conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                       float* __restrict__ dW, const WgradGeom g, const TapTableW taps,
                       float invQ, float invP) {
-  using Cf = WdCfg<WM, WN>;
+  using Cf = WdCfg<WM, WN, BK, NS>;
   constexpr int BMw = Cf::BMw, BNw = Cf::BNw;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -314,7 +316,7 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
   const int M = g.N * g.P * g.Q;
   const int ms = split * (int)g.m_per_split;
   const int me = min(ms + (int)g.m_per_split, M);
-  const int nk = (me - ms + BKM - 1) / BKM;
+  const int nk = (me - ms + BK - 1) / BK;
   const i32x4_t rx = rsrc_quad(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
   const i32x4_t ry = rsrc_quad(dY, (uint32_t)M * g.Kout * 2u);
   const uint32_t lds0 = lds_addr(lds);
@@ -363,7 +365,7 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
   // get its decode by ds_bpermute -- one divmod pair per lane per step.
   auto issue = [&](int kt, int stage) {
     const uint32_t base = lds0 + (uint32_t)(stage * Cf::STAGE) * 2u;
-    const int mk = ms + kt * BKM;                     // wave-uniform first pixel of the step
+    const int mk = ms + kt * BK;                     // wave-uniform first pixel of the step
     const int live = me - mk;                         // rows < live are inside this split
     const int mp = mk + lane;
     int t, q, n, p;
@@ -388,7 +390,7 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
       const int h = (hwr >> 16) + b_dh[i], w = (hwr & 0xFFFF) + b_dw[i];
       const bool bok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
       const uint32_t bo = bok ? (uint32_t)(pbr + b_toff[i]) : kOOB;
-      dma16(rx, base + (uint32_t)(BKM * BMw * 2) + (uint32_t)(wave + 4 * i) * 1024u, bo);
+      dma16(rx, base + (uint32_t)(BK * BMw * 2) + (uint32_t)(wave + 4 * i) * 1024u, bo);
     }
   };
 
@@ -400,15 +402,31 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
 
   const int gq = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
-  if (nk > 0) issue(0, 0);
-  for (int kt = 0; kt < nk; ++kt) {
-    DTF_WAIT_VM(0);            // this wave's DMAs of step kt landed ...
-    __syncthreads();           // ... and everyone's; everyone also finished reading step kt-1
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-    const bf16_t* sa = lds + (kt & 1) * Cf::STAGE;
-    const bf16_t* sb = sa + BKM * BMw;
+  // NS-stage ring: step k's DMAs were issued NS - 1 steps earlier; steps past nk are issued too,
+  // fully out of range (no traffic), so every wait below leaves exactly (NS - 2) steps in flight
+  constexpr int PER = Cf::IA + Cf::IB;     // DMAs per wave per step
 #pragma unroll
-    for (int ks = 0; ks < BKM / 32; ++ks) {
+  for (int s0 = 0; s0 < NS - 1; ++s0) issue(s0, s0);
+  for (int kt = 0; kt < nk; ++kt) {
+    if constexpr (NS == 2) {
+      DTF_WAIT_VM(0);
+      __syncthreads();         // everyone's step kt landed; everyone finished reading kt - 1
+    } else {
+      static_assert(NS != 3 || PER == 4 || PER == 8 || PER == 10, "vmcnt literal table");
+      if constexpr (NS == 4 && PER == 4) DTF_WAIT_VM(8);
+      else if constexpr (NS == 4 && PER == 5) DTF_WAIT_VM(10);
+      else if constexpr (NS == 3 && PER == 4) DTF_WAIT_VM(4);
+      else if constexpr (NS == 3 && PER == 5) DTF_WAIT_VM(5);
+      else if constexpr (NS == 3 && PER == 8) DTF_WAIT_VM(8);
+      else if constexpr (NS == 3 && PER == 10) DTF_WAIT_VM(10);
+      else static_assert(NS == 2, "no vmcnt literal for this pipeline");
+      raw_barrier();           // no vmcnt(0) drain: the younger stages stay in flight
+    }
+    issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const bf16_t* sa = lds + (kt % NS) * Cf::STAGE;
+    const bf16_t* sb = sa + BK * BMw;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8_t af[4], bfr[4];
       const int r0 = 32 * ks + 8 * gq + tq;
 #pragma unroll
@@ -491,6 +509,10 @@ slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n
 // -1 / 1: LDS-DMA kernel whenever legal (default), 0: the register-staged kernel (A/B tests)
 static int g_wgrad_dma_mode = -1;
 void dtf_wgrad_set_dma_mode(int mode) { g_wgrad_dma_mode = mode; }
+// LDS-DMA pipeline: 0 = 64-pixel steps double-buffered (default: same-box A/B, 1 was 0.8 % slower
+// on the ResNet-50 step), 1 = 32-pixel steps in a 4-stage ring, 2 = 64-pixel steps, 3 stages
+static int g_wgrad_pipe = 0;
+void dtf_wgrad_set_pipe(int p) { g_wgrad_pipe = p; }
 // 1 x 4 waves (64 x 256 tile) for multi-tap Kout <= 64 layers (stage-1 3x3, the stem): the 2 x 2
 // tile would leave half its MFMA rows empty.  Measured (tools/wgrad_ab.sh, b512): stem 611 ->
 // 493 us, 3x3 337 -> 288 us, but the bandwidth-bound 1x1 layers are 11-20 % slower with it, so
@@ -549,15 +571,21 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   const long tiles = (long)((g.Kout + bm - 1) / bm) * ((TC + bn - 1) / bn);
   const dim3 grid((unsigned)(tiles * nsplit));
   if (dma) {
-    if (narrow) {
-      using Cf = WdCfg<1, 4>;
-      hipLaunchKernelGGL((conv_wgrad_dma_kernel<1, 4>), grid, dim3(kThreads), Cf::LDS, st, X, dY,
-                         target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
-    } else {
-      using Cf = WdCfg<2, 2>;
-      hipLaunchKernelGGL((conv_wgrad_dma_kernel<2, 2>), grid, dim3(kThreads), Cf::LDS, st, X, dY,
-                         target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+    const float iq = 1.0f / (float)g.Q, ip = 1.0f / (float)g.P;
+#define DTF_WGRAD_LAUNCH(WM_, WN_, BK_, NS_)                                                     \
+  hipLaunchKernelGGL((conv_wgrad_dma_kernel<WM_, WN_, BK_, NS_>), grid, dim3(kThreads),         \
+                     (WdCfg<WM_, WN_, BK_, NS_>::LDS), st, X, dY, target, g, taps, iq, ip)
+    if (g_wgrad_pipe == 1) {   // 32-pixel steps, 4-stage ring (3 steps of DMA in flight)
+      if (narrow) DTF_WGRAD_LAUNCH(1, 4, 32, 4);
+      else DTF_WGRAD_LAUNCH(2, 2, 32, 4);
+    } else if (g_wgrad_pipe == 2) {   // 64-pixel steps, 3-stage ring (1 block / CU)
+      if (narrow) DTF_WGRAD_LAUNCH(1, 4, 64, 3);
+      else DTF_WGRAD_LAUNCH(2, 2, 64, 3);
+    } else {                   // 64-pixel steps, double buffer
+      if (narrow) DTF_WGRAD_LAUNCH(1, 4, 64, 2);
+      else DTF_WGRAD_LAUNCH(2, 2, 64, 2);
     }
+#undef DTF_WGRAD_LAUNCH
   } else if (!(tr_mode & 1)) {  // debug path: element-wise LDS reads instead of ds_read_b64_tr_b16
     if (generic) hipLaunchKernelGGL((conv_wgrad_kernel<true, false>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);
     else hipLaunchKernelGGL((conv_wgrad_kernel<false, false>), grid, dim3(kThreads), lds, st, X, dY, target, g, taps, tr_mode >> 1);

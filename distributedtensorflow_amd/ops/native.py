@@ -31,6 +31,8 @@ _BF16 = torch.bfloat16
 # kernel-variant switches for A/B runs on one box (defaults = the measured best)
 if os.environ.get("DTF_WGRAD_MODE"):
     _K.wgrad_set_dma_mode(int(os.environ["DTF_WGRAD_MODE"]))
+if os.environ.get("DTF_WGRAD_PIPE"):
+    _K.wgrad_set_pipe(int(os.environ["DTF_WGRAD_PIPE"]))
 if os.environ.get("DTF_CONV_SMALL_K"):
     _K.conv_set_small_k(int(os.environ["DTF_CONV_SMALL_K"]))
 
