@@ -7,18 +7,21 @@
 namespace {
 constexpr int kT = 256;
 
+// IT: index type of the flat element loop -- 32-bit whenever the tensor allows (a 64-bit
+// divide/modulo is a ~100-instruction software sequence per element on CDNA)
+template <typename IT>
 __global__ void __launch_bounds__(kT)
 maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                    uint8_t* __restrict__ arg, int N, int H, int W, int C, int P, int Q, int kh,
                    int kw, int sh, int sw, int ph, int pw) {
-  const int cv = C >> 3;
-  const long total = (long)N * P * Q * cv;
-  for (long i = (long)blockIdx.x * kT + threadIdx.x; i < total; i += (long)gridDim.x * kT) {
+  const IT cv = (IT)(C >> 3);
+  const IT total = (IT)N * P * Q * cv;
+  for (IT i = (IT)blockIdx.x * kT + threadIdx.x; i < total; i += (IT)gridDim.x * kT) {
     const int cg = (int)(i % cv);
-    long t = i / cv;
-    const int q = (int)(t % Q); t /= Q;
-    const int p = (int)(t % P);
-    const int n = (int)(t / P);
+    IT t = i / cv;
+    const int q = (int)(t % (IT)Q); t /= (IT)Q;
+    const int p = (int)(t % (IT)P);
+    const int n = (int)(t / (IT)P);
     float best[8];
     uint8_t bi[8];
 #pragma unroll
@@ -44,18 +47,19 @@ maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
   }
 }
 
+template <typename IT>
 __global__ void __launch_bounds__(kT)
 maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
                    bf16_t* __restrict__ dx, int N, int H, int W, int C, int P, int Q, int kh,
                    int kw, int sh, int sw, int ph, int pw) {
-  const int cv = C >> 3;
-  const long total = (long)N * H * W * cv;
-  for (long i = (long)blockIdx.x * kT + threadIdx.x; i < total; i += (long)gridDim.x * kT) {
+  const IT cv = (IT)(C >> 3);
+  const IT total = (IT)N * H * W * cv;
+  for (IT i = (IT)blockIdx.x * kT + threadIdx.x; i < total; i += (IT)gridDim.x * kT) {
     const int cg = (int)(i % cv);
-    long t = i / cv;
-    const int w = (int)(t % W); t /= W;
-    const int h = (int)(t % H);
-    const int n = (int)(t / H);
+    IT t = i / cv;
+    const int w = (int)(t % (IT)W); t /= (IT)W;
+    const int h = (int)(t % (IT)H);
+    const int n = (int)(t / (IT)H);
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -138,15 +142,25 @@ inline int grid_for(long n) {
 void dtf_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* arg, int N, int H, int W, int C,
                      int P, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
                      hipStream_t st) {
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)N * P * Q * (C / 8))), dim3(kT), 0,
-                     st, x, y, arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const long total = (long)N * P * Q * (C / 8);
+  if (total < (1L << 31))
+    hipLaunchKernelGGL(maxpool_fwd_kernel<uint32_t>, dim3(grid_for(total)), dim3(kT), 0, st, x, y,
+                       arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<uint64_t>, dim3(grid_for(total)), dim3(kT), 0, st, x, y,
+                       arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
 }
 
 void dtf_maxpool_bwd(const bf16_t* dy, const uint8_t* arg, bf16_t* dx, int N, int H, int W,
                      int C, int P, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
                      hipStream_t st) {
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(kT), 0,
-                     st, dy, arg, dx, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  const long total = (long)N * H * W * (C / 8);
+  if (total < (1L << 31))
+    hipLaunchKernelGGL(maxpool_bwd_kernel<uint32_t>, dim3(grid_for(total)), dim3(kT), 0, st, dy,
+                       arg, dx, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<uint64_t>, dim3(grid_for(total)), dim3(kT), 0, st, dy,
+                       arg, dx, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
 }
 
 void dtf_gap_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st) {
