@@ -44,7 +44,9 @@ void dtf_bn_fwd_finalize(const float*, long, int, const float*, const float*, fl
 void dtf_bn_fwd_finalize_g(const float*, int, long, int, const float*, const float*, float*,
                            float*, float, float, float*, float*, float*, float*, hipStream_t);
 long dtf_bn_workspace_floats_g(int, int);
-int dtf_conv_stats_rows(long, int, int, int);
+int dtf_conv_stats_rows(long, int, int, int, int);
+void dtf_conv_set_halo(int);
+int dtf_conv_tile_rows(const ConvGeom&, const TapTable&);
 void dtf_conv_set_dma_mode(int);
 void dtf_conv_set_small_k(int);
 void dtf_bn_infer_finalize(int, const float*, const float*, const float*, const float*, float,
@@ -141,7 +143,16 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("bn_workspace_floats", &dtf_bn_workspace_floats);
   m.def("bn_workspace_floats_g", &dtf_bn_workspace_floats_g);
   m.def("conv_stats_rows", &dtf_conv_stats_rows, py::arg("M"), py::arg("Kout"), py::arg("C") = 0,
-        py::arg("taps") = 1);
+        py::arg("taps") = 1, py::arg("W") = 0);
+  m.def("conv_set_halo", &dtf_conv_set_halo);
+  m.def("conv_tile_rows", [](std::vector<int> geom, std::vector<int> dh, std::vector<int> dw) {
+    if (geom.size() != 16 && geom.size() != 17)
+      throw std::runtime_error("conv_tile_rows: geom needs 16 (+acc) ints");
+    ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
+               geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15],
+               geom.size() == 17 ? geom[16] : 0};
+    return dtf_conv_tile_rows(g, make_taps<TapTable>(dh, dw));
+  });
   m.def("conv_set_dma_mode", &dtf_conv_set_dma_mode);
   m.def("filter_transpose", [](std::vector<uintptr_t> src, std::vector<uintptr_t> dst,
                                std::vector<int> K, std::vector<int> T, std::vector<int> C,

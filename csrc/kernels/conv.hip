@@ -706,6 +706,153 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Halo-tiled 3x3 stride-1 conv for the 56 x 56 x 64 -> 64 layers (stage 1 c2 forward AND its data
+// gradient, which is the same conv with flipped taps).  The implicit-GEMM kernels re-fetch every
+// input pixel once per tap (9x) through L2 and run these K=64-channel layers at ~0.14 of the MFMA
+// roof; here a block owns 4 full output rows of one image (224 pixels x 64 channels), loads the
+// 6 x 58-pixel input patch ONCE into LDS by LDS-DMA (zero halo from the buffer range check) and
+// reads all 9 taps' A fragments from it; the 9 per-tap 64 x 64 filter slices stream through a
+// double-buffered LDS ring (8 KB each).  4 waves as 2 (M: 7 fragments = 112 px) x 2 (N: 32).
+// LDS rows are 128 B (64 bf16) with the chunk XOR swizzle of swz_chunk<64> by row (patch pixel
+// index / filter row), applied on the DMA source side.
+constexpr int kHaloTH = 4, kHaloW = 56, kHaloC = 64;
+constexpr int kHaloPW = kHaloW + 2;                              // patch width (pixels)
+constexpr int kHaloPix = (kHaloTH + 2) * kHaloPW;                // 348 patch pixels
+constexpr int kHaloPixAl = (kHaloPix + 7) / 8 * 8;               // 352: whole 1-KB DMAs
+constexpr int kHaloM = kHaloTH * kHaloW;                         // 224 output pixels
+constexpr int kHaloWStage = 64 * kHaloC;                         // one tap's filter slice
+
+__global__ void __launch_bounds__(kThreads, 2)
+conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+                    bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
+                    float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  bf16_t* const patch = lds;                                     // [352][64]
+  bf16_t* const wst = lds + kHaloPixAl * kHaloC;                 // [2][64][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_h = g.H / kHaloTH;
+  const int tm = blockIdx.x;                                     // (image, row-tile)
+  const int n = tm / tiles_h, h0 = (tm % tiles_h) * kHaloTH;
+  const int n0 = blockIdx.y * 64;                                // output-channel tile
+  const i32x4_t rx = rsrc_quad(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
+  const i32x4_t rw = rsrc_quad(Wt, (uint32_t)g.Kout * g.Kpad * 2u);
+  const uint32_t lds_patch = lds_addr(patch), lds_w = lds_addr(wst);
+
+  // ---- patch: 44 DMAs of 8 pixels x 8 chunks; wave w issues q = w, w + 4, ...
+  const int lp = lane >> 3, slot = lane & 7;
+  for (int q = wave; q < kHaloPixAl / 8; q += 4) {
+    const int pix = q * 8 + lp;
+    const int pr = pix / kHaloPW, pc = pix - pr * kHaloPW;
+    const int h = h0 - 1 + pr, w = pc - 1;
+    const int chunk = slot ^ ((pix >> 1) & 7);
+    const bool ok = pix < kHaloPix && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+    const uint32_t off = ok ? (uint32_t)((((n * g.H + h) * g.W + w) * kHaloC + chunk * 8) * 2) : kOOB;
+    dma16(rx, lds_patch + (uint32_t)q * 1024u, off);
+  }
+  // ---- filter slice of tap t: 64 output-channel rows x 64 channels, 2 DMAs per wave
+  auto issue_w = [&](int t, int stage) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = wave + 4 * i;
+      const int row = q * 8 + lp;
+      const int chunk = slot ^ ((row >> 1) & 7);
+      const int kr = n0 + row;
+      const uint32_t off = (t < taps.n && kr < g.Kout)
+                               ? (uint32_t)((kr * g.Kpad + t * kHaloC + chunk * 8) * 2) : kOOB;
+      dma16(rw, lds_w + (uint32_t)(stage * kHaloWStage) * 2u + (uint32_t)q * 1024u, off);
+    }
+  };
+  issue_w(0, 0);
+
+  // per-lane A rows: output pixel m = wm*112 + 16 i + frow -> patch pixel of tap (0, 0)
+  const int frow = lane & 15, fq = lane >> 4;
+  int pbase[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int m = wm * 112 + 16 * i + frow;
+    const int orow = m / kHaloW, ocol = m - orow * kHaloW;
+    pbase[i] = (orow + 1) * kHaloPW + ocol + 1;
+  }
+  f32x4_t acc[7][2];
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < taps.n; ++t) {
+    DTF_WAIT_VM(0);            // patch (t == 0) and this tap's filter slice landed (own DMAs) ...
+    __syncthreads();           // ... everyone's; everyone done reading the other filter stage
+    issue_w(t + 1, (t + 1) & 1);   // past the last tap: out-of-range, no traffic
+    const int dpix = taps.dh[t] * kHaloPW + taps.dw[t];          // wave-uniform
+    const bf16_t* sw = wst + (t & 1) * kHaloWStage;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + fq;
+      bf16x8_t bfr[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 32 + 16 * j + frow;
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sw + r * kHaloC + ((ch ^ ((r >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const int p = pbase[i] + dpix;
+        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(patch + p * kHaloC + ((ch ^ ((p >> 1) & 7)) << 3));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  DTF_WAIT_VM(0);
+  __syncthreads();
+  // ---- epilogue: bf16 tile [224][64 + 8] in LDS (over the patch) -> 16-B stores; BN partials
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr int LDC = 64 + 8;
+  bf16_t* st = lds;
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        st[(wm * 112 + 16 * i + fq * 4 + r) * LDC + wn * 32 + 16 * j + frow] = f2bf(acc[i][j][r]);
+  __syncthreads();
+  const long ybase = ((long)n * g.H + h0) * g.W;                 // first output pixel of the tile
+  const int oc = tid & 7;                                        // 8 chunks per 64-channel row
+  const bool col_ok = n0 + oc * 8 < g.Kout;
+  for (int r = tid >> 3; r < kHaloM; r += kThreads / 8) {
+    if (!col_ok) continue;
+    *reinterpret_cast<uint4*>(Y + (ybase + r) * g.Kout + n0 + oc * 8) =
+        *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
+  }
+  if (stats) {   // per-channel sum / sum of squares of the rounded outputs -> slab row tm
+    float* red = reinterpret_cast<float*>(st + kHaloM * LDC);    // [4][2][64]
+    const int col = tid & 63, grp = tid >> 6;
+    float a1 = 0.f, a2 = 0.f;
+    for (int r = grp * (kHaloM / 4); r < (grp + 1) * (kHaloM / 4); ++r) {
+      const float v = bf2f(st[r * LDC + col]);
+      a1 += v;
+      a2 += v * v;
+    }
+    red[(grp * 2 + 0) * 64 + col] = a1;
+    red[(grp * 2 + 1) * 64 + col] = a2;
+    __syncthreads();
+    if (grp == 0 && n0 + col < g.Kout) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { a += red[(k * 2 + 0) * 64 + col]; b += red[(k * 2 + 1) * 64 + col]; }
+      stats[((long)tm * 2 + 0) * g.Kout + n0 + col] = a;
+      stats[((long)tm * 2 + 1) * g.Kout + n0 + col] = b;
+    }
+  }
+}
+
 }  // namespace
 
 // Host launcher.  Caller guarantees: Kout % 8 == 0, Kpad % BK == 0 (filter rows zero-padded),
@@ -728,9 +875,33 @@ static bool use_dma_kernel(long M, int Kout, int C, int taps, int bk) {
   return taps > 1 && C >= 256;
 }
 
-int dtf_conv_stats_rows(long M, int Kout, int C, int taps) {
+// the halo kernel's layer family: 3x3 stride 1 "same", 56 x 56 x 64 input, Kout % 64 == 0
+static int g_halo = 1;
+void dtf_conv_set_halo(int on) { g_halo = on; }
+static bool use_halo(const ConvGeom& g, const TapTable& taps) {
+  if (!g_halo || g.C != kHaloC || g.W != kHaloW || g.H % kHaloTH || g.Kout % 64 || taps.n != 9 ||
+      g.sh != 1 || g.sw != 1 || g.P != g.H || g.Q != g.W || g.Ho != g.H || g.Wo != g.W ||
+      g.osh != 1 || g.osw != 1 || g.oh0 || g.ow0 || g.acc || g.Kpad != 9 * kHaloC)
+    return false;
+  for (int t = 0; t < 9; ++t)
+    if (taps.dh[t] < -1 || taps.dh[t] > 1 || taps.dw[t] < -1 || taps.dw[t] > 1) return false;
+  return true;
+}
+
+// M tiles of a launch WITHOUT the halo kernel (the fused-BN-backward dgrad path, which never
+// takes it); W is accepted for API symmetry and ignored
+int dtf_conv_stats_rows(long M, int Kout, int C, int taps, int W) {
+  (void)W;
   const int BM = use_dma_kernel(M, Kout, C, taps, 64) ? kDmaBM : (Kout <= 64 ? 256 : 128);
   return (int)((M + BM - 1) / BM);
+}
+
+// M tiles (= BN-statistics slab rows) of exactly the kernel dtf_conv_igemm will pick for this
+// forward launch (no fused BN-backward epilogue)
+int dtf_conv_tile_rows(const ConvGeom& g, const TapTable& taps) {
+  if (g.C % 32 == 0 && use_halo(g, taps)) return g.N * (g.H / kHaloTH);
+  const long M = (long)g.N * g.P * g.Q;
+  return dtf_conv_stats_rows(M, g.Kout, g.C, taps.n, 0);
 }
 
 void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
@@ -757,6 +928,14 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
       if (narrow) launch_cfg<4, 1, 32, 1>(X, Wt, Y, g, taps, stats, bnb, st);
       else launch_cfg<2, 2, 32, 1>(X, Wt, Y, g, taps, stats, bnb, st);
     }
+    return;
+  }
+  if (!bnb.part && use_halo(g, taps)) {
+    const size_t lds = (size_t)(kHaloPixAl * kHaloC + 2 * kHaloWStage) * sizeof(bf16_t);
+    static_assert((size_t)(kHaloPixAl * kHaloC + 2 * kHaloWStage) * 2 >=
+                  (size_t)kHaloM * 72 * 2 + 4 * 2 * 64 * 4, "halo epilogue LDS");
+    hipLaunchKernelGGL(conv3x3_halo_kernel, dim3((unsigned)(g.N * (g.H / kHaloTH)),
+                       (unsigned)(g.Kout / 64)), dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats);
     return;
   }
   if (use_dma_kernel((long)m, g.Kout, g.C, taps.n, bk) && g.Kpad % 64 == 0) {

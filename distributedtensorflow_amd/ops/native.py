@@ -33,6 +33,8 @@ if os.environ.get("DTF_WGRAD_MODE"):
     _K.wgrad_set_dma_mode(int(os.environ["DTF_WGRAD_MODE"]))
 if os.environ.get("DTF_WGRAD_PIPE"):
     _K.wgrad_set_pipe(int(os.environ["DTF_WGRAD_PIPE"]))
+if os.environ.get("DTF_CONV_HALO"):
+    _K.conv_set_halo(int(os.environ["DTF_CONV_HALO"]))
 if os.environ.get("DTF_CONV_SMALL_K"):
     _K.conv_set_small_k(int(os.environ["DTF_CONV_SMALL_K"]))
 
@@ -96,6 +98,12 @@ def _conv_geom_fwd(x, K, R, S, stride, padding):
     P = (h + pt + pb - R) // sh + 1
     Q = (w + pl + pr - S) // sw + 1
     return n, h, w, c, P, Q, sh, sw, pt, pl
+
+
+def _fwd_geom(xshape, K, taps, P, Q, sh, sw, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0, accumulate=False):
+    n, h, w, c = xshape
+    kpad = -(-(len(taps) * c) // 32) * 32
+    return [n, h, w, c, P, Q, sh, sw, K, kpad, Ho, Wo, osh, osw, oh0, ow0, int(accumulate)]
 
 
 def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
@@ -363,7 +371,10 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
         return _Conv2d.apply(x, w, stride, padding, None, grad_share)
     n, h, wd, c, P, Q, sh, sw, pt, pl = _conv_geom_fwd(x, K, R, S, stride, padding)
     M = n * P * Q
-    G = _K.conv_stats_rows(M, K, c, R * S)
+    taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
+    cp = -(-c // 8) * 8                      # the op zero-pads C to 8 before launching
+    G = _K.conv_tile_rows(_fwd_geom((n, h, wd, cp), K, taps, P, Q, sh, sw, P, Q),
+                          [t[0] for t in taps], [t[1] for t in taps])
     part = torch.empty(_K.bn_workspace_floats_g(G, K), device=x.device, dtype=torch.float32)
     y = _Conv2d.apply(x, w, stride, padding, part, grad_share)
     y._dtf_bn_part = (part, G, M, K)

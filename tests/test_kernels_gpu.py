@@ -295,3 +295,34 @@ def test_batched_filter_transpose():
                             torch.cuda.current_stream().cuda_stream)
     for w, o in zip(ws, outs):
         assert torch.equal(o, w.permute(2, 1, 0))
+
+
+@pytest.mark.parametrize("N,K", [(2, 64), (3, 128)])
+def test_halo_conv3x3_matches_implicit_gemm(N, K):
+    """Halo-tiled 3x3 kernel (56x56x64 layers) == the implicit-GEMM kernel bit for bit (same tap /
+    k order) for the forward and the data gradient; fused BN statistics match."""
+    nat = _native()
+    torch.manual_seed(0)
+    x = torch.randn(N, 56, 56, 64, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K, 3, 3, 64, device=dev) / 24).to(torch.bfloat16)
+    dy = torch.randn(N, 56, 56, K, device=dev).to(torch.bfloat16)
+    outs = []
+    try:
+        for halo in (1, 0):
+            nat._K.conv_set_halo(halo)
+            y = nat.conv2d_forward(x, w, 1, 1)
+            dx = nat.conv2d_dgrad(dy[..., :64].contiguous(), w[:64], x.shape, 1, 1) if K == 64 \
+                else nat.conv2d_dgrad(dy, w, x.shape, 1, 1)
+            gamma = torch.ones(K, device=dev)
+            beta = torch.zeros(K, device=dev)
+            ys = nat.conv2d(x, w.float(), 1, 1, bn_stats=True)
+            z = nat.batch_norm(ys, gamma, beta, None, None, True, 0.9, 1e-5, relu=True)
+            outs.append((y, dx, z.float()))
+    finally:
+        nat._K.conv_set_halo(1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    torch.testing.assert_close(outs[0][2], outs[1][2], atol=2e-2, rtol=1e-2)
+    ref = _ref()
+    yr = ref.conv2d(x.float(), w.float(), 1, 1)
+    assert _rel(outs[0][0], yr) < 1e-2
