@@ -64,7 +64,7 @@ struct ConvGeom {
 // BN's finalize combines.  Saves the backward reduce pass its full re-read of dy.
 // bit 0: one LDS stage when the whole reduction is one K-step; bit 1: BK 32 for 1x1 convs with
 // C <= 128 (see dtf_conv_igemm)
-static int g_small_k = 3;   // both on: measured -4..-6 % on the stage-1/2 1x1 convs (b512)
+static int g_small_k = 7;   // bits 0-2 on: same-box A/B +2.4 % step for bit 2 (BK 32 on every 1x1)
 
 struct BnBwdEpi {
   const bf16_t* x;          // BN input, same [N, Ho, Wo, Kout] layout as Y
@@ -951,6 +951,8 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
   // small-K 1x1 convs (one or two 64-deep K-steps: latency-bound blocks): optionally BK 32 with
   // 16-KB stages -> more blocks per CU (g_small_k bit 1; A/B-measured by tools/conv_bench.py)
   if ((g_small_k & 2) && taps.n == 1 && g.C <= 128) bk = 32;
+  if ((g_small_k & 4) && taps.n == 1) bk = 32;            // every 1x1 conv
+  if ((g_small_k & 8) && !use_dma_kernel((long)m, g.Kout, g.C, taps.n, 64)) bk = 32;   // all reg.
   if (bk == 64 && g.C % 64 == 0) {
     if (narrow) launch_cfg<4, 1, 64, 0>(X, Wt, Y, g, taps, stats, bnb, st);
     else launch_cfg<2, 2, 64, 0>(X, Wt, Y, g, taps, stats, bnb, st);
