@@ -63,8 +63,9 @@ struct ConvGeom {
 // (after a fused residual accumulation) -- into row `row0 + tile` of a [rows][2][Kout] slab the
 // BN's finalize combines.  Saves the backward reduce pass its full re-read of dy.
 // bit 0: one LDS stage when the whole reduction is one K-step; bit 1: BK 32 for 1x1 convs with
-// C <= 128 (see dtf_conv_igemm)
-static int g_small_k = 7;   // bits 0-2 on: same-box A/B +2.4 % step for bit 2 (BK 32 on every 1x1)
+// C <= 128; bit 2: BK 32 for every 1x1; bit 3: BK 32 for every register-kernel conv; bit 4:
+// the <= 128-VGPR (4 waves/SIMD) build of the BK-32 kernels (see dtf_conv_igemm)
+static int g_small_k = 23;  // bits 0-2 + 4: same-box A/B +2.4 % (bit 2), +2.0 % (bit 4)
 
 struct BnBwdEpi {
   const bf16_t* x;          // BN input, same [N, Ho, Wo, Kout] layout as Y
@@ -167,8 +168,10 @@ DTF_DEV uint32_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
 }
 
-template <int WAVES_M, int WAVES_N, int BK, int GATHER, bool BNB>
-__global__ void __launch_bounds__(kThreads, 2)
+// HI_OCC (BK 32, g_small_k bit 4): ask for <= 128 VGPRs -> 4 waves/SIMD, so the 35-KB-LDS 1x1
+// launches can run 4 blocks per CU instead of 3
+template <int WAVES_M, int WAVES_N, int BK, int GATHER, bool BNB, bool HI_OCC = false>
+__global__ void __launch_bounds__(kThreads, HI_OCC ? 4 : 2)
 conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                   bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
                   float* __restrict__ stats, const BnBwdEpi bnb) {
@@ -471,6 +474,9 @@ void launch_cfg(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
                          dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
     else
       throw std::runtime_error("conv: fused BN-backward sums need a C % 32 == 0 dgrad");
+  } else if (BK == 32 && GEN == 0 && (g_small_k & 16)) {
+    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, false, BK == 32 && GEN == 0>),
+                       dim3((unsigned)tiles), dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
   } else {
     hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, false>), dim3((unsigned)tiles),
                        dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
