@@ -286,13 +286,16 @@ struct WdCfg {
   static constexpr int IA = BK / RPI_A / 4, IB = BK / RPI_B / 4;             // DMAs per wave
   static constexpr int STAGE = BK * (BMw + BNw);                             // bf16 per stage
   static constexpr int LDO = BNw + 4;
-  static constexpr size_t LDS = (size_t)(NS * STAGE * 2) > (size_t)(BMw * LDO * 4)
-                                    ? (size_t)(NS * STAGE * 2) : (size_t)(BMw * LDO * 4);
+  // BK 32 variants stage the fp32 epilogue tile in two row halves (-> ~34-40 KB of LDS, up to
+  // 4 blocks per CU with the <= 128-VGPR build)
+  static constexpr int EPI_PASSES = BK == 32 ? 2 : 1;
+  static constexpr size_t EPI = (size_t)(BMw / EPI_PASSES) * LDO * 4;
+  static constexpr size_t LDS = (size_t)(NS * STAGE * 2) > EPI ? (size_t)(NS * STAGE * 2) : EPI;
   static_assert(IA >= 1 && IB >= 1 && BK % 32 == 0, "wgrad DMA plan");
 };
 
 template <int WM, int WN, int BK, int NS>
-__global__ void __launch_bounds__(kThreads, 2)
+__global__ void __launch_bounds__(kThreads, (BK == 32 && NS == 2) ? 4 : 2)
 conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                       float* __restrict__ dW, const WgradGeom g, const TapTableW taps,
                       float invQ, float invP) {
@@ -456,22 +459,28 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   constexpr int LDO = Cf::LDO;
+  constexpr int HR = BMw / Cf::EPI_PASSES;          // tile rows staged per pass
   float* so = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = acc[i][j][r] + 0.0f;
-        so[(wm * 64 + 16 * i + 4 * gq + r) * LDO + wn * 64 + 16 * j + li] = v;
-      }
-  __syncthreads();
   float* out = dW + (long)split * g.slab;
-  for (int idx = tid; idx < BMw * BNw; idx += kThreads) {
-    const int r = idx / BNw, c = idx % BNw;
-    const int row = k0 + r, col = j0 + c;
-    if (row < g.Kout && col < TC) out[(long)row * g.ldw + col] = so[r * LDO + c];
+#pragma unroll
+  for (int pass = 0; pass < Cf::EPI_PASSES; ++pass) {
+    if (pass) __syncthreads();                      // previous half fully read
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * 64 + 16 * i + 4 * gq + r - pass * HR;
+          if (row >= 0 && row < HR)
+            so[row * LDO + wn * 64 + 16 * j + li] = acc[i][j][r] + 0.0f;
+        }
+    __syncthreads();
+    for (int idx = tid; idx < HR * BNw; idx += kThreads) {
+      const int r = idx / BNw, c = idx % BNw;
+      const int row = k0 + pass * HR + r, col = j0 + c;
+      if (row < g.Kout && col < TC) out[(long)row * g.ldw + col] = so[r * LDO + c];
+    }
   }
 }
 
@@ -509,10 +518,13 @@ slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n
 // -1 / 1: LDS-DMA kernel whenever legal (default), 0: the register-staged kernel (A/B tests)
 static int g_wgrad_dma_mode = -1;
 void dtf_wgrad_set_dma_mode(int mode) { g_wgrad_dma_mode = mode; }
-// LDS-DMA pipeline: 0 = 64-pixel steps double-buffered (default: same-box A/B, 1 was 0.8 % slower
-// on the ResNet-50 step), 1 = 32-pixel steps in a 4-stage ring, 2 = 64-pixel steps, 3 stages
-static int g_wgrad_pipe = 0;
+// LDS-DMA pipeline: 0 = 64-pixel steps double-buffered; 1 = 32-pixel steps in a 4-stage ring
+// (-0.8 % vs 0); 2 = 64-pixel steps, 3 stages, 1 block/CU (-5.6 %); 3 (default) = 32-pixel steps
+// double-buffered with a two-pass epilogue: ~34-40 KB of LDS and <= 128 VGPRs -> 4 blocks/CU
+// (+1.1 % step vs 0; same-box A/B, profiles/measurements/r1_ab_wgrad_*.txt)
+static int g_wgrad_pipe = 3;
 void dtf_wgrad_set_pipe(int p) { g_wgrad_pipe = p; }
+int dtf_wgrad_get_pipe() { return g_wgrad_pipe; }
 // 1 x 4 waves (64 x 256 tile) for multi-tap Kout <= 64 layers (stage-1 3x3, the stem): the 2 x 2
 // tile would leave half its MFMA rows empty.  Measured (tools/wgrad_ab.sh, b512): stem 611 ->
 // 493 us, 3x3 337 -> 288 us, but the bandwidth-bound 1x1 layers are 11-20 % slower with it, so
@@ -578,6 +590,9 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
     if (g_wgrad_pipe == 1) {   // 32-pixel steps, 4-stage ring (3 steps of DMA in flight)
       if (narrow) DTF_WGRAD_LAUNCH(1, 4, 32, 4);
       else DTF_WGRAD_LAUNCH(2, 2, 32, 4);
+    } else if (g_wgrad_pipe == 3) {   // 32-pixel steps, double buffer, half epilogue: 4 blk/CU
+      if (narrow) DTF_WGRAD_LAUNCH(1, 4, 32, 2);
+      else DTF_WGRAD_LAUNCH(2, 2, 32, 2);
     } else if (g_wgrad_pipe == 2) {   // 64-pixel steps, 3-stage ring (1 block / CU)
       if (narrow) DTF_WGRAD_LAUNCH(1, 4, 64, 3);
       else DTF_WGRAD_LAUNCH(2, 2, 64, 3);

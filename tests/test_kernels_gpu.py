@@ -131,14 +131,20 @@ def test_wgrad_dma_kernel_bit_identical(case):
     Q = (W + 2 * pad - R) // stride + 1
     dy = torch.randn(N, P, Q, K, device=dev).to(torch.bfloat16)
     outs = []
+    pipe0 = nat._K.wgrad_get_pipe()
     try:
         for mode in (0, 1, 2):     # register-staged, LDS-DMA (narrow for Kout <= 64), DMA 2x2
             nat._K.wgrad_set_dma_mode(mode)
             outs.append(nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad))
+        nat._K.wgrad_set_dma_mode(-1)
+        for pipe in (1, 2, 3):    # LDS-DMA ring variants (32/4, 64/3, 32/2 + half epilogue)
+            nat._K.wgrad_set_pipe(pipe)
+            outs.append(nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad))
     finally:
         nat._K.wgrad_set_dma_mode(-1)
-    assert torch.equal(outs[0], outs[1])
-    assert torch.equal(outs[0], outs[2])
+        nat._K.wgrad_set_pipe(pipe0)
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
     wr = torch.zeros(K, R, R, C, device=dev, requires_grad=True)
     ref.conv2d(x.float(), wr, stride, pad).backward(dy.float())
     assert _rel(outs[1], wr.grad) < 1e-2
