@@ -65,7 +65,7 @@ struct ConvGeom {
 // bit 0: one LDS stage when the whole reduction is one K-step; bit 1: BK 32 for 1x1 convs with
 // C <= 128; bit 2: BK 32 for every 1x1; bit 3: BK 32 for every register-kernel conv; bit 4:
 // the <= 128-VGPR (4 waves/SIMD) build of the BK-32 kernels (see dtf_conv_igemm)
-static int g_small_k = 23;  // bits 0-2 + 4: same-box A/B +2.4 % (bit 2), +2.0 % (bit 4)
+static int g_small_k = 31;  // bits 0-4: same-box A/B +2.4 % (bit 2), +2.0 % (bit 4), +0.5 % (bit 3)
 
 struct BnBwdEpi {
   const bf16_t* x;          // BN input, same [N, Ho, Wo, Kout] layout as Y
