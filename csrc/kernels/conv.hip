@@ -722,137 +722,176 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
 // double-buffered LDS ring (8 KB each).  4 waves as 2 (M: 7 fragments = 112 px) x 2 (N: 32).
 // LDS rows are 128 B (64 bf16) with the chunk XOR swizzle of swz_chunk<64> by row (patch pixel
 // index / filter row), applied on the DMA source side.
-constexpr int kHaloTH = 4, kHaloW = 56, kHaloC = 64;
-constexpr int kHaloPW = kHaloW + 2;                              // patch width (pixels)
-constexpr int kHaloPix = (kHaloTH + 2) * kHaloPW;                // 348 patch pixels
-constexpr int kHaloPixAl = (kHaloPix + 7) / 8 * 8;               // 352: whole 1-KB DMAs
-constexpr int kHaloM = kHaloTH * kHaloW;                         // 224 output pixels
-constexpr int kHaloWStage = 64 * kHaloC;                         // one tap's filter slice
+constexpr int kHaloTH = 4;        // output rows per block (whole image rows)
 
+// C: input channels (64 | 128), W: image width (56 | 28), WMW x (4 / WMW) waves, NT output
+// channels per block.  7 x 2 MFMA fragments per wave in both families:
+//   56 x 56 x 64  -> 64 : M 224 = 2 waves x 7 frags, NT 64  = 2 waves x 2 frags
+//   28 x 28 x 128 -> 128: M 112 = 1 wave  x 7 frags, NT 128 = 4 waves x 2 frags
+template <int C, int W, int WMW, int NT>
+struct HaloCfg {
+  static constexpr int PW = W + 2;                       // patch width (pixels)
+  static constexpr int PIX = (kHaloTH + 2) * PW;         // patch pixels
+  static constexpr int ROWB = C * 2;                     // bytes per patch pixel
+  static constexpr int PPI = 1024 / ROWB;                // pixels per 1-KB DMA
+  static constexpr int PIXAL = (PIX + PPI - 1) / PPI * PPI;
+  static constexpr int M = kHaloTH * W;                  // output pixels per block
+  static constexpr int WNW = 4 / WMW;
+  static constexpr int MF = M / 16 / WMW;                // M fragments per wave
+  static constexpr int NF = NT / WNW / 16;               // N fragments per wave
+  static constexpr int KS = C / 64;                      // 64-channel slices per tap
+  static constexpr int WST = NT * 64;                    // filter elements per stage
+  static constexpr int LDC = NT + 8;
+  static constexpr size_t LDS = (size_t)(PIXAL * C + 2 * WST) * 2;
+  static_assert(M % (16 * WMW) == 0 && NT % (16 * WNW) == 0, "halo tiling");
+  static_assert((size_t)M * LDC * 2 + (size_t)2 * NT * (kThreads / NT) * 4 <= (size_t)PIXAL * C * 2,
+                "halo epilogue must fit in the patch region");
+};
+
+// chunk swizzle of a patch pixel row: 128-B rows (two per 256-B bank row) by (p >> 1) & 7,
+// 256-B rows by p & 15 -- 16 consecutive pixels read at one chunk hit distinct banks
+template <int C>
+DTF_DEV int halo_swz(int p) { return C == 64 ? ((p >> 1) & 7) : (p & 15); }
+
+template <int C, int W, int WMW, int NT>
 __global__ void __launch_bounds__(kThreads, 2)
 conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                     bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
                     float* __restrict__ stats) {
+  using H = HaloCfg<C, W, WMW, NT>;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  bf16_t* const patch = lds;                                     // [352][64]
-  bf16_t* const wst = lds + kHaloPixAl * kHaloC;                 // [2][64][64]
+  bf16_t* const patch = lds;                                     // [PIXAL][C]
+  bf16_t* const wst = lds + H::PIXAL * C;                        // [2][NT][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / H::WNW, wn = wave % H::WNW;
   const int tiles_h = g.H / kHaloTH;
   const int tm = blockIdx.x;                                     // (image, row-tile)
   const int n = tm / tiles_h, h0 = (tm % tiles_h) * kHaloTH;
-  const int n0 = blockIdx.y * 64;                                // output-channel tile
+  const int n0 = blockIdx.y * NT;                                // output-channel tile
   const i32x4_t rx = rsrc_quad(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
   const i32x4_t rw = rsrc_quad(Wt, (uint32_t)g.Kout * g.Kpad * 2u);
   const uint32_t lds_patch = lds_addr(patch), lds_w = lds_addr(wst);
 
-  // ---- patch: 44 DMAs of 8 pixels x 8 chunks; wave w issues q = w, w + 4, ...
-  const int lp = lane >> 3, slot = lane & 7;
-  for (int q = wave; q < kHaloPixAl / 8; q += 4) {
-    const int pix = q * 8 + lp;
-    const int pr = pix / kHaloPW, pc = pix - pr * kHaloPW;
-    const int h = h0 - 1 + pr, w = pc - 1;
-    const int chunk = slot ^ ((pix >> 1) & 7);
-    const bool ok = pix < kHaloPix && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-    const uint32_t off = ok ? (uint32_t)((((n * g.H + h) * g.W + w) * kHaloC + chunk * 8) * 2) : kOOB;
-    dma16(rx, lds_patch + (uint32_t)q * 1024u, off);
+  // ---- patch: whole 1-KB DMAs of PPI pixels; wave w issues q = w, w + 4, ...
+  {
+    constexpr int CPP = H::ROWB / 16;                            // chunks per pixel
+    const int lp = lane / CPP, slot = lane % CPP;
+    for (int q = wave; q < H::PIXAL / H::PPI; q += 4) {
+      const int pix = q * H::PPI + lp;
+      const int pr = pix / H::PW, pc = pix - pr * H::PW;
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const int chunk = slot ^ halo_swz<C>(pix);
+      const bool ok = pix < H::PIX && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const uint32_t off = ok ? (uint32_t)((((n * g.H + h) * g.W + w) * C + chunk * 8) * 2) : kOOB;
+      dma16(rx, lds_patch + (uint32_t)q * 1024u, off);
+    }
   }
-  // ---- filter slice of tap t: 64 output-channel rows x 64 channels, 2 DMAs per wave
-  auto issue_w = [&](int t, int stage) {
+  // ---- filter slice of step (tap t, channel slice s): NT rows x 64 channels (128-B rows)
+  const int lp8 = lane >> 3, slot8 = lane & 7;
+  auto issue_w = [&](int step, int stage) {
+    const int t = step / H::KS, s = step - t * H::KS;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NT / 32; ++i) {
       const int q = wave + 4 * i;
-      const int row = q * 8 + lp;
-      const int chunk = slot ^ ((row >> 1) & 7);
+      const int row = q * 8 + lp8;
+      const int chunk = slot8 ^ ((row >> 1) & 7);
       const int kr = n0 + row;
       const uint32_t off = (t < taps.n && kr < g.Kout)
-                               ? (uint32_t)((kr * g.Kpad + t * kHaloC + chunk * 8) * 2) : kOOB;
-      dma16(rw, lds_w + (uint32_t)(stage * kHaloWStage) * 2u + (uint32_t)q * 1024u, off);
+                               ? (uint32_t)((kr * g.Kpad + t * C + s * 64 + chunk * 8) * 2) : kOOB;
+      dma16(rw, lds_w + (uint32_t)(stage * H::WST) * 2u + (uint32_t)q * 1024u, off);
     }
   };
   issue_w(0, 0);
 
-  // per-lane A rows: output pixel m = wm*112 + 16 i + frow -> patch pixel of tap (0, 0)
+  // per-lane A rows: output pixel m = wm * (MF * 16) + 16 i + frow -> patch pixel of tap (0, 0)
   const int frow = lane & 15, fq = lane >> 4;
-  int pbase[7];
+  int pbase[H::MF];
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int m = wm * 112 + 16 * i + frow;
-    const int orow = m / kHaloW, ocol = m - orow * kHaloW;
-    pbase[i] = (orow + 1) * kHaloPW + ocol + 1;
+  for (int i = 0; i < H::MF; ++i) {
+    const int m = wm * (H::MF * 16) + 16 * i + frow;
+    const int orow = m / W, ocol = m - orow * W;
+    pbase[i] = (orow + 1) * H::PW + ocol + 1;
   }
-  f32x4_t acc[7][2];
+  f32x4_t acc[H::MF][H::NF];
 #pragma unroll
-  for (int i = 0; i < 7; ++i)
+  for (int i = 0; i < H::MF; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < H::NF; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  for (int t = 0; t < taps.n; ++t) {
-    DTF_WAIT_VM(0);            // patch (t == 0) and this tap's filter slice landed (own DMAs) ...
+  const int nsteps = taps.n * H::KS;
+  for (int step = 0; step < nsteps; ++step) {
+    DTF_WAIT_VM(0);            // patch (step 0) and this step's filter slice landed (own DMAs)...
     __syncthreads();           // ... everyone's; everyone done reading the other filter stage
-    issue_w(t + 1, (t + 1) & 1);   // past the last tap: out-of-range, no traffic
-    const int dpix = taps.dh[t] * kHaloPW + taps.dw[t];          // wave-uniform
-    const bf16_t* sw = wst + (t & 1) * kHaloWStage;
+    issue_w(step + 1, (step + 1) & 1);   // past the last step: out-of-range, no traffic
+    const int t = step / H::KS, s = step - t * H::KS;
+    const int dpix = taps.dh[t] * H::PW + taps.dw[t];            // wave-uniform
+    const bf16_t* sw = wst + (step & 1) * H::WST;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int ch = ks * 4 + fq;
-      bf16x8_t bfr[2];
+      const int ch = ks * 4 + fq;                                // chunk within the 64-ch slice
+      bf16x8_t bfr[H::NF];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = wn * 32 + 16 * j + frow;
-        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sw + r * kHaloC + ((ch ^ ((r >> 1) & 7)) << 3));
+      for (int j = 0; j < H::NF; ++j) {
+        const int r = wn * (H::NF * 16) + 16 * j + frow;
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sw + r * 64 + ((ch ^ ((r >> 1) & 7)) << 3));
       }
+      const int pch = s * 8 + ch;                                // chunk within the pixel row
 #pragma unroll
-      for (int i = 0; i < 7; ++i) {
+      for (int i = 0; i < H::MF; ++i) {
         const int p = pbase[i] + dpix;
-        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(patch + p * kHaloC + ((ch ^ ((p >> 1) & 7)) << 3));
+        const bf16x8_t af =
+            *reinterpret_cast<const bf16x8_t*>(patch + p * C + ((pch ^ halo_swz<C>(p)) << 3));
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < H::NF; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
     }
   }
   DTF_WAIT_VM(0);
   __syncthreads();
-  // ---- epilogue: bf16 tile [224][64 + 8] in LDS (over the patch) -> 16-B stores; BN partials
+  // ---- epilogue: bf16 tile [M][NT + 8] in LDS (over the patch) -> 16-B stores; BN partials
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  constexpr int LDC = 64 + 8;
+  constexpr int LDC = H::LDC;
   bf16_t* st = lds;
 #pragma unroll
-  for (int i = 0; i < 7; ++i)
+  for (int i = 0; i < H::MF; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < H::NF; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        st[(wm * 112 + 16 * i + fq * 4 + r) * LDC + wn * 32 + 16 * j + frow] = f2bf(acc[i][j][r]);
+        st[(wm * (H::MF * 16) + 16 * i + fq * 4 + r) * LDC + wn * (H::NF * 16) + 16 * j + frow] =
+            f2bf(acc[i][j][r]);
   __syncthreads();
   const long ybase = ((long)n * g.H + h0) * g.W;                 // first output pixel of the tile
-  const int oc = tid & 7;                                        // 8 chunks per 64-channel row
+  constexpr int OCPR = NT / 8;
+  const int oc = tid % OCPR;
   const bool col_ok = n0 + oc * 8 < g.Kout;
-  for (int r = tid >> 3; r < kHaloM; r += kThreads / 8) {
+  for (int r = tid / OCPR; r < H::M; r += kThreads / OCPR) {
     if (!col_ok) continue;
     *reinterpret_cast<uint4*>(Y + (ybase + r) * g.Kout + n0 + oc * 8) =
         *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
   }
   if (stats) {   // per-channel sum / sum of squares of the rounded outputs -> slab row tm
-    float* red = reinterpret_cast<float*>(st + kHaloM * LDC);    // [4][2][64]
-    const int col = tid & 63, grp = tid >> 6;
+    constexpr int GROUPS = kThreads / NT;
+    constexpr int RPG = H::M / GROUPS;
+    float* red = reinterpret_cast<float*>(st + H::M * LDC);      // [GROUPS][2][NT]
+    const int col = tid % NT, grp = tid / NT;
     float a1 = 0.f, a2 = 0.f;
-    for (int r = grp * (kHaloM / 4); r < (grp + 1) * (kHaloM / 4); ++r) {
+    for (int r = grp * RPG; r < (grp + 1) * RPG; ++r) {
       const float v = bf2f(st[r * LDC + col]);
       a1 += v;
       a2 += v * v;
     }
-    red[(grp * 2 + 0) * 64 + col] = a1;
-    red[(grp * 2 + 1) * 64 + col] = a2;
+    red[(grp * 2 + 0) * NT + col] = a1;
+    red[(grp * 2 + 1) * NT + col] = a2;
     __syncthreads();
     if (grp == 0 && n0 + col < g.Kout) {
       float a = 0.f, b = 0.f;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { a += red[(k * 2 + 0) * 64 + col]; b += red[(k * 2 + 1) * 64 + col]; }
+      for (int k = 0; k < GROUPS; ++k) { a += red[(k * 2 + 0) * NT + col]; b += red[(k * 2 + 1) * NT + col]; }
       stats[((long)tm * 2 + 0) * g.Kout + n0 + col] = a;
       stats[((long)tm * 2 + 1) * g.Kout + n0 + col] = b;
     }
@@ -881,18 +920,23 @@ static bool use_dma_kernel(long M, int Kout, int C, int taps, int bk) {
   return taps > 1 && C >= 256;
 }
 
-// the halo kernel's layer family: 3x3 stride 1 "same", 56 x 56 x 64 input, Kout % 64 == 0
-static int g_halo = 1;
+// halo kernel families (bit 0: 56 x 56 x 64 -> 64k, bit 1: 28 x 28 x 128 -> 128k): 3x3 stride-1
+// "same" convs (forward and data gradient)
+static int g_halo = 3;
 void dtf_conv_set_halo(int on) { g_halo = on; }
-static bool use_halo(const ConvGeom& g, const TapTable& taps) {
-  if (!g_halo || g.C != kHaloC || g.W != kHaloW || g.H % kHaloTH || g.Kout % 64 || taps.n != 9 ||
-      g.sh != 1 || g.sw != 1 || g.P != g.H || g.Q != g.W || g.Ho != g.H || g.Wo != g.W ||
-      g.osh != 1 || g.osw != 1 || g.oh0 || g.ow0 || g.acc || g.Kpad != 9 * kHaloC)
-    return false;
+// 0: not eligible; 1: the 56 x 56 x 64 family; 2: the 28 x 28 x 128 family
+static int halo_family(const ConvGeom& g, const TapTable& taps) {
+  if (!g_halo || g.H % kHaloTH || taps.n != 9 || g.sh != 1 || g.sw != 1 || g.P != g.H ||
+      g.Q != g.W || g.Ho != g.H || g.Wo != g.W || g.osh != 1 || g.osw != 1 || g.oh0 || g.ow0 ||
+      g.acc || g.Kpad != 9 * g.C)
+    return 0;
   for (int t = 0; t < 9; ++t)
-    if (taps.dh[t] < -1 || taps.dh[t] > 1 || taps.dw[t] < -1 || taps.dw[t] > 1) return false;
-  return true;
+    if (taps.dh[t] < -1 || taps.dh[t] > 1 || taps.dw[t] < -1 || taps.dw[t] > 1) return 0;
+  if (g.C == 64 && g.W == 56 && g.Kout % 64 == 0) return 1;
+  if ((g_halo & 2) && g.C == 128 && g.W == 28 && g.Kout % 128 == 0) return 2;
+  return 0;
 }
+static bool use_halo(const ConvGeom& g, const TapTable& taps) { return halo_family(g, taps) != 0; }
 
 // M tiles of a launch WITHOUT the halo kernel (the fused-BN-backward dgrad path, which never
 // takes it); W is accepted for API symmetry and ignored
@@ -937,11 +981,16 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
     return;
   }
   if (!bnb.part && use_halo(g, taps)) {
-    const size_t lds = (size_t)(kHaloPixAl * kHaloC + 2 * kHaloWStage) * sizeof(bf16_t);
-    static_assert((size_t)(kHaloPixAl * kHaloC + 2 * kHaloWStage) * 2 >=
-                  (size_t)kHaloM * 72 * 2 + 4 * 2 * 64 * 4, "halo epilogue LDS");
-    hipLaunchKernelGGL(conv3x3_halo_kernel, dim3((unsigned)(g.N * (g.H / kHaloTH)),
-                       (unsigned)(g.Kout / 64)), dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats);
+    const dim3 grid0((unsigned)(g.N * (g.H / kHaloTH)));
+    if (halo_family(g, taps) == 1) {
+      using Hc = HaloCfg<64, 56, 2, 64>;
+      hipLaunchKernelGGL((conv3x3_halo_kernel<64, 56, 2, 64>), dim3(grid0.x, g.Kout / 64),
+                         dim3(kThreads), Hc::LDS, st, X, Wt, Y, g, taps, stats);
+    } else {
+      using Hc = HaloCfg<128, 28, 1, 128>;
+      hipLaunchKernelGGL((conv3x3_halo_kernel<128, 28, 1, 128>), dim3(grid0.x, g.Kout / 128),
+                         dim3(kThreads), Hc::LDS, st, X, Wt, Y, g, taps, stats);
+    }
     return;
   }
   if (use_dma_kernel((long)m, g.Kout, g.C, taps.n, bk) && g.Kpad % 64 == 0) {

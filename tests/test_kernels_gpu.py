@@ -303,29 +303,31 @@ def test_batched_filter_transpose():
         assert torch.equal(o, w.permute(2, 1, 0))
 
 
-@pytest.mark.parametrize("N,K", [(2, 64), (3, 128)])
-def test_halo_conv3x3_matches_implicit_gemm(N, K):
-    """Halo-tiled 3x3 kernel (56x56x64 layers) == the implicit-GEMM kernel bit for bit (same tap /
-    k order) for the forward and the data gradient; fused BN statistics match."""
+@pytest.mark.parametrize("N,H,C,K", [(2, 56, 64, 64), (3, 56, 64, 128), (2, 28, 128, 128),
+                                     (2, 28, 128, 256)])
+def test_halo_conv3x3_matches_implicit_gemm(N, H, C, K):
+    """Halo-tiled 3x3 kernels (56x56x64 and 28x28x128 families) == the implicit-GEMM kernel bit
+    for bit (same tap / k order) for the forward and the data gradient; fused BN statistics
+    match."""
     nat = _native()
     torch.manual_seed(0)
-    x = torch.randn(N, 56, 56, 64, device=dev).to(torch.bfloat16)
-    w = (torch.randn(K, 3, 3, 64, device=dev) / 24).to(torch.bfloat16)
-    dy = torch.randn(N, 56, 56, K, device=dev).to(torch.bfloat16)
+    x = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K, 3, 3, C, device=dev) / (3 * C ** 0.5)).to(torch.bfloat16)
+    wd = w[:C].contiguous()                     # dgrad operand: Kout = C, so the halo path applies
+    dy = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
     outs = []
     try:
-        for halo in (1, 0):
+        for halo in (3, 0):
             nat._K.conv_set_halo(halo)
             y = nat.conv2d_forward(x, w, 1, 1)
-            dx = nat.conv2d_dgrad(dy[..., :64].contiguous(), w[:64], x.shape, 1, 1) if K == 64 \
-                else nat.conv2d_dgrad(dy, w, x.shape, 1, 1)
+            dx = nat.conv2d_dgrad(dy, wd, x.shape, 1, 1)
             gamma = torch.ones(K, device=dev)
             beta = torch.zeros(K, device=dev)
             ys = nat.conv2d(x, w.float(), 1, 1, bn_stats=True)
             z = nat.batch_norm(ys, gamma, beta, None, None, True, 0.9, 1e-5, relu=True)
             outs.append((y, dx, z.float()))
     finally:
-        nat._K.conv_set_halo(1)
+        nat._K.conv_set_halo(3)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
     torch.testing.assert_close(outs[0][2], outs[1][2], atol=2e-2, rtol=1e-2)
