@@ -71,12 +71,12 @@ DTF_DEV void load8f(const float* __restrict__ p, int cg, float* v) {
 // MODE 0: forward stats   acc0 += x,           acc1 += x*x
 // MODE 1: backward reduce acc0 += dz,          acc1 += dz*(x-mean)*invstd
 // mkind (MODE 1): 0 no ReLU, 1 bit mask, 2 recompute from x, 3 from y
-template <int MODE>
+template <int MODE, int MK>
 __global__ void __launch_bounds__(kThreads)
 bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                  const bf16_t* __restrict__ y, const uint8_t* __restrict__ mask,
                  const float* __restrict__ mean, const float* __restrict__ invstd, int M, int C,
-                 int rows_per_block, int mkind, float* __restrict__ partial,
+                 int rows_per_block, int mkind_unused, float* __restrict__ partial,
                  const float* __restrict__ fsc, const float* __restrict__ fsh) {
   extern __shared__ __attribute__((aligned(16))) float red[];   // [rpi][2][C]
   const int tpr = C >> 3;
@@ -90,7 +90,7 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
   if (MODE == 1 && active) {
     load8f(mean, cg, mu);
     load8f(invstd, cg, is);
-    if (mkind == 2) { load8f(fsc, cg, ksc); load8f(fsh, cg, ksh); }
+    if (MK == 2) { load8f(fsc, cg, ksc); load8f(fsh, cg, ksh); }
   }
   const int m0 = blockIdx.x * rows_per_block;
   const int m1 = min(m0 + rows_per_block, M);
@@ -109,8 +109,8 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
         xr[u] = ok ? X4[v] : make_uint4(0, 0, 0, 0);
         if (MODE == 1) {
           dr[u] = ok ? D4[v] : make_uint4(0, 0, 0, 0);
-          mb[u] = (ok && mkind == 1) ? (uint32_t)mask[v] : 0u;
-          yr[u] = (ok && mkind == 3) ? Y4[v] : make_uint4(0, 0, 0, 0);
+          mb[u] = (ok && MK == 1) ? (uint32_t)mask[v] : 0u;
+          yr[u] = (ok && MK == 3) ? Y4[v] : make_uint4(0, 0, 0, 0);
         }
       }
 #pragma unroll
@@ -123,7 +123,7 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
         } else {
           float g[8];
           unpack8(dr[u], g);
-          relu_mask8(g, xv, mb[u], yr[u], mkind, ksc, ksh);
+          relu_mask8(g, xv, mb[u], yr[u], MK, ksc, ksh);
 #pragma unroll
           for (int i = 0; i < 8; ++i) { a0[i] += g[i]; a1[i] += g[i] * (xv[i] - mu[i]) * is[i]; }
         }
@@ -328,12 +328,13 @@ bn_bwd_finalize_kernel(const double* __restrict__ level2, int S, int C, long M,
   coefC[c] = -k * db * invM - B * mean[c];
 }
 
+template <int MK>
 __global__ void __launch_bounds__(kThreads)
 bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                     const uint8_t* __restrict__ mask, const bf16_t* __restrict__ x,
                     const float* __restrict__ cA, const float* __restrict__ cB,
                     const float* __restrict__ cC, bf16_t* __restrict__ dx,
-                    bf16_t* __restrict__ dres, int M, int C, int mkind,
+                    bf16_t* __restrict__ dres, int M, int C, int mkind_unused,
                     const float* __restrict__ fsc, const float* __restrict__ fsh) {
   const int tpr = C >> 3, rpi = kThreads / tpr;
   const int cg = threadIdx.x % tpr, ro = threadIdx.x / tpr;
@@ -342,7 +343,7 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
   load8f(cA, cg, ka);
   load8f(cB, cg, kb);
   load8f(cC, cg, kc);
-  if (mkind == 2) { load8f(fsc, cg, ksc); load8f(fsh, cg, ksh); }
+  if (MK == 2) { load8f(fsc, cg, ksc); load8f(fsh, cg, ksh); }
   const uint4* D4 = reinterpret_cast<const uint4*>(dy);
   const uint4* X4 = reinterpret_cast<const uint4*>(x);
   const uint4* Y4 = reinterpret_cast<const uint4*>(y);
@@ -359,8 +360,8 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
       if (r < M) {
         dr[u] = D4[v];
         xr[u] = X4[v];
-        if (mkind == 1) mb[u] = mask[v];
-        if (mkind == 3) yr[u] = Y4[v];
+        if (MK == 1) mb[u] = mask[v];
+        if (MK == 3) yr[u] = Y4[v];
       }
     }
 #pragma unroll
@@ -371,8 +372,8 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
       float g[8], xv[8], o[8];
       unpack8(dr[u], g);
       unpack8(xr[u], xv);
-      relu_mask8(g, xv, mkind == 1 ? mb[u] : 0u, mkind == 3 ? yr[u] : make_uint4(0, 0, 0, 0),
-                 mkind, ksc, ksh);
+      relu_mask8(g, xv, MK == 1 ? mb[u] : 0u, MK == 3 ? yr[u] : make_uint4(0, 0, 0, 0),
+                 MK, ksc, ksh);
       if (dres) DR4[v] = pack8(g);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = ka[i] * g[i] + kb[i] * xv[i] + kc[i];
@@ -418,7 +419,7 @@ void dtf_bn_fwd_stats(const bf16_t* x, long M, int C, float* partial, hipStream_
   const int G = stats_grid(M, C, &rpb);
   const int rpi = kThreads / (C / 8);
   const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
-  hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(G), dim3(kThreads), lds, st, x, nullptr, nullptr,
+  hipLaunchKernelGGL((bn_reduce_kernel<0, 0>), dim3(G), dim3(kThreads), lds, st, x, nullptr, nullptr,
                      nullptr, nullptr, nullptr, (int)M, C, rpb, 0, partial, nullptr, nullptr);
 }
 
@@ -480,8 +481,17 @@ void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, c
   const int G = stats_grid(M, C, &rpb);
   const int rpi = kThreads / (C / 8);
   const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
-  hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(G), dim3(kThreads), lds, st, x, dy, y, mask, mean,
-                     invstd, (int)M, C, rpb, mk, partial, fsc, fsh);
+  // mask kind is a template parameter: the unused mask operands take no registers
+#define DTF_BN_RED(MK_)                                                                    \
+  hipLaunchKernelGGL((bn_reduce_kernel<1, MK_>), dim3(G), dim3(kThreads), lds, st, x, dy, y, mask, \
+                     mean, invstd, (int)M, C, rpb, mk, partial, fsc, fsh)
+  switch (mk) {
+    case 0: DTF_BN_RED(0); break;
+    case 1: DTF_BN_RED(1); break;
+    case 2: DTF_BN_RED(2); break;
+    default: DTF_BN_RED(3); break;
+  }
+#undef DTF_BN_RED
 }
 
 void dtf_bn_bwd_finalize_g(const float* partial, int G, long M, int C, const float* gamma,
@@ -516,6 +526,14 @@ void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, co
                       hipStream_t st) {
   check_rows(M, C);
   const int mk = mask_kind(relu, mask, fsc, fsh, y);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, dy, y,
-                     mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh);
+#define DTF_BN_BWD(MK_)                                                                    \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_>), dim3(sweep_grid(M, C)), dim3(kThreads), 0, st,   \
+                     dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh)
+  switch (mk) {
+    case 0: DTF_BN_BWD(0); break;
+    case 1: DTF_BN_BWD(1); break;
+    case 2: DTF_BN_BWD(2); break;
+    default: DTF_BN_BWD(3); break;
+  }
+#undef DTF_BN_BWD
 }
