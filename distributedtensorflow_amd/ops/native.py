@@ -33,6 +33,8 @@ if os.environ.get("DTF_WGRAD_MODE"):
     _K.wgrad_set_dma_mode(int(os.environ["DTF_WGRAD_MODE"]))
 if os.environ.get("DTF_WGRAD_PIPE"):
     _K.wgrad_set_pipe(int(os.environ["DTF_WGRAD_PIPE"]))
+if os.environ.get("DTF_CONV_DMA"):
+    _K.conv_set_dma_mode(int(os.environ["DTF_CONV_DMA"]))
 if os.environ.get("DTF_CONV_HALO"):
     _K.conv_set_halo(int(os.environ["DTF_CONV_HALO"]))
 if os.environ.get("DTF_CONV_SMALL_K"):
