@@ -405,7 +405,33 @@ inline int sweep_grid(long M, int C) {
   return (int)g;
 }
 
+// out = dy * relu_mask (1 bit per element): materialises a lazily kept residual gradient on the
+// rare paths whose consumer cannot form it in an epilogue (see ops/native.py _MaskedGrad)
+__global__ void __launch_bounds__(kThreads)
+relu_mask_apply_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+                       bf16_t* __restrict__ out, long nv) {
+  const uint4* D4 = reinterpret_cast<const uint4*>(dy);
+  uint4* O4 = reinterpret_cast<uint4*>(out);
+  for (long v = (long)blockIdx.x * kThreads + threadIdx.x; v < nv; v += (long)gridDim.x * kThreads) {
+    float g[8];
+    unpack8(D4[v], g);
+    relu_mask8(g, nullptr, mask[v], make_uint4(0, 0, 0, 0), 1, nullptr, nullptr);
+    O4[v] = pack8(g);
+  }
+}
+
 }  // namespace
+
+void dtf_relu_mask_apply(const bf16_t* dy, const uint8_t* mask, bf16_t* out, long n,
+                         hipStream_t st) {
+  if (n % 8) throw std::runtime_error("relu_mask_apply: n must be a multiple of 8");
+  const long nv = n / 8;
+  long g = (nv + kThreads - 1) / kThreads;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(relu_mask_apply_kernel, dim3((int)g), dim3(kThreads), 0, st, dy, mask, out,
+                     nv);
+}
 
 // ------------------------------------------------------------------ launchers (host)
 int dtf_bn_partial_blocks(long M, int C) {

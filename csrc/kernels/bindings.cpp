@@ -19,7 +19,11 @@ namespace py = pybind11;
 #define DTF_MAX_TAPS 64
 struct TapTable { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
 struct TapTableW { int n; int dh[DTF_MAX_TAPS]; int dw[DTF_MAX_TAPS]; };
-struct ConvGeom { int N, H, W, C, P, Q, sh, sw, Kout, Kpad, Ho, Wo, osh, osw, oh0, ow0, acc; };
+struct ConvGeom {
+  int N, H, W, C, P, Q, sh, sw, Kout, Kpad, Ho, Wo, osh, osw, oh0, ow0, acc;
+  const bf16_t* acc_src;
+  const uint8_t* acc_mask;
+};
 struct BnBwdEpi {
   const bf16_t* x; const float* mean; const float* invstd; const float* fsc; const float* fsh;
   const uint8_t* mask; float* part; int mkind; int row0;
@@ -60,6 +64,7 @@ void dtf_bn_bwd_finalize_g(const float*, int, long, int, const float*, const flo
                            float*, float*, float*, float*, float*, int, hipStream_t);
 void dtf_bn_bwd_finalize(const float*, long, int, const float*, const float*, const float*,
                          float*, float*, float*, float*, float*, int, hipStream_t);
+void dtf_relu_mask_apply(const bf16_t*, const uint8_t*, bf16_t*, long, hipStream_t);
 void dtf_bn_bwd_apply(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, const float*,
                       const float*, const float*, bf16_t*, bf16_t*, long, int, int, const float*,
                       const float*, hipStream_t);
@@ -235,6 +240,10 @@ PYBIND11_MODULE(_dtf_hip, m) {
                         P<float>(b), P<float>(c), accumulate, S(st));
     check_launch("bn_bwd_finalize");
   });
+  m.def("relu_mask_apply", [](uintptr_t dy, uintptr_t mask, uintptr_t out, long n, uintptr_t st) {
+    dtf_relu_mask_apply(P<const bf16_t>(dy), P<const uint8_t>(mask), P<bf16_t>(out), n, S(st));
+    check_launch("relu_mask_apply");
+  });
   m.def("bn_bwd_apply", [](uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t a, uintptr_t b,
                            uintptr_t c, uintptr_t dx, uintptr_t dres, long M, int C, int relu,
                            uintptr_t st, uintptr_t fsc, uintptr_t fsh, uintptr_t mask) {
@@ -314,12 +323,16 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("conv_igemm", [](uintptr_t x, uintptr_t w, uintptr_t y, std::vector<int> geom,
                          std::vector<int> dh, std::vector<int> dw, int bk, uintptr_t st,
-                         uintptr_t stats, std::vector<uintptr_t> bnb) {
+                         uintptr_t stats, std::vector<uintptr_t> bnb, uintptr_t acc_src,
+                         uintptr_t acc_mask) {
     if (geom.size() != 16 && geom.size() != 17)
       throw std::runtime_error("conv_igemm: geom needs 16 (+acc) ints");
     ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
                geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15],
-               geom.size() == 17 ? geom[16] : 0};
+               geom.size() == 17 ? geom[16] : 0, P<const bf16_t>(acc_src),
+               P<const uint8_t>(acc_mask)};
+    if (g.acc == 2 && (!g.acc_src || !g.acc_mask))
+      throw std::runtime_error("conv_igemm: acc 2 needs acc_src and acc_mask");
     // bnb = [x, mean, invstd, fsc, fsh, mask, part, mkind, row0] (fused BN-backward sums) or []
     BnBwdEpi e{};
     if (!bnb.empty()) {
@@ -333,7 +346,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("conv_igemm");
   }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("dh"), py::arg("dw"),
      py::arg("bk"), py::arg("stream"), py::arg("stats") = 0,
-     py::arg("bnb") = std::vector<uintptr_t>{});
+     py::arg("bnb") = std::vector<uintptr_t>{}, py::arg("acc_src") = 0, py::arg("acc_mask") = 0);
   m.def("bn_bwd_finalize_g", [](uintptr_t part, int G, long M, int C, uintptr_t gamma,
                                 uintptr_t mean, uintptr_t invstd, uintptr_t dg, uintptr_t db,
                                 uintptr_t a, uintptr_t b, uintptr_t c, int accumulate,

@@ -54,7 +54,30 @@ struct ConvGeom {
   int Ho, Wo;            // output tensor spatial dims
   int osh, osw, oh0, ow0;// output placement
   int acc;               // 1: Y += result (dgrad accumulating onto a residual gradient)
+                         // 2: Y = result + acc_src * relu_mask (see acc_add8)
+  const bf16_t* acc_src; // acc 2: the residual BN's incoming dy, [N, Ho, Wo, Kout] like Y
+  const uint8_t* acc_mask;  // acc 2: that BN's forward ReLU bit mask (1 byte per 8 channels)
 };
+
+// Residual-gradient accumulation in the dgrad epilogue.  acc 1 reads the materialised residual
+// gradient back from Y; acc 2 forms it on the fly as dy * relu_mask from the residual BN's own
+// inputs, so that BN's backward never writes it (saves one full-tensor write per identity block;
+// bit-identical: the masked copy is exact).
+DTF_DEV uint4 acc_add8(const ConvGeom& g, const bf16_t* Y, long off, uint4 v) {
+  float a[8], b[8];
+  unpack8(v, a);
+  if (g.acc == 2) {
+    unpack8(*reinterpret_cast<const uint4*>(g.acc_src + off), b);
+    const uint32_t m = g.acc_mask[off >> 3];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = (m >> e) & 1u ? b[e] : 0.f;
+  } else {
+    unpack8(*reinterpret_cast<const uint4*>(Y + off), b);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] += b[e];
+  return pack8(a);
+}
 
 // Fused BatchNorm-backward statistics in the DATA-GRADIENT epilogue: when this launch produces
 // dy of a training-mode BN's output (the BN sits right before this conv in the forward pass), the
@@ -408,14 +431,8 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     const int r = tid / OCPR + k * OROWS;
     const long off = offs[k];
     uint4 v = *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
-    if (g.acc) {   // fused residual-gradient add: one extra 16-B read instead of an add kernel
-      float a[8], b[8];
-      unpack8(v, a);
-      unpack8(*reinterpret_cast<const uint4*>(Y + off), b);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a[e] += b[e];
-      v = pack8(a);
-    }
+    // fused residual-gradient add: one extra 16-B read instead of an add kernel
+    if (g.acc) v = acc_add8(g, Y, off, v);
     *reinterpret_cast<uint4*>(Y + off) = v;
     if constexpr (BNB) ba.add_pre(bnb, v, xpre[k], (mpre[k >> 2] >> (8 * (k & 3))) & 0xFFu);
   }
@@ -672,14 +689,7 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
     const long off = offs[k];
     const bf16_t* st = r < 128 ? s0 : s1;
     uint4 v = *reinterpret_cast<const uint4*>(st + (r & 127) * LDC + oc * 8);
-    if (g.acc) {
-      float a[8], b[8];
-      unpack8(v, a);
-      unpack8(*reinterpret_cast<const uint4*>(Y + off), b);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a[e] += b[e];
-      v = pack8(a);
-    }
+    if (g.acc) v = acc_add8(g, Y, off, v);
     *reinterpret_cast<uint4*>(Y + off) = v;
     if constexpr (BNB) ba.add_pre(bnb, v, xpre[k], mpre[k]);
   }

@@ -109,8 +109,10 @@ def _fwd_geom(xshape, K, taps, P, Q, sh, sw, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
 
 
 def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
-                stats=None, accumulate=False, bnb=()):
-    """wmat: [K, T*C] bf16 (rows zero-padded here to a multiple of 32 for the gather path)."""
+                stats=None, accumulate=False, bnb=(), acc_from=None):
+    """wmat: [K, T*C] bf16 (rows zero-padded here to a multiple of 32 for the gather path).
+    ``acc_from``: a :class:`_MaskedGrad` the epilogue adds (as dy * mask) instead of reading
+    ``out`` back (geom acc mode 2)."""
     n, h, w, c = x.shape
     dh = [t[0] for t in taps]
     dw = [t[1] for t in taps]
@@ -120,7 +122,14 @@ def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0
         padded = torch.zeros(K, kpad, device=x.device, dtype=_BF16)
         padded[:, :kdim] = wmat
         wmat = padded
-    geom = [n, h, w, c, P, Q, sh, sw, K, kpad, Ho, Wo, osh, osw, oh0, ow0, int(accumulate)]
+    geom = [n, h, w, c, P, Q, sh, sw, K, kpad, Ho, Wo, osh, osw, oh0, ow0,
+            2 if acc_from is not None else int(accumulate)]
+    if acc_from is not None:
+        if tuple(acc_from.dy.shape) != tuple(out.shape) or acc_from.dy.dtype != _BF16:
+            raise ValueError("masked residual gradient does not match the dgrad output")
+        _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
+                      _p(stats), list(bnb), acc_from.dy.data_ptr(), acc_from.mask.data_ptr())
+        return
     _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
                   _p(stats), list(bnb))
 
@@ -177,11 +186,12 @@ def _dgrad_filter(wflat):
     return wflat.permute(2, 1, 0).contiguous()
 
 
-def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None):
+def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_from=None):
     """dX of conv2d via per-phase-class tap tables (see csrc/kernels/conv.hip header).
     ``out``: an existing bf16 gradient of x to ADD into.  ``bnb``: the BatchNorm whose output x
     is (its ``_dtf_bnb`` record): the epilogue then also emits that BN's backward partial sums,
-    attached to the result as ``_dtf_bnb_part`` (see :class:`_BatchNorm`)."""
+    attached to the result as ``_dtf_bnb_part`` (see :class:`_BatchNorm`).  ``acc_from``: a
+    :class:`_MaskedGrad` to add (single-phase launches only: stride 1)."""
     K, R, S, C = w_bf16.shape
     n, h, wd, c = x_shape
     sh, sw = _pair(stride)
@@ -209,11 +219,15 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None):
                 need_zero = True
                 continue
             launches.append((a, b, Pc, Qc, taps, idx))
+    if acc_from is not None and (out is not None or len(launches) != 1 or need_zero):
+        out = acc_from.materialize() if out is None else out.add_(acc_from.materialize())
+        acc_from = None
     acc = out is not None
     # accumulating: phases without taps contribute zero (nothing to add); the phase launches
     # partition the output, so every element is read-modified-written at most once
     dx = out if acc else (torch.zeros if need_zero else torch.empty)(
         n, h, wd, C, device=dy.device, dtype=_BF16)
+    acc = acc or acc_from is not None
     dyc = dy.contiguous()
     part, row0 = None, 0
     if bnb is not None:
@@ -237,7 +251,7 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None):
             extra = base + [row0]
             row0 += rows[li]
         _launch_fwd(dyc, wd_mat.reshape(C, -1), C, taps, Pc, Qc, 1, 1, dx, h, wd, sh, sw, a, b,
-                    accumulate=acc, bnb=extra)
+                    accumulate=acc, bnb=extra, acc_from=acc_from)
     if part is not None:
         dx._dtf_bnb_part = (part, G, n * h * wd, C, tok)
     return dx
@@ -336,8 +350,12 @@ class _Conv2d(torch.autograd.Function):
                 # identity shortcut: the block's final BN left d(residual) here; accumulate this
                 # conv's dgrad onto it in the epilogue instead of a separate bf16 add kernel
                 del ctx.x_ref._dtf_pending_grad
-                dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding, out=pending,
-                                  bnb=ctx.bnb)
+                if isinstance(pending, _MaskedGrad):
+                    dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding, bnb=ctx.bnb,
+                                      acc_from=pending)
+                else:
+                    dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding, out=pending,
+                                      bnb=ctx.bnb)
             else:
                 dx = conv2d_dgrad(dy, wb, xb.shape, ctx.stride, ctx.padding,
                                   bnb=ctx.bnb if pending is None and not padded else None)
@@ -345,6 +363,8 @@ class _Conv2d(torch.autograd.Function):
                     dx = dx[..., :C].contiguous()
                 if pending is not None:
                     del ctx.x_ref._dtf_pending_grad
+                    if isinstance(pending, _MaskedGrad):
+                        pending = pending.materialize()
                     dx = dx + pending
         ctx.x_ref = None
         ctx.bnb = None
@@ -386,6 +406,23 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
 # ----------------------------------------------------------------------------- batch norm
 
 _FUSE_RESIDUAL_GRAD = os.environ.get("DTF_FUSE_RESIDUAL_GRAD", "1") == "1"
+_LAZY_RESIDUAL_GRAD = os.environ.get("DTF_LAZY_RESIDUAL_GRAD", "1") == "1"
+
+
+class _MaskedGrad:
+    """d(residual) of a residual+ReLU BatchNorm kept as (dy, forward ReLU bit mask) rather
+    than a materialised bf16 tensor; the identity-shortcut dgrad adds dy * mask in its epilogue."""
+
+    __slots__ = ("dy", "mask")
+
+    def __init__(self, dy, mask):
+        self.dy, self.mask = dy, mask
+
+    def materialize(self):
+        out = torch.empty_like(self.dy)
+        _K.relu_mask_apply(self.dy.data_ptr(), self.mask.data_ptr(), out.data_ptr(),
+                           self.dy.numel(), _st())
+        return out
 
 
 class _BatchNorm(torch.autograd.Function):
@@ -482,11 +519,17 @@ class _BatchNorm(torch.autograd.Function):
             for p in ctx.params:
                 _grad_ready(p)
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if ctx.has_res else None
+        lazy = (ctx.has_res and ctx.res_ref is not None and _LAZY_RESIDUAL_GRAD
+                and mask is not None)
+        dres = torch.empty_like(x) if ctx.has_res and not lazy else None
         _K.bn_bwd_apply(dy.data_ptr(), 0, x.data_ptr(), gb[2].data_ptr(),
                         gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
                         int(ctx.relu), st, sc_ptr, sh_ptr, _p(mask))
-        if dres is not None and ctx.res_ref is not None:
+        if lazy:
+            # d(residual) = dy * relu_mask is never written: the consuming dgrad forms it in its
+            # epilogue from dy and the bit mask (conv geom acc mode 2)
+            ctx.res_ref._dtf_pending_grad = _MaskedGrad(dy, mask)
+        elif dres is not None and ctx.res_ref is not None:
             ctx.res_ref._dtf_pending_grad = dres
             dres = None
         ctx.res_ref = None

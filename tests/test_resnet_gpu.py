@@ -22,12 +22,13 @@ def _inputs(n=4, s=64):
     return x.cuda().bfloat16(), y.cuda()
 
 
-def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False):
+def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False, lazy=True):
     """Gradients of one step.  The fused BN-backward sums (summation order differs from the
     reduce kernel) stay off unless asked for, so the other fusions can be checked bit-exactly."""
     prev, prev_r, prev_s = native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD, native._SHARE_INPUT_GRAD
-    prev_b = native._FUSE_BN_BWD
+    prev_b, prev_l = native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD
     native._FUSE_BN_BWD = fuse_bnb
+    native._LAZY_RESIDUAL_GRAD = lazy
     native._DIRECT_GRAD = direct
     native._FUSE_RESIDUAL_GRAD = fuse_res
     native._SHARE_INPUT_GRAD = share
@@ -42,7 +43,7 @@ def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False):
     finally:
         native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD = prev, prev_r
         native._SHARE_INPUT_GRAD = prev_s
-        native._FUSE_BN_BWD = prev_b
+        native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD = prev_b, prev_l
 
 
 def test_direct_grad_path_bit_identical():
@@ -140,6 +141,34 @@ def test_residual_grad_fusion_bit_identical():
     lb, gb = _grads(copy.deepcopy(base), True, fuse_res=False)
     assert la == lb
     assert torch.equal(ga, gb)
+
+
+@pytest.mark.parametrize("dma", [-1, 0, 1])
+def test_lazy_residual_grad_bit_identical(dma):
+    """Identity blocks: d(residual) formed as dy * relu_mask inside c1's dgrad epilogue (geom
+    acc mode 2, never materialised) == the BN writing it and the epilogue reading it back; for
+    the register-staged and the LDS-DMA dgrad kernels."""
+    torch.manual_seed(0)
+    base = resnet50().cuda()
+    native._K.conv_set_dma_mode(dma)
+    try:
+        la, ga = _grads(copy.deepcopy(base), True, lazy=True)
+        lb, gb = _grads(copy.deepcopy(base), True, lazy=False)
+    finally:
+        native._K.conv_set_dma_mode(-1)
+    assert la == lb
+    assert torch.equal(ga, gb)
+
+
+def test_masked_grad_materialize():
+    """Fallback of the lazy residual gradient: dy * bit mask, vs torch."""
+    torch.manual_seed(0)
+    dy = torch.randn(4, 7, 5, 24, device="cuda").to(torch.bfloat16)
+    keep = torch.rand(dy.shape, device="cuda") > 0.4
+    bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)
+    mask = bits.sum(dim=1).to(torch.uint8)
+    out = native._MaskedGrad(dy, mask).materialize()
+    assert torch.equal(out, torch.where(keep, dy, torch.zeros_like(dy)))
 
 
 def test_shared_input_dgrad_bit_identical():
