@@ -334,8 +334,12 @@ void col_sum(const float* part, long region, int nq, int P, int N, ColSumOut out
 }
 
 // Column sums of a bf16 [T][N] matrix into fp32 (bias gradients of library-GEMM dense layers):
-// level 1 reads 16 B (8 columns) per lane, 4 row groups per block, grid (N/512, S slices) ->
-// ws[S][N]; level 2 = col_sum_final_kernel (optionally accumulating into `out`).
+// level 1 reads 16 B (8 columns) per lane, 4 row groups per block, 4 rows in flight per lane,
+// grid (N/512, S slices of R rows) -> ws[S][N]; level 2 (bf16_col_sum_final_kernel) sums the S
+// slices in a fixed order with 16 row groups per 16 float4 columns, so even N = 768 spreads over
+// enough blocks (the first version used 32 slices: 64 blocks for N = 768, ~0.4 TB/s).
+constexpr int kBf16ColSplits = 256;
+
 __global__ void __launch_bounds__(256)
 bf16_col_sum_split_kernel(const bf16_t* __restrict__ x, int T, int N, float* __restrict__ ws, int R) {
   __shared__ float red[4][64][9];
@@ -344,9 +348,24 @@ bf16_col_sum_split_kernel(const bf16_t* __restrict__ x, int T, int N, float* __r
   const int r0 = blockIdx.y * R, r1 = min(T, r0 + R);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (cv * 8 < N) {
-    for (int r = r0 + rg; r < r1; r += 4) {
+    const uint4* X4 = reinterpret_cast<const uint4*>(x) + cv;
+    const long rs = N / 8;
+    int r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = X4[(long)(r + 4 * u) * rs];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += f[e];
+      }
+    }
+    for (; r < r1; r += 4) {
       float f[8];
-      unpack8(reinterpret_cast<const uint4*>(x + (long)r * N)[cv], f);
+      unpack8(X4[(long)r * rs], f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += f[e];
     }
@@ -365,19 +384,47 @@ bf16_col_sum_split_kernel(const bf16_t* __restrict__ x, int T, int N, float* __r
   }
 }
 
+// level 2: 16 float4 columns x 16 slice groups per block, fixed-order combine (+= into out)
+__global__ void __launch_bounds__(256)
+bf16_col_sum_final_kernel(const float* __restrict__ ws, int S, int N, float* __restrict__ out,
+                          int accumulate) {
+  __shared__ float4 red[16][16];
+  const int c4 = blockIdx.x * 16 + (threadIdx.x & 15);
+  const int rg = threadIdx.x >> 4;
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c4 * 4 < N)
+    for (int k = rg; k < S; k += 16) {
+      const float4 v = reinterpret_cast<const float4*>(ws + (long)k * N)[c4];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+  red[rg][threadIdx.x & 15] = t;
+  __syncthreads();
+  if (rg == 0 && c4 * 4 < N) {
+    float4 u = red[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      const float4 v = red[k][threadIdx.x];
+      u.x += v.x; u.y += v.y; u.z += v.z; u.w += v.w;
+    }
+    float4* o = reinterpret_cast<float4*>(out) + c4;
+    if (accumulate) { const float4 v = *o; u.x += v.x; u.y += v.y; u.z += v.z; u.w += v.w; }
+    *o = u;
+  }
+}
+
 }  // namespace
 
-int dtf_bf16_col_sum_ws_floats(int N) { return kColSplits * N; }
+int dtf_bf16_col_sum_ws_floats(int N) { return kBf16ColSplits * N; }
 
 void dtf_bf16_col_sum(const bf16_t* x, int T, int N, float* ws, float* out, int accumulate,
                       hipStream_t st) {
   if (N % 8) throw std::runtime_error("bf16_col_sum: N % 8 != 0");
   int S = T / 64;
-  S = S < 1 ? 1 : (S > kColSplits ? kColSplits : S);
+  S = S < 1 ? 1 : (S > kBf16ColSplits ? kBf16ColSplits : S);
   const int R = (T + S - 1) / S;
   hipLaunchKernelGGL(bf16_col_sum_split_kernel, dim3((N / 8 + 63) / 64, S), dim3(256), 0, st, x, T, N, ws, R);
-  hipLaunchKernelGGL(col_sum_final_kernel, dim3((N / 4 + 63) / 64, 1, 1), dim3(256), 0, st, ws, 0L, 0, S,
-                     N, ColSumOut{{out, nullptr, nullptr}}, accumulate);
+  hipLaunchKernelGGL(bf16_col_sum_final_kernel, dim3((N / 4 + 15) / 16), dim3(256), 0, st, ws, S,
+                     N, out, accumulate);
 }
 
 namespace {
