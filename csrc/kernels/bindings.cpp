@@ -106,14 +106,14 @@ void dtf_ln_fwd(const bf16_t*, const float*, const bf16_t*, const float*, const 
 int dtf_ln_bwd_blocks(int);
 void dtf_ln_bwd(const bf16_t*, const bf16_t*, const float*, const float*, const float*, bf16_t*,
                 bf16_t*, float*, float*, float*, float*, int, int, float, uint32_t, float,
-                uint32_t, hipStream_t);
+                uint32_t, hipStream_t, int);
 void dtf_bias_gelu_fwd(const bf16_t*, const float*, bf16_t*, long, int, hipStream_t);
 int dtf_bias_gelu_bwd_blocks(int);
 int dtf_bf16_col_sum_ws_floats(int);
 void dtf_bf16_col_sum(const bf16_t*, int, int, float*, float*, int, hipStream_t);
 void dtf_slab_reduce(const float*, float*, long, int, int, hipStream_t);
 void dtf_bias_gelu_bwd(const bf16_t*, const bf16_t*, const float*, bf16_t*, float*, float*, int,
-                       int, hipStream_t);
+                       int, hipStream_t, int);
 void dtf_attn_fwd(const bf16_t*, const float*, bf16_t*, float*, int, int, int, float, float,
                   uint32_t, hipStream_t);
 void dtf_attn_bwd(const bf16_t*, const float*, const bf16_t*, const bf16_t*, const float*, float*,
@@ -396,13 +396,17 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("ln_bwd", [](uintptr_t dy, uintptr_t s, uintptr_t mean, uintptr_t rstd, uintptr_t gamma,
                      uintptr_t ds, uintptr_t da, uintptr_t part, uintptr_t dgamma,
                      uintptr_t dbeta, uintptr_t dbias, int M, int H, float p_pre,
-                     uint32_t seed_pre, float p_post, uint32_t seed_post, uintptr_t st) {
+                     uint32_t seed_pre, float p_post, uint32_t seed_post, uintptr_t st,
+                     int accumulate) {
     dtf_ln_bwd(P<const bf16_t>(dy), P<const bf16_t>(s), P<const float>(mean),
                P<const float>(rstd), P<const float>(gamma), P<bf16_t>(ds), P<bf16_t>(da),
                P<float>(part), P<float>(dgamma), P<float>(dbeta), P<float>(dbias), M, H, p_pre,
-               seed_pre, p_post, seed_post, S(st));
+               seed_pre, p_post, seed_post, S(st), accumulate);
     check_launch("ln_bwd");
-  });
+  }, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
+     py::arg("ds"), py::arg("da"), py::arg("part"), py::arg("dgamma"), py::arg("dbeta"),
+     py::arg("dbias"), py::arg("M"), py::arg("H"), py::arg("p_pre"), py::arg("seed_pre"),
+     py::arg("p_post"), py::arg("seed_post"), py::arg("stream"), py::arg("accumulate") = 0);
   m.def("bias_gelu_fwd", [](uintptr_t a, uintptr_t bias, uintptr_t y, long M, int N,
                             uintptr_t st) {
     dtf_bias_gelu_fwd(P<const bf16_t>(a), P<const float>(bias), P<bf16_t>(y), M, N, S(st));
@@ -419,11 +423,13 @@ PYBIND11_MODULE(_dtf_hip, m) {
     dtf_slab_reduce(P<const float>(ws), P<float>(out), n, nsplit, accumulate, S(stream));
   });
   m.def("bias_gelu_bwd", [](uintptr_t dy, uintptr_t a, uintptr_t bias, uintptr_t da,
-                            uintptr_t part, uintptr_t dbias, int M, int N, uintptr_t st) {
+                            uintptr_t part, uintptr_t dbias, int M, int N, uintptr_t st,
+                            int accumulate) {
     dtf_bias_gelu_bwd(P<const bf16_t>(dy), P<const bf16_t>(a), P<const float>(bias),
-                      P<bf16_t>(da), P<float>(part), P<float>(dbias), M, N, S(st));
+                      P<bf16_t>(da), P<float>(part), P<float>(dbias), M, N, S(st), accumulate);
     check_launch("bias_gelu_bwd");
-  });
+  }, py::arg("dy"), py::arg("a"), py::arg("bias"), py::arg("da"), py::arg("part"),
+     py::arg("dbias"), py::arg("M"), py::arg("N"), py::arg("stream"), py::arg("accumulate") = 0);
   m.def("attn_fwd", [](uintptr_t qkv, uintptr_t mask, uintptr_t out, uintptr_t lse, int B, int S_,
                        int H, float scale, float p, uint32_t seed, uintptr_t st) {
     dtf_attn_fwd(P<const bf16_t>(qkv), P<const float>(mask), P<bf16_t>(out), P<float>(lse), B,

@@ -324,13 +324,15 @@ col_sum_final_kernel(const float* __restrict__ part, long region, int P, int S, 
 
 // part: nq quantities, each `region` floats apart: [P][N] partial rows then kColSplits rows of
 // workspace.  Two launches regardless of nq.
-void col_sum(const float* part, long region, int nq, int P, int N, ColSumOut outs, hipStream_t st) {
+void col_sum(const float* part, long region, int nq, int P, int N, ColSumOut outs, hipStream_t st,
+             int accumulate = 0) {
   int S = P / 16;
   S = S < 1 ? 1 : (S > kColSplits ? kColSplits : S);
   const int R = (P + S - 1) / S;
   const int gx = (N / 4 + 63) / 64;
   hipLaunchKernelGGL(col_sum_split_kernel, dim3(gx, S, nq), dim3(256), 0, st, part, region, P, N, R);
-  hipLaunchKernelGGL(col_sum_final_kernel, dim3(gx, 1, nq), dim3(256), 0, st, part, region, P, S, N, outs, 0);
+  hipLaunchKernelGGL(col_sum_final_kernel, dim3(gx, 1, nq), dim3(256), 0, st, part, region, P, S, N, outs,
+                     accumulate);
 }
 
 // Column sums of a bf16 [T][N] matrix into fp32 (bias gradients of library-GEMM dense layers):
@@ -953,7 +955,7 @@ int dtf_ln_bwd_blocks(int M) { return ln_bwd_rows(M) + kColSplits; }
 void dtf_ln_bwd(const bf16_t* dy, const bf16_t* s, const float* mean, const float* rstd,
                 const float* gamma, bf16_t* ds, bf16_t* da, float* part, float* dgamma,
                 float* dbeta, float* dbias, int M, int H, float p_pre, uint32_t seed_pre,
-                float p_post, uint32_t seed_post, hipStream_t st) {
+                float p_post, uint32_t seed_post, hipStream_t st, int accumulate) {
   if (H % 256 != 0 || H > 1024) throw std::runtime_error("ln_bwd: H must be 256/512/768/1024");
   const int nblk = ln_bwd_rows(M);
   const long region = (long)dtf_ln_bwd_blocks(M) * H;   // partial rows + col-sum workspace
@@ -970,7 +972,7 @@ void dtf_ln_bwd(const bf16_t* dy, const bf16_t* s, const float* mean, const floa
     case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, st, g); break;
     default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, block, 0, st, g); break;
   }
-  col_sum(part, region, dbias ? 3 : 2, nblk, H, ColSumOut{{dgamma, dbeta, dbias}}, st);
+  col_sum(part, region, dbias ? 3 : 2, nblk, H, ColSumOut{{dgamma, dbeta, dbias}}, st, accumulate);
 }
 
 void dtf_bias_gelu_fwd(const bf16_t* a, const float* bias, bf16_t* y, long M, int N,
@@ -989,12 +991,12 @@ static int bias_gelu_rows(int M) { return (M + 15) / 16; }
 int dtf_bias_gelu_bwd_blocks(int M) { return bias_gelu_rows(M) + kColSplits; }
 
 void dtf_bias_gelu_bwd(const bf16_t* dy, const bf16_t* a, const float* bias, bf16_t* da,
-                       float* part, float* dbias, int M, int N, hipStream_t st) {
+                       float* part, float* dbias, int M, int N, hipStream_t st, int accumulate) {
   if (N % 8) throw std::runtime_error("bias_gelu: N % 8 != 0");
   const int nblk = bias_gelu_rows(M);
   hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3(nblk), dim3(256), 0, st, dy, a, bias, da,
                      dbias ? part : nullptr, M, N, 16);
-  if (dbias) col_sum(part, 0, 1, nblk, N, ColSumOut{{dbias, nullptr, nullptr}}, st);
+  if (dbias) col_sum(part, 0, 1, nblk, N, ColSumOut{{dbias, nullptr, nullptr}}, st, accumulate);
 }
 
 static AttnGeom attn_geom(int B, int S, int H, float scale, float p, uint32_t seed) {

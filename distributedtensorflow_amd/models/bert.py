@@ -110,14 +110,18 @@ class BertLayer(nn.Module):
         ctx = ops.attention_qkv(qkv, mask, B, S, cfg.num_attention_heads,
                                 cfg.attention_probs_dropout_prob, self.training)
         a = self.attn_out.gemm(ctx)
+        # x feeds the QKV dense above and the residual here: its two gradients are summed by
+        # that dense's dgrad GEMM (beta = 1), not by a separate add
         x = ops.bias_dropout_add_layer_norm(a, self.attn_out.bias, x, self.attn_ln.gamma,
                                             self.attn_ln.beta, cfg.hidden_dropout_prob,
-                                            self.training, cfg.layer_norm_eps)
+                                            self.training, cfg.layer_norm_eps,
+                                            residual_to_dense=True)
         h = ops.bias_gelu(self.inter.gemm(x), self.inter.bias)
         o = self.out.gemm(h)
         return ops.bias_dropout_add_layer_norm(o, self.out.bias, x, self.out_ln.gamma,
                                                self.out_ln.beta, cfg.hidden_dropout_prob,
-                                               self.training, cfg.layer_norm_eps)
+                                               self.training, cfg.layer_norm_eps,
+                                               residual_to_dense=True)
 
 
 class BertForPreTraining(Layer):

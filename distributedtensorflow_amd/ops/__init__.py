@@ -135,10 +135,15 @@ def _nlp():
     return native_nlp
 
 
-def bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p=0.0, training=True, eps=1e-12):
-    """LN(dropout(a + bias) + residual): the BERT sub-layer output, one fused kernel."""
+def bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p=0.0, training=True, eps=1e-12,
+                                residual_to_dense=False):
+    """LN(dropout(a + bias) + residual): the BERT sub-layer output, one fused kernel.
+    ``residual_to_dense``: the caller guarantees ``residual`` is also the input of a later
+    :func:`dense` (native path: that GEMM's dgrad then accumulates d(residual) with beta = 1
+    instead of autograd adding the two bf16 gradients)."""
     if _use_native(a):
-        return _nlp().bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p, training, eps)
+        return _nlp().bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p, training, eps,
+                                                  residual_to_dense)
     return reference.bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p, training, eps)
 
 

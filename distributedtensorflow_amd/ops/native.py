@@ -645,6 +645,7 @@ class _Dense(torch.autograd.Function):
     def forward(ctx, x, w_master, wb, b):
         ctx.save_for_backward(x, wb)
         ctx.w_param, ctx.b_param = w_master, b
+        ctx.x_ref = x     # a fused LayerNorm may leave d(x) here (residual_to_dense)
         ctx.has_b = b is not None
         return torch.nn.functional.linear(x, wb, None if b is None else b.to(x.dtype))
 
@@ -655,8 +656,18 @@ class _Dense(torch.autograd.Function):
         x2, dy2 = x.reshape(-1, i), dy.reshape(-1, o)
         T = x2.shape[0]
         dx = dw = db = None
+        pending = getattr(ctx.x_ref, "_dtf_pending_grad", None)
+        if pending is not None:
+            del ctx.x_ref._dtf_pending_grad
+        ctx.x_ref = None
         if ctx.needs_input_grad[0]:
-            dx = (dy2 @ wb).reshape(x.shape)
+            if pending is not None and pending.dtype == dy2.dtype and pending.is_contiguous():
+                # d(x) = d(residual) + dy @ W as one GEMM with beta = 1 on the residual gradient
+                dx = pending.view(-1, i).addmm_(dy2, wb).view(x.shape)
+            else:
+                dx = (dy2 @ wb).reshape(x.shape)
+                if pending is not None:
+                    dx = dx + pending.view(x.shape)
         if ctx.needs_input_grad[1]:
             target = _direct_grad(ctx.w_param)
             S = _wgrad_splits(T, o, i) if (o * i) % 4 == 0 and dy2.dtype == x2.dtype else 1

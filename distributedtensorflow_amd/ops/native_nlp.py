@@ -12,11 +12,15 @@ dropout after the embedding LayerNorm, ``LN(dropout(dense(x)) + x)`` sub-layer o
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
-from .native import _K, _BF16, _bf16_weight, _p, _st
+from .native import _K, _BF16, _bf16_weight, _direct_grad, _grad_ready, _p, _st
 
 AD = 64   # attention head dim supported by the MFMA kernels
+# fused LayerNorm -> dense dgrad hand-off of the residual gradient (bias_dropout_add_layer_norm)
+_RESIDUAL_TO_DENSE = os.environ.get("DTF_RESIDUAL_TO_DENSE", "1") == "1"
 
 
 def next_seed() -> int:
@@ -33,7 +37,7 @@ class _FusedLayerNorm(torch.autograd.Function):
     """y = LN(dropout(a + bias) + res) * gamma + beta   (bias / res / dropout optional)."""
 
     @staticmethod
-    def forward(ctx, a, bias, res, gamma, beta, p, eps):
+    def forward(ctx, a, bias, res, gamma, beta, p, eps, res_to_dense=False):
         H = a.shape[-1]
         a2 = a.reshape(-1, H).contiguous()
         M = a2.shape[0]
@@ -50,6 +54,9 @@ class _FusedLayerNorm(torch.autograd.Function):
                   float(p), seed, 0.0, 0, 0, 0, 0, 0, 0, 1, _st())
         ctx.save_for_backward(s if fused else a2, mean, rstd, g32)
         ctx.cfg = (M, H, float(p), seed, bias is not None, res is not None, a.shape)
+        ctx.params = (gamma, beta, bias)
+        # d(res) handed to the dense layer that also reads res (see _Dense.backward)
+        ctx.res_ref = res if res_to_dense else None
         return y.view(a.shape)
 
     @staticmethod
@@ -61,22 +68,45 @@ class _FusedLayerNorm(torch.autograd.Function):
         da = torch.empty_like(dy2) if p > 0 else None
         nblk = _K.ln_bwd_blocks(M)
         part = torch.empty(3 * nblk * H, device=dy.device, dtype=torch.float32)
-        dgamma = torch.empty(H, device=dy.device, dtype=torch.float32)
-        dbeta = torch.empty_like(dgamma)
-        dbias = torch.empty_like(dgamma) if has_bias else None
+        # gamma / beta / bias gradients summed straight into the optimizer's flat fp32 buffer
+        # when it exposes one (saves autograd's separate `grad += g` launch per parameter)
+        gamma_p, beta_p, bias_p = ctx.params
+        ctx.params = None
+        tgt = [_direct_grad(gamma_p), _direct_grad(beta_p),
+               _direct_grad(bias_p) if has_bias else None]
+        direct = tgt[0] is not None and tgt[1] is not None and (not has_bias or tgt[2] is not None)
+        if direct:
+            dgamma, dbeta, dbias = tgt
+        else:
+            dgamma = torch.empty(H, device=dy.device, dtype=torch.float32)
+            dbeta = torch.empty_like(dgamma)
+            dbias = torch.empty_like(dgamma) if has_bias else None
         _K.ln_bwd(dy2.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(), g32.data_ptr(),
                   ds.data_ptr(), _p(da), part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(),
-                  _p(dbias), M, H, p, seed, 0.0, 0, _st())
+                  _p(dbias), M, H, p, seed, 0.0, 0, _st(), int(direct))
+        if direct:
+            for q in (gamma_p, beta_p, bias_p if has_bias else None):
+                if q is not None:
+                    _grad_ready(q)
+            dgamma = dbeta = dbias = None
         d_a = (da if da is not None else ds).view(shape)
-        return (d_a, dbias, ds.view(shape) if has_res else None, dgamma, dbeta, None, None)
+        d_res = ds.view(shape) if has_res else None
+        if d_res is not None and ctx.res_ref is not None:
+            ctx.res_ref._dtf_pending_grad = d_res
+            d_res = None
+        ctx.res_ref = None
+        return (d_a, dbias, d_res, dgamma, dbeta, None, None, None)
 
 
 def layer_norm(x, gamma, beta, eps=1e-12):
     return _FusedLayerNorm.apply(x, None, None, gamma, beta, 0.0, eps)
 
 
-def bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p=0.0, training=True, eps=1e-12):
-    return _FusedLayerNorm.apply(a, bias, residual, gamma, beta, p if training else 0.0, eps)
+def bias_dropout_add_layer_norm(a, bias, residual, gamma, beta, p=0.0, training=True, eps=1e-12,
+                                residual_to_dense=False):
+    return _FusedLayerNorm.apply(a, bias, residual, gamma, beta, p if training else 0.0, eps,
+                                 bool(residual_to_dense and _RESIDUAL_TO_DENSE
+                                      and residual is not None and residual.requires_grad))
 
 
 # ----------------------------------------------------------------------------- embeddings
@@ -151,6 +181,7 @@ class _BiasGelu(torch.autograd.Function):
         _K.bias_gelu_fwd(a2.data_ptr(), _p(b32), y.data_ptr(), a2.shape[0], N, _st())
         ctx.save_for_backward(a2, b32)
         ctx.cfg = (bias is not None, a.shape)
+        ctx.bias_p = bias
         return y.view(a.shape)
 
     @staticmethod
@@ -160,11 +191,17 @@ class _BiasGelu(torch.autograd.Function):
         M, N = a2.shape
         dy2 = dy.reshape(M, N).to(_BF16).contiguous()
         da = torch.empty_like(a2)
-        dbias = torch.empty(N, device=dy.device, dtype=torch.float32) if has_bias else None
+        bias_p, ctx.bias_p = ctx.bias_p, None
+        target = _direct_grad(bias_p) if has_bias else None
+        dbias = target if target is not None else (
+            torch.empty(N, device=dy.device, dtype=torch.float32) if has_bias else None)
         part = torch.empty(_K.bias_gelu_bwd_blocks(M) * N, device=dy.device,
                            dtype=torch.float32) if has_bias else None
         _K.bias_gelu_bwd(dy2.data_ptr(), a2.data_ptr(), _p(b32), da.data_ptr(), _p(part),
-                         _p(dbias), M, N, _st())
+                         _p(dbias), M, N, _st(), int(target is not None))
+        if target is not None:
+            _grad_ready(bias_p)
+            dbias = None
         return da.view(shape), dbias
 
 
