@@ -56,6 +56,11 @@ def parse():
     p.add_argument("--num-ps", type=int, default=1)
     p.add_argument("--seq-len", type=int, default=128)
     p.add_argument("--max-predictions", type=int, default=20)
+    p.add_argument("--gemm-tuning", choices=("auto", "off", "tune"), default="auto",
+                   help="hipBLASLt solution choice for the library GEMMs (PyTorch TunableOp): "
+                        "auto = use this repo's tuned table for the model when present, tune = "
+                        "benchmark every solution once and write the table to --gemm-tuning-out")
+    p.add_argument("--gemm-tuning-out", default=None)
     args = p.parse_args()
     if args.batch is None:
         args.batch = 512 if args.model == "bert_base" else 1024
@@ -65,6 +70,39 @@ def parse():
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
+
+
+def tuned_gemm_table(model):
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "distributedtensorflow_amd",
+                        "tuning", f"tunableop_{model}.csv")
+
+
+def setup_gemm_tuning(args):
+    """Offline GEMM autotuning, like cuDNN's benchmark mode but ahead of time: the table maps
+    each library-GEMM shape of the model to its fastest hipBLASLt solution on MI355X (measured
+    once with --gemm-tuning tune; no tuning ever runs inside the timed steps)."""
+    if args.gemm_tuning == "off" or args.impl != "dtf":
+        return None
+    import torch.cuda.tunable as tun
+    if args.gemm_tuning == "tune":
+        out = args.gemm_tuning_out or tuned_gemm_table(args.model)
+        tun.enable(True)
+        tun.tuning_enable(True)
+        tun.set_max_tuning_duration(20)
+        tun.set_max_tuning_iterations(20)
+        tun.set_filename(out, insert_device_ordinal=False)
+        return out
+    table = tuned_gemm_table(args.model)
+    if not os.path.exists(table):
+        return None
+    tun.enable(True)
+    tun.tuning_enable(False)
+    tun.set_filename(table, insert_device_ordinal=False)
+    if not tun.read_file(table):
+        log(f"gemm tuning table {table} rejected (library versions differ); using defaults")
+        tun.enable(False)
+        return None
+    return table
 
 
 def build_dtf(args, dev):
@@ -203,6 +241,7 @@ def main():
         from distributedtensorflow_amd.parallel import init_process_group_from_env
         init_process_group_from_env("nccl")
     torch.backends.cudnn.benchmark = True
+    gemm_table = setup_gemm_tuning(args)
 
     B, S = args.batch, args.image_size
     g = torch.Generator(device=dev)
@@ -269,6 +308,7 @@ def main():
                        "parallelism": f"dp{world}", "impl": args.impl,
                        "optimizer": "lamb+wd0.01" if args.impl == "dtf" else "torch fused AdamW+wd0.01",
                        "dropout": 0.1, "tflops_per_gpu": round(tps * fpt / world / 1e12, 1),
+                       "gemm_tuning": os.path.basename(gemm_table) if gemm_table else "default",
                        "final_loss": round(final_loss, 4),
                        "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1)},
         }

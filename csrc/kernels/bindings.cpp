@@ -118,6 +118,9 @@ void dtf_attn_fwd(const bf16_t*, const float*, bf16_t*, float*, int, int, int, f
                   uint32_t, hipStream_t);
 void dtf_attn_bwd(const bf16_t*, const float*, const bf16_t*, const bf16_t*, const float*, float*,
                   bf16_t*, int, int, int, float, float, uint32_t, hipStream_t);
+int dtf_pos_type_grad_ws_floats(int, int, int);
+void dtf_pos_type_grad(const bf16_t*, const int64_t*, int, int, int, int, float*, float*, float*,
+                       hipStream_t);
 void dtf_segment_sum(const int64_t*, const int64_t*, const bf16_t*, float*, int, int,
                      hipStream_t);
 void dtf_mlm_xent(const bf16_t*, const int64_t*, const float*, const float*, int, int, float*,
@@ -443,6 +446,13 @@ PYBIND11_MODULE(_dtf_hip, m) {
                  P<const bf16_t>(dout), P<const float>(lse), P<float>(delta), P<bf16_t>(dqkv), B,
                  S_, H, scale, p, seed, S(st));
     check_launch("attn_bwd");
+  });
+  m.def("pos_type_grad_ws_floats", &dtf_pos_type_grad_ws_floats);
+  m.def("pos_type_grad", [](uintptr_t ds, uintptr_t tt, int B, int S_, int H, int NT,
+                            uintptr_t dpos, uintptr_t dtyp, uintptr_t ws, uintptr_t st) {
+    dtf_pos_type_grad(P<const bf16_t>(ds), P<const int64_t>(tt), B, S_, H, NT, P<float>(dpos),
+                      P<float>(dtyp), P<float>(ws), S(st));
+    check_launch("pos_type_grad");
   });
   m.def("segment_sum", [](uintptr_t sorted_ids, uintptr_t perm, uintptr_t src, uintptr_t out,
                           int T, int H, uintptr_t st) {

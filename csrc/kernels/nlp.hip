@@ -1038,6 +1038,90 @@ void dtf_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* out, const
   }
 }
 
+namespace {
+
+// Position- and token-type-embedding gradients of the embedding LayerNorm's output gradient ds
+// [B*S][H] (bf16): dpos[s] = sum_b ds[b*S + s], dtyp[t] = sum of the rows whose type id is t.
+// Level 1: block (s, 512-column chunk), 4 row groups x 64 lanes x 8 columns; the per-position
+// type partials go to ws[s][t][H]; level 2 sums ws over s in a fixed order (deterministic; was a
+// one-hot GEMM with N = 2 plus a bf16 -> fp32 copy and a reduction).
+constexpr int kPosTypeMaxTypes = 4;
+
+__global__ void __launch_bounds__(256)
+pos_type_grad_kernel(const bf16_t* __restrict__ ds, const int64_t* __restrict__ tt, int B, int S,
+                     int H, int NT, float* __restrict__ dpos, float* __restrict__ ws) {
+  __shared__ float red[4][64][9];
+  const int s = blockIdx.x;
+  const int cv = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const bool ok = cv * 8 < H;
+  float ap[8], at[kPosTypeMaxTypes][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    ap[e] = 0.f;
+#pragma unroll
+    for (int t = 0; t < kPosTypeMaxTypes; ++t) at[t][e] = 0.f;
+  }
+  if (ok) {
+    for (int b = rg; b < B; b += 4) {
+      const long r = (long)b * S + s;
+      float f[8];
+      unpack8(reinterpret_cast<const uint4*>(ds + r * H)[cv], f);
+      const int t = tt ? (int)tt[r] : 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ap[e] += f[e];
+#pragma unroll
+      for (int q = 0; q < kPosTypeMaxTypes; ++q)
+        if (q == t) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) at[q][e] += f[e];
+        }
+    }
+  }
+  // fixed-order combine of the 4 row groups: positions, then each type
+#pragma unroll
+  for (int q = -1; q < kPosTypeMaxTypes; ++q) {   // unrolled: at[q] stays in registers
+    if (q >= NT) break;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[rg][threadIdx.x & 63][e] = q < 0 ? ap[e] : at[q < 0 ? 0 : q][e];
+    __syncthreads();
+    if (rg == 0 && ok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = red[0][threadIdx.x][e] + red[1][threadIdx.x][e] + red[2][threadIdx.x][e] +
+                        red[3][threadIdx.x][e];
+        if (q < 0) dpos[(long)s * H + cv * 8 + e] = v;
+        else ws[((long)s * NT + q) * H + cv * 8 + e] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256)
+type_grad_final_kernel(const float* __restrict__ ws, int S, int H, int NT, float* __restrict__ dtyp) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int t = blockIdx.y;
+  if (c >= H) return;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += ws[((long)s * NT + t) * H + c];
+  dtyp[(long)t * H + c] = v;
+}
+
+}  // namespace
+
+int dtf_pos_type_grad_ws_floats(int S, int H, int NT) { return S * NT * H; }
+
+void dtf_pos_type_grad(const bf16_t* ds, const int64_t* tt, int B, int S, int H, int NT,
+                       float* dpos, float* dtyp, float* ws, hipStream_t st) {
+  if (H % 8) throw std::runtime_error("pos_type_grad: H % 8 != 0");
+  if (NT < 1 || NT > kPosTypeMaxTypes) throw std::runtime_error("pos_type_grad: 1..4 token types");
+  hipLaunchKernelGGL(pos_type_grad_kernel, dim3(S, (H / 8 + 63) / 64), dim3(256), 0, st, ds, tt,
+                     B, S, H, NT, dpos, ws);
+  hipLaunchKernelGGL(type_grad_final_kernel, dim3((H + 255) / 256, NT), dim3(256), 0, st, ws, S,
+                     H, NT, dtyp);
+}
+
 void dtf_segment_sum(const int64_t* sorted_ids, const int64_t* perm, const bf16_t* src,
                      float* out, int T, int H, hipStream_t st) {
   if (H % 4) throw std::runtime_error("segment_sum: H % 4 != 0");

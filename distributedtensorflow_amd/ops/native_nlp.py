@@ -154,13 +154,21 @@ class _EmbeddingLayerNorm(torch.autograd.Function):
         _K.segment_sum(sorted_ids.data_ptr(), perm.data_ptr(), ds.data_ptr(), dword.data_ptr(),
                        M, H, _st())
         dpos = torch.zeros(P, H, device=dy.device, dtype=torch.float32)
-        dpos[:S] = ds.view(B, S, H).float().sum(0)
-        if has_tt:
-            onehot = torch.nn.functional.one_hot(tt_c, NT).to(_BF16)
-            dtype_ = (onehot.t() @ ds).float()
+        if NT <= 4 and H % 8 == 0:
+            # position sums over the batch and per-type sums in one pass over ds
+            dtype_ = torch.empty(NT, H, device=dy.device, dtype=torch.float32)
+            ws = torch.empty(_K.pos_type_grad_ws_floats(S, H, NT), device=dy.device,
+                             dtype=torch.float32)
+            _K.pos_type_grad(ds.data_ptr(), tt_c.data_ptr() if has_tt else 0, B, S, H, NT,
+                             dpos.data_ptr(), dtype_.data_ptr(), ws.data_ptr(), _st())
         else:
-            dtype_ = torch.zeros(NT, H, device=dy.device, dtype=torch.float32)
-            dtype_[0] = ds.float().sum(0)
+            dpos[:S] = ds.view(B, S, H).float().sum(0)
+            if has_tt:
+                onehot = torch.nn.functional.one_hot(tt_c, NT).to(_BF16)
+                dtype_ = (onehot.t() @ ds).float()
+            else:
+                dtype_ = torch.zeros(NT, H, device=dy.device, dtype=torch.float32)
+                dtype_[0] = ds.float().sum(0)
         return None, None, dword, dpos, dtype_, dgamma, dbeta, None, None
 
 

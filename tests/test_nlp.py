@@ -160,17 +160,19 @@ def test_fused_layer_norm_gpu(p, H):
 
 
 @pytest.mark.gpu
-def test_embedding_layer_norm_gpu():
+@pytest.mark.parametrize("with_tt,B", [(True, 3), (False, 5)])
+def test_embedding_layer_norm_gpu(with_tt, B):
     torch.manual_seed(0)
-    V, P, T, H, B, S = 500, 128, 2, 768, 3, 128
+    V, P, T, H, S = 500, 128, 2, 768, 128
     word, pos, typ = torch.randn(V, H) * 0.02, torch.randn(P, H) * 0.02, torch.randn(T, H) * 0.02
     gamma, beta = 1 + 0.1 * torch.randn(H), 0.1 * torch.randn(H)
     ids = torch.randint(0, 50, (B, S))          # many repeats -> exercises the segment sum
-    tt = torch.randint(0, 2, (B, S))
+    tt = torch.randint(0, 2, (B, S)) if with_tt else None
     dy = torch.randn(B * S, H)
     leaves = [_leaf(t, torch.float32) for t in (word, pos, typ, gamma, beta)]
     torch.manual_seed(3)
-    y, gr = _grads_of(lambda: ops.embedding_layer_norm(ids.cuda(), tt.cuda(), *leaves, p=0.1),
+    y, gr = _grads_of(lambda: ops.embedding_layer_norm(ids.cuda(), tt.cuda() if with_tt else None,
+                                                       *leaves, p=0.1),
                       leaves, dy.cuda().bfloat16())
     leaves_ = [t.clone().requires_grad_(True) for t in (word, pos, typ, gamma, beta)]
     torch.manual_seed(3)
