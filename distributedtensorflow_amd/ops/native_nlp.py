@@ -21,6 +21,8 @@ from .native import _K, _BF16, _bf16_weight, _direct_grad, _grad_ready, _p, _st
 AD = 64   # attention head dim supported by the MFMA kernels
 # fused LayerNorm -> dense dgrad hand-off of the residual gradient (bias_dropout_add_layer_norm)
 _RESIDUAL_TO_DENSE = os.environ.get("DTF_RESIDUAL_TO_DENSE", "1") == "1"
+if os.environ.get("DTF_ATTN_WIDE"):
+    _K.attn_set_wide(int(os.environ["DTF_ATTN_WIDE"]))
 
 
 def next_seed() -> int:

@@ -202,7 +202,8 @@ def test_bias_gelu_gpu(M, N):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,S,H,p,masked", [(2, 128, 2, 0.0, True), (2, 128, 3, 0.1, True),
-                                            (1, 512, 2, 0.0, False), (1, 64, 1, 0.1, False)])
+                                            (1, 512, 2, 0.0, False), (1, 64, 1, 0.1, False),
+                                            (2, 192, 2, 0.1, True)])
 def test_attention_gpu(B, S, H, p, masked):
     torch.manual_seed(0)
     D = 64
@@ -221,6 +222,33 @@ def test_attention_gpu(B, S, H, p, masked):
                                                    True), [x_], dy.bfloat16().float())
     torch.testing.assert_close(y.cpu(), y_, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(dx.cpu(), dx_, atol=5e-2, rtol=5e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_wide_blocks_bit_identical(p):
+    """8-wave / 128-row attention blocks (fwd and dQ, S % 128 == 0) == the 4-wave / 64-row shape: same
+    per-lane summation order, so forward output and dQKV match bit for bit."""
+    from distributedtensorflow_amd.ops import native
+    torch.manual_seed(0)
+    B, S, H = 3, 256, 2
+    qkv = torch.randn(B * S, 3 * H * 64, device="cuda").bfloat16().requires_grad_(True)
+    mask = torch.zeros(B, S, device="cuda")
+    mask[1, S - 50:] = -10000.0
+    dy = torch.randn(B * S, H * 64, device="cuda").bfloat16()
+    outs = []
+    for wide in (1, 0):
+        native._K.attn_set_wide(wide)
+        try:
+            torch.manual_seed(5)
+            y = ops.attention_qkv(qkv, mask, B, S, H, p, True)
+            (g,) = torch.autograd.grad(y, [qkv], dy)
+            torch.cuda.synchronize()
+        finally:
+            native._K.attn_set_wide(1)
+        outs.append((y, g))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.gpu
