@@ -74,6 +74,8 @@ void dtf_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int,
                      int, int, int, int, int, hipStream_t);
 void dtf_gap_fwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void dtf_gap_bwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
+void dtf_s2d_input(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int,
+                   hipStream_t);
 void dtf_softmax_xent(const float*, const void*, int, int, int, float*, float*, float,
                       hipStream_t);
 void dtf_sgd_momentum(float*, const float*, float*, bf16_t*, long, const float*, float, float,
@@ -276,6 +278,11 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("gap_fwd", [](uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t st) {
     dtf_gap_fwd(P<const bf16_t>(x), P<bf16_t>(y), N, HW, C, S(st));
     check_launch("gap_fwd");
+  });
+  m.def("s2d_input", [](uintptr_t x, uintptr_t xs, int N, int H, int W, int C, int Ho, int Wo,
+                        int s_, int cp, int pad, uintptr_t st) {
+    dtf_s2d_input(P<const bf16_t>(x), P<bf16_t>(xs), N, H, W, C, Ho, Wo, s_, cp, pad, S(st));
+    check_launch("s2d_input");
   });
   m.def("gap_bwd", [](uintptr_t dy, uintptr_t dx, int N, int HW, int C, uintptr_t st) {
     dtf_gap_bwd(P<const bf16_t>(dy), P<bf16_t>(dx), N, HW, C, S(st));

@@ -4,6 +4,8 @@
 // (ResNet-50 3x3/2 pad 1, 7x7 global average).  8 channels (16 B) per lane.
 #include "common.h"
 
+#include <stdexcept>
+
 namespace {
 constexpr int kT = 256;
 
@@ -137,6 +139,48 @@ inline int grid_for(long n) {
   if (g > 4096) g = 4096;
   return (int)(g < 1 ? 1 : g);
 }
+// Space-to-depth input of the strided stem (ops/reference.py space_to_depth_operands), one pass:
+// xs[n, i, j, (a*s + b)*cp + ch] = x[n, s*i + a - pad, s*j + b - pad, ch] (zero outside the image
+// and for ch >= C).  One lane per output pixel; cp*s*s = 16 channels = 32 B per lane.  Replaces
+// torch's zero-fill + padded copy + permute copy (three full passes over the padded image).
+template <int SS, int CP>
+__global__ void __launch_bounds__(kT)
+s2d_input_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ xs, int N, int H, int W,
+                 int C, int Ho, int Wo, int pad) {
+  constexpr int OC = SS * SS * CP;
+  static_assert(OC % 8 == 0, "s2d channels must fill 16-B chunks");
+  const long total = (long)N * Ho * Wo;
+  for (long pix = (long)blockIdx.x * kT + threadIdx.x; pix < total; pix += (long)gridDim.x * kT) {
+    const int j = (int)(pix % Wo);
+    const long t = pix / Wo;
+    const int i = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    bf16_t v[OC];
+#pragma unroll
+    for (int a = 0; a < SS; ++a) {
+      const int h = SS * i + a - pad;
+#pragma unroll
+      for (int b = 0; b < SS; ++b) {
+        const int w = SS * j + b - pad;
+        const bool in = h >= 0 && h < H && w >= 0 && w < W;
+        const bf16_t* src = x + (((long)n * H + (in ? h : 0)) * W + (in ? w : 0)) * C;
+#pragma unroll
+        for (int ch = 0; ch < CP; ++ch) v[(a * SS + b) * CP + ch] = (in && ch < C) ? src[ch] : (bf16_t)0;
+      }
+    }
+    uint4* dst = reinterpret_cast<uint4*>(xs + pix * OC);
+#pragma unroll
+    for (int k = 0; k < OC / 8; ++k) {
+      uint4 u;
+      u.x = (uint32_t)v[8 * k + 0] | ((uint32_t)v[8 * k + 1] << 16);
+      u.y = (uint32_t)v[8 * k + 2] | ((uint32_t)v[8 * k + 3] << 16);
+      u.z = (uint32_t)v[8 * k + 4] | ((uint32_t)v[8 * k + 5] << 16);
+      u.w = (uint32_t)v[8 * k + 6] | ((uint32_t)v[8 * k + 7] << 16);
+      dst[k] = u;
+    }
+  }
+}
+
 }  // namespace
 
 void dtf_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* arg, int N, int H, int W, int C,
@@ -172,4 +216,19 @@ void dtf_gap_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t s
 void dtf_gap_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st) {
   hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(kT), 0, st, dy,
                      dx, N, HW, C);
+}
+
+void dtf_s2d_input(const bf16_t* x, bf16_t* xs, int N, int H, int W, int C, int Ho, int Wo,
+                   int s, int cp, int pad, hipStream_t st) {
+  if (s != 2 || (cp != 2 && cp != 4) || C > cp)
+    throw std::runtime_error("s2d_input: stride 2 with C <= 4 channels only (image stems)");
+  const long total = (long)N * Ho * Wo;
+  long g = (total + kT - 1) / kT;
+  if (g > 65536) g = 65536;
+  if (cp == 4)
+    hipLaunchKernelGGL((s2d_input_kernel<2, 4>), dim3((int)g), dim3(kT), 0, st, x, xs, N, H, W, C,
+                       Ho, Wo, pad);
+  else
+    hipLaunchKernelGGL((s2d_input_kernel<2, 2>), dim3((int)g), dim3(kT), 0, st, x, xs, N, H, W, C,
+                       Ho, Wo, pad);
 }

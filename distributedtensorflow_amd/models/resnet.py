@@ -41,7 +41,12 @@ class StemConvBN(ConvBN):
         if not (ops._use_native(x) and self.conv.strides in (2, (2, 2)) and S2D_STEM):
             return super().forward(x, relu, residual, residual_to_conv, grad_share)
         from ..ops import reference
-        xs, ws = reference.space_to_depth_operands(x, self.conv.kernel, 2, self.conv.padding)
+        xs, ws = reference.space_to_depth_operands(x, self.conv.kernel, 2, self.conv.padding,
+                                                   want_x=x.requires_grad)
+        if xs is None:   # the image: one-pass HIP layout kernel instead of pad + permute copies
+            from ..ops import native
+            kh, kw = self.conv.kernel.shape[1:3]
+            xs = native.space_to_depth_input(x, 2, self.conv.padding, kh, kw)
         y = ops.conv2d(xs, ws, 1, 0, bn_stats=self.bn.training)
         return self.bn(y, relu=relu)
 

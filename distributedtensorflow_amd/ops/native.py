@@ -281,6 +281,23 @@ def conv2d_wgrad(x, dy, w_shape, stride, padding, out=None):
     return dW.reshape(K, R, S, C)
 
 
+def space_to_depth_input(x, stride, pad, R, S):
+    """The x half of ``reference.space_to_depth_operands`` (same layout, bit-identical) in one
+    HIP pass; for an input that needs no gradient (the image)."""
+    n, h, wd, c = x.shape
+    s = stride
+    P = (h + 2 * pad - R) // s + 1
+    Q = (wd + 2 * pad - S) // s + 1
+    Ho, Wo = P + -(-R // s) - 1, Q + -(-S // s) - 1
+    cp = c
+    while (s * s * cp) % 8:
+        cp += 1
+    x = x.contiguous()
+    xs = torch.empty(n, Ho, Wo, s * s * cp, device=x.device, dtype=_BF16)
+    _K.s2d_input(x.data_ptr(), xs.data_ptr(), n, h, wd, c, Ho, Wo, s, cp, pad, _st())
+    return xs
+
+
 def _pad_c8(t):
     """Zero-pad the channel (last) axis to a multiple of 8 so every 16-B load holds whole taps."""
     c = t.shape[-1]

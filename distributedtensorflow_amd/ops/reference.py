@@ -276,7 +276,7 @@ def mlm_loss(logits, labels, weights=None):
     return (w * nll).sum() / w.sum().clamp_min(1e-5)
 
 
-def space_to_depth_operands(x, w, stride, pad):
+def space_to_depth_operands(x, w, stride, pad, want_x=True):
     """Rewrite a strided conv (the ResNet stem: 7x7 / 2, pad 3, C = 3) as a stride-1 VALID conv
     on the space-to-depth input.  Output pixel p reads padded input rows s*p + r, r < R; with
     r = s*i + a that is row p + i of the s2d image at sub-row a, so
@@ -286,7 +286,8 @@ def space_to_depth_operands(x, w, stride, pad):
 
     compute exactly the original conv.  For the stem: 16 taps x 16 channels = K 256 of which
     147 are real (vs 49 taps x 8 padded channels = 392), and whole 32-B tap rows per pixel.
-    Both rewrites are differentiable torch views/pads (w' keeps autograd back to the master)."""
+    Both rewrites are differentiable torch views/pads (w' keeps autograd back to the master).
+    ``want_x=False`` skips x' (returned as None) for callers with a native layout kernel."""
     n, h, wd, c = x.shape
     K, R, S, C = w.shape
     s = stride
@@ -297,9 +298,11 @@ def space_to_depth_operands(x, w, stride, pad):
     while (s * s * cp) % 8:
         cp += 1
     Hn, Wn = s * (P + Rp - 1), s * (Q + Sp - 1)
+    wp = torch.nn.functional.pad(w, (0, cp - C, 0, s * Sp - S, 0, s * Rp - R))
+    ws = wp.view(K, Rp, s, Sp, s, cp).permute(0, 1, 3, 2, 4, 5).reshape(K, Rp, Sp, s * s * cp)
+    if not want_x:
+        return None, ws
     xp = torch.nn.functional.pad(x, (0, cp - c, pad, Wn - wd - pad, pad, Hn - h - pad))
     xs = xp.view(n, Hn // s, s, Wn // s, s, cp).permute(0, 1, 3, 2, 4, 5).reshape(
         n, Hn // s, Wn // s, s * s * cp)
-    wp = torch.nn.functional.pad(w, (0, cp - C, 0, s * Sp - S, 0, s * Rp - R))
-    ws = wp.view(K, Rp, s, Sp, s, cp).permute(0, 1, 3, 2, 4, 5).reshape(K, Rp, Sp, s * s * cp)
     return xs.contiguous(), ws

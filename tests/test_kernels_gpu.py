@@ -290,6 +290,19 @@ def test_bf16_col_sum(T, N):
                                rtol=1e-4)
 
 
+@pytest.mark.parametrize("n,h,w,c", [(2, 224, 224, 3), (3, 33, 31, 3), (1, 20, 18, 1)])
+def test_space_to_depth_input_kernel(n, h, w, c):
+    """One-pass HIP space-to-depth of the stem input == the torch pad + permute rewrite."""
+    from distributedtensorflow_amd.ops import reference as ref
+    nat = _native()
+    x = torch.randn(n, h, w, c, device=dev).to(torch.bfloat16)
+    wt = torch.randn(64, 7, 7, c, device=dev)
+    xs_ref, _ = ref.space_to_depth_operands(x, wt, 2, 3)
+    xs = nat.space_to_depth_input(x, 2, 3, 7, 7)
+    assert xs.shape == xs_ref.shape
+    assert torch.equal(xs, xs_ref)
+
+
 def test_batched_filter_transpose():
     """filter_transpose_kernel: [K,T,C] -> [C,T,K] for a batch of ragged filters (> 48 jobs ->
     two launches), exactly equal to torch's permute."""
