@@ -115,11 +115,14 @@ class BucketedAllReduce:
         self.launched = [False] * len(ranges)
         self._hooks = []
         for i, v in enumerate(order):
-            hook = self._make_hook(i)
-            self._hooks.append(v.register_post_accumulate_grad_hook(hook))
-            # ops that write their gradient straight into the flat buffer (ops/native.py
-            # _direct_grad) raise the same readiness event themselves
-            v._dtf_grad_ready = (lambda h=hook, p=v: h(p))
+            self._hooks.append(v.register_post_accumulate_grad_hook(self._make_hook(i)))
+            # Ops that write their gradient straight into the flat buffer (ops/native.py
+            # _direct_grad) return None for the variable, and autograd still runs the variable's
+            # AccumulateGrad node -- once per backward, after every op that consumes the variable
+            # (tied weights included) -- so the hook above already fires exactly once, after the
+            # direct write.  Counting the ops' own readiness call as well launched buckets early
+            # (caught by tests/test_distributed.py direct_grad_writes), so it is a no-op here.
+            v._dtf_grad_ready = None
 
     def _make_hook(self, i):
         def hook(_p):

@@ -26,6 +26,39 @@ def make_optimizer(name):
     return AdamOptimizer(1e-3) if name == "adam" else MomentumOptimizer(0.05, 0.9)
 
 
+class _DirectDense(torch.autograd.Function):
+    """Dense layer whose backward writes dW / db straight into the optimizer's flat gradient
+    buffer and raises the parameter's readiness event itself -- the contract of the native
+    kernels (ops/native.py _direct_grad / _grad_ready), reproduced on CPU so the bucketed
+    all-reduce's handling of it is covered by gloo runs."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.params = (w, b)
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        grads = [dy.t() @ x, None if ctx.params[1] is None else dy.sum(0)]
+        out = []
+        for p, g in zip(ctx.params, grads):
+            if g is not None and getattr(p, "_dtf_flat", False) and p.grad is not None:
+                p.grad.add_(g)
+                ready = getattr(p, "_dtf_grad_ready", None)
+                if ready is not None:
+                    ready()
+                g = None
+            out.append(g)
+        return (dy @ w, *out)
+
+
+def _direct_dense(x, w, b=None, relu=False):
+    y = _DirectDense.apply(x, w, b)
+    return torch.relu(y) if relu else y
+
+
 def main():
     kind, out = sys.argv[1], sys.argv[2]
     kw = dict(a.split("=", 1) for a in sys.argv[3:])
@@ -48,6 +81,8 @@ def main():
     else:
         raise SystemExit(f"unknown strategy {kind}")
     rank, world = strat.replica_id, strat.num_replicas_in_sync
+    if kw.get("direct", "0") == "1":
+        ops.dense = _direct_dense
     torch.manual_seed(17 + 101 * rank)
     with strat.scope():
         model = MnistCNN()

@@ -78,7 +78,8 @@ def _assert_replicas(results, ref, atol=2e-6, steps=3):
     assert all(r["global_step"] == steps for r in results)
 
 
-@pytest.mark.parametrize("args", [(), ("bucket_mb=0.05",)], ids=["default_buckets", "many_buckets"])
+@pytest.mark.parametrize("args", [(), ("bucket_mb=0.05",), ("bucket_mb=0.05", "direct=1")],
+                         ids=["default_buckets", "many_buckets", "direct_grad_writes"])
 def test_mirrored_two_ranks_matches_single_process(tmp_path, args):
     res = _launch("mirrored", 2, tmp_path, *args)
     _assert_replicas(res, _single_process())
