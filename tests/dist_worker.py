@@ -70,6 +70,8 @@ def main():
                                                     ParameterServerStrategy)
     if kind == "heartbeat":
         return heartbeat_probe(out)
+    if kind == "resnet_gpu":
+        return resnet_gpu_grads(out)
     if kind == "mirrored":
         strat = MirroredStrategy(bucket_mb=float(kw.get("bucket_mb", 64)),
                                  first_bucket_mb=float(kw.get("bucket_mb", 4)),
@@ -101,6 +103,39 @@ def main():
                 "global_step": gstep.value(), "world": world, "mean_loss": mean_loss,
                 "fingerprints": fps},
                os.path.join(out, f"rank{rank}.pt"))
+    strat.barrier()
+
+
+def resnet_batch():
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(4, 64, 64, 3, generator=g, device="cpu").to(torch.bfloat16)
+    return x, torch.randint(0, 1000, (4,), generator=g, device="cpu")
+
+
+def resnet_gpu_grads(out):
+    """Two ranks sharing one GPU over gloo: ResNet-50 gradients through the native kernels
+    (direct flat-buffer writes, lazy residual gradients, bucketed all-reduce).  Saves the
+    all-reduced (summed) gradient buffer and the broadcast initial variables."""
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.models import resnet50
+    from distributedtensorflow_amd.optimizers import MomentumOptimizer
+    from distributedtensorflow_amd.parallel import MirroredStrategy
+    strat = MirroredStrategy(bucket_mb=8, first_bucket_mb=1, backend="gloo")
+    rank = strat.replica_id
+    torch.manual_seed(17 + 101 * rank)
+    with strat.scope():
+        model = resnet50().cuda()
+        opt = MomentumOptimizer(0.1, 0.9)
+        opt.build(list(model.parameters()))
+        init = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+        x, y = resnet_batch()
+        x, y = x[2 * rank:2 * rank + 2].cuda(), y[2 * rank:2 * rank + 2].cuda()
+        loss = ops.sparse_softmax_cross_entropy(model(x), y)
+        opt.compute_gradients(loss, list(model.parameters()))
+        torch.cuda.synchronize()
+        torch.save({"init": init, "grad": opt.space.grad.cpu().clone(),
+                    "order": [n for n, p in model.named_parameters()]},
+                   os.path.join(out, f"rank{rank}.pt"))
     strat.barrier()
 
 
