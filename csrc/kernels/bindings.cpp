@@ -74,6 +74,8 @@ void dtf_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int,
                      int, int, int, int, int, hipStream_t);
 void dtf_gap_fwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void dtf_gap_bwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
+void dtf_bn_relu_maxpool_fwd(const bf16_t*, const float*, const float*, bf16_t*, uint8_t*, int,
+                             int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void dtf_s2d_input(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int,
                    hipStream_t);
 void dtf_softmax_xent(const float*, const void*, int, int, int, float*, float*, float,
@@ -278,6 +280,14 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("gap_fwd", [](uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t st) {
     dtf_gap_fwd(P<const bf16_t>(x), P<bf16_t>(y), N, HW, C, S(st));
     check_launch("gap_fwd");
+  });
+  m.def("bn_relu_maxpool_fwd", [](uintptr_t x, uintptr_t scale, uintptr_t shift, uintptr_t y,
+                                  uintptr_t arg, int N, int H, int W, int C, int P_, int Q,
+                                  int kh, int kw, int sh, int sw, int ph, int pw, uintptr_t st) {
+    dtf_bn_relu_maxpool_fwd(P<const bf16_t>(x), P<const float>(scale), P<const float>(shift),
+                            P<bf16_t>(y), P<uint8_t>(arg), N, H, W, C, P_, Q, kh, kw, sh, sw, ph,
+                            pw, S(st));
+    check_launch("bn_relu_maxpool_fwd");
   });
   m.def("s2d_input", [](uintptr_t x, uintptr_t xs, int N, int H, int W, int C, int Ho, int Wo,
                         int s_, int cp, int pad, uintptr_t st) {

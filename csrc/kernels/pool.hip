@@ -49,6 +49,58 @@ maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
   }
 }
 
+// BatchNorm apply + ReLU + max-pool in one pass (the ResNet stem): the window maximum of
+// bf16(relu(x * scale + shift)) -- exactly the values bn_apply would have written, rounded the
+// same way -- so the 112x112x64 BN output is never stored or re-read.  The BN backward
+// recomputes its ReLU mask from x, and the pool backward needs only `arg`.
+template <typename IT>
+__global__ void __launch_bounds__(kT)
+bn_relu_maxpool_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                           const float* __restrict__ shift, bf16_t* __restrict__ y,
+                           uint8_t* __restrict__ arg, int N, int H, int W, int C, int P, int Q,
+                           int kh, int kw, int sh, int sw, int ph, int pw) {
+  const IT cv = (IT)(C >> 3);
+  const IT total = (IT)N * P * Q * cv;
+  for (IT i = (IT)blockIdx.x * kT + threadIdx.x; i < total; i += (IT)gridDim.x * kT) {
+    const int cg = (int)(i % cv);
+    IT t = i / cv;
+    const int q = (int)(t % (IT)Q); t /= (IT)Q;
+    const int p = (int)(t % (IT)P);
+    const int n = (int)(t / (IT)P);
+    float sc[8], sf[8], best[8];
+    uint8_t bi[8];
+    const float4* S4 = reinterpret_cast<const float4*>(scale + cg * 8);
+    const float4* F4 = reinterpret_cast<const float4*>(shift + cg * 8);
+    const float4 s0 = S4[0], s1 = S4[1], f0 = F4[0], f1 = F4[1];
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+    sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    sf[0] = f0.x; sf[1] = f0.y; sf[2] = f0.z; sf[3] = f0.w;
+    sf[4] = f1.x; sf[5] = f1.y; sf[6] = f1.z; sf[7] = f1.w;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int r = 0; r < kh; ++r) {
+      const int h = p * sh - ph + r;
+      if (h < 0 || h >= H) continue;
+      for (int s = 0; s < kw; ++s) {
+        const int w = q * sw - pw + s;
+        if (w < 0 || w >= W) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * H + h) * W + w) * C + cg * 8), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float o = bf2f(f2bf(fmaxf(__builtin_fmaf(v[j], sc[j], sf[j]), 0.f)));
+          if (o > best[j]) { best[j] = o; bi[j] = (uint8_t)(r * kw + s); }
+        }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+    uint2 a;
+    a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    reinterpret_cast<uint2*>(arg)[i] = a;
+  }
+}
+
 template <typename IT>
 __global__ void __launch_bounds__(kT)
 maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
@@ -231,4 +283,18 @@ void dtf_s2d_input(const bf16_t* x, bf16_t* xs, int N, int H, int W, int C, int 
   else
     hipLaunchKernelGGL((s2d_input_kernel<2, 2>), dim3((int)g), dim3(kT), 0, st, x, xs, N, H, W, C,
                        Ho, Wo, pad);
+}
+
+void dtf_bn_relu_maxpool_fwd(const bf16_t* x, const float* scale, const float* shift, bf16_t* y,
+                             uint8_t* arg, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                             int sh, int sw, int ph, int pw, hipStream_t st) {
+  if (C % 8) throw std::runtime_error("bn_relu_maxpool: C % 8 != 0");
+  if (kh * kw > 255) throw std::runtime_error("bn_relu_maxpool: window too large");
+  const long total = (long)N * P * Q * (C / 8);
+  if (total < 2147483647L && (long)N * H * W * C < 2147483647L)
+    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<uint32_t>, dim3(grid_for(total)), dim3(kT), 0,
+                       st, x, scale, shift, y, arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+  else
+    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<uint64_t>, dim3(grid_for(total)), dim3(kT), 0,
+                       st, x, scale, shift, y, arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
 }

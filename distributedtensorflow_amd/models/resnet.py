@@ -37,9 +37,13 @@ class StemConvBN(ConvBN):
     [7,7,3,64] kernel (checkpoint key conv1_conv/kernel) and its gradient flows back through the
     rewrite."""
 
-    def forward(self, x, relu=True, residual=None, residual_to_conv=False, grad_share=None):
+    def forward(self, x, relu=True, residual=None, residual_to_conv=False, grad_share=None,
+                pool=False):
+        """``pool``: also apply the 3x3/2 max-pool (fused with the BN + ReLU on the native
+        path, so the 112x112x64 BN output is never stored)."""
         if not (ops._use_native(x) and self.conv.strides in (2, (2, 2)) and S2D_STEM):
-            return super().forward(x, relu, residual, residual_to_conv, grad_share)
+            y = super().forward(x, relu, residual, residual_to_conv, grad_share)
+            return ops.max_pool2d(y, 3, 2, 1) if pool else y
         from ..ops import reference
         xs, ws = reference.space_to_depth_operands(x, self.conv.kernel, 2, self.conv.padding,
                                                    want_x=x.requires_grad)
@@ -48,10 +52,17 @@ class StemConvBN(ConvBN):
             kh, kw = self.conv.kernel.shape[1:3]
             xs = native.space_to_depth_input(x, 2, self.conv.padding, kh, kw)
         y = ops.conv2d(xs, ws, 1, 0, bn_stats=self.bn.training)
-        return self.bn(y, relu=relu)
+        if pool and relu and FUSE_STEM_POOL:
+            bn = self.bn
+            return ops.batch_norm_relu_max_pool(y, bn.gamma, bn.beta, bn.moving_mean,
+                                                bn.moving_variance, bn.training, bn.momentum,
+                                                bn.epsilon, 3, 2, 1)
+        y = self.bn(y, relu=relu)
+        return ops.max_pool2d(y, 3, 2, 1) if pool else y
 
 
 S2D_STEM = True
+FUSE_STEM_POOL = True
 
 
 class Bottleneck(nn.Module):
@@ -97,8 +108,7 @@ class ResNet(Layer):
 
     def forward(self, x):
         """x: [N, 224, 224, 3] NHWC (compute dtype) -> logits [N, classes] fp32."""
-        y = self.stem(x)
-        y = ops.max_pool2d(y, 3, 2, 1)
+        y = self.stem(x, pool=True)
         for b in self.blocks:
             y = b(y)
         y = ops.global_avg_pool(y)

@@ -74,6 +74,18 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
                                 momentum, eps, relu, residual)
 
 
+def batch_norm_relu_max_pool(x, gamma, beta, running_mean=None, running_var=None, training=True,
+                             momentum=0.997, eps=1e-5, kernel=3, stride=2, padding=1):
+    """max_pool2d(batch_norm(x, relu=True)): the ResNet stem's BN -> ReLU -> 3x3/2 max-pool.
+    Native path: one fused kernel that never stores the BN output."""
+    if _use_native(x):
+        return _native().batch_norm_relu_max_pool(x, gamma, beta, running_mean, running_var,
+                                                  training, momentum, eps, kernel, stride, padding)
+    y = reference.batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, eps,
+                             True, None)
+    return max_pool2d(y, kernel, stride, padding)
+
+
 def relu(x):
     if _use_native(x):
         return _native().relu(x)

@@ -450,29 +450,10 @@ class _BatchNorm(torch.autograd.Function):
         C = x.shape[-1]
         M = x.numel() // C
         dev = x.device
-        stats = torch.empty(4, C, device=dev, dtype=torch.float32)  # mean, invstd, scale, shift
-        mean, invstd, scale, shift = stats[0], stats[1], stats[2], stats[3]
         st = _st()
-        g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
-        fused = getattr(x, "_dtf_bn_part", None)
-        if training and fused is not None and fused[2:] == (M, C):
-            # statistics already produced by the producing conv's epilogue
-            part, G = fused[0], fused[1]
-            _K.bn_fwd_finalize_g(part.data_ptr(), G, M, C, g32.data_ptr(), b32.data_ptr(),
-                                 _p(running_mean), _p(running_var), float(momentum), float(eps),
-                                 mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
-                                 shift.data_ptr(), st)
-        elif training:
-            part = torch.empty(_K.bn_workspace_floats(M, C), device=dev, dtype=torch.float32)
-            _K.bn_fwd_stats(x.data_ptr(), M, C, part.data_ptr(), st)
-            _K.bn_fwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), b32.data_ptr(),
-                               _p(running_mean), _p(running_var), float(momentum), float(eps),
-                               mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
-                               shift.data_ptr(), st)
-        else:
-            _K.bn_infer_finalize(C, g32.data_ptr(), b32.data_ptr(), running_mean.data_ptr(),
-                                 running_var.data_ptr(), float(eps), mean.data_ptr(),
-                                 invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), st)
+        stats, g32 = _bn_forward_stats(x, gamma, beta, running_mean, running_var, training,
+                                       momentum, eps)
+        scale, shift = stats[2], stats[3]
         res = residual.contiguous() if residual is not None else None
         y = torch.empty_like(x)
         # residual + ReLU: the backward's ReLU mask cannot be recomputed from x alone, so the
@@ -498,62 +479,101 @@ class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, mask, g32, stats = ctx.saved_tensors
-        dy = dy.contiguous()
-        C = x.shape[-1]
-        M = x.numel() // C
-        dev = x.device
-        st = _st()
-        mean, invstd = stats[0], stats[1]
-        # ReLU mask: the forward's bit mask when a residual was added before the ReLU, else
-        # recomputed from x with the forward's scale/shift (neither pass reads y)
-        mask_x = ctx.relu and not ctx.has_res
-        sc_ptr, sh_ptr = (stats[2].data_ptr(), stats[3].data_ptr()) if mask_x else (0, 0)
-        fused = getattr(dy, "_dtf_bnb_part", None)
-        tok = getattr(ctx, "bnb_token", None)
-        if fused is not None and tok is not None and fused[4] is tok and fused[2:4] == (M, C):
-            # sums already produced by the dgrad epilogue of the conv that consumed y
-            part, G = fused[0], fused[1]
-        else:
-            part, G = torch.empty(_K.bn_workspace_floats(M, C), device=dev,
-                                  dtype=torch.float32), None
-            _K.bn_bwd_reduce(dy.data_ptr(), 0, x.data_ptr(), mean.data_ptr(),
-                             invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st,
-                             sc_ptr, sh_ptr, _p(mask))
-        gb = torch.empty(5, C, device=dev, dtype=torch.float32)  # dgamma dbeta A B C
-        tg, tb = (_direct_grad(p) for p in ctx.params)
-        direct = tg is not None and tb is not None
-        dg_ptr, db_ptr = ((tg.data_ptr(), tb.data_ptr()) if direct
-                          else (gb[0].data_ptr(), gb[1].data_ptr()))
-        if G is None:
-            _K.bn_bwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), mean.data_ptr(),
-                               invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
-                               gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
-        else:
-            _K.bn_bwd_finalize_g(part.data_ptr(), G, M, C, g32.data_ptr(), mean.data_ptr(),
-                                 invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
-                                 gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
-        if direct:
-            for p in ctx.params:
-                _grad_ready(p)
-        dx = torch.empty_like(x)
-        lazy = (ctx.has_res and ctx.res_ref is not None and _LAZY_RESIDUAL_GRAD
-                and mask is not None)
-        dres = torch.empty_like(x) if ctx.has_res and not lazy else None
-        _K.bn_bwd_apply(dy.data_ptr(), 0, x.data_ptr(), gb[2].data_ptr(),
-                        gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
-                        int(ctx.relu), st, sc_ptr, sh_ptr, _p(mask))
-        if lazy:
-            # d(residual) = dy * relu_mask is never written: the consuming dgrad forms it in its
-            # epilogue from dy and the bit mask (conv geom acc mode 2)
-            ctx.res_ref._dtf_pending_grad = _MaskedGrad(dy, mask)
-        elif dres is not None and ctx.res_ref is not None:
-            ctx.res_ref._dtf_pending_grad = dres
-            dres = None
-        ctx.res_ref = None
-        if direct:
-            return dx, None, None, None, None, None, None, None, None, dres, None
-        return (dx, gb[0].to(ctx.gdt), gb[1].to(ctx.bdt), None, None, None, None, None, None,
-                dres, None)
+        dx, dg, db, dres = _bn_backward_core(ctx, dy, x, mask, g32, stats)
+        return dx, dg, db, None, None, None, None, None, None, dres, None
+
+
+def _bn_forward_stats(x, gamma, beta, running_mean, running_var, training, momentum, eps):
+    """Per-channel (mean, invstd, scale, shift) as a [4, C] fp32 tensor, from the producing
+    conv's fused partial sums when present, else a statistics pass; plus fp32 gamma."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    dev = x.device
+    stats = torch.empty(4, C, device=dev, dtype=torch.float32)  # mean, invstd, scale, shift
+    mean, invstd, scale, shift = stats[0], stats[1], stats[2], stats[3]
+    st = _st()
+    g32, b32 = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
+    fused = getattr(x, "_dtf_bn_part", None)
+    if training and fused is not None and fused[2:] == (M, C):
+        # statistics already produced by the producing conv's epilogue
+        part, G = fused[0], fused[1]
+        _K.bn_fwd_finalize_g(part.data_ptr(), G, M, C, g32.data_ptr(), b32.data_ptr(),
+                             _p(running_mean), _p(running_var), float(momentum), float(eps),
+                             mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
+                             shift.data_ptr(), st)
+    elif training:
+        part = torch.empty(_K.bn_workspace_floats(M, C), device=dev, dtype=torch.float32)
+        _K.bn_fwd_stats(x.data_ptr(), M, C, part.data_ptr(), st)
+        _K.bn_fwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), b32.data_ptr(),
+                           _p(running_mean), _p(running_var), float(momentum), float(eps),
+                           mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
+                           shift.data_ptr(), st)
+    else:
+        _K.bn_infer_finalize(C, g32.data_ptr(), b32.data_ptr(), running_mean.data_ptr(),
+                             running_var.data_ptr(), float(eps), mean.data_ptr(),
+                             invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), st)
+    return stats, g32
+
+
+def _bn_backward_core(ctx, dy, x, mask, g32, stats):
+    """BatchNorm(+ReLU)(+residual) backward shared by :class:`_BatchNorm` and
+    :class:`_BatchNormReluMaxPool`; returns (dx, dgamma, dbeta, dresidual) (None where the
+    gradient went straight into the flat buffer or to a consuming conv)."""
+    dy = dy.contiguous()
+    C = x.shape[-1]
+    M = x.numel() // C
+    dev = x.device
+    st = _st()
+    mean, invstd = stats[0], stats[1]
+    # ReLU mask: the forward's bit mask when a residual was added before the ReLU, else
+    # recomputed from x with the forward's scale/shift (neither pass reads y)
+    mask_x = ctx.relu and not ctx.has_res
+    sc_ptr, sh_ptr = (stats[2].data_ptr(), stats[3].data_ptr()) if mask_x else (0, 0)
+    fused = getattr(dy, "_dtf_bnb_part", None)
+    tok = getattr(ctx, "bnb_token", None)
+    if fused is not None and tok is not None and fused[4] is tok and fused[2:4] == (M, C):
+        # sums already produced by the dgrad epilogue of the conv that consumed y
+        part, G = fused[0], fused[1]
+    else:
+        part, G = torch.empty(_K.bn_workspace_floats(M, C), device=dev,
+                              dtype=torch.float32), None
+        _K.bn_bwd_reduce(dy.data_ptr(), 0, x.data_ptr(), mean.data_ptr(),
+                         invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st,
+                         sc_ptr, sh_ptr, _p(mask))
+    gb = torch.empty(5, C, device=dev, dtype=torch.float32)  # dgamma dbeta A B C
+    tg, tb = (_direct_grad(p) for p in ctx.params)
+    direct = tg is not None and tb is not None
+    dg_ptr, db_ptr = ((tg.data_ptr(), tb.data_ptr()) if direct
+                      else (gb[0].data_ptr(), gb[1].data_ptr()))
+    if G is None:
+        _K.bn_bwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), mean.data_ptr(),
+                           invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
+                           gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
+    else:
+        _K.bn_bwd_finalize_g(part.data_ptr(), G, M, C, g32.data_ptr(), mean.data_ptr(),
+                             invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
+                             gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
+    if direct:
+        for p in ctx.params:
+            _grad_ready(p)
+    dx = torch.empty_like(x)
+    lazy = (ctx.has_res and ctx.res_ref is not None and _LAZY_RESIDUAL_GRAD
+            and mask is not None)
+    dres = torch.empty_like(x) if ctx.has_res and not lazy else None
+    _K.bn_bwd_apply(dy.data_ptr(), 0, x.data_ptr(), gb[2].data_ptr(),
+                    gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
+                    int(ctx.relu), st, sc_ptr, sh_ptr, _p(mask))
+    if lazy:
+        # d(residual) = dy * relu_mask is never written: the consuming dgrad forms it in its
+        # epilogue from dy and the bit mask (conv geom acc mode 2)
+        ctx.res_ref._dtf_pending_grad = _MaskedGrad(dy, mask)
+    elif dres is not None and ctx.res_ref is not None:
+        ctx.res_ref._dtf_pending_grad = dres
+        dres = None
+    ctx.res_ref = None
+    if direct:
+        return dx, None, None, dres
+    return dx, gb[0].to(ctx.gdt), gb[1].to(ctx.bdt), dres
 
 
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True,
@@ -566,6 +586,57 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
         raise ValueError("residual shape mismatch")
     return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps,
                             relu, residual, residual_to_conv)
+
+
+class _BatchNormReluMaxPool(torch.autograd.Function):
+    """maxpool(relu(BN(x))) without storing the BN output (the ResNet stem: 112x112x64 per
+    image): one kernel computes the window maxima of the rounded BN+ReLU values and the argmax;
+    the backward is the pool's gather into d(BN output), then the usual BN backward (its ReLU
+    mask recomputed from x)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, kernel,
+                stride, padding):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        stats, g32 = _bn_forward_stats(x, gamma, beta, running_mean, running_var, training,
+                                       momentum, eps)
+        kh, kw = _pair(kernel)
+        sh, sw = _pair(stride)
+        pt, pb, pl, pr = resolve_padding(padding, h, w, kh, kw, stride)
+        P = (h + pt + pb - kh) // sh + 1
+        Q = (w + pl + pr - kw) // sw + 1
+        y = torch.empty(n, P, Q, c, device=x.device, dtype=x.dtype)
+        arg = torch.empty(n, P, Q, c, device=x.device, dtype=torch.uint8)
+        _K.bn_relu_maxpool_fwd(x.data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
+                               y.data_ptr(), arg.data_ptr(), n, h, w, c, P, Q, kh, kw, sh, sw,
+                               pt, pl, _st())
+        ctx.save_for_backward(x, g32, stats, arg)
+        ctx.geom = (n, h, w, c, P, Q, kh, kw, sh, sw, pt, pl)
+        ctx.relu, ctx.has_res, ctx.res_ref = True, False, None
+        ctx.gdt, ctx.bdt = gamma.dtype, beta.dtype
+        ctx.params = (gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dp):
+        x, g32, stats, arg = ctx.saved_tensors
+        n, h, w, c, P, Q, kh, kw, sh, sw, pt, pl = ctx.geom
+        dy = torch.empty(n, h, w, c, device=dp.device, dtype=dp.dtype)
+        _K.maxpool_bwd(dp.contiguous().data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, c, P,
+                       Q, kh, kw, sh, sw, pt, pl, _st())
+        dx, dg, db, _ = _bn_backward_core(ctx, dy, x, None, g32, stats)
+        return dx, dg, db, None, None, None, None, None, None, None, None
+
+
+def batch_norm_relu_max_pool(x, gamma, beta, running_mean=None, running_var=None, training=True,
+                             momentum=0.997, eps=1e-5, kernel=3, stride=2, padding=1):
+    _check_cuda_bf16(x)
+    C = x.shape[-1]
+    if C % 8 or C > 2048:
+        raise ValueError(f"native batch_norm: unsupported channel count {C}")
+    return _BatchNormReluMaxPool.apply(x, gamma, beta, running_mean, running_var, training,
+                                       momentum, eps, kernel, stride, padding)
 
 
 # ----------------------------------------------------------------------------- ReLU (standalone)

@@ -160,6 +160,24 @@ def test_lazy_residual_grad_bit_identical(dma):
     assert torch.equal(ga, gb)
 
 
+def test_fused_stem_bn_relu_maxpool_bit_identical():
+    """Stem BN + ReLU + 3x3/2 max-pool in one kernel (BN output never stored) == BN apply then
+    max-pool: same rounded values, same argmax, so loss and every gradient match exactly."""
+    from distributedtensorflow_amd.models import resnet as rn
+    torch.manual_seed(0)
+    base = resnet50().cuda()
+    prev = rn.FUSE_STEM_POOL
+    try:
+        rn.FUSE_STEM_POOL = True
+        la, ga = _grads(copy.deepcopy(base), True)
+        rn.FUSE_STEM_POOL = False
+        lb, gb = _grads(copy.deepcopy(base), True)
+    finally:
+        rn.FUSE_STEM_POOL = prev
+    assert la == lb
+    assert torch.equal(ga, gb)
+
+
 def test_masked_grad_materialize():
     """Fallback of the lazy residual gradient: dy * bit mask, vs torch."""
     torch.manual_seed(0)
