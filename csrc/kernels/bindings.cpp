@@ -76,6 +76,7 @@ void dtf_gap_fwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void dtf_gap_bwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void dtf_bn_relu_maxpool_fwd(const bf16_t*, const float*, const float*, bf16_t*, uint8_t*, int,
                              int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+void dtf_pool_set_blocked(int);
 void dtf_s2d_input(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int,
                    hipStream_t);
 void dtf_softmax_xent(const float*, const void*, int, int, int, float*, float*, float,
@@ -289,6 +290,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
                             pw, S(st));
     check_launch("bn_relu_maxpool_fwd");
   });
+  m.def("pool_set_blocked", &dtf_pool_set_blocked);
   m.def("s2d_input", [](uintptr_t x, uintptr_t xs, int N, int H, int W, int C, int Ho, int Wo,
                         int s_, int cp, int pad, uintptr_t st) {
     dtf_s2d_input(P<const bf16_t>(x), P<bf16_t>(xs), N, H, W, C, Ho, Wo, s_, cp, pad, S(st));

@@ -186,6 +186,67 @@ gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N, in
   }
 }
 
+// 3x3 / stride 2 / pad 1 backward (the ResNet stem pool), blocked: one lane owns a 2x2 block
+// of input pixels x 8 channels, which together read exactly output rows {a, a+1} x cols
+// {b, b+1}; each output (dy, argmax) is loaded once instead of once per input pixel it covers
+// (2.25x on average).  Same accumulation order as maxpool_bwd_kernel (p, then q ascending).
+__global__ void __launch_bounds__(kT)
+maxpool3s2_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                      bf16_t* __restrict__ dx, int N, int H, int W, int C, int P, int Q) {
+  const int cv = C >> 3;
+  const int HB = (H + 1) >> 1, WB = (W + 1) >> 1;
+  const uint32_t total = (uint32_t)N * HB * WB * cv;
+  for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < total; i += gridDim.x * kT) {
+    const int cg = (int)(i % cv);
+    uint32_t t = i / cv;
+    const int b = (int)(t % WB); t /= WB;
+    const int a = (int)(t % HB);
+    const int n = (int)(t / HB);
+    float acc[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+#pragma unroll
+    for (int da = 0; da < 2; ++da) {
+      const int p = a + da;
+      if (p >= P) continue;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const int q = b + db;
+        if (q >= Q) continue;
+        const long o = (((long)n * P + p) * Q + q) * cv + cg;
+        float g[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[o], g);
+        const uint2 am = reinterpret_cast<const uint2*>(arg)[o];
+        const uint32_t aw[2] = {am.x, am.y};
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int r = ii - 2 * da + 1, s = jj - 2 * db + 1;
+            if (r < 0 || r > 2 || s < 0 || s > 2) continue;     // compile-time after unrolling
+            const uint32_t me = (uint32_t)(r * 3 + s);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (((aw[e >> 2] >> ((e & 3) * 8)) & 0xffu) == me) acc[ii * 2 + jj][e] += g[e];
+          }
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int h = 2 * a + ii;
+      if (h >= H) continue;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int w = 2 * b + jj;
+        if (w >= W) continue;
+        reinterpret_cast<uint4*>(dx)[(((long)n * H + h) * W + w) * cv + cg] = pack8(acc[ii * 2 + jj]);
+      }
+    }
+  }
+}
+
 inline int grid_for(long n) {
   long g = (n + kT - 1) / kT;
   if (g > 4096) g = 4096;
@@ -247,11 +308,18 @@ void dtf_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* arg, int N, int H, int
                        arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
 }
 
+static int g_pool_blocked = 1;   // 0: always the generic gather (tests compare both)
+void dtf_pool_set_blocked(int v) { g_pool_blocked = v; }
+
 void dtf_maxpool_bwd(const bf16_t* dy, const uint8_t* arg, bf16_t* dx, int N, int H, int W,
                      int C, int P, int Q, int kh, int kw, int sh, int sw, int ph, int pw,
                      hipStream_t st) {
   const long total = (long)N * H * W * (C / 8);
-  if (total < (1L << 31))
+  if (g_pool_blocked && kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 &&
+      P == (H - 1) / 2 + 1 && Q == (W - 1) / 2 + 1 && total < (1L << 31))
+    hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3(grid_for(total / 4 + 1)), dim3(kT), 0, st, dy,
+                       arg, dx, N, H, W, C, P, Q);
+  else if (total < (1L << 31))
     hipLaunchKernelGGL(maxpool_bwd_kernel<uint32_t>, dim3(grid_for(total)), dim3(kT), 0, st, dy,
                        arg, dx, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
   else

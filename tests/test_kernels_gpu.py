@@ -220,6 +220,28 @@ def test_max_pool(shape, k, s, p):
     assert _rel(xn.grad, xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 112, 112, 64), (3, 15, 13, 16), (1, 7, 8, 8)])
+def test_max_pool_3s2_blocked_backward_bit_identical(shape):
+    """2x2-blocked 3x3/2/pad-1 pool backward == the generic per-pixel gather, bit for bit
+    (ties included: integer-valued inputs make many windows share their maximum)."""
+    torch.manual_seed(4)
+    nat = _native()
+    x = torch.randint(-3, 4, shape, device=dev).to(torch.bfloat16)
+    grads = []
+    for blocked in (1, 0):
+        nat._K.pool_set_blocked(blocked)
+        try:
+            xn = x.clone().requires_grad_(True)
+            y = nat.max_pool2d(xn, 3, 2, 1)
+            torch.manual_seed(5)
+            y.backward(torch.randn_like(y))
+            grads.append(xn.grad.clone())
+        finally:
+            nat._K.pool_set_blocked(1)
+    assert torch.equal(grads[0], grads[1])
+    assert grads[0].abs().sum() > 0
+
+
 def test_global_avg_pool():
     x = torch.randn(8, 7, 7, 2048, device=dev).to(torch.bfloat16)
     nat, ref = _native(), _ref()
