@@ -474,13 +474,38 @@ class _BatchNorm(torch.autograd.Function):
         # identity-shortcut blocks: hand d(residual) to the conv that also reads the residual
         # tensor (it accumulates its dgrad onto it) instead of returning it to autograd
         ctx.res_ref = residual if (residual_to_conv and _FUSE_RESIDUAL_GRAD) else None
+        # projection shortcuts: this BN (no ReLU, no residual) feeds a residual BN as its
+        # residual; that BN leaves d(y) here as (dy, ReLU bit mask) instead of writing it
+        ctx.slot = None
+        if training and not relu and residual is None and _LAZY_RESIDUAL_GRAD:
+            ctx.slot = _GradSlot()
+            y._dtf_grad_slot = ctx.slot
+            ctx.set_materialize_grads(False)
+        ctx.res_slot = (getattr(residual, "_dtf_grad_slot", None)
+                        if residual is not None and not residual_to_conv else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mask, g32, stats = ctx.saved_tensors
-        dx, dg, db, dres = _bn_backward_core(ctx, dy, x, mask, g32, stats)
+        relu = None
+        if dy is None:
+            mg = ctx.slot.grad if ctx.slot is not None else None
+            if mg is None:
+                return (None,) * 11
+            ctx.slot.grad = None
+            # d(y) = dy_res * mask: the reduce / apply kernels apply the bit mask on load
+            dy, mask, relu = mg.dy, mg.mask, True
+        ctx.slot = None
+        dx, dg, db, dres = _bn_backward_core(ctx, dy, x, mask, g32, stats, relu)
         return dx, dg, db, None, None, None, None, None, None, dres, None
+
+
+class _GradSlot:
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
 
 
 def _bn_forward_stats(x, gamma, beta, running_mean, running_var, training, momentum, eps):
@@ -515,7 +540,7 @@ def _bn_forward_stats(x, gamma, beta, running_mean, running_var, training, momen
     return stats, g32
 
 
-def _bn_backward_core(ctx, dy, x, mask, g32, stats):
+def _bn_backward_core(ctx, dy, x, mask, g32, stats, relu=None):
     """BatchNorm(+ReLU)(+residual) backward shared by :class:`_BatchNorm` and
     :class:`_BatchNormReluMaxPool`; returns (dx, dgamma, dbeta, dresidual) (None where the
     gradient went straight into the flat buffer or to a consuming conv)."""
@@ -527,7 +552,8 @@ def _bn_backward_core(ctx, dy, x, mask, g32, stats):
     mean, invstd = stats[0], stats[1]
     # ReLU mask: the forward's bit mask when a residual was added before the ReLU, else
     # recomputed from x with the forward's scale/shift (neither pass reads y)
-    mask_x = ctx.relu and not ctx.has_res
+    relu = ctx.relu if relu is None else relu
+    mask_x = relu and mask is None
     sc_ptr, sh_ptr = (stats[2].data_ptr(), stats[3].data_ptr()) if mask_x else (0, 0)
     fused = getattr(dy, "_dtf_bnb_part", None)
     tok = getattr(ctx, "bnb_token", None)
@@ -538,7 +564,7 @@ def _bn_backward_core(ctx, dy, x, mask, g32, stats):
         part, G = torch.empty(_K.bn_workspace_floats(M, C), device=dev,
                               dtype=torch.float32), None
         _K.bn_bwd_reduce(dy.data_ptr(), 0, x.data_ptr(), mean.data_ptr(),
-                         invstd.data_ptr(), M, C, int(ctx.relu), part.data_ptr(), st,
+                         invstd.data_ptr(), M, C, int(relu), part.data_ptr(), st,
                          sc_ptr, sh_ptr, _p(mask))
     gb = torch.empty(5, C, device=dev, dtype=torch.float32)  # dgamma dbeta A B C
     tg, tb = (_direct_grad(p) for p in ctx.params)
@@ -559,14 +585,21 @@ def _bn_backward_core(ctx, dy, x, mask, g32, stats):
     dx = torch.empty_like(x)
     lazy = (ctx.has_res and ctx.res_ref is not None and _LAZY_RESIDUAL_GRAD
             and mask is not None)
-    dres = torch.empty_like(x) if ctx.has_res and not lazy else None
+    res_slot = getattr(ctx, "res_slot", None)
+    lazy_slot = (ctx.has_res and not lazy and res_slot is not None and _LAZY_RESIDUAL_GRAD
+                 and mask is not None)
+    dres = torch.empty_like(x) if ctx.has_res and not (lazy or lazy_slot) else None
     _K.bn_bwd_apply(dy.data_ptr(), 0, x.data_ptr(), gb[2].data_ptr(),
                     gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
-                    int(ctx.relu), st, sc_ptr, sh_ptr, _p(mask))
+                    int(relu), st, sc_ptr, sh_ptr, _p(mask))
     if lazy:
         # d(residual) = dy * relu_mask is never written: the consuming dgrad forms it in its
         # epilogue from dy and the bit mask (conv geom acc mode 2)
         ctx.res_ref._dtf_pending_grad = _MaskedGrad(dy, mask)
+    elif lazy_slot:
+        # projection shortcut: the shortcut BN's backward reads dy and the mask itself
+        res_slot.grad = _MaskedGrad(dy, mask)
+        ctx.res_slot = None
     elif dres is not None and ctx.res_ref is not None:
         ctx.res_ref._dtf_pending_grad = dres
         dres = None
