@@ -77,6 +77,13 @@ void dtf_gap_bwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void dtf_bn_relu_maxpool_fwd(const bf16_t*, const float*, const float*, bf16_t*, uint8_t*, int,
                              int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void dtf_pool_set_blocked(int);
+int dtf_pool_bn_bwd_blocks(int, int, int, int);
+void dtf_pool_bn_bwd_reduce(const bf16_t*, const uint8_t*, const bf16_t*, const float*,
+                            const float*, const float*, const float*, float*, int, int, int, int,
+                            int, int, hipStream_t);
+void dtf_pool_bn_bwd_apply(const bf16_t*, const uint8_t*, const bf16_t*, const float*,
+                           const float*, const float*, const float*, const float*, bf16_t*, int,
+                           int, int, int, int, int, hipStream_t);
 void dtf_s2d_input(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int,
                    hipStream_t);
 void dtf_softmax_xent(const float*, const void*, int, int, int, float*, float*, float,
@@ -291,6 +298,25 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("bn_relu_maxpool_fwd");
   });
   m.def("pool_set_blocked", &dtf_pool_set_blocked);
+  m.def("pool_bn_bwd_blocks", &dtf_pool_bn_bwd_blocks);
+  m.def("pool_bn_bwd_reduce", [](uintptr_t dy, uintptr_t arg, uintptr_t x, uintptr_t mean,
+                                 uintptr_t invstd, uintptr_t fsc, uintptr_t fsh, uintptr_t part,
+                                 int N, int H, int W, int C, int P_, int Q, uintptr_t st) {
+    dtf_pool_bn_bwd_reduce(P<const bf16_t>(dy), P<const uint8_t>(arg), P<const bf16_t>(x),
+                           P<const float>(mean), P<const float>(invstd), P<const float>(fsc),
+                           P<const float>(fsh), P<float>(part), N, H, W, C, P_, Q, S(st));
+    check_launch("pool_bn_bwd_reduce");
+  });
+  m.def("pool_bn_bwd_apply", [](uintptr_t dy, uintptr_t arg, uintptr_t x, uintptr_t a,
+                                uintptr_t b, uintptr_t c, uintptr_t fsc, uintptr_t fsh,
+                                uintptr_t dx, int N, int H, int W, int C, int P_, int Q,
+                                uintptr_t st) {
+    dtf_pool_bn_bwd_apply(P<const bf16_t>(dy), P<const uint8_t>(arg), P<const bf16_t>(x),
+                          P<const float>(a), P<const float>(b), P<const float>(c),
+                          P<const float>(fsc), P<const float>(fsh), P<bf16_t>(dx), N, H, W, C,
+                          P_, Q, S(st));
+    check_launch("pool_bn_bwd_apply");
+  });
   m.def("s2d_input", [](uintptr_t x, uintptr_t xs, int N, int H, int W, int C, int Ho, int Wo,
                         int s_, int cp, int pad, uintptr_t st) {
     dtf_s2d_input(P<const bf16_t>(x), P<bf16_t>(xs), N, H, W, C, Ho, Wo, s_, cp, pad, S(st));

@@ -247,6 +247,127 @@ maxpool3s2_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__
   }
 }
 
+// Stem backward without the pooled gradient's full-size round trip: the 3x3/2 pool gather of
+// maxpool3s2_bwd_kernel (same 2x2 input blocks, same fp32 order, same bf16 rounding) feeds the
+// BatchNorm backward directly -- the reduce pass (per-channel sum(dz), sum(dz * xhat) into one
+// [2][C] row per block, combined by bn_bwd_finalize_g) and the apply pass (dx = A dz + B x + C)
+// each regather it instead of reading a materialised 112x112x64 d(BN output).  The ReLU mask is
+// recomputed from x with the forward scale / shift.  Requires 256 % (C / 8) == 0 so every lane
+// keeps one channel group across its grid-stride loop.
+DTF_DEV void pool3s2_gather(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, int n,
+                            int a, int b, int cg, int cv, int P, int Q, float (&g)[4][8]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[k][e] = 0.f;
+#pragma unroll
+  for (int da = 0; da < 2; ++da) {
+    const int p = a + da;
+    if (p >= P) continue;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int q = b + db;
+      if (q >= Q) continue;
+      const long o = (((long)n * P + p) * Q + q) * cv + cg;
+      float gv[8];
+      unpack8(reinterpret_cast<const uint4*>(dy)[o], gv);
+      const uint2 am = reinterpret_cast<const uint2*>(arg)[o];
+      const uint32_t aw[2] = {am.x, am.y};
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int r = ii - 2 * da + 1, s = jj - 2 * db + 1;
+          if (r < 0 || r > 2 || s < 0 || s > 2) continue;
+          const uint32_t me = (uint32_t)(r * 3 + s);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (((aw[e >> 2] >> ((e & 3) * 8)) & 0xffu) == me) g[ii * 2 + jj][e] += gv[e];
+        }
+    }
+  }
+  // the unfused path stores d(BN output) as bf16: round exactly like it
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[k][e] = bf2f(f2bf(g[k][e]));
+}
+
+DTF_DEV void load8(const float* __restrict__ p, int cg, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p + cg * 8)[0];
+  const float4 b = reinterpret_cast<const float4*>(p + cg * 8)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+template <bool APPLY>
+__global__ void __launch_bounds__(kT)
+pool3s2_bn_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                      const bf16_t* __restrict__ x, const float* __restrict__ c0,
+                      const float* __restrict__ c1, const float* __restrict__ c2,
+                      const float* __restrict__ fsc, const float* __restrict__ fsh,
+                      bf16_t* __restrict__ dx, float* __restrict__ partial, int N, int H, int W,
+                      int C, int P, int Q) {
+  // REDUCE: c0 = mean, c1 = invstd;  APPLY: c0/c1/c2 = A/B/C coefficients
+  const int cv = C >> 3;
+  const int HB = (H + 1) >> 1, WB = (W + 1) >> 1;
+  const uint32_t total = (uint32_t)N * HB * WB * cv;
+  const int cg = (int)((blockIdx.x * kT + threadIdx.x) % cv);   // fixed: kT % cv == 0
+  float k0[8], k1[8], k2[8], ksc[8], ksh[8], a0[8], a1[8];
+  load8(c0, cg, k0);
+  load8(c1, cg, k1);
+  if (APPLY) load8(c2, cg, k2);
+  load8(fsc, cg, ksc);
+  load8(fsh, cg, ksh);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { a0[e] = 0.f; a1[e] = 0.f; }
+  for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < total; i += gridDim.x * kT) {
+    uint32_t t = i / cv;
+    const int b = (int)(t % WB); t /= WB;
+    const int a = (int)(t % HB);
+    const int n = (int)(t / HB);
+    float g[4][8];
+    pool3s2_gather(dy, arg, n, a, b, cg, cv, P, Q, g);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int h = 2 * a + ii;
+      if (h >= H) continue;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int w = 2 * b + jj;
+        if (w >= W) continue;
+        const long v = (((long)n * H + h) * W + w) * cv + cg;
+        float xv[8];
+        unpack8(reinterpret_cast<const uint4*>(x)[v], xv);
+        float* gk = g[ii * 2 + jj];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gk[e] = __builtin_fmaf(xv[e], ksc[e], ksh[e]) > 0.f ? gk[e] : 0.f;
+        if (APPLY) {
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = k0[e] * gk[e] + k1[e] * xv[e] + k2[e];
+          reinterpret_cast<uint4*>(dx)[v] = pack8(o);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { a0[e] += gk[e]; a1[e] += gk[e] * (xv[e] - k0[e]) * k1[e]; }
+        }
+      }
+    }
+  }
+  if (!APPLY) {
+    __shared__ float red[kT][17];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[threadIdx.x][e] = a0[e]; red[threadIdx.x][8 + e] = a1[e]; }
+    __syncthreads();
+    // channel c = cg*8 + e, quantity q: fixed-order sum over the lanes of channel group cg
+    for (int idx = threadIdx.x; idx < 2 * C; idx += kT) {
+      const int q = idx / C, c = idx % C, g8 = c >> 3, e = c & 7;
+      float sacc = 0.f;
+      for (int l = g8; l < kT; l += cv) sacc += red[l][q * 8 + e];
+      partial[((long)blockIdx.x * 2 + q) * C + c] = sacc;
+    }
+  }
+}
+
 inline int grid_for(long n) {
   long g = (n + kT - 1) / kT;
   if (g > 4096) g = 4096;
@@ -365,4 +486,36 @@ void dtf_bn_relu_maxpool_fwd(const bf16_t* x, const float* scale, const float* s
   else
     hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<uint64_t>, dim3(grid_for(total)), dim3(kT), 0,
                        st, x, scale, shift, y, arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
+}
+
+int dtf_pool_bn_bwd_blocks(int N, int H, int W, int C) {
+  const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  long g = (total + kT - 1) / kT;
+  if (g > 1024) g = 1024;
+  return (int)(g < 1 ? 1 : g);
+}
+
+static void pool_bn_check(int H, int W, int C, int P, int Q) {
+  if (C % 8 || kT % (C / 8) || P != (H - 1) / 2 + 1 || Q != (W - 1) / 2 + 1 ||
+      (long)H * W * C >= 2147483647L)
+    throw std::runtime_error("pool3s2_bn_bwd: unsupported shape");
+}
+
+void dtf_pool_bn_bwd_reduce(const bf16_t* dy, const uint8_t* arg, const bf16_t* x,
+                            const float* mean, const float* invstd, const float* fsc,
+                            const float* fsh, float* partial, int N, int H, int W, int C, int P,
+                            int Q, hipStream_t st) {
+  pool_bn_check(H, W, C, P, Q);
+  hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<false>, dim3(dtf_pool_bn_bwd_blocks(N, H, W, C)),
+                     dim3(kT), 0, st, dy, arg, x, mean, invstd, nullptr, fsc, fsh, nullptr,
+                     partial, N, H, W, C, P, Q);
+}
+
+void dtf_pool_bn_bwd_apply(const bf16_t* dy, const uint8_t* arg, const bf16_t* x, const float* cA,
+                           const float* cB, const float* cC, const float* fsc, const float* fsh,
+                           bf16_t* dx, int N, int H, int W, int C, int P, int Q, hipStream_t st) {
+  pool_bn_check(H, W, C, P, Q);
+  const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<true>, dim3(grid_for(total)), dim3(kT), 0, st, dy, arg,
+                     x, cA, cB, cC, fsc, fsh, dx, nullptr, N, H, W, C, P, Q);
 }

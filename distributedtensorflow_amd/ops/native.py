@@ -424,6 +424,8 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
 
 _FUSE_RESIDUAL_GRAD = os.environ.get("DTF_FUSE_RESIDUAL_GRAD", "1") == "1"
 _LAZY_RESIDUAL_GRAD = os.environ.get("DTF_LAZY_RESIDUAL_GRAD", "1") == "1"
+# stem backward: pool gather fused into both BatchNorm backward passes (_BatchNormReluMaxPool)
+_FUSE_STEM_POOL_BWD = os.environ.get("DTF_FUSE_STEM_POOL_BWD", "1") == "1"
 
 
 class _MaskedGrad:
@@ -540,6 +542,31 @@ def _bn_forward_stats(x, gamma, beta, running_mean, running_var, training, momen
     return stats, g32
 
 
+def _bn_bwd_finalize(ctx, part, G, M, C, g32, stats):
+    """Combine the backward partial sums -> dgamma / dbeta (straight into the flat gradient
+    buffer when it exposes one) and the dx = A dz + B x + C coefficients; returns (gb, direct)
+    with gb = [dgamma, dbeta, A, B, C]."""
+    st = _st()
+    mean, invstd = stats[0], stats[1]
+    gb = torch.empty(5, C, device=g32.device, dtype=torch.float32)
+    tg, tb = (_direct_grad(p) for p in ctx.params)
+    direct = tg is not None and tb is not None
+    dg_ptr, db_ptr = ((tg.data_ptr(), tb.data_ptr()) if direct
+                      else (gb[0].data_ptr(), gb[1].data_ptr()))
+    if G is None:
+        _K.bn_bwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), mean.data_ptr(),
+                           invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
+                           gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
+    else:
+        _K.bn_bwd_finalize_g(part.data_ptr(), G, M, C, g32.data_ptr(), mean.data_ptr(),
+                             invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
+                             gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
+    if direct:
+        for p in ctx.params:
+            _grad_ready(p)
+    return gb, direct
+
+
 def _bn_backward_core(ctx, dy, x, mask, g32, stats, relu=None):
     """BatchNorm(+ReLU)(+residual) backward shared by :class:`_BatchNorm` and
     :class:`_BatchNormReluMaxPool`; returns (dx, dgamma, dbeta, dresidual) (None where the
@@ -566,22 +593,7 @@ def _bn_backward_core(ctx, dy, x, mask, g32, stats, relu=None):
         _K.bn_bwd_reduce(dy.data_ptr(), 0, x.data_ptr(), mean.data_ptr(),
                          invstd.data_ptr(), M, C, int(relu), part.data_ptr(), st,
                          sc_ptr, sh_ptr, _p(mask))
-    gb = torch.empty(5, C, device=dev, dtype=torch.float32)  # dgamma dbeta A B C
-    tg, tb = (_direct_grad(p) for p in ctx.params)
-    direct = tg is not None and tb is not None
-    dg_ptr, db_ptr = ((tg.data_ptr(), tb.data_ptr()) if direct
-                      else (gb[0].data_ptr(), gb[1].data_ptr()))
-    if G is None:
-        _K.bn_bwd_finalize(part.data_ptr(), M, C, g32.data_ptr(), mean.data_ptr(),
-                           invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
-                           gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
-    else:
-        _K.bn_bwd_finalize_g(part.data_ptr(), G, M, C, g32.data_ptr(), mean.data_ptr(),
-                             invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
-                             gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
-    if direct:
-        for p in ctx.params:
-            _grad_ready(p)
+    gb, direct = _bn_bwd_finalize(ctx, part, G, M, C, g32, stats)
     dx = torch.empty_like(x)
     lazy = (ctx.has_res and ctx.res_ref is not None and _LAZY_RESIDUAL_GRAD
             and mask is not None)
@@ -655,6 +667,24 @@ class _BatchNormReluMaxPool(torch.autograd.Function):
     def backward(ctx, dp):
         x, g32, stats, arg = ctx.saved_tensors
         n, h, w, c, P, Q, kh, kw, sh, sw, pt, pl = ctx.geom
+        if (_FUSE_STEM_POOL_BWD and (kh, kw, sh, sw, pt, pl) == (3, 3, 2, 2, 1, 1)
+                and 256 % (c // 8) == 0):
+            # the pool gather feeds both BN backward passes; d(BN output) is never stored
+            dp = dp.contiguous()
+            M, st = n * h * w, _st()
+            G = _K.pool_bn_bwd_blocks(n, h, w, c)
+            part = torch.empty(_K.bn_workspace_floats_g(G, c), device=x.device,
+                               dtype=torch.float32)
+            _K.pool_bn_bwd_reduce(dp.data_ptr(), arg.data_ptr(), x.data_ptr(),
+                                  stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(),
+                                  stats[3].data_ptr(), part.data_ptr(), n, h, w, c, P, Q, st)
+            gb, direct = _bn_bwd_finalize(ctx, part, G, M, c, g32, stats)
+            dx = torch.empty_like(x)
+            _K.pool_bn_bwd_apply(dp.data_ptr(), arg.data_ptr(), x.data_ptr(), gb[2].data_ptr(),
+                                 gb[3].data_ptr(), gb[4].data_ptr(), stats[2].data_ptr(),
+                                 stats[3].data_ptr(), dx.data_ptr(), n, h, w, c, P, Q, st)
+            dg, db = (None, None) if direct else (gb[0].to(ctx.gdt), gb[1].to(ctx.bdt))
+            return dx, dg, db, None, None, None, None, None, None, None, None
         dy = torch.empty(n, h, w, c, device=dp.device, dtype=dp.dtype)
         _K.maxpool_bwd(dp.contiguous().data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, c, P,
                        Q, kh, kw, sh, sw, pt, pl, _st())
