@@ -117,7 +117,7 @@ def build_dtf(args, dev):
 
     if args.strategy == "ps":
         from distributedtensorflow_amd.parallel import ParameterServerStrategy
-        strategy = ParameterServerStrategy(num_ps=args.num_ps)
+        strategy = ParameterServerStrategy(num_ps=args.num_ps, bucket_mb=args.bucket_mb)
     else:
         strategy = MirroredStrategy(bucket_mb=args.bucket_mb)
     with strategy.scope():
@@ -137,6 +137,7 @@ def build_dtf(args, dev):
         opt.minimize(loss, global_step=gstep)
         return loss
 
+    step.optimizer = opt
     return step, strategy
 
 
@@ -162,6 +163,7 @@ def build_bert(args, dev):
         opt.minimize(loss, global_step=gstep)
         return loss
 
+    step.optimizer = opt
     return step, strategy
 
 
@@ -245,6 +247,15 @@ def main():
         init_process_group_from_env("nccl")
     torch.backends.cudnn.benchmark = True
     gemm_table = setup_gemm_tuning(args)
+    native_info = {"backend": "torch (stock comparator)", "native_ext": None}
+    if args.impl == "dtf":
+        from distributedtensorflow_amd import ops
+        from distributedtensorflow_amd.ops import native
+        if ops.get_backend() == "reference":
+            raise SystemExit("bench.py --impl dtf refuses DTF_OPS_BACKEND=reference: the "
+                             "measured step must run this framework's HIP kernels")
+        native_info = {"backend": ops.get_backend(),
+                       "native_ext": os.path.relpath(native.extension_path(), ROOT)}
 
     B, S = args.batch, args.image_size
     g = torch.Generator(device=dev)
@@ -254,6 +265,7 @@ def main():
         if args.lr == 0.1 and "--lr" not in sys.argv:
             args.lr = 1e-3
         bert_step, _ = (build_bert if args.impl == "dtf" else build_torch_bert)(args, dev)
+        opt_for_stats = getattr(bert_step, "optimizer", None)
         d = next(iter(SyntheticMLM(B, args.seq_len, max_predictions=args.max_predictions,
                                    device=dev, seed=1234 + rank)))
         batch = (d["input_ids"], d["segment_ids"], d["input_mask"], d["masked_lm_positions"],
@@ -264,8 +276,10 @@ def main():
         images = labels = None
     elif args.impl == "dtf":
         step, _ = build_dtf(args, dev)
+        opt_for_stats = step.optimizer
         images = torch.randn(B, S, S, 3, device=dev, generator=g).to(torch.bfloat16)  # NHWC
     else:
+        opt_for_stats = None
         step, _ = build_torch(args, dev)
         images = torch.randn(B, 3, S, S, device=dev, generator=g).contiguous(
             memory_format=torch.channels_last)
@@ -283,12 +297,19 @@ def main():
     sync()
     log(f"warmup {args.warmup} steps in {time.time() - t0:.1f}s, loss={float(loss):.4f}")
 
+    comm = getattr(getattr(opt_for_stats, "_reducer", None), "stats", None)
+    if comm is not None:
+        comm.reset_timing()
+        comm.timing = True
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(images, labels)
     sync()
     elapsed = time.perf_counter() - t0
+    # exposed communication: compute-stream wait for RCCL after backward (0 buckets at N=1)
+    comm_info = comm.as_dict() if comm is not None else {"buckets": 0,
+                                                         "exposed_ms_per_step": 0.0}
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -313,7 +334,8 @@ def main():
                        "dropout": 0.1, "tflops_per_gpu": round(tps * fpt / world / 1e12, 1),
                        "gemm_tuning": os.path.basename(gemm_table) if gemm_table else "default",
                        "final_loss": round(final_loss, 4),
-                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1)},
+                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+                       "comm": comm_info, **native_info},
         }
         print(json.dumps(rec), flush=True)
     elif rank == 0:
@@ -330,7 +352,8 @@ def main():
                                        f"ps{min(args.num_ps, world)}+dp{world}"),
                        "impl": args.impl, "optimizer": "momentum0.9+wd1e-4, lr 0.1*B/256 warmup500+cosine",
                        "final_loss": round(final_loss, 4),
-                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1)},
+                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+                       "comm": comm_info, **native_info},
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -139,6 +139,51 @@ void dtf_segment_sum(const int64_t*, const int64_t*, const bf16_t*, float*, int,
 void dtf_mlm_xent(const bf16_t*, const int64_t*, const float*, const float*, int, int, float*,
                   bf16_t*, hipStream_t);
 
+// ---- HIP IPC buffers (ipc.cpp) handed to torch as DLPack capsules
+uintptr_t dtf_ipc_alloc(size_t, int);
+std::string dtf_ipc_handle(uintptr_t, int);
+uintptr_t dtf_ipc_open(const std::string&, int);
+void dtf_ipc_close(uintptr_t, int);
+void dtf_ipc_free(uintptr_t, int);
+
+namespace dlp {   // DLPack ABI (v0.8 DLManagedTensor, "dltensor" capsule)
+struct Device { int32_t device_type; int32_t device_id; };
+struct DataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct Tensor { void* data; Device device; int32_t ndim; DataType dtype; int64_t* shape;
+                int64_t* strides; uint64_t byte_offset; };
+struct Managed { Tensor t; void* ctx; void (*deleter)(Managed*); };
+constexpr int32_t kROCM = 10;
+struct Ctx { int64_t shape[1]; int64_t strides[1]; uintptr_t ptr; int device; bool opened; };
+void deleter(Managed* m) {
+  auto* c = static_cast<Ctx*>(m->ctx);
+  if (c->opened) dtf_ipc_close(c->ptr, c->device);
+  else dtf_ipc_free(c->ptr, c->device);
+  delete c;
+  delete m;
+}
+void capsule_destructor(PyObject* cap) {   // capsule dropped without being consumed by torch
+  if (PyCapsule_IsValid(cap, "dltensor")) {
+    auto* m = static_cast<Managed*>(PyCapsule_GetPointer(cap, "dltensor"));
+    if (m && m->deleter) m->deleter(m);
+  }
+}
+// 1-D float32 (or uint8 when dtype_bits == 8) view of an IPC buffer as a DLPack capsule
+py::capsule make(uintptr_t ptr, int64_t numel, int device, bool opened, int dtype_bits) {
+  auto* c = new Ctx{{numel}, {1}, ptr, device, opened};
+  auto* m = new Managed{};
+  m->t.data = reinterpret_cast<void*>(ptr);
+  m->t.device = {kROCM, device};
+  m->t.ndim = 1;
+  m->t.dtype = dtype_bits == 8 ? DataType{1, 8, 1} : DataType{2, 32, 1};
+  m->t.shape = c->shape;
+  m->t.strides = c->strides;
+  m->t.byte_offset = 0;
+  m->ctx = c;
+  m->deleter = deleter;
+  return py::reinterpret_steal<py::capsule>(PyCapsule_New(m, "dltensor", capsule_destructor));
+}
+}  // namespace dlp
+
 template <typename T>
 static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
 static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -160,6 +205,18 @@ static TT make_taps(const std::vector<int>& dh, const std::vector<int>& dw) {
 
 PYBIND11_MODULE(_dtf_hip, m) {
   m.doc() = "distributedtensorflow_amd HIP/CDNA4 kernels (gfx950)";
+
+  // parameter-server data plane: exported / mapped HBM buffers (ipc.cpp)
+  m.def("ipc_alloc", [](int64_t numel, int device, int dtype_bits) {
+    const size_t bytes = (size_t)numel * (dtype_bits == 8 ? 1 : 4);
+    uintptr_t p = dtf_ipc_alloc(bytes, device);
+    py::bytes h(dtf_ipc_handle(p, device));
+    return py::make_tuple(dlp::make(p, numel, device, false, dtype_bits), h);
+  }, py::arg("numel"), py::arg("device"), py::arg("dtype_bits") = 32);
+  m.def("ipc_open", [](py::bytes handle, int64_t numel, int device, int dtype_bits) {
+    uintptr_t p = dtf_ipc_open(std::string(handle), device);
+    return dlp::make(p, numel, device, true, dtype_bits);
+  }, py::arg("handle"), py::arg("numel"), py::arg("device"), py::arg("dtype_bits") = 32);
 
   m.def("bn_partial_blocks", &dtf_bn_partial_blocks);
   m.def("bn_workspace_floats", &dtf_bn_workspace_floats);

@@ -9,6 +9,7 @@
 #include "crc32c.h"
 #include "data.h"
 #include "records.h"
+#include "shm_ctl.h"
 
 namespace py = pybind11;
 using namespace dtf;
@@ -166,4 +167,47 @@ PYBIND11_MODULE(_dtf_native, m) {
       })
       .def("epoch", &BatchPrefetcher::epoch)
       .def("stop", &BatchPrefetcher::stop);
+
+  // parameter-server data-plane control block (shm_ctl.h); every wait releases the GIL
+  py::class_<ShmControl>(m, "ShmControl")
+      .def(py::init<const std::string&, bool, int>(), py::arg("name"), py::arg("create"),
+           py::arg("n_workers") = 0)
+      .def_property_readonly("n_workers", &ShmControl::n_workers)
+      .def_property_readonly("name", &ShmControl::name)
+      .def("post", [](ShmControl& c, int w, int64_t step) {
+        py::gil_scoped_release nogil;
+        c.post(w, step);
+      })
+      .def("wait_done", [](ShmControl& c, int w, int64_t timeout_ms) -> py::object {
+        int64_t reply = 0;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = c.wait_done(w, timeout_ms, &reply);
+        }
+        if (!ok) return py::none();
+        return py::int_(reply);
+      }, py::arg("worker"), py::arg("timeout_ms") = -1)
+      .def("wait_any", [](ShmControl& c, int64_t timeout_ms) -> py::object {
+        std::vector<int> ws(c.n_workers());
+        std::vector<int64_t> steps(c.n_workers());
+        int n;
+        {
+          py::gil_scoped_release nogil;
+          n = c.wait_any(timeout_ms, ws.data(), steps.data(), (int)ws.size());
+        }
+        if (n < 0) return py::none();
+        py::list out;
+        for (int i = 0; i < n; ++i) out.append(py::make_tuple(ws[i], steps[i]));
+        return out;
+      }, py::arg("timeout_ms") = -1)
+      .def("done", &ShmControl::done)
+      .def("stop", &ShmControl::stop)
+      .def("unlink", &ShmControl::unlink)
+      .def_property_readonly("stopped", &ShmControl::stopped)
+      .def_property("global_step", &ShmControl::global_step, &ShmControl::set_global_step)
+      .def("beat", &ShmControl::beat)
+      .def_property_readonly("heartbeat", &ShmControl::heartbeat)
+      .def("posts", &ShmControl::posts)
+      .def("state", &ShmControl::state);
 }

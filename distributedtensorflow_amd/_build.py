@@ -103,7 +103,7 @@ def build_native(verbose=False):
     os.makedirs(LIBDIR, exist_ok=True)
     if not (os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key):
         inc = ["-I" + src_dir] + ["-I" + p for p in _py_includes()]
-        _run(["g++"] + flags + inc + srcs + ["-o", out])
+        _run(["g++"] + flags + inc + srcs + ["-o", out, "-lrt"])
         with open(stamp, "w") as f:
             f.write(key)
     if verbose:

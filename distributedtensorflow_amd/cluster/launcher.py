@@ -52,8 +52,10 @@ def launch_local(script, num_ps=1, num_workers=2, workdir=None, extra_args=(), e
     for job, n in (("ps", num_ps), ("worker", num_workers)):
         for i in range(n):
             e = dict(base_env)
-            if job == "ps":
-                e["HIP_VISIBLE_DEVICES"] = e.get("DTF_PS_VISIBLE_DEVICES", "")
+            if job == "ps" and "DTF_PS_VISIBLE_DEVICES" in e:
+                # e.g. "" = a host-memory PS as in the reference (ps_device="/job:ps/cpu:0");
+                # by default the PS task keeps the GPU that will hold its HBM-resident shard
+                e["HIP_VISIBLE_DEVICES"] = e["DTF_PS_VISIBLE_DEVICES"]
             elif gpus_per_host:
                 e["LOCAL_RANK"] = str(i % gpus_per_host)
             log = open(os.path.join(workdir, f"{job}{i}.log"), "w")

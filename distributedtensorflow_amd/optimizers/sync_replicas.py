@@ -4,8 +4,9 @@ Wraps an optimizer; under a between-graph :class:`ParameterServerStrategy` it sw
 shards to synchronous aggregation: per global step the PS averages the first
 ``replicas_to_aggregate`` gradients computed at that step (``total_num_replicas`` may be larger:
 backup workers), drops stale ones, applies once and releases the workers (the token queue).
-Under Mirrored/MultiWorkerMirrored strategies training is already synchronous, so it simply
-delegates.  The queue-runner / init-token API of TF1 is provided as no-ops for drop-in use.
+Under Mirrored/MultiWorkerMirrored (and the colocated PS) training is already synchronous over
+every replica, so it delegates -- and raises if asked for backup workers
+(``replicas_to_aggregate < replicas``), which only the arrival-order between-graph PS provides.  The queue-runner / init-token API of TF1 is provided as no-ops for drop-in use.
 """
 from __future__ import annotations
 
@@ -32,6 +33,16 @@ class SyncReplicasOptimizer:
         if getattr(strat, "mode", None) == "between_graph":
             strat.sync = True
             strat.replicas_to_aggregate = self.replicas_to_aggregate
+        elif strat.num_replicas_in_sync > 1 and \
+                self.replicas_to_aggregate < strat.num_replicas_in_sync:
+            # collective strategies (RCCL all-reduce / reduce-to-owner) need EVERY replica's
+            # gradient each step: "first N of M" backup-worker aggregation only exists on the
+            # between-graph PS, whose owners take gradients in arrival order
+            raise ValueError(
+                f"replicas_to_aggregate={self.replicas_to_aggregate} < "
+                f"{strat.num_replicas_in_sync} replicas: backup workers need the between-graph "
+                f"ParameterServerStrategy (Server with ps tasks); {type(strat).__name__} "
+                f"aggregates every replica each step")
         self.local_step_init_op = _NoOp()
         self.chief_init_op = _NoOp()
         self.ready_for_local_init_op = _NoOp()

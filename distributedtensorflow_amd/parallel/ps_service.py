@@ -15,11 +15,13 @@ Reference behaviour being reproduced:
   * variables are sharded over PS tasks: round-robin by variable (TF parity) or greedy
     byte-balanced (default; SURVEY §2.5 notes round-robin puts 99.97 % of the CNN on ps0).
 
-Transport: torch.distributed point-to-point on the ``gloo`` world (any-source receives are what
-an arrival-order PS needs; RCCL has none).  This is the control plane AND the data plane of the
-between-graph mode; the GPU data-parallel strategies (MirroredStrategy, colocated
-ParameterServerStrategy) use RCCL collectives instead.  PS shards live in host memory as in the
-reference (``ps_device="/job:ps/cpu:0"``), optionally on the PS task's GPU.
+Transport.  CONTROL plane: torch.distributed point-to-point on the ``gloo`` world (registration,
+checkpoint state, stop/shutdown; any-source receives).  DATA plane (``ps_device.py``, default on
+one node): the shard lives in the PS task's HBM (or a /dev/shm file for CPU tasks), workers map it
+with hipIpc, write gradients into per-worker mailbox slots and read variables back with device
+copies; a futex-signalled shared-memory control block replaces the per-step messages.  The
+round-1 host path (every tensor ``.cpu()``-ed through gloo) remains as ``data_plane="gloo"``
+for clusters that span hosts.
 
 Clean shutdown (the reference's TODO, ``README.md:7``): workers send STOP when done; ``join()``
 returns when every worker stopped, on SIGINT/SIGTERM, or on the chief's SHUTDOWN.
@@ -80,6 +82,19 @@ def assign_shards(sizes, num_ps, policy="balanced"):
         owner[i] = k
         load[k] += sizes[i]
     return owner
+
+
+def choose_plane(requested, ps_device):
+    """Data plane of a PS shard: ``ipc`` (HBM shard, hipIpc-mapped by GPU workers) when the PS
+    task has a GPU, ``shm`` (/dev/shm shard) for a CPU PS on the workers' host, ``gloo`` (host
+    tensors over TCP, cross-host clusters) when asked for."""
+    requested = requested or "gloo"
+    if requested == "gloo":
+        return "gloo"
+    dev = torch.device(ps_device)
+    if requested in ("auto", "ipc") and dev.type == "cuda":
+        return "ipc"
+    return "shm"
 
 
 # ----------------------------------------------------------------------------- PS side
@@ -152,6 +167,7 @@ class ParameterServerService:
         self._sync_waiters = []
         self._shutdown = False
         self.stats = {"applied": 0, "dropped_stale": 0, "pulls": 0}
+        self.plane = "gloo"
 
     def _install_signal_handlers(self):
         def handler(signum, frame):
@@ -170,13 +186,33 @@ class ParameterServerService:
         self._error = None
         t = threading.Thread(target=self._loop, name="dtf-ps-service", daemon=True)
         t.start()
-        while t.is_alive() and not self._shutdown:
-            t.join(timeout=0.2)
-        if self._error is not None:
-            raise self._error
-        self.stats["global_step"] = self.global_step
+        try:
+            while t.is_alive() and not self._shutdown:
+                t.join(timeout=0.2)
+                dev_err = getattr(self.shard, "_error", None)
+                if dev_err is not None:
+                    raise dev_err
+            if self._error is not None:
+                raise self._error
+        finally:
+            if self.plane != "gloo" and self.shard is not None:
+                self.stats.update({k: v for k, v in self.shard.stats.items()})
+                self.shard.stop()
+        self.stats["global_step"] = self._gstep()
+        self.stats["data_plane"] = self.plane
         self.stats["interrupted"] = t.is_alive()
         return self.stats
+
+    def _gstep(self):
+        return self.shard.global_step if self.plane != "gloo" and self.shard is not None \
+            else self.global_step
+
+    def _ready_reply(self, dst):
+        if self.plane == "gloo":
+            dist.send(_hdr(1, self.global_step, 0), dst, group=self.group)
+        else:
+            dist.send(_hdr(1, self._gstep(), 1), dst, group=self.group)
+            _send_bytes(json.dumps(self.shard.descriptor()).encode(), dst, self.group)
 
     def _loop(self):
         hdr = torch.zeros(HDR, dtype=torch.int64)
@@ -194,19 +230,26 @@ class ParameterServerService:
             spec = json.loads(_recv_bytes(src, self.group).decode())
             vals = torch.zeros(int(h[2]), dtype=torch.float32)
             dist.recv(vals, src, group=self.group)
-            self.shard = _Shard(spec, vals, self.device)
             self.sync = bool(spec.get("sync", False))
             self.replicas_to_aggregate = int(spec.get("replicas_to_aggregate") or
                                              len(self.worker_ranks))
             self.global_step = int(spec.get("global_step", 0))
+            self.plane = choose_plane(spec.get("data_plane", "gloo"), self.device)
+            if self.plane == "gloo":
+                self.shard = _Shard(spec, vals, self.device)
+            else:
+                from .ps_device import OwnerShard
+                self.shard = OwnerShard(spec, vals, self.device, self.worker_ranks,
+                                        self.ps_index)
+                self.shard.start()
             for w in self.waiting_ready:
-                dist.send(_hdr(1, self.global_step), w, group=self.group)
+                self._ready_reply(w)
             self.waiting_ready = []
         elif op == OP_WAIT_READY:
             if self.shard is None:
                 self.waiting_ready.append(src)
             else:
-                dist.send(_hdr(1, self.global_step), src, group=self.group)
+                self._ready_reply(src)
         elif op == OP_PULL:
             self.stats["pulls"] += 1
             dist.send(_hdr(self.global_step, self.shard.numel), src, group=self.group)
@@ -226,15 +269,17 @@ class ParameterServerService:
             else:
                 self._sync_push(src, grad, step_of_grad, inc, want)
         elif op == OP_GET_STEP:
-            dist.send(_hdr(self.global_step), src, group=self.group)
+            dist.send(_hdr(self._gstep()), src, group=self.group)
         elif op == OP_STOP:
             self.stopped.add(src)
+            if self.plane != "gloo" and self.shard is not None:
+                self.shard.worker_stopped(src)
             # a stopped worker must not hold the sync barrier of the others
             if self.sync and self._sync_waiters and \
                     len(self.stopped) + len(self._sync_waiters) >= len(self.worker_ranks):
                 self._close_sync_step(force=True)
         elif op == OP_GET_STATE:
-            st = {"global_step": self.global_step, "names": self.shard.names,
+            st = {"global_step": self._gstep(), "names": self.shard.names,
                   "shapes": [list(s) for s in self.shard.shapes],
                   "slots": [s.name for s in self.shard.opt.slots],
                   "iterations": self.shard.opt.iterations}
@@ -244,8 +289,11 @@ class ParameterServerService:
                 dist.send(torch.cat([self.shard.opt.space.view_of(s.buf, p).reshape(-1)
                                      for p in self.shard.params]).cpu(), src, group=self.group)
         elif op == OP_SET_STATE:
-            vals = torch.zeros(self.shard.numel, dtype=torch.float32)
+            vals = torch.zeros(sum(_prod(sh) for sh in self.shard.shapes), dtype=torch.float32)
             dist.recv(vals, src, group=self.group)
+            if self.plane != "gloo":
+                self.shard.set_values(vals, int(h[2]))
+                return
             with torch.no_grad():
                 for p, v in zip(self.shard.params, _split(vals, self.shard.shapes)):
                     p.copy_(v)
@@ -301,20 +349,40 @@ class PSClient:
     ``pull()`` copies the PS values into the local parameters, ``push()`` sends the local
     gradients and returns the new global step."""
 
-    def __init__(self, ps_ranks, group=None, policy="balanced"):
+    def __init__(self, ps_ranks, group=None, policy="balanced", space=None, data_plane=None):
+        import os
         self.ps_ranks = list(ps_ranks)
         self.group = group
         self.policy = policy
+        self.space = space
+        # device data plane needs the flat buffers (ps_device.py); "gloo" = round-1 host path
+        self.data_plane = (data_plane or os.environ.get("DTF_PS_DATA_PLANE", "auto")) \
+            if space is not None else "gloo"
         self.params = None
         self.owner = None
         self.global_step = 0
+        self.links = None
+        self.plans = None
 
     def _layout(self, params):
         self.params = list(params)
+        if self.space is not None:
+            from .ps_device import shard_plan
+            self.plans = shard_plan(self.space, len(self.ps_ranks), self.policy)
+            self.by_ps = [pl["vars"] for pl in self.plans]
+            self.owner = [0] * len(self.params)
+            for k, idx in enumerate(self.by_ps):
+                for i in idx:
+                    self.owner[i] = k
+            return
         self.owner = assign_shards([p.numel() for p in self.params], len(self.ps_ranks),
                                    self.policy)
         self.by_ps = [[i for i, o in enumerate(self.owner) if o == k]
                       for k in range(len(self.ps_ranks))]
+
+    @property
+    def data_plane_in_use(self):
+        return "gloo" if not self.links else self.links[0].desc.get("plane", "?")
 
     def register(self, params, optimizer_cfg, names=None, sync=False, replicas_to_aggregate=None,
                  global_step=0):
@@ -326,7 +394,10 @@ class PSClient:
                     "shapes": [list(self.params[i].shape) for i in idx],
                     "optimizer": optimizer_cfg, "sync": sync,
                     "replicas_to_aggregate": replicas_to_aggregate,
-                    "global_step": global_step}
+                    "global_step": global_step, "data_plane": self.data_plane}
+            if self.plans is not None:
+                from .ps_device import spec_for
+                spec.update(spec_for(self.space, self.plans[k], names))
             vals = (torch.cat([self.params[i].detach().float().reshape(-1).cpu() for i in idx])
                     if idx else torch.zeros(0))
             dist.send(_hdr(OP_INIT, dist.get_rank(), vals.numel()), rank, group=self.group)
@@ -338,12 +409,24 @@ class PSClient:
         self._layout(params)
         for rank in self.ps_ranks:
             dist.send(_hdr(OP_WAIT_READY, dist.get_rank()), rank, group=self.group)
+        descs = []
         for rank in self.ps_ranks:
             r = torch.zeros(HDR, dtype=torch.int64)
             dist.recv(r, rank, group=self.group)
             self.global_step = max(self.global_step, int(r[1]))
+            descs.append(json.loads(_recv_bytes(rank, self.group).decode()) if int(r[2]) else None)
+        if all(d is not None for d in descs) and descs:
+            from .ps_device import PSLink
+            me = dist.get_rank()
+            self.links = [PSLink(d, self.plans[k], d["workers"].index(me), self.space.device, k)
+                          for k, d in enumerate(descs)]
 
     def pull(self):
+        if self.links:
+            for link in self.links:
+                link.pull(self.space)
+            self.global_step = self.links[0].global_step
+            return self.global_step
         for k, rank in enumerate(self.ps_ranks):
             dist.send(_hdr(OP_PULL, dist.get_rank()), rank, group=self.group)
         for k, rank in enumerate(self.ps_ranks):
@@ -360,6 +443,19 @@ class PSClient:
         """Send gradients (default: ``p.grad``) computed at ``self.global_step``; with
         ``pull`` the reply carries the updated shard values, copied into the local variables
         (push + pull in one round trip).  Returns the new global step."""
+        if self.links:
+            from .ps_device import sync_device
+            for link in self.links:                  # gradients straight into the mailboxes
+                link.copy_grads(self.space)
+            sync_device(self.space.device)
+            for link in self.links:
+                link.post(self.global_step)
+            steps = [link.wait() for link in self.links]
+            self.global_step = steps[0]
+            if pull:
+                for link in self.links:
+                    link.pull(self.space)
+            return self.global_step
         grads = grads or [p.grad for p in self.params]
         for k, rank in enumerate(self.ps_ranks):
             idx = self.by_ps[k]
@@ -392,6 +488,9 @@ class PSClient:
                     s.copy_(p.detach())
 
     def get_global_step(self):
+        if self.links:
+            self.global_step = self.links[0].global_step
+            return self.global_step
         dist.send(_hdr(OP_GET_STEP, dist.get_rank()), self.ps_ranks[0], group=self.group)
         r = torch.zeros(HDR, dtype=torch.int64)
         dist.recv(r, self.ps_ranks[0], group=self.group)

@@ -9,10 +9,11 @@ compute gradients, owners apply the optimizer, workers read back the new values:
   SyncReplicasOptimizer aggregation with stale-gradient drop).
 * **colocated, synchronous, on RCCL** (no ``server``; one process per GPU under torchrun): the
   PS shards are hosted by the GPU ranks themselves (``num_ps`` owners; 1 = "1 PS + N workers",
-  default = every rank owns a byte-balanced slice).  Per step: each owner's slice of the flat
-  gradient buffer is ``reduce``d to its owner over xGMI, the owner runs the fused optimizer on
-  exactly that slice, and ``broadcast``s the updated master slice back.  With num_ps == world
-  and equal slices this is a reduce-scatter / all-gather step.
+  default = every rank owns a byte-balanced slice).  Per step: as soon as a gradient bucket is
+  complete during backward, each owner's piece of it is ``reduce``d to its owner over xGMI
+  (overlapped with the rest of backward); after backward the owner runs the fused optimizer on
+  exactly its slices and ``broadcast``s the updated master slices back.  With num_ps == world
+  this is a bucketed reduce-scatter / all-gather step.
 """
 from __future__ import annotations
 
@@ -21,7 +22,8 @@ import os
 import torch
 import torch.distributed as dist
 
-from .strategy import MirroredStrategy, Strategy, _NullReducer, init_process_group_from_env
+from .strategy import (BucketedAllReduce, MirroredStrategy, Strategy, _NullReducer,
+                       init_process_group_from_env)
 
 
 class _RemotePSReducer(_NullReducer):
@@ -39,23 +41,36 @@ class _RemotePSReducer(_NullReducer):
         return self.client.push([p.grad for p in params], pull=True)
 
 
-class _ColocatedPSReducer(_NullReducer):
-    """Colocated sync PS on RCCL: reduce slice -> owner apply -> broadcast slice."""
+class _ColocatedPSReducer(BucketedAllReduce):
+    """Colocated sync PS on RCCL, overlapped with backward.
+
+    The gradient buffer is cut into the same buckets as MirroredStrategy's all-reduce.  When a
+    bucket's last gradient lands (post-accumulate hook, during backward) each owner's piece of
+    it is ``reduce``d to that owner on RCCL's stream -- the gradient push of the reference's
+    ``SyncReplicasOptimizer`` (``templates/00_mnist_replica.py:168-191``) happens while autograd
+    is still producing earlier layers.  After backward: each owner applies the fused optimizer
+    to the slices it owns and ``broadcast``s the updated master slices (the variable pull)."""
 
     applies_update = True
 
-    def __init__(self, space, owners_ranges, group=None):
-        super().__init__(space)
+    def __init__(self, space, owners_ranges, group=None, bucket_bytes=64 << 20,
+                 first_bucket_bytes=4 << 20):
+        super().__init__(space, group, bucket_bytes, first_bucket_bytes)
         self.ranges = owners_ranges          # [(owner_rank, start, end)]
-        self.group = group
-        self.world = dist.get_world_size(group)
         self.rank = dist.get_rank()
+        # per bucket: [(owner, start, end)] pieces (bucket ∩ owner range)
+        self.pieces = []
+        for bs, be, _ in self.buckets:
+            self.pieces.append([(o, max(bs, s), min(be, e)) for o, s, e in owners_ranges
+                                if min(be, e) > max(bs, s)])
 
-    def finish(self):
-        works = [dist.reduce(self.space.grad[s:e], dst=o, group=self.group, async_op=True)
-                 for o, s, e in self.ranges if e > s]
-        for w in works:
-            w.wait()
+    def _launch(self, b):
+        if self.launched[b]:
+            return
+        self.launched[b] = True
+        for o, s, e in self.pieces[b]:
+            self.works.append((dist.reduce(self.space.grad[s:e], dst=o, group=self.group,
+                                           async_op=True), None, None))
 
     def grad_scale(self):
         return 1.0 / self.world
@@ -88,8 +103,12 @@ def balanced_ranges(space, num_owners, owner_ranks):
 
 class ParameterServerStrategy(Strategy):
     def __init__(self, cluster_resolver=None, server=None, num_ps=None, sync=None,
-                 replicas_to_aggregate=None, variable_placement="balanced", device=None):
+                 replicas_to_aggregate=None, variable_placement="balanced", device=None,
+                 data_plane=None, bucket_mb=64, first_bucket_mb=4):
         self.server = server
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.first_bucket_bytes = int(first_bucket_mb * (1 << 20))
+        self.data_plane = data_plane
         self.variable_placement = variable_placement
         self.replicas_to_aggregate = replicas_to_aggregate
         self._client = None
@@ -143,12 +162,14 @@ class ParameterServerStrategy(Strategy):
     def make_gradient_reducer(self, space):
         if self.mode == "between_graph":
             from .ps_service import PSClient
-            self._client = PSClient(self.server.ps_ranks(), policy=self.variable_placement)
+            self._client = PSClient(self.server.ps_ranks(), policy=self.variable_placement,
+                                    space=space, data_plane=self.data_plane)
             return _RemotePSReducer(space, self._client)
         if not dist.is_initialized() or dist.get_world_size() == 1:
             return _NullReducer(space)
         ranges = balanced_ranges(space, self.num_ps, list(range(self.num_ps)))
-        return _ColocatedPSReducer(space, ranges)
+        return _ColocatedPSReducer(space, ranges, None, self.bucket_bytes,
+                                   self.first_bucket_bytes)
 
     def broadcast_space(self, space):
         if self.mode == "colocated":

@@ -73,11 +73,55 @@ class _NullReducer:
         return 1.0
 
 
+class CommStats:
+    """What the step's communication did, for the bench JSON and the overlap test.
+
+    ``early`` / ``late``: buckets launched from the backward hooks (overlapped with autograd) vs
+    launched only when ``finish()`` ran after backward.  ``exposed_ms``: time the compute stream
+    waited for communication after backward (CUDA events around ``finish()``; host clock on
+    CPU) -- the part of the all-reduce the overlap did not hide."""
+
+    def __init__(self, n_buckets, bucket_bytes):
+        self.n_buckets = n_buckets
+        self.bucket_bytes = list(bucket_bytes)
+        self.steps = 0
+        self.early = 0
+        self.late = 0
+        self.last_early = 0
+        self.timing = False
+        self._events = []
+        self._host_s = 0.0
+
+    def reset_timing(self):
+        self._events, self._host_s, self.steps, self.early, self.late = [], 0.0, 0, 0, 0
+
+    def exposed_ms(self):
+        """Total exposed communication time since ``reset_timing`` (synchronises)."""
+        if self._events:
+            torch.cuda.synchronize()
+            return sum(a.elapsed_time(b) for a, b in self._events)
+        return self._host_s * 1e3
+
+    def as_dict(self):
+        ms = self.exposed_ms()
+        return {"buckets": self.n_buckets,
+                "bucket_mb": [round(b / 2**20, 2) for b in self.bucket_bytes],
+                "steps": self.steps, "early_launches": self.early, "late_launches": self.late,
+                "exposed_ms_total": round(ms, 3),
+                "exposed_ms_per_step": round(ms / max(self.steps, 1), 3)}
+
+
 class BucketedAllReduce:
-    """Overlapped bucketed all-reduce of a FlatSpace's gradient buffer."""
+    """Overlapped bucketed all-reduce of a FlatSpace's gradient buffer.
+
+    ``compress_bf16``: gradients travel as bf16 but are SUMMED in fp32 -- an all-to-all of bf16
+    chunks (the reduce-scatter's data movement), a local fp32 sum of the W chunks each rank owns,
+    then an all-gather of the bf16-rounded sums.  Each element is rounded twice (once per input,
+    once per output: relative error <= 2^-8 of each term and of the sum, independent of the
+    rank count), where an all-reduce run in bf16 would round at every one of the W-1 hops."""
 
     def __init__(self, space, group=None, bucket_bytes=64 << 20, first_bucket_bytes=4 << 20,
-                 average=True, compress_bf16=False):
+                 average=True, compress_bf16=False, overlap=True):
         self.space = space
         self.group = group
         self.world = dist.get_world_size(group)
@@ -113,9 +157,11 @@ class BucketedAllReduce:
         self.pending = [0] * len(ranges)
         self.works = []
         self.launched = [False] * len(ranges)
+        self.stats = CommStats(len(ranges), [(e - s) * 4 for s, e, _ in ranges])
         self._hooks = []
         for i, v in enumerate(order):
-            self._hooks.append(v.register_post_accumulate_grad_hook(self._make_hook(i)))
+            if overlap:
+                self._hooks.append(v.register_post_accumulate_grad_hook(self._make_hook(i)))
             # Ops that write their gradient straight into the flat buffer (ops/native.py
             # _direct_grad) return None for the variable, and autograd still runs the variable's
             # AccumulateGrad node -- once per backward, after every op that consumes the variable
@@ -139,27 +185,72 @@ class BucketedAllReduce:
         s, e, _ = self.buckets[b]
         view = self.space.grad[s:e]
         if self.compress:
-            tmp = view.to(torch.bfloat16)
-            w = dist.all_reduce(tmp, group=self.group, async_op=True)
-            self.works.append((w, view, tmp))
+            W, L = self.world, e - s
+            c = -(-L // W)
+            send = torch.zeros(W * c, dtype=torch.bfloat16, device=view.device)
+            send[:L].copy_(view)
+            recv = torch.empty_like(send)
+            w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
+            self.works.append((w, view, (recv, c, L)))
         else:
             self.works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+
+    def _finish_compressed(self, view, recv, c, L):
+        W = self.world
+        part = recv.view(W, c).float().sum(0).to(torch.bfloat16)   # fp32 sum of my chunk
+        parts = [torch.empty_like(part) for _ in range(W)]
+        return dist.all_gather(parts, part, group=self.group, async_op=True), view, parts, L
 
     def begin_step(self):
         self.pending = [len(m) for (_, _, m) in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.works = []
 
+    def _timing_begin(self):
+        st = self.stats
+        if not st.timing:
+            return None
+        if self.space.grad.is_cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        import time
+        return time.perf_counter()
+
+    def _timing_end(self, t0):
+        st = self.stats
+        if t0 is None:
+            return
+        if isinstance(t0, torch.cuda.Event):
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            st._events.append((t0, ev))
+        else:
+            import time
+            st._host_s += time.perf_counter() - t0
+
     def finish(self):
+        st = self.stats
+        early = sum(self.launched)
+        st.steps += 1
+        st.early += early
+        st.late += len(self.buckets) - early
+        st.last_early = early
+        t0 = self._timing_begin()
         # buckets whose variables received no gradient this step still have to be reduced
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
-        for w, view, tmp in self.works:
+        gathers = []
+        for w, view, extra in self.works:
             w.wait()
-            if view is not None:
-                view.copy_(tmp)
+            if extra is not None:
+                gathers.append(self._finish_compressed(view, *extra))
+        for w, view, parts, L in gathers:
+            w.wait()
+            view.copy_(torch.cat(parts)[:L])
         self.works = []
+        self._timing_end(t0)
 
     def grad_scale(self):
         return 1.0 / self.world if self.average else 1.0
@@ -289,7 +380,7 @@ class MirroredStrategy(Strategy):
     """
 
     def __init__(self, devices=None, cross_device_ops=None, bucket_mb=64, first_bucket_mb=4,
-                 compress_bf16=False, backend=None):
+                 compress_bf16=False, backend=None, overlap=True):
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
@@ -300,6 +391,7 @@ class MirroredStrategy(Strategy):
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.first_bucket_bytes = int(first_bucket_mb * (1 << 20))
         self.compress_bf16 = compress_bf16
+        self.overlap = overlap
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             init_process_group_from_env(backend)
         self._dist = dist.is_initialized() and dist.get_world_size() > 1
@@ -316,7 +408,7 @@ class MirroredStrategy(Strategy):
         if not self._dist:
             return _NullReducer(space)
         return BucketedAllReduce(space, None, self.bucket_bytes, self.first_bucket_bytes,
-                                 compress_bf16=self.compress_bf16)
+                                 compress_bf16=self.compress_bf16, overlap=self.overlap)
 
     def broadcast_space(self, space):
         if self._dist:

@@ -4,7 +4,7 @@
 
 Here it is a small object holding an int64 tensor (checkpointed as ``global_step``) plus a host
 mirror so hooks (StopAtStepHook) can read it without a device sync.  In async parameter-server
-mode the authoritative value lives with the PS service (see ``parallel/ps.py``) and
+mode the authoritative value lives with the PS service (``parallel/ps_service.py`` / ``ps_device.py``) and
 ``assign()`` syncs the local mirror.
 """
 from __future__ import annotations

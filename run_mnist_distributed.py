@@ -45,9 +45,17 @@ def main():
     config = Config(FLAGS.config)
     ps_hosts, worker_hosts = config.get_ps_and_worker_hosts()
     cluster = ClusterSpec({"ps": list(ps_hosts), "worker": list(worker_hosts)})
-    server = Server(cluster, job_name=FLAGS.job_name, task_index=FLAGS.task_index)
+    ps_device = FLAGS.ps_device
+    if ps_device == "auto":
+        ps_device = "gpu" if torch.cuda.is_available() else "cpu"
+    ps_device = (f"cuda:{FLAGS.task_index % torch.cuda.device_count()}" if ps_device == "gpu"
+                 else "cpu")
+    server = Server(cluster, job_name=FLAGS.job_name, task_index=FLAGS.task_index,
+                    ps_device=ps_device)
 
     if FLAGS.job_name == "ps":
+        if ps_device != "cpu":
+            torch.cuda.set_device(torch.device(ps_device))
         print("Started Parameter Server ...", flush=True)
         stats = server.join()
         print("Close Parameter Server ...", stats, flush=True)
@@ -76,7 +84,8 @@ def main():
           .repeat().batch(batch_size).prefetch(4))
     it = iter(ds)
 
-    strategy = ParameterServerStrategy(server=server, sync=FLAGS.sync_replicas, device=device)
+    strategy = ParameterServerStrategy(server=server, sync=FLAGS.sync_replicas, device=device,
+                                       data_plane=FLAGS.data_plane)
     with strategy.scope():
         model = MnistCNN()
         opt = dtf.train.AdamOptimizer(FLAGS.learning_rate)
@@ -146,6 +155,12 @@ def parse(argv=None):
     parser.add_argument("--checkpoint_dir", default=None)
     parser.add_argument("--sync_replicas", action="store_true")
     parser.add_argument("--device", choices=("auto", "cpu", "gpu"), default="auto")
+    parser.add_argument("--ps_device", choices=("auto", "cpu", "gpu"), default="auto",
+                        help="where a ps task keeps its variable shard (auto: its GPU's HBM)")
+    parser.add_argument("--data_plane", choices=("auto", "ipc", "shm", "gloo"), default=None,
+                        help="PS push/pull transport: auto = HBM shard mapped over hipIpc (GPU "
+                             "PS) or /dev/shm (CPU PS); gloo = host tensors over TCP "
+                             "(cross-host clusters)")
     flags, _unparsed = parser.parse_known_args(argv)
     return flags
 

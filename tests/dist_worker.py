@@ -75,11 +75,14 @@ def main():
     if kind == "mirrored":
         strat = MirroredStrategy(bucket_mb=float(kw.get("bucket_mb", 64)),
                                  first_bucket_mb=float(kw.get("bucket_mb", 4)),
-                                 compress_bf16=kw.get("bf16", "0") == "1")
+                                 compress_bf16=kw.get("bf16", "0") == "1",
+                                 overlap=kw.get("overlap", "1") == "1")
     elif kind == "multiworker":
         strat = MultiWorkerMirroredStrategy()
     elif kind == "colocated_ps":
-        strat = ParameterServerStrategy(num_ps=int(kw.get("num_ps", 1)))
+        strat = ParameterServerStrategy(num_ps=int(kw.get("num_ps", 1)),
+                                        bucket_mb=float(kw.get("bucket_mb", 64)),
+                                        first_bucket_mb=float(kw.get("bucket_mb", 4)))
     else:
         raise SystemExit(f"unknown strategy {kind}")
     rank, world = strat.replica_id, strat.num_replicas_in_sync
@@ -92,16 +95,20 @@ def main():
         gstep = dtf.train.get_or_create_global_step()
         opt.build(list(model.parameters()))
         per = 16 // world
+        early = []
         for step in range(steps):
             x, y = global_batch(step)
             x, y = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
             loss = ops.sparse_softmax_cross_entropy(model(x), y)
             opt.minimize(loss, global_step=gstep)
+            st = getattr(opt._reducer, "stats", None)
+            if st is not None:
+                early.append((st.last_early, st.n_buckets))
         mean_loss = float(strat.reduce(dtf.distribute.ReduceOp.MEAN, loss.detach()))
         fps = dtf.distribute.check_replicas_consistent(opt)      # raises if replicas diverged
     torch.save({"state": {k: v.detach().clone() for k, v in model.state_dict().items()},
                 "global_step": gstep.value(), "world": world, "mean_loss": mean_loss,
-                "fingerprints": fps},
+                "fingerprints": fps, "early_launches": early},
                os.path.join(out, f"rank{rank}.pt"))
     strat.barrier()
 

@@ -86,6 +86,23 @@ def test_mirrored_two_ranks_matches_single_process(tmp_path, args):
     assert res[0]["mean_loss"] == res[1]["mean_loss"]
 
 
+@pytest.mark.parametrize("kind,args", [("mirrored", ("bucket_mb=0.05",)),
+                                       ("colocated_ps", ("bucket_mb=0.05", "num_ps=2",
+                                                         "opt=adam"))],
+                         ids=["mirrored", "colocated_ps"])
+def test_buckets_launch_during_backward(tmp_path, kind, args):
+    """Overlap: every bucket but (at most) the last is launched from the post-accumulate hooks,
+    i.e. before loss.backward() returned -- the negative control (hooks off) launches none."""
+    res = _launch(kind, 2, tmp_path, *args)
+    for r in res:
+        assert r["early_launches"], "no bucket statistics recorded"
+        for early, n in r["early_launches"]:
+            assert n >= 3 and early >= n - 1, r["early_launches"]
+    off = _launch("mirrored", 2, tmp_path, "bucket_mb=0.05", "overlap=0")
+    _assert_replicas(off, _single_process())
+    assert all(e == 0 for r in off for e, _ in r["early_launches"])
+
+
 def test_mirrored_bf16_gradient_compression(tmp_path):
     res = _launch("mirrored", 2, tmp_path, "bf16=1", "opt=adam")
     ref = _single_process("adam")
@@ -170,3 +187,20 @@ def test_heartbeat_detects_silent_peer(tmp_path):
     assert all(p.returncode == 0 for p in procs), outs
     res = json.load(open(tmp_path / "hb.json"))
     assert res["failed"] == [1] and res["after_s"] < 8
+
+
+def test_allreduce_bandwidth_tool_gloo(tmp_path):
+    """tools/allreduce_bw.py (SURVEY §5.8 bus-bandwidth sweep) runs under torchrun, 2 ranks."""
+    port = free_ports(1)[0]
+    out = tmp_path / "bw.jsonl"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "tools", "allreduce_bw.py"), "--min-mb", "0.25",
+                        "--max-mb", "0.5", "--iters", "2", "--warmup", "1", "--bucket-mb", "64",
+                        "--out", str(out)],
+                       env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2"),
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    rows = [json.loads(line) for line in open(out)]
+    assert [x["size_mb"] for x in rows[:-1]] == [0.25, 0.5]
+    assert all(x["busbw_GBps"] > 0 for x in rows[:-1]) and rows[-1]["bucketed_allreduce_ms"] > 0

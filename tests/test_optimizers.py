@@ -258,3 +258,20 @@ def test_optimizer_config_roundtrip():
         kind = cfg.pop("type")
         clone = type(opt)(**cfg)
         assert clone.get_config()["type"] == kind
+
+
+def test_sync_replicas_backup_workers_need_between_graph_ps():
+    """Collective strategies aggregate every replica each step; asking them for backup workers
+    (replicas_to_aggregate < replicas) must raise instead of silently ignoring it."""
+    from distributedtensorflow_amd.optimizers import AdamOptimizer
+    from distributedtensorflow_amd.optimizers.sync_replicas import SyncReplicasOptimizer
+    from distributedtensorflow_amd.parallel.strategy import Strategy
+
+    class TwoReplicas(Strategy):
+        num_replicas_in_sync = 2
+
+    with TwoReplicas("cpu").scope():
+        SyncReplicasOptimizer(AdamOptimizer(0.1), replicas_to_aggregate=2)     # all replicas: ok
+        with pytest.raises(ValueError, match="backup workers"):
+            SyncReplicasOptimizer(AdamOptimizer(0.1), replicas_to_aggregate=1,
+                                  total_num_replicas=2)

@@ -79,7 +79,7 @@ def test_resnet50_train_first_stage_matches_reference():
 
     Deeper outputs are not compared: a random-init BN ResNet is chaotic — feeding the fp32
     reference graph the bf16-ROUNDED input (0.17% change) already moves the final block by 23%
-    (tools/debug_resnet_layers.py), so end-to-end agreement is not a kernel-accuracy test."""
+    (a per-layer probe in round 1), so end-to-end agreement is not a kernel-accuracy test."""
     torch.manual_seed(0)
     m = resnet50().cuda().train()
     x, _ = _inputs(n=16, s=96)
