@@ -23,6 +23,8 @@ struct ConvGeom {
   int N, H, W, C, P, Q, sh, sw, Kout, Kpad, Ho, Wo, osh, osw, oh0, ow0, acc;
   const bf16_t* acc_src;
   const uint8_t* acc_mask;
+  const float* bias;
+  int relu;
 };
 struct BnBwdEpi {
   const bf16_t* x; const float* mean; const float* invstd; const float* fsc; const float* fsh;
@@ -139,6 +141,14 @@ void dtf_segment_sum(const int64_t*, const int64_t*, const bf16_t*, float*, int,
 void dtf_mlm_xent(const bf16_t*, const int64_t*, const float*, const float*, int, int, float*,
                   bf16_t*, hipStream_t);
 
+// ---- dense GEMM (gemm.hip)
+void dtf_gemm_nt(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int,
+                 const float*, const bf16_t*, int, hipStream_t);
+void dtf_gemm_set_variant(int);
+int dtf_bias_relu_bwd_ws_floats(int);
+void dtf_bias_relu_bwd(const bf16_t*, const bf16_t*, bf16_t*, int, int, float*, float*, int, int,
+                       hipStream_t);
+
 // ---- HIP IPC buffers (ipc.cpp) handed to torch as DLPack capsules
 uintptr_t dtf_ipc_alloc(size_t, int);
 std::string dtf_ipc_handle(uintptr_t, int);
@@ -206,6 +216,20 @@ static TT make_taps(const std::vector<int>& dh, const std::vector<int>& dw) {
 PYBIND11_MODULE(_dtf_hip, m) {
   m.doc() = "distributedtensorflow_amd HIP/CDNA4 kernels (gfx950)";
 
+  m.def("gemm_nt", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, int lda,
+                      int ldb, int ldc, uintptr_t bias, uintptr_t cin, int relu, uintptr_t st) {
+    dtf_gemm_nt(P<bf16_t>(a), P<bf16_t>(b), P<bf16_t>(c), M, N, K, lda, ldb, ldc,
+                P<float>(bias), P<bf16_t>(cin), relu, S(st));
+    check_launch("gemm_nt");
+  });
+  m.def("gemm_set_variant", &dtf_gemm_set_variant);
+  m.def("bias_relu_bwd_ws_floats", &dtf_bias_relu_bwd_ws_floats);
+  m.def("bias_relu_bwd", [](uintptr_t dy, uintptr_t y, uintptr_t dz, int T, int N, uintptr_t ws,
+                            uintptr_t db, int accumulate, int relu, uintptr_t st) {
+    dtf_bias_relu_bwd(P<bf16_t>(dy), P<bf16_t>(y), P<bf16_t>(dz), T, N, P<float>(ws), P<float>(db),
+                      accumulate, relu, S(st));
+    check_launch("bias_relu_bwd");
+  });
   // parameter-server data plane: exported / mapped HBM buffers (ipc.cpp)
   m.def("ipc_alloc", [](int64_t numel, int device, int dtype_bits) {
     const size_t bytes = (size_t)numel * (dtype_bits == 8 ? 1 : 4);
@@ -430,13 +454,13 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("conv_igemm", [](uintptr_t x, uintptr_t w, uintptr_t y, std::vector<int> geom,
                          std::vector<int> dh, std::vector<int> dw, int bk, uintptr_t st,
                          uintptr_t stats, std::vector<uintptr_t> bnb, uintptr_t acc_src,
-                         uintptr_t acc_mask) {
+                         uintptr_t acc_mask, uintptr_t bias, int relu) {
     if (geom.size() != 16 && geom.size() != 17)
       throw std::runtime_error("conv_igemm: geom needs 16 (+acc) ints");
     ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
                geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15],
                geom.size() == 17 ? geom[16] : 0, P<const bf16_t>(acc_src),
-               P<const uint8_t>(acc_mask)};
+               P<const uint8_t>(acc_mask), P<const float>(bias), relu};
     if (g.acc == 2 && (!g.acc_src || !g.acc_mask))
       throw std::runtime_error("conv_igemm: acc 2 needs acc_src and acc_mask");
     // bnb = [x, mean, invstd, fsc, fsh, mask, part, mkind, row0] (fused BN-backward sums) or []
@@ -452,7 +476,8 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("conv_igemm");
   }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("dh"), py::arg("dw"),
      py::arg("bk"), py::arg("stream"), py::arg("stats") = 0,
-     py::arg("bnb") = std::vector<uintptr_t>{}, py::arg("acc_src") = 0, py::arg("acc_mask") = 0);
+     py::arg("bnb") = std::vector<uintptr_t>{}, py::arg("acc_src") = 0, py::arg("acc_mask") = 0,
+     py::arg("bias") = 0, py::arg("relu") = 0);
   m.def("bn_bwd_finalize_g", [](uintptr_t part, int G, long M, int C, uintptr_t gamma,
                                 uintptr_t mean, uintptr_t invstd, uintptr_t dg, uintptr_t db,
                                 uintptr_t a, uintptr_t b, uintptr_t c, int accumulate,

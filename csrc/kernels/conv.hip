@@ -57,6 +57,8 @@ struct ConvGeom {
                          // 2: Y = result + acc_src * relu_mask (see acc_add8)
   const bf16_t* acc_src; // acc 2: the residual BN's incoming dy, [N, Ho, Wo, Kout] like Y
   const uint8_t* acc_mask;  // acc 2: that BN's forward ReLU bit mask (1 byte per 8 channels)
+  const float* bias;        // fused epilogue (register kernel only): Y = act(conv + bias[k])
+  int relu;                 //   tf.layers.conv2d(activation=tf.nn.relu) -- MNIST K3/K5
 };
 
 // Residual-gradient accumulation in the dgrad epilogue.  acc 1 reads the materialised residual
@@ -411,6 +413,14 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   __builtin_amdgcn_sched_barrier(0);
   constexpr int LDC = BN + 8;
   bf16_t* st = lds;
+  float bj[4] = {0.f, 0.f, 0.f, 0.f};
+  if (g.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn * 64 + j * 16 + frow;
+      bj[j] = col < g.Kout ? g.bias[col] : 0.f;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -419,7 +429,9 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
       for (int r = 0; r < 4; ++r) {
         const int row = wm * 64 + i * 16 + fq * 4 + r;
         const int col = wn * 64 + j * 16 + frow;
-        st[row * LDC + col] = f2bf(acc[i][j][r]);
+        float v = acc[i][j][r] + bj[j];
+        if (g.relu) v = fmaxf(v, 0.f);
+        st[row * LDC + col] = f2bf(v);
       }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();
@@ -979,6 +991,9 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
   if (xbytes >= 2147483647.0 || wbytes >= 2147483647.0 || m >= 2147483647.0)
     throw std::runtime_error("conv: tensor too large for 32-bit buffer offsets");
   const bool narrow = g.Kout <= 64;        // 256 x 64 tile for 64-wide layers
+  const bool epi = g.bias || g.relu;       // fused bias / ReLU: register kernel only
+  if (epi && (bnb.part || g.acc))
+    throw std::runtime_error("conv: fused bias/ReLU epilogue excludes BN / accumulate epilogues");
   if (g.C % 32 != 0) {
     if (g.Kpad % 32) throw std::runtime_error("conv: Kpad % 32 != 0");
     if (g.C % 8 == 0) {                    // chunk gather (stem / MNIST conv1, C padded to 8)
@@ -990,7 +1005,7 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
     }
     return;
   }
-  if (!bnb.part && use_halo(g, taps)) {
+  if (!bnb.part && !epi && use_halo(g, taps)) {
     const dim3 grid0((unsigned)(g.N * (g.H / kHaloTH)));
     if (halo_family(g, taps) == 1) {
       using Hc = HaloCfg<64, 56, 2, 64>;
@@ -1003,7 +1018,7 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
     }
     return;
   }
-  if (use_dma_kernel((long)m, g.Kout, g.C, taps.n, bk) && g.Kpad % 64 == 0) {
+  if (!epi && use_dma_kernel((long)m, g.Kout, g.C, taps.n, bk) && g.Kpad % 64 == 0) {
     const long tiles = (((long)m + kDmaBM - 1) / kDmaBM) * (g.Kout / kDmaBN);
     if (bnb.part)
       hipLaunchKernelGGL(conv_igemm_dma_kernel<true>, dim3((unsigned)tiles), dim3(kDmaThreads), 0,

@@ -1,0 +1,102 @@
+// Dense-layer backward epilogue (MatMul grads + BiasAddGrad + ReluGrad).
+//
+//   dz = relu ? dy * (y > 0) : dy          (y = the layer's forward output, already ReLU-ed)
+//   db = sum_rows(dz)                      (fp32, deterministic two-level reduction)
+//
+// One pass over dy / y writes dz (the operand of the data- and weight-gradient GEMMs) and the
+// per-slice column sums; a second tiny launch sums the S slices in a fixed order into db (added
+// to it with `accumulate`: direct writes into the optimizer's flat gradient buffer).  Replaces
+// autograd's ReluGrad kernel + a separate BiasAddGrad reduction over the same tensor.
+#include <stdexcept>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kDSplits = 256;
+
+__global__ void __launch_bounds__(256)
+bias_relu_bwd_split_kernel(const bf16_t* dy, const bf16_t* __restrict__ y, bf16_t* dz, int T, int N, float* __restrict__ ws, int R, int relu) {
+  __shared__ float red[4][64][9];
+  const int cv = blockIdx.x * 64 + (threadIdx.x & 63);      // 8-column vector index
+  const int rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * R, r1 = min(T, r0 + R);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cv * 8 < N) {
+    const long rs = N / 8;
+    const uint4* D4 = reinterpret_cast<const uint4*>(dy) + cv;
+    const uint4* Y4 = reinterpret_cast<const uint4*>(y) + cv;
+    uint4* Z4 = reinterpret_cast<uint4*>(dz) + cv;
+    for (int r = r0 + rg; r < r1; r += 4) {
+      float f[8];
+      uint4 d = D4[(long)r * rs];
+      if (relu) {
+        const uint4 yv = Y4[(long)r * rs];
+        const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+        uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {     // bf16 y > 0 <=> sign clear and non-zero
+          const uint32_t lo = (yw[i] & 0x8000u) || !(yw[i] & 0x7FFFu) ? 0u : 0xFFFFu;
+          const uint32_t hi = (yw[i] & 0x80000000u) || !(yw[i] & 0x7FFF0000u) ? 0u : 0xFFFF0000u;
+          dw[i] &= lo | hi;
+        }
+        d = make_uint4(dw[0], dw[1], dw[2], dw[3]);
+        Z4[(long)r * rs] = d;
+      } else if (dz != dy) {
+        Z4[(long)r * rs] = d;
+      }
+      unpack8(d, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += f[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rg][threadIdx.x & 63][e] = acc[e];
+  __syncthreads();
+  if (rg == 0 && cv * 8 < N) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = red[0][threadIdx.x][e];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) t += red[k][threadIdx.x][e];
+      ws[(long)blockIdx.y * N + cv * 8 + e] = t;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+col_slices_final_kernel(const float* __restrict__ ws, int S, int N, float* __restrict__ out,
+                        int accumulate) {
+  __shared__ float red[16][17];
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const int rg = threadIdx.x >> 4;
+  float t = 0.f;
+  if (c < N)
+    for (int k = rg; k < S; k += 16) t += ws[(long)k * N + c];
+  red[rg][threadIdx.x & 15] = t;
+  __syncthreads();
+  if (rg == 0 && c < N) {
+    float u = red[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) u += red[k][threadIdx.x];
+    out[c] = accumulate ? out[c] + u : u;
+  }
+}
+
+}  // namespace
+
+int dtf_bias_relu_bwd_ws_floats(int N) { return kDSplits * N; }
+
+void dtf_bias_relu_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dz, int T, int N, float* ws,
+                       float* db, int accumulate, int relu, hipStream_t st) {
+  if (N % 8) throw std::runtime_error("bias_relu_bwd: N % 8 != 0");
+  if (T <= 0) return;
+  int S = T / 64;
+  S = S < 1 ? 1 : (S > kDSplits ? kDSplits : S);
+  const int R = (T + S - 1) / S;
+  hipLaunchKernelGGL(bias_relu_bwd_split_kernel, dim3((N / 8 + 63) / 64, S), dim3(256), 0, st, dy,
+                     y, dz, T, N, ws, R, relu);
+  if (db)
+    hipLaunchKernelGGL(col_slices_final_kernel, dim3((N + 15) / 16), dim3(256), 0, st, ws, S, N,
+                       db, accumulate);
+}

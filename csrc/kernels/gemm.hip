@@ -1,0 +1,318 @@
+// Dense bf16 GEMM on MFMA (gfx950): C[M, N] = A[M, K] . B[N, K]^T  (+ bias[N]) (ReLU) (+ Cin)
+//
+// The "NT" form -- both operands K-contiguous rows -- is what every dense layer of the framework
+// needs: forward y = x W^T (W stored [out][in], the TF/BERT layout) and data gradient
+// dx = dy W, with W^T staged once per step by the batched filter-transpose kernel (the weight
+// gradient, a sum over tokens, is the conv_wgrad kernel's TN form).  SURVEY.md K8/K9/N-K4/N-K6.
+//
+// Tiling (cdna_hip_programming.md §5, "glds vs register staging" first row; §5.5 T1/T2/T5):
+//   * 512 threads = 8 waves as 2 (M) x 4 (N); block tile 256 x 256, wave tile 128 x 64 built from
+//     8 x 4 v_mfma_f32_16x16x32_bf16 fragments (16x16x32 holds a higher clock than 32x32x16 under
+//     load: MI355X_MICROARCH.md "DVFS give-back" (7)); BK = 64.
+//   * both tiles staged by LDS-DMA (buffer_load_dwordx4 ... lds: no staging VGPRs, no ds_write
+//     pass), two 64-KB stages, the next K-step's DMAs issued before the current step's MFMAs;
+//     one counted vmcnt + raw s_barrier per K-step (a __syncthreads() would drain the DMAs).
+//   * the DMA writes a wave-instruction's 64 x 16 B lane-linearly, so the XOR chunk swizzle that
+//     makes the 16-row ds_read_b128 fragment reads conflict-free is applied on the SOURCE side:
+//     LDS slot s of row r receives source chunk s ^ ((r >> 1) & 7).
+//   * rows past M and K-chunks past K get an out-of-range buffer offset: the hardware range check
+//     returns zeros -- no branches, no padding copies.  Each block's buffer descriptors are based
+//     at ITS first row (64-bit pointer arithmetic on the host side of the descriptor), so the
+//     32-bit offsets only ever span one 256-row panel: tensors far beyond 2 GiB are fine.
+//   * XCD-aware bijective block remap, N-tile fastest: blocks sharing an A panel share an L2.
+//   * epilogue: accumulators (+bias, ReLU) -> bf16 -> LDS -> 16-B coalesced stores (+Cin: the
+//     beta = 1 accumulation used to fold a residual gradient into a data-gradient GEMM).
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kGT = 512;                     // threads (8 waves)
+constexpr uint32_t kGOOB = 0xFFFFFFF0u;
+
+struct GemmArgs {
+  const bf16_t* A; const bf16_t* B; bf16_t* C;
+  const float* bias;      // [N] fp32 or null
+  const bf16_t* Cin;      // accumulate source ([M][ldc], may alias C) or null
+  int M, N, K, lda, ldb, ldc;
+  int relu;
+};
+
+// chunk swizzle of a [rows][BK] bf16 tile: 16-row ds_read_b128 fragment reads hit 16 slots
+template <int BK>
+DTF_DEV int gswz(int row, int ch) {
+  constexpr int CPR = BK / 8, RPB = 16 / CPR;
+  return ch ^ ((row / RPB) % CPR);
+}
+
+// s_waitcnt vmcnt(N) with N a template literal
+template <int N>
+DTF_DEV void wait_vm() {
+  static_assert(N == 0 || N == 6 || N == 8 || N == 12 || N == 16, "add the wait count");
+  if constexpr (N == 0) DTF_WAIT_VM(0);
+  else if constexpr (N == 6) DTF_WAIT_VM(6);
+  else if constexpr (N == 8) DTF_WAIT_VM(8);
+  else if constexpr (N == 12) DTF_WAIT_VM(12);
+  else DTF_WAIT_VM(16);
+}
+
+// BM x BN block tile, BK-deep K-steps, NS-slot LDS ring (DMAs issued NS-1 steps ahead), NW waves.
+//   NW 8: 2 (M) x BN/64 (N) waves, 64-column wave tiles, 2 waves per SIMD;
+//   NW 4: 2 x 2 waves of 128 x 128 -- ONE wave per SIMD whose 64 accumulator fragments live in
+//         the AGPR half of the unified register file (the per-wave tile hipBLASLt's fastest
+//         MI355X kernels use: 16 fragment reads per 64 MFMAs instead of 12 per 32, and no second
+//         wave competing for the SIMD's matrix pipe).
+template <int BM, int BN, int BK, int NS, int NW = 8>
+struct GCfg {
+  static constexpr int NT = NW * 64;
+  static constexpr int WN = NW == 8 ? BN / 64 : 2, WM = NW / WN;   // wave grid
+  static constexpr int WTM = BM / WM, WTN = BN / WN;               // wave tile
+  static constexpr int FM = WTM / 16, FN = WTN / 16;               // 16x16 fragments per wave
+  static constexpr int CPR = BK / 8;                       // 16-B chunks per row
+  static constexpr int RPI = 64 / CPR;                     // rows per 1-KB DMA instruction
+  static constexpr int DA = BM / RPI / NW, DB = BN / RPI / NW;   // DMAs per wave per stage
+  static constexpr int SA = BM * BK, STAGE = (BM + BN) * BK;   // bf16 elements
+  static constexpr int LDC = BN + 8;
+  static constexpr size_t LDS = (size_t)NS * STAGE * 2 > (size_t)BM * LDC * 2
+                                    ? (size_t)NS * STAGE * 2 : (size_t)BM * LDC * 2;
+};
+
+// SCHED 0: per K-step {wait; barrier; issue next; reads + MFMAs of both 32-deep halves}.
+// SCHED 1 (BK 64, NS 2): fragments double-buffered in registers and the barrier moved between
+// the two halves -- the reads of half 1 fly under the MFMAs of half 0, the reads of the next
+// step's half 0 under the MFMAs of half 1, so no wave waits on LDS latency at a phase start.
+template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8>
+__global__ void __launch_bounds__(NW * 64, 1)
+gemm_nt_kernel(const GemmArgs g) {
+  using Cf = GCfg<BM, BN, BK, NS, NW>;
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cf::WN, wn = wave % Cf::WN;
+  (void)kGT;
+
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int tiles_m = (g.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (g.K + BK - 1) / BK;
+
+  // descriptors based at this block's first row / column: 32-bit offsets span one panel only
+  const int rows_a = min(BM, g.M - m0), rows_b = min(BN, g.N - n0);
+  const i32x4_t ra = rsrc_quad(g.A + (long)m0 * g.lda, (uint32_t)((long)(rows_a - 1) * g.lda + g.K) * 2u);
+  const i32x4_t rb = rsrc_quad(g.B + (long)n0 * g.ldb, (uint32_t)((long)(rows_b - 1) * g.ldb + g.K) * 2u);
+  const uint32_t lds0 = lds_addr(lds);
+
+  // this wave fills DMA row-groups (RPI rows x BK) wave + 8 j of A, then of B
+  const int lrow = lane / Cf::CPR, slot = lane % Cf::CPR;
+  uint32_t a_off[Cf::DA], b_off[Cf::DB];
+  int a_ch[Cf::DA], b_ch[Cf::DB];
+#pragma unroll
+  for (int j = 0; j < Cf::DA; ++j) {
+    const int row = Cf::RPI * (wave + NW * j) + lrow;
+    a_ch[j] = gswz<BK>(row, slot) * 8;
+    a_off[j] = row < rows_a ? (uint32_t)(row * g.lda + a_ch[j]) * 2u : kGOOB;
+  }
+#pragma unroll
+  for (int j = 0; j < Cf::DB; ++j) {
+    const int row = Cf::RPI * (wave + NW * j) + lrow;
+    b_ch[j] = gswz<BK>(row, slot) * 8;
+    b_off[j] = row < rows_b ? (uint32_t)(row * g.ldb + b_ch[j]) * 2u : kGOOB;
+  }
+
+  // steps past the end are issued too, every lane out of range (no traffic): the number of
+  // DMAs in flight behind each step is then a constant and the wait count a literal
+  auto issue = [&](int kt, int stage) {
+    const bool live = kt < nk;
+    const int k0 = (live ? kt : 0) * BK;
+    const uint32_t base = lds0 + (uint32_t)(stage * Cf::STAGE + wave * 512) * 2u;
+#pragma unroll
+    for (int j = 0; j < Cf::DA; ++j) {
+      const bool ok = live && k0 + a_ch[j] < g.K && a_off[j] != kGOOB;
+      dma16(ra, base + j * NW * 1024, ok ? a_off[j] + k0 * 2u : kGOOB);
+    }
+#pragma unroll
+    for (int j = 0; j < Cf::DB; ++j) {
+      const bool ok = live && k0 + b_ch[j] < g.K && b_off[j] != kGOOB;
+      dma16(rb, base + Cf::SA * 2 + j * NW * 1024, ok ? b_off[j] + k0 * 2u : kGOOB);
+    }
+  };
+
+  f32x4_t acc[Cf::FM][Cf::FN];
+#pragma unroll
+  for (int i = 0; i < Cf::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fq = lane >> 4;
+  auto compute = [&](const bf16_t* sa) {
+    const bf16_t* sb = sa + Cf::SA;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8_t af[Cf::FM], bfr[Cf::FN];
+      const int ch = ks * 4 + fq;
+#pragma unroll
+      for (int j = 0; j < Cf::FN; ++j) {
+        const int r = wn * Cf::WTN + j * 16 + frow;
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < Cf::FM; ++i) {
+        const int r = wm * Cf::WTM + i * 16 + frow;
+        af[i] = *reinterpret_cast<const bf16x8_t*>(sa + r * BK + gswz<BK>(r, ch) * 8);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < Cf::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < Cf::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  if constexpr (SCHED == 1) {
+    static_assert(BK == 64 && NS == 2, "SCHED 1: two 32-deep halves per step, two slots");
+    bf16x8_t fa0[Cf::FM], fb0[Cf::FN], fa1[Cf::FM], fb1[Cf::FN];
+    auto rd = [&](bf16x8_t* fa, bf16x8_t* fb, const bf16_t* sa, int ks) {
+      const bf16_t* sb = sa + Cf::SA;
+      const int ch = ks * 4 + fq;
+#pragma unroll
+      for (int j = 0; j < Cf::FN; ++j) {
+        const int r = wn * Cf::WTN + j * 16 + frow;
+        fb[j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < Cf::FM; ++i) {
+        const int r = wm * Cf::WTM + i * 16 + frow;
+        fa[i] = *reinterpret_cast<const bf16x8_t*>(sa + r * BK + gswz<BK>(r, ch) * 8);
+      }
+    };
+    auto mm = [&](const bf16x8_t* fa, const bf16x8_t* fb) {
+#pragma unroll
+      for (int i = 0; i < Cf::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < Cf::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    };
+    issue(0, 0);
+    DTF_WAIT_VM(0);
+    raw_barrier();
+    issue(1, 1);
+    rd(fa0, fb0, lds, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* cur = lds + (kt & 1) * Cf::STAGE;
+      rd(fa1, fb1, cur, 1);
+      mm(fa0, fb0);
+      DTF_WAIT_VM(0);                             // step kt+1 landed (this wave) ...
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();                              // ... every wave's; step kt fully read
+      issue(kt + 2, kt & 1);
+      if (kt + 1 < nk) rd(fa0, fb0, lds + ((kt + 1) & 1) * Cf::STAGE, 0);
+      mm(fa1, fb1);
+    }
+  } else {
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's DMAs of step kt landed (the NS-2 younger steps may still fly) ...
+    wait_vm<(NS - 2) * (Cf::DA + Cf::DB)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();      // ... and every wave's; every wave finished reading step kt-1's slot
+    issue(kt + NS - 1, (kt + NS - 1) % NS);
+    compute(lds + (kt % NS) * Cf::STAGE);
+  }
+  }
+  DTF_WAIT_VM(0);       // the trailing no-op DMAs still target the ring
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();        // all fragment reads done: reuse LDS for C
+
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  float bj[Cf::FN];
+#pragma unroll
+  for (int j = 0; j < Cf::FN; ++j) {
+    const int col = n0 + wn * Cf::WTN + j * 16 + frow;
+    bj[j] = (g.bias && col < g.N) ? g.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < Cf::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * Cf::WTM + i * 16 + fq * 4 + r;
+        const int col = wn * Cf::WTN + j * 16 + frow;
+        float v = acc[i][j][r] + bj[j];
+        if (g.relu) v = fmaxf(v, 0.f);
+        lds[row * Cf::LDC + col] = f2bf(v);
+      }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+  constexpr int OCPR = BN / 8;                 // 16-B chunks per output row
+  constexpr int OROWS = Cf::NT / OCPR;
+  const int oc = tid % OCPR;
+  const bool col_ok = n0 + oc * 8 < g.N;
+#pragma unroll 4
+  for (int k = 0; k < BM / OROWS; ++k) {
+    const int r = tid / OCPR + k * OROWS;
+    if (!col_ok || m0 + r >= g.M) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::LDC + oc * 8);
+    const long off = (long)(m0 + r) * g.ldc + n0 + oc * 8;
+    if (g.Cin) {
+      float a[8], b[8];
+      unpack8(v, a);
+      unpack8(*reinterpret_cast<const uint4*>(g.Cin + off), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+      v = pack8(a);
+    }
+    *reinterpret_cast<uint4*>(g.C + off) = v;
+  }
+}
+
+int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
+
+template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8>
+void launch_gemm(const GemmArgs& g, hipStream_t st) {
+  using Cf = GCfg<BM, BN, BK, NS, NW>;
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cf::LDS));
+    attr = true;
+  }
+  const long tiles = (long)((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW>), dim3((unsigned)tiles), dim3(Cf::NT), Cf::LDS,
+                     st, g);
+}
+
+}  // namespace
+
+void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
+
+void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda,
+                 int ldb, int ldc, const float* bias, const bf16_t* Cin, int relu,
+                 hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0) return;
+  if (K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N)
+    throw std::runtime_error("gemm_nt: K, N and the leading dimensions must be multiples of 8");
+  // the per-block descriptors span at most one 256-row panel
+  if ((long)256 * lda * 2 >= (1L << 32) || (long)256 * ldb * 2 >= (1L << 32))
+    throw std::runtime_error("gemm_nt: leading dimension too large");
+  GemmArgs g{A, B, C, bias, Cin, M, N, K, lda, ldb, ldc, relu};
+  switch (g_gemm_variant < 0 ? 0 : g_gemm_variant) {
+    case 1: launch_gemm<256, 128, 64, 3>(g, st); break;
+    case 2: launch_gemm<256, 256, 32, 4>(g, st); break;
+    case 3: launch_gemm<256, 128, 32, 4>(g, st); break;
+    case 4: launch_gemm<256, 256, 64, 2, 1>(g, st); break;
+    case 5: launch_gemm<256, 256, 64, 2, 0, 4>(g, st); break;
+    case 6: launch_gemm<256, 256, 64, 2, 1, 4>(g, st); break;
+    case 7: launch_gemm<256, 256, 32, 4, 0, 4>(g, st); break;
+    default: launch_gemm<256, 256, 64, 2>(g, st); break;
+  }
+}

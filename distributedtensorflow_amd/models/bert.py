@@ -20,12 +20,20 @@ MI355X layout choices:
 from __future__ import annotations
 
 import dataclasses
+import os
 
 import torch
 import torch.nn as nn
 
 from .. import ops
 from .layers import Layer, _tag, truncated_normal_
+
+
+# BERT's plain GEMMs (bias left to the fused consumer kernels) stay on hipBLASLt by default: on
+# the BERT-base shapes the library kernels run 1.1-1.3x our MFMA GEMM (tools/gemm_bench.py,
+# profiles/measurements/r2_gemm_vs_hipblaslt.jsonl); DTF_BERT_GEMM=native routes them through
+# csrc/kernels/gemm.hip instead.
+BERT_GEMM = os.environ.get("DTF_BERT_GEMM", "library")
 
 
 @dataclasses.dataclass
@@ -73,7 +81,7 @@ class _Dense(nn.Module):
         self.bias = _param((n_out,), f"{name}/bias", fill=0.0)
 
     def gemm(self, x):
-        return ops.dense(x, self.kernel, None)
+        return ops.dense(x, self.kernel, None, impl=BERT_GEMM)
 
 
 class _LayerNorm(nn.Module):
@@ -106,7 +114,7 @@ class BertLayer(nn.Module):
 
     def forward(self, x, mask, B, S):
         cfg = self.cfg
-        qkv = ops.dense(x, self.qkv_kernel, self.qkv_bias)
+        qkv = ops.dense(x, self.qkv_kernel, self.qkv_bias, impl=BERT_GEMM)
         ctx = ops.attention_qkv(qkv, mask, B, S, cfg.num_attention_heads,
                                 cfg.attention_probs_dropout_prob, self.training)
         a = self.attn_out.gemm(ctx)
@@ -185,7 +193,7 @@ class BertForPreTraining(Layer):
         h = ops.bias_gelu(self.mlm_transform.gemm(h), self.mlm_transform.bias)
         h = ops.bias_dropout_add_layer_norm(h, None, None, self.mlm_ln.gamma, self.mlm_ln.beta,
                                             0.0, self.training, cfg.layer_norm_eps)
-        logits = ops.dense(h, self.word_embeddings, self.mlm_bias)     # tied decoder
+        logits = ops.dense(h, self.word_embeddings, self.mlm_bias, impl=BERT_GEMM)  # tied decoder
         if masked_lm_ids is None:
             return logits
         return ops.mlm_loss(logits, masked_lm_ids, masked_lm_weights)

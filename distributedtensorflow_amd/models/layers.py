@@ -122,12 +122,11 @@ class Conv2D(Layer):
             self.bias = None
 
     def forward(self, x):
-        y = ops.conv2d(x, self.kernel, self.strides, self.padding)
-        if self.bias is not None:
-            y = y + self.bias.to(y.dtype)
-        if self.relu:
-            y = ops.relu(y)
-        return y
+        if self.bias is not None or self.relu:
+            # bias + ReLU fused into the conv epilogue on the native path
+            return ops.conv2d_bias_relu(x, self.kernel, self.bias, self.strides, self.padding,
+                                        self.relu)
+        return ops.conv2d(x, self.kernel, self.strides, self.padding)
 
 
 class Dense(Layer):

@@ -63,6 +63,17 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
     return reference.conv2d(x, w, stride, padding)
 
 
+def conv2d_bias_relu(x, w, bias=None, stride=1, padding=0, relu=True):
+    """relu(conv2d(x, w) + bias): tf.layers.conv2d with ``activation=tf.nn.relu``.  Native path:
+    bias and ReLU in the conv kernel's epilogue; backward ReluGrad + BiasAddGrad fused."""
+    if _use_native(x):
+        return _native().conv2d_bias_relu(x, w, bias, stride, padding, relu)
+    y = reference.conv2d(x, w, stride, padding)
+    if bias is not None:
+        y = y + bias.to(y.dtype)
+    return reference.relu(y) if relu else y
+
+
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True,
                momentum=0.997, eps=1e-5, relu=False, residual=None, residual_to_conv=False):
     """``residual_to_conv``: the residual tensor is also the input of a stride-1 conv whose
@@ -104,9 +115,11 @@ def global_avg_pool(x):
     return reference.global_avg_pool(x)
 
 
-def dense(x, w, b=None, relu=False):
+def dense(x, w, b=None, relu=False, impl=None):
+    """``impl`` (native path): None/"native" = the hand-written MFMA GEMM with fused bias/ReLU
+    epilogues; "library" = hipBLASLt (a plain library GEMM, used by BERT by default)."""
     if _use_native(x):
-        return _native().dense(x, w, b, relu)
+        return _native().dense(x, w, b, relu, impl)
     return reference.dense(x, w, b, relu)
 
 
@@ -189,8 +202,8 @@ def mlm_loss(logits, labels, weights=None):
 
 
 __all__ = [
-    "set_backend", "get_backend", "GradShare", "conv2d", "batch_norm", "relu", "max_pool2d",
-    "global_avg_pool", "dense", "sparse_softmax_cross_entropy",
+    "set_backend", "get_backend", "GradShare", "conv2d", "conv2d_bias_relu", "batch_norm", "relu",
+    "max_pool2d", "global_avg_pool", "dense", "sparse_softmax_cross_entropy",
     "softmax_cross_entropy_clipped_sum", "layer_norm", "gelu", "attention", "dropout",
     "bias_dropout_add_layer_norm", "embedding_layer_norm", "bias_gelu", "attention_qkv",
     "mlm_loss",

@@ -27,6 +27,7 @@ except ImportError as e:  # pragma: no cover - exercised on boxes without a buil
         f"Original error: {e}") from e
 
 _BF16 = torch.bfloat16
+_DENSE_IMPL = os.environ.get("DTF_DENSE", "native")     # native | library (hipBLASLt)
 
 # kernel-variant switches for A/B runs on one box (defaults = the measured best)
 if os.environ.get("DTF_WGRAD_MODE"):
@@ -109,7 +110,7 @@ def _fwd_geom(xshape, K, taps, P, Q, sh, sw, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
 
 
 def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
-                stats=None, accumulate=False, bnb=(), acc_from=None):
+                stats=None, accumulate=False, bnb=(), acc_from=None, bias=None, relu=False):
     """wmat: [K, T*C] bf16 (rows zero-padded here to a multiple of 32 for the gather path).
     ``acc_from``: a :class:`_MaskedGrad` the epilogue adds (as dy * mask) instead of reading
     ``out`` back (geom acc mode 2)."""
@@ -131,10 +132,10 @@ def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0
                       _p(stats), list(bnb), acc_from.dy.data_ptr(), acc_from.mask.data_ptr())
         return
     _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
-                  _p(stats), list(bnb))
+                  _p(stats), list(bnb), 0, 0, _p(bias), int(relu))
 
 
-def conv2d_forward(x, w_bf16, stride, padding, stats=None):
+def conv2d_forward(x, w_bf16, stride, padding, stats=None, bias=None, relu=False):
     """x [N,H,W,C] bf16, w [K,R,S,C] bf16 -> y [N,P,Q,K].  ``stats``: fp32 workspace that also
     receives the per-M-tile BatchNorm partial sums of y (see conv2d(bn_stats=True))."""
     K, R, S, C = w_bf16.shape
@@ -142,7 +143,8 @@ def conv2d_forward(x, w_bf16, stride, padding, stats=None):
     assert c == C, (x.shape, w_bf16.shape)
     taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
     y = torch.empty(n, P, Q, K, device=x.device, dtype=_BF16)
-    _launch_fwd(x, w_bf16.reshape(K, R * S * C), K, taps, P, Q, sh, sw, y, P, Q, stats=stats)
+    _launch_fwd(x, w_bf16.reshape(K, R * S * C), K, taps, P, Q, sh, sw, y, P, Q, stats=stats,
+                bias=bias, relu=relu)
     return y
 
 
@@ -386,6 +388,79 @@ class _Conv2d(torch.autograd.Function):
         ctx.x_ref = None
         ctx.bnb = None
         return dx, dw, None, None, None, None
+
+
+class _Conv2dBiasRelu(torch.autograd.Function):
+    """tf.layers.conv2d(..., activation=tf.nn.relu) with the bias add and ReLU in the conv
+    kernel's epilogue (reference ``run_mnist_distributed.py:52-64``).  Backward:
+    ReluGrad + BiasAddGrad in one fused pass over dy (csrc/kernels/dense.hip), then the
+    MFMA weight-gradient (fp32 straight into the flat buffer) and data-gradient kernels."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, b_master, stride, padding, relu):
+        xb = x.contiguous()
+        wb = _bf16_weight(w_master)
+        C = xb.shape[-1]
+        if C % 8:
+            xb, wb = _pad_c8(xb), _pad_c8(wb)
+        bias = b_master.detach().float().contiguous() if b_master is not None else None
+        y = conv2d_forward(xb, wb, stride, padding, bias=bias, relu=relu)
+        ctx.save_for_backward(xb, wb, y if relu else None)
+        ctx.meta = (stride, padding, relu, C)
+        ctx.params = (w_master, b_master)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb, y = ctx.saved_tensors
+        stride, padding, relu, C = ctx.meta
+        w_master, b_master = ctx.params
+        ctx.params = None
+        dy = dy.contiguous()
+        K = dy.shape[-1]
+        M = dy.numel() // K
+        dx = dw = db = None
+        need_b = b_master is not None and ctx.needs_input_grad[2]
+        dz = dy
+        if relu or need_b:
+            dz = torch.empty_like(dy) if relu else dy
+            ws = torch.empty(_K.bias_relu_bwd_ws_floats(K), device=dy.device, dtype=torch.float32)
+            tb = _direct_grad(b_master) if need_b else None
+            dbuf = (tb if tb is not None else torch.empty(K, device=dy.device,
+                                                          dtype=torch.float32)) if need_b else None
+            _K.bias_relu_bwd(dy.data_ptr(), _p(y) if relu else dy.data_ptr(), dz.data_ptr(), M, K,
+                             ws.data_ptr(), _p(dbuf), int(tb is not None), int(relu), _st())
+            if need_b:
+                if tb is not None:
+                    _grad_ready(b_master)
+                else:
+                    db = dbuf.to(b_master.dtype)
+        padded = xb.shape[-1] != C
+        if ctx.needs_input_grad[1]:
+            target = _direct_grad(w_master)
+            if target is not None and not padded:
+                conv2d_wgrad(xb, dz, wb.shape, stride, padding, out=target)
+                _grad_ready(w_master)
+            else:
+                g = conv2d_wgrad(xb, dz, wb.shape, stride, padding)[..., :C]
+                if target is not None:
+                    target.add_(g)
+                    _grad_ready(w_master)
+                else:
+                    dw = g.to(w_master.dtype)
+        if ctx.needs_input_grad[0]:
+            dx = conv2d_dgrad(dz, wb, xb.shape, stride, padding)
+            if padded:
+                dx = dx[..., :C].contiguous()
+        return dx, dw, db, None, None, None
+
+
+def conv2d_bias_relu(x, w, bias=None, stride=1, padding=0, relu=True):
+    _check_cuda_bf16(x)
+    K, R, S, C = w.shape
+    if K % 8 or R * S > 64:
+        raise ValueError(f"native conv2d: unsupported filter {tuple(w.shape)}")
+    return _Conv2dBiasRelu.apply(x, w, bias, stride, padding, bool(relu))
 
 
 _SHARE_INPUT_GRAD = os.environ.get("DTF_SHARE_INPUT_GRAD", "1") == "1"
@@ -788,6 +863,28 @@ def _wgrad_splits(T, o, i):
     return best
 
 
+def gemm_nt(a, b, out=None, bias=None, cin=None, relu=False):
+    """C[M, N] = A[M, K] . B[N, K]^T (+ bias) (ReLU) (+ cin) on the hand-written MFMA GEMM
+    (csrc/kernels/gemm.hip).  A, B bf16 with unit-stride rows; K and N multiples of 8."""
+    _check_cuda_bf16(a, b)
+    a2 = a.reshape(-1, a.shape[-1])
+    if a2.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("gemm_nt: operands need unit-stride rows")
+    M, K = a2.shape
+    N = b.shape[0]
+    if b.shape[1] != K:
+        raise ValueError(f"gemm_nt: K mismatch {tuple(a.shape)} x {tuple(b.shape)}")
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=_BF16)
+    if cin is not None and (cin.shape != out.shape or cin.dtype != _BF16 or not cin.is_contiguous()):
+        raise ValueError("gemm_nt: cin must be a contiguous bf16 [M, N] tensor")
+    if bias is not None:
+        bias = bias.detach().float().contiguous()
+    _K.gemm_nt(a2.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a2.stride(0), b.stride(0),
+               out.stride(0), _p(bias), _p(cin), int(relu), _st())
+    return out
+
+
 class _Dense(torch.autograd.Function):
     """y = x @ W^T (+ b) on hipBLASLt with the bf16 weight shadow; backward produces dW and db in
     fp32 straight into the optimizer's flat gradient buffer (no bf16 dW, no cast/add kernels)."""
@@ -862,9 +959,121 @@ class _Dense(torch.autograd.Function):
         return dx, dw, None, db
 
 
-def dense(x, w, b=None, relu=False):
-    """Plain GEMM -> hipBLASLt (a *library* GEMM per the design rules); the bias stays fused in
-    the GEMM epilogue.  Trainable fp32 masters go through :class:`_Dense` (fp32 dW/db)."""
+def _transposed_bf16(wb):
+    """[o, i] bf16 weight -> contiguous [i, o] (the data-gradient GEMM's B operand): the dense
+    weights are registered with the conv filters in forward, so the first data gradient of the
+    step transposes all of them in ONE batched launch (see _dgrad_filter)."""
+    o, i = wb.shape
+    return _dgrad_filter(wb.view(o, 1, i)).view(i, o)
+
+
+class _NativeDense(torch.autograd.Function):
+    """y = act(x W^T + b) on the hand-written MFMA GEMM (csrc/kernels/gemm.hip) with the bias and
+    ReLU in its epilogue (reference ``tf.layers.dense(..., activation=tf.nn.relu)``,
+    ``run_mnist_distributed.py:67-69``).  Backward: one fused pass for
+    ReluGrad + BiasAddGrad (csrc/kernels/dense.hip), dX on the same GEMM with the transposed
+    weight, dW (fp32, straight into the flat gradient buffer) on the conv weight-gradient
+    kernel's TN form (a 1x1 conv over M = tokens).  Output widths that are not a multiple of 8
+    (the 10-way logits) run zero-padded to the next multiple of 8."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, b_master, relu):
+        wb = _bf16_weight(w_master)
+        o, i = wb.shape
+        x2 = x.reshape(-1, i)
+        x2 = x2 if x2.is_contiguous() else x2.contiguous()
+        op = -(-o // 8) * 8
+        bias = b_master
+        if op != o:
+            wp = torch.zeros(op, i, device=x.device, dtype=_BF16)
+            wp[:o] = wb
+            wb = wp
+            if b_master is not None:
+                bias = torch.zeros(op, device=x.device, dtype=torch.float32)
+                bias[:o] = b_master.detach()
+        elif x.requires_grad and wb.is_contiguous():
+            _register_dgrad_filter(wb.view(o, 1, 1, i))
+        y = gemm_nt(x2, wb, bias=bias, relu=relu)
+        ctx.save_for_backward(x2, wb, y if relu else None)
+        ctx.meta = (o, op, relu, x.shape)
+        ctx.params = (w_master, b_master)
+        ctx.x_ref = x     # a fused LayerNorm may leave d(x) here (residual_to_dense)
+        out = y if op == o else y[:, :o]
+        return out.view(*x.shape[:-1], o)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wb, y = ctx.saved_tensors
+        o, op, relu, xshape = ctx.meta
+        w_master, b_master = ctx.params
+        M, i = x2.shape
+        dy2 = dy.reshape(M, o)
+        if op != o:
+            dp = torch.zeros(M, op, device=dy.device, dtype=_BF16)
+            dp[:, :o] = dy2
+            dy2 = dp
+        dy2 = dy2.contiguous() if dy2.dtype == _BF16 else dy2.to(_BF16).contiguous()
+        dx = dw = db = None
+        need_b = b_master is not None and ctx.needs_input_grad[2]
+        if relu or need_b:
+            dz = torch.empty_like(dy2) if relu else dy2
+            ws = torch.empty(_K.bias_relu_bwd_ws_floats(op), device=dy.device, dtype=torch.float32)
+            tb = _direct_grad(b_master) if need_b and op == o else None
+            dbuf = None
+            if need_b:
+                dbuf = tb if tb is not None else torch.empty(op, device=dy.device,
+                                                             dtype=torch.float32)
+            _K.bias_relu_bwd(dy2.data_ptr(), _p(y) if relu else dy2.data_ptr(), dz.data_ptr(), M,
+                             op, ws.data_ptr(), _p(dbuf), int(tb is not None), int(relu), _st())
+            if need_b:
+                if tb is not None:
+                    _grad_ready(b_master)
+                else:
+                    db = dbuf[:o].to(b_master.dtype)
+        else:
+            dz = dy2
+        if ctx.needs_input_grad[1]:
+            target = _direct_grad(w_master) if op == o else None
+            if target is not None:
+                conv2d_wgrad(x2.view(1, M, 1, i), dz.view(1, M, 1, op), (op, 1, 1, i), 1, 0,
+                             out=target.view(op, 1, 1, i))
+                _grad_ready(w_master)
+            else:
+                dw = conv2d_wgrad(x2.view(1, M, 1, i), dz.view(1, M, 1, op), (op, 1, 1, i), 1,
+                                  0).view(op, i)[:o]
+                tw = _direct_grad(w_master)
+                if tw is not None:
+                    tw.add_(dw)
+                    _grad_ready(w_master)
+                    dw = None
+                else:
+                    dw = dw.to(w_master.dtype)
+        pending = getattr(ctx.x_ref, "_dtf_pending_grad", None)
+        if pending is not None:
+            del ctx.x_ref._dtf_pending_grad
+        ctx.x_ref = None
+        if ctx.needs_input_grad[0]:
+            wt = _transposed_bf16(wb)                     # [i, op]
+            if pending is not None and pending.dtype == _BF16 and pending.is_contiguous():
+                # d(x) = d(residual) + dz W in one GEMM (beta = 1 epilogue)
+                dx = gemm_nt(dz, wt, out=pending.view(M, i), cin=pending.view(M, i)).view(xshape)
+            else:
+                dx = gemm_nt(dz, wt).view(xshape)
+                if pending is not None:
+                    dx = dx + pending.view(xshape)
+        ctx.params = None
+        return dx, dw, db, None
+
+
+def dense(x, w, b=None, relu=False, impl=None):
+    """Dense layer.  ``impl``: "native" (default; the hand-written MFMA GEMM with fused
+    bias / ReLU epilogues) or "library" (hipBLASLt; kept for BERT's plain GEMMs, where the
+    library kernels are still faster -- tools/gemm_bench.py -- and the task rules allow plain
+    library GEMMs).  Trainable fp32 masters get fp32 dW / db straight in the flat buffer."""
+    impl = impl or _DENSE_IMPL
+    if (impl == "native" and w.dtype == torch.float32 and x.dtype == _BF16 and x.is_cuda
+            and w.dim() == 2 and x.shape[-1] % 8 == 0):
+        return _NativeDense.apply(x, w, b, bool(relu))
     if w.dtype == torch.float32 and x.dtype == _BF16 and w.requires_grad and x.is_cuda:
         y = _Dense.apply(x, w, _bf16_weight(w), b)
         return torch.relu(y) if relu else y
