@@ -146,6 +146,23 @@ void dtf_gemm_nt(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int,
                  const float*, const bf16_t*, int, hipStream_t);
 void dtf_gemm_set_variant(int);
 int dtf_bias_relu_bwd_ws_floats(int);
+void dtf_gather_u8_scale(const uint8_t*, const int64_t*, void*, int, int, float, int, hipStream_t);
+// ---- fp32 path (f32.hip)
+void dtf_gemm_f32(const float*, const float*, float*, const float*, int, int, int, long, long,
+                  long, long, long, long, float, int, int, float*, hipStream_t);
+int dtf_gemm_f32_splits(int, int, int);
+void dtf_im2col_f32(const float*, float*, int, int, int, int, int, int, int, int, int, int, int,
+                    int, hipStream_t);
+void dtf_col2im_f32(const float*, float*, int, int, int, int, int, int, int, int, int, int, int,
+                    int, hipStream_t);
+void dtf_maxpool_f32_fwd(const float*, float*, uint8_t*, int, int, int, int, int, int, int, int,
+                         hipStream_t);
+void dtf_maxpool_f32_bwd(const float*, const uint8_t*, float*, int, int, int, int, int, int, int,
+                         int, hipStream_t);
+int dtf_bias_relu_bwd_f32_ws_floats(int);
+void dtf_bias_relu_bwd_f32(const float*, const float*, float*, int, int, float*, float*, int, int,
+                           hipStream_t);
+void dtf_clipped_xent(const float*, const float*, int, int, float*, float*, float, hipStream_t);
 void dtf_bias_relu_bwd(const bf16_t*, const bf16_t*, bf16_t*, int, int, float*, float*, int, int,
                        hipStream_t);
 
@@ -224,6 +241,52 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("gemm_set_variant", &dtf_gemm_set_variant);
   m.def("bias_relu_bwd_ws_floats", &dtf_bias_relu_bwd_ws_floats);
+  m.def("gather_u8_scale", [](uintptr_t images, uintptr_t idx, uintptr_t out, int B, int D,
+                              float scale, int out_bf16, uintptr_t st) {
+    dtf_gather_u8_scale(P<uint8_t>(images), P<int64_t>(idx), P<void>(out), B, D, scale, out_bf16,
+                        S(st));
+    check_launch("gather_u8_scale");
+  });
+  m.def("gemm_f32_splits", &dtf_gemm_f32_splits);
+  m.def("gemm_f32", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t bias, int M, int N, int K,
+                       long sam, long sak, long sbn, long sbk, long scm, long scn, float alpha,
+                       int relu, int accumulate, uintptr_t ws, uintptr_t st) {
+    dtf_gemm_f32(P<float>(a), P<float>(b), P<float>(c), P<float>(bias), M, N, K, sam, sak, sbn,
+                 sbk, scm, scn, alpha, relu, accumulate, P<float>(ws), S(st));
+    check_launch("gemm_f32");
+  });
+  m.def("im2col_f32", [](uintptr_t x, uintptr_t cols, int N, int H, int W, int C, int P_, int Q,
+                         int sh, int sw, int R, int S_, int pt, int pl, uintptr_t st) {
+    dtf_im2col_f32(P<float>(x), P<float>(cols), N, H, W, C, P_, Q, sh, sw, R, S_, pt, pl, S(st));
+    check_launch("im2col_f32");
+  });
+  m.def("col2im_f32", [](uintptr_t dc, uintptr_t dx, int N, int H, int W, int C, int P_, int Q,
+                         int sh, int sw, int R, int S_, int pt, int pl, uintptr_t st) {
+    dtf_col2im_f32(P<float>(dc), P<float>(dx), N, H, W, C, P_, Q, sh, sw, R, S_, pt, pl, S(st));
+    check_launch("col2im_f32");
+  });
+  m.def("maxpool_f32_fwd", [](uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W, int C,
+                              int P_, int Q, int k, int s, uintptr_t st) {
+    dtf_maxpool_f32_fwd(P<float>(x), P<float>(y), P<uint8_t>(arg), N, H, W, C, P_, Q, k, s, S(st));
+    check_launch("maxpool_f32_fwd");
+  });
+  m.def("maxpool_f32_bwd", [](uintptr_t dy, uintptr_t arg, uintptr_t dx, int N, int H, int W,
+                              int C, int P_, int Q, int k, int s, uintptr_t st) {
+    dtf_maxpool_f32_bwd(P<float>(dy), P<uint8_t>(arg), P<float>(dx), N, H, W, C, P_, Q, k, s, S(st));
+    check_launch("maxpool_f32_bwd");
+  });
+  m.def("bias_relu_bwd_f32_ws_floats", &dtf_bias_relu_bwd_f32_ws_floats);
+  m.def("bias_relu_bwd_f32", [](uintptr_t dy, uintptr_t y, uintptr_t dz, int T, int N,
+                                uintptr_t ws, uintptr_t db, int accumulate, int relu, uintptr_t st) {
+    dtf_bias_relu_bwd_f32(P<float>(dy), P<float>(y), P<float>(dz), T, N, P<float>(ws),
+                          P<float>(db), accumulate, relu, S(st));
+    check_launch("bias_relu_bwd_f32");
+  });
+  m.def("clipped_xent", [](uintptr_t z, uintptr_t t, int B, int V, uintptr_t rows, uintptr_t dz,
+                           float scale, uintptr_t st) {
+    dtf_clipped_xent(P<float>(z), P<float>(t), B, V, P<float>(rows), P<float>(dz), scale, S(st));
+    check_launch("clipped_xent");
+  });
   m.def("bias_relu_bwd", [](uintptr_t dy, uintptr_t y, uintptr_t dz, int T, int N, uintptr_t ws,
                             uintptr_t db, int accumulate, int relu, uintptr_t st) {
     dtf_bias_relu_bwd(P<bf16_t>(dy), P<bf16_t>(y), P<bf16_t>(dz), T, N, P<float>(ws), P<float>(db),

@@ -100,3 +100,47 @@ void dtf_bias_relu_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dz, int T, int
     hipLaunchKernelGGL(col_slices_final_kernel, dim3((N + 15) / 16), dim3(256), 0, st, ws, S, N,
                        db, accumulate);
 }
+
+// ---- the input pipeline's DecodeRaw u8 -> float / 255 fused into the batch gather of
+// an HBM-resident dataset (data/device.py): out[b, :] = images[idx[b], :] * scale, written as
+// bf16 or fp32.  One thread per 8 bytes (an 8-byte load, a 16-/32-byte store).
+namespace {
+template <typename OutT>
+__global__ void __launch_bounds__(256)
+gather_u8_scale_kernel(const uint8_t* __restrict__ images, const int64_t* __restrict__ idx,
+                       OutT* __restrict__ out, int B, int D, float scale) {
+  const int per_row = D / 8;
+  const long total = (long)B * per_row;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+    const int b = (int)(t / per_row), c8 = (int)(t - (long)b * per_row);
+    const uint2 v = *reinterpret_cast<const uint2*>(images + idx[b] * (long)D + c8 * 8);
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[e] = (float)((v.x >> (8 * e)) & 0xFFu) * scale;
+      f[4 + e] = (float)((v.y >> (8 * e)) & 0xFFu) * scale;
+    }
+    if constexpr (sizeof(OutT) == 2) {
+      *reinterpret_cast<uint4*>(out + (long)b * D + c8 * 8) = pack8(f);
+    } else {
+      float4* o = reinterpret_cast<float4*>(out + (long)b * D + c8 * 8);
+      o[0] = make_float4(f[0], f[1], f[2], f[3]);
+      o[1] = make_float4(f[4], f[5], f[6], f[7]);
+    }
+  }
+}
+}  // namespace
+
+void dtf_gather_u8_scale(const uint8_t* images, const int64_t* idx, void* out, int B, int D,
+                         float scale, int out_bf16, hipStream_t st) {
+  if (D % 8) throw std::runtime_error("gather_u8_scale: row bytes % 8 != 0");
+  const long total = (long)B * (D / 8);
+  const int grid = (int)((total + 255) / 256 > 65536 ? 65536 : (total + 255) / 256);
+  if (total <= 0) return;
+  if (out_bf16)
+    hipLaunchKernelGGL(gather_u8_scale_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, images, idx,
+                       static_cast<bf16_t*>(out), B, D, scale);
+  else
+    hipLaunchKernelGGL(gather_u8_scale_kernel<float>, dim3(grid), dim3(256), 0, st, images, idx,
+                       static_cast<float*>(out), B, D, scale);
+}

@@ -61,6 +61,18 @@ class DeviceArrayDataset:
         return self._gather(idx)
 
     def _gather(self, idx):
+        if (self.device.type == "cuda" and self.images.dtype == torch.uint8
+                and self.dtype in (torch.bfloat16, torch.float32)
+                and (self.images[0].numel() % 8) == 0):
+            # u8 decode + /255 fused into the gather, one HIP kernel per batch
+            from ..ops import native
+            B = idx.numel()
+            x = torch.empty(B, *self.images.shape[1:], device=self.device, dtype=self.dtype)
+            native.kernels().gather_u8_scale(
+                self.images.data_ptr(), idx.contiguous().data_ptr(), x.data_ptr(), B,
+                self.images[0].numel(), float(self.scale), int(self.dtype == torch.bfloat16),
+                torch.cuda.current_stream().cuda_stream)
+            return x, self.labels.index_select(0, idx)
         x = self.images.index_select(0, idx).to(self.dtype)
         if self.scale != 1.0:
             x = x * self.scale

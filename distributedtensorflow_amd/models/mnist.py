@@ -53,6 +53,9 @@ class MnistMLP(Layer):
         self.sm_b = _tag(nn.Parameter(torch.zeros(num_classes)), "sm_b")
 
     def forward(self, x):
-        """Returns logits; the template applies softmax + clipped-log loss on top."""
-        h = torch.relu(x.float() @ self.hid_w + self.hid_b)   # tf.nn.xw_plus_b + relu
-        return h @ self.sm_w + self.sm_b
+        """Returns logits; the template applies softmax + clipped-log loss on top.  fp32 like
+        the template; on the GPU both ``tf.nn.xw_plus_b`` GEMMs (+ReLU) run on the f32 MFMA
+        kernel with the bias / ReLU in its epilogue."""
+        x = x.float()
+        h = ops.dense(x, self.hid_w, self.hid_b, relu=True, layout="IO")
+        return ops.dense(h, self.sm_w, self.sm_b, layout="IO")

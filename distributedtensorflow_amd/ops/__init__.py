@@ -42,6 +42,17 @@ def _native():
     return native
 
 
+def _f32(t: torch.Tensor) -> bool:
+    """fp32 GPU tensors run the fp32 HIP kernels (csrc/kernels/f32.hip): the reference
+    workload at the reference's precision."""
+    return _use_native(t) and t.dtype == torch.float32
+
+
+def _native_f32():
+    from . import native_f32
+    return native_f32
+
+
 class GradShare:
     """Marks the convs that read ONE input tensor (a projection block's x feeds both the 1x1
     shortcut conv and c1): on the native path their data gradients accumulate into one buffer
@@ -58,6 +69,8 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
     """``bn_stats``: a training-mode batch_norm consumes the result (native path fuses the BN
     statistics into the conv epilogue; ignored by the reference path).  ``grad_share``: a
     :class:`GradShare` common to every conv reading ``x`` (native path only)."""
+    if _f32(x):
+        return _native_f32().conv2d(x, w, stride, padding)
     if _use_native(x):
         return _native().conv2d(x, w, stride, padding, bn_stats, grad_share)
     return reference.conv2d(x, w, stride, padding)
@@ -66,6 +79,8 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
 def conv2d_bias_relu(x, w, bias=None, stride=1, padding=0, relu=True):
     """relu(conv2d(x, w) + bias): tf.layers.conv2d with ``activation=tf.nn.relu``.  Native path:
     bias and ReLU in the conv kernel's epilogue; backward ReluGrad + BiasAddGrad fused."""
+    if _f32(x):
+        return _native_f32().conv2d_bias_relu(x, w, bias, stride, padding, relu)
     if _use_native(x):
         return _native().conv2d_bias_relu(x, w, bias, stride, padding, relu)
     y = reference.conv2d(x, w, stride, padding)
@@ -104,6 +119,8 @@ def relu(x):
 
 
 def max_pool2d(x, kernel=2, stride=2, padding=0):
+    if _f32(x):
+        return _native_f32().max_pool2d(x, kernel, stride, padding)
     if _use_native(x):
         return _native().max_pool2d(x, kernel, stride, padding)
     return reference.max_pool2d(x, kernel, stride, padding)
@@ -115,9 +132,17 @@ def global_avg_pool(x):
     return reference.global_avg_pool(x)
 
 
-def dense(x, w, b=None, relu=False, impl=None):
+def dense(x, w, b=None, relu=False, impl=None, layout="OI"):
     """``impl`` (native path): None/"native" = the hand-written MFMA GEMM with fused bias/ReLU
-    epilogues; "library" = hipBLASLt (a plain library GEMM, used by BERT by default)."""
+    epilogues; "library" = hipBLASLt (a plain library GEMM, used by BERT by default).
+    ``layout``: "OI" (kernel [out, in], tf.layers / BERT) or "IO" ([in, out], the MLP template's
+    ``tf.nn.xw_plus_b`` weights)."""
+    if _f32(x):
+        return _native_f32().dense(x, w, b, relu, layout)
+    if layout == "IO":
+        w = w.t()
+        if _use_native(x):
+            w = w.contiguous()
     if _use_native(x):
         return _native().dense(x, w, b, relu, impl)
     return reference.dense(x, w, b, relu)
@@ -130,6 +155,9 @@ def sparse_softmax_cross_entropy(logits, labels):
 
 
 def softmax_cross_entropy_clipped_sum(logits, onehot):
+    """The MLP template's loss (templates/00_mnist_replica.py:160-164), a batch SUM."""
+    if _use_native(logits):
+        return _native_f32().softmax_cross_entropy_clipped_sum(logits, onehot)
     return reference.softmax_cross_entropy_clipped_sum(logits, onehot)
 
 

@@ -117,6 +117,8 @@ class Optimizer:
         self._nonfinite = None
         self._reducer = None
         self.use_locking = use_locking
+        # bf16 compute shadow of the fp32 masters ("auto": on GPUs); None for fp32-compute models
+        self.shadow_dtype = "auto"
 
     # ------------------------------------------------------------------ hyper-parameters
     def learning_rate(self, step=None):
@@ -130,7 +132,8 @@ class Optimizer:
         from ..parallel import strategy as _strat
         variables = list(variables)
         dev = variables[0].device
-        shadow = torch.bfloat16 if dev.type == "cuda" else None
+        shadow = (torch.bfloat16 if dev.type == "cuda" else None) if self.shadow_dtype == "auto" \
+            else self.shadow_dtype
         self.space = FlatSpace(variables, self.decay_filter, shadow)
         self._build_slots()
         self._lr_dev = torch.zeros(4, device=dev, dtype=torch.float32)

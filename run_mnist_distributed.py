@@ -75,20 +75,30 @@ def main():
         device = torch.device("cuda", FLAGS.task_index % ndev)   # task_index % num_gpus (R7)
     else:
         device = torch.device("cpu")
-    dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+    if FLAGS.dtype == "auto":
+        dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+    else:   # fp32 = the reference's own precision (dataset.py:93-95, tf.layers default dtype)
+        dtype = torch.bfloat16 if FLAGS.dtype == "bf16" else torch.float32
 
-    # input pipeline: ds.repeat().batch(128).prefetch(...) (reference :77-85); HBM-resident
+    # input pipeline: ds.repeat().batch(128).prefetch(...) (reference :77-85) -- same order, no
+    # shuffle, every worker the same batches; on a GPU the whole uint8 set lives in HBM and each
+    # batch is one fused gather + u8->float/255 kernel (data/device.py), no per-step H2D copy
     batch_size = FLAGS.batch_size
     imgs, labels = mnist.load_arrays(FLAGS.data_dir, "train")
-    ds = (dtf.data.Dataset.from_tensor_slices((imgs, labels))
-          .repeat().batch(batch_size).prefetch(4))
-    it = iter(ds)
+    if device.type == "cuda":
+        it = dtf.data.DeviceArrayDataset(imgs, labels, batch_size, device, dtype=dtype)
+    else:
+        ds = (dtf.data.Dataset.from_tensor_slices((imgs, labels))
+              .repeat().batch(batch_size).prefetch(4))
+        it = iter(ds)
 
     strategy = ParameterServerStrategy(server=server, sync=FLAGS.sync_replicas, device=device,
                                        data_plane=FLAGS.data_plane)
     with strategy.scope():
         model = MnistCNN()
         opt = dtf.train.AdamOptimizer(FLAGS.learning_rate)
+        if dtype == torch.float32:
+            opt.shadow_dtype = None          # fp32 compute reads the fp32 masters directly
         if FLAGS.sync_replicas:
             opt = dtf.train.SyncReplicasOptimizer(opt, replicas_to_aggregate=len(worker_hosts),
                                                   total_num_replicas=len(worker_hosts))
@@ -97,8 +107,9 @@ def main():
 
     def train_op():
         x, y = next(it)
-        x = torch.as_tensor(x).to(device, non_blocking=True).to(dtype) / 255.0
-        y = torch.as_tensor(y).to(device, non_blocking=True).long()
+        if device.type != "cuda":
+            x = torch.as_tensor(x).to(dtype) / 255.0
+            y = torch.as_tensor(y).long()
         loss = ops.sparse_softmax_cross_entropy(model(x), y)
         opt.minimize(loss, global_step=global_step)
         return {"loss": loss}
@@ -155,6 +166,9 @@ def parse(argv=None):
     parser.add_argument("--checkpoint_dir", default=None)
     parser.add_argument("--sync_replicas", action="store_true")
     parser.add_argument("--device", choices=("auto", "cpu", "gpu"), default="auto")
+    parser.add_argument("--dtype", choices=("auto", "bf16", "fp32"), default="auto",
+                        help="compute dtype: fp32 = the reference's precision (f32 MFMA kernels); "
+                             "auto = bf16 on GPUs, fp32 on CPUs")
     parser.add_argument("--ps_device", choices=("auto", "cpu", "gpu"), default="auto",
                         help="where a ps task keeps its variable shard (auto: its GPU's HBM)")
     parser.add_argument("--data_plane", choices=("auto", "ipc", "shm", "gloo"), default=None,

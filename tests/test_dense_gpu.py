@@ -118,3 +118,107 @@ def test_mnist_cnn_trains_on_native_kernels():
         opt.minimize(loss)
         losses.append(float(loss))
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+# ----------------------------------------------------------------------------- fp32 path
+def _rel64(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("layout", ["OI", "IO"])
+def test_fp32_dense_fwd_bwd(layout):
+    """f32-input MFMA GEMM (exact fp32 fma chains): tight agreement with fp64."""
+    from distributedtensorflow_amd.ops import native_f32
+    g = torch.Generator(device="cuda").manual_seed(5)
+    M, i, o = 128, 784, 100
+    x = torch.randn(M, i, device="cuda", generator=g).requires_grad_()
+    w = torch.randn(*((o, i) if layout == "OI" else (i, o)), device="cuda", generator=g)
+    w = (w / i ** 0.5).requires_grad_()
+    b = torch.randn(o, device="cuda", generator=g).requires_grad_()
+    y = native_f32.dense(x, w, b, True, layout)
+    dy = torch.randn(M, o, device="cuda", generator=g)
+    y.backward(dy)
+    xr, wr, br = (t.detach().double().requires_grad_() for t in (x, w, b))
+    yr = torch.relu(xr @ (wr.t() if layout == "OI" else wr) + br)
+    yr.backward(dy.double())
+    assert _rel64(y, yr) < 1e-5
+    for got, ref in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert _rel64(got, ref) < 1e-5
+
+
+@pytest.mark.parametrize("C,K,H", [(1, 32, 28), (32, 64, 14)])
+def test_fp32_conv_bias_relu_and_pool(C, K, H):
+    from distributedtensorflow_amd.ops import native_f32
+    g = torch.Generator(device="cuda").manual_seed(C + K)
+    x = torch.randn(8, H, H, C, device="cuda", generator=g).requires_grad_()
+    w = (torch.randn(K, 5, 5, C, device="cuda", generator=g) * 0.1).requires_grad_()
+    b = (torch.randn(K, device="cuda", generator=g) * 0.1).requires_grad_()
+    y = native_f32.max_pool2d(native_f32.conv2d_bias_relu(x, w, b, 1, "same", True), 2, 2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().double().requires_grad_() for t in (x, w, b))
+    conv = torch.nn.functional.conv2d(xr.permute(0, 3, 1, 2), wr.permute(0, 3, 1, 2), br,
+                                      padding=2)
+    yr = torch.nn.functional.max_pool2d(torch.relu(conv), 2, 2).permute(0, 2, 3, 1)
+    yr.backward(dy.double())
+    assert _rel64(y, yr) < 1e-5
+    for got, ref in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert _rel64(got, ref) < 1e-5
+
+
+def test_clipped_softmax_xent_matches_reference_formula():
+    """templates/00_mnist_replica.py:160-164 loss and its TF gradient (clip passes inside)."""
+    from distributedtensorflow_amd.ops import native_f32, reference
+    g = torch.Generator(device="cuda").manual_seed(9)
+    z = (torch.randn(100, 10, device="cuda", generator=g) * 3).requires_grad_()
+    t = torch.nn.functional.one_hot(torch.randint(0, 10, (100,), device="cuda", generator=g),
+                                    10).float()
+    loss = native_f32.softmax_cross_entropy_clipped_sum(z, t)
+    loss.backward()
+    zr = z.detach().double().requires_grad_()
+    lr = reference.softmax_cross_entropy_clipped_sum(zr, t.double())
+    lr.backward()
+    assert abs(float(loss) - float(lr)) < 1e-4 * abs(float(lr))
+    assert _rel64(z.grad, zr.grad) < 1e-5
+
+
+def test_fused_u8_gather_normalise():
+    from distributedtensorflow_amd.data import DeviceArrayDataset
+    import numpy as np
+    rng = np.random.default_rng(0)
+    imgs = rng.integers(0, 256, (300, 784), dtype=np.uint8)
+    labs = rng.integers(0, 10, 300).astype(np.int32)
+    for dt in (torch.float32, torch.bfloat16):
+        ds = DeviceArrayDataset(imgs, labs, 128, "cuda", dtype=dt, shuffle=True, seed=3)
+        x, y = next(ds)
+        idx = ds._order[:128]
+        ref = torch.as_tensor(imgs, device="cuda")[idx].float() / 255.0
+        assert torch.equal(x, ref.to(dt)) and torch.equal(y, ds.labels[idx])
+
+
+def test_mnist_cnn_and_mlp_train_fp32_on_native_kernels():
+    import distributedtensorflow_amd as dtf
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.models import MnistCNN, MnistMLP
+    from distributedtensorflow_amd.parallel import OneDeviceStrategy
+    torch.manual_seed(0)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.rand(128, 784, device="cuda", generator=g)
+    y = torch.randint(0, 10, (128,), device="cuda", generator=g)
+    with OneDeviceStrategy("/gpu:0").scope():
+        cnn, mlp = MnistCNN(), MnistMLP()
+        o1, o2 = dtf.train.AdamOptimizer(1e-3), dtf.train.AdamOptimizer(1e-3)
+        o1.shadow_dtype = o2.shadow_dtype = None
+        o1.build(list(cnn.parameters()))
+        o2.build(list(mlp.parameters()))
+    assert o1.space.shadow is None
+    onehot = torch.nn.functional.one_hot(y, 10).float()
+    l1, l2 = [], []
+    for _ in range(30):
+        loss = ops.sparse_softmax_cross_entropy(cnn(x), y)
+        o1.minimize(loss)
+        l1.append(float(loss))
+        loss2 = ops.softmax_cross_entropy_clipped_sum(mlp(x), onehot)
+        o2.minimize(loss2)
+        l2.append(float(loss2))
+    assert l1[-1] < 0.6 * l1[0] and l2[-1] < 0.7 * l2[0], (l1, l2)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # The reference's own workload (run_mnist_distributed.py: MNIST CNN, batch 128, Adam 5e-4, async
-# PS, 1000 global steps) timed end to end on the GPU box.  PLANES: ipc = PS shard in HBM, workers
+# PS, 1000 global steps) timed end to end on the GPU box (EXTRA="--dtype fp32" = reference precision).  PLANES: ipc = PS shard in HBM, workers
 # push/pull through hipIpc mappings (default); gloo = round-1 host path (PS on the CPU, tensors
 # over TCP).
 R="${GRAFT_REPO_ROOT:-/root/repo}"
