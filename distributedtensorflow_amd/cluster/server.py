@@ -10,6 +10,14 @@ protocol (any-source receives); GPU workers additionally get an RCCL group among
 ``join()`` on a ``ps`` task runs the parameter-server service and RETURNS cleanly when all
 workers are done, on SIGINT/SIGTERM or on the chief's shutdown request (the reference's PS never
 exits: ``README.md:7`` TODO).
+
+Recovery (TF's ``_RecoverableSession`` recreating the session after a PS restart, reference
+``run_mnist_distributed.py:146``): the rendezvous TCPStore is created once by the
+chief and outlives process groups.  Every (re)join of a rank bumps that rank's join counter in the
+store and uses it as the GENERATION of the process group it joins (``PrefixStore("g<n>")``): a
+PS task restarted by the launcher after a crash is a new process whose first join is its rank's
+second, so it meets the surviving tasks -- which called :meth:`restart_group` when they saw the
+failure -- in generation 1 without any extra coordination.
 """
 from __future__ import annotations
 
@@ -39,6 +47,8 @@ class Server:
         self.timeout_s = timeout_s
         self.ps_device = ps_device
         self.worker_group = None
+        self.store = None
+        self.generation = -1
         self._started = False
         if start:
             self.start()
@@ -69,9 +79,16 @@ class Server:
         if self._started:
             return
         if not dist.is_initialized():
+            if self.store is None:
+                # the chief hosts the store; every other task (and a restarted one) connects
+                self.store = dist.TCPStore(self.host, self.port, None, self.rank == 0,
+                                           timeout=datetime.timedelta(seconds=self.timeout_s),
+                                           wait_for_workers=False)
+            self.generation = int(self.store.add(f"dtf/join/{self.rank}", 1)) - 1
             dist.init_process_group(
-                "gloo", init_method=f"tcp://{self.host}:{self.port}", rank=self.rank,
-                world_size=self.world_size, timeout=datetime.timedelta(seconds=self.timeout_s))
+                "gloo", store=dist.PrefixStore(f"g{self.generation}", self.store),
+                rank=self.rank, world_size=self.world_size,
+                timeout=datetime.timedelta(seconds=self.timeout_s))
         wb = self.worker_backend
         if wb is None:
             wb = "gloo"
@@ -87,6 +104,19 @@ class Server:
         svc = ParameterServerService(self.task_index, self.worker_ranks(), device=self.ps_device)
         stats = svc.serve()
         return stats
+
+    def restart_group(self):
+        """Tear down this generation's process group (a peer died) and join the next one; blocks
+        until every task -- including the restarted one -- has joined."""
+        if dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:           # the group may already be broken
+                pass
+        self._started = False
+        self.worker_group = None
+        self.start()
+        return self.generation
 
     def shutdown(self):
         if dist.is_initialized():

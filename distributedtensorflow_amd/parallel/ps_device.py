@@ -225,6 +225,7 @@ class OwnerShard:
         self.space = LayoutSpace(self.master, self.names, self.shapes, offsets, spec["decay"])
         self.params = self.space.order
         self.opt = _make_optimizer(spec["optimizer"], self.space)
+        self.opt.iterations = int(spec.get("iterations", spec.get("global_step", 0)))
         self.sync = bool(spec.get("sync", False))
         self.replicas_to_aggregate = int(spec.get("replicas_to_aggregate") or nw)
         self.global_step = int(spec.get("global_step", 0))
@@ -246,7 +247,7 @@ class OwnerShard:
         return {"plane": "ipc" if self.master_desc["kind"] == "ipc" else "shm",
                 "master": self.master_desc, "mail": self.mail_desc, "numel": self.numel,
                 "ctl": self.ctl_name, "workers": self.worker_ranks,
-                "global_step": self.global_step}
+                "global_step": self.global_step, "pid": os.getpid()}
 
     # -- control-plane API shared with ps_service._Shard
     def flat_values(self):
@@ -261,6 +262,14 @@ class OwnerShard:
             self.ctl.global_step = self.global_step
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
+
+    def load_slot(self, name, flat):
+        """Restore one optimizer slot (e.g. ``Adam``) from an unpadded flat of the shard's
+        variables (checkpoint restore after a PS restart)."""
+        slot = next(s for s in self.opt.slots if s.name == name)
+        with self.lock, torch.no_grad():
+            for p, v in zip(self.params, _split(flat, self.shapes)):
+                self.space.view_of(slot.buf, p).copy_(v.to(slot.buf.device))
 
     def worker_stopped(self, worker_rank):
         with self.lock:
@@ -321,6 +330,14 @@ class OwnerShard:
         self.stats["applied"] += 1
         self.stats["apply_s"] += time.perf_counter() - t0
 
+    def _maybe_fault(self):
+        """DTF_FAULT_KILL_PS_AT_STEP=n (tests): this PS task dies (SIGKILL, no cleanup, like a
+        preempted host) once its global step reaches n -- only in the first incarnation."""
+        n = int(os.environ.get("DTF_FAULT_KILL_PS_AT_STEP", "0") or 0)
+        if n and self.global_step >= n and not int(os.environ.get("DTF_RESTART_COUNT", "0")):
+            import signal
+            os.kill(os.getpid(), signal.SIGKILL)
+
     def _on_push(self, w, step):
         with self.lock:
             self.stats["pushes"] += 1
@@ -328,6 +345,7 @@ class OwnerShard:
                 self._run_apply(self._slot(w), 1.0)
                 self.global_step += 1
                 self.ctl.global_step = self.global_step
+                self._maybe_fault()
                 self.ctl.done(w, self.global_step)
                 return
             if step < self.global_step:                  # stale gradient: drop, release now
@@ -405,13 +423,35 @@ class PSLink:
     def post(self, step):
         self.ctl.post(self.w, int(step))
 
+    def _owner_alive(self):
+        pid = self.desc.get("pid")
+        if not pid:
+            return True
+        try:
+            os.kill(int(pid), 0)          # same host: signal 0 probes the PS task
+            return True
+        except ProcessLookupError:
+            return False
+        except PermissionError:
+            return True
+
     def wait(self):
-        r = self.ctl.wait_done(self.w, self.timeout_ms)
-        if r is None:
-            raise ConnectionError(f"parameter server {self.ps_index} did not answer within "
-                                  f"{self.timeout_ms / 1000:.0f} s (heartbeat "
-                                  f"{self.ctl.heartbeat})")
-        return int(r)
+        """The owner's answer (new global step).  Sleeps on the futex in 200 ms slices and
+        probes the owner process between them, so a dead PS surfaces as ConnectionError at once
+        (MonitoredTrainingSession recovers from it) instead of after the full timeout."""
+        waited = 0
+        while True:
+            r = self.ctl.wait_done(self.w, 200)
+            if r is not None:
+                return int(r)
+            waited += 200
+            if not self._owner_alive():
+                raise ConnectionError(f"parameter server {self.ps_index} (pid "
+                                      f"{self.desc.get('pid')}) died")
+            if waited >= self.timeout_ms:
+                raise ConnectionError(f"parameter server {self.ps_index} did not answer within "
+                                      f"{self.timeout_ms / 1000:.0f} s (heartbeat "
+                                      f"{self.ctl.heartbeat})")
 
     def pull(self, space):
         for wo, oo, n in self.plan["segments"]:

@@ -119,7 +119,14 @@ class _Shard:
         from ..parallel import strategy as _st
         with _st.OneDeviceStrategy(device).scope():
             self.opt.build(self.params)
+        self.opt.iterations = int(spec.get("iterations", spec.get("global_step", 0)))
         self.lock = threading.Lock()
+
+    def load_slot(self, name, flat):
+        slot = next(s for s in self.opt.slots if s.name == name)
+        with self.lock, torch.no_grad():
+            for p, v in zip(self.params, _split(flat, self.shapes)):
+                self.opt.space.view_of(slot.buf, p).copy_(v.to(slot.buf.device))
 
     def flat_values(self):
         return torch.cat([p.detach().reshape(-1) for p in self.params]).cpu() if self.params \
@@ -235,12 +242,20 @@ class ParameterServerService:
                                              len(self.worker_ranks))
             self.global_step = int(spec.get("global_step", 0))
             self.plane = choose_plane(spec.get("data_plane", "gloo"), self.device)
+            slot_vals = {}
+            for sname in spec.get("slot_values", []):   # restored optimizer slots
+                t = torch.zeros(vals.numel(), dtype=torch.float32)
+                dist.recv(t, src, group=self.group)
+                slot_vals[sname] = t
             if self.plane == "gloo":
                 self.shard = _Shard(spec, vals, self.device)
             else:
                 from .ps_device import OwnerShard
                 self.shard = OwnerShard(spec, vals, self.device, self.worker_ranks,
                                         self.ps_index)
+            for sname, t in slot_vals.items():
+                self.shard.load_slot(sname, t)
+            if self.plane != "gloo":
                 self.shard.start()
             for w in self.waiting_ready:
                 self._ready_reply(w)
@@ -385,7 +400,9 @@ class PSClient:
         return "gloo" if not self.links else self.links[0].desc.get("plane", "?")
 
     def register(self, params, optimizer_cfg, names=None, sync=False, replicas_to_aggregate=None,
-                 global_step=0):
+                 global_step=0, slots=None, iterations=None):
+        """Chief: ship each shard's variables (and, on a restore, its optimizer slots:
+        ``slots = {name: per-variable tensors aligned with params}``) to its PS."""
         self._layout(params)
         for k, rank in enumerate(self.ps_ranks):
             idx = self.by_ps[k]
@@ -394,7 +411,9 @@ class PSClient:
                     "shapes": [list(self.params[i].shape) for i in idx],
                     "optimizer": optimizer_cfg, "sync": sync,
                     "replicas_to_aggregate": replicas_to_aggregate,
-                    "global_step": global_step, "data_plane": self.data_plane}
+                    "global_step": global_step, "data_plane": self.data_plane,
+                    "iterations": int(global_step if iterations is None else iterations),
+                    "slot_values": sorted(slots) if slots else []}
             if self.plans is not None:
                 from .ps_device import spec_for
                 spec.update(spec_for(self.space, self.plans[k], names))
@@ -403,6 +422,10 @@ class PSClient:
             dist.send(_hdr(OP_INIT, dist.get_rank(), vals.numel()), rank, group=self.group)
             _send_bytes(json.dumps(spec).encode(), rank, self.group)
             dist.send(vals, rank, group=self.group)
+            for sname in spec["slot_values"]:
+                sv = (torch.cat([slots[sname][i].detach().float().reshape(-1).cpu() for i in idx])
+                      if idx else torch.zeros(0))
+                dist.send(sv, rank, group=self.group)
 
     def wait_ready(self, params):
         """Non-chief: block until the chief initialised every PS shard (TF WorkerSessionCreator)."""

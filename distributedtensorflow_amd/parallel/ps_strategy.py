@@ -177,17 +177,40 @@ class ParameterServerStrategy(Strategy):
                 dist.broadcast(space.master, 0)
                 space.refresh_shadow()
 
-    def register_with_ps(self, optimizer, global_step=0):
-        """Chief: ship variables + optimizer config to the PS shards; others: wait for it."""
+    def register_with_ps(self, optimizer, global_step=0, restored_slots=False):
+        """Chief: ship variables + optimizer config (+ the optimizer slots just restored from a
+        checkpoint) to the PS shards; others: wait for it."""
         if self.mode != "between_graph":
             return
         params = optimizer.space.order
         if self.is_chief:
+            slots = None
+            if restored_slots and optimizer.slots:
+                slots = {s.name: [optimizer.space.view_of(s.buf, p) for p in params]
+                         for s in optimizer.slots}
             self._client.register(params, optimizer.get_config(), sync=self.sync,
                                   replicas_to_aggregate=self.replicas_to_aggregate,
-                                  global_step=int(global_step))
+                                  global_step=int(global_step), slots=slots,
+                                  iterations=optimizer.iterations if restored_slots else None)
         self._client.wait_ready(params)
         self._client.pull()          # every worker starts from the PS values
+
+    def recover_cluster(self, optimizer):
+        """A task of the cluster died (a PS crashed and is being restarted by the launcher):
+        leave the broken process group, join the next generation (blocks until the restarted
+        PS joins too) and re-map the new shard's buffers.  The caller restores the checkpoint
+        and calls :meth:`register_with_ps` again (chief re-initialises the PS; others wait)."""
+        if self.mode != "between_graph":
+            raise RuntimeError("cluster recovery is for between-graph parameter servers")
+        self.server.restart_group()
+        from .ps_service import PSClient
+        old = self._client
+        self._client = PSClient(self.server.ps_ranks(), policy=self.variable_placement,
+                                space=old.space, data_plane=self.data_plane)
+        reducer = getattr(optimizer, "_reducer", None)
+        if reducer is not None and hasattr(reducer, "client"):
+            reducer.client = self._client
+        return self.server.generation
 
     @property
     def ps_client(self):

@@ -146,6 +146,22 @@ def _execute(fetches, feed_dict, session):
     return out
 
 
+def _recoverable(exc):
+    """Errors TF's _RecoverableSession would recreate the session for: injected faults, a
+    vanished peer (ConnectionError from the PS data plane, torch.distributed's DistError
+    family), and gloo transport failures surfacing as RuntimeError."""
+    import torch.distributed as dist
+    if isinstance(exc, (InjectedFault, ConnectionError, TimeoutError)):
+        return True
+    if isinstance(exc, getattr(dist, "DistError", ())):
+        return True
+    if isinstance(exc, RuntimeError):
+        msg = str(exc).lower()
+        return any(k in msg for k in ("gloo", "connection", "peer", "broken pipe",
+                                      "parameter server"))
+    return False
+
+
 class MonitoredTrainingSession:
     RECOVERABLE = (InjectedFault, ConnectionError, TimeoutError)
 
@@ -182,6 +198,7 @@ class MonitoredTrainingSession:
         self._session = None
         self._should_stop = False
         self._closed = False
+        self.recoveries = 0
         self._create()
 
     # -- creation / recovery
@@ -209,7 +226,31 @@ class MonitoredTrainingSession:
         for h in self.hooks:
             h.after_create_session(self._session, None)
 
-    def _recover(self):
+    def _recover(self, exc=None):
+        self.recoveries += 1
+        strat = self.strategy
+        sc = self.scaffold
+        if exc is not None and not isinstance(exc, InjectedFault) and \
+                getattr(strat, "mode", None) == "between_graph" and \
+                hasattr(strat, "recover_cluster") and sc.optimizer is not None:
+            # a task died: next process-group generation (the launcher restarts a crashed PS),
+            # chief restores the latest checkpoint and re-initialises the PS shards with it,
+            # the other workers wait for that and pull
+            print(f"[dtf] recovering from {type(exc).__name__}: {exc}", flush=True)
+            gen = strat.recover_cluster(sc.optimizer)
+            restored = False
+            ckpt = latest_checkpoint(self.checkpoint_dir) if self.checkpoint_dir else None
+            if self.is_chief and ckpt and sc.saver is not None:
+                sc.saver.restore(None, ckpt, strict=False)
+                restored = True
+            strat.register_with_ps(sc.optimizer, sc.global_step.value(), restored_slots=restored)
+            client = getattr(strat, "ps_client", None)
+            if client is not None:
+                sc.global_step.assign(client.global_step)
+                self._session.strategy = strat
+            print(f"[dtf] recovered: generation {gen}, restored={ckpt if restored else None}, "
+                  f"global step {sc.global_step.value()}", flush=True)
+            return
         ckpt = latest_checkpoint(self.checkpoint_dir) if self.checkpoint_dir else None
         if ckpt and self.scaffold.saver is not None:
             self.scaffold.saver.restore(None, ckpt, strict=False)
@@ -241,13 +282,16 @@ class MonitoredTrainingSession:
                 for h in self.hooks:
                     h.after_run(ctx, rv)
                 break
-            except self.RECOVERABLE:
+            except Exception as e:
                 # the step (or a hook observing it) failed: roll back to the latest checkpoint
-                # and run the step again, like TF's _RecoverableSession
+                # (re-forming the cluster when a task died) and run the step again, like TF's
+                # _RecoverableSession
+                if not _recoverable(e):
+                    raise
                 attempts += 1
                 if attempts > self.max_recovery_attempts:
                     raise
-                self._recover()
+                self._recover(e)
         if ctx.stop_requested:
             self._should_stop = True
         return results

@@ -124,6 +124,7 @@ def main():
                                   checkpoint_dir=FLAGS.checkpoint_dir, config=tf_config,
                                   hooks=hooks, model=model, optimizer=opt,
                                   global_step=global_step, strategy=strategy,
+                                  save_checkpoint_steps=FLAGS.save_checkpoint_steps,
                                   log_step_count_steps=None, save_summaries_steps=None) as mon_sess:
         if is_chief:
             date_string = datetime.datetime.now().strftime("%Y_%m_%d__%H_%M_%S")
@@ -143,6 +144,8 @@ def main():
                 logs.writekvs({"Global Step": gstep, "Loss": train_loss}, global_step=gstep)
             else:
                 mon_sess.run(train_op)
+    if mon_sess.recoveries:
+        print(f"Recovered {mon_sess.recoveries} time(s) from a failed task", flush=True)
     if is_chief:
         logs.close()
         if t_start is not None:
@@ -164,6 +167,8 @@ def parse(argv=None):
     parser.add_argument("--data_dir", default="/tmp/data/")
     parser.add_argument("--log_dir", default="/tmp/distributed_logs")
     parser.add_argument("--checkpoint_dir", default=None)
+    parser.add_argument("--save_checkpoint_steps", type=int, default=None,
+                        help="chief checkpoints every N global steps (default: every 600 s)")
     parser.add_argument("--sync_replicas", action="store_true")
     parser.add_argument("--device", choices=("auto", "cpu", "gpu"), default="auto")
     parser.add_argument("--dtype", choices=("auto", "bf16", "fp32"), default="auto",

@@ -204,3 +204,37 @@ def test_allreduce_bandwidth_tool_gloo(tmp_path):
     rows = [json.loads(line) for line in open(out)]
     assert [x["size_mb"] for x in rows[:-1]] == [0.25, 0.5]
     assert all(x["busbw_GBps"] > 0 for x in rows[:-1]) and rows[-1]["bucketed_allreduce_ms"] > 0
+
+
+def test_ps_killed_mid_run_is_restarted_and_training_resumes(tmp_path, mnist_dir):
+    """Real failure recovery (reference run_mnist_distributed.py:146): the PS task
+    dies (SIGKILL at global step 25, DTF_FAULT_KILL_PS_AT_STEP), the launcher restarts it as a
+    fresh process, every task joins the next process-group generation, the chief restores the
+    latest checkpoint (variables + Adam slots + step) into the new PS, training reaches
+    max_steps and the final checkpoint is consistent with the final global step."""
+    ckpt = tmp_path / "ckpt"
+    codes, logs = launch_local(os.path.join(ROOT, "run_mnist_distributed.py"), 1, 2,
+                               str(tmp_path),
+                               ["--max_steps=45", f"--data_dir={mnist_dir}",
+                                f"--log_dir={tmp_path}/tb", "--batch_size=32",
+                                f"--checkpoint_dir={ckpt}", "--save_checkpoint_steps=10"],
+                               env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2",
+                                    "DTF_FAULT_KILL_PS_AT_STEP": "25"},
+                               timeout_s=300, max_ps_restarts=1)
+    text = {k: open(v).read() for k, v in logs.items()}
+    assert all(c == 0 for c in codes.values()), {k: t[-3000:] for k, t in text.items()}
+    assert "restarting (1/1)" in text["ps0"]                    # the PS really died once
+    assert text["ps0"].count("Started Parameter Server") == 2
+    for w in ("worker0", "worker1"):
+        assert "recovered: generation 1" in text[w], text[w][-3000:]
+    # the chief restored a checkpoint taken before the crash (every ~10 async global steps)
+    m = re.search(r"restored=(\S+model\.ckpt-(\d+))", text["worker0"])
+    assert m and 10 <= int(m.group(2)) <= 25, text["worker0"][-3000:]
+    steps = [int(s) for s in re.findall(r"global step: (\d+)\)", text["worker0"])]
+    assert steps[-1] >= 45
+    from distributedtensorflow_amd.train.checkpoint import latest_checkpoint, load_variable
+    last = latest_checkpoint(str(ckpt))
+    assert last.endswith(f"model.ckpt-{int(load_variable(last, 'global_step'))}")
+    assert int(load_variable(last, "global_step")) >= 45
+    assert abs(load_variable(last, "conv2d/kernel/Adam")).sum() > 0     # slots survived
+

@@ -54,3 +54,26 @@ def test_sync_replicas_ps_hbm_shard_ipc(tmp_path):
     # every closed step consumed both workers' fresh gradients (or a stale one was dropped)
     assert stats["pushes"] == 2 * stats["applied"] + stats["dropped_stale"] or \
         stats["pushes"] >= 2 * stats["applied"]
+
+
+def test_ps_killed_on_gpu_restarts_and_resumes(tmp_path):
+    """The recovery path on the HBM data plane: the PS dies holding its exported HBM shard,
+    the launcher restarts it, the workers drop their hipIpc mappings, join generation 1 and the
+    chief re-seeds the new shard from the latest checkpoint."""
+    from distributedtensorflow_amd.cluster.launcher import launch_local
+    ckpt = tmp_path / "ckpt"
+    codes, logs = launch_local(os.path.join(ROOT, "run_mnist_distributed.py"), 1, 2,
+                               str(tmp_path),
+                               ["--max_steps=60", f"--data_dir={tmp_path}/data",
+                                f"--log_dir={tmp_path}/tb", "--ps_device=gpu",
+                                f"--checkpoint_dir={ckpt}", "--save_checkpoint_steps=10"],
+                               env={"PYTHONPATH": ROOT, "DTF_FAULT_KILL_PS_AT_STEP": "30"},
+                               timeout_s=150, grace_s=20, max_ps_restarts=1)
+    text = {k: open(v).read() for k, v in logs.items()}
+    assert all(c == 0 for c in codes.values()), {k: t[-2500:] for k, t in text.items()}
+    assert "restarting (1/1)" in text["ps0"]
+    assert all("recovered: generation 1" in text[w] for w in ("worker0", "worker1"))
+    m = re.search(r"Close Parameter Server \.\.\. (\{.*\})", text["ps0"])
+    assert m and ast.literal_eval(m.group(1))["data_plane"] == "ipc"
+    steps = [int(s) for s in re.findall(r"global step: (\d+)\)", text["worker0"])]
+    assert steps[-1] >= 60

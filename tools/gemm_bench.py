@@ -27,6 +27,13 @@ SHAPES = [  # (name, M, N, K): C = A . B^T
 ]
 
 
+# ResNet-50 1x1 stride-1 convs at batch 1280 as GEMMs: (name, H*W, C, Kout)
+RESNET_1X1 = [("s0c1", 3136, 64, 64), ("s0c3", 3136, 64, 256), ("s0b1c1", 3136, 256, 64),
+              ("s1b0c1", 3136, 256, 128), ("s1c3", 784, 128, 512), ("s1b1c1", 784, 512, 128),
+              ("s2b0c1", 784, 512, 256), ("s2c3", 196, 256, 1024), ("s2b1c1", 196, 1024, 256),
+              ("s3b0c1", 196, 1024, 512), ("s3c3", 49, 512, 2048), ("s3b1c1", 49, 2048, 512)]
+
+
 def timeit(fn, iters):
     fn()
     torch.cuda.synchronize()
@@ -44,11 +51,39 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--resnet1x1", type=int, default=0,
+                    help="batch: time the ResNet-50 1x1 convs as GEMMs next to the conv kernel")
     ap.add_argument("--variants", default="0",
                     help="comma list of gemm.hip pipeline variants to time (gemm_set_variant)")
     a = ap.parse_args()
     rows = []
-    for name, M, N, K in SHAPES:
+    if a.resnet1x1:
+        for name, hw, C, Kout in RESNET_1X1:
+            M = a.resnet1x1 * hw
+            g = torch.Generator(device="cuda").manual_seed(0)
+            x = torch.randn(M, C, device="cuda", generator=g).bfloat16()
+            w = (torch.randn(Kout, C, device="cuda", generator=g) / C ** 0.5).bfloat16()
+            x4 = x.view(a.resnet1x1, hw, 1, C)
+            w4 = w.view(Kout, 1, 1, C)
+            t_conv = timeit(lambda: native.conv2d_forward(x4, w4, 1, 0), a.iters)
+            fl = 2.0 * M * Kout * C
+            for v in [int(x) for x in a.variants.split(",")]:
+                native._K.gemm_set_variant(v)
+                t_g = timeit(lambda: native.gemm_nt(x, w), a.iters)
+                row = {"shape": f"resnet1x1_{name}", "variant": v, "M": M, "N": Kout, "K": C,
+                       "gemm_us": round(t_g * 1e6, 1), "conv_us": round(t_conv * 1e6, 1),
+                       "gemm_tflops": round(fl / t_g / 1e12, 1),
+                       "conv_tflops": round(fl / t_conv / 1e12, 1),
+                       "gemm_speedup_vs_conv": round(t_conv / t_g, 3)}
+                rows.append(row)
+                print(json.dumps(row), flush=True)
+            native._K.gemm_set_variant(-1)
+            del x, w
+            torch.cuda.empty_cache()
+        SHAPES_RUN = []
+    else:
+        SHAPES_RUN = SHAPES
+    for name, M, N, K in SHAPES_RUN:
         if a.only and name not in a.only.split(","):
             continue
         g = torch.Generator(device="cuda").manual_seed(0)
