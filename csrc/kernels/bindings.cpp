@@ -143,7 +143,9 @@ void dtf_mlm_xent(const bf16_t*, const int64_t*, const float*, const float*, int
 
 // ---- dense GEMM (gemm.hip)
 void dtf_gemm_nt(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int,
-                 const float*, const bf16_t*, int, hipStream_t);
+                 const float*, const bf16_t*, int, float*, hipStream_t, const bf16_t*,
+                 const uint8_t*);
+int dtf_gemm_tile_rows(int);
 void dtf_gemm_set_variant(int);
 int dtf_bias_relu_bwd_ws_floats(int);
 void dtf_gather_u8_scale(const uint8_t*, const int64_t*, void*, int, int, float, int, hipStream_t);
@@ -234,11 +236,17 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.doc() = "distributedtensorflow_amd HIP/CDNA4 kernels (gfx950)";
 
   m.def("gemm_nt", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, int lda,
-                      int ldb, int ldc, uintptr_t bias, uintptr_t cin, int relu, uintptr_t st) {
+                      int ldb, int ldc, uintptr_t bias, uintptr_t cin, int relu, uintptr_t st,
+                      uintptr_t stats, uintptr_t acc_src, uintptr_t acc_mask) {
     dtf_gemm_nt(P<bf16_t>(a), P<bf16_t>(b), P<bf16_t>(c), M, N, K, lda, ldb, ldc,
-                P<float>(bias), P<bf16_t>(cin), relu, S(st));
+                P<float>(bias), P<bf16_t>(cin), relu, P<float>(stats), S(st), P<bf16_t>(acc_src),
+                P<uint8_t>(acc_mask));
     check_launch("gemm_nt");
-  });
+  }, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("M"), py::arg("N"), py::arg("K"),
+     py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("bias"), py::arg("cin"),
+     py::arg("relu"), py::arg("stream"), py::arg("stats") = 0, py::arg("acc_src") = 0,
+     py::arg("acc_mask") = 0);
+  m.def("gemm_tile_rows", &dtf_gemm_tile_rows);
   m.def("gemm_set_variant", &dtf_gemm_set_variant);
   m.def("bias_relu_bwd_ws_floats", &dtf_bias_relu_bwd_ws_floats);
   m.def("gather_u8_scale", [](uintptr_t images, uintptr_t idx, uintptr_t out, int B, int D,

@@ -38,6 +38,9 @@ struct GemmArgs {
   const bf16_t* Cin;      // accumulate source ([M][ldc], may alias C) or null
   int M, N, K, lda, ldb, ldc;
   int relu;
+  float* stats;           // BatchNorm partial sums of the bf16 outputs: [tiles_m][2][N] or null
+  const bf16_t* acc_src;  // C += acc_src * relu_bit (a residual BN's masked dy; conv acc mode 2)
+  const uint8_t* acc_mask;//   1 bit per element, 1 byte per 8 channels ([M][N] dense C only)
 };
 
 // chunk swizzle of a [rows][BK] bf16 tile: 16-row ds_read_b128 fragment reads hit 16 slots
@@ -75,8 +78,8 @@ struct GCfg {
   static constexpr int DA = BM / RPI / NW, DB = BN / RPI / NW;   // DMAs per wave per stage
   static constexpr int SA = BM * BK, STAGE = (BM + BN) * BK;   // bf16 elements
   static constexpr int LDC = BN + 8;
-  static constexpr size_t LDS = (size_t)NS * STAGE * 2 > (size_t)BM * LDC * 2
-                                    ? (size_t)NS * STAGE * 2 : (size_t)BM * LDC * 2;
+  static constexpr size_t EPI = (size_t)BM * LDC * 2 + (size_t)WM * 2 * BN * 4;  // + stats
+  static constexpr size_t LDS = (size_t)NS * STAGE * 2 > EPI ? (size_t)NS * STAGE * 2 : EPI;
 };
 
 // SCHED 0: per K-step {wait; barrier; issue next; reads + MFMAs of both 32-deep halves}.
@@ -239,6 +242,15 @@ gemm_nt_kernel(const GemmArgs g) {
     const int col = n0 + wn * Cf::WTN + j * 16 + frow;
     bj[j] = (g.bias && col < g.N) ? g.bias[col] : 0.f;
   }
+  // BN statistics from the registers: each lane sums its column's bf16-rounded values over its
+  // 4 * FM rows, then the 4 lane groups sharing a column (lanes l, l+16, l+32, l+48) combine
+  // by cross-lane adds; the WM waves of a column meet in LDS after the staging barrier.  (A
+  // pass over the staged tile instead costs ~128 LDS reads per thread -- exposed, since this
+  // kernel runs one block per CU.)
+  float s1[Cf::FN], s2[Cf::FN];
+#pragma unroll
+  for (int j = 0; j < Cf::FN; ++j) s1[j] = s2[j] = 0.f;
+  const bool do_stats = g.stats != nullptr;
 #pragma unroll
   for (int i = 0; i < Cf::FM; ++i)
 #pragma unroll
@@ -249,10 +261,42 @@ gemm_nt_kernel(const GemmArgs g) {
         const int col = wn * Cf::WTN + j * 16 + frow;
         float v = acc[i][j][r] + bj[j];
         if (g.relu) v = fmaxf(v, 0.f);
-        lds[row * Cf::LDC + col] = f2bf(v);
+        const bf16_t h = f2bf(v);
+        lds[row * Cf::LDC + col] = h;
+        if (do_stats && m0 + row < g.M) {
+          const float q = bf2f(h);
+          s1[j] += q;
+          s2[j] += q * q;
+        }
       }
+  if (do_stats) {
+#pragma unroll
+    for (int j = 0; j < Cf::FN; ++j) {
+      s1[j] += __shfl_xor(s1[j], 16, 64);
+      s1[j] += __shfl_xor(s1[j], 32, 64);
+      s2[j] += __shfl_xor(s2[j], 16, 64);
+      s2[j] += __shfl_xor(s2[j], 32, 64);
+    }
+    float* red = reinterpret_cast<float*>(lds + BM * Cf::LDC);   // [WM][2][BN], past the tile
+    if (fq == 0) {
+#pragma unroll
+      for (int j = 0; j < Cf::FN; ++j) {
+        const int col = wn * Cf::WTN + j * 16 + frow;
+        red[(wm * 2 + 0) * BN + col] = s1[j];
+        red[(wm * 2 + 1) * BN + col] = s2[j];
+      }
+    }
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();
+  if (do_stats && tid < BN && n0 + tid < g.N) {
+    const float* red = reinterpret_cast<const float*>(lds + BM * Cf::LDC);
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < Cf::WM; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
+    g.stats[((long)tm * 2 + 0) * g.N + n0 + tid] = a;
+    g.stats[((long)tm * 2 + 1) * g.N + n0 + tid] = b;
+  }
   constexpr int OCPR = BN / 8;                 // 16-B chunks per output row
   constexpr int OROWS = Cf::NT / OCPR;
   const int oc = tid % OCPR;
@@ -269,6 +313,14 @@ gemm_nt_kernel(const GemmArgs g) {
       unpack8(*reinterpret_cast<const uint4*>(g.Cin + off), b);
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += b[e];
+      v = pack8(a);
+    } else if (g.acc_mask) {
+      float a[8], b[8];
+      unpack8(v, a);
+      unpack8(*reinterpret_cast<const uint4*>(g.acc_src + off), b);
+      const uint32_t mb = g.acc_mask[off >> 3];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += (mb >> e) & 1u ? b[e] : 0.f;
       v = pack8(a);
     }
     *reinterpret_cast<uint4*>(g.C + off) = v;
@@ -295,17 +347,27 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
 
 void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
 
+// block-tile rows of every variant (the BatchNorm statistics slab has one row per M tile)
+int dtf_gemm_tile_rows(int M) { return (M + 255) / 256; }
+
 void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda,
-                 int ldb, int ldc, const float* bias, const bf16_t* Cin, int relu,
-                 hipStream_t st) {
+                 int ldb, int ldc, const float* bias, const bf16_t* Cin, int relu, float* stats,
+                 hipStream_t st, const bf16_t* acc_src, const uint8_t* acc_mask) {
   if (M <= 0 || N <= 0 || K <= 0) return;
   if (K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N)
     throw std::runtime_error("gemm_nt: K, N and the leading dimensions must be multiples of 8");
   // the per-block descriptors span at most one 256-row panel
   if ((long)256 * lda * 2 >= (1L << 32) || (long)256 * ldb * 2 >= (1L << 32))
     throw std::runtime_error("gemm_nt: leading dimension too large");
-  GemmArgs g{A, B, C, bias, Cin, M, N, K, lda, ldb, ldc, relu};
-  switch (g_gemm_variant < 0 ? 0 : g_gemm_variant) {
+  if (stats && (bias || relu || Cin))
+    throw std::runtime_error("gemm_nt: BN statistics epilogue excludes bias / ReLU / accumulate");
+  if (acc_mask && (!acc_src || Cin || ldc != N))
+    throw std::runtime_error("gemm_nt: masked accumulation needs acc_src and a dense C");
+  GemmArgs g{A, B, C, bias, Cin, M, N, K, lda, ldb, ldc, relu, stats, acc_src, acc_mask};
+  // auto: 256 x 128 tiles when N <= 128 (measured 1.02-1.07x the 256 x 256 tile on the N = 128
+  // ResNet 1x1 convs, profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl)
+  const int variant = g_gemm_variant >= 0 ? g_gemm_variant : (N <= 128 ? 1 : 0);
+  switch (variant) {
     case 1: launch_gemm<256, 128, 64, 3>(g, st); break;
     case 2: launch_gemm<256, 256, 32, 4>(g, st); break;
     case 3: launch_gemm<256, 128, 32, 4>(g, st); break;

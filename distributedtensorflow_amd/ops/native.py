@@ -141,6 +141,10 @@ def conv2d_forward(x, w_bf16, stride, padding, stats=None, bias=None, relu=False
     K, R, S, C = w_bf16.shape
     n, h, wd, c, P, Q, sh, sw, pt, pl = _conv_geom_fwd(x, K, R, S, stride, padding)
     assert c == C, (x.shape, w_bf16.shape)
+    if bias is None and not relu and _gemm_1x1(C, K, R, S, stride, (pt, pl)) and \
+            x.is_contiguous() and w_bf16.is_contiguous():
+        y = gemm_nt(x.view(-1, C), w_bf16.view(K, C), stats=stats)
+        return y.view(n, P, Q, K)
     taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
     y = torch.empty(n, P, Q, K, device=x.device, dtype=_BF16)
     _launch_fwd(x, w_bf16.reshape(K, R * S * C), K, taps, P, Q, sh, sw, y, P, Q, stats=stats,
@@ -200,6 +204,20 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_f
     pt, pb, pl, pr = resolve_padding(padding, h, wd, R, S, stride)
     dx = None
     wflat = w_bf16.reshape(K, R * S, C)
+    if bnb is None and _gemm_1x1(K, C, R, S, stride, (pt, pl)):
+        # 1x1 stride 1: dX[M, C] = dY[M, K] . Wt[C, K]^T on the GEMM kernel, residual
+        # gradients (materialised or masked) folded into its epilogue
+        M = n * h * wd
+        wt = _dgrad_filter(wflat).view(C, K)
+        dyc = dy.contiguous().view(M, K)
+        if out is not None:
+            o2 = out.view(M, C)
+            gemm_nt(dyc, wt, out=o2, cin=o2)
+            if acc_from is not None:
+                out.add_(acc_from.materialize())
+            return out
+        dx = gemm_nt(dyc, wt, acc_from=acc_from)
+        return dx.view(n, h, wd, C)
     need_zero = False
     launches = []
     for a in range(sh):
@@ -487,8 +505,11 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
     M = n * P * Q
     taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
     cp = -(-c // 8) * 8                      # the op zero-pads C to 8 before launching
-    G = _K.conv_tile_rows(_fwd_geom((n, h, wd, cp), K, taps, P, Q, sh, sw, P, Q),
-                          [t[0] for t in taps], [t[1] for t in taps])
+    if _gemm_1x1(cp, K, R, S, stride, (pt, pl)):
+        G = _K.gemm_tile_rows(M)
+    else:
+        G = _K.conv_tile_rows(_fwd_geom((n, h, wd, cp), K, taps, P, Q, sh, sw, P, Q),
+                              [t[0] for t in taps], [t[1] for t in taps])
     part = torch.empty(_K.bn_workspace_floats_g(G, K), device=x.device, dtype=torch.float32)
     y = _Conv2d.apply(x, w, stride, padding, part, grad_share)
     y._dtf_bn_part = (part, G, M, K)
@@ -863,9 +884,11 @@ def _wgrad_splits(T, o, i):
     return best
 
 
-def gemm_nt(a, b, out=None, bias=None, cin=None, relu=False):
+def gemm_nt(a, b, out=None, bias=None, cin=None, relu=False, stats=None, acc_from=None):
     """C[M, N] = A[M, K] . B[N, K]^T (+ bias) (ReLU) (+ cin) on the hand-written MFMA GEMM
-    (csrc/kernels/gemm.hip).  A, B bf16 with unit-stride rows; K and N multiples of 8."""
+    (csrc/kernels/gemm.hip).  A, B bf16 with unit-stride rows; K and N multiples of 8.
+    ``stats``: fp32 [tiles_m, 2, N] BatchNorm partial sums of the bf16 output (tiles_m =
+    ``gemm_tile_rows(M)``).  ``acc_from``: a :class:`_MaskedGrad` added as dy * mask."""
     _check_cuda_bf16(a, b)
     a2 = a.reshape(-1, a.shape[-1])
     if a2.stride(-1) != 1 or b.stride(-1) != 1:
@@ -880,9 +903,28 @@ def gemm_nt(a, b, out=None, bias=None, cin=None, relu=False):
         raise ValueError("gemm_nt: cin must be a contiguous bf16 [M, N] tensor")
     if bias is not None:
         bias = bias.detach().float().contiguous()
+    src = mask = 0
+    if acc_from is not None:
+        if acc_from.dy.numel() != out.numel() or acc_from.dy.dtype != _BF16:
+            raise ValueError("gemm_nt: masked residual gradient does not match the output")
+        src, mask = acc_from.dy.data_ptr(), acc_from.mask.data_ptr()
     _K.gemm_nt(a2.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a2.stride(0), b.stride(0),
-               out.stride(0), _p(bias), _p(cin), int(relu), _st())
+               out.stride(0), _p(bias), _p(cin), int(relu), _st(), _p(stats), src, mask)
     return out
+
+
+_CONV_GEMM = os.environ.get("DTF_CONV_GEMM", "1") == "1"
+
+
+def _gemm_1x1(C, K, R, S, stride, pads):
+    """1x1 stride-1 unpadded convs with a deep reduction or a wide output run on the GEMM
+    kernel (NHWC makes them exactly [N*H*W, C] x [K, C]^T).  With the fused BN statistics the
+    GEMM is 1.13-1.40x the implicit-GEMM conv kernel where the reduction C >= 512 and the
+    output K >= 256, and within noise or slower below: shallow reductions leave the one-block-
+    per-CU GEMM's prologue / epilogue exposed, where the conv kernel runs 3-4 blocks per CU
+    (profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl, same-box bench A/B)."""
+    return (_CONV_GEMM and R == 1 and S == 1 and tuple(_pair(stride)) == (1, 1)
+            and not any(pads) and C % 64 == 0 and K % 8 == 0 and C >= 512 and K >= 256)
 
 
 class _Dense(torch.autograd.Function):

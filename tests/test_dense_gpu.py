@@ -222,3 +222,27 @@ def test_mnist_cnn_and_mlp_train_fp32_on_native_kernels():
         o2.minimize(loss2)
         l2.append(float(loss2))
     assert l1[-1] < 0.6 * l1[0] and l2[-1] < 0.7 * l2[0], (l1, l2)
+
+
+def test_gemm_bn_stats_and_masked_residual_epilogues():
+    """The 1x1-conv epilogues of the GEMM: per-M-tile BatchNorm sums of the bf16 output and the
+    masked residual-gradient add (dy * relu bit) -- vs the same quantities computed by torch."""
+    from distributedtensorflow_amd.ops import native
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K = 1000, 256, 128
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    G = native.kernels().gemm_tile_rows(M)
+    stats = torch.empty(G, 2, N, device="cuda")
+    y = native.gemm_nt(a, b, stats=stats)
+    yf = y.float()
+    torch.testing.assert_close(stats[:, 0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-4, atol=1e-1)
+    torch.testing.assert_close(stats[0, 0], yf[:256].sum(0), rtol=1e-4, atol=1e-2)
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    bits = torch.randint(0, 2, (M, N), device="cuda", generator=g, dtype=torch.uint8)
+    w8 = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], device="cuda", dtype=torch.int32)
+    mask = (bits.view(M, N // 8, 8).int() * w8).sum(-1).to(torch.uint8).contiguous()
+    y2 = native.gemm_nt(a, b, acc_from=native._MaskedGrad(dy, mask))
+    ref = (y.float() + dy.float() * bits.float())
+    assert _rel(y2, ref) < 1e-2

@@ -231,7 +231,7 @@ def test_ps_killed_mid_run_is_restarted_and_training_resumes(tmp_path, mnist_dir
     m = re.search(r"restored=(\S+model\.ckpt-(\d+))", text["worker0"])
     assert m and 10 <= int(m.group(2)) <= 25, text["worker0"][-3000:]
     steps = [int(s) for s in re.findall(r"global step: (\d+)\)", text["worker0"])]
-    assert steps[-1] >= 45
+    assert steps[-1] >= 44           # async: the other worker may take the last step
     from distributedtensorflow_amd.train.checkpoint import latest_checkpoint, load_variable
     last = latest_checkpoint(str(ckpt))
     assert last.endswith(f"model.ckpt-{int(load_variable(last, 'global_step'))}")

@@ -67,6 +67,15 @@ def main():
             w4 = w.view(Kout, 1, 1, C)
             t_conv = timeit(lambda: native.conv2d_forward(x4, w4, 1, 0), a.iters)
             fl = 2.0 * M * Kout * C
+            # the training path: conv + fused BN statistics, routed (GEMM) vs conv kernel
+            native._CONV_GEMM = True
+            t_route = timeit(lambda: native.conv2d(x4, w4, 1, 0, bn_stats=True), a.iters)
+            native._CONV_GEMM = False
+            t_conv_st = timeit(lambda: native.conv2d(x4, w4, 1, 0, bn_stats=True), a.iters)
+            native._CONV_GEMM = True
+            print(json.dumps({"shape": f"resnet1x1_{name}_bnstats", "routed_us":
+                              round(t_route * 1e6, 1), "conv_kernel_us": round(t_conv_st * 1e6, 1),
+                              "speedup": round(t_conv_st / t_route, 3)}), flush=True)
             for v in [int(x) for x in a.variants.split(",")]:
                 native._K.gemm_set_variant(v)
                 t_g = timeit(lambda: native.gemm_nt(x, w), a.iters)
