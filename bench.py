@@ -36,14 +36,14 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=None,
-                   help="per-GPU batch (default 1280 for ResNet-50: 51 GB of the 288 GB HBM3E; the "
-                        "largest batch whose 112x112x64 stem activations stay under the kernels' "
-                        "2^31-byte buffer-offset limit; head-of-round-1 A/B 1024 vs 1280 -> "
-                        "12.53-12.54k vs 12.68-12.77k img/s; earlier sweep "
-                        "512/640/768/1024/1280 -> 10.26k/10.57k/10.67k/10.85k/"
-                        "10.99k img/s: larger batches amortise launches and fill the 256 CUs "
-                        "with whole tile rounds; 512 sequences for BERT: sweep 128/256/512/1024 "
-                        "-> 875k/1.03M/1.14M/1.15M tok/s)")
+                   help="per-GPU batch (default 2048 for ResNet-50: 82 GB of the 288 GB HBM3E; "
+                        "the conv kernels rebase their buffer descriptors per tile, so no 2 GiB "
+                        "tensor cap remains; round-2 sweep 1280/1536/2048 -> 12.76k/12.81k/12.83k "
+                        "img/s (profiles/measurements/r2_resnet_batch_sweep_1280_1536_2048.jsonl); "
+                        "earlier 512/640/768/1024/1280 -> 10.26k/10.57k/10.67k/10.85k/10.99k: "
+                        "larger batches amortise launches, fill the 256 CUs with whole tile "
+                        "rounds and shrink the all-reduce share per step; 512 sequences for BERT: "
+                        "sweep 128/256/512/1024 -> 875k/1.03M/1.14M/1.15M tok/s)")
     p.add_argument("--impl", choices=("dtf", "torch"), default="dtf")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--lr", type=float, default=0.1)
@@ -66,7 +66,7 @@ def parse():
     p.add_argument("--gemm-tuning-out", default=None)
     args = p.parse_args()
     if args.batch is None:
-        args.batch = 512 if args.model == "bert_base" else 1280
+        args.batch = 512 if args.model == "bert_base" else 2048
     return args
 
 

@@ -224,7 +224,13 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
 
   const int K = taps.n * g.C;
   const int nk = (K + BK - 1) / BK;
-  const auto rx = rsrc(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
+  // X descriptor based at the first image this tile's rows touch (64-bit pointer math): the
+  // 32-bit buffer offsets then span a few images only, so no tensor-size limit remains
+  const int PQ = g.P * g.Q;
+  const int n_lo = m0 / PQ;
+  const int n_hi = min(g.N - 1, (min(m0 + BM, M) - 1) / PQ);
+  const long img = (long)g.H * g.W * g.C;
+  const auto rx = rsrc(X + n_lo * img, (uint32_t)((n_hi - n_lo + 1) * img * 2));
   const auto rw = rsrc(Wt, (uint32_t)g.Kout * g.Kpad * 2u);
 
   if constexpr (GATHER != 0) {
@@ -244,7 +250,7 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     const int t = mm / g.Q;
     const int p = t % g.P;
     const int n = t / g.P;
-    a_pix[i] = n * g.H * g.W;                 // image base pixel
+    a_pix[i] = (n - n_lo) * g.H * g.W;        // image base pixel (relative to the descriptor)
     a_h[i] = ok ? p * g.sh : -(1 << 24);      // invalid rows fail every bounds test
     a_w[i] = q * g.sw;
   }
@@ -342,17 +348,17 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   constexpr int NR = BM / OROWS;               // rows per thread
   const int oc = tid % OCPR;
   const bool col_ok = n0 + oc * 8 < g.Kout;
-  // output element offset of this thread's k-th epilogue row (-1: none); int32 (host-checked)
-  auto row_off = [&](int k) -> int {
+  // output element offset of this thread's k-th epilogue row (-1: none); 64-bit
+  auto row_off = [&](int k) -> long {
     const int m = m0 + tid / OCPR + k * OROWS;
     const int q = m % g.Q;
     const int t = m / g.Q;
     const int p = t % g.P;
     const int n = t / g.P;
     const int ho = p * g.osh + g.oh0, wo = q * g.osw + g.ow0;
-    return (m < M && col_ok) ? ((n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8 : -1;
+    return (m < M && col_ok) ? (((long)n * g.Ho + ho) * g.Wo + wo) * g.Kout + n0 + oc * 8 : -1;
   };
-  int offs[NR];
+  long offs[NR];
   uint4 xpre[BNB ? NR : 1];
   uint32_t mpre[BNB ? (NR + 3) / 4 : 1];       // the rows' mask bytes, 4 per register
   auto prefetch_epilogue = [&]() {
@@ -545,7 +551,11 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * kDmaBM, n0 = tn * kDmaBN;
   const int nk = taps.n * g.C / kDmaBK;
-  const i32x4_t rx = rsrc_quad(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
+  const int PQ = g.P * g.Q;                          // descriptor rebased per tile (see above)
+  const int n_lo = m0 / PQ;
+  const int n_hi = min(g.N - 1, (min(m0 + kDmaBM, M) - 1) / PQ);
+  const long img = (long)g.H * g.W * g.C;
+  const i32x4_t rx = rsrc_quad(X + n_lo * img, (uint32_t)((n_hi - n_lo + 1) * img * 2));
   const i32x4_t rw = rsrc_quad(Wt, (uint32_t)g.Kout * g.Kpad * 2u);
   const uint32_t lds0 = lds_addr(lds);
 
@@ -563,7 +573,7 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
     const int t = mm / g.Q;
     const int p = t % g.P;
     const int n = t / g.P;
-    a_pix[j] = n * g.H * g.W;
+    a_pix[j] = (n - n_lo) * g.H * g.W;
     a_h[j] = ok ? p * g.sh : -(1 << 24);
     a_w[j] = q * g.sw;
     a_ch[j] = (slot ^ ((row >> 1) & 7)) * 8;
@@ -791,7 +801,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   const int tm = blockIdx.x;                                     // (image, row-tile)
   const int n = tm / tiles_h, h0 = (tm % tiles_h) * kHaloTH;
   const int n0 = blockIdx.y * NT;                                // output-channel tile
-  const i32x4_t rx = rsrc_quad(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
+  const i32x4_t rx = rsrc_quad(X + (long)n * g.H * g.W * g.C, (uint32_t)g.H * g.W * g.C * 2u);
   const i32x4_t rw = rsrc_quad(Wt, (uint32_t)g.Kout * g.Kpad * 2u);
   const uint32_t lds_patch = lds_addr(patch), lds_w = lds_addr(wst);
 
@@ -805,7 +815,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
       const int h = h0 - 1 + pr, w = pc - 1;
       const int chunk = slot ^ halo_swz<C>(pix);
       const bool ok = pix < H::PIX && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-      const uint32_t off = ok ? (uint32_t)((((n * g.H + h) * g.W + w) * C + chunk * 8) * 2) : kOOB;
+      const uint32_t off = ok ? (uint32_t)(((h * g.W + w) * C + chunk * 8) * 2) : kOOB;
       dma16(rx, lds_patch + (uint32_t)q * 1024u, off);
     }
   }
@@ -979,17 +989,19 @@ int dtf_conv_tile_rows(const ConvGeom& g, const TapTable& taps) {
 void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
                     const TapTable& taps, int bk, float* stats, const BnBwdEpi& bnb,
                     hipStream_t st) {
-  if (bnb.part && (double)g.N * g.Ho * g.Wo * g.Kout >= 2147483647.0)
-    throw std::runtime_error("conv: fused BN-backward epilogue needs a < 2^31-element output");
   if (bnb.part && (stats || !bnb.x || !bnb.mean || !bnb.invstd ||
                    (bnb.mkind == 1 && !bnb.mask) || (bnb.mkind == 2 && !(bnb.fsc && bnb.fsh))))
     throw std::runtime_error("conv: bad fused BN-backward epilogue arguments");
   if (taps.n <= 0 || taps.n > DTF_MAX_TAPS) throw std::runtime_error("conv: bad tap count");
   if (g.Kout % 8) throw std::runtime_error("conv: Kout % 8 != 0");
-  const double xbytes = 2.0 * g.N * g.H * g.W * g.C, wbytes = 2.0 * g.Kout * g.Kpad;
+  // buffer descriptors are rebased per tile at its first image: only a few images (and the
+  // filter) must fit 32-bit offsets; the row count itself is a 32-bit int
+  const double ibytes = 2.0 * g.H * g.W * g.C, wbytes = 2.0 * g.Kout * g.Kpad;
   const double m = (double)g.N * g.P * g.Q;
-  if (xbytes >= 2147483647.0 || wbytes >= 2147483647.0 || m >= 2147483647.0)
-    throw std::runtime_error("conv: tensor too large for 32-bit buffer offsets");
+  const double span = (double)(255 / (g.P * g.Q) + 2);   // images one 256-row tile touches
+  if (ibytes * span >= 2147483647.0 || wbytes >= 2147483647.0 || m >= 2147483647.0 ||
+      (double)g.N * g.Ho * g.Wo >= 2147483647.0)
+    throw std::runtime_error("conv: image / filter too large for 32-bit buffer offsets");
   const bool narrow = g.Kout <= 64;        // 256 x 64 tile for 64-wide layers
   const bool epi = g.bias || g.relu;       // fused bias / ReLU: register kernel only
   if (epi && (bnb.part || g.acc))

@@ -104,8 +104,13 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
   const int bc = jc - bt * g.C;
   const int bdh = lds_taps[bt], bdw = lds_taps[DTF_MAX_TAPS + bt];
   const bool a_col_ok = (k0 + cc * 8) < g.Kout;
-  const auto rx = rsrc(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
-  const auto ry = rsrc(dY, (uint32_t)M * g.Kout * 2u);
+  // descriptors rebased at this split's first dY row / first X image (64-bit pointer math):
+  // the 32-bit buffer offsets only span one split, never the whole tensor
+  const int PQ = g.P * g.Q;
+  const int n_lo = ms / PQ, n_hi = max(n_lo, (me - 1) / PQ);
+  const long img = (long)g.H * g.W * g.C;
+  const auto rx = rsrc(X + n_lo * img, (uint32_t)((n_hi - n_lo + 1) * img * 2));
+  const auto ry = rsrc(dY + (long)ms * g.Kout, (uint32_t)max(me - ms, 0) * g.Kout * 2u);
   const int HW = g.H * g.W;
 
   // branch-free loads: padding / out-of-range lanes get an out-of-range buffer offset -> zeros
@@ -114,12 +119,12 @@ conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
     for (int i = 0; i < 4; ++i) {
       const int m = ms + kt * BKM + rr + 16 * i;
       const bool mok = m < me;
-      ra[i] = bload16(ry, (mok && a_col_ok) ? (uint32_t)((m * g.Kout + k0 + cc * 8) * 2) : kOOB);
-      const int mm = mok ? m : 0;
+      ra[i] = bload16(ry, (mok && a_col_ok) ? (uint32_t)(((m - ms) * g.Kout + k0 + cc * 8) * 2) : kOOB);
+      const int mm = mok ? m : ms;
       const int q = mm % g.Q;
       const int t = mm / g.Q;
       const int p = t % g.P;
-      const int n = t / g.P;
+      const int n = t / g.P - n_lo;
       if constexpr (!GENERIC) {
         const int h = p * g.sh + bdh, w = q * g.sw + bdw;
         const bool ok = mok && b_col_ok && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
@@ -320,8 +325,11 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
   const int ms = split * (int)g.m_per_split;
   const int me = min(ms + (int)g.m_per_split, M);
   const int nk = (me - ms + BK - 1) / BK;
-  const i32x4_t rx = rsrc_quad(X, (uint32_t)g.N * g.H * g.W * g.C * 2u);
-  const i32x4_t ry = rsrc_quad(dY, (uint32_t)M * g.Kout * 2u);
+  const int PQ = g.P * g.Q;                 // split-relative descriptors (see conv_wgrad_kernel)
+  const int n_lo = ms / PQ, n_hi = max(n_lo, (me - 1) / PQ);
+  const long img = (long)g.H * g.W * g.C;
+  const i32x4_t rx = rsrc_quad(X + n_lo * img, (uint32_t)((n_hi - n_lo + 1) * img * 2));
+  const i32x4_t ry = rsrc_quad(dY + (long)ms * g.Kout, (uint32_t)max(me - ms, 0) * g.Kout * 2u);
   const uint32_t lds0 = lds_addr(lds);
   // tap table -> LDS (read once below, before any DMA reuses the space) so per-lane lookups
   // never index the kernarg struct
@@ -376,9 +384,9 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
     fdivmod(t, g.P, invP, n, p);
     const int hb = lane < live ? p * g.sh : 0x3FFF;   // an invalid row fails every bounds test
     const int wb = q * g.sw;
-    const int pb = ((n * HW + hb * g.W + wb) * g.C) * 2;
+    const int pb = (((n - n_lo) * HW + hb * g.W + wb) * g.C) * 2;
     const int hw = (hb << 16) | wb;
-    const uint32_t a_base = (uint32_t)mk * g.Kout * 2u;
+    const uint32_t a_base = (uint32_t)(mk - ms) * g.Kout * 2u;
 #pragma unroll
     for (int i = 0; i < Cf::IA; ++i) {
       const int r = rowa[i];
@@ -563,12 +571,16 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   if (g.Kout % 8) throw std::runtime_error("wgrad: Kout % 8 != 0");
   const bool via_ws = splits > 1 || accumulate;
   if (splits < 1 || (via_ws && !ws)) throw std::runtime_error("wgrad: bad split workspace");
-  if (2.0 * g.N * g.H * g.W * g.C >= 2147483647.0 || 2.0 * g.N * g.P * g.Q * g.Kout >= 2147483647.0)
-    throw std::runtime_error("wgrad: tensor too large for 32-bit buffer offsets");
   const long M = (long)g.N * g.P * g.Q;
   const int TC = taps.n * g.C;
   long mps = (M + splits - 1) / splits;
   mps = ((mps + BKM - 1) / BKM) * BKM;
+  // the kernels rebase X / dY at each split's first image / row: one split's span (not the
+  // tensor) must fit 32-bit byte offsets
+  const double span_imgs = (double)mps / ((double)g.P * g.Q) + 2.0;
+  if (M >= 2147483647L || 2.0 * mps * g.Kout >= 2147483647.0 ||
+      2.0 * span_imgs * g.H * g.W * g.C >= 2147483647.0)
+    throw std::runtime_error("wgrad: split span too large for 32-bit buffer offsets (more splits)");
   g.m_per_split = mps;
   g.slab = (long)g.Kout * g.ldw;
   const int nsplit = (int)((M + mps - 1) / mps);
@@ -576,8 +588,8 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   float* target = via_ws ? ws : dW;
   const size_t lds = (size_t)2 * (OPER_A + OPER_B) * sizeof(bf16_t) + 2 * DTF_MAX_TAPS * sizeof(int);
   const bool generic = (g.C % 8) != 0;
-  const bool dma = g_wgrad_dma_mode != 0 && !generic && (tr_mode & 1) && M < (1L << 24) &&
-                   g.N * g.H * g.W < (1L << 24);
+  // fdivmod (float reciprocal + one correction step) is exact while m / Q < 2^21
+  const bool dma = g_wgrad_dma_mode != 0 && !generic && (tr_mode & 1) && M / g.Q < (1L << 21);
   const bool narrow = dma && wgrad_narrow(g.Kout, taps.n);
   const int bm = narrow ? 64 : BM, bn = narrow ? 256 : BN;
   const long tiles = (long)((g.Kout + bm - 1) / bm) * ((TC + bn - 1) / bn);
