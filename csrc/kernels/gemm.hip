@@ -86,7 +86,7 @@ struct GCfg {
 // SCHED 1 (BK 64, NS 2): fragments double-buffered in registers and the barrier moved between
 // the two halves -- the reads of half 1 fly under the MFMAs of half 0, the reads of the next
 // step's half 0 under the MFMAs of half 1, so no wave waits on LDS latency at a phase start.
-template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8>
+template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1>
 __global__ void __launch_bounds__(NW * 64, 1)
 gemm_nt_kernel(const GemmArgs g) {
   using Cf = GCfg<BM, BN, BK, NS, NW>;
@@ -177,7 +177,133 @@ gemm_nt_kernel(const GemmArgs g) {
     }
   };
 
-  if constexpr (SCHED == 1) {
+  if constexpr (SCHED == 2) {
+    // Ping-pong schedule (cdna_hip_programming.md "256^2 8-phase template"; our own derivation):
+    // every K-step is 4 phases, one per quadrant of the 128 x 64 wave tile (64 x 32 x K64 = 16
+    // MFMAs).  Phase = {fragment reads | one 16-KB LDS-DMA piece (2 per thread) | counted vmcnt |
+    // barrier | MFMAs | barrier}.  The wave rows (wm = 1) run ONE barrier behind the wm = 0
+    // waves, so on every SIMD (one wave of each group) one wave is in its MFMA section while the
+    // other reads LDS and issues DMAs -- the two barriers per phase enforce the alternation.
+    //   reads:  q0: A-top(t)  q1: B-right(t)  q2: A-bottom(t)  q3: B-left(t+1) (8/4/8/4 reads:
+    //           the load section of every phase fits under the other group's 16 MFMAs)
+    //   DMA pieces issued:  q0: (t+1).B-right  q1: (t+1).A-bottom  q2: (t+2).A-top  q3: (t+2).B-left
+    // RAW: a piece is waited (counted vmcnt: q0/q1/q3 leave the 4 youngest pieces in flight, q2
+    // the 3 youngest) in the phase BEFORE the one that reads it, ahead of that phase's first
+    // barrier -- with the one-barrier stagger every reader then passes a barrier that follows
+    // every issuer's wait.  WAR: a region is restaged >= 2 phases after its last read (reads
+    // retire by lgkmcnt(0) right after the reading phase's first barrier).
+    static_assert(BM == 256 && BN == 256 && BK == 64 && NS == 2 && NW == 8, "SCHED 2 geometry");
+    // piece p, instruction j: this wave's 8-row group (first row r0) of A top (p0) / B left (p1)
+    // / B right (p2) / A bottom (p3)
+    uint32_t poff[4][2], plds[4][2];
+    int pch[4][2];
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool isA = pc == 0 || pc == 3;
+        const int r0 = pc == 0 ? j * 128 + 8 * wave
+                     : pc == 3 ? 64 + j * 128 + 8 * wave
+                               : (2 * j + (wave >> 2)) * 64 + (pc == 2 ? 32 : 0) + (wave & 3) * 8;
+        const int row = r0 + lrow;
+        const int ch = gswz<BK>(row, slot) * 8;
+        pch[pc][j] = ch;
+        const int rows = isA ? rows_a : rows_b;
+        const int ld = isA ? g.lda : g.ldb;
+        // rows past the operand: offset 2^31, past every descriptor (the host keeps each panel
+        // under 2^31 bytes), so "+ k0" stays out of range without a per-lane test
+        poff[pc][j] = row < rows ? (uint32_t)(row * ld + ch) * 2u : 0x80000000u;
+        plds[pc][j] = (uint32_t)((isA ? 0 : Cf::SA) + r0 * BK) * 2u;
+      }
+    const bool ktail = (g.K % BK) != 0;
+    // steps past the end re-read step 0 into a slot nobody reads again (constant vmcnt counts)
+    auto issue_piece = [&](int kt, int pc) {
+      const bool live = kt < nk;
+      const int k0 = (live ? kt : 0) * BK;
+      const uint32_t base = lds0 + (uint32_t)((kt & 1) * Cf::STAGE) * 2u;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        uint32_t off = poff[pc][j] + (uint32_t)k0 * 2u;
+        if (ktail && k0 + pch[pc][j] >= g.K) off = kGOOB;
+        dma16((pc == 0 || pc == 3) ? ra : rb, base + plds[pc][j], off);
+      }
+    };
+    bf16x8_t fA[8], fBl0[4], fBl1[4], fBr[4];
+    auto rdA = [&](const bf16_t* sa, int half) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = wm * 128 + half * 64 + i * 16 + frow, ch = ks * 4 + fq;
+          fA[ks * 4 + i] = *reinterpret_cast<const bf16x8_t*>(sa + r * BK + gswz<BK>(r, ch) * 8);
+        }
+    };
+    auto rdB = [&](bf16x8_t* fb, const bf16_t* sa, int half) {
+      const bf16_t* sb = sa + Cf::SA;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int r = wn * 64 + half * 32 + j * 16 + frow, ch = ks * 4 + fq;
+          fb[ks * 2 + j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
+        }
+    };
+    auto sync = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mfma_phase = [&](const bf16x8_t* fb, int ah, int bh) {
+      sync();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (PP_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[ah * 4 + i][bh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fA[ks * 4 + i], fb[ks * 2 + j], acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
+      if (PP_PRIO) __builtin_amdgcn_s_setprio(0);
+      sync();
+    };
+    // one K-step; bl holds this step's B-left fragments, bn receives the next step's
+    auto step = [&](int kt, const bf16x8_t* bl, bf16x8_t* bn) {
+      const bf16_t* cur = lds + (kt & 1) * Cf::STAGE;
+      const bf16_t* nxt = lds + ((kt + 1) & 1) * Cf::STAGE;
+      rdA(cur, 0);
+      issue_piece(kt + 1, 2);
+      DTF_WAIT_VM(8);
+      mfma_phase(bl, 0, 0);                    // q0: top x left
+      rdB(fBr, cur, 1);
+      issue_piece(kt + 1, 3);
+      DTF_WAIT_VM(8);
+      mfma_phase(fBr, 0, 1);                   // q1: top x right
+      rdA(cur, 1);
+      issue_piece(kt + 2, 0);
+      DTF_WAIT_VM(6);
+      mfma_phase(fBr, 1, 1);                   // q2: bottom x right
+      if (kt + 1 < nk) rdB(bn, nxt, 0);
+      issue_piece(kt + 2, 1);
+      DTF_WAIT_VM(8);
+      mfma_phase(bl, 1, 0);                    // q3: bottom x left
+    };
+    // prologue: step 0 whole + step 1's A-top / B-left; step 0's A-top / B-left landed
+    issue_piece(0, 0); issue_piece(0, 1); issue_piece(0, 2); issue_piece(0, 3);
+    issue_piece(1, 0); issue_piece(1, 1);
+    DTF_WAIT_VM(8);
+    sync();
+    rdB(fBl0, lds, 0);
+    if (wm == 1) sync();                       // the one-barrier stagger
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      step(kt, fBl0, fBl1);
+      step(kt + 1, fBl1, fBl0);
+    }
+    if (kt < nk) step(kt, fBl0, fBl1);
+    if (wm == 0) sync();                       // re-align the barrier counts
+  } else if constexpr (SCHED == 1) {
     static_assert(BK == 64 && NS == 2, "SCHED 1: two 32-deep halves per step, two slots");
     bf16x8_t fa0[Cf::FM], fb0[Cf::FN], fa1[Cf::FM], fb1[Cf::FN];
     auto rd = [&](bf16x8_t* fa, bf16x8_t* fb, const bf16_t* sa, int ks) {
@@ -329,18 +455,18 @@ gemm_nt_kernel(const GemmArgs g) {
 
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
 
-template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8>
+template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1>
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
   using Cf = GCfg<BM, BN, BK, NS, NW>;
   static bool attr = false;
   if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW>,
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cf::LDS));
     attr = true;
   }
   const long tiles = (long)((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW>), dim3((unsigned)tiles), dim3(Cf::NT), Cf::LDS,
-                     st, g);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO>), dim3((unsigned)tiles),
+                     dim3(Cf::NT), Cf::LDS, st, g);
 }
 
 }  // namespace
@@ -357,7 +483,7 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
   if (K % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldb < K || ldc < N)
     throw std::runtime_error("gemm_nt: K, N and the leading dimensions must be multiples of 8");
   // the per-block descriptors span at most one 256-row panel
-  if ((long)256 * lda * 2 >= (1L << 32) || (long)256 * ldb * 2 >= (1L << 32))
+  if ((long)256 * lda * 2 + 2L * K >= (1L << 31) || (long)256 * ldb * 2 + 2L * K >= (1L << 31))
     throw std::runtime_error("gemm_nt: leading dimension too large");
   if (stats && (bias || relu || Cin))
     throw std::runtime_error("gemm_nt: BN statistics epilogue excludes bias / ReLU / accumulate");
@@ -366,7 +492,7 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
   GemmArgs g{A, B, C, bias, Cin, M, N, K, lda, ldb, ldc, relu, stats, acc_src, acc_mask};
   // auto: 256 x 128 tiles when N <= 128 (measured 1.02-1.07x the 256 x 256 tile on the N = 128
   // ResNet 1x1 convs, profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl)
-  const int variant = g_gemm_variant >= 0 ? g_gemm_variant : (N <= 128 ? 1 : 0);
+  const int variant = g_gemm_variant >= 0 ? g_gemm_variant : (N <= 128 ? 1 : 8);
   switch (variant) {
     case 1: launch_gemm<256, 128, 64, 3>(g, st); break;
     case 2: launch_gemm<256, 256, 32, 4>(g, st); break;
@@ -375,6 +501,8 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
     case 5: launch_gemm<256, 256, 64, 2, 0, 4>(g, st); break;
     case 6: launch_gemm<256, 256, 64, 2, 1, 4>(g, st); break;
     case 7: launch_gemm<256, 256, 32, 4, 0, 4>(g, st); break;
+    case 8: launch_gemm<256, 256, 64, 2, 2>(g, st); break;
+    case 9: launch_gemm<256, 256, 64, 2, 2, 8, 0>(g, st); break;
     default: launch_gemm<256, 256, 64, 2>(g, st); break;
   }
 }

@@ -246,3 +246,29 @@ def test_gemm_bn_stats_and_masked_residual_epilogues():
     y2 = native.gemm_nt(a, b, acc_from=native._MaskedGrad(dy, mask))
     ref = (y.float() + dy.float() * bits.float())
     assert _rel(y2, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 776, 200), (4096, 2304, 768), (300, 264, 1000),
+                                   (513, 512, 64), (256, 256, 4096)])
+def test_gemm_pingpong_schedule_bit_identical(M, N, K):
+    """The ping-pong (two-group, barrier-staggered) K-loop of gemm.hip (variant 8) accumulates
+    every output in the same MFMA order as the default pipeline: results must be bit-identical,
+    with bias+ReLU, with Cin accumulation, and on M / N / K tails."""
+    from distributedtensorflow_amd.ops import native
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    cin = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    outs = []
+    try:
+        for v in (0, 8):
+            native._K.gemm_set_variant(v)
+            outs.append((native.gemm_nt(a, b), native.gemm_nt(a, b, bias=bias, relu=True),
+                         native.gemm_nt(a, b, cin=cin.clone())))
+    finally:
+        native._K.gemm_set_variant(-1)
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    ref = a.float() @ b.float().t()
+    assert ((outs[1][0].float() - ref).norm() / ref.norm()).item() < 1e-2
