@@ -492,6 +492,225 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong wgrad for the compute-bound shapes (Kout >= 256 and T*C >= 256: the 3x3 convs of
+// stages 2-4, the late 1x1 convs, every dense layer of BERT): 256 x 256 tile, 8 waves as
+// 2 (Kout) x 4 (T*C) of 128 x 64, 64-pixel K-steps in two 64-KB LDS slots.  The schedule is the
+// GEMM's (gemm.hip SCHED 2): each K-step is 4 phases {fragment tr-reads | one 16-KB LDS-DMA
+// piece (2 per thread) | counted vmcnt | barrier | 16 MFMAs | barrier}, the wm = 1 waves one
+// barrier behind the wm = 0 waves, so on every SIMD one wave computes while the other loads.
+//   phase:  q0 = (pixels 0-31, Kout top half)   q1 = (0-31, bottom)
+//           q2 = (pixels 32-63, top)            q3 = (32-63, bottom)
+//   reads:  q0: B(ks0) + A-top(ks0)  q1: A-bottom(ks0)  q2: B(ks1) + A-top(ks1)  q3: A-bottom(ks1)
+//   pieces (rows = pixels, row-contiguous 16 KB):  K-step t+1's dY[0:32] at q0, X[0:32] at q1,
+//           dY[32:64] at q2, X[32:64] at q3
+// RAW: a half is waited (vmcnt(4): the 2 youngest pieces may fly) in the phase before its first
+// reader (q1 for the step's second half, q3 for the next step's first), ahead of that phase's
+// first barrier.  WAR: every half is restaged >= 3 phases after its last read.
+// LDS image rows are 512 B (256 bf16), chunk-swizzled with wswz<512> on the DMA source side.
+constexpr int kPpT = 512;
+constexpr int kPpBK = 64;                   // pixels per K-step
+constexpr int kPpW = 256;                   // operand image width (elements)
+constexpr int kPpImg = kPpBK * kPpW;        // one operand image per slot (32 KB)
+constexpr int kPpStage = 2 * kPpImg;        // dY image + X image
+constexpr int kPpLDO = 260;                 // fp32 epilogue pitch (floats)
+constexpr size_t kPpLDS = (size_t)128 * kPpLDO * 4 > (size_t)2 * kPpStage * 2
+                              ? (size_t)128 * kPpLDO * 4 : (size_t)2 * kPpStage * 2;
+
+__global__ void __launch_bounds__(kPpT, 1)
+conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
+                     float* __restrict__ dW, const WgradGeom g, const TapTableW taps,
+                     float invQ, float invP) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int TC = taps.n * g.C;
+  const int tiles_m = (g.Kout + 255) / 256, tiles_n = (TC + 255) / 256;
+  const int ntiles = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int k0 = tm * 256, j0 = tn * 256;
+  const int M = g.N * g.P * g.Q;
+  const int ms = split * (int)g.m_per_split;
+  const int me = min(ms + (int)g.m_per_split, M);
+  const int nk = (me - ms + kPpBK - 1) / kPpBK;
+  const int PQ = g.P * g.Q;                 // split-relative descriptors (see conv_wgrad_kernel)
+  const int n_lo = ms / PQ, n_hi = max(n_lo, (me - 1) / PQ);
+  const long img = (long)g.H * g.W * g.C;
+  const i32x4_t rx = rsrc_quad(X + n_lo * img, (uint32_t)((n_hi - n_lo + 1) * img * 2));
+  const i32x4_t ry = rsrc_quad(dY + (long)ms * g.Kout, (uint32_t)max(me - ms, 0) * g.Kout * 2u);
+  const uint32_t lds0 = lds_addr(lds);
+  int* lds_taps = reinterpret_cast<int*>(lds);
+  if (tid == 0)
+    for (int t = 0; t < taps.n; ++t) { lds_taps[t] = taps.dh[t]; lds_taps[DTF_MAX_TAPS + t] = taps.dw[t]; }
+  __syncthreads();
+  // DMA plan: instruction j (0, 1) of a piece fills image rows 2 (wave + 8 j) + {0, 1} of the
+  // 32-row half; lane l fetches row (l >> 5)'s logical chunk (l & 31) ^ swizzle
+  int a_off[2], b_dh[2], b_dw[2], b_toff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int rr = 2 * (wave + 8 * j) + (lane >> 5);
+    const int chunk = (lane & 31) ^ wswz<512>(rr);
+    const int kc = k0 + chunk * 8;
+    a_off[j] = kc < g.Kout ? kc * 2 : -1;
+    const int jc = j0 + chunk * 8;
+    if (jc < TC) {
+      const int t = jc / g.C, c = jc - t * g.C;
+      b_dh[j] = lds_taps[t];
+      b_dw[j] = lds_taps[DTF_MAX_TAPS + t];
+      b_toff[j] = ((b_dh[j] * g.W + b_dw[j]) * g.C + c) * 2;
+    } else {
+      b_dh[j] = 1 << 20;
+      b_dw[j] = 0;
+      b_toff[j] = 0;
+    }
+  }
+  __syncthreads();                          // the tap table is dead: slot 0 may now be filled
+  const int HW = g.H * g.W;
+  // pixel decode of the K-step being issued: lane l holds pixel mk + l's base offset / (h, w)
+  int dec_pb = 0, dec_hw = 0, dec_live = 0;
+  auto decode = [&](int kt) {
+    const int mk = ms + kt * kPpBK;
+    dec_live = me - mk;
+    const int mp = mk + lane;
+    int t, q, n, p;
+    fdivmod(mp < me ? mp : ms, g.Q, invQ, t, q);
+    fdivmod(t, g.P, invP, n, p);
+    const int hb = lane < dec_live ? p * g.sh : 0x3FFF;   // an invalid row fails every test
+    const int wb = q * g.sw;
+    dec_pb = (((n - n_lo) * HW + hb * g.W + wb) * g.C) * 2;
+    dec_hw = (hb << 16) | wb;
+  };
+  // piece pc: 0 = dY rows 0-31, 1 = X rows 0-31, 2 = dY rows 32-63, 3 = X rows 32-63
+  auto issue = [&](int kt, int pc) {
+    const int h = pc >> 1;
+    const bool isB = pc & 1;
+    const int mk = ms + kt * kPpBK;
+    const uint32_t base = lds0 + (uint32_t)(((kt & 1) * kPpStage + (isB ? kPpImg : 0) +
+                                             h * 32 * kPpW) * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int R = 32 * h + 2 * (wave + 8 * j) + (lane >> 5);   // pixel row of the K-step
+      const uint32_t dst = base + (uint32_t)(2 * (wave + 8 * j) * kPpW * 2);
+      if (!isB) {
+        const uint32_t off = (R < dec_live && a_off[j] >= 0)
+                                 ? (uint32_t)(mk - ms + R) * g.Kout * 2u + (uint32_t)a_off[j] : kOOB;
+        dma16(ry, dst, off);
+      } else {
+        const int hwr = __shfl(dec_hw, R, 64);
+        const int pbr = __shfl(dec_pb, R, 64);
+        const int hh = (hwr >> 16) + b_dh[j], ww = (hwr & 0xFFFF) + b_dw[j];
+        const bool ok = (unsigned)hh < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+        dma16(rx, dst, ok ? (uint32_t)(pbr + b_toff[j]) : kOOB);
+      }
+    }
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const int gq = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;
+  bf16x8_t fA[4], fB[4];
+  auto rdA = [&](const bf16_t* sa, int ks, int half) {
+    const int r0 = 32 * ks + 8 * gq + tq;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c0 = wm * 128 + half * 64 + 16 * i + 4 * tp;
+      const s4_t lo = tr_read(sa + lds_el<kPpW>(r0, c0));
+      const s4_t hi = tr_read(sa + lds_el<kPpW>(r0 + 4, c0));
+      fA[i] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  };
+  auto rdB = [&](const bf16_t* sb, int ks) {
+    const int r0 = 32 * ks + 8 * gq + tq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c0 = wn * 64 + 16 * j + 4 * tp;
+      const s4_t lo = tr_read(sb + lds_el<kPpW>(r0, c0));
+      const s4_t hi = tr_read(sb + lds_el<kPpW>(r0 + 4, c0));
+      fB[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  };
+  auto sync = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mfma_phase = [&](int half) {
+    sync();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[half * 4 + i][j] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(fA[i], fB[j], acc[half * 4 + i][j], 0, 0, 0);
+    sync();
+  };
+
+  decode(0);
+  issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
+  DTF_WAIT_VM(4);                           // step 0's first half landed
+  sync();
+  if (wm == 1) sync();                      // the one-barrier stagger
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16_t* sa = lds + (kt & 1) * kPpStage;
+    const bf16_t* sb = sa + kPpImg;
+    rdB(sb, 0);
+    rdA(sa, 0, 0);
+    decode(kt + 1);
+    issue(kt + 1, 0);
+    mfma_phase(0);                          // q0
+    rdA(sa, 0, 1);
+    issue(kt + 1, 1);
+    DTF_WAIT_VM(4);                         // this step's second half landed
+    mfma_phase(1);                          // q1
+    rdB(sb, 1);
+    rdA(sa, 1, 0);
+    issue(kt + 1, 2);
+    mfma_phase(0);                          // q2
+    rdA(sa, 1, 1);
+    issue(kt + 1, 3);
+    DTF_WAIT_VM(4);                         // the next step's first half landed
+    mfma_phase(1);                          // q3
+  }
+  if (wm == 0) sync();                      // re-align the barrier counts
+  DTF_WAIT_VM(0);                           // the trailing no-op pieces still target the slots
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  float* so = reinterpret_cast<float*>(lds);
+  float* out = dW + (long)split * g.slab;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {    // the wm == pass waves stage their 128 rows
+    if (pass) __syncthreads();
+    if (wm == pass) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            so[(16 * i + 4 * gq + r) * kPpLDO + wn * 64 + 16 * j + li] = acc[i][j][r] + 0.0f;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < 128 * 64; idx += kPpT) {
+      const int r = idx >> 6, c4 = idx & 63;
+      const int row = k0 + pass * 128 + r, col = j0 + c4 * 4;
+      if (row < g.Kout && col < TC)
+        *reinterpret_cast<float4*>(out + (long)row * g.ldw + col) =
+            *reinterpret_cast<const float4*>(so + r * kPpLDO + c4 * 4);
+    }
+  }
+}
+
 // Deterministic slab sum: block = 64 float4 columns x 4 split groups; group q sums splits
 // q, q+4, ... in order, the 4 group partials are added in a fixed order through LDS.
 __global__ void __launch_bounds__(256)
@@ -530,6 +749,13 @@ void dtf_wgrad_set_dma_mode(int mode) { g_wgrad_dma_mode = mode; }
 // (-0.8 % vs 0); 2 = 64-pixel steps, 3 stages, 1 block/CU (-5.6 %); 3 (default) = 32-pixel steps
 // double-buffered with a two-pass epilogue: ~34-40 KB of LDS and <= 128 VGPRs -> 4 blocks/CU
 // (+1.1 % step vs 0; same-box A/B, profiles/measurements/r1_ab_wgrad_*.txt)
+static int g_wgrad_pp = 1;        // ping-pong 256 x 256 kernel for Kout >= 256, T*C >= 256
+static int g_wgrad_pp_rounds = 1; // its split-K target: this many rounds of 256 blocks
+void dtf_wgrad_set_pp(int v) {
+  g_wgrad_pp = v > 0;
+  if (v > 0) g_wgrad_pp_rounds = v;
+}
+static bool wgrad_pp(int Kout, int TC) { return g_wgrad_pp && Kout >= 256 && TC >= 256; }
 static int g_wgrad_pipe = 3;
 void dtf_wgrad_set_pipe(int p) { g_wgrad_pipe = p; }
 int dtf_wgrad_get_pipe() { return g_wgrad_pipe; }
@@ -544,12 +770,14 @@ static bool wgrad_narrow(int Kout, int taps) {
 // Number of reduction splits: aim for ~1024 blocks (4 per CU), keep >= 4 K-steps per split and
 // the fp32 slab workspace (splits x Kout x TC) under `ws_cap` floats.
 int dtf_conv_wgrad_splits(long M, int Kout, int TC, long ws_cap, int taps) {
-  const bool nar = wgrad_narrow(Kout, taps);
-  const int bm = nar ? 64 : BM, bn = nar ? 256 : BN;
+  const bool pp = wgrad_pp(Kout, TC);
+  const bool nar = !pp && wgrad_narrow(Kout, taps);
+  const int bm = pp ? 256 : nar ? 64 : BM, bn = pp ? 256 : nar ? 256 : BN;
   const long tiles = (long)((Kout + bm - 1) / bm) * ((TC + bn - 1) / bn);
   // never overshoot 1024 = exactly two rounds of 512 block slots (2 blocks x 256 CUs): one block
-  // past a round costs a whole extra round (29 splits x 36 tiles = 1044 blocks ran 3 rounds)
-  long splits = 1024 / tiles;
+  // past a round costs a whole extra round (29 splits x 36 tiles = 1044 blocks ran 3 rounds);
+  // the ping-pong kernel runs one block per CU: two rounds of 256
+  long splits = (pp ? 256 * g_wgrad_pp_rounds : 1024) / tiles;
   const long max_splits = (M + 4 * BKM - 1) / (4 * BKM);
   if (splits > max_splits) splits = max_splits;
   const long cap = ws_cap / ((long)Kout * TC);
@@ -588,13 +816,25 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   float* target = via_ws ? ws : dW;
   const size_t lds = (size_t)2 * (OPER_A + OPER_B) * sizeof(bf16_t) + 2 * DTF_MAX_TAPS * sizeof(int);
   const bool generic = (g.C % 8) != 0;
-  // fdivmod (float reciprocal + one correction step) is exact while m / Q < 2^21
-  const bool dma = g_wgrad_dma_mode != 0 && !generic && (tr_mode & 1) && M / g.Q < (1L << 21);
+  // fdivmod (float reciprocal + one correction step) is exact while m / Q < 2^21; the DMA
+  // kernels pack a pixel's (h, w) as (h << 16) | w
+  const bool dma = g_wgrad_dma_mode != 0 && !generic && (tr_mode & 1) && M / g.Q < (1L << 21) &&
+                   g.H < 16000 && g.W < 65536;
   const bool narrow = dma && wgrad_narrow(g.Kout, taps.n);
   const int bm = narrow ? 64 : BM, bn = narrow ? 256 : BN;
   const long tiles = (long)((g.Kout + bm - 1) / bm) * ((TC + bn - 1) / bn);
   const dim3 grid((unsigned)(tiles * nsplit));
-  if (dma) {
+  if (dma && wgrad_pp(g.Kout, TC) && g.ldw % 4 == 0) {
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
+      attr = true;
+    }
+    const long ptiles = (long)((g.Kout + 255) / 256) * ((TC + 255) / 256);
+    hipLaunchKernelGGL(conv_wgrad_pp_kernel, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT), kPpLDS,
+                       st, X, dY, target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+  } else if (dma) {
     const float iq = 1.0f / (float)g.Q, ip = 1.0f / (float)g.P;
 #define DTF_WGRAD_LAUNCH(WM_, WN_, BK_, NS_)                                                     \
   hipLaunchKernelGGL((conv_wgrad_dma_kernel<WM_, WN_, BK_, NS_>), grid, dim3(kThreads),         \

@@ -1077,11 +1077,11 @@ class _NativeDense(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             target = _direct_grad(w_master) if op == o else None
             if target is not None:
-                conv2d_wgrad(x2.view(1, M, 1, i), dz.view(1, M, 1, op), (op, 1, 1, i), 1, 0,
+                conv2d_wgrad(x2.view(M, 1, 1, i), dz.view(M, 1, 1, op), (op, 1, 1, i), 1, 0,
                              out=target.view(op, 1, 1, i))
                 _grad_ready(w_master)
             else:
-                dw = conv2d_wgrad(x2.view(1, M, 1, i), dz.view(1, M, 1, op), (op, 1, 1, i), 1,
+                dw = conv2d_wgrad(x2.view(M, 1, 1, i), dz.view(M, 1, 1, op), (op, 1, 1, i), 1,
                                   0).view(op, i)[:o]
                 tw = _direct_grad(w_master)
                 if tw is not None:

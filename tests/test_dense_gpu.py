@@ -272,3 +272,18 @@ def test_gemm_pingpong_schedule_bit_identical(M, N, K):
         assert torch.equal(x, y)
     ref = a.float() @ b.float().t()
     assert ((outs[1][0].float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("T,i,o", [(40000, 256, 512), (65536, 768, 768)])
+def test_native_dense_wgrad_many_tokens(T, i, o):
+    """dW of the native dense layer over more tokens than the wgrad kernels' packed pixel
+    coordinates could once index (tokens run as T images of 1x1, not one T x 1 image): every
+    token must contribute."""
+    from distributedtensorflow_amd.ops import native
+    g = torch.Generator(device="cuda").manual_seed(T + i)
+    x = torch.randn(T, i, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(o, i, device="cuda", generator=g) / i ** 0.5).requires_grad_(True)
+    dy = torch.randn(T, o, device="cuda", generator=g).bfloat16()
+    native.dense(x, w, None, False, impl="native").backward(dy)
+    ref = dy.float().t() @ x.float()
+    assert ((w.grad.float() - ref).norm() / ref.norm()).item() < 1e-3

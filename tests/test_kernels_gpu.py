@@ -371,3 +371,37 @@ def test_halo_conv3x3_matches_implicit_gemm(N, H, C, K):
     ref = _ref()
     yr = ref.conv2d(x.float(), w.float(), 1, 1)
     assert _rel(outs[0][0], yr) < 1e-2
+
+
+WGRAD_PP_CASES = [
+    (2, 14, 14, 256, 256, 3, 1, 1),      # stage-3 3x3
+    (2, 7, 7, 512, 512, 3, 1, 1),        # stage-4 3x3
+    (3, 9, 11, 128, 384, 3, 1, 1),       # partial Kout / T*C tiles, M not a multiple of 64
+    (2, 28, 28, 256, 256, 3, 2, 1),      # stride 2, padding taps
+    (4, 14, 14, 1024, 256, 1, 1, 0),     # late 1x1
+    (4096, 1, 1, 768, 3072, 1, 1, 0),    # a dense layer's dW (tokens as pixels)
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_PP_CASES)
+def test_wgrad_pingpong_kernel(case):
+    """The 256 x 256 ping-pong wgrad kernel (Kout, T*C >= 256) against the fp32 reference and
+    the 128 x 128 LDS-DMA kernel it replaces for these shapes."""
+    N, H, W, C, K, R, stride, pad = case
+    nat, ref = _native(), _ref()
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, P, Q, K, device=dev).to(torch.bfloat16)
+    try:
+        nat._K.wgrad_set_pp(1)
+        pp = nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad)
+        nat._K.wgrad_set_pp(0)
+        old = nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad)
+    finally:
+        nat._K.wgrad_set_pp(1)
+    wr = torch.zeros(K, R, R, C, device=dev, requires_grad=True)
+    ref.conv2d(x.float(), wr, stride, pad).backward(dy.float())
+    assert _rel(pp, wr.grad) < 1e-3, _rel(pp, wr.grad)
+    assert _rel(pp, old) < 1e-4, _rel(pp, old)

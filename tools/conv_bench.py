@@ -69,7 +69,11 @@ def main():
     ap.add_argument("--wgrad-mode", type=int, default=-1,
                     help="wgrad_set_dma_mode: -1/1 LDS-DMA (narrow 1x4 for Kout <= 64), "
                          "2 LDS-DMA 2x2 only, 0 register-staged")
+    ap.add_argument("--wgrad-pp", type=int, default=1,
+                    help="wgrad_set_pp: 0 off, n > 0: 256 x 256 ping-pong kernel for Kout, T*C >= 256 "
+                         "with a split-K target of n rounds of 256 blocks")
     args = ap.parse_args()
+    native._K.wgrad_set_pp(args.wgrad_pp)
     native._K.conv_set_dma_mode(args.dma)
     native._K.wgrad_set_dma_mode(args.wgrad_mode)
     if args.small_k is not None:
