@@ -978,9 +978,29 @@ int dtf_conv_stats_rows(long M, int Kout, int C, int taps, int W) {
   return (int)((M + BM - 1) / BM);
 }
 
+// multi-tap convs with C % 64 == 0 and Kout >= 256 whose outputs map one-to-one onto the M rows
+// (forward convs, stride-1 data gradients) run as implicit GEMMs on gemm.hip's ping-pong
+// kernel (256 x 256 tiles, 1.2-1.3 PF on long-K GEMMs vs ~0.9 for the 256 x 128 DMA kernel)
+static int g_conv_gemm = 1;
+void dtf_conv_set_gemm(int v) { g_conv_gemm = v; }
+static bool use_conv_gemm(const ConvGeom& g, const TapTable& taps) {
+  const bool unit = g.osh == 1 && g.osw == 1 && g.oh0 == 0 && g.ow0 == 0 && g.Ho == g.P &&
+                    g.Wo == g.Q;
+  // strided-dgrad phase classes qualify too (any tap count, no masked-residual epilogue)
+  return g_conv_gemm && g.C % 64 == 0 && g.Kout >= 256 && g.Kout % 8 == 0 && taps.n <= 9 &&
+         (unit ? taps.n > 1 : g.acc != 2) && g.Kpad == taps.n * g.C && !g.bias && !g.relu &&
+         g.H < 16384 && g.W < 32768;
+}
+void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, int W, int C,
+                   int P, int Q, int sh, int sw, int Kout, int ntaps, const int* dh, const int* dw,
+                   int Ho, int Wo, int osh, int osw, int oh0, int ow0,
+                   float* stats, const bf16_t* Cin, const bf16_t* acc_src,
+                   const uint8_t* acc_mask, hipStream_t st);
+
 // M tiles (= BN-statistics slab rows) of exactly the kernel dtf_conv_igemm will pick for this
 // forward launch (no fused BN-backward epilogue)
 int dtf_conv_tile_rows(const ConvGeom& g, const TapTable& taps) {
+  if (use_conv_gemm(g, taps)) return (int)(((long)g.N * g.P * g.Q + 255) / 256);
   if (g.C % 32 == 0 && use_halo(g, taps)) return g.N * (g.H / kHaloTH);
   const long M = (long)g.N * g.P * g.Q;
   return dtf_conv_stats_rows(M, g.Kout, g.C, taps.n, 0);
@@ -1015,6 +1035,13 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
       if (narrow) launch_cfg<4, 1, 32, 1>(X, Wt, Y, g, taps, stats, bnb, st);
       else launch_cfg<2, 2, 32, 1>(X, Wt, Y, g, taps, stats, bnb, st);
     }
+    return;
+  }
+  if (!bnb.part && use_conv_gemm(g, taps)) {
+    dtf_gemm_conv(X, Wt, Y, g.N, g.H, g.W, g.C, g.P, g.Q, g.sh, g.sw, g.Kout, taps.n, taps.dh,
+                  taps.dw, g.Ho, g.Wo, g.osh, g.osw, g.oh0, g.ow0, stats,
+                  g.acc == 1 ? Y : nullptr, g.acc == 2 ? g.acc_src : nullptr,
+                  g.acc == 2 ? g.acc_mask : nullptr, st);
     return;
   }
   if (!bnb.part && !epi && use_halo(g, taps)) {

@@ -41,6 +41,11 @@ struct GemmArgs {
   float* stats;           // BatchNorm partial sums of the bf16 outputs: [tiles_m][2][N] or null
   const bf16_t* acc_src;  // C += acc_src * relu_bit (a residual BN's masked dy; conv acc mode 2)
   const uint8_t* acc_mask;//   1 bit per element, 1 byte per 8 channels ([M][N] dense C only)
+  // implicit-GEMM convolution (CONV kernels): A = the NHWC input X [N][H][W][C] read through a
+  // tap table; row m = output pixel (n, p, q), K index = tap * C + channel (C % 64 == 0)
+  int H, W, Cc, P, Q, sh, sw, ntaps;
+  int tdh[9], tdw[9];
+  int Ho, Wo, osh, osw, oh0, ow0;   // output rows: (n, p*osh + oh0, q*osw + ow0) of [N][Ho][Wo]
 };
 
 // chunk swizzle of a [rows][BK] bf16 tile: 16-row ds_read_b128 fragment reads hit 16 slots
@@ -86,7 +91,8 @@ struct GCfg {
 // SCHED 1 (BK 64, NS 2): fragments double-buffered in registers and the barrier moved between
 // the two halves -- the reads of half 1 fly under the MFMAs of half 0, the reads of the next
 // step's half 0 under the MFMAs of half 1, so no wave waits on LDS latency at a phase start.
-template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1>
+template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1,
+          int CONV = 0>
 __global__ void __launch_bounds__(NW * 64, 1)
 gemm_nt_kernel(const GemmArgs g) {
   using Cf = GCfg<BM, BN, BK, NS, NW>;
@@ -105,7 +111,14 @@ gemm_nt_kernel(const GemmArgs g) {
 
   // descriptors based at this block's first row / column: 32-bit offsets span one panel only
   const int rows_a = min(BM, g.M - m0), rows_b = min(BN, g.N - n0);
-  const i32x4_t ra = rsrc_quad(g.A + (long)m0 * g.lda, (uint32_t)((long)(rows_a - 1) * g.lda + g.K) * 2u);
+  // CONV: the A descriptor spans the input images this tile's output rows come from
+  const int PQc = CONV ? g.P * g.Q : 1;
+  const int n_lo = CONV ? m0 / PQc : 0;
+  const long img = CONV ? (long)g.H * g.W * g.Cc : 0;
+  const i32x4_t ra =
+      CONV ? rsrc_quad(g.A + n_lo * img,
+                       (uint32_t)(((m0 + rows_a - 1) / PQc - n_lo + 1) * img * 2))
+           : rsrc_quad(g.A + (long)m0 * g.lda, (uint32_t)((long)(rows_a - 1) * g.lda + g.K) * 2u);
   const i32x4_t rb = rsrc_quad(g.B + (long)n0 * g.ldb, (uint32_t)((long)(rows_b - 1) * g.ldb + g.K) * 2u);
   const uint32_t lds0 = lds_addr(lds);
 
@@ -184,29 +197,45 @@ gemm_nt_kernel(const GemmArgs g) {
     // barrier | MFMAs | barrier}.  The wave rows (wm = 1) run ONE barrier behind the wm = 0
     // waves, so on every SIMD (one wave of each group) one wave is in its MFMA section while the
     // other reads LDS and issues DMAs -- the two barriers per phase enforce the alternation.
-    //   reads:  q0: A-top(t)  q1: B-right(t)  q2: A-bottom(t)  q3: B-left(t+1) (8/4/8/4 reads:
-    //           the load section of every phase fits under the other group's 16 MFMAs)
+    //   reads:  q0: B-left + A-top   q1: B-right   q2: A-bottom   q3: -
     //   DMA pieces issued:  q0: (t+1).B-right  q1: (t+1).A-bottom  q2: (t+2).A-top  q3: (t+2).B-left
-    // RAW: a piece is waited (counted vmcnt: q0/q1/q3 leave the 4 youngest pieces in flight, q2
-    // the 3 youngest) in the phase BEFORE the one that reads it, ahead of that phase's first
-    // barrier -- with the one-barrier stagger every reader then passes a barrier that follows
-    // every issuer's wait.  WAR: a region is restaged >= 2 phases after its last read (reads
-    // retire by lgkmcnt(0) right after the reading phase's first barrier).
+    // (reading the next step's B-left in q3 instead balances the reads 8/4/8/4 but costs 16
+    // more VGPRs for a second B-left set and measured the same.)
+    // RAW: a piece is waited (vmcnt(8): the 4 youngest pieces may fly) in the phase BEFORE the
+    // one that reads it, ahead of that phase's first barrier -- with the one-barrier stagger
+    // every reader then passes a barrier that follows every issuer's wait.  WAR: a region is
+    // restaged >= 2 phases after its last read (reads retire by lgkmcnt(0) right after the
+    // reading phase's first barrier).
     static_assert(BM == 256 && BN == 256 && BK == 64 && NS == 2 && NW == 8, "SCHED 2 geometry");
     // piece p, instruction j: this wave's 8-row group (first row r0) of A top (p0) / B left (p1)
     // / B right (p2) / A bottom (p3)
     uint32_t poff[4][2], plds[4][2];
     int pch[4][2];
+    // CONV: per A row (pieces 0 / 3) the input image base pixel and the top-left input (h, w)
+    // of its receptive field; invalid rows get h far out of range
+    int cpix[4][2], chw[4][2];
 #pragma unroll
     for (int pc = 0; pc < 4; ++pc)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
+        if constexpr (CONV) {
+          if (pc == 0 || pc == 3) {
+            const int r0c = pc == 0 ? j * 128 + 8 * wave : 64 + j * 128 + 8 * wave;
+            const int m = m0 + r0c + lrow;
+            const bool ok = m < g.M;
+            const int mm = ok ? m : m0;
+            const int q = mm % g.Q, t = mm / g.Q;
+            const int p = t % g.P, n = t / g.P;
+            cpix[pc][j] = (n - n_lo) * g.H * g.W;
+            chw[pc][j] = ((ok ? p * g.sh : 0x7000) << 16) | (q * g.sw);   // invalid: h far out
+          }
+        }
         const bool isA = pc == 0 || pc == 3;
         const int r0 = pc == 0 ? j * 128 + 8 * wave
                      : pc == 3 ? 64 + j * 128 + 8 * wave
                                : (2 * j + (wave >> 2)) * 64 + (pc == 2 ? 32 : 0) + (wave & 3) * 8;
         const int row = r0 + lrow;
-        const int ch = gswz<BK>(row, slot) * 8;
+        const int ch = gswz<BK>(row, slot) * 8;   // the same for every piece (rows 8k + lrow)
         pch[pc][j] = ch;
         const int rows = isA ? rows_a : rows_b;
         const int ld = isA ? g.lda : g.ldb;
@@ -221,6 +250,23 @@ gemm_nt_kernel(const GemmArgs g) {
       const bool live = kt < nk;
       const int k0 = (live ? kt : 0) * BK;
       const uint32_t base = lds0 + (uint32_t)((kt & 1) * Cf::STAGE) * 2u;
+      if constexpr (CONV) {
+        if (pc == 0 || pc == 3) {
+          // K-step -> (tap, 64-channel block): wave-uniform
+          const int cb = g.Cc / BK;
+          const int tap = (live ? kt : 0) / cb, c0 = ((live ? kt : 0) % cb) * BK;
+          const int dh = g.tdh[tap], dw = g.tdw[tap];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int h = (chw[pc][j] >> 16) + dh, w = (chw[pc][j] & 0xFFFF) + dw;
+            const bool ok = live && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+            const uint32_t off =
+                ok ? (uint32_t)(((cpix[pc][j] + h * g.W + w) * g.Cc + c0 + pch[0][0]) * 2) : kGOOB;
+            dma16(ra, base + plds[pc][j], off);
+          }
+          return;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         uint32_t off = poff[pc][j] + (uint32_t)k0 * 2u;
@@ -228,7 +274,7 @@ gemm_nt_kernel(const GemmArgs g) {
         dma16((pc == 0 || pc == 3) ? ra : rb, base + plds[pc][j], off);
       }
     };
-    bf16x8_t fA[8], fBl0[4], fBl1[4], fBr[4];
+    bf16x8_t fA[8], fBl[4], fBr[4];
     auto rdA = [&](const bf16_t* sa, int half) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -268,40 +314,32 @@ gemm_nt_kernel(const GemmArgs g) {
       if (PP_PRIO) __builtin_amdgcn_s_setprio(0);
       sync();
     };
-    // one K-step; bl holds this step's B-left fragments, bn receives the next step's
-    auto step = [&](int kt, const bf16x8_t* bl, bf16x8_t* bn) {
+    // prologue: step 0 whole + step 1's A-top / B-left; step 0's A-top / B-left landed
+    issue_piece(0, 0); issue_piece(0, 1); issue_piece(0, 2); issue_piece(0, 3);
+    issue_piece(1, 0); issue_piece(1, 1);
+    DTF_WAIT_VM(8);
+    sync();
+    if (wm == 1) sync();                       // the one-barrier stagger
+    for (int kt = 0; kt < nk; ++kt) {
       const bf16_t* cur = lds + (kt & 1) * Cf::STAGE;
-      const bf16_t* nxt = lds + ((kt + 1) & 1) * Cf::STAGE;
+      rdB(fBl, cur, 0);
+      __builtin_amdgcn_sched_barrier(0);
       rdA(cur, 0);
       issue_piece(kt + 1, 2);
       DTF_WAIT_VM(8);
-      mfma_phase(bl, 0, 0);                    // q0: top x left
+      mfma_phase(fBl, 0, 0);                   // q0: top x left
       rdB(fBr, cur, 1);
       issue_piece(kt + 1, 3);
       DTF_WAIT_VM(8);
       mfma_phase(fBr, 0, 1);                   // q1: top x right
       rdA(cur, 1);
       issue_piece(kt + 2, 0);
-      DTF_WAIT_VM(6);
+      DTF_WAIT_VM(8);
       mfma_phase(fBr, 1, 1);                   // q2: bottom x right
-      if (kt + 1 < nk) rdB(bn, nxt, 0);
       issue_piece(kt + 2, 1);
       DTF_WAIT_VM(8);
-      mfma_phase(bl, 1, 0);                    // q3: bottom x left
-    };
-    // prologue: step 0 whole + step 1's A-top / B-left; step 0's A-top / B-left landed
-    issue_piece(0, 0); issue_piece(0, 1); issue_piece(0, 2); issue_piece(0, 3);
-    issue_piece(1, 0); issue_piece(1, 1);
-    DTF_WAIT_VM(8);
-    sync();
-    rdB(fBl0, lds, 0);
-    if (wm == 1) sync();                       // the one-barrier stagger
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
-      step(kt, fBl0, fBl1);
-      step(kt + 1, fBl1, fBl0);
+      mfma_phase(fBl, 1, 0);                   // q3: bottom x left
     }
-    if (kt < nk) step(kt, fBl0, fBl1);
     if (wm == 0) sync();                       // re-align the barrier counts
   } else if constexpr (SCHED == 1) {
     static_assert(BK == 64 && NS == 2, "SCHED 1: two 32-deep halves per step, two slots");
@@ -432,7 +470,16 @@ gemm_nt_kernel(const GemmArgs g) {
     const int r = tid / OCPR + k * OROWS;
     if (!col_ok || m0 + r >= g.M) continue;
     uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::LDC + oc * 8);
-    const long off = (long)(m0 + r) * g.ldc + n0 + oc * 8;
+    long orow = m0 + r;
+    if constexpr (CONV) {
+      if (g.osh != 1 || g.osw != 1) {   // a data-gradient phase: pixel (n, p, q) of the phase grid
+        const int m = m0 + r;
+        const int q = m % g.Q, t = m / g.Q;
+        const int p = t % g.P, n = t / g.P;
+        orow = ((long)n * g.Ho + p * g.osh + g.oh0) * g.Wo + q * g.osw + g.ow0;
+      }
+    }
+    const long off = orow * g.ldc + n0 + oc * 8;
     if (g.Cin) {
       float a[8], b[8];
       unpack8(v, a);
@@ -455,23 +502,54 @@ gemm_nt_kernel(const GemmArgs g) {
 
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
 
-template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1>
+template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1,
+          int CONV = 0>
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
   using Cf = GCfg<BM, BN, BK, NS, NW>;
   static bool attr = false;
   if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cf::LDS));
+    HIP_CHECK(hipFuncSetAttribute(
+        (const void*)gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO, CONV>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cf::LDS));
     attr = true;
   }
   const long tiles = (long)((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO>), dim3((unsigned)tiles),
-                     dim3(Cf::NT), Cf::LDS, st, g);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO, CONV>),
+                     dim3((unsigned)tiles), dim3(Cf::NT), Cf::LDS, st, g);
 }
 
 }  // namespace
 
 void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
+
+// Implicit-GEMM convolution on the ping-pong GEMM: Y[M = N*P*Q][Kout] (+= Cin / masked acc)
+// = X (through the tap table) . Wt[Kout][Kpad]^T, Kpad = taps * C, C % 64 == 0, <= 9 taps.
+// Output row m = (n, p, q) lands at pixel (n, p*osh + oh0, q*osw + ow0) of [N][Ho][Wo] (the
+// phase classes of a strided data gradient; forward convs: osh = 1, Ho = P).  BN statistics
+// slab rows = dtf_gemm_tile_rows(M).
+void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, int W, int C,
+                   int P, int Q, int sh, int sw, int Kout, int ntaps, const int* dh, const int* dw,
+                   int Ho, int Wo, int osh, int osw, int oh0, int ow0,
+                   float* stats, const bf16_t* Cin, const bf16_t* acc_src,
+                   const uint8_t* acc_mask, hipStream_t st) {
+  if (C % 64 || Kout % 8 || ntaps < 1 || ntaps > 9 || H >= 16384 || W >= 32768)
+    throw std::runtime_error("gemm_conv: C % 64, Kout % 8, 1..9 taps, H < 2^14, W < 2^15");
+  const long M = (long)N * P * Q;
+  if (M >= (1L << 31) || 2.0 * H * W * C * (256.0 / (P * Q) + 2) >= 2147483647.0)
+    throw std::runtime_error("gemm_conv: tile span too large for 32-bit buffer offsets");
+  GemmArgs g{};
+  g.A = X; g.B = Wt; g.C = Y; g.Cin = Cin; g.stats = stats; g.acc_src = acc_src;
+  g.acc_mask = acc_mask;
+  g.M = (int)M; g.N = Kout; g.K = ntaps * C; g.lda = C; g.ldb = ntaps * C; g.ldc = Kout;
+  g.H = H; g.W = W; g.Cc = C; g.P = P; g.Q = Q; g.sh = sh; g.sw = sw; g.ntaps = ntaps;
+  for (int t = 0; t < ntaps; ++t) { g.tdh[t] = dh[t]; g.tdw[t] = dw[t]; }
+  g.Ho = Ho; g.Wo = Wo; g.osh = osh; g.osw = osw; g.oh0 = oh0; g.ow0 = ow0;
+  if ((osh != 1 || osw != 1) && (stats || acc_mask))
+    throw std::runtime_error("gemm_conv: strided outputs take no BN statistics / masked acc");
+  if ((long)256 * g.ldb * 2 + 2L * g.K >= (1L << 31))
+    throw std::runtime_error("gemm_conv: filter too large");
+  launch_gemm<256, 256, 64, 2, 2, 8, 1, 1>(g, st);
+}
 
 // block-tile rows of every variant (the BatchNorm statistics slab has one row per M tile)
 int dtf_gemm_tile_rows(int M) { return (M + 255) / 256; }

@@ -405,3 +405,49 @@ def test_wgrad_pingpong_kernel(case):
     ref.conv2d(x.float(), wr, stride, pad).backward(dy.float())
     assert _rel(pp, wr.grad) < 1e-3, _rel(pp, wr.grad)
     assert _rel(pp, old) < 1e-4, _rel(pp, old)
+
+
+CONV_GEMM_CASES = [
+    (2, 14, 14, 256, 256, 3, 1, 1),
+    (3, 9, 11, 128, 384, 3, 1, 1),       # partial tiles, image edges in every tile
+    (2, 28, 28, 256, 256, 3, 2, 1),      # strided: forward + the 4 dgrad phase classes
+    (4, 7, 7, 512, 512, 3, 1, 1),
+    (2, 14, 14, 512, 256, 1, 2, 0),      # 1x1 stride-2 projection: one dgrad phase, rest zero
+]
+
+
+@pytest.mark.parametrize("case", CONV_GEMM_CASES)
+def test_conv_implicit_gemm_route(case):
+    """Convs with C % 64 == 0 and Kout >= 256 on the ping-pong GEMM (implicit-GEMM A loader;
+    strided data gradients as phase classes with remapped output rows): forward and data
+    gradient vs the fp32 reference and vs the conv kernels, plus the BatchNorm statistics."""
+    N, H, W, C, K, R, stride, pad = case
+    nat, ref = _native(), _ref()
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(K, R, R, C, device=dev) / (R * R * C) ** 0.5
+    outs = []
+    try:
+        for route in (1, 0):
+            nat._K.conv_set_gemm(route)
+            xn = x.clone().requires_grad_(True)
+            wn = w.clone().requires_grad_(True)
+            yn = nat.conv2d(xn, wn, stride, pad, bn_stats=True)
+            g = torch.randn(yn.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(1)).bfloat16()
+            yn.backward(g)
+            part = yn._dtf_bn_part
+            outs.append((yn.detach(), xn.grad, wn.grad, part))
+    finally:
+        nat._K.conv_set_gemm(1)
+    (y1, dx1, dw1, p1), (y0, dx0, dw0, p0) = outs
+    xr = x.float().requires_grad_(True)
+    yr = ref.conv2d(xr, w.to(torch.bfloat16).float(), stride, pad)
+    yr.backward(g.float())
+    assert _rel(y1, yr) < 1e-2 and _rel(y1, y0) < 1e-2
+    assert _rel(dx1, xr.grad) < 2e-2 and _rel(dx1, dx0) < 2e-2
+    # BN statistics: per-channel sums of the bf16 outputs, whatever the slab's row count
+    pt, G = p1[0], p1[1]
+    s1 = pt[:G * 2 * K].view(G, 2, K).double().sum(0)
+    yf = y1.double().reshape(-1, K)
+    torch.testing.assert_close(s1[0], yf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(s1[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
