@@ -71,7 +71,30 @@ DTF_DEV void load8f(const float* __restrict__ p, int cg, float* v) {
 // MODE 0: forward stats   acc0 += x,           acc1 += x*x
 // MODE 1: backward reduce acc0 += dz,          acc1 += dz*(x-mean)*invstd
 // mkind (MODE 1): 0 no ReLU, 1 bit mask, 2 recompute from x, 3 from y
-template <int MODE, int MK>
+// 16-B streaming accesses; NT: non-temporal (the tensors are far larger than L2 / MALL and
+// every byte is touched once per pass)
+typedef uint32_t u32x4_nt __attribute__((ext_vector_type(4)));
+template <bool NT>
+DTF_DEV uint4 ldv(const uint4* p) {
+  if constexpr (NT) {
+    const u32x4_nt v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *p;
+  }
+}
+template <bool NT>
+DTF_DEV void stv(uint4* p, const uint4& v) {
+  if constexpr (NT) {
+    const u32x4_nt w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_nt*>(p));
+  } else {
+    *p = v;
+  }
+}
+static int g_bn_nt = 7;   // bit 0 apply, 1 bwd apply, 2 bwd reduce (tools/bn_bench.py --nt A/B: -6..8 %)
+
+template <int MODE, int MK, bool NT = false>
 __global__ void __launch_bounds__(kThreads)
 bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                  const bf16_t* __restrict__ y, const uint8_t* __restrict__ mask,
@@ -106,9 +129,9 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
         const int r = m + u * rpi;
         const uint32_t v = (uint32_t)r * tpr + cg;
         const bool ok = r < m1;
-        xr[u] = ok ? X4[v] : make_uint4(0, 0, 0, 0);
+        xr[u] = ok ? ldv<NT>(X4 + v) : make_uint4(0, 0, 0, 0);
         if (MODE == 1) {
-          dr[u] = ok ? D4[v] : make_uint4(0, 0, 0, 0);
+          dr[u] = ok ? ldv<NT>(D4 + v) : make_uint4(0, 0, 0, 0);
           mb[u] = (ok && MK == 1) ? (uint32_t)mask[v] : 0u;
           yr[u] = (ok && MK == 3) ? Y4[v] : make_uint4(0, 0, 0, 0);
         }
@@ -245,8 +268,10 @@ __global__ void bn_infer_finalize_kernel(int C, const float* __restrict__ gamma,
   shift[c] = beta[c] - run_mean[c] * gamma[c] * is;
 }
 
+
 // y = [relu](x*scale + shift [+ res]); with `mask` also the ReLU bit mask (bit i of byte v =
 // element 8v+i > 0) the backward reads instead of y.
+template <bool NT>
 __global__ void __launch_bounds__(kThreads)
 bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                 bf16_t* __restrict__ y, uint8_t* __restrict__ mask,
@@ -269,8 +294,8 @@ bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
       const int r = m + u * rpi;
       const uint32_t v = (uint32_t)r * tpr + cg;
       if (r < M) {
-        xr[u] = X4[v];
-        if (res) rr[u] = R4[v];
+        xr[u] = ldv<NT>(X4 + v);
+        if (res) rr[u] = ldv<NT>(R4 + v);
       }
     }
 #pragma unroll
@@ -293,7 +318,7 @@ bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
         for (int i = 0; i < 8; ++i) o[i] = fmaxf(o[i], 0.f);
       }
       const uint4 packed = pack8(o);
-      Y4[v] = packed;
+      stv<NT>(Y4 + v, packed);
       if (mask) {
         // the mask is taken from the ROUNDED output, exactly what a y-based mask would see
         float ov[8];
@@ -328,7 +353,7 @@ bn_bwd_finalize_kernel(const double* __restrict__ level2, int S, int C, long M,
   coefC[c] = -k * db * invM - B * mean[c];
 }
 
-template <int MK>
+template <int MK, bool NT>
 __global__ void __launch_bounds__(kThreads)
 bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                     const uint8_t* __restrict__ mask, const bf16_t* __restrict__ x,
@@ -358,8 +383,8 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
       const int r = m + u * rpi;
       const uint32_t v = (uint32_t)r * tpr + cg;
       if (r < M) {
-        dr[u] = D4[v];
-        xr[u] = X4[v];
+        dr[u] = ldv<NT>(D4 + v);
+        xr[u] = ldv<NT>(X4 + v);
         if (MK == 1) mb[u] = mask[v];
         if (MK == 3) yr[u] = Y4[v];
       }
@@ -374,10 +399,10 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
       unpack8(xr[u], xv);
       relu_mask8(g, xv, MK == 1 ? mb[u] : 0u, MK == 3 ? yr[u] : make_uint4(0, 0, 0, 0),
                  MK, ksc, ksh);
-      if (dres) DR4[v] = pack8(g);
+      if (dres) stv<NT>(DR4 + v, pack8(g));
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = ka[i] * g[i] + kb[i] * xv[i] + kc[i];
-      DX4[v] = pack8(o);
+      stv<NT>(DX4 + v, pack8(o));
     }
   }
 }
@@ -494,9 +519,15 @@ void dtf_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, uint8_t* mask,
                   const float* scale, const float* shift, long M, int C, int relu,
                   hipStream_t st) {
   check_rows(M, C);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, x, res, y,
-                     mask, scale, shift, (int)M, C, relu);
+  if (g_bn_nt & 1)
+    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, x,
+                       res, y, mask, scale, shift, (int)M, C, relu);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, x,
+                       res, y, mask, scale, shift, (int)M, C, relu);
 }
+
+void dtf_bn_set_nt(int v) { g_bn_nt = v; }
 
 void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16_t* x,
                        const float* mean, const float* invstd, long M, int C, int relu,
@@ -509,8 +540,12 @@ void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, c
   const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
   // mask kind is a template parameter: the unused mask operands take no registers
 #define DTF_BN_RED(MK_)                                                                    \
-  hipLaunchKernelGGL((bn_reduce_kernel<1, MK_>), dim3(G), dim3(kThreads), lds, st, x, dy, y, mask, \
-                     mean, invstd, (int)M, C, rpb, mk, partial, fsc, fsh)
+  if (g_bn_nt & 4)                                                                         \
+    hipLaunchKernelGGL((bn_reduce_kernel<1, MK_, true>), dim3(G), dim3(kThreads), lds, st, x, dy, \
+                       y, mask, mean, invstd, (int)M, C, rpb, mk, partial, fsc, fsh);          \
+  else                                                                                     \
+    hipLaunchKernelGGL((bn_reduce_kernel<1, MK_>), dim3(G), dim3(kThreads), lds, st, x, dy, y,   \
+                       mask, mean, invstd, (int)M, C, rpb, mk, partial, fsc, fsh)
   switch (mk) {
     case 0: DTF_BN_RED(0); break;
     case 1: DTF_BN_RED(1); break;
@@ -553,8 +588,12 @@ void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, co
   check_rows(M, C);
   const int mk = mask_kind(relu, mask, fsc, fsh, y);
 #define DTF_BN_BWD(MK_)                                                                    \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_>), dim3(sweep_grid(M, C)), dim3(kThreads), 0, st,   \
-                     dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh)
+  if (g_bn_nt & 2)                                                                         \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_, true>), dim3(sweep_grid(M, C)), dim3(kThreads), \
+                       0, st, dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh);  \
+  else                                                                                     \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_, false>), dim3(sweep_grid(M, C)), dim3(kThreads), \
+                       0, st, dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh)
   switch (mk) {
     case 0: DTF_BN_BWD(0); break;
     case 1: DTF_BN_BWD(1); break;

@@ -111,6 +111,7 @@ void dtf_wgrad_set_dma_mode(int);
 void dtf_wgrad_set_pipe(int);
 void dtf_wgrad_set_pp(int);
 void dtf_conv_set_gemm(int);
+void dtf_bn_set_nt(int);
 int dtf_wgrad_get_pipe();
 void dtf_lds_probe(int, int, int*, int, hipStream_t);
 int dtf_max_dynamic_lds(int);
@@ -578,6 +579,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("wgrad_set_pipe", &dtf_wgrad_set_pipe);
   m.def("wgrad_set_pp", &dtf_wgrad_set_pp);
   m.def("conv_set_gemm", &dtf_conv_set_gemm);
+  m.def("bn_set_nt", &dtf_bn_set_nt);
   m.def("wgrad_get_pipe", &dtf_wgrad_get_pipe);
   m.def("lds_probe", [](int bytes, int blocks, uintptr_t errors, int spin, uintptr_t st) {
     dtf_lds_probe(bytes, blocks, P<int>(errors), spin, S(st));

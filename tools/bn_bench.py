@@ -59,7 +59,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--nt", type=int, default=7, help="bn_set_nt bitmask: 1 apply, 2 bwd apply, 4 reduce")
     args = ap.parse_args()
+    K.bn_set_nt(args.nt)
     dev = torch.device("cuda")
     st = torch.cuda.current_stream().cuda_stream
     rows, tot = [], {"apply": 0.0, "reduce": 0.0, "bwd_apply": 0.0, "copy": 0.0}
