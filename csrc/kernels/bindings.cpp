@@ -25,6 +25,7 @@ struct ConvGeom {
   const uint8_t* acc_mask;
   const float* bias;
   int relu;
+  int nt;
 };
 struct BnBwdEpi {
   const bf16_t* x; const float* mean; const float* invstd; const float* fsc; const float* fsh;
@@ -112,6 +113,8 @@ void dtf_wgrad_set_pipe(int);
 void dtf_wgrad_set_pp(int);
 void dtf_conv_set_gemm(int);
 void dtf_bn_set_nt(int);
+void dtf_conv_set_nt(int);
+void dtf_gemm_set_nt(int);
 int dtf_wgrad_get_pipe();
 void dtf_lds_probe(int, int, int*, int, hipStream_t);
 int dtf_max_dynamic_lds(int);
@@ -580,6 +583,8 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("wgrad_set_pp", &dtf_wgrad_set_pp);
   m.def("conv_set_gemm", &dtf_conv_set_gemm);
   m.def("bn_set_nt", &dtf_bn_set_nt);
+  m.def("conv_set_nt", &dtf_conv_set_nt);
+  m.def("gemm_set_nt", &dtf_gemm_set_nt);
   m.def("wgrad_get_pipe", &dtf_wgrad_get_pipe);
   m.def("lds_probe", [](int bytes, int blocks, uintptr_t errors, int spin, uintptr_t st) {
     dtf_lds_probe(bytes, blocks, P<int>(errors), spin, S(st));

@@ -42,6 +42,18 @@ DTF_DEV uint4 pack8(const float* f) {
   return r;
 }
 
+// 16-B store, non-temporal when `nt` (a wave-uniform flag): outputs written once and read by a
+// later kernel pass, far larger than L2 / MALL
+typedef uint32_t u32x4_st __attribute__((ext_vector_type(4)));
+DTF_DEV void st16(void* p, const uint4& v, bool nt) {
+  if (nt) {
+    const u32x4_st w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_st*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+
 DTF_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

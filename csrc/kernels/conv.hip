@@ -59,6 +59,7 @@ struct ConvGeom {
   const uint8_t* acc_mask;  // acc 2: that BN's forward ReLU bit mask (1 byte per 8 channels)
   const float* bias;        // fused epilogue (register kernel only): Y = act(conv + bias[k])
   int relu;                 //   tf.layers.conv2d(activation=tf.nn.relu) -- MNIST K3/K5
+  int nt;                   // non-temporal output stores (set by dtf_conv_igemm)
 };
 
 // Residual-gradient accumulation in the dgrad epilogue.  acc 1 reads the materialised residual
@@ -451,7 +452,7 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     uint4 v = *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
     // fused residual-gradient add: one extra 16-B read instead of an add kernel
     if (g.acc) v = acc_add8(g, Y, off, v);
-    *reinterpret_cast<uint4*>(Y + off) = v;
+    st16(Y + off, v, g.nt);
     if constexpr (BNB) ba.add_pre(bnb, v, xpre[k], (mpre[k >> 2] >> (8 * (k & 3))) & 0xFFu);
   }
   if constexpr (BNB)
@@ -712,7 +713,7 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
     const bf16_t* st = r < 128 ? s0 : s1;
     uint4 v = *reinterpret_cast<const uint4*>(st + (r & 127) * LDC + oc * 8);
     if (g.acc) v = acc_add8(g, Y, off, v);
-    *reinterpret_cast<uint4*>(Y + off) = v;
+    st16(Y + off, v, g.nt);
     if constexpr (BNB) ba.add_pre(bnb, v, xpre[k], mpre[k]);
   }
   if constexpr (BNB)   // [32][2][128] floats = 32 KB in the third stage buffer
@@ -903,8 +904,8 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   const bool col_ok = n0 + oc * 8 < g.Kout;
   for (int r = tid / OCPR; r < H::M; r += kThreads / OCPR) {
     if (!col_ok) continue;
-    *reinterpret_cast<uint4*>(Y + (ybase + r) * g.Kout + n0 + oc * 8) =
-        *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
+    st16(Y + (ybase + r) * g.Kout + n0 + oc * 8,
+         *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8), g.nt);
   }
   if (stats) {   // per-channel sum / sum of squares of the rounded outputs -> slab row tm
     constexpr int GROUPS = kThreads / NT;
@@ -1006,9 +1007,14 @@ int dtf_conv_tile_rows(const ConvGeom& g, const TapTable& taps) {
   return dtf_conv_stats_rows(M, g.Kout, g.C, taps.n, 0);
 }
 
-void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
+static int g_conv_nt = 0;   // measured neutral on ResNet-50 b2048 (DTF_STORE_NT A/B)
+void dtf_conv_set_nt(int v) { g_conv_nt = v; }
+
+void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g_in,
                     const TapTable& taps, int bk, float* stats, const BnBwdEpi& bnb,
                     hipStream_t st) {
+  ConvGeom g = g_in;
+  g.nt = g_conv_nt;
   if (bnb.part && (stats || !bnb.x || !bnb.mean || !bnb.invstd ||
                    (bnb.mkind == 1 && !bnb.mask) || (bnb.mkind == 2 && !(bnb.fsc && bnb.fsh))))
     throw std::runtime_error("conv: bad fused BN-backward epilogue arguments");

@@ -46,6 +46,7 @@ struct GemmArgs {
   int H, W, Cc, P, Q, sh, sw, ntaps;
   int tdh[9], tdw[9];
   int Ho, Wo, osh, osw, oh0, ow0;   // output rows: (n, p*osh + oh0, q*osw + ow0) of [N][Ho][Wo]
+  int nt;                           // non-temporal C stores
 };
 
 // chunk swizzle of a [rows][BK] bf16 tile: 16-row ds_read_b128 fragment reads hit 16 slots
@@ -496,11 +497,12 @@ gemm_nt_kernel(const GemmArgs g) {
       for (int e = 0; e < 8; ++e) a[e] += (mb >> e) & 1u ? b[e] : 0.f;
       v = pack8(a);
     }
-    *reinterpret_cast<uint4*>(g.C + off) = v;
+    st16(g.C + off, v, g.nt);
   }
 }
 
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
+int g_gemm_nt = 0;         // non-temporal C stores (ResNet-50 A/B: neutral; off keeps BERT outputs cached)
 
 template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1,
           int CONV = 0>
@@ -521,6 +523,7 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
 }  // namespace
 
 void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
+void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
 
 // Implicit-GEMM convolution on the ping-pong GEMM: Y[M = N*P*Q][Kout] (+= Cin / masked acc)
 // = X (through the tap table) . Wt[Kout][Kpad]^T, Kpad = taps * C, C % 64 == 0, <= 9 taps.
@@ -544,6 +547,7 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
   g.H = H; g.W = W; g.Cc = C; g.P = P; g.Q = Q; g.sh = sh; g.sw = sw; g.ntaps = ntaps;
   for (int t = 0; t < ntaps; ++t) { g.tdh[t] = dh[t]; g.tdw[t] = dw[t]; }
   g.Ho = Ho; g.Wo = Wo; g.osh = osh; g.osw = osw; g.oh0 = oh0; g.ow0 = ow0;
+  g.nt = g_gemm_nt;
   if ((osh != 1 || osw != 1) && (stats || acc_mask))
     throw std::runtime_error("gemm_conv: strided outputs take no BN statistics / masked acc");
   if ((long)256 * g.ldb * 2 + 2L * g.K >= (1L << 31))
@@ -568,6 +572,7 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
   if (acc_mask && (!acc_src || Cin || ldc != N))
     throw std::runtime_error("gemm_nt: masked accumulation needs acc_src and a dense C");
   GemmArgs g{A, B, C, bias, Cin, M, N, K, lda, ldb, ldc, relu, stats, acc_src, acc_mask};
+  g.nt = g_gemm_nt;
   // auto: 256 x 128 tiles when N <= 128 (measured 1.02-1.07x the 256 x 256 tile on the N = 128
   // ResNet 1x1 convs, profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl)
   const int variant = g_gemm_variant >= 0 ? g_gemm_variant : (N <= 128 ? 1 : 8);

@@ -40,6 +40,11 @@ if os.environ.get("DTF_CONV_HALO"):
     _K.conv_set_halo(int(os.environ["DTF_CONV_HALO"]))
 if os.environ.get("DTF_CONV_SMALL_K"):
     _K.conv_set_small_k(int(os.environ["DTF_CONV_SMALL_K"]))
+if os.environ.get("DTF_STORE_NT"):      # non-temporal output stores: bit 0 conv, 1 GEMM, 2 BN
+    _nt = int(os.environ["DTF_STORE_NT"])
+    _K.conv_set_nt(_nt & 1)
+    _K.gemm_set_nt((_nt >> 1) & 1)
+    _K.bn_set_nt(7 if _nt & 4 else 0)
 
 
 def _st():
