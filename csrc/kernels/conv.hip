@@ -988,7 +988,10 @@ static bool use_conv_gemm(const ConvGeom& g, const TapTable& taps) {
   const bool unit = g.osh == 1 && g.osw == 1 && g.oh0 == 0 && g.ow0 == 0 && g.Ho == g.P &&
                     g.Wo == g.Q;
   // strided-dgrad phase classes qualify too (any tap count, no masked-residual epilogue)
-  return g_conv_gemm && g.C % 64 == 0 && g.Kout >= 256 && g.Kout % 8 == 0 && taps.n <= 9 &&
+  // bit 1: also 64 < Kout <= 128 on the 256 x 128 ping-pong tile -- measured SLOWER than the
+  // halo / register kernels (profiles/measurements/r2_conv_kout128_pingpong_ab.txt), off
+  const bool wide = g.Kout >= 256 || ((g_conv_gemm & 2) && g.Kout > 64 && g.Kout <= 128);
+  return (g_conv_gemm & 1) && g.C % 64 == 0 && wide && g.Kout % 8 == 0 && taps.n <= 9 &&
          (unit ? taps.n > 1 : g.acc != 2) && g.Kpad == taps.n * g.C && !g.bias && !g.relu &&
          g.H < 16384 && g.W < 32768;
 }

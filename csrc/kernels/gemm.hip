@@ -342,6 +342,132 @@ gemm_nt_kernel(const GemmArgs g) {
       mfma_phase(fBl, 1, 0);                   // q3: bottom x left
     }
     if (wm == 0) sync();                       // re-align the barrier counts
+  } else if constexpr (SCHED == 3) {
+    // 256 x 128 ping-pong (N <= 128): 8 waves as 4 (M) x 2 (N) of 64 x 64, three 48-KB LDS
+    // slots; each 64-deep K-step is 2 phases, one per 32-row half of the wave tile (2 x 4 x 2 =
+    // 16 MFMAs), waves 4-7 one barrier behind waves 0-3 (one wave of each group per SIMD).
+    //   reads:  q0: B + A-top   q1: A-bottom
+    //   pieces issued in step t:  q0: (t+2).A-top + (t+2).B   q1: (t+2).A-bottom
+    // RAW: A-top/B of step t+1 are waited (vmcnt(8)) in t.q1, A-bottom of step t (vmcnt(10))
+    // in t.q0 -- always the phase before the reader.  WAR: step t+2 reuses step t-1's slot,
+    // whose regions were last read 2 phases before they are restaged.
+    static_assert(BM == 256 && BN == 128 && BK == 64 && NS == 3 && NW == 8, "SCHED 3 geometry");
+    const int grp = wave >> 2;
+    uint32_t poff[3][2], plds[3][2];
+    int pch[3][2], cpix[3][2], chw[3][2];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool isA = pc != 1;
+        const int r0 = pc == 1 ? j * 64 + 8 * wave
+                               : (2 * j + (wave >> 2)) * 64 + (pc == 2 ? 32 : 0) + (wave & 3) * 8;
+        const int row = r0 + lrow;
+        const int ch = gswz<BK>(row, slot) * 8;
+        pch[pc][j] = ch;
+        const int rows = isA ? rows_a : rows_b;
+        const int ld = isA ? g.lda : g.ldb;
+        poff[pc][j] = row < rows ? (uint32_t)(row * ld + ch) * 2u : 0x80000000u;
+        plds[pc][j] = (uint32_t)((isA ? 0 : Cf::SA) + r0 * BK) * 2u;
+        cpix[pc][j] = chw[pc][j] = 0;
+        if constexpr (CONV) {
+          if (isA) {
+            const int m = m0 + row;
+            const bool ok = m < g.M;
+            const int mm = ok ? m : m0;
+            const int q = mm % g.Q, t = mm / g.Q;
+            const int p = t % g.P, n = t / g.P;
+            cpix[pc][j] = (n - n_lo) * g.H * g.W;
+            chw[pc][j] = ((ok ? p * g.sh : 0x7000) << 16) | (q * g.sw);
+          }
+        }
+      }
+    const bool ktail = (g.K % BK) != 0;
+    auto issue_piece = [&](int kt, int pc) {
+      const bool live = kt < nk;
+      const int k0 = (live ? kt : 0) * BK;
+      const uint32_t base = lds0 + (uint32_t)((kt % 3) * Cf::STAGE) * 2u;
+      if constexpr (CONV) {
+        if (pc != 1) {
+          const int cb = g.Cc / BK;
+          const int tap = (live ? kt : 0) / cb, c0 = ((live ? kt : 0) % cb) * BK;
+          const int dh = g.tdh[tap], dw = g.tdw[tap];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int h = (chw[pc][j] >> 16) + dh, w = (chw[pc][j] & 0xFFFF) + dw;
+            const bool ok = live && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+            const uint32_t off =
+                ok ? (uint32_t)(((cpix[pc][j] + h * g.W + w) * g.Cc + c0 + pch[pc][j]) * 2) : kGOOB;
+            dma16(ra, base + plds[pc][j], off);
+          }
+          return;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        uint32_t off = poff[pc][j] + (uint32_t)k0 * 2u;
+        if (ktail && k0 + pch[pc][j] >= g.K) off = kGOOB;
+        dma16(pc != 1 ? ra : rb, base + plds[pc][j], off);
+      }
+    };
+    bf16x8_t fA[4], fB[8];
+    auto rdA = [&](const bf16_t* sa, int half) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = wm * 64 + half * 32 + i * 16 + frow, ch = ks * 4 + fq;
+          fA[ks * 2 + i] = *reinterpret_cast<const bf16x8_t*>(sa + r * BK + gswz<BK>(r, ch) * 8);
+        }
+    };
+    auto rdB = [&](const bf16_t* sa) {
+      const bf16_t* sb = sa + Cf::SA;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = wn * 64 + j * 16 + frow, ch = ks * 4 + fq;
+          fB[ks * 4 + j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
+        }
+    };
+    auto sync = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mfma_phase = [&](int half) {
+      sync();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[half * 2 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fA[ks * 2 + i], fB[ks * 4 + j], acc[half * 2 + i][j], 0, 0, 0);
+      sync();
+    };
+    issue_piece(0, 0); issue_piece(0, 1); issue_piece(0, 2);
+    issue_piece(1, 0); issue_piece(1, 1); issue_piece(1, 2);
+    DTF_WAIT_VM(8);                            // step 0's A-top / B landed
+    sync();
+    if (grp == 1) sync();                      // the one-barrier stagger
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* cur = lds + (kt % 3) * Cf::STAGE;
+      rdB(cur);
+      __builtin_amdgcn_sched_barrier(0);
+      rdA(cur, 0);
+      issue_piece(kt + 2, 0);
+      issue_piece(kt + 2, 1);
+      DTF_WAIT_VM(10);                         // this step's A-bottom landed
+      mfma_phase(0);
+      rdA(cur, 1);
+      issue_piece(kt + 2, 2);
+      DTF_WAIT_VM(8);                          // the next step's A-top / B landed
+      mfma_phase(1);
+    }
+    if (grp == 0) sync();
   } else if constexpr (SCHED == 1) {
     static_assert(BK == 64 && NS == 2, "SCHED 1: two 32-deep halves per step, two slots");
     bf16x8_t fa0[Cf::FM], fb0[Cf::FN], fa1[Cf::FM], fb1[Cf::FN];
@@ -552,7 +678,8 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
     throw std::runtime_error("gemm_conv: strided outputs take no BN statistics / masked acc");
   if ((long)256 * g.ldb * 2 + 2L * g.K >= (1L << 31))
     throw std::runtime_error("gemm_conv: filter too large");
-  launch_gemm<256, 256, 64, 2, 2, 8, 1, 1>(g, st);
+  if (Kout <= 128) launch_gemm<256, 128, 64, 3, 3, 8, 1, 1>(g, st);
+  else launch_gemm<256, 256, 64, 2, 2, 8, 1, 1>(g, st);
 }
 
 // block-tile rows of every variant (the BatchNorm statistics slab has one row per M tile)
@@ -586,6 +713,7 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
     case 7: launch_gemm<256, 256, 32, 4, 0, 4>(g, st); break;
     case 8: launch_gemm<256, 256, 64, 2, 2>(g, st); break;
     case 9: launch_gemm<256, 256, 64, 2, 2, 8, 0>(g, st); break;
+    case 10: launch_gemm<256, 128, 64, 3, 3>(g, st); break;
     default: launch_gemm<256, 256, 64, 2>(g, st); break;
   }
 }

@@ -251,9 +251,10 @@ def test_gemm_bn_stats_and_masked_residual_epilogues():
 @pytest.mark.parametrize("M,N,K", [(1000, 776, 200), (4096, 2304, 768), (300, 264, 1000),
                                    (513, 512, 64), (256, 256, 4096)])
 def test_gemm_pingpong_schedule_bit_identical(M, N, K):
-    """The ping-pong (two-group, barrier-staggered) K-loop of gemm.hip (variant 8) accumulates
-    every output in the same MFMA order as the default pipeline: results must be bit-identical,
-    with bias+ReLU, with Cin accumulation, and on M / N / K tails."""
+    """The ping-pong (two-group, barrier-staggered) K-loops of gemm.hip -- variant 8 (256 x 256)
+    and variant 10 (256 x 128, three LDS slots) -- accumulate every output in the same MFMA
+    order as the default pipeline: results must be bit-identical, with bias+ReLU, with Cin
+    accumulation, and on M / N / K tails."""
     from distributedtensorflow_amd.ops import native
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
@@ -262,14 +263,15 @@ def test_gemm_pingpong_schedule_bit_identical(M, N, K):
     cin = torch.randn(M, N, device="cuda", generator=g).bfloat16()
     outs = []
     try:
-        for v in (0, 8):
+        for v in (0, 8, 10):
             native._K.gemm_set_variant(v)
             outs.append((native.gemm_nt(a, b), native.gemm_nt(a, b, bias=bias, relu=True),
                          native.gemm_nt(a, b, cin=cin.clone())))
     finally:
         native._K.gemm_set_variant(-1)
-    for x, y in zip(*outs):
-        assert torch.equal(x, y)
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert torch.equal(x, y)
     ref = a.float() @ b.float().t()
     assert ((outs[1][0].float() - ref).norm() / ref.norm()).item() < 1e-2
 

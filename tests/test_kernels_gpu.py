@@ -408,6 +408,8 @@ def test_wgrad_pingpong_kernel(case):
 
 
 CONV_GEMM_CASES = [
+    (2, 28, 28, 128, 128, 3, 1, 1),      # Kout 128: the 256 x 128 ping-pong tile
+    (3, 15, 13, 128, 128, 3, 2, 1),      #   strided, odd sizes
     (2, 14, 14, 256, 256, 3, 1, 1),
     (3, 9, 11, 128, 384, 3, 1, 1),       # partial tiles, image edges in every tile
     (2, 28, 28, 256, 256, 3, 2, 1),      # strided: forward + the 4 dgrad phase classes
@@ -428,7 +430,7 @@ def test_conv_implicit_gemm_route(case):
     w = torch.randn(K, R, R, C, device=dev) / (R * R * C) ** 0.5
     outs = []
     try:
-        for route in (1, 0):
+        for route in (3, 0):
             nat._K.conv_set_gemm(route)
             xn = x.clone().requires_grad_(True)
             wn = w.clone().requires_grad_(True)

@@ -72,8 +72,12 @@ def main():
     ap.add_argument("--wgrad-pp", type=int, default=1,
                     help="wgrad_set_pp: 0 off, n > 0: 256 x 256 ping-pong kernel for Kout, T*C >= 256 "
                          "with a split-K target of n rounds of 256 blocks")
+    ap.add_argument("--conv-gemm", type=int, default=1,
+                    help="conv_set_gemm bitmask: 1 implicit-GEMM route for Kout >= 256, 2 also "
+                         "for 64 < Kout <= 128 (256 x 128 tile)")
     args = ap.parse_args()
     native._K.wgrad_set_pp(args.wgrad_pp)
+    native._K.conv_set_gemm(args.conv_gemm)
     native._K.conv_set_dma_mode(args.dma)
     native._K.wgrad_set_dma_mode(args.wgrad_mode)
     if args.small_k is not None:
