@@ -47,6 +47,7 @@ struct GemmArgs {
   int tdh[9], tdw[9];
   int Ho, Wo, osh, osw, oh0, ow0;   // output rows: (n, p*osh + oh0, q*osw + ow0) of [N][Ho][Wo]
   int nt;                           // non-temporal C stores
+  int dbg;                          // timing probes (tools/gemm_overhead.py): 1 = skip epilogue
 };
 
 // chunk swizzle of a [rows][BK] bf16 tile: 16-row ds_read_b128 fragment reads hit 16 slots
@@ -523,6 +524,15 @@ gemm_nt_kernel(const GemmArgs g) {
   DTF_WAIT_VM(0);       // the trailing no-op DMAs still target the ring
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();        // all fragment reads done: reuse LDS for C
+  if (g.dbg & 1) {      // timing probe: keep the accumulators live, skip staging and stores
+    float keep = 0.f;
+#pragma unroll
+    for (int i = 0; i < Cf::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < Cf::FN; ++j) keep += acc[i][j][0];
+    if (keep == 1.2345f) g.C[tid] = 0;
+    return;
+  }
 
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -629,6 +639,7 @@ gemm_nt_kernel(const GemmArgs g) {
 
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
 int g_gemm_nt = 0;         // non-temporal C stores (ResNet-50 A/B: neutral; off keeps BERT outputs cached)
+int g_gemm_dbg = 0;        // GemmArgs::dbg for timing probes
 
 template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1,
           int CONV = 0>
@@ -650,6 +661,7 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
 
 void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
 void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
+void dtf_gemm_set_dbg(int v) { g_gemm_dbg = v; }
 
 // Implicit-GEMM convolution on the ping-pong GEMM: Y[M = N*P*Q][Kout] (+= Cin / masked acc)
 // = X (through the tap table) . Wt[Kout][Kpad]^T, Kpad = taps * C, C % 64 == 0, <= 9 taps.
@@ -700,6 +712,7 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
     throw std::runtime_error("gemm_nt: masked accumulation needs acc_src and a dense C");
   GemmArgs g{A, B, C, bias, Cin, M, N, K, lda, ldb, ldc, relu, stats, acc_src, acc_mask};
   g.nt = g_gemm_nt;
+  g.dbg = g_gemm_dbg;
   // auto: 256 x 128 tiles when N <= 128 (measured 1.02-1.07x the 256 x 256 tile on the N = 128
   // ResNet 1x1 convs, profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl)
   const int variant = g_gemm_variant >= 0 ? g_gemm_variant : (N <= 128 ? 1 : 8);
