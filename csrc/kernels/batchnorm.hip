@@ -70,6 +70,10 @@ DTF_DEV void load8f(const float* __restrict__ p, int cg, float* v) {
 
 // MODE 0: forward stats   acc0 += x,           acc1 += x*x
 // MODE 1: backward reduce acc0 += dz,          acc1 += dz*(x-mean)*invstd
+// MODE 2: MODE 1 for TWO BatchNorms summed before one ReLU (a projection block's residual BN:
+//         z = relu(bn(x) + bn_p(xp))): both see the same dz, so one pass reads dz and the mask
+//         once and also accumulates acc2 += dz*(xp-mean_p)*invstd_p; the slabs are (acc0, acc1)
+//         and (acc0, acc2) -- each exactly what MODE 1 over that BN alone would write
 // mkind (MODE 1): 0 no ReLU, 1 bit mask, 2 recompute from x, 3 from y
 // 16-B streaming accesses; NT: non-temporal (the tensors are far larger than L2 / MALL and
 // every byte is touched once per pass)
@@ -100,29 +104,34 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                  const bf16_t* __restrict__ y, const uint8_t* __restrict__ mask,
                  const float* __restrict__ mean, const float* __restrict__ invstd, int M, int C,
                  int rows_per_block, int mkind_unused, float* __restrict__ partial,
-                 const float* __restrict__ fsc, const float* __restrict__ fsh) {
-  extern __shared__ __attribute__((aligned(16))) float red[];   // [rpi][2][C]
+                 const float* __restrict__ fsc, const float* __restrict__ fsh,
+                 const bf16_t* __restrict__ xp, const float* __restrict__ meanp,
+                 const float* __restrict__ invstdp, float* __restrict__ partialp) {
+  extern __shared__ __attribute__((aligned(16))) float red[];   // [rpi][NQ][C]
+  constexpr int NQ = MODE == 2 ? 3 : 2;
   const int tpr = C >> 3;
   const int rpi = kThreads / tpr;
   const int tid = threadIdx.x;
   const int cg = tid % tpr, ro = tid / tpr;
   const bool active = ro < rpi;
-  float a0[8], a1[8], mu[8], is[8], ksc[8], ksh[8];
+  float a0[8], a1[8], a2[8], mu[8], is[8], mup[8], isp[8], ksc[8], ksh[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { a0[i] = 0.f; a1[i] = 0.f; ksc[i] = 0.f; ksh[i] = 0.f; }
-  if (MODE == 1 && active) {
+  for (int i = 0; i < 8; ++i) { a0[i] = 0.f; a1[i] = 0.f; a2[i] = 0.f; ksc[i] = 0.f; ksh[i] = 0.f; }
+  if (MODE >= 1 && active) {
     load8f(mean, cg, mu);
     load8f(invstd, cg, is);
     if (MK == 2) { load8f(fsc, cg, ksc); load8f(fsh, cg, ksh); }
+    if (MODE == 2) { load8f(meanp, cg, mup); load8f(invstdp, cg, isp); }
   }
   const int m0 = blockIdx.x * rows_per_block;
   const int m1 = min(m0 + rows_per_block, M);
   const uint4* X4 = reinterpret_cast<const uint4*>(x);
   const uint4* D4 = reinterpret_cast<const uint4*>(dy);
   const uint4* Y4 = reinterpret_cast<const uint4*>(y);
+  const uint4* XP4 = reinterpret_cast<const uint4*>(xp);
   if (active) {
     for (int m = m0 + ro; m < m1; m += rpi * kUnroll) {
-      uint4 xr[kUnroll], dr[kUnroll], yr[kUnroll];
+      uint4 xr[kUnroll], dr[kUnroll], yr[kUnroll], pr[kUnroll];
       uint32_t mb[kUnroll];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
@@ -130,11 +139,12 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
         const uint32_t v = (uint32_t)r * tpr + cg;
         const bool ok = r < m1;
         xr[u] = ok ? ldv<NT>(X4 + v) : make_uint4(0, 0, 0, 0);
-        if (MODE == 1) {
+        if (MODE >= 1) {
           dr[u] = ok ? ldv<NT>(D4 + v) : make_uint4(0, 0, 0, 0);
           mb[u] = (ok && MK == 1) ? (uint32_t)mask[v] : 0u;
           yr[u] = (ok && MK == 3) ? Y4[v] : make_uint4(0, 0, 0, 0);
         }
+        if (MODE == 2) pr[u] = ok ? ldv<NT>(XP4 + v) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
@@ -149,6 +159,12 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
           relu_mask8(g, xv, mb[u], yr[u], MK, ksc, ksh);
 #pragma unroll
           for (int i = 0; i < 8; ++i) { a0[i] += g[i]; a1[i] += g[i] * (xv[i] - mu[i]) * is[i]; }
+          if (MODE == 2) {
+            float pv[8];
+            unpack8(pr[u], pv);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a2[i] += g[i] * (pv[i] - mup[i]) * isp[i];
+          }
         }
       }
     }
@@ -156,17 +172,20 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
   if (active) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      red[(ro * 2 + 0) * C + cg * 8 + i] = a0[i];
-      red[(ro * 2 + 1) * C + cg * 8 + i] = a1[i];
+      red[(ro * NQ + 0) * C + cg * 8 + i] = a0[i];
+      red[(ro * NQ + 1) * C + cg * 8 + i] = a1[i];
+      if (MODE == 2) red[(ro * NQ + 2) * C + cg * 8 + i] = a2[i];
     }
   }
   __syncthreads();
   // tree-free final sum: thread t reduces channel-slot t over the rpi row groups
-  for (int idx = tid; idx < 2 * C; idx += kThreads) {
+  for (int idx = tid; idx < NQ * C; idx += kThreads) {
     const int which = idx / C, c = idx % C;
     float s = 0.f;
-    for (int r = 0; r < rpi; ++r) s += red[(r * 2 + which) * C + c];
-    partial[((long)blockIdx.x * 2 + which) * C + c] = s;
+    for (int r = 0; r < rpi; ++r) s += red[(r * NQ + which) * C + c];
+    if (which < 2) partial[((long)blockIdx.x * 2 + which) * C + c] = s;
+    if (MODE == 2 && which != 1)
+      partialp[((long)blockIdx.x * 2 + (which ? 1 : 0)) * C + c] = s;
   }
 }
 
@@ -271,18 +290,22 @@ __global__ void bn_infer_finalize_kernel(int C, const float* __restrict__ gamma,
 
 // y = [relu](x*scale + shift [+ res]); with `mask` also the ReLU bit mask (bit i of byte v =
 // element 8v+i > 0) the backward reads instead of y.
-template <bool NT>
+// DUAL: res is itself a BatchNorm INPUT (a projection shortcut's conv output) normalised on the
+// fly with (rscale, rshift) and rounded to bf16 exactly as its own apply pass would have stored
+// it -- the shortcut BN's output is never written or re-read (bit-identical to the two passes).
+template <bool NT, bool DUAL = false>
 __global__ void __launch_bounds__(kThreads)
 bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                 bf16_t* __restrict__ y, uint8_t* __restrict__ mask,
                 const float* __restrict__ scale, const float* __restrict__ shift, int M, int C,
-                int relu) {
+                int relu, const float* __restrict__ rscale, const float* __restrict__ rshift) {
   const int tpr = C >> 3, rpi = kThreads / tpr;
   const int cg = threadIdx.x % tpr, ro = threadIdx.x / tpr;
   if (ro >= rpi) return;
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
   load8f(scale, cg, sc);
   load8f(shift, cg, sh);
+  if (DUAL) { load8f(rscale, cg, rsc); load8f(rshift, cg, rsh); }
   const uint4* X4 = reinterpret_cast<const uint4*>(x);
   const uint4* R4 = reinterpret_cast<const uint4*>(res);
   uint4* Y4 = reinterpret_cast<uint4*>(y);
@@ -310,6 +333,10 @@ bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
       if (res) {
         float rv[8];
         unpack8(rr[u], rv);
+        if (DUAL) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) rv[i] = bf2f(f2bf(__builtin_fmaf(rv[i], rsc[i], rsh[i])));
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] += rv[i];
       }
@@ -353,22 +380,30 @@ bn_bwd_finalize_kernel(const double* __restrict__ level2, int S, int C, long M,
   coefC[c] = -k * db * invM - B * mean[c];
 }
 
-template <int MK, bool NT>
+// DUAL: also dxp = Ap*dz + Bp*xp + Cp for the second BatchNorm of a projection block (the one
+// whose output was the residual), from the same masked dz (see bn_reduce_kernel MODE 2)
+template <int MK, bool NT, bool DUAL = false>
 __global__ void __launch_bounds__(kThreads)
 bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                     const uint8_t* __restrict__ mask, const bf16_t* __restrict__ x,
                     const float* __restrict__ cA, const float* __restrict__ cB,
                     const float* __restrict__ cC, bf16_t* __restrict__ dx,
                     bf16_t* __restrict__ dres, int M, int C, int mkind_unused,
-                    const float* __restrict__ fsc, const float* __restrict__ fsh) {
+                    const float* __restrict__ fsc, const float* __restrict__ fsh,
+                    const bf16_t* __restrict__ xp, const float* __restrict__ cAp,
+                    const float* __restrict__ cBp, const float* __restrict__ cCp,
+                    bf16_t* __restrict__ dxp) {
   const int tpr = C >> 3, rpi = kThreads / tpr;
   const int cg = threadIdx.x % tpr, ro = threadIdx.x / tpr;
   if (ro >= rpi) return;
-  float ka[8], kb[8], kc[8], ksc[8], ksh[8];
+  float ka[8], kb[8], kc[8], ksc[8], ksh[8], pa[8], pb[8], pc[8];
   load8f(cA, cg, ka);
   load8f(cB, cg, kb);
   load8f(cC, cg, kc);
   if (MK == 2) { load8f(fsc, cg, ksc); load8f(fsh, cg, ksh); }
+  if (DUAL) { load8f(cAp, cg, pa); load8f(cBp, cg, pb); load8f(cCp, cg, pc); }
+  const uint4* XP4 = reinterpret_cast<const uint4*>(xp);
+  uint4* DXP4 = reinterpret_cast<uint4*>(dxp);
   const uint4* D4 = reinterpret_cast<const uint4*>(dy);
   const uint4* X4 = reinterpret_cast<const uint4*>(x);
   const uint4* Y4 = reinterpret_cast<const uint4*>(y);
@@ -376,7 +411,7 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
   uint4* DR4 = reinterpret_cast<uint4*>(dres);
   const int step = gridDim.x * rpi * kUnroll;
   for (int m = blockIdx.x * rpi * kUnroll + ro; m < M; m += step) {
-    uint4 dr[kUnroll], xr[kUnroll], yr[kUnroll];
+    uint4 dr[kUnroll], xr[kUnroll], yr[kUnroll], pr[kUnroll];
     uint32_t mb[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
@@ -387,6 +422,7 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
         xr[u] = ldv<NT>(X4 + v);
         if (MK == 1) mb[u] = mask[v];
         if (MK == 3) yr[u] = Y4[v];
+        if (DUAL) pr[u] = ldv<NT>(XP4 + v);
       }
     }
 #pragma unroll
@@ -403,6 +439,13 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = ka[i] * g[i] + kb[i] * xv[i] + kc[i];
       stv<NT>(DX4 + v, pack8(o));
+      if (DUAL) {
+        float pv[8];
+        unpack8(pr[u], pv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = pa[i] * g[i] + pb[i] * pv[i] + pc[i];
+        stv<NT>(DXP4 + v, pack8(o));
+      }
     }
   }
 }
@@ -471,7 +514,8 @@ void dtf_bn_fwd_stats(const bf16_t* x, long M, int C, float* partial, hipStream_
   const int rpi = kThreads / (C / 8);
   const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
   hipLaunchKernelGGL((bn_reduce_kernel<0, 0>), dim3(G), dim3(kThreads), lds, st, x, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, (int)M, C, rpb, 0, partial, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, (int)M, C, rpb, 0, partial, nullptr, nullptr,
+                     nullptr, nullptr, nullptr, nullptr);
 }
 
 void dtf_bn_fwd_finalize_g(const float* partial, int G, long M, int C, const float* gamma,
@@ -521,10 +565,24 @@ void dtf_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, uint8_t* mask,
   check_rows(M, C);
   if (g_bn_nt & 1)
     hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, x,
-                       res, y, mask, scale, shift, (int)M, C, relu);
+                       res, y, mask, scale, shift, (int)M, C, relu, nullptr, nullptr);
   else
     hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, x,
-                       res, y, mask, scale, shift, (int)M, C, relu);
+                       res, y, mask, scale, shift, (int)M, C, relu, nullptr, nullptr);
+}
+
+// y = relu(bn(x) + bn_p(xp)) (+ ReLU bit mask): a projection block's two BatchNorms in one pass
+void dtf_bn_apply_dual(const bf16_t* x, const bf16_t* xp, bf16_t* y, uint8_t* mask,
+                       const float* scale, const float* shift, const float* pscale,
+                       const float* pshift, long M, int C, int relu, hipStream_t st) {
+  check_rows(M, C);
+  if (!xp || !pscale || !pshift) throw std::runtime_error("bn_apply_dual: missing operands");
+  if (g_bn_nt & 1)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(sweep_grid(M, C)), dim3(kThreads), 0, st,
+                       x, xp, y, mask, scale, shift, (int)M, C, relu, pscale, pshift);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(sweep_grid(M, C)), dim3(kThreads), 0,
+                       st, x, xp, y, mask, scale, shift, (int)M, C, relu, pscale, pshift);
 }
 
 void dtf_bn_set_nt(int v) { g_bn_nt = v; }
@@ -542,10 +600,12 @@ void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, c
 #define DTF_BN_RED(MK_)                                                                    \
   if (g_bn_nt & 4)                                                                         \
     hipLaunchKernelGGL((bn_reduce_kernel<1, MK_, true>), dim3(G), dim3(kThreads), lds, st, x, dy, \
-                       y, mask, mean, invstd, (int)M, C, rpb, mk, partial, fsc, fsh);          \
+                       y, mask, mean, invstd, (int)M, C, rpb, mk, partial, fsc, fsh, nullptr,   \
+                       nullptr, nullptr, nullptr);                                          \
   else                                                                                     \
     hipLaunchKernelGGL((bn_reduce_kernel<1, MK_>), dim3(G), dim3(kThreads), lds, st, x, dy, y,   \
-                       mask, mean, invstd, (int)M, C, rpb, mk, partial, fsc, fsh)
+                       mask, mean, invstd, (int)M, C, rpb, mk, partial, fsc, fsh, nullptr,      \
+                       nullptr, nullptr, nullptr)
   switch (mk) {
     case 0: DTF_BN_RED(0); break;
     case 1: DTF_BN_RED(1); break;
@@ -590,10 +650,12 @@ void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, co
 #define DTF_BN_BWD(MK_)                                                                    \
   if (g_bn_nt & 2)                                                                         \
     hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_, true>), dim3(sweep_grid(M, C)), dim3(kThreads), \
-                       0, st, dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh);  \
+                       0, st, dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh,   \
+                       nullptr, nullptr, nullptr, nullptr, nullptr);                        \
   else                                                                                     \
     hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_, false>), dim3(sweep_grid(M, C)), dim3(kThreads), \
-                       0, st, dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh)
+                       0, st, dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh,   \
+                       nullptr, nullptr, nullptr, nullptr, nullptr)
   switch (mk) {
     case 0: DTF_BN_BWD(0); break;
     case 1: DTF_BN_BWD(1); break;
@@ -601,4 +663,43 @@ void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, co
     default: DTF_BN_BWD(3); break;
   }
 #undef DTF_BN_BWD
+}
+
+// Backward of y = relu(bn(x) + bn_p(xp)) with the forward's ReLU bit mask: one reduce pass for
+// both BatchNorms' sums (dz and the mask read once), then -- after the two finalizes -- one apply
+// pass writing dx and dxp.  Each slab / output is bit-identical to the single-BN passes.
+void dtf_bn_bwd_reduce_dual(const bf16_t* dy, const uint8_t* mask, const bf16_t* x,
+                            const float* mean, const float* invstd, const bf16_t* xp,
+                            const float* meanp, const float* invstdp, long M, int C,
+                            float* partial, float* partialp, hipStream_t st) {
+  check_rows(M, C);
+  if (!mask) throw std::runtime_error("bn_bwd_reduce_dual: needs the forward ReLU bit mask");
+  int rpb;
+  const int G = stats_grid(M, C, &rpb);
+  const int rpi = kThreads / (C / 8);
+  const size_t lds = (size_t)rpi * 3 * C * sizeof(float);
+  if (g_bn_nt & 4)
+    hipLaunchKernelGGL((bn_reduce_kernel<2, 1, true>), dim3(G), dim3(kThreads), lds, st, x, dy,
+                       nullptr, mask, mean, invstd, (int)M, C, rpb, 1, partial, nullptr, nullptr,
+                       xp, meanp, invstdp, partialp);
+  else
+    hipLaunchKernelGGL((bn_reduce_kernel<2, 1>), dim3(G), dim3(kThreads), lds, st, x, dy, nullptr,
+                       mask, mean, invstd, (int)M, C, rpb, 1, partial, nullptr, nullptr, xp, meanp,
+                       invstdp, partialp);
+}
+
+void dtf_bn_bwd_apply_dual(const bf16_t* dy, const uint8_t* mask, const bf16_t* x,
+                           const float* cA, const float* cB, const float* cC, bf16_t* dx,
+                           const bf16_t* xp, const float* cAp, const float* cBp,
+                           const float* cCp, bf16_t* dxp, long M, int C, hipStream_t st) {
+  check_rows(M, C);
+  if (!mask) throw std::runtime_error("bn_bwd_apply_dual: needs the forward ReLU bit mask");
+  if (g_bn_nt & 2)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, true, true>), dim3(sweep_grid(M, C)), dim3(kThreads),
+                       0, st, dy, nullptr, mask, x, cA, cB, cC, dx, nullptr, (int)M, C, 1, nullptr,
+                       nullptr, xp, cAp, cBp, cCp, dxp);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, false, true>), dim3(sweep_grid(M, C)),
+                       dim3(kThreads), 0, st, dy, nullptr, mask, x, cA, cB, cC, dx, nullptr, (int)M,
+                       C, 1, nullptr, nullptr, xp, cAp, cBp, cCp, dxp);
 }

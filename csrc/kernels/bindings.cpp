@@ -68,6 +68,14 @@ void dtf_bn_bwd_finalize_g(const float*, int, long, int, const float*, const flo
 void dtf_bn_bwd_finalize(const float*, long, int, const float*, const float*, const float*,
                          float*, float*, float*, float*, float*, int, hipStream_t);
 void dtf_relu_mask_apply(const bf16_t*, const uint8_t*, bf16_t*, long, hipStream_t);
+void dtf_bn_apply_dual(const bf16_t*, const bf16_t*, bf16_t*, uint8_t*, const float*, const float*,
+                       const float*, const float*, long, int, int, hipStream_t);
+void dtf_bn_bwd_reduce_dual(const bf16_t*, const uint8_t*, const bf16_t*, const float*,
+                            const float*, const bf16_t*, const float*, const float*, long, int,
+                            float*, float*, hipStream_t);
+void dtf_bn_bwd_apply_dual(const bf16_t*, const uint8_t*, const bf16_t*, const float*,
+                           const float*, const float*, bf16_t*, const bf16_t*, const float*,
+                           const float*, const float*, bf16_t*, long, int, hipStream_t);
 void dtf_bn_bwd_apply(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, const float*,
                       const float*, const float*, bf16_t*, bf16_t*, long, int, int, const float*,
                       const float*, hipStream_t);
@@ -414,6 +422,34 @@ PYBIND11_MODULE(_dtf_hip, m) {
                         P<const float>(invstd), P<float>(dg), P<float>(db), P<float>(a),
                         P<float>(b), P<float>(c), accumulate, S(st));
     check_launch("bn_bwd_finalize");
+  });
+  m.def("bn_apply_dual", [](uintptr_t x, uintptr_t xp, uintptr_t y, uintptr_t mask,
+                            uintptr_t scale, uintptr_t shift, uintptr_t pscale, uintptr_t pshift,
+                            long M, int C, int relu, uintptr_t st) {
+    dtf_bn_apply_dual(P<const bf16_t>(x), P<const bf16_t>(xp), P<bf16_t>(y), P<uint8_t>(mask),
+                      P<const float>(scale), P<const float>(shift), P<const float>(pscale),
+                      P<const float>(pshift), M, C, relu, S(st));
+    check_launch("bn_apply_dual");
+  });
+  m.def("bn_bwd_reduce_dual", [](uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t mean,
+                                 uintptr_t invstd, uintptr_t xp, uintptr_t meanp,
+                                 uintptr_t invstdp, long M, int C, uintptr_t part,
+                                 uintptr_t partp, uintptr_t st) {
+    dtf_bn_bwd_reduce_dual(P<const bf16_t>(dy), P<const uint8_t>(mask), P<const bf16_t>(x),
+                           P<const float>(mean), P<const float>(invstd), P<const bf16_t>(xp),
+                           P<const float>(meanp), P<const float>(invstdp), M, C, P<float>(part),
+                           P<float>(partp), S(st));
+    check_launch("bn_bwd_reduce_dual");
+  });
+  m.def("bn_bwd_apply_dual", [](uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t a,
+                                uintptr_t b, uintptr_t c, uintptr_t dx, uintptr_t xp,
+                                uintptr_t ap, uintptr_t bp, uintptr_t cp, uintptr_t dxp, long M,
+                                int C, uintptr_t st) {
+    dtf_bn_bwd_apply_dual(P<const bf16_t>(dy), P<const uint8_t>(mask), P<const bf16_t>(x),
+                          P<const float>(a), P<const float>(b), P<const float>(c), P<bf16_t>(dx),
+                          P<const bf16_t>(xp), P<const float>(ap), P<const float>(bp),
+                          P<const float>(cp), P<bf16_t>(dxp), M, C, S(st));
+    check_launch("bn_bwd_apply_dual");
   });
   m.def("relu_mask_apply", [](uintptr_t dy, uintptr_t mask, uintptr_t out, long n, uintptr_t st) {
     dtf_relu_mask_apply(P<const bf16_t>(dy), P<const uint8_t>(mask), P<bf16_t>(out), n, S(st));

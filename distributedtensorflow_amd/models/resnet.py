@@ -10,6 +10,8 @@ bottleneck block is 3-4 conv launches + 3-4 fused BN launches forward.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -63,6 +65,8 @@ class StemConvBN(ConvBN):
 
 S2D_STEM = True
 FUSE_STEM_POOL = True
+# projection blocks: shortcut BN fused into the block-output BN (ops.batch_norm_add_batch_norm)
+FUSE_PROJ_BN = os.environ.get("DTF_FUSE_PROJ_BN", "1") == "1"
 
 
 class Bottleneck(nn.Module):
@@ -81,6 +85,18 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         # projection blocks: proj and c1 both read x -> one dgrad buffer, no autograd add
         share = ops.GradShare(2) if self.has_proj else None
+        if self.has_proj and FUSE_PROJ_BN:
+            # the shortcut's BN is applied inside the block-output BN (one pass forward, one
+            # reduce + one apply pass backward for both)
+            p, b = self.proj, self.proj.bn
+            sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
+                            bn_stats=b.training, grad_share=share)
+            y = self.c2(self.c1(x, grad_share=share))
+            c, b3 = self.c3, self.c3.bn
+            y = ops.conv2d(y, c.conv.kernel, c.conv.strides, c.conv.padding, bn_stats=b3.training)
+            return ops.batch_norm_add_batch_norm(
+                y, b3.gamma, b3.beta, b3.moving_mean, b3.moving_variance, sc, b.gamma, b.beta,
+                b.moving_mean, b.moving_variance, b3.training, b3.momentum, b3.epsilon)
         sc = self.proj(x, relu=False, grad_share=share) if self.has_proj else x
         y = self.c1(x, grad_share=share)
         y = self.c2(y)

@@ -100,6 +100,21 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
                                 momentum, eps, relu, residual)
 
 
+def batch_norm_add_batch_norm(x, gamma, beta, running_mean, running_var, xp, gamma_p, beta_p,
+                              running_mean_p, running_var_p, training=True, momentum=0.997,
+                              eps=1e-5):
+    """relu(batch_norm(x) + batch_norm(xp)): a ResNet projection block's output.  Native path:
+    one fused op (the shortcut BN's output is never stored; one backward pass for both BNs)."""
+    if _use_native(x):
+        return _native().batch_norm_add_batch_norm(x, gamma, beta, running_mean, running_var, xp,
+                                                   gamma_p, beta_p, running_mean_p,
+                                                   running_var_p, training, momentum, eps)
+    sc = reference.batch_norm(xp, gamma_p, beta_p, running_mean_p, running_var_p, training,
+                              momentum, eps, False, None)
+    return reference.batch_norm(x, gamma, beta, running_mean, running_var, training, momentum,
+                                eps, True, sc)
+
+
 def batch_norm_relu_max_pool(x, gamma, beta, running_mean=None, running_var=None, training=True,
                              momentum=0.997, eps=1e-5, kernel=3, stride=2, padding=1):
     """max_pool2d(batch_norm(x, relu=True)): the ResNet stem's BN -> ReLU -> 3x3/2 max-pool.
@@ -231,6 +246,7 @@ def mlm_loss(logits, labels, weights=None):
 
 __all__ = [
     "set_backend", "get_backend", "GradShare", "conv2d", "conv2d_bias_relu", "batch_norm", "relu",
+    "batch_norm_add_batch_norm",
     "max_pool2d", "global_avg_pool", "dense", "sparse_softmax_cross_entropy",
     "softmax_cross_entropy_clipped_sum", "layer_norm", "gelu", "attention", "dropout",
     "bias_dropout_add_layer_norm", "embedding_layer_norm", "bias_gelu", "attention_qkv",

@@ -647,10 +647,14 @@ def _bn_bwd_finalize(ctx, part, G, M, C, g32, stats):
     """Combine the backward partial sums -> dgamma / dbeta (straight into the flat gradient
     buffer when it exposes one) and the dx = A dz + B x + C coefficients; returns (gb, direct)
     with gb = [dgamma, dbeta, A, B, C]."""
+    return _bn_bwd_finalize_p(ctx.params, part, G, M, C, g32, stats)
+
+
+def _bn_bwd_finalize_p(params, part, G, M, C, g32, stats):
     st = _st()
     mean, invstd = stats[0], stats[1]
     gb = torch.empty(5, C, device=g32.device, dtype=torch.float32)
-    tg, tb = (_direct_grad(p) for p in ctx.params)
+    tg, tb = (_direct_grad(p) for p in params)
     direct = tg is not None and tb is not None
     dg_ptr, db_ptr = ((tg.data_ptr(), tb.data_ptr()) if direct
                       else (gb[0].data_ptr(), gb[1].data_ptr()))
@@ -663,7 +667,7 @@ def _bn_bwd_finalize(ctx, part, G, M, C, g32, stats):
                              invstd.data_ptr(), dg_ptr, db_ptr, gb[2].data_ptr(),
                              gb[3].data_ptr(), gb[4].data_ptr(), int(direct), st)
     if direct:
-        for p in ctx.params:
+        for p in params:
             _grad_ready(p)
     return gb, direct
 
@@ -732,6 +736,78 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
         raise ValueError("residual shape mismatch")
     return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps,
                             relu, residual, residual_to_conv)
+
+
+class _BatchNormAddBatchNorm(torch.autograd.Function):
+    """relu(BN(x) + BN_p(xp)): a projection block's residual BatchNorm and its shortcut's
+    BatchNorm as ONE op.  Forward: one apply pass normalises both conv outputs (the shortcut
+    BN's output is never stored or re-read; it is rounded to bf16 in registers exactly as its own
+    pass would have stored it, so the result is bit-identical to the two-op form).  Backward:
+    both BNs see the same dz = dy * relu_mask, so one reduce pass reads dy and the bit mask once
+    for both BNs' sums and one apply pass writes dx and dxp (csrc/kernels/batchnorm.hip DUAL
+    variants).  Saves ~8 B of HBM traffic per shortcut element per step."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, xp, gamma_p, beta_p,
+                running_mean_p, running_var_p, training, momentum, eps):
+        x, xp = x.contiguous(), xp.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        stats, g32 = _bn_forward_stats(x, gamma, beta, running_mean, running_var, training,
+                                       momentum, eps)
+        stats_p, g32_p = _bn_forward_stats(xp, gamma_p, beta_p, running_mean_p, running_var_p,
+                                           training, momentum, eps)
+        y = torch.empty_like(x)
+        mask = torch.empty(M * C // 8, device=x.device, dtype=torch.uint8)
+        _K.bn_apply_dual(x.data_ptr(), xp.data_ptr(), y.data_ptr(), mask.data_ptr(),
+                         stats[2].data_ptr(), stats[3].data_ptr(), stats_p[2].data_ptr(),
+                         stats_p[3].data_ptr(), M, C, 1, _st())
+        ctx.save_for_backward(x, xp, mask, g32, g32_p, stats, stats_p)
+        ctx.params = (gamma, beta)
+        ctx.params_p = (gamma_p, beta_p)
+        ctx.dtypes = (gamma.dtype, beta.dtype, gamma_p.dtype, beta_p.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, xp, mask, g32, g32_p, stats, stats_p = ctx.saved_tensors
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        st = _st()
+        ws = _K.bn_workspace_floats(M, C)
+        part = torch.empty(ws, device=x.device, dtype=torch.float32)
+        part_p = torch.empty(ws, device=x.device, dtype=torch.float32)
+        _K.bn_bwd_reduce_dual(dy.data_ptr(), mask.data_ptr(), x.data_ptr(), stats[0].data_ptr(),
+                              stats[1].data_ptr(), xp.data_ptr(), stats_p[0].data_ptr(),
+                              stats_p[1].data_ptr(), M, C, part.data_ptr(), part_p.data_ptr(), st)
+        gb, direct = _bn_bwd_finalize_p(ctx.params, part, None, M, C, g32, stats)
+        gbp, direct_p = _bn_bwd_finalize_p(ctx.params_p, part_p, None, M, C, g32_p, stats_p)
+        dx, dxp = torch.empty_like(x), torch.empty_like(xp)
+        _K.bn_bwd_apply_dual(dy.data_ptr(), mask.data_ptr(), x.data_ptr(), gb[2].data_ptr(),
+                             gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), xp.data_ptr(),
+                             gbp[2].data_ptr(), gbp[3].data_ptr(), gbp[4].data_ptr(),
+                             dxp.data_ptr(), M, C, st)
+        gd, bd, gpd, bpd = ctx.dtypes
+        ctx.params = ctx.params_p = None
+        dg, db = (None, None) if direct else (gb[0].to(gd), gb[1].to(bd))
+        dgp, dbp = (None, None) if direct_p else (gbp[0].to(gpd), gbp[1].to(bpd))
+        return dx, dg, db, None, None, dxp, dgp, dbp, None, None, None, None, None
+
+
+def batch_norm_add_batch_norm(x, gamma, beta, running_mean, running_var, xp, gamma_p, beta_p,
+                              running_mean_p, running_var_p, training=True, momentum=0.997,
+                              eps=1e-5):
+    """relu(batch_norm(x) + batch_norm(xp)) (training or inference statistics)."""
+    _check_cuda_bf16(x, xp)
+    C = x.shape[-1]
+    if C % 8 or C > 2048:
+        raise ValueError(f"native batch_norm: unsupported channel count {C}")
+    if xp.shape != x.shape:
+        raise ValueError("batch_norm_add_batch_norm: shortcut shape mismatch")
+    return _BatchNormAddBatchNorm.apply(x, gamma, beta, running_mean, running_var, xp, gamma_p,
+                                        beta_p, running_mean_p, running_var_p, training,
+                                        momentum, eps)
 
 
 class _BatchNormReluMaxPool(torch.autograd.Function):

@@ -356,3 +356,65 @@ def test_resnet50_per_block_teacher_forced_vs_fp32():
     check("head", _Head(m.fc), act.bfloat16().requires_grad_(True))
     print("\nteacher-forced relative errors vs fp32:\n" + "\n".join(lines))
     assert not failures, failures
+
+
+def test_fused_projection_bn_bit_identical():
+    """Projection blocks with the shortcut BN fused into the block-output BN
+    (ops.batch_norm_add_batch_norm: one apply pass forward, one reduce + one apply pass backward
+    for both BNs) against the two-op form: loss, every gradient and the moving statistics are
+    bit-identical (the fused kernels round the shortcut BN output to bf16 in registers exactly
+    as its own pass stored it, and each reduce slab is the single-BN slab)."""
+    from distributedtensorflow_amd.models import resnet as rn
+    torch.manual_seed(0)
+    base = resnet50().cuda()
+    a, b = copy.deepcopy(base), copy.deepcopy(base)
+    prev = rn.FUSE_PROJ_BN
+    try:
+        rn.FUSE_PROJ_BN = True
+        la, ga = _grads(a, True)
+        rn.FUSE_PROJ_BN = False
+        lb, gb = _grads(b, True)
+    finally:
+        rn.FUSE_PROJ_BN = prev
+    assert la == lb
+    assert torch.equal(ga, gb)
+    for (n1, t1), (n2, t2) in zip(a.named_buffers(), b.named_buffers()):
+        assert n1 == n2 and torch.equal(t1, t2), n1
+
+
+def test_batch_norm_add_batch_norm_vs_fp32():
+    """The fused op against the fp32 reference formula relu(bn(x) + bn(xp)) with batch
+    statistics, forward and backward."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    M, C = 4096, 256
+    x = (torch.randn(8, 16, 32, C, device="cuda", generator=g) * 2 + 1).bfloat16().requires_grad_()
+    xp = (torch.randn(8, 16, 32, C, device="cuda", generator=g) - 0.5).bfloat16().requires_grad_()
+    gam, bet = torch.rand(C, device="cuda", generator=g) + 0.5, torch.randn(C, device="cuda", generator=g)
+    gp, bp = torch.rand(C, device="cuda", generator=g) + 0.5, torch.randn(C, device="cuda", generator=g)
+    params = [t.clone().requires_grad_() for t in (gam, bet, gp, bp)]
+    rm, rv, rmp, rvp = (torch.zeros(C, device="cuda"), torch.ones(C, device="cuda"),
+                        torch.zeros(C, device="cuda"), torch.ones(C, device="cuda"))
+    y = native.batch_norm_add_batch_norm(x, params[0], params[1], rm, rv, xp, params[2],
+                                         params[3], rmp, rvp, True, 0.9, 1e-5)
+    dy = torch.randn(y.shape, device="cuda", generator=g).bfloat16()
+    y.backward(dy)
+
+    def bn(t, ga, be):
+        t = t.float()
+        mu = t.mean((0, 1, 2))
+        var = t.var((0, 1, 2), unbiased=False)
+        return (t - mu) / torch.sqrt(var + 1e-5) * ga + be
+
+    xr, xpr = x.detach().float().requires_grad_(), xp.detach().float().requires_grad_()
+    rp = [t.clone().requires_grad_() for t in (gam, bet, gp, bp)]
+    # the ReLU mask of the native (bf16-rounded) output, so mask flips at ~0 do not count
+    yr = (bn(xr, rp[0], rp[1]) + bn(xpr, rp[2], rp[3])) * (y.detach().float() > 0)
+    yr.backward(dy.float())
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+    assert rel(y, yr) < 1e-2
+    assert rel(x.grad, xr.grad) < 1e-2 and rel(xp.grad, xpr.grad) < 1e-2
+    for p, r in zip(params, rp):
+        assert rel(p.grad, r.grad) < 1e-2
+    torch.testing.assert_close(rm, 0.1 * x.detach().float().mean((0, 1, 2)), rtol=1e-3, atol=1e-3)
