@@ -269,7 +269,7 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_f
         if len(idx) == R * S:
             wd_mat = _dgrad_filter(wflat)                      # [C, T, K]
         else:
-            sel = wflat[:, torch.tensor(idx, device=dy.device), :]
+            sel = wflat[:, _tap_index(idx, dy.device), :]
             wd_mat = sel.permute(2, 1, 0).contiguous()
         extra = ()
         if part is not None:
@@ -280,6 +280,19 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_f
     if part is not None:
         dx._dtf_bnb_part = (part, G, n * h * wd, C, tok)
     return dx
+
+
+_TAP_IDX = {}
+
+
+def _tap_index(idx, device):
+    """Device index tensor of a dgrad phase class's taps, built once (no host-to-device copy in
+    the step: a HIP-graph capture of the step must not contain one)."""
+    key = (tuple(idx), device)
+    t = _TAP_IDX.get(key)
+    if t is None:
+        t = _TAP_IDX[key] = torch.tensor(idx, device=device)
+    return t
 
 
 _WGRAD_WS_CAP = 32 << 20   # floats of split-K slab workspace per call (128 MB)

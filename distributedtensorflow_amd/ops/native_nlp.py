@@ -25,8 +25,12 @@ if os.environ.get("DTF_ATTN_WIDE"):
     _K.attn_set_wide(int(os.environ["DTF_ATTN_WIDE"]))
 
 
+SEED_DRAWS = [0]   # host-side seed draws so far (train/graphed.py refuses to freeze them)
+
+
 def next_seed() -> int:
     """Dropout seed from torch's CPU generator (so torch.manual_seed makes runs reproducible)."""
+    SEED_DRAWS[0] += 1
     return int(torch.randint(0, 2 ** 31 - 1, (1,), device="cpu").item())
 
 

@@ -119,6 +119,9 @@ class Optimizer:
         self.use_locking = use_locking
         # bf16 compute shadow of the fp32 masters ("auto": on GPUs); None for fp32-compute models
         self.shadow_dtype = "auto"
+        # True while a training step is being captured into a HIP graph (train/graphed.py): the
+        # per-step hyper-parameters are then written by the replay wrapper, not by the step
+        self._capturing = False
 
     # ------------------------------------------------------------------ hyper-parameters
     def learning_rate(self, step=None):
@@ -190,6 +193,17 @@ class Optimizer:
         return self.apply_gradients(None, global_step)
 
     # ------------------------------------------------------------------ update
+    def _refresh_hyper(self):
+        """Write this step's hyper-parameters into the device buffers the fused kernels read
+        (learning rate; Adam's lr_t; LAMB's bias corrections)."""
+        self._lr_dev[0].fill_(self.learning_rate())
+
+    def _maybe_refresh_hyper(self):
+        # inside a graph capture the fill would be recorded with THIS step's constant; the
+        # replay wrapper refreshes the buffers before every replay instead
+        if not self._capturing:
+            self._refresh_hyper()
+
     def _apply(self, gscale, rng=None):
         """Run the update over the whole flat buffer, or only over ``rng = (start, end)`` (the
         slice a parameter-server shard owns)."""

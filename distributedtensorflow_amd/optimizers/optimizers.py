@@ -40,7 +40,7 @@ class GradientDescentOptimizer(Optimizer):
                 "weight_decay": self.weight_decay}
 
     def _apply_native(self, gscale):
-        self._lr_dev[0].fill_(self.learning_rate())
+        self._maybe_refresh_hyper()
         K, sp = _K(), self.space
         for s, e, dec in self._regions():
             K.sgd_momentum(sp.master.data_ptr() + 4 * s, sp.grad.data_ptr() + 4 * s,
@@ -79,7 +79,7 @@ class MomentumOptimizer(Optimizer):
                 "weight_decay": self.weight_decay}
 
     def _apply_native(self, gscale):
-        self._lr_dev[0].fill_(self.learning_rate())
+        self._maybe_refresh_hyper()
         K, sp, a = _K(), self.space, self.slots[0].buf
         for s, e, dec in self._regions():
             K.sgd_momentum(sp.master.data_ptr() + 4 * s, sp.grad.data_ptr() + 4 * s,
@@ -123,8 +123,11 @@ class AdamOptimizer(Optimizer):
     def lr_t(self):
         return tf_adam_lr_t(self.learning_rate(), self.beta1, self.beta2, self.iterations)
 
-    def _apply_native(self, gscale):
+    def _refresh_hyper(self):
         self._lr_dev[0].fill_(self.lr_t())
+
+    def _apply_native(self, gscale):
+        self._maybe_refresh_hyper()
         K, sp = _K(), self.space
         m, v = self.slots[0].buf, self.slots[1].buf
         for s, e, dec in self._regions():
@@ -171,7 +174,7 @@ class AdagradOptimizer(Optimizer):
                 "initial_accumulator_value": self.initial_accumulator_value}
 
     def _apply_native(self, gscale):
-        self._lr_dev[0].fill_(self.learning_rate())
+        self._maybe_refresh_hyper()
         K, sp, acc = _K(), self.space, self.slots[0].buf
         for s, e, _ in self._regions():
             K.adagrad(sp.master.data_ptr() + 4 * s, sp.grad.data_ptr() + 4 * s,
@@ -235,11 +238,14 @@ class LAMBOptimizer(Optimizer):
             self._tables[key] = (tbl.to(self.space.device), len(rows))
         return self._tables[key]
 
-    def _apply_native(self, gscale):
+    def _refresh_hyper(self):
         t = self.iterations
         self._hyper[0].fill_(1.0 / (1 - self.beta1 ** t))
         self._hyper[1].fill_(1.0 / (1 - self.beta2 ** t))
         self._lr_dev[0].fill_(self.learning_rate())
+
+    def _apply_native(self, gscale):
+        self._maybe_refresh_hyper()
         self._norms.zero_()
         sp, m, v = self.space, self.slots[0].buf, self.slots[1].buf
         chunks, nchunks = self._chunk_table()

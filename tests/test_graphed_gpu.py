@@ -1,0 +1,125 @@
+"""Training steps captured as HIP graphs (train/graphed.py) replay bit-identically to eager
+steps: the reference MNIST CNN (bf16 and fp32 compute, TF-exact Adam) and a small ResNet (BN
+running statistics, momentum), with per-step learning rates and the global step advanced by the
+replay wrapper."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+def _batches(n, shape, classes, dtype, seed=1):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return [(torch.rand(*shape, device="cuda", generator=g).to(dtype),
+             torch.randint(0, classes, (shape[0],), device="cuda", generator=g)) for _ in range(n)]
+
+
+def _run(model, opt, gstep, batches, graphed, warm):
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.train import GraphedTrainStep
+
+    def step(x, y):
+        loss = ops.sparse_softmax_cross_entropy(model(x), y)
+        opt.minimize(loss, global_step=gstep)
+        return loss
+
+    losses = []
+    if graphed:
+        sx, sy = warm[0].clone(), warm[1].clone()
+        gstep_fn = GraphedTrainStep(step, opt, [sx, sy], global_step=gstep, warmup=2)
+        for x, y in batches:
+            losses.append(gstep_fn(x, y).clone())
+    else:
+        for _ in range(2):                       # the graphed run's eager warm-up steps
+            step(*warm)
+        for x, y in batches:
+            losses.append(step(x, y))
+    torch.cuda.synchronize()
+    return torch.stack(losses), opt.space.master.clone()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_graphed_mnist_cnn_matches_eager(dtype):
+    import distributedtensorflow_amd as dtf
+    from distributedtensorflow_amd.models import MnistCNN
+    from distributedtensorflow_amd.parallel import OneDeviceStrategy
+    from distributedtensorflow_amd.train import GlobalStep
+    torch.manual_seed(0)
+    with OneDeviceStrategy("/gpu:0").scope():
+        base = MnistCNN()
+    if dtype == torch.float32:
+        base = base.float()
+    res = []
+    for graphed in (False, True):
+        model = copy.deepcopy(base)
+        with OneDeviceStrategy("/gpu:0").scope():
+            # a decaying learning rate: every replay must see its own step's value
+            opt = dtf.train.AdamOptimizer(lambda t: 1e-3 / (1 + 0.1 * t))
+            if dtype == torch.float32:
+                opt.shadow_dtype = None
+            opt.build(list(model.parameters()))
+        gstep = GlobalStep()
+        batches = _batches(6, (128, 784), 10, dtype)
+        res.append(_run(model, opt, gstep, batches[1:], graphed, batches[0]) + (int(gstep),))
+    (la, pa, sa), (lb, pb, sb) = res
+    assert torch.equal(la, lb), (la, lb)
+    assert torch.equal(pa, pb)
+    assert sa == sb == 7
+    assert float(la[-1]) < float(la[0])
+
+
+def test_graphed_resnet_matches_eager():
+    from distributedtensorflow_amd.models import resnet50
+    from distributedtensorflow_amd.optimizers import MomentumOptimizer
+    from distributedtensorflow_amd.parallel import OneDeviceStrategy
+    torch.manual_seed(0)
+    with OneDeviceStrategy("/gpu:0").scope():
+        base = resnet50(num_classes=100)
+    res = []
+    for graphed in (False, True):
+        model = copy.deepcopy(base)
+        with OneDeviceStrategy("/gpu:0").scope():
+            opt = MomentumOptimizer(lambda t: 0.05 * (t + 1) / 8, 0.9, weight_decay=1e-4)
+            opt.build(list(model.parameters()))
+        batches = _batches(4, (8, 64, 64, 3), 100, torch.bfloat16, seed=3)
+        losses, p = _run(model, opt, None, batches[1:], graphed, batches[0])
+        res.append((losses, p, [b.clone() for b in model.buffers()]))
+    (la, pa, ba), (lb, pb, bb) = res
+    assert torch.equal(la, lb)
+    assert torch.equal(pa, pb)
+    for x, y in zip(ba, bb):
+        assert torch.equal(x, y)
+
+
+def test_graphed_step_refuses_dropout():
+    """A step that draws dropout seeds on the host cannot be frozen into a graph."""
+    from distributedtensorflow_amd.models.bert import BertConfig, BertForPreTraining
+    from distributedtensorflow_amd.optimizers import LAMBOptimizer
+    from distributedtensorflow_amd.parallel import OneDeviceStrategy
+    from distributedtensorflow_amd.train import GraphedTrainStep
+    cfg = BertConfig(vocab_size=512, hidden_size=256, num_hidden_layers=1, num_attention_heads=4,
+                     intermediate_size=1024, max_position_embeddings=64)
+    with OneDeviceStrategy("/gpu:0").scope():
+        model = BertForPreTraining(cfg)
+        opt = LAMBOptimizer(1e-3)
+        opt.build(list(model.parameters()))
+    from distributedtensorflow_amd.data.synthetic import SyntheticMLM
+    d = next(iter(SyntheticMLM(4, 64, max_predictions=4, device="cuda", seed=0, vocab_size=512)))
+    batch = [d["input_ids"], d["segment_ids"], d["input_mask"], d["masked_lm_positions"],
+             d["masked_lm_ids"], torch.ones_like(d["masked_lm_ids"], dtype=torch.float32)]
+
+    def step(*b):
+        loss = model(*b)
+        opt.minimize(loss)
+        return loss
+
+    with pytest.raises(RuntimeError, match="dropout"):
+        GraphedTrainStep(step, opt, batch, warmup=1)

@@ -275,3 +275,14 @@ def test_sync_replicas_backup_workers_need_between_graph_ps():
         with pytest.raises(ValueError, match="backup workers"):
             SyncReplicasOptimizer(AdamOptimizer(0.1), replicas_to_aggregate=1,
                                   total_num_replicas=2)
+
+
+def test_graphed_train_step_needs_gpu():
+    """HIP-graph capture of a training step (train/graphed.py) is GPU-only; on a CPU host it
+    refuses up front instead of failing inside torch.cuda.graph."""
+    import torch as _t
+    from distributedtensorflow_amd.train import GraphedTrainStep
+    if _t.cuda.is_available():
+        pytest.skip("CPU-only check")
+    with pytest.raises(RuntimeError, match="GPU"):
+        GraphedTrainStep(lambda x: x, None, [_t.zeros(1)])
