@@ -931,6 +931,143 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// ResNet stem as a halo conv: the 7x7/2 conv on the 3-channel image runs as a 4x4 stride-1 conv
+// over the 2x2 space-to-depth image (16 channels, [N][P+3][Q+3][16], padding already applied).
+// The register kernel's chunk gather re-reads each input pixel from L2 for all 16 taps (~0.5 KB
+// of L2 traffic per output pixel) and ran at ~0.35 of its roof.  Here a block owns kStemTH whole
+// output rows of one image: the kStemTH + 3 input rows it needs are ONE contiguous span of
+// global memory, copied into LDS by lane-linear LDS-DMA, and the full 64 x 256 filter sits in
+// LDS (row pitch padded to 528 B: conflict-free fragment reads); every tap is then an LDS read.
+// K order = tap-major, channel-minor (the filter layout [64][4][4][16]): one 32-deep K-step is
+// taps (r, s), (r, s + 1) of one row -- 64 contiguous patch bytes -- so each A fragment is a
+// single 16-B LDS read.  Epilogue as the 3x3 halo kernel (bf16 tile through LDS, 16-B stores,
+// BatchNorm partial sums of the rounded outputs, one slab row per block).  Same MFMA chain
+// order as the register kernel (K in order, 32 at a time): bit-identical outputs.
+constexpr int kStemTH = 4;                 // output rows per block
+constexpr int kStemC = 16, kStemK = 64, kStemKD = 256;
+constexpr int kStemWP = kStemKD + 8;       // filter LDS row pitch (elements)
+
+template <int Q>
+struct StemCfg {
+  static constexpr int PW = Q + 3;                                // s2d row width (pixels)
+  static constexpr int PATCH = (kStemTH + 3) * PW * kStemC;       // elements
+  static constexpr int PATCH_DMA = (PATCH * 2 + 1023) / 1024;     // 1-KB DMA instructions
+  static constexpr int PATCH_AL = PATCH_DMA * 512;                // elements (DMA-rounded)
+  static constexpr int M = kStemTH * Q;                           // output pixels per block
+  static constexpr int MF = M / 16 / 4;                           // M fragments per wave
+  static constexpr int LDC = kStemK + 8;
+  static constexpr size_t MAIN = ((size_t)PATCH_AL + (size_t)kStemK * kStemWP) * 2;
+  static constexpr size_t EPI = (size_t)M * LDC * 2 + (size_t)2 * kStemK * (kThreads / kStemK) * 4;
+  static constexpr size_t LDS = MAIN > EPI ? MAIN : EPI;
+  static_assert(M % 64 == 0, "stem tiling: 4 waves x 16-row fragments");
+};
+
+template <int Q>
+__global__ void __launch_bounds__(kThreads, 2)
+conv_stem_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+                      bf16_t* __restrict__ Y, const ConvGeom g, float* __restrict__ stats) {
+  using H = StemCfg<Q>;
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  bf16_t* const patch = lds;                                      // [(TH+3) * PW][16]
+  bf16_t* const wl = lds + H::PATCH_AL;                           // [64][kStemWP]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_h = g.P / kStemTH;
+  const int tm = blockIdx.x;
+  const int n = tm / tiles_h, p0 = (tm % tiles_h) * kStemTH;
+  // ---- patch: input rows p0 .. p0 + TH + 2 of image n, one contiguous span
+  {
+    const long base = ((long)n * g.H + p0) * g.W * kStemC;        // elements
+    const i32x4_t rx = rsrc_quad(X + base, (uint32_t)(H::PATCH * 2));
+    const uint32_t lp = lds_addr(patch);
+    for (int q = wave; q < H::PATCH_DMA; q += 4)
+      dma16(rx, lp + (uint32_t)q * 1024u, (uint32_t)(q * 1024 + lane * 16));   // tail: OOB -> 0
+  }
+  // ---- filter [64][256] -> padded LDS rows (16-B loads + ds_write; L2-resident after block 0)
+  for (int c = tid; c < kStemK * kStemKD / 8; c += kThreads) {
+    const int row = c / (kStemKD / 8), ch = c % (kStemKD / 8);
+    *reinterpret_cast<uint4*>(wl + row * kStemWP + ch * 8) =
+        *reinterpret_cast<const uint4*>(Wt + (long)row * g.Kpad + ch * 8);
+  }
+  DTF_WAIT_VM(0);
+  __syncthreads();
+
+  const int frow = lane & 15, fq = lane >> 4;
+  int pb[H::MF];                                                  // patch pixel of tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < H::MF; ++i) {
+    const int m = wave * (H::MF * 16) + 16 * i + frow;
+    const int orow = m / Q, ocol = m - orow * Q;
+    pb[i] = orow * H::PW + ocol;
+  }
+  f32x4_t acc[H::MF][4];
+#pragma unroll
+  for (int i = 0; i < H::MF; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+  for (int kc = 0; kc < kStemKD / 32; ++kc) {
+    const int r = kc >> 1, sc = (kc & 1) * 2;                    // taps (r, sc), (r, sc + 1)
+    const int dpix = r * H::PW + sc;
+    bf16x8_t bfr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8_t*>(wl + (16 * j + frow) * kStemWP + kc * 32 + fq * 8);
+#pragma unroll
+    for (int i = 0; i < H::MF; ++i) {
+      const bf16x8_t af =
+          *reinterpret_cast<const bf16x8_t*>(patch + (pb[i] + dpix) * kStemC + fq * 8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  // ---- epilogue: bf16 tile [M][64 + 8] in LDS -> 16-B stores; BN partials of the rounded values
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr int LDC = H::LDC;
+  bf16_t* st = lds;
+#pragma unroll
+  for (int i = 0; i < H::MF; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        st[(wave * (H::MF * 16) + 16 * i + fq * 4 + rr) * LDC + 16 * j + frow] = f2bf(acc[i][j][rr]);
+  __syncthreads();
+  const long ybase = ((long)n * g.P + p0) * Q;
+  constexpr int OCPR = kStemK / 8;
+  const int oc = tid % OCPR;
+  for (int rr = tid / OCPR; rr < H::M; rr += kThreads / OCPR)
+    st16(Y + (ybase + rr) * kStemK + oc * 8, *reinterpret_cast<const uint4*>(st + rr * LDC + oc * 8),
+         g.nt);
+  if (stats) {
+    constexpr int GROUPS = kThreads / kStemK;
+    constexpr int RPG = H::M / GROUPS;
+    float* red = reinterpret_cast<float*>(st + H::M * LDC);       // [GROUPS][2][64]
+    const int col = tid % kStemK, grp = tid / kStemK;
+    float a1 = 0.f, a2 = 0.f;
+    for (int rr = grp * RPG; rr < (grp + 1) * RPG; ++rr) {
+      const float v = bf2f(st[rr * LDC + col]);
+      a1 += v;
+      a2 += v * v;
+    }
+    red[(grp * 2 + 0) * kStemK + col] = a1;
+    red[(grp * 2 + 1) * kStemK + col] = a2;
+    __syncthreads();
+    if (grp == 0) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int k = 0; k < GROUPS; ++k) { a += red[(k * 2 + 0) * kStemK + col]; b += red[(k * 2 + 1) * kStemK + col]; }
+      stats[((long)tm * 2 + 0) * kStemK + col] = a;
+      stats[((long)tm * 2 + 1) * kStemK + col] = b;
+    }
+  }
+}
 }  // namespace
 
 // Host launcher.  Caller guarantees: Kout % 8 == 0, Kpad % BK == 0 (filter rows zero-padded),
@@ -971,6 +1108,20 @@ static int halo_family(const ConvGeom& g, const TapTable& taps) {
 }
 static bool use_halo(const ConvGeom& g, const TapTable& taps) { return halo_family(g, taps) != 0; }
 
+// the space-to-depth ResNet stem (4x4 taps over 16 channels -> 64, output 112 x 112)
+static int g_stem_halo = 1;
+void dtf_conv_set_stem_halo(int v) { g_stem_halo = v; }
+static bool use_stem_halo(const ConvGeom& g, const TapTable& taps) {
+  if (!g_stem_halo || g.C != kStemC || g.Kout != kStemK || g.Kpad != kStemKD || taps.n != 16 ||
+      g.sh != 1 || g.sw != 1 || g.Q != 112 || g.P % kStemTH || g.H != g.P + 3 || g.W != g.Q + 3 ||
+      g.Ho != g.P || g.Wo != g.Q || g.osh != 1 || g.osw != 1 || g.oh0 || g.ow0 || g.acc ||
+      g.bias || g.relu)
+    return false;
+  for (int t = 0; t < 16; ++t)
+    if (taps.dh[t] != t / 4 || taps.dw[t] != t % 4) return false;
+  return true;
+}
+
 // M tiles of a launch WITHOUT the halo kernel (the fused-BN-backward dgrad path, which never
 // takes it); W is accepted for API symmetry and ignored
 int dtf_conv_stats_rows(long M, int Kout, int C, int taps, int W) {
@@ -1006,6 +1157,7 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
 int dtf_conv_tile_rows(const ConvGeom& g, const TapTable& taps) {
   if (use_conv_gemm(g, taps)) return (int)(((long)g.N * g.P * g.Q + 255) / 256);
   if (g.C % 32 == 0 && use_halo(g, taps)) return g.N * (g.H / kHaloTH);
+  if (use_stem_halo(g, taps)) return g.N * (g.P / kStemTH);
   const long M = (long)g.N * g.P * g.Q;
   return dtf_conv_stats_rows(M, g.Kout, g.C, taps.n, 0);
 }
@@ -1035,6 +1187,18 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
   const bool epi = g.bias || g.relu;       // fused bias / ReLU: register kernel only
   if (epi && (bnb.part || g.acc))
     throw std::runtime_error("conv: fused bias/ReLU epilogue excludes BN / accumulate epilogues");
+  if (!bnb.part && use_stem_halo(g, taps)) {
+    using Sc = StemCfg<112>;
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_stem_halo_kernel<112>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)Sc::LDS));
+      attr = true;
+    }
+    hipLaunchKernelGGL(conv_stem_halo_kernel<112>, dim3((unsigned)(g.N * (g.P / kStemTH))),
+                       dim3(kThreads), Sc::LDS, st, X, Wt, Y, g, stats);
+    return;
+  }
   if (g.C % 32 != 0) {
     if (g.Kpad % 32) throw std::runtime_error("conv: Kpad % 32 != 0");
     if (g.C % 8 == 0) {                    // chunk gather (stem / MNIST conv1, C padded to 8)

@@ -38,6 +38,8 @@ if os.environ.get("DTF_CONV_DMA"):
     _K.conv_set_dma_mode(int(os.environ["DTF_CONV_DMA"]))
 if os.environ.get("DTF_CONV_HALO"):
     _K.conv_set_halo(int(os.environ["DTF_CONV_HALO"]))
+if os.environ.get("DTF_CONV_STEM_HALO"):
+    _K.conv_set_stem_halo(int(os.environ["DTF_CONV_STEM_HALO"]))
 if os.environ.get("DTF_CONV_SMALL_K"):
     _K.conv_set_small_k(int(os.environ["DTF_CONV_SMALL_K"]))
 if os.environ.get("DTF_STORE_NT"):      # non-temporal output stores: bit 0 conv, 1 GEMM, 2 BN

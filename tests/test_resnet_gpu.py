@@ -418,3 +418,34 @@ def test_batch_norm_add_batch_norm_vs_fp32():
     for p, r in zip(params, rp):
         assert rel(p.grad, r.grad) < 1e-2
     torch.testing.assert_close(rm, 0.1 * x.detach().float().mean((0, 1, 2)), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("n", [2, 5])
+def test_stem_halo_conv_bit_identical(n):
+    """The space-to-depth stem conv (4x4 taps over 16 channels -> 64) on the halo kernel (input
+    rows + whole filter in LDS) against the register kernel's chunk gather: identical outputs and
+    BatchNorm partial sums; and against the fp32 7x7/2 convolution of the image."""
+    from distributedtensorflow_amd.ops import reference
+    g = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randn(n, 224, 224, 3, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(64, 7, 7, 3, device="cuda", generator=g) * 0.1)
+    xs = native.space_to_depth_input(x, 2, 3, 7, 7)
+    _, ws = reference.space_to_depth_operands(x, w, 2, 3, want_x=False)
+    ws = ws.bfloat16().contiguous()
+    outs = []
+    try:
+        for halo in (1, 0):
+            native._K.conv_set_stem_halo(halo)
+            y = native.conv2d(xs, ws, 1, 0, bn_stats=True)
+            part, G, M, K = y._dtf_bn_part
+            s = part[: G * 2 * K].view(G, 2, K)
+            outs.append((y.clone(), s.sum(0)))
+    finally:
+        native._K.conv_set_stem_halo(1)
+    (y1, s1), (y0, s0) = outs
+    assert torch.equal(y1, y0)
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-2)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2),
+                                     w.bfloat16().float().permute(0, 3, 1, 2), stride=2, padding=3)
+    ref = ref.permute(0, 2, 3, 1)
+    assert float((y1.float() - ref).norm() / ref.norm()) < 1e-2
