@@ -117,6 +117,8 @@ void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, con
                     int, int, int, hipStream_t);
 
 int dtf_conv_wgrad_splits(long, int, int, long, int);
+int dtf_conv_wgrad_halo_splits(int, int, int, int, int, int, int, int, int, const TapTableW&);
+void dtf_wgrad_set_halo(int);
 void dtf_wgrad_set_dma_mode(int);
 void dtf_wgrad_set_pipe(int);
 void dtf_wgrad_set_pp(int);
@@ -617,6 +619,12 @@ PYBIND11_MODULE(_dtf_hip, m) {
      py::arg("accumulate") = 0);
   m.def("conv_wgrad_splits", &dtf_conv_wgrad_splits, py::arg("M"), py::arg("Kout"), py::arg("TC"),
         py::arg("ws_cap"), py::arg("taps") = 1);
+  m.def("conv_wgrad_halo_splits", [](std::vector<int> geom, std::vector<int> dh, std::vector<int> dw) {
+    if (geom.size() != 10) throw std::runtime_error("conv_wgrad_halo_splits: geom needs 10 ints");
+    return dtf_conv_wgrad_halo_splits(geom[0], geom[1], geom[2], geom[3], geom[4], geom[5],
+                                      geom[8], geom[6], geom[7], make_taps<TapTableW>(dh, dw));
+  });
+  m.def("wgrad_set_halo", &dtf_wgrad_set_halo);
   m.def("wgrad_set_dma_mode", &dtf_wgrad_set_dma_mode);
   m.def("wgrad_set_pipe", &dtf_wgrad_set_pipe);
   m.def("wgrad_set_pp", &dtf_wgrad_set_pp);

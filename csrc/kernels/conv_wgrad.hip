@@ -740,6 +740,120 @@ slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n
     reinterpret_cast<float4*>(out)[i] = t;
   }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Halo wgrad for the 56 x 56 x 64 -> 64 3x3 stride-1 convs (ResNet-50 stage 1).  The tiled
+// kernels gather every tap's X rows from L2 per output-column tile (~1.5 KB of L2 -> LDS per
+// pixel, L2-bound at ~0.35 of the MFMA roof).  Here a block walks whole strips of kHwTH output
+// rows: the strip's dY rows and the (kHwTH + 2)-row X patch (zero halo columns) are LDS-DMA'd
+// once (double-buffered: the next strip streams in under this strip's MFMAs), and the 9 waves
+// each own one tap: dW[:, tap, :] (64 x 64 = 16 fragments in registers) accumulates over every
+// strip the block visits.  The tap's B fragments are the patch rows of 8 consecutive output
+// pixels shifted by (dh, dw) -- 8 consecutive patch rows, read with the same transposed
+// ds_read_b64_tr_b16 pairs as the tiled kernels.  Each block leaves one fp32 slab (64 x 576);
+// slab_reduce sums the G slabs in order (deterministic).
+constexpr int kHwTH = 4, kHwW = 56, kHwC = 64;
+constexpr int kHwT = 9 * 64;                                   // threads: one wave per tap
+constexpr int kHwDy = kHwTH * kHwW;                            // dY rows (pixels) per strip
+constexpr int kHwPW = kHwW + 2;                                // patch row width
+constexpr int kHwPx = (kHwTH + 2) * kHwPW;                     // patch pixels (348)
+constexpr int kHwPxAl = (kHwPx + 7) / 8 * 8;                   // DMA-rounded (8 rows / 1 KB)
+constexpr int kHwStage = (kHwDy + kHwPxAl) * kHwC;             // elements per stage
+constexpr size_t kHwLDS = (size_t)2 * kHwStage * 2;
+
+__global__ void __launch_bounds__(kHwT, 1)
+conv_wgrad_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
+                       float* __restrict__ ws, int N, int H) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = tap (dh, dw) = (w/3-1, w%3-1)
+  const int dh = wave / 3 - 1, dw = wave % 3 - 1;
+  const int tiles_h = H / kHwTH;
+  const int nstrip = N * tiles_h;
+  const int G = gridDim.x;
+  const uint32_t lds0 = lds_addr(lds);
+  const long img = (long)H * kHwW * kHwC;                      // elements per image
+  // X / dY descriptors span the whole tensors (checked < 2^31 bytes on the host)
+  const i32x4_t rx = rsrc_quad(X, (uint32_t)((long)N * img * 2));
+  const i32x4_t ry = rsrc_quad(dY, (uint32_t)((long)N * img * 2));
+
+  // DMA plan per stage: dY 28 instructions (8 pixels of 128 B each), patch 44; 72 = 8 per wave
+  auto issue = [&](int strip, int stage) {
+    const bool live = strip < nstrip;
+    const int sn = live ? strip / tiles_h : 0, h0 = live ? (strip % tiles_h) * kHwTH : 0;
+    const uint32_t base = lds0 + (uint32_t)(stage * kHwStage) * 2u;
+    const int rloc = lane >> 3, slot = lane & 7;
+    for (int q = wave; q < kHwDy / 8 + kHwPxAl / 8; q += 9) {
+      const bool isdy = q < kHwDy / 8;
+      const int r = (isdy ? q : q - kHwDy / 8) * 8 + rloc;           // LDS row of the image
+      const int chunk = slot ^ wswz<128>(r);
+      uint32_t off = kOOB;
+      if (isdy) {
+        if (live) off = (uint32_t)(((long)sn * img + ((long)h0 * kHwW + r) * kHwC + chunk * 8) * 2);
+      } else if (live && r < kHwPx) {
+        const int pr = r / kHwPW, pc = r - pr * kHwPW;
+        const int h = h0 - 1 + pr, w = pc - 1;
+        if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)kHwW)
+          off = (uint32_t)(((long)sn * img + ((long)h * kHwW + w) * kHwC + chunk * 8) * 2);
+      }
+      dma16(isdy ? ry : rx, base + (uint32_t)(q * 1024), off);
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const int gq = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;
+
+  int s = blockIdx.x, it = 0;
+  issue(s, 0);
+  for (; s < nstrip; s += G, ++it) {
+    DTF_WAIT_VM(0);            // this strip's DMAs (own) landed ...
+    __syncthreads();           // ... everyone's; everyone finished reading the other stage
+    issue(s + G, (it + 1) & 1);                 // past the end: out of range, no traffic
+    const bf16_t* sy = lds + (it & 1) * kHwStage;
+    const bf16_t* sx = sy + kHwDy * kHwC;
+#pragma unroll 1
+    for (int kc = 0; kc < kHwDy / 32; ++kc) {
+      const int px0 = 32 * kc + 8 * gq;                        // this lane group's 8 pixels
+      const int orow = px0 / kHwW, ocol = px0 - orow * kHwW;   // 8 | 56: one output row
+      const int pr0 = (orow + 1 + dh) * kHwPW + ocol + 1 + dw;   // their tap-shifted patch rows
+      bf16x8_t af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c0 = 16 * i + 4 * tp;
+        const s4_t lo = tr_read(sy + lds_el<64>(px0 + tq, c0));
+        const s4_t hi = tr_read(sy + lds_el<64>(px0 + tq + 4, c0));
+        af[i] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c0 = 16 * j + 4 * tp;
+        const s4_t lo = tr_read(sx + lds_el<64>(pr0 + tq, c0));
+        const s4_t hi = tr_read(sx + lds_el<64>(pr0 + tq + 4, c0));
+        bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  DTF_WAIT_VM(0);              // the trailing no-op DMAs still target the LDS
+  // slab of this block: ws[blockIdx.x][k][tap * 64 + c]
+  float* out = ws + (long)blockIdx.x * (64 * 576);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        out[(long)(16 * i + 4 * gq + r) * 576 + wave * 64 + 16 * j + li] = acc[i][j][r];
+}
 }  // namespace
 
 // -1 / 1: LDS-DMA kernel whenever legal (default), 0: the register-staged kernel (A/B tests)
@@ -769,6 +883,32 @@ static bool wgrad_narrow(int Kout, int taps) {
 
 // Number of reduction splits: aim for ~1024 blocks (4 per CU), keep >= 4 K-steps per split and
 // the fp32 slab workspace (splits x Kout x TC) under `ws_cap` floats.
+static int g_wgrad_halo = 1;   // stage-1 3x3 wgrad on the halo kernel (0: tiled kernels)
+void dtf_wgrad_set_halo(int v) { g_wgrad_halo = v; }
+// the halo route: 3x3 stride-1 "same" conv, 56 x 56 x 64 -> 64, standard tap order
+static bool wgrad_halo_ok(const WgradGeom& g, const TapTableW& taps) {
+  if (!g_wgrad_halo || g.C != kHwC || g.Kout != 64 || g.W != kHwW || g.Q != kHwW || g.P != g.H ||
+      g.H % kHwTH || g.sh != 1 || g.sw != 1 || taps.n != 9 || g.ldw != 576 ||
+      2.0 * g.N * g.H * g.W * g.C >= 2147483647.0)
+    return false;
+  for (int t = 0; t < 9; ++t)
+    if (taps.dh[t] != t / 3 - 1 || taps.dw[t] != t % 3 - 1) return false;
+  return true;
+}
+static int wgrad_halo_blocks(int N, int H) {
+  const int strips = N * (H / kHwTH);
+  return strips < 256 ? strips : 256;
+}
+// split count (= fp32 slabs) of the halo route; 0 when it does not apply (Python sizes the
+// workspace from this before calling conv_wgrad)
+int dtf_conv_wgrad_halo_splits(int N, int H, int W, int C, int P, int Q, int Kout, int sh,
+                               int sw, const TapTableW& taps) {
+  WgradGeom g{};
+  g.N = N; g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.sh = sh; g.sw = sw; g.Kout = Kout;
+  g.ldw = taps.n * C;
+  return wgrad_halo_ok(g, taps) ? wgrad_halo_blocks(N, H) : 0;
+}
+
 int dtf_conv_wgrad_splits(long M, int Kout, int TC, long ws_cap, int taps) {
   const bool pp = wgrad_pp(Kout, TC);
   const bool nar = !pp && wgrad_narrow(Kout, taps);
@@ -799,6 +939,22 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   if (g.Kout % 8) throw std::runtime_error("wgrad: Kout % 8 != 0");
   const bool via_ws = splits > 1 || accumulate;
   if (splits < 1 || (via_ws && !ws)) throw std::runtime_error("wgrad: bad split workspace");
+  if (wgrad_halo_ok(g, taps) && splits == wgrad_halo_blocks(g.N, g.H)) {
+    if (!ws) throw std::runtime_error("wgrad halo: needs the slab workspace");
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_halo_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHwLDS));
+      attr = true;
+    }
+    hipLaunchKernelGGL(conv_wgrad_halo_kernel, dim3((unsigned)splits), dim3(kHwT), kHwLDS, st, X,
+                       dY, ws, g.N, g.H);
+    const long slab = 64L * 576, n4 = slab / 4;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, ws,
+                       dW, slab, slab, splits, accumulate);
+    return;
+  }
+
   const long M = (long)g.N * g.P * g.Q;
   const int TC = taps.n * g.C;
   long mps = (M + splits - 1) / splits;

@@ -38,6 +38,8 @@ if os.environ.get("DTF_CONV_DMA"):
     _K.conv_set_dma_mode(int(os.environ["DTF_CONV_DMA"]))
 if os.environ.get("DTF_CONV_HALO"):
     _K.conv_set_halo(int(os.environ["DTF_CONV_HALO"]))
+if os.environ.get("DTF_WGRAD_HALO"):
+    _K.wgrad_set_halo(int(os.environ["DTF_WGRAD_HALO"]))
 if os.environ.get("DTF_CONV_STEM_HALO"):
     _K.conv_set_stem_halo(int(os.environ["DTF_CONV_STEM_HALO"]))
 if os.environ.get("DTF_CONV_SMALL_K"):
@@ -310,14 +312,17 @@ def conv2d_wgrad(x, dy, w_shape, stride, padding, out=None):
     _, P, Q, _ = dy.shape
     taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
     tc = R * S * C
-    splits = _K.conv_wgrad_splits(n * P * Q, K, tc, _WGRAD_WS_CAP, R * S)
+    geom = [n, h, wd, c, P, Q, sh, sw, K, tc]
+    dhs, dws = [t[0] for t in taps], [t[1] for t in taps]
+    # stage-1 3x3 layers: the halo kernel (one fp32 slab per block) when it applies
+    splits = _K.conv_wgrad_halo_splits(geom, dhs, dws) or \
+        _K.conv_wgrad_splits(n * P * Q, K, tc, _WGRAD_WS_CAP, R * S)
     acc = out is not None
     dW = out if acc else torch.empty(K, tc, device=x.device, dtype=torch.float32)
     ws = (torch.empty(splits * K * tc, device=x.device, dtype=torch.float32)
           if splits > 1 or acc else None)
-    geom = [n, h, wd, c, P, Q, sh, sw, K, tc]
     _K.conv_wgrad(x.data_ptr(), dy.contiguous().data_ptr(), dW.data_ptr(), _p(ws), geom,
-                  [t[0] for t in taps], [t[1] for t in taps], splits, _st(), 1, int(acc))
+                  dhs, dws, splits, _st(), 1, int(acc))
     return dW.reshape(K, R, S, C)
 
 

@@ -449,3 +449,29 @@ def test_stem_halo_conv_bit_identical(n):
                                      w.bfloat16().float().permute(0, 3, 1, 2), stride=2, padding=3)
     ref = ref.permute(0, 2, 3, 1)
     assert float((y1.float() - ref).norm() / ref.norm()) < 1e-2
+
+
+@pytest.mark.parametrize("n,acc", [(3, False), (8, True)])
+def test_wgrad_halo_kernel_vs_fp32(n, acc):
+    """Stage-1 3x3 weight gradient (56x56x64 -> 64) on the halo kernel (strip-persistent blocks,
+    one tap per wave, per-block fp32 slabs reduced in order) against the fp32 reference and the
+    tiled kernel; with accumulation into an existing gradient."""
+    g = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randn(n, 56, 56, 64, device="cuda", generator=g).bfloat16()
+    dy = torch.randn(n, 56, 56, 64, device="cuda", generator=g).bfloat16()
+    base = torch.randn(64, 3, 3, 64, device="cuda", generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 64, 3, 3),
+                                      dy.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    if acc:
+        ref = ref + base
+    outs = []
+    try:
+        for halo in (1, 0):
+            native._K.wgrad_set_halo(halo)
+            out = base.clone().contiguous() if acc else None
+            outs.append(native.conv2d_wgrad(x, dy, (64, 3, 3, 64), 1, 1, out=out))
+    finally:
+        native._K.wgrad_set_halo(1)
+    for o in outs:
+        assert float((o - ref).norm() / ref.norm()) < 1e-5, float((o - ref).norm() / ref.norm())
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-3)
