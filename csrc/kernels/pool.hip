@@ -101,6 +101,68 @@ bn_relu_maxpool_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict
   }
 }
 
+// The 3x3 / stride-2 / pad-1 case of the kernel above (the ResNet stem): the window is unrolled
+// so its nine 16-B loads are all in flight before the first max (the generic loop waits on each
+// in turn), and the channel group -- fixed per lane since kT % (C / 8) == 0 -- loads its scale /
+// shift once.  Same visiting order and tie rule: bit-identical outputs and argmax bytes.
+__global__ void __launch_bounds__(kT)
+bn_relu_maxpool3s2_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                              const float* __restrict__ shift, bf16_t* __restrict__ y,
+                              uint8_t* __restrict__ arg, int N, int H, int W, int C, int P, int Q) {
+  const uint32_t cv = (uint32_t)(C >> 3);
+  const uint32_t total = (uint32_t)N * P * Q * cv;
+  const int cg = (int)((blockIdx.x * kT + threadIdx.x) % cv);
+  float sc[8], sf[8];
+  {
+    const float4* S4 = reinterpret_cast<const float4*>(scale + cg * 8);
+    const float4* F4 = reinterpret_cast<const float4*>(shift + cg * 8);
+    const float4 s0 = S4[0], s1 = S4[1], f0 = F4[0], f1 = F4[1];
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+    sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    sf[0] = f0.x; sf[1] = f0.y; sf[2] = f0.z; sf[3] = f0.w;
+    sf[4] = f1.x; sf[5] = f1.y; sf[6] = f1.z; sf[7] = f1.w;
+  }
+  const uint4* X4 = reinterpret_cast<const uint4*>(x);
+  for (uint32_t i = blockIdx.x * kT + threadIdx.x; i < total; i += gridDim.x * kT) {
+    uint32_t t = i / cv;
+    const int q = (int)(t % (uint32_t)Q); t /= (uint32_t)Q;
+    const int p = (int)(t % (uint32_t)P);
+    const int n = (int)(t / (uint32_t)P);
+    const int h0 = 2 * p - 1, w0 = 2 * q - 1;
+    uint4 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int h = h0 + r, w = w0 + s;
+        ok[r * 3 + s] = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        const int hc = ok[r * 3 + s] ? h : 0, wc = ok[r * 3 + s] ? w : 0;
+        v[r * 3 + s] = X4[(((uint32_t)n * H + hc) * W + wc) * cv + cg];
+      }
+    float best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      if (!ok[k]) continue;
+      float f[8];
+      unpack8(v[k], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float o = bf2f(f2bf(fmaxf(__builtin_fmaf(f[j], sc[j], sf[j]), 0.f)));
+        if (o > best[j]) { best[j] = o; bi[j] = (uint32_t)k; }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+    uint2 a;
+    a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+    reinterpret_cast<uint2*>(arg)[i] = a;
+  }
+}
+
 template <typename IT>
 __global__ void __launch_bounds__(kT)
 maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
@@ -254,25 +316,24 @@ maxpool3s2_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__
 // each regather it instead of reading a materialised 112x112x64 d(BN output).  The ReLU mask is
 // recomputed from x with the forward scale / shift.  Requires 256 % (C / 8) == 0 so every lane
 // keeps one channel group across its grid-stride loop.
-DTF_DEV void pool3s2_gather(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, int n,
-                            int a, int b, int cg, int cv, int P, int Q, float (&g)[4][8]) {
+// g[ii * 2 + jj] = the pooled gradient of input pixel (2a + ii, 2b + jj): the sum over the up to
+// four output windows (a + da, b + db) whose argmax byte names that pixel.  dyr / amr hold the
+// windows' (clamped, preloaded) gradients and argmax words; windows past P / Q are skipped.
+DTF_DEV void pool3s2_gather(const uint4 (&dyr)[4], const uint2 (&amr)[4], int a, int b, int P,
+                            int Q, float (&g)[4][8]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[k][e] = 0.f;
 #pragma unroll
   for (int da = 0; da < 2; ++da) {
-    const int p = a + da;
-    if (p >= P) continue;
+    if (a + da >= P) continue;
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
-      const int q = b + db;
-      if (q >= Q) continue;
-      const long o = (((long)n * P + p) * Q + q) * cv + cg;
+      if (b + db >= Q) continue;
       float gv[8];
-      unpack8(reinterpret_cast<const uint4*>(dy)[o], gv);
-      const uint2 am = reinterpret_cast<const uint2*>(arg)[o];
-      const uint32_t aw[2] = {am.x, am.y};
+      unpack8(dyr[da * 2 + db], gv);
+      const uint32_t aw[2] = {amr[da * 2 + db].x, amr[da * 2 + db].y};
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
@@ -325,8 +386,21 @@ pool3s2_bn_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__
     const int b = (int)(t % WB); t /= WB;
     const int a = (int)(t % HB);
     const int n = (int)(t / HB);
+    // every load of the 2x2 block up front (clamped addresses): 12 requests in flight per lane
+    // instead of a chain of dependent ones behind the boundary branches
+    uint4 dyr[4], xr[4];
+    uint2 amr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = min(a + (k >> 1), P - 1), q = min(b + (k & 1), Q - 1);
+      const uint32_t o = (((uint32_t)n * P + p) * Q + q) * cv + cg;
+      dyr[k] = reinterpret_cast<const uint4*>(dy)[o];
+      amr[k] = reinterpret_cast<const uint2*>(arg)[o];
+      const int h = min(2 * a + (k >> 1), H - 1), w = min(2 * b + (k & 1), W - 1);
+      xr[k] = reinterpret_cast<const uint4*>(x)[(((uint32_t)n * H + h) * W + w) * cv + cg];
+    }
     float g[4][8];
-    pool3s2_gather(dy, arg, n, a, b, cg, cv, P, Q, g);
+    pool3s2_gather(dyr, amr, a, b, P, Q, g);
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii) {
       const int h = 2 * a + ii;
@@ -335,9 +409,9 @@ pool3s2_bn_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__
       for (int jj = 0; jj < 2; ++jj) {
         const int w = 2 * b + jj;
         if (w >= W) continue;
-        const long v = (((long)n * H + h) * W + w) * cv + cg;
+        const uint32_t v = (((uint32_t)n * H + h) * W + w) * cv + cg;
         float xv[8];
-        unpack8(reinterpret_cast<const uint4*>(x)[v], xv);
+        unpack8(xr[ii * 2 + jj], xv);
         float* gk = g[ii * 2 + jj];
 #pragma unroll
         for (int e = 0; e < 8; ++e) gk[e] = __builtin_fmaf(xv[e], ksc[e], ksh[e]) > 0.f ? gk[e] : 0.f;
@@ -480,7 +554,11 @@ void dtf_bn_relu_maxpool_fwd(const bf16_t* x, const float* scale, const float* s
   if (C % 8) throw std::runtime_error("bn_relu_maxpool: C % 8 != 0");
   if (kh * kw > 255) throw std::runtime_error("bn_relu_maxpool: window too large");
   const long total = (long)N * P * Q * (C / 8);
-  if (total < 2147483647L && (long)N * H * W * C < 2147483647L)
+  if (g_pool_blocked && kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 &&
+      kT % (C / 8) == 0 && (long)N * H * W * (C / 8) < 2147483647L)
+    hipLaunchKernelGGL(bn_relu_maxpool3s2_fwd_kernel, dim3(grid_for(total)), dim3(kT), 0, st, x,
+                       scale, shift, y, arg, N, H, W, C, P, Q);
+  else if (total < 2147483647L && (long)N * H * W * C < 2147483647L)
     hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<uint32_t>, dim3(grid_for(total)), dim3(kT), 0,
                        st, x, scale, shift, y, arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
   else
@@ -495,9 +573,10 @@ int dtf_pool_bn_bwd_blocks(int N, int H, int W, int C) {
   return (int)(g < 1 ? 1 : g);
 }
 
-static void pool_bn_check(int H, int W, int C, int P, int Q) {
+static void pool_bn_check(int N, int H, int W, int C, int P, int Q) {
+  // 16-B-chunk indices are 32-bit in the kernel
   if (C % 8 || kT % (C / 8) || P != (H - 1) / 2 + 1 || Q != (W - 1) / 2 + 1 ||
-      (long)H * W * C >= 2147483647L)
+      (long)N * H * W * (C / 8) >= 2147483647L)
     throw std::runtime_error("pool3s2_bn_bwd: unsupported shape");
 }
 
@@ -505,7 +584,7 @@ void dtf_pool_bn_bwd_reduce(const bf16_t* dy, const uint8_t* arg, const bf16_t* 
                             const float* mean, const float* invstd, const float* fsc,
                             const float* fsh, float* partial, int N, int H, int W, int C, int P,
                             int Q, hipStream_t st) {
-  pool_bn_check(H, W, C, P, Q);
+  pool_bn_check(N, H, W, C, P, Q);
   hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<false>, dim3(dtf_pool_bn_bwd_blocks(N, H, W, C)),
                      dim3(kT), 0, st, dy, arg, x, mean, invstd, nullptr, fsc, fsh, nullptr,
                      partial, N, H, W, C, P, Q);
@@ -514,7 +593,7 @@ void dtf_pool_bn_bwd_reduce(const bf16_t* dy, const uint8_t* arg, const bf16_t* 
 void dtf_pool_bn_bwd_apply(const bf16_t* dy, const uint8_t* arg, const bf16_t* x, const float* cA,
                            const float* cB, const float* cC, const float* fsc, const float* fsh,
                            bf16_t* dx, int N, int H, int W, int C, int P, int Q, hipStream_t st) {
-  pool_bn_check(H, W, C, P, Q);
+  pool_bn_check(N, H, W, C, P, Q);
   const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
   hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<true>, dim3(grid_for(total)), dim3(kT), 0, st, dy, arg,
                      x, cA, cB, cC, fsc, fsh, dx, nullptr, N, H, W, C, P, Q);
