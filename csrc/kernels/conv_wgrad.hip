@@ -711,26 +711,41 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
   }
 }
 
-// Deterministic slab sum: block = 64 float4 columns x 4 split groups; group q sums splits
-// q, q+4, ... in order, the 4 group partials are added in a fixed order through LDS.
+// Deterministic slab sum: block = (256 / G) float4 columns x G split groups; group q sums splits
+// q, q+G, ... in order (4 loads in flight per lane), the G group partials are added in a fixed
+// order through LDS.  G = 16 for small slabs with many splits (the halo wgrad's 64 x 576 slab x
+// 256 blocks: 576 blocks instead of 144 latency-bound ones), else 4.
+template <int G>
 __global__ void __launch_bounds__(256)
 slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n, long slab,
                    int nsplit, int accumulate) {
-  __shared__ float4 red[4][64];
-  const int col = threadIdx.x & 63, q = threadIdx.x >> 6;
+  constexpr int CB = 256 / G;
+  __shared__ float4 red[G][CB];
+  const int col = threadIdx.x % CB, q = threadIdx.x / CB;
   const long n4 = n >> 2;
-  const long i = (long)blockIdx.x * 64 + col;
+  const long i = (long)blockIdx.x * CB + col;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (i < n4)
-    for (int k = q; k < nsplit; k += 4) {
-      const float4 v = reinterpret_cast<const float4*>(ws + k * slab)[i];
+  if (i < n4) {
+    const float4* base = reinterpret_cast<const float4*>(ws) + i;
+    const long s4 = slab >> 2;
+    int k = q;
+    for (; k + 3 * G < nsplit; k += 4 * G) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = base[(long)(k + u * G) * s4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+    for (; k < nsplit; k += G) {
+      const float4 v = base[(long)k * s4];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
+  }
   red[q][col] = s;
   __syncthreads();
   if (q == 0 && i < n4) {
     float4 t = red[0][col];
-    for (int k = 1; k < 4; ++k) {
+    for (int k = 1; k < G; ++k) {
       t.x += red[k][col].x; t.y += red[k][col].y; t.z += red[k][col].z; t.w += red[k][col].w;
     }
     if (accumulate) {   // gradient written straight into the optimizer's flat fp32 grad buffer
@@ -739,6 +754,18 @@ slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, long n
     }
     reinterpret_cast<float4*>(out)[i] = t;
   }
+}
+
+// slabs of n floats (n % 4 == 0) at stride `slab` -> out
+void launch_slab_reduce(const float* ws, float* out, long n, long slab, int nsplit, int accumulate,
+                        hipStream_t st) {
+  const long n4 = n / 4;
+  if (nsplit >= 32 && (n4 + 63) / 64 < 512)
+    hipLaunchKernelGGL(slab_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st,
+                       ws, out, n, slab, nsplit, accumulate);
+  else
+    hipLaunchKernelGGL(slab_reduce_kernel<4>, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st,
+                       ws, out, n, slab, nsplit, accumulate);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -949,9 +976,7 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
     }
     hipLaunchKernelGGL(conv_wgrad_halo_kernel, dim3((unsigned)splits), dim3(kHwT), kHwLDS, st, X,
                        dY, ws, g.N, g.H);
-    const long slab = 64L * 576, n4 = slab / 4;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, ws,
-                       dW, slab, slab, splits, accumulate);
+    launch_slab_reduce(ws, dW, 64L * 576, 64L * 576, splits, accumulate, st);
     return;
   }
 
@@ -1019,9 +1044,7 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   }
   if (via_ws) {
     // slab = Kout * ldw floats, Kout % 8 == 0 -> slab % 4 == 0 (float4 path covers it)
-    const long n4 = g.slab / 4;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, ws,
-                       dW, g.slab, g.slab, nsplit, accumulate);
+    launch_slab_reduce(ws, dW, g.slab, g.slab, nsplit, accumulate, st);
   }
 }
 
@@ -1029,8 +1052,6 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
 // (+= when accumulate): the split-K combine of the dense-layer weight-gradient GEMMs.
 void dtf_slab_reduce(const float* ws, float* out, long n, int nsplit, int accumulate, hipStream_t st) {
   if (n % 4) throw std::runtime_error("slab_reduce: n % 4 != 0");
-  const long n4 = n / 4;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, ws, out,
-                     n, n, nsplit, accumulate);
+  launch_slab_reduce(ws, out, n, n, nsplit, accumulate, st);
 }
 
