@@ -196,9 +196,11 @@ bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
 // fp64 slice sums in order.  Deterministic and placement-independent (kernel boundary = the
 // release/acquire between the stages).
 inline int combine_slices(int G, int C) {
+  // ~1024 combine blocks (the stage-1 layers have G ~ 25k slab rows at b2048: 32 blocks left the
+  // GPU idle); stage 2 is block-parallel (8 slices in flight per channel), so S may be large
   const int groups = (C + 31) / 32;
-  int S = 256 / groups;
-  if (S > 16) S = 16;        // stage 2 reads S values per channel serially: keep it short
+  int S = 1024 / groups;
+  if (S > 256) S = 256;
   if (S > G / 8) S = G / 8;
   return S < 1 ? 1 : S;
 }
@@ -231,16 +233,28 @@ bn_combine_kernel(const float* __restrict__ partial, int G, int C, int S,
   level2[((long)j * 2 + 1) * C + c] = ss;
 }
 
+// stage 2: block = 32 channels x 8 slice lanes; lane k sums slices k, k + 8, ... in order, the 8
+// lane sums are added in order through LDS.  True (with the totals) on the slot-0 threads only.
 DTF_DEV bool combine_partials(const double* __restrict__ level2, int S, int C, double* a,
                               double* b, int* c_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return false;
+  __shared__ double red[2][8][32];
+  const int cl = threadIdx.x & 31, slot = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
   double s = 0.0, ss = 0.0;
-#pragma unroll 16
-  for (int j = 0; j < S; ++j) {
-    s += level2[((long)j * 2 + 0) * C + c];
-    ss += level2[((long)j * 2 + 1) * C + c];
+  if (c < C) {
+#pragma unroll 4
+    for (int j = slot; j < S; j += 8) {
+      s += level2[((long)j * 2 + 0) * C + c];
+      ss += level2[((long)j * 2 + 1) * C + c];
+    }
   }
+  red[0][slot][cl] = s;
+  red[1][slot][cl] = ss;
+  __syncthreads();
+  if (slot != 0 || c >= C) return false;
+  s = 0.0;
+  ss = 0.0;
+  for (int k = 0; k < 8; ++k) { s += red[0][k][cl]; ss += red[1][k][cl]; }
   *a = s;
   *b = ss;
   *c_out = c;
@@ -526,7 +540,7 @@ void dtf_bn_fwd_finalize_g(const float* partial, int G, long M, int C, const flo
   double* level2 = reinterpret_cast<double*>(const_cast<float*>(partial) + (long)G * 2 * C);
   hipLaunchKernelGGL(bn_combine_kernel, dim3((C + 31) / 32, S), dim3(256), 0, st, partial, G, C,
                      S, level2);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, level2, S,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, level2, S,
                      C, M, gamma, beta, run_mean, run_var, momentum, eps, mean, invstd, scale,
                      shift);
 }
@@ -623,7 +637,7 @@ void dtf_bn_bwd_finalize_g(const float* partial, int G, long M, int C, const flo
   double* level2 = reinterpret_cast<double*>(const_cast<float*>(partial) + (long)G * 2 * C);
   hipLaunchKernelGGL(bn_combine_kernel, dim3((C + 31) / 32, S), dim3(256), 0, st, partial, G, C,
                      S, level2);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, level2, S,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, level2, S,
                      C, M, gamma, mean, invstd, dgamma, dbeta, coefA, coefB, coefC, accumulate);
 }
 
@@ -637,7 +651,7 @@ void dtf_bn_bwd_finalize(const float* partial, long M, int C, const float* gamma
   double* level2 = reinterpret_cast<double*>(const_cast<float*>(partial) + (long)G * 2 * C);
   hipLaunchKernelGGL(bn_combine_kernel, dim3((C + 31) / 32, S), dim3(256), 0, st, partial, G, C,
                      S, level2);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, level2, S,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, level2, S,
                      C, M, gamma, mean, invstd, dgamma, dbeta, coefA, coefB, coefC, accumulate);
 }
 
