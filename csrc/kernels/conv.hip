@@ -776,6 +776,7 @@ struct HaloCfg {
   static constexpr int WST = NT * 64;                    // filter elements per stage
   static constexpr int LDC = NT + 8;
   static constexpr size_t LDS = (size_t)(PIXAL * C + 2 * WST) * 2;
+  static constexpr size_t lds(int st) { return (size_t)(st * PIXAL * C + 2 * WST) * 2; }
   static_assert(M % (16 * WMW) == 0 && NT % (16 * WNW) == 0, "halo tiling");
   static_assert((size_t)M * LDC * 2 + (size_t)2 * NT * (kThreads / NT) * 4 <= (size_t)PIXAL * C * 2,
                 "halo epilogue must fit in the patch region");
@@ -786,21 +787,27 @@ struct HaloCfg {
 template <int C>
 DTF_DEV int halo_swz(int p) { return C == 64 ? ((p >> 1) & 7) : (p & 15); }
 
-template <int C, int W, int WMW, int NT>
-__global__ void __launch_bounds__(kThreads, 2)
+// ST strips per block (ST x 4 waves): the per-tap filter slices stream through LDS once per
+// block, so two strips per block halve the filter's L2 -> LDS traffic.  Measured no faster at
+// b2048 (one 8-wave block per CU instead of two 4-wave blocks: the blocks' barrier phases no
+// longer overlap; profiles/measurements/r2_halo_strips_ab_b2048.txt), so ST = 1 by default.
+template <int C, int W, int WMW, int NT, int ST = 1>
+__global__ void __launch_bounds__(kThreads * ST, ST == 1 ? 2 : 1)
 conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                     bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
                     float* __restrict__ stats) {
   using H = HaloCfg<C, W, WMW, NT>;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  bf16_t* const patch = lds;                                     // [PIXAL][C]
-  bf16_t* const wst = lds + H::PIXAL * C;                        // [2][NT][64]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = threadIdx.x & (kThreads - 1), lane = tid & 63;   // tid within the strip
+  const int wall = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int sid = wall >> 2, wave = wall & 3;                    // strip, wave within the strip
+  bf16_t* const patch = lds + sid * (H::PIXAL * C);              // [ST][PIXAL][C]
+  bf16_t* const wst = lds + ST * (H::PIXAL * C);                 // [2][NT][64]
   const int wm = wave / H::WNW, wn = wave % H::WNW;
   const int tiles_h = g.H / kHaloTH;
-  const int tm = blockIdx.x;                                     // (image, row-tile)
-  const int n = tm / tiles_h, h0 = (tm % tiles_h) * kHaloTH;
+  const int tm = blockIdx.x * ST + sid;                          // (image, row-tile)
+  const bool live = tm < g.N * tiles_h;                          // odd tail: a dead strip
+  const int n = live ? tm / tiles_h : 0, h0 = live ? (tm % tiles_h) * kHaloTH : 0;
   const int n0 = blockIdx.y * NT;                                // output-channel tile
   const i32x4_t rx = rsrc_quad(X + (long)n * g.H * g.W * g.C, (uint32_t)g.H * g.W * g.C * 2u);
   const i32x4_t rw = rsrc_quad(Wt, (uint32_t)g.Kout * g.Kpad * 2u);
@@ -815,7 +822,8 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
       const int pr = pix / H::PW, pc = pix - pr * H::PW;
       const int h = h0 - 1 + pr, w = pc - 1;
       const int chunk = slot ^ halo_swz<C>(pix);
-      const bool ok = pix < H::PIX && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const bool ok = live && pix < H::PIX && (unsigned)h < (unsigned)g.H &&
+                      (unsigned)w < (unsigned)g.W;
       const uint32_t off = ok ? (uint32_t)(((h * g.W + w) * C + chunk * 8) * 2) : kOOB;
       dma16(rx, lds_patch + (uint32_t)q * 1024u, off);
     }
@@ -825,8 +833,8 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   auto issue_w = [&](int step, int stage) {
     const int t = step / H::KS, s = step - t * H::KS;
 #pragma unroll
-    for (int i = 0; i < NT / 32; ++i) {
-      const int q = wave + 4 * i;
+    for (int i = 0; i < NT / (32 * ST); ++i) {
+      const int q = wall + 4 * ST * i;
       const int row = q * 8 + lp8;
       const int chunk = slot8 ^ ((row >> 1) & 7);
       const int kr = n0 + row;
@@ -888,7 +896,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   constexpr int LDC = H::LDC;
-  bf16_t* st = lds;
+  bf16_t* st = patch;
 #pragma unroll
   for (int i = 0; i < H::MF; ++i)
 #pragma unroll
@@ -903,7 +911,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   const int oc = tid % OCPR;
   const bool col_ok = n0 + oc * 8 < g.Kout;
   for (int r = tid / OCPR; r < H::M; r += kThreads / OCPR) {
-    if (!col_ok) continue;
+    if (!col_ok || !live) continue;
     st16(Y + (ybase + r) * g.Kout + n0 + oc * 8,
          *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8), g.nt);
   }
@@ -921,7 +929,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     red[(grp * 2 + 0) * NT + col] = a1;
     red[(grp * 2 + 1) * NT + col] = a2;
     __syncthreads();
-    if (grp == 0 && n0 + col < g.Kout) {
+    if (grp == 0 && n0 + col < g.Kout && live) {
       float a = 0.f, b = 0.f;
 #pragma unroll
       for (int k = 0; k < GROUPS; ++k) { a += red[(k * 2 + 0) * NT + col]; b += red[(k * 2 + 1) * NT + col]; }
@@ -1107,6 +1115,28 @@ static int halo_family(const ConvGeom& g, const TapTable& taps) {
   return 0;
 }
 static bool use_halo(const ConvGeom& g, const TapTable& taps) { return halo_family(g, taps) != 0; }
+// strips per halo block, per family (bit 0: 56 x 56 x 64, bit 1: 28 x 28 x 128)
+static int g_halo_st = 0;   // measured: no faster (one 8-wave block per CU), see r2_halo_strips_ab_b2048.txt
+void dtf_conv_set_halo_strips(int v) { g_halo_st = v; }
+template <int C, int W, int WMW, int NT>
+static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
+                        const TapTable& taps, float* stats, int tiles, int strips, hipStream_t st) {
+  using Hc = HaloCfg<C, W, WMW, NT>;
+  if (strips == 2) {
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_kernel<C, W, WMW, NT, 2>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)Hc::lds(2)));
+      attr = true;
+    }
+    hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 2>),
+                       dim3((unsigned)((tiles + 1) / 2), g.Kout / NT), dim3(2 * kThreads), Hc::lds(2),
+                       st, X, Wt, Y, g, taps, stats);
+  } else {
+    hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 1>), dim3((unsigned)tiles, g.Kout / NT),
+                       dim3(kThreads), Hc::lds(1), st, X, Wt, Y, g, taps, stats);
+  }
+}
 
 // the space-to-depth ResNet stem (4x4 taps over 16 channels -> 64, output 112 x 112)
 static int g_stem_halo = 1;
@@ -1218,16 +1248,10 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
     return;
   }
   if (!bnb.part && !epi && use_halo(g, taps)) {
-    const dim3 grid0((unsigned)(g.N * (g.H / kHaloTH)));
-    if (halo_family(g, taps) == 1) {
-      using Hc = HaloCfg<64, 56, 2, 64>;
-      hipLaunchKernelGGL((conv3x3_halo_kernel<64, 56, 2, 64>), dim3(grid0.x, g.Kout / 64),
-                         dim3(kThreads), Hc::LDS, st, X, Wt, Y, g, taps, stats);
-    } else {
-      using Hc = HaloCfg<128, 28, 1, 128>;
-      hipLaunchKernelGGL((conv3x3_halo_kernel<128, 28, 1, 128>), dim3(grid0.x, g.Kout / 128),
-                         dim3(kThreads), Hc::LDS, st, X, Wt, Y, g, taps, stats);
-    }
+    const int fam = halo_family(g, taps);
+    const int tiles = g.N * (g.H / kHaloTH);
+    if (fam == 1) launch_halo<64, 56, 2, 64>(X, Wt, Y, g, taps, stats, tiles, (g_halo_st & 1) ? 2 : 1, st);
+    else launch_halo<128, 28, 1, 128>(X, Wt, Y, g, taps, stats, tiles, (g_halo_st & 2) ? 2 : 1, st);
     return;
   }
   if (!epi && use_dma_kernel((long)m, g.Kout, g.C, taps.n, bk) && g.Kpad % 64 == 0) {

@@ -341,11 +341,12 @@ def test_batched_filter_transpose():
 
 
 @pytest.mark.parametrize("N,H,C,K", [(2, 56, 64, 64), (3, 56, 64, 128), (2, 28, 128, 128),
-                                     (2, 28, 128, 256)])
+                                     (2, 28, 128, 256), (3, 28, 128, 128)])
 def test_halo_conv3x3_matches_implicit_gemm(N, H, C, K):
     """Halo-tiled 3x3 kernels (56x56x64 and 28x28x128 families) == the implicit-GEMM kernel bit
-    for bit (same tap / k order) for the forward and the data gradient; fused BN statistics
-    match."""
+    for bit (same tap / k order) for the forward and the data gradient, with one and with two
+    row strips per block (N=3 at 28x28: an odd strip count, the last block's second strip is
+    dead); fused BN statistics match."""
     nat = _native()
     torch.manual_seed(0)
     x = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
@@ -354,8 +355,9 @@ def test_halo_conv3x3_matches_implicit_gemm(N, H, C, K):
     dy = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
     outs = []
     try:
-        for halo in (3, 0):
+        for halo, strips in ((3, 0), (3, 3), (0, 0)):
             nat._K.conv_set_halo(halo)
+            nat._K.conv_set_halo_strips(strips)
             y = nat.conv2d_forward(x, w, 1, 1)
             dx = nat.conv2d_dgrad(dy, wd, x.shape, 1, 1)
             gamma = torch.ones(K, device=dev)
@@ -365,9 +367,12 @@ def test_halo_conv3x3_matches_implicit_gemm(N, H, C, K):
             outs.append((y, dx, z.float()))
     finally:
         nat._K.conv_set_halo(3)
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-    torch.testing.assert_close(outs[0][2], outs[1][2], atol=2e-2, rtol=1e-2)
+        nat._K.conv_set_halo_strips(0)
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        assert torch.equal(outs[0][1], o[1])
+    assert torch.equal(outs[0][2], outs[1][2])      # same strips -> same BN statistics slab rows
+    torch.testing.assert_close(outs[0][2], outs[2][2], atol=2e-2, rtol=1e-2)
     ref = _ref()
     yr = ref.conv2d(x.float(), w.float(), 1, 1)
     assert _rel(outs[0][0], yr) < 1e-2
