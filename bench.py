@@ -36,14 +36,16 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=None,
-                   help="per-GPU batch (default 2048 for ResNet-50: 82 GB of the 288 GB HBM3E; "
+                   help="per-GPU batch (default 1984 for ResNet-50: ~80 GB of the 288 GB HBM3E; "
                         "the conv kernels rebase their buffer descriptors per tile, so no 2 GiB "
-                        "tensor cap remains; round-2 sweep 1280/1536/2048 -> 12.76k/12.81k/12.83k "
-                        "img/s (profiles/measurements/r2_resnet_batch_sweep_1280_1536_2048.jsonl); "
-                        "earlier 512/640/768/1024/1280 -> 10.26k/10.57k/10.67k/10.85k/10.99k: "
-                        "larger batches amortise launches, fill the 256 CUs with whole tile "
-                        "rounds and shrink the all-reduce share per step; 512 sequences for BERT: "
-                        "sweep 128/256/512/1024 -> 875k/1.03M/1.14M/1.15M tok/s)")
+                        "tensor cap remains).  1984 = 31 x 64 fills whole rounds of 256-row tiles "
+                        "on the 256 CUs in the GEMM-routed stage-3/4 convs (M = B*196 and B*49: "
+                        "1984 -> 1519 / 380 tiles per 256-wide N slab, the tile rounds 0.99 "
+                        "busy; 2048 -> 1568 / 392, 0.875 / 0.766); same-box sweeps "
+                        "1856/1920/1984/2006/2048/2112/2240/2304/2560/3072 -> 1984 best, +1.7-2.3 %% "
+                        "over 2048 (profiles/measurements/r2_resnet_batch_sweep_tile_rounds_*.jsonl); "
+                        "512 sequences for BERT: sweep 128/256/512/1024 -> 875k/1.03M/1.14M/1.15M "
+                        "tok/s)")
     p.add_argument("--impl", choices=("dtf", "torch"), default="dtf")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--lr", type=float, default=0.1)
@@ -66,7 +68,7 @@ def parse():
     p.add_argument("--gemm-tuning-out", default=None)
     args = p.parse_args()
     if args.batch is None:
-        args.batch = 512 if args.model == "bert_base" else 2048
+        args.batch = 512 if args.model == "bert_base" else 1984
     return args
 
 
