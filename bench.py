@@ -246,7 +246,13 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1 and not dist.is_initialized():
         from distributedtensorflow_amd.parallel import init_process_group_from_env
-        init_process_group_from_env("nccl")
+        # RCCL (backend "nccl") is the measured path; DTF_BENCH_BACKEND=gloo exists only for the
+        # multi-rank rehearsal on a one-GPU box (tests/test_bench_multirank_gpu.py), where RCCL
+        # refuses two ranks on one device
+        backend = os.environ.get("DTF_BENCH_BACKEND", "nccl")
+        if backend not in ("nccl", "gloo"):
+            raise SystemExit(f"DTF_BENCH_BACKEND={backend!r}: expected nccl or gloo")
+        init_process_group_from_env(backend)
     torch.backends.cudnn.benchmark = True
     gemm_table = setup_gemm_tuning(args)
     native_info = {"backend": "torch (stock comparator)", "native_ext": None}
@@ -258,6 +264,9 @@ def main():
                              "measured step must run this framework's HIP kernels")
         native_info = {"backend": ops.get_backend(),
                        "native_ext": os.path.relpath(native.extension_path(), ROOT)}
+
+    # the process group that carried the gradients ("nccl" = RCCL on ROCm; None at N = 1)
+    native_info["comm_backend"] = dist.get_backend() if dist.is_initialized() else None
 
     B, S = args.batch, args.image_size
     g = torch.Generator(device=dev)

@@ -1,0 +1,81 @@
+"""Rehearsal of the driver's multi-GPU bench launch on a one-GPU box.
+
+The round-end driver runs ``bench.py --gpus N`` under ``torch.distributed.run`` with one rank per
+GPU over RCCL.  RCCL refuses two ranks on one device, so here two ``bench.py`` ranks share
+cuda:0 over gloo (``DTF_BENCH_BACKEND=gloo``).  Everything else is the N > 1 path of the bench:
+the bucketed all-reduce hooks firing during backward, the exposed-comm figures, the MAX-over-ranks
+timing and the rank-0 JSON line.  Both the mirrored strategy and the colocated parameter-server
+strategy (BASELINE config 4) run.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_two_ranks(tmp_path, extra):
+    from distributedtensorflow_amd.cluster.launcher import free_ports
+    port = free_ports(1)[0]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT,
+                   OMP_NUM_THREADS="2", DTF_BENCH_BACKEND="gloo")
+        out = open(tmp_path / f"rank{r}.out", "w")
+        err = open(tmp_path / f"rank{r}.err", "w")
+        procs.append((subprocess.Popen(
+            [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "16",
+             "--image-size", "96", "--steps", "3", "--warmup", "2", *extra],
+            env=env, stdout=out, stderr=err, cwd=ROOT), out, err))
+    try:
+        for p, _, _ in procs:
+            p.wait(timeout=100)
+    finally:
+        for p, out, err in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+            out.close()
+            err.close()
+    for r, (p, _, _) in enumerate(procs):
+        assert p.returncode == 0, open(tmp_path / f"rank{r}.err").read()[-3000:]
+    lines = [ln for ln in open(tmp_path / "rank0.out").read().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, lines
+    # only rank 0 reports (gloo itself may print a connection line)
+    assert not any(ln.startswith("{") for ln in open(tmp_path / "rank1.out").read().splitlines())
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_mirrored(tmp_path):
+    rec = _run_two_ranks(tmp_path, [])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 2
+    cfg = rec["config"]
+    assert cfg["global_batch"] == 32 and cfg["per_gpu_batch"] == 16
+    assert cfg["parallelism"] == "dp2"
+    assert cfg["comm_backend"] == "gloo" and cfg["backend"] != "reference"
+    assert cfg["native_ext"].startswith("distributedtensorflow_amd/_lib/_dtf_hip")
+    comm = cfg["comm"]
+    assert comm["buckets"] >= 2 and comm["steps"] == 3
+    # every bucket but the last launches from a backward hook, before backward returns
+    assert comm["early_launches"] >= 3 * (comm["buckets"] - 1), comm
+    assert comm["exposed_ms_per_step"] >= 0.0
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0
+    assert abs(rec["value"] - 32 * 1000.0 / rec["ms_per_step"]) / rec["value"] < 1e-3
+    assert rec["config"]["final_loss"] == rec["config"]["final_loss"]   # finite, not NaN
+
+
+def test_bench_two_ranks_colocated_ps(tmp_path):
+    rec = _run_two_ranks(tmp_path, ["--strategy", "ps", "--num-ps", "1"])
+    cfg = rec["config"]
+    assert cfg["parallelism"] == "ps1+dp2"
+    assert cfg["comm_backend"] == "gloo"
+    # the owner reduces and broadcasts on the same bucket plan, launched from backward hooks
+    assert cfg["comm"]["buckets"] >= 2 and cfg["comm"]["early_launches"] >= 3
+    assert rec["value"] > 0
