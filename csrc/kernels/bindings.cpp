@@ -58,6 +58,7 @@ void dtf_conv_set_dma_mode(int);
 void dtf_conv_set_small_k(int);
 void dtf_conv_set_stem_halo(int);
 void dtf_conv_set_halo_strips(int);
+void dtf_conv_set_halo_freg(int);
 void dtf_bn_infer_finalize(int, const float*, const float*, const float*, const float*, float,
                            float*, float*, float*, float*, hipStream_t);
 void dtf_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, uint8_t*, const float*, const float*,
@@ -373,6 +374,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("conv_set_stem_halo", &dtf_conv_set_stem_halo);
   m.def("conv_set_halo_strips", &dtf_conv_set_halo_strips);
+  m.def("conv_set_halo_freg", &dtf_conv_set_halo_freg);
   m.def("conv_set_small_k", &dtf_conv_set_small_k);
   m.def("bn_fwd_finalize_g", [](uintptr_t part, int G, long M, int C, uintptr_t gamma,
                                 uintptr_t beta, uintptr_t rm, uintptr_t rv, float mom, float eps,

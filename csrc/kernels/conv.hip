@@ -777,6 +777,7 @@ struct HaloCfg {
   static constexpr int LDC = NT + 8;
   static constexpr size_t LDS = (size_t)(PIXAL * C + 2 * WST) * 2;
   static constexpr size_t lds(int st) { return (size_t)(st * PIXAL * C + 2 * WST) * 2; }
+  static constexpr size_t LDS_FREG = (size_t)PIXAL * C * 2;    // FREG: the patch only
   static_assert(M % (16 * WMW) == 0 && NT % (16 * WNW) == 0, "halo tiling");
   static_assert((size_t)M * LDC * 2 + (size_t)2 * NT * (kThreads / NT) * 4 <= (size_t)PIXAL * C * 2,
                 "halo epilogue must fit in the patch region");
@@ -798,7 +799,14 @@ DTF_DEV int halo_swz(int u) { return C == 64 ? (((u >> 1) & 3) << 1) : ((u & 7) 
 // block, so two strips per block halve the filter's L2 -> LDS traffic.  Measured no faster at
 // b2048 (one 8-wave block per CU instead of two 4-wave blocks: the blocks' barrier phases no
 // longer overlap; profiles/measurements/r2_halo_strips_ab_b2048.txt), so ST = 1 by default.
-template <int C, int W, int WMW, int NT, int ST = 1>
+//
+// FREG: the filter never enters LDS.  Each wave streams its own B fragments (its NF x 16 output
+// channels x 64 input channels per step) from L2 straight into VGPRs, D steps ahead of the MFMAs
+// that use them (a register ring), so the K loop has no barrier and no per-step wait on a DMA that
+// was issued only one step earlier (~190 ns of MFMA cover against an L2 round trip several times
+// that).  LDS holds only the patch: 44-46 KB per block instead of 60-78 KB, which leaves room for
+// a third block per CU.  The MFMA order is unchanged, so the outputs are bit-identical.
+template <int C, int W, int WMW, int NT, int ST = 1, bool FREG = false>
 __global__ void __launch_bounds__(kThreads * ST, ST == 1 ? 2 : 1)
 conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                     bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
@@ -850,7 +858,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
       dma16(rw, lds_w + (uint32_t)(stage * H::WST) * 2u + (uint32_t)q * 1024u, off);
     }
   };
-  issue_w(0, 0);
+  if constexpr (!FREG) issue_w(0, 0);
 
   // per-lane A rows: output pixel m = wm * (MF * 16) + 16 i + frow -> patch pixel of tap (0, 0)
   const int frow = lane & 15, fq = lane >> 4;
@@ -868,6 +876,57 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
 #pragma unroll
     for (int j = 0; j < H::NF; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (FREG) {
+    static_assert(ST == 1, "FREG: one strip per block");
+    constexpr int NSTEP = 9 * H::KS;                 // halo_family() admits 9-tap convs only
+    constexpr int D = H::KS == 2 ? 3 : 2;            // register-ring depth (steps in flight)
+    const bf16_t* wr[H::NF];
+#pragma unroll
+    for (int j = 0; j < H::NF; ++j)
+      wr[j] = Wt + (long)(n0 + wn * (H::NF * 16) + 16 * j + frow) * g.Kpad + fq * 8;
+    bf16x8_t bq[D][2][H::NF];
+    auto ldB = [&](int step, bf16x8_t (&b)[2][H::NF]) {
+      const int t = step / H::KS, s = step - t * H::KS;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < H::NF; ++j)
+          b[ks][j] = *reinterpret_cast<const bf16x8_t*>(wr[j] + t * C + s * 64 + ks * 32);
+    };
+#pragma unroll
+    for (int p = 0; p < D; ++p) ldB(p, bq[p]);
+    // the patch DMAs were issued before these D * 2 * NF loads: waiting until only those are
+    // outstanding means this wave's patch pieces have landed; the barrier covers everyone's
+    static_assert(D * 2 * H::NF == 8 || D * 2 * H::NF == 12, "add the wait count");
+    if constexpr (D * 2 * H::NF == 8) DTF_WAIT_VM(8);
+    else DTF_WAIT_VM(12);
+    __syncthreads();
+#pragma unroll
+    for (int step = 0; step < NSTEP; ++step) {
+      const int t = step / H::KS, s = step - t * H::KS;
+      const int dpix = taps.dh[t] * H::PW + taps.dw[t];
+      const int dupix = taps.dh[t] * W + taps.dw[t];
+      bf16x8_t (&cur)[2][H::NF] = bq[step % D];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int pch = s * 8 + ks * 4 + fq;
+#pragma unroll
+        for (int i = 0; i < H::MF; ++i) {
+          const int p = pbase[i] + dpix;
+          const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(
+              patch + p * C + ((pch ^ halo_swz<C>(ubase[i] + dupix)) << 3));
+#pragma unroll
+          for (int j = 0; j < H::NF; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, cur[ks][j], acc[i][j], 0, 0, 0);
+        }
+      }
+      // refill the slot this step consumed; the scheduling fences keep the loads here (left
+      // alone, the compiler sinks them next to their use and the ring degenerates to vmcnt(1-3))
+      __builtin_amdgcn_sched_barrier(0);
+      if (step + D < NSTEP) ldB(step + D, cur);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
   const int nsteps = taps.n * H::KS;
   for (int step = 0; step < nsteps; ++step) {
     DTF_WAIT_VM(0);            // patch (step 0) and this step's filter slice landed (own DMAs)...
@@ -897,6 +956,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
       }
     }
+  }
   }
   DTF_WAIT_VM(0);
   __syncthreads();
@@ -1127,6 +1187,10 @@ static bool use_halo(const ConvGeom& g, const TapTable& taps) { return halo_fami
 // strips per halo block, per family (bit 0: 56 x 56 x 64, bit 1: 28 x 28 x 128)
 static int g_halo_st = 0;   // measured: no faster (one 8-wave block per CU), see r2_halo_strips_ab_b2048.txt
 void dtf_conv_set_halo_strips(int v) { g_halo_st = v; }
+// filter streamed into registers instead of an LDS ring, per family (bit 0: 56 x 56 x 64,
+// bit 1: 28 x 28 x 128); see conv3x3_halo_kernel FREG
+static int g_halo_freg = 0;
+void dtf_conv_set_halo_freg(int v) { g_halo_freg = v; }
 template <int C, int W, int WMW, int NT>
 static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
                         const TapTable& taps, float* stats, int tiles, int strips, hipStream_t st) {
@@ -1141,6 +1205,10 @@ static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const Conv
     hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 2>),
                        dim3((unsigned)((tiles + 1) / 2), g.Kout / NT), dim3(2 * kThreads), Hc::lds(2),
                        st, X, Wt, Y, g, taps, stats);
+  } else if (g_halo_freg & (C == 64 ? 1 : 2)) {
+    hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 1, true>),
+                       dim3((unsigned)tiles, g.Kout / NT), dim3(kThreads), Hc::LDS_FREG, st, X, Wt,
+                       Y, g, taps, stats);
   } else {
     hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 1>), dim3((unsigned)tiles, g.Kout / NT),
                        dim3(kThreads), Hc::lds(1), st, X, Wt, Y, g, taps, stats);

@@ -346,7 +346,7 @@ def test_halo_conv3x3_matches_implicit_gemm(N, H, C, K):
     """Halo-tiled 3x3 kernels (56x56x64 and 28x28x128 families) == the implicit-GEMM kernel bit
     for bit (same tap / k order) for the forward and the data gradient, with one and with two
     row strips per block (N=3 at 28x28: an odd strip count, the last block's second strip is
-    dead); fused BN statistics match."""
+    dead) and with the filter streamed through registers (FREG); fused BN statistics match."""
     nat = _native()
     torch.manual_seed(0)
     x = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
@@ -355,9 +355,10 @@ def test_halo_conv3x3_matches_implicit_gemm(N, H, C, K):
     dy = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
     outs = []
     try:
-        for halo, strips in ((3, 0), (3, 3), (0, 0)):
+        for halo, strips, freg in ((3, 0, 0), (3, 0, 3), (3, 3, 0), (0, 0, 0)):
             nat._K.conv_set_halo(halo)
             nat._K.conv_set_halo_strips(strips)
+            nat._K.conv_set_halo_freg(freg)
             y = nat.conv2d_forward(x, w, 1, 1)
             dx = nat.conv2d_dgrad(dy, wd, x.shape, 1, 1)
             gamma = torch.ones(K, device=dev)
@@ -368,11 +369,13 @@ def test_halo_conv3x3_matches_implicit_gemm(N, H, C, K):
     finally:
         nat._K.conv_set_halo(3)
         nat._K.conv_set_halo_strips(0)
+        nat._K.conv_set_halo_freg(0)
     for o in outs[1:]:
         assert torch.equal(outs[0][0], o[0])
         assert torch.equal(outs[0][1], o[1])
     assert torch.equal(outs[0][2], outs[1][2])      # same strips -> same BN statistics slab rows
-    torch.testing.assert_close(outs[0][2], outs[2][2], atol=2e-2, rtol=1e-2)
+    assert torch.equal(outs[0][2], outs[2][2])
+    torch.testing.assert_close(outs[0][2], outs[3][2], atol=2e-2, rtol=1e-2)
     ref = _ref()
     yr = ref.conv2d(x.float(), w.float(), 1, 1)
     assert _rel(outs[0][0], yr) < 1e-2
