@@ -196,7 +196,10 @@ DTF_DEV uint32_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 
 // HI_OCC (BK 32, g_small_k bit 4): ask for <= 128 VGPRs -> 4 waves/SIMD, so the 35-KB-LDS 1x1
 // launches can run 4 blocks per CU instead of 3
-template <int WAVES_M, int WAVES_N, int BK, int GATHER, bool BNB, bool HI_OCC = false>
+// STATS: the launch fuses the BatchNorm statistics (stats != nullptr); a template flag so the
+// launches without them (data gradients) keep their register budget
+template <int WAVES_M, int WAVES_N, int BK, int GATHER, bool BNB, bool HI_OCC = false,
+          bool STATS = false>
 __global__ void __launch_bounds__(kThreads, HI_OCC ? 4 : 2)
 conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                   bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
@@ -428,6 +431,15 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
       bj[j] = col < g.Kout ? g.bias[col] : 0.f;
     }
   }
+  // Fused BatchNorm statistics (training forward) from the registers: per output channel, the
+  // sum and sum of squares of this tile's bf16-ROUNDED outputs (exactly what the BN will
+  // normalise).  Each lane sums its column over its 16 rows, the 4 lane groups sharing a column
+  // combine by cross-lane adds, and the WAVES_M waves of a column meet in LDS; thread `col`
+  // writes row `tm` of the [tiles_m][2][Kout] slab that the BN finalize combines in a fixed
+  // order.  (The earlier pass over the staged tile cost 64 dependent 2-byte LDS reads per thread
+  // in the epilogue of every tile.)
+  constexpr bool do_stats = STATS;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -438,10 +450,41 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
         const int col = wn * 64 + j * 16 + frow;
         float v = acc[i][j][r] + bj[j];
         if (g.relu) v = fmaxf(v, 0.f);
-        st[row * LDC + col] = f2bf(v);
+        const bf16_t h = f2bf(v);
+        st[row * LDC + col] = h;
+        if (do_stats && m0 + row < M) {
+          const float q = bf2f(h);
+          s1[j] += q;
+          s2[j] += q * q;
+        }
       }
+  float* red = reinterpret_cast<float*>(st + BM * LDC);   // [WAVES_M][2][BN], past the tile
+  if (do_stats) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[j] += __shfl_xor(s1[j], 16, 64);
+      s1[j] += __shfl_xor(s1[j], 32, 64);
+      s2[j] += __shfl_xor(s2[j], 16, 64);
+      s2[j] += __shfl_xor(s2[j], 32, 64);
+    }
+    if (fq == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + frow;
+        red[(wm * 2 + 0) * BN + col] = s1[j];
+        red[(wm * 2 + 1) * BN + col] = s2[j];
+      }
+    }
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();
+  if (do_stats && tid < BN && n0 + tid < g.Kout) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < WAVES_M; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
+    stats[((long)tm * 2 + 0) * g.Kout + n0 + tid] = a;
+    stats[((long)tm * 2 + 1) * g.Kout + n0 + tid] = b;
+  }
   BnbAcc ba;
   if constexpr (BNB) ba.init(bnb, n0 + oc * 8, col_ok);
 #pragma unroll
@@ -458,33 +501,6 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   if constexpr (BNB)
     ba.template flush<BN, kThreads>(bnb, reinterpret_cast<float*>(st + BM * LDC), tid / OCPR, oc,
                                     OROWS, tid, tm, n0, g.Kout);
-  if (stats) {
-    // Fused BatchNorm statistics (training forward): per output channel, sum and sum of
-    // squares of this tile's bf16-ROUNDED outputs (exactly what the BN will normalise), written
-    // as row `tm` of a [tiles_m][2][Kout] partial slab that the BN finalize combines in a fixed
-    // order -- replaces a full re-read of the conv output by a separate stats kernel.
-    constexpr int GROUPS = kThreads / BN;          // row groups per column
-    constexpr int RPG = BM / GROUPS;
-    float* red = reinterpret_cast<float*>(st + BM * LDC);   // [GROUPS][2][BN], past the tile
-    const int col = tid % BN, grp = tid / BN;
-    float s1 = 0.f, s2 = 0.f;
-    const int rend = min(RPG * (grp + 1), M - m0);
-    for (int r = RPG * grp; r < rend; ++r) {
-      const float v = bf2f(st[r * LDC + col]);
-      s1 += v;
-      s2 += v * v;
-    }
-    red[(grp * 2 + 0) * BN + col] = s1;
-    red[(grp * 2 + 1) * BN + col] = s2;
-    __syncthreads();
-    if (grp == 0 && n0 + col < g.Kout) {
-      float a = 0.f, b = 0.f;
-#pragma unroll
-      for (int k = 0; k < GROUPS; ++k) { a += red[(k * 2 + 0) * BN + col]; b += red[(k * 2 + 1) * BN + col]; }
-      stats[((long)tm * 2 + 0) * g.Kout + n0 + col] = a;
-      stats[((long)tm * 2 + 1) * g.Kout + n0 + col] = b;
-    }
-  }
 }
 
 template <int WM, int WN, int BK, int GEN>
@@ -511,11 +527,19 @@ void launch_cfg(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
     else
       throw std::runtime_error("conv: fused BN-backward sums need a C % 32 == 0 dgrad");
   } else if (BK == 32 && GEN == 0 && (g_small_k & 16)) {
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, false, BK == 32 && GEN == 0>),
-                       dim3((unsigned)tiles), dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
+    if (stats)
+      hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, false, BK == 32 && GEN == 0, true>),
+                         dim3((unsigned)tiles), dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
+    else
+      hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, false, BK == 32 && GEN == 0>),
+                         dim3((unsigned)tiles), dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
   } else {
-    hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, false>), dim3((unsigned)tiles),
-                       dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
+    if (stats)
+      hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, false, false, true>),
+                         dim3((unsigned)tiles), dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
+    else
+      hipLaunchKernelGGL((conv_igemm_kernel<WM, WN, BK, GEN, false>), dim3((unsigned)tiles),
+                         dim3(kThreads), lds, st, X, Wt, Y, g, taps, stats, bnb);
   }
 }
 

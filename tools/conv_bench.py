@@ -60,7 +60,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None, help="comma list of layer names to run")
-    ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
+    ap.add_argument("--kinds", default="fwd,dgrad,wgrad", help="fwd,fwdbn,dgrad,wgrad")
     ap.add_argument("--dma", type=int, default=-1,
                     help="conv kernel choice: -1 auto, 0 register-staged only, 1 LDS-DMA when legal")
     ap.add_argument("--small-k", type=int, default=None,
@@ -97,7 +97,10 @@ def main():
         dy = torch.randn_like(y)
         flops = 2.0 * B * P * Q * K * R * R * C
         xb, yb, wb = x.numel() * 2, y.numel() * 2, w.numel() * 2
-        cases = [("fwd", lambda: native.conv2d_forward(x, w, s, p), xb + yb + wb)]
+        # fwdbn: the training-step forward, BatchNorm partial sums fused into the epilogue
+        part = torch.empty(((B * P * Q) // 64 + 2) * 2 * K, device="cuda", dtype=torch.float32)
+        cases = [("fwd", lambda: native.conv2d_forward(x, w, s, p), xb + yb + wb),
+                 ("fwdbn", lambda: native.conv2d_forward(x, w, s, p, stats=part), xb + yb + wb)]
         if C % 8 == 0:
             cases.append(("dgrad", lambda: native.conv2d_dgrad(dy, w, x.shape, s, p),
                           xb + yb + wb))
