@@ -29,9 +29,64 @@ from .hooks import (CheckpointSaverHook, InjectedFault, SessionRunContext, Sessi
                     StepCounterHook, SummarySaverHook)
 
 
+class GPUOptions:
+    """``tf.GPUOptions`` subset.  ``per_process_gpu_memory_fraction`` caps this process's share
+    of the device's HBM in PyTorch's caching allocator; ``allow_growth`` is the allocator's native
+    behaviour (memory is reserved on demand, never up front); ``visible_device_list`` picks the
+    device by index into the listed ids (the process keeps one GPU, as everywhere here)."""
+
+    def __init__(self, per_process_gpu_memory_fraction=0.0, allow_growth=True,
+                 visible_device_list=""):
+        self.per_process_gpu_memory_fraction = float(per_process_gpu_memory_fraction or 0.0)
+        self.allow_growth = bool(allow_growth)
+        self.visible_device_list = str(visible_device_list or "")
+
+    def apply(self):
+        if not torch.cuda.is_available():
+            return None
+        dev = torch.cuda.current_device()
+        if self.visible_device_list:
+            ids = [int(t) for t in self.visible_device_list.split(",") if t.strip()]
+            dev = ids[0]
+            torch.cuda.set_device(dev)
+        if 0.0 < self.per_process_gpu_memory_fraction <= 1.0:
+            torch.cuda.set_per_process_memory_fraction(self.per_process_gpu_memory_fraction, dev)
+        return dev
+
+
+def parse_device_filter(spec):
+    """'/job:ps', '/job:worker/task:3', '/job:worker/replica:0/task:1' -> (job, task or None).
+    Fields TF allows but this framework has one of (replica, device) are accepted and ignored."""
+    job, task = None, None
+    for part in str(spec).strip().strip("/").split("/"):
+        if not part:
+            continue
+        key, _, val = part.partition(":")
+        key = key.lower()
+        if key == "job":
+            job = val
+        elif key == "task":
+            task = int(val)
+        elif key in ("replica", "device", "cpu", "gpu"):
+            pass
+        else:
+            raise ValueError(f"bad device filter {spec!r}: unknown field {key!r}")
+    if job is None:
+        raise ValueError(f"bad device filter {spec!r}: no /job:")
+    return job, task
+
+
 class ConfigProto:
     """``tf.ConfigProto`` subset (``run_mnist_distributed.py:122-124``,
-    ``templates/00_mnist_replica.py:213-217``).  Thread counts are applied to torch's CPU pools."""
+    ``templates/00_mnist_replica.py:213-217``).  Thread counts are applied to torch's CPU pools;
+    ``gpu_options`` (a :class:`GPUOptions` or a dict of its fields) to the device allocator.
+
+    ``device_filters`` (e.g. ``["/job:ps", "/job:worker/task:1"]``): the tasks this session may
+    depend on.  :meth:`device_visible` answers for a (job, task); the between-graph PS client only
+    ever talks to PS tasks and its own task, so the reference's usual filter is always satisfied,
+    and a filter that hides every PS task while variables live there is refused at session start
+    (TF would hang waiting for an invisible device).  ``log_device_placement`` prints where each
+    variable lives when the session is created."""
 
     def __init__(self, allow_soft_placement=True, log_device_placement=False,
                  intra_op_parallelism_threads=0, inter_op_parallelism_threads=0,
@@ -41,8 +96,28 @@ class ConfigProto:
         self.intra_op_parallelism_threads = intra_op_parallelism_threads
         self.inter_op_parallelism_threads = inter_op_parallelism_threads
         self.device_filters = list(device_filters or [])
+        self._filters = [parse_device_filter(f) for f in self.device_filters]
+        if isinstance(gpu_options, dict):
+            gpu_options = GPUOptions(**gpu_options)
         self.gpu_options = gpu_options
         self.extra = kw
+
+    def device_visible(self, job, task=None):
+        if not self._filters:
+            return True
+        return any(j == job and (t is None or task is None or t == task) for j, t in self._filters)
+
+    def check_placement(self, strategy):
+        """Refuse filters that hide the parameter servers this session's variables live on."""
+        server = getattr(strategy, "server", None)
+        if server is None or not self._filters:
+            return
+        num_ps = server.cluster.num_tasks("ps")
+        if num_ps <= 0:
+            return
+        if not any(self.device_visible("ps", t) for t in range(num_ps)):
+            raise ValueError(f"device_filters {self.device_filters} hide every /job:ps task, but "
+                             f"the variables live on {num_ps} parameter server(s)")
 
     def apply(self):
         # clamp to the CPUs this process may use (utils.cpu.usable_cpus): the reference passes
@@ -56,6 +131,26 @@ class ConfigProto:
                 torch.set_num_interop_threads(min(int(self.inter_op_parallelism_threads), cap))
             except RuntimeError:
                 pass   # can only be set once per process
+        if self.gpu_options is not None:
+            self.gpu_options.apply()
+
+
+def log_placement(model=None, optimizer=None, strategy=None, out=None):
+    """``log_device_placement``: one line per variable -- its name, shape and where it lives
+    (the owning PS task for sharded variables, else this replica's device)."""
+    import sys
+    out = out or sys.stderr
+    params = []
+    if optimizer is not None and getattr(optimizer, "space", None) is not None:
+        params = list(optimizer.space.order)
+    elif model is not None:
+        params = list(model.parameters())
+    owner = getattr(strategy, "variable_owner", None)
+    for p in params:
+        name = getattr(p, "_dtf_name", None) or getattr(p, "name", None) or "variable"
+        where = owner(p) if callable(owner) else None
+        where = where or str(p.device)
+        print(f"{name} {tuple(p.shape)}: {where}", file=out)
 
 
 RunConfig = ConfigProto
@@ -206,6 +301,8 @@ class MonitoredTrainingSession:
         if self.config is not None and hasattr(self.config, "apply"):
             self.config.apply()
         sc = self.scaffold
+        if self.config is not None and hasattr(self.config, "check_placement"):
+            self.config.check_placement(self.strategy)
         restored = False
         if self.is_chief and self.checkpoint_dir and sc.saver is not None:
             ckpt = latest_checkpoint(self.checkpoint_dir)
@@ -219,6 +316,8 @@ class MonitoredTrainingSession:
             client = getattr(self.strategy, "ps_client", None)
             if client is not None:
                 sc.global_step.assign(client.global_step)
+        if self.config is not None and getattr(self.config, "log_device_placement", False):
+            log_placement(sc.model, sc.optimizer, self.strategy)
         self._session = _Session(sc, self.strategy, self.is_chief, self.checkpoint_dir,
                                  self._writer)
         for h in self.hooks:
