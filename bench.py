@@ -49,7 +49,10 @@ def parse():
     p.add_argument("--impl", choices=("dtf", "torch"), default="dtf")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--lr", type=float, default=0.1)
-    p.add_argument("--bucket-mb", type=float, default=64)
+    p.add_argument("--bucket-mb", default="64",
+                   help="all-reduce bucket size in MB, or 'auto': at N > 1, after the warm-up, "
+                        "time 2 steps at each of 16/32/64/128 MB (max over ranks) and keep the "
+                        "fastest for the timed steps (SURVEY.md 5.8)")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--model", choices=("resnet50", "bert_base"), default="resnet50",
                    help="resnet50: the headline metric; bert_base: BASELINE config 5 "
@@ -67,6 +70,8 @@ def parse():
                         "benchmark every solution once and write the table to --gemm-tuning-out")
     p.add_argument("--gemm-tuning-out", default=None)
     args = p.parse_args()
+    args.bucket_auto = args.bucket_mb == "auto"
+    args.bucket_mb = 64.0 if args.bucket_auto else float(args.bucket_mb)
     if args.batch is None:
         args.batch = 512 if args.model == "bert_base" else 1984
     return args
@@ -230,6 +235,34 @@ def build_torch(args, dev):
     return step, None
 
 
+def tune_buckets(args, opt, strategy, step, images, labels, sync, dev, steps=2):
+    """All-reduce bucket size chosen by measurement (SURVEY.md 5.8 "auto-tune in the benchmark"):
+    each candidate replaces the optimizer's reducer (hooks detached and re-registered), runs one
+    untimed step and ``steps`` timed ones; the rank-max time decides, identically on every rank."""
+    results = {}
+    for mb in (16, 32, 64, 128):
+        opt._reducer.close()
+        strategy.bucket_bytes = int(mb * (1 << 20))
+        opt._reducer = strategy.make_gradient_reducer(opt.space)
+        step(images, labels)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(images, labels)
+        sync()
+        t = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        results[mb] = round(float(t.item()) / steps * 1e3, 3)
+    best = min(results, key=results.get)
+    opt._reducer.close()
+    strategy.bucket_bytes = int(best * (1 << 20))
+    opt._reducer = strategy.make_gradient_reducer(opt.space)
+    step(images, labels)
+    sync()
+    args.bucket_mb = float(best)
+    return results
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,6 +301,7 @@ def main():
     # the process group that carried the gradients ("nccl" = RCCL on ROCm; None at N = 1)
     native_info["comm_backend"] = dist.get_backend() if dist.is_initialized() else None
 
+    strategy = None
     B, S = args.batch, args.image_size
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -275,7 +309,7 @@ def main():
         from distributedtensorflow_amd.data.synthetic import SyntheticMLM
         if args.lr == 0.1 and "--lr" not in sys.argv:
             args.lr = 1e-3
-        bert_step, _ = (build_bert if args.impl == "dtf" else build_torch_bert)(args, dev)
+        bert_step, strategy = (build_bert if args.impl == "dtf" else build_torch_bert)(args, dev)
         opt_for_stats = getattr(bert_step, "optimizer", None)
         d = next(iter(SyntheticMLM(B, args.seq_len, max_predictions=args.max_predictions,
                                    device=dev, seed=1234 + rank)))
@@ -286,7 +320,7 @@ def main():
             return bert_step(batch)
         images = labels = None
     elif args.impl == "dtf":
-        step, _ = build_dtf(args, dev)
+        step, strategy = build_dtf(args, dev)
         opt_for_stats = step.optimizer
         images = torch.randn(B, S, S, 3, device=dev, generator=g).to(torch.bfloat16)  # NHWC
     else:
@@ -308,6 +342,10 @@ def main():
     sync()
     log(f"warmup {args.warmup} steps in {time.time() - t0:.1f}s, loss={float(loss):.4f}")
 
+    bucket_tune = None
+    if args.bucket_auto and world > 1 and hasattr(getattr(opt_for_stats, "_reducer", None), "close"):
+        bucket_tune = tune_buckets(args, opt_for_stats, strategy, step, images, labels, sync, dev)
+        log(f"bucket auto-tune (ms/step): {bucket_tune}; using {args.bucket_mb:g} MB")
     comm = getattr(getattr(opt_for_stats, "_reducer", None), "stats", None)
     if comm is not None:
         comm.reset_timing()
@@ -346,7 +384,8 @@ def main():
                        "gemm_tuning": os.path.basename(gemm_table) if gemm_table else "default",
                        "final_loss": round(final_loss, 4),
                        "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
-                       "comm": comm_info, **native_info},
+                       "comm": comm_info, "bucket_mb": args.bucket_mb,
+                       "bucket_tune_ms": bucket_tune, **native_info},
         }
         print(json.dumps(rec), flush=True)
     elif rank == 0:
@@ -364,7 +403,8 @@ def main():
                        "impl": args.impl, "optimizer": "momentum0.9+wd1e-4, lr 0.1*B/256 warmup500+cosine",
                        "final_loss": round(final_loss, 4),
                        "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
-                       "comm": comm_info, **native_info},
+                       "comm": comm_info, "bucket_mb": args.bucket_mb,
+                       "bucket_tune_ms": bucket_tune, **native_info},
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -170,6 +170,12 @@ class BucketedAllReduce:
             # (caught by tests/test_distributed.py direct_grad_writes), so it is a no-op here.
             v._dtf_grad_ready = None
 
+    def close(self):
+        """Detach the backward hooks (before a re-bucketed reducer replaces this one)."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
     def _make_hook(self, i):
         def hook(_p):
             b = self.var_bucket[i]

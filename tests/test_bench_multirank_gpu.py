@@ -79,3 +79,17 @@ def test_bench_two_ranks_colocated_ps(tmp_path):
     # the owner reduces and broadcasts on the same bucket plan, launched from backward hooks
     assert cfg["comm"]["buckets"] >= 2 and cfg["comm"]["early_launches"] >= 3
     assert rec["value"] > 0
+
+
+def test_bench_two_ranks_bucket_autotune(tmp_path):
+    """--bucket-mb auto: every candidate re-buckets the live reducer (hooks detached and
+    re-registered), the rank-max timing picks one, and the timed steps run on it."""
+    rec = _run_two_ranks(tmp_path, ["--bucket-mb", "auto"])
+    cfg = rec["config"]
+    tune = cfg["bucket_tune_ms"]
+    assert sorted(int(k) for k in tune) == [16, 32, 64, 128]
+    assert all(v > 0 for v in tune.values())
+    best = min(tune, key=tune.get)
+    assert cfg["bucket_mb"] == float(best)
+    comm = cfg["comm"]
+    assert comm["steps"] == 3 and comm["early_launches"] >= 3 * (comm["buckets"] - 1)
