@@ -780,6 +780,12 @@ conv_igemm_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
 // LDS rows are 128 B (64 bf16) with the chunk XOR swizzle of swz_chunk<64> by row (patch pixel
 // index / filter row), applied on the DMA source side.
 constexpr int kHaloTH = 4;        // output rows per block (whole image rows)
+#ifndef DTF_HALO_FREG_D1
+#define DTF_HALO_FREG_D1 2        // FREG register-ring depth, 56 x 56 x 64 family (steps)
+#endif
+#ifndef DTF_HALO_FREG_D2
+#define DTF_HALO_FREG_D2 3        // FREG register-ring depth, 28 x 28 x 128 family (steps)
+#endif
 
 // C: input channels (64 | 128), W: image width (56 | 28), WMW x (4 / WMW) waves, NT output
 // channels per block.  7 x 2 MFMA fragments per wave in both families:
@@ -903,7 +909,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   if constexpr (FREG) {
     static_assert(ST == 1, "FREG: one strip per block");
     constexpr int NSTEP = 9 * H::KS;                 // halo_family() admits 9-tap convs only
-    constexpr int D = H::KS == 2 ? 3 : 2;            // register-ring depth (steps in flight)
+    constexpr int D = H::KS == 2 ? DTF_HALO_FREG_D2 : DTF_HALO_FREG_D1;   // ring depth (steps)
     const bf16_t* wr[H::NF];
 #pragma unroll
     for (int j = 0; j < H::NF; ++j)
@@ -921,9 +927,16 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     for (int p = 0; p < D; ++p) ldB(p, bq[p]);
     // the patch DMAs were issued before these D * 2 * NF loads: waiting until only those are
     // outstanding means this wave's patch pieces have landed; the barrier covers everyone's
-    static_assert(D * 2 * H::NF == 8 || D * 2 * H::NF == 12, "add the wait count");
+    static_assert(D * 2 * H::NF <= 40 && D * 2 * H::NF % 4 == 0, "add the wait count");
     if constexpr (D * 2 * H::NF == 8) DTF_WAIT_VM(8);
-    else DTF_WAIT_VM(12);
+    else if constexpr (D * 2 * H::NF == 12) DTF_WAIT_VM(12);
+    else if constexpr (D * 2 * H::NF == 16) DTF_WAIT_VM(16);
+    else if constexpr (D * 2 * H::NF == 20) DTF_WAIT_VM(20);
+    else if constexpr (D * 2 * H::NF == 24) DTF_WAIT_VM(24);
+    else if constexpr (D * 2 * H::NF == 28) DTF_WAIT_VM(28);
+    else if constexpr (D * 2 * H::NF == 32) DTF_WAIT_VM(32);
+    else if constexpr (D * 2 * H::NF == 36) DTF_WAIT_VM(36);
+    else DTF_WAIT_VM(40);
     __syncthreads();
 #pragma unroll
     for (int step = 0; step < NSTEP; ++step) {

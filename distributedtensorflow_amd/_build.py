@@ -65,6 +65,8 @@ def build_hip(verbose=False, jobs=None):
     headers = glob.glob(os.path.join(src_dir, "*.h")) + glob.glob(os.path.join(src_dir, "*.cuh"))
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
              "-munsafe-fp-atomics", "-ffp-contract=fast"]
+    # experiment builds only (e.g. -DDTF_HALO_FREG_D2=6); part of the object-cache key
+    flags += os.environ.get("DTF_HIP_EXTRA_FLAGS", "").split()
     inc = ["-I" + src_dir] + ["-I" + p for p in _py_includes()]
     os.makedirs(os.path.join(BUILD, "hip"), exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
