@@ -93,3 +93,16 @@ def test_bench_two_ranks_bucket_autotune(tmp_path):
     assert cfg["bucket_mb"] == float(best)
     comm = cfg["comm"]
     assert comm["steps"] == 3 and comm["early_launches"] >= 3 * (comm["buckets"] - 1)
+
+
+def test_bench_two_ranks_bert(tmp_path):
+    """BASELINE config 5 flow at N = 2: BERT-base MLM under MultiWorkerMirroredStrategy (fused
+    LAMB, bucketed all-reduce), tokens/sec JSON from rank 0."""
+    rec = _run_two_ranks(tmp_path, ["--model", "bert_base", "--seq-len", "64",
+                                    "--max-predictions", "10"])
+    cfg = rec["config"]
+    assert rec["unit"] == "tokens/sec" and cfg["model"] == "bert_base"
+    assert cfg["parallelism"] == "dp2" and cfg["global_batch"] == 32
+    assert cfg["comm_backend"] == "gloo" and cfg["comm"]["buckets"] >= 2
+    assert cfg["comm"]["early_launches"] >= 3
+    assert abs(rec["value"] - 32 * 64 * 1000.0 / rec["ms_per_step"]) / rec["value"] < 1e-3
