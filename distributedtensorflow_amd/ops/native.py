@@ -1029,7 +1029,12 @@ def _gemm_1x1(C, K, R, S, stride, pads):
     per-CU GEMM's prologue / epilogue exposed, where the conv kernel runs 3-4 blocks per CU
     (profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl, same-box bench A/B)."""
     return (_CONV_GEMM and R == 1 and S == 1 and tuple(_pair(stride)) == (1, 1)
-            and not any(pads) and C % 64 == 0 and K % 8 == 0 and C >= 512 and K >= 256)
+            and not any(pads) and C % 64 == 0 and K % 8 == 0 and C >= _GEMM_1X1_MIN_C
+            and K >= 256)
+
+
+# reduction depth from which a 1x1 conv runs on the GEMM kernel (A/B knob)
+_GEMM_1X1_MIN_C = int(os.environ.get("DTF_GEMM_1X1_MIN_C", "512"))
 
 
 class _Dense(torch.autograd.Function):
