@@ -54,6 +54,9 @@ def parse():
                         "time 2 steps at each of 16/32/64/128 MB (max over ranks) and keep the "
                         "fastest for the timed steps (SURVEY.md 5.8)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--dump-master", default=None,
+                   help="after the timed steps, save the (rank-0) fp32 master weights to this "
+                        "file (tests compare the forced-reducer run bit for bit with the plain one)")
     p.add_argument("--model", choices=("resnet50", "bert_base"), default="resnet50",
                    help="resnet50: the headline metric; bert_base: BASELINE config 5 "
                         "(MLM, LAMB, MultiWorkerMirroredStrategy) in tokens/sec")
@@ -277,7 +280,10 @@ def main():
     torch.set_num_threads(max(1, usable_cpus() // max(per_node, 1)))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1 and not dist.is_initialized():
+    # DTF_FORCE_REDUCER=1 (parallel/strategy.py): a one-rank torchrun run still builds the
+    # process group and the communicating reducer, so every RCCL call of the N > 1 path runs
+    force = os.environ.get("DTF_FORCE_REDUCER", "0") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         from distributedtensorflow_amd.parallel import init_process_group_from_env
         # RCCL (backend "nccl") is the measured path; DTF_BENCH_BACKEND=gloo exists only for the
         # multi-rank rehearsal on a one-GPU box (tests/test_bench_multirank_gpu.py), where RCCL
@@ -303,6 +309,7 @@ def main():
 
     strategy = None
     B, S = args.batch, args.image_size
+    torch.manual_seed(1234)          # random-init weights, reproducible run to run
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     if args.model == "bert_base":
@@ -332,7 +339,7 @@ def main():
         labels = torch.randint(0, 1000, (B,), device=dev, generator=g)
 
     def sync():
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -343,7 +350,7 @@ def main():
     log(f"warmup {args.warmup} steps in {time.time() - t0:.1f}s, loss={float(loss):.4f}")
 
     bucket_tune = None
-    if args.bucket_auto and world > 1 and hasattr(getattr(opt_for_stats, "_reducer", None), "close"):
+    if args.bucket_auto and dist.is_initialized() and hasattr(getattr(opt_for_stats, "_reducer", None), "close"):
         bucket_tune = tune_buckets(args, opt_for_stats, strategy, step, images, labels, sync, dev)
         log(f"bucket auto-tune (ms/step): {bucket_tune}; using {args.bucket_mb:g} MB")
     comm = getattr(getattr(opt_for_stats, "_reducer", None), "stats", None)
@@ -359,7 +366,17 @@ def main():
     # exposed communication: compute-stream wait for RCCL after backward (0 buckets at N=1)
     comm_info = comm.as_dict() if comm is not None else {"buckets": 0,
                                                          "exposed_ms_per_step": 0.0}
-    if world > 1:
+    reducer = getattr(opt_for_stats, "_reducer", None)
+    if reducer is not None:
+        comm_info["reducer"] = type(reducer).__name__
+        if hasattr(reducer, "sharded"):
+            comm_info["sharded_owners"] = bool(reducer.sharded)
+    comm_info["forced_reducer"] = force
+    if args.dump_master and opt_for_stats is not None:
+        opt_for_stats.synchronize_variables()
+        if rank == 0:
+            torch.save(opt_for_stats.space.master.detach().cpu(), args.dump_master)
+    if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -407,7 +424,7 @@ def main():
                        "bucket_tune_ms": bucket_tune, **native_info},
         }
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -1,4 +1,4 @@
-"""Local cluster launcher: start every task of a PS/worker cluster as its own process.
+"""Local cluster launcher: start every task of a cluster as its own process and keep it alive.
 
 The reference starts each task by hand (``python run_mnist_distributed.py --job_name=ps
 --task_index=0`` on every host; README).  ``launch_local`` does the same on one host: it writes a
@@ -49,20 +49,97 @@ def _cleanup_shm(pid):
             pass
 
 
+class _Task:
+    def __init__(self, job, index, spawn):
+        self.job, self.index, self._spawn = job, index, spawn
+        self.restarts = 0
+        self.log = None
+        self.proc = None
+        self.done = False           # exited 0
+        self.start()
+
+    def start(self):
+        self.proc, self.log = self._spawn(self.job, self.index, self.restarts, self.log)
+
+    @property
+    def name(self):
+        return f"{self.job}{self.index}"
+
+
+def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script):
+    """Wait for the worker tasks, restarting failed tasks meanwhile.
+
+    A task that exits non-zero while the job runs is restarted as a FRESH process (never a
+    re-exec of a process that touched the GPU) after the cluster epoch is bumped, so every
+    survivor re-forms its process group with it (cluster/rendezvous.py).  Exit code
+    ``REJOIN_EXIT_CODE`` is a parameter-server task leaving voluntarily for the new epoch: it is
+    restarted without counting against ``max_restarts``.  Once a worker finished cleanly the job
+    is ending and failures are no longer recovered."""
+    from .rendezvous import bump_epoch
+    from .server import Server
+    t0 = time.time()
+    used = 0
+    while True:
+        ending = any(t.done for t in tasks if is_worker(t))
+        for t in tasks:
+            rc = t.proc.poll()
+            if rc is None or t.done:
+                continue
+            if rc == 0:
+                t.done = True
+                continue
+            workers_alive = any(x.proc.poll() is None for x in tasks if is_worker(x))
+            voluntary = rc == Server.REJOIN_EXIT_CODE
+            if ending or not (workers_alive or not is_worker(t)) or \
+                    (not voluntary and used >= max_restarts):
+                continue                                  # final: reported as its exit code
+            if not voluntary:
+                used += 1
+                epoch = bump_epoch(store)
+            else:
+                epoch = None
+            _cleanup_shm(t.proc.pid)
+            t.log.write(f"\n[launcher] {t.name} (pid {t.proc.pid}) exited with {rc}; "
+                        + (f"restarting ({used}/{max_restarts}), cluster epoch {epoch}\n"
+                           if not voluntary else "rejoining the new cluster epoch\n"))
+            t.log.flush()
+            t.restarts += 1
+            t.start()
+        workers = [t for t in tasks if is_worker(t)]
+        if all(t.proc.poll() is not None for t in workers):
+            failed = [t for t in workers if t.proc.returncode not in (0, None) and not t.done]
+            # a crashed worker may still be restarted above; finish when none is pending
+            if not failed or used >= max_restarts or any(t.done for t in workers):
+                return
+        if time.time() - t0 > timeout_s:
+            raise subprocess.TimeoutExpired(script, timeout_s)
+        time.sleep(0.1)
+
+
 def launch_local(script, num_ps=1, num_workers=2, workdir=None, extra_args=(), env=None,
-                 timeout_s=600, grace_s=30, gpus_per_host=None, max_ps_restarts=0):
-    """``max_ps_restarts``: a PS task that dies (non-zero exit, e.g. killed) while workers are
-    still running is restarted as a FRESH process (same flags, ``DTF_RESTART_COUNT`` set) up
-    to this many times; it rejoins the next process-group generation and the workers recover
+                 timeout_s=600, grace_s=30, gpus_per_host=None, max_ps_restarts=0,
+                 max_restarts=0):
+    """Start a PS/worker cluster of ``script`` on this host and supervise it.
+
+    The launcher hosts the cluster's rendezvous store (at the chief's ``config.json`` address),
+    so any task -- the chief included -- may die: up to ``max_restarts`` failed tasks (or
+    ``max_ps_restarts``, the round-2 name) are restarted as fresh processes in a new cluster
+    epoch; survivors re-form the cluster with them and the chief re-seeds the parameter servers
     from the latest checkpoint (MonitoredTrainingSession)."""
+    from .rendezvous import connect
+    from .spec import Config
+    max_restarts = max(int(max_restarts), int(max_ps_restarts))
     workdir = os.path.abspath(workdir or os.getcwd())
     script = os.path.abspath(script)          # tasks run with cwd=workdir
     os.makedirs(workdir, exist_ok=True)
     cfg_path = os.path.join(workdir, "config.json")
     write_config(cfg_path, num_ps, num_workers)
+    host, port = Config(cfg_path).cluster_spec().rendezvous_address()
+    store = connect(timeout_s=60, host=host, port=port, is_master=True)
     base_env = dict(os.environ)
     base_env.update(env or {})
-    procs = []
+    base_env["DTF_STORE_ADDR"] = f"{host}:{port}"
+    base_env["DTF_MAX_RESTARTS"] = str(max_restarts)
 
     def spawn(job, i, restarts=0, log=None):
         e = dict(base_env)
@@ -78,48 +155,67 @@ def launch_local(script, num_ps=1, num_workers=2, workdir=None, extra_args=(), e
                f"--config={cfg_path}", *extra_args]
         return subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, env=e, cwd=workdir), log
 
-    for job, n in (("ps", num_ps), ("worker", num_workers)):
-        for i in range(n):
-            p, log = spawn(job, i)
-            procs.append([job, i, p, log, 0])
-    t0 = time.time()
+    tasks = [_Task(job, i, spawn) for job, n in (("ps", num_ps), ("worker", num_workers))
+             for i in range(n)]
     rc = {}
     try:
-        # supervise: wait for the workers, restarting crashed PS tasks meanwhile
-        while True:
-            workers_alive = [q for q in procs if q[0] == "worker" and q[2].poll() is None]
-            for q in procs:
-                job, i, p, log, restarts = q
-                if job == "ps" and p.poll() not in (None, 0) and workers_alive and \
-                        restarts < max_ps_restarts:
-                    _cleanup_shm(p.pid)
-                    log.write(f"\n[launcher] ps{i} (pid {p.pid}) exited with {p.returncode}; "
-                              f"restarting ({restarts + 1}/{max_ps_restarts})\n")
-                    log.flush()
-                    q[2], q[3] = spawn(job, i, restarts + 1, log)
-                    q[4] = restarts + 1
-            if not workers_alive:
-                break
-            if time.time() - t0 > timeout_s:
-                raise subprocess.TimeoutExpired(script, timeout_s)
-            time.sleep(0.2)
-        for job, i, p, log, _ in procs:
-            if job == "worker":
-                rc[(job, i)] = p.wait()
-        for job, i, p, log, _ in procs:
-            if job == "ps":
+        _supervise(tasks, store, lambda t: t.job == "worker", max_restarts, timeout_s, script)
+        for t in tasks:
+            if t.job == "worker":
+                rc[(t.job, t.index)] = t.proc.wait()
+        for t in tasks:
+            if t.job == "ps":
                 try:
-                    rc[(job, i)] = p.wait(timeout=grace_s)
+                    rc[(t.job, t.index)] = t.proc.wait(timeout=grace_s)
                 except subprocess.TimeoutExpired:
-                    p.terminate()
-                    rc[(job, i)] = p.wait(timeout=10)
+                    t.proc.terminate()
+                    rc[(t.job, t.index)] = t.proc.wait(timeout=10)
     finally:
-        for job, i, p, log, _ in procs:
-            if p.poll() is None:
-                p.kill()
-                p.wait()
-            log.close()
-    return rc, {f"{j}{i}": os.path.join(workdir, f"{j}{i}.log") for j, i, _, _, _ in procs}
+        for t in tasks:
+            if t.proc.poll() is None:
+                t.proc.kill()
+                t.proc.wait()
+            t.log.close()
+    return rc, {t.name: os.path.join(workdir, f"{t.name}.log") for t in tasks}
+
+
+def launch_collective(script, nproc, workdir=None, extra_args=(), env=None, timeout_s=600,
+                      max_restarts=0):
+    """torchrun-style launch of a synchronous world (Mirrored / MultiWorkerMirrored / colocated
+    PS): ``nproc`` ranks with RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* set, the rendezvous store
+    hosted HERE.  A rank that dies is restarted alone (up to ``max_restarts``) in a new cluster
+    epoch; the surviving ranks re-form the world with it in-process and continue from the
+    chief's latest checkpoint (unlike torchrun, which restarts every rank)."""
+    from .rendezvous import connect
+    workdir = os.path.abspath(workdir or os.getcwd())
+    os.makedirs(workdir, exist_ok=True)
+    port = free_ports(1)[0]
+    store = connect(timeout_s=60, host="127.0.0.1", port=port, is_master=True)
+    base_env = dict(os.environ)
+    base_env.update(env or {})
+    base_env.update({"WORLD_SIZE": str(nproc), "LOCAL_WORLD_SIZE": str(nproc),
+                     "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                     "DTF_STORE_ADDR": f"127.0.0.1:{port}", "DTF_MAX_RESTARTS": str(max_restarts)})
+
+    def spawn(job, r, restarts=0, log=None):
+        e = dict(base_env, RANK=str(r), LOCAL_RANK=str(r), DTF_RESTART_COUNT=str(restarts))
+        log = log or open(os.path.join(workdir, f"rank{r}.log"), "w")
+        return subprocess.Popen([sys.executable, os.path.abspath(script), *extra_args],
+                                stdout=log, stderr=subprocess.STDOUT, env=e, cwd=workdir), log
+
+    tasks = [_Task("rank", r, spawn) for r in range(nproc)]
+    rc = {}
+    try:
+        _supervise(tasks, store, lambda t: True, max_restarts, timeout_s, script)
+        for t in tasks:
+            rc[t.index] = t.proc.wait()
+    finally:
+        for t in tasks:
+            if t.proc.poll() is None:
+                t.proc.kill()
+                t.proc.wait()
+            t.log.close()
+    return rc, {t.name: os.path.join(workdir, f"{t.name}.log") for t in tasks}
 
 
 if __name__ == "__main__":
@@ -129,9 +225,9 @@ if __name__ == "__main__":
     ap.add_argument("--num_ps", type=int, default=1)
     ap.add_argument("--num_workers", type=int, default=2)
     ap.add_argument("--workdir", default=None)
-    ap.add_argument("--max_ps_restarts", type=int, default=0)
+    ap.add_argument("--max_restarts", "--max_ps_restarts", type=int, default=0)
     a, rest = ap.parse_known_args()
     codes, logs = launch_local(a.script, a.num_ps, a.num_workers, a.workdir, rest,
-                               max_ps_restarts=a.max_ps_restarts)
+                               max_restarts=a.max_restarts)
     print(json.dumps({"exit_codes": {f"{k[0]}{k[1]}": v for k, v in codes.items()},
                       "logs": logs}, indent=2))

@@ -11,22 +11,21 @@ protocol (any-source receives); GPU workers additionally get an RCCL group among
 workers are done, on SIGINT/SIGTERM or on the chief's shutdown request (the reference's PS never
 exits: ``README.md:7`` TODO).
 
-Recovery (TF's ``_RecoverableSession`` recreating the session after a PS restart, reference
-``run_mnist_distributed.py:146``): the rendezvous TCPStore is created once by the
-chief and outlives process groups.  Every (re)join of a rank bumps that rank's join counter in the
-store and uses it as the GENERATION of the process group it joins (``PrefixStore("g<n>")``): a
-PS task restarted by the launcher after a crash is a new process whose first join is its rank's
-second, so it meets the surviving tasks -- which called :meth:`restart_group` when they saw the
-failure -- in generation 1 without any extra coordination.
+Recovery (TF's ``_RecoverableSession`` recreating the session after a task of the cluster died,
+reference ``run_mnist_distributed.py:146``): see :mod:`.rendezvous`.  Under the
+launcher the rendezvous TCPStore lives in the launcher process, so ANY task -- the chief
+included -- can die and be restarted; every process group is created for the cluster EPOCH the
+launcher bumps before each restart, and :meth:`restart_group` moves a surviving task to it.
+Hand-started clusters (the reference's deployment) keep the chief-hosted store and fail fast.
 """
 from __future__ import annotations
 
-import datetime
 import os
 
 import torch
 import torch.distributed as dist
 
+from . import rendezvous
 from .spec import ClusterSpec, Config
 
 
@@ -49,6 +48,7 @@ class Server:
         self.worker_group = None
         self.store = None
         self.generation = -1
+        self.watcher = None
         self._started = False
         if start:
             self.start()
@@ -80,15 +80,15 @@ class Server:
             return
         if not dist.is_initialized():
             if self.store is None:
-                # the chief hosts the store; every other task (and a restarted one) connects
-                self.store = dist.TCPStore(self.host, self.port, None, self.rank == 0,
-                                           timeout=datetime.timedelta(seconds=self.timeout_s),
-                                           wait_for_workers=False)
-            self.generation = int(self.store.add(f"dtf/join/{self.rank}", 1)) - 1
-            dist.init_process_group(
-                "gloo", store=dist.PrefixStore(f"g{self.generation}", self.store),
-                rank=self.rank, world_size=self.world_size,
-                timeout=datetime.timedelta(seconds=self.timeout_s))
+                # the launcher's store (DTF_STORE_ADDR); without a launcher the chief hosts it
+                self.store = rendezvous.connect(self.timeout_s, self.host, self.port,
+                                                is_master=self.rank == 0)
+            self.generation = rendezvous.current_epoch(self.store)
+            rendezvous.init_group("gloo", self.rank, self.world_size, self.store,
+                                  self.generation, self.timeout_s)
+            if self.watcher is not None:
+                self.watcher.stop()
+            self.watcher = rendezvous.EpochWatcher(self.generation).start()
         wb = self.worker_backend
         if wb is None:
             wb = "gloo"
@@ -101,24 +101,42 @@ class Server:
         if self.job_name != "ps":
             return None
         from ..parallel.ps_service import ParameterServerService
-        svc = ParameterServerService(self.task_index, self.worker_ranks(), device=self.ps_device)
+        svc = ParameterServerService(self.task_index, self.worker_ranks(), device=self.ps_device,
+                                     cluster_changed=self.cluster_changed)
         stats = svc.serve()
         return stats
 
-    def restart_group(self):
-        """Tear down this generation's process group (a peer died) and join the next one; blocks
-        until every task -- including the restarted one -- has joined."""
-        if dist.is_initialized():
-            try:
-                dist.destroy_process_group()
-            except Exception:           # the group may already be broken
-                pass
+    REJOIN_EXIT_CODE = 75
+
+    @classmethod
+    def exit_for_rejoin(cls, stats):
+        """A PS task whose cluster moved to a new epoch (a peer died and was restarted) holds
+        no state worth keeping -- the chief re-seeds every shard from the latest checkpoint --
+        so it leaves as a whole and the launcher starts a fresh one in the new epoch.  Uses
+        ``os._exit``: the service thread may still sit in a receive on the broken group."""
+        if stats.get("rejoin"):
+            print(f"[dtf] cluster moved to a new epoch; parameter server task restarts "
+                  f"(exit {cls.REJOIN_EXIT_CODE})", flush=True)
+            os._exit(cls.REJOIN_EXIT_CODE)
+
+    def cluster_changed(self):
+        """True once the launcher restarted a task (the cluster moved to a new epoch)."""
+        return self.watcher is not None and self.watcher.changed
+
+    def restart_group(self, timeout_s=120.0):
+        """Tear down this epoch's process group (a peer died) and join the next epoch; blocks
+        until every task -- including the restarted one -- has joined.  The wait for the
+        launcher's epoch bump is bounded: a death nobody restarts raises TimeoutError."""
+        rendezvous.leave_group()
+        rendezvous.wait_for_epoch_after(self.store, self.generation, timeout_s)
         self._started = False
         self.worker_group = None
         self.start()
         return self.generation
 
     def shutdown(self):
+        if self.watcher is not None:
+            self.watcher.stop()
         if dist.is_initialized():
             dist.destroy_process_group()
         self._started = False

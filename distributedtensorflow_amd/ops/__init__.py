@@ -244,6 +244,37 @@ def mlm_loss(logits, labels, weights=None):
     return reference.mlm_loss(logits, labels, weights)
 
 
+# ----------------------------------------------------------------------------- variable fence
+# A colocated parameter server gathers the updated variable shards AFTER the optimizer step,
+# asynchronously, bucket by bucket, while the next forward already runs (parallel/ps_strategy.py).
+# Every op that reads variables first passes them to the fence, which makes the compute stream
+# wait for exactly the gather that writes them (nothing to do -- and no scan -- when no gather
+# is pending: the fence is then None).
+_PARAM_FENCE = None
+
+
+def set_param_fence(fn):
+    global _PARAM_FENCE
+    _PARAM_FENCE = fn
+
+
+def _fenced(fn):
+    import functools
+
+    @functools.wraps(fn)
+    def op(*args, **kw):
+        if _PARAM_FENCE is not None:
+            _PARAM_FENCE(args, kw)
+        return fn(*args, **kw)
+    return op
+
+
+for _name in ("conv2d", "conv2d_bias_relu", "batch_norm", "batch_norm_add_batch_norm",
+              "batch_norm_relu_max_pool", "dense", "layer_norm", "bias_dropout_add_layer_norm",
+              "embedding_layer_norm", "bias_gelu"):
+    globals()[_name] = _fenced(globals()[_name])
+del _name
+
 __all__ = [
     "set_backend", "get_backend", "GradShare", "conv2d", "conv2d_bias_relu", "batch_norm", "relu",
     "batch_norm_add_batch_norm",

@@ -103,6 +103,10 @@ class Optimizer:
     """Base class.  Subclasses implement ``_build_slots`` and ``_apply_native/_apply_reference``."""
 
     slot_names: tuple = ()
+    # the update of each element depends only on that element's gradient / slots (a sharded
+    # parameter server may then split variables between owners); LAMB's per-tensor trust ratio
+    # is not elementwise
+    elementwise: bool = True
 
     def __init__(self, learning_rate, name, weight_decay=0.0, decay_filter=None,
                  use_locking=False):
@@ -138,6 +142,7 @@ class Optimizer:
         shadow = (torch.bfloat16 if dev.type == "cuda" else None) if self.shadow_dtype == "auto" \
             else self.shadow_dtype
         self.space = FlatSpace(variables, self.decay_filter, shadow)
+        self.space.elementwise = self.elementwise      # read by sharding gradient reducers
         self._build_slots()
         self._lr_dev = torch.zeros(4, device=dev, dtype=torch.float32)
         self._nonfinite = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -223,6 +228,19 @@ class Optimizer:
             return regs
         lo, hi = rng
         return [(max(s, lo), min(e, hi), d) for s, e, d in regs if min(e, hi) > max(s, lo)]
+
+    def synchronize_variables(self):
+        """Wait for communication still writing the variables (a colocated parameter server
+        gathers updated shards overlapped with the next forward); call before reading the
+        master weights outside a training step (checkpoint, replica check, evaluation)."""
+        if self._reducer is not None:
+            self._reducer.drain()
+
+    def gather_state(self):
+        """Collective: complete every optimizer slot on every rank (a sharded parameter server
+        keeps each slot slice only on its owner) -- before a checkpoint of the slots."""
+        if self._reducer is not None:
+            self._reducer.gather_state(self.state_tensors())
 
     def nonfinite_flag(self):
         return bool(self._nonfinite.item()) if self._nonfinite is not None else False

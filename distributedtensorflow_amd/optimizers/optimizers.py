@@ -196,6 +196,7 @@ class LAMBOptimizer(Optimizer):
     (BASELINE.json config 5): per-variable trust ratio |p|/|u|."""
 
     slot_names = ("adam_m", "adam_v")     # google-research/bert optimization.py slot names
+    elementwise = False
 
     def __init__(self, learning_rate, beta1=0.9, beta2=0.999, epsilon=1e-6, weight_decay=0.01,
                  name="LAMB", chunk=4096, **kw):

@@ -47,6 +47,8 @@ def check_replicas_consistent(tensors, group=None, raise_on_mismatch=True):
     """``tensors``: a tensor, a list of tensors, or an object with a ``master`` buffer (FlatSpace)
     / a ``space`` (Optimizer).  Returns the list of per-rank fingerprints."""
     if hasattr(tensors, "space") and tensors.space is not None:
+        if hasattr(tensors, "synchronize_variables"):
+            tensors.synchronize_variables()      # pending overlapped variable gathers
         tensors = tensors.space.master
     elif hasattr(tensors, "master"):
         tensors = tensors.master

@@ -36,6 +36,8 @@ import time
 import torch
 import torch.distributed as dist
 
+from .strategy import comm_call
+
 OP_INIT, OP_PULL, OP_PUSH, OP_STOP, OP_WAIT_READY, OP_GET_STATE, OP_SET_STATE, OP_SHUTDOWN, \
     OP_GET_STEP = range(1, 10)
 HDR = 8
@@ -158,8 +160,9 @@ def _split(flat, shapes):
 class ParameterServerService:
     """The loop run by ``Server.join()`` on a ``ps`` task."""
 
-    def __init__(self, ps_index, worker_ranks, device="cpu", group=None):
+    def __init__(self, ps_index, worker_ranks, device="cpu", group=None, cluster_changed=None):
         self.ps_index = ps_index
+        self.cluster_changed = cluster_changed
         self.worker_ranks = list(worker_ranks)
         self.device = torch.device(device)
         self.group = group
@@ -189,8 +192,10 @@ class ParameterServerService:
         """Blocking any-source receives run on a service thread (gloo's ``is_completed`` is
         not updated for receives, so the loop cannot poll); the calling (main) thread keeps
         SIGINT/SIGTERM responsive and returns as soon as the service ends or is shut down."""
+        from ..cluster import rendezvous
         self._install_signal_handlers()
         self._error = None
+        rejoin = False
         t = threading.Thread(target=self._loop, name="dtf-ps-service", daemon=True)
         t.start()
         try:
@@ -199,8 +204,14 @@ class ParameterServerService:
                 dev_err = getattr(self.shard, "_error", None)
                 if dev_err is not None:
                     raise dev_err
-            if self._error is not None:
-                raise self._error
+                if self.cluster_changed is not None and self.cluster_changed():
+                    rejoin = True        # a peer died and was restarted: new epoch
+                    break
+            if self._error is not None and not rejoin:
+                if rendezvous.recovery_enabled():
+                    rejoin = True        # our group broke under a dead peer: restart with it
+                else:
+                    raise self._error
         finally:
             if self.plane != "gloo" and self.shard is not None:
                 self.stats.update({k: v for k, v in self.shard.stats.items()})
@@ -208,6 +219,7 @@ class ParameterServerService:
         self.stats["global_step"] = self._gstep()
         self.stats["data_plane"] = self.plane
         self.stats["interrupted"] = t.is_alive()
+        self.stats["rejoin"] = rejoin
         return self.stats
 
     def _gstep(self):
@@ -399,6 +411,7 @@ class PSClient:
     def data_plane_in_use(self):
         return "gloo" if not self.links else self.links[0].desc.get("plane", "?")
 
+    @comm_call
     def register(self, params, optimizer_cfg, names=None, sync=False, replicas_to_aggregate=None,
                  global_step=0, slots=None, iterations=None):
         """Chief: ship each shard's variables (and, on a restore, its optimizer slots:
@@ -427,6 +440,7 @@ class PSClient:
                       if idx else torch.zeros(0))
                 dist.send(sv, rank, group=self.group)
 
+    @comm_call
     def wait_ready(self, params):
         """Non-chief: block until the chief initialised every PS shard (TF WorkerSessionCreator)."""
         self._layout(params)
@@ -444,6 +458,7 @@ class PSClient:
             self.links = [PSLink(d, self.plans[k], d["workers"].index(me), self.space.device, k)
                           for k, d in enumerate(descs)]
 
+    @comm_call
     def pull(self):
         if self.links:
             for link in self.links:
@@ -462,6 +477,7 @@ class PSClient:
             self._assign(k, vals)
         return self.global_step
 
+    @comm_call
     def push(self, grads=None, pull=True):
         """Send gradients (default: ``p.grad``) computed at ``self.global_step``; with
         ``pull`` the reply carries the updated shard values, copied into the local variables
@@ -510,6 +526,7 @@ class PSClient:
                 if s is not None:
                     s.copy_(p.detach())
 
+    @comm_call
     def get_global_step(self):
         if self.links:
             self.global_step = self.links[0].global_step
@@ -520,6 +537,7 @@ class PSClient:
         self.global_step = int(r[0])
         return self.global_step
 
+    @comm_call
     def get_state(self):
         """(global_step, {name: tensor}, {slot_name: {name: tensor}}) across all shards."""
         values, slots, gstep = {}, {}, 0
@@ -540,6 +558,7 @@ class PSClient:
                     slots.setdefault(sname, {})[name] = t.clone()
         return gstep, values, slots
 
+    @comm_call
     def set_state(self, global_step):
         """Push the local parameter values to the PS (restore from checkpoint)."""
         for k, rank in enumerate(self.ps_ranks):

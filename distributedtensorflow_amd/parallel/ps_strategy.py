@@ -9,11 +9,12 @@ compute gradients, owners apply the optimizer, workers read back the new values:
   SyncReplicasOptimizer aggregation with stale-gradient drop).
 * **colocated, synchronous, on RCCL** (no ``server``; one process per GPU under torchrun): the
   PS shards are hosted by the GPU ranks themselves (``num_ps`` owners; 1 = "1 PS + N workers",
-  default = every rank owns a byte-balanced slice).  Per step: as soon as a gradient bucket is
-  complete during backward, each owner's piece of it is ``reduce``d to its owner over xGMI
-  (overlapped with the rest of backward); after backward the owner runs the fused optimizer on
-  exactly its slices and ``broadcast``s the updated master slices back.  With num_ps == world
-  this is a bucketed reduce-scatter / all-gather step.
+  default = every rank owns an equal chunk of every gradient bucket).  Per step: as soon as a
+  gradient bucket is complete during backward it is reduce-scattered to its owners over xGMI
+  (``reduce`` per owner piece when num_ps < world), overlapped with the rest of backward; after
+  backward each owner runs the fused optimizer on exactly its chunks and the updated masters
+  are all-gathered (``broadcast`` from the owner when num_ps < world) bucket by bucket,
+  overlapped with the next forward (see :class:`_ColocatedPSReducer`).
 """
 from __future__ import annotations
 
@@ -22,8 +23,9 @@ import os
 import torch
 import torch.distributed as dist
 
-from .strategy import (BucketedAllReduce, MirroredStrategy, Strategy, _NullReducer,
-                       init_process_group_from_env)
+from .strategy import (BucketedAllReduce, MirroredStrategy, Strategy, _broadcast_training_state,
+                       _NullReducer, collective_cluster_changed, comm_call,
+                       force_reducer_default, init_process_group_from_env, rejoin_collective)
 
 
 class _RemotePSReducer(_NullReducer):
@@ -42,49 +44,183 @@ class _RemotePSReducer(_NullReducer):
 
 
 class _ColocatedPSReducer(BucketedAllReduce):
-    """Colocated sync PS on RCCL, overlapped with backward.
+    """Colocated sync PS on RCCL: push overlapped with backward, pull overlapped with forward.
 
-    The gradient buffer is cut into the same buckets as MirroredStrategy's all-reduce.  When a
-    bucket's last gradient lands (post-accumulate hook, during backward) each owner's piece of
-    it is ``reduce``d to that owner on RCCL's stream -- the gradient push of the reference's
-    ``SyncReplicasOptimizer`` (``templates/00_mnist_replica.py:168-191``) happens while autograd
-    is still producing earlier layers.  After backward: each owner applies the fused optimizer
-    to the slices it owns and ``broadcast``s the updated master slices (the variable pull)."""
+    The gradient buffer is cut into the same buckets as MirroredStrategy's all-reduce.
+
+    * **Sharded owners** (``num_ps == world``, an elementwise optimizer, every bucket a multiple
+      of ``world`` elements -- always true for world 1/2/4/8, the flat layout pads every variable
+      to 64 elements): rank ``r`` owns chunk ``r`` of EVERY bucket.  When a bucket's last
+      gradient lands (post-accumulate hook, during backward) ONE in-place
+      ``reduce_scatter_tensor`` sums it into the owners' chunks (the gradient push of the
+      reference's ``SyncReplicasOptimizer``, ``templates/00_mnist_replica.py:168-191``); after
+      backward each owner runs the fused optimizer on its chunks, then ONE in-place
+      ``all_gather_into_tensor`` per bucket hands the updated fp32 masters to every rank (the
+      variable pull).  Equal chunks balance the update work and the link traffic exactly.
+    * **Owner ranges** (``num_ps < world`` -- "1 PS + N workers" --, or a non-elementwise
+      optimizer such as LAMB): variable-aligned owner slices; each owner's piece of a bucket is
+      ``reduce``d to it, and the owner ``broadcast``s its updated piece.
+
+    The pulls are launched last-layer-bucket LAST (the forward needs the first layers first) and
+    are NOT waited for after the step: each bucket's wait is deferred to the first op of the next
+    forward that reads one of its variables (``ops`` variable fence + a module forward pre-hook),
+    so the gather of late layers overlaps the early layers' compute.  ``begin_step`` (before the
+    next backward) and :meth:`drain` complete whatever the forward did not touch."""
 
     applies_update = True
 
     def __init__(self, space, owners_ranges, group=None, bucket_bytes=64 << 20,
-                 first_bucket_bytes=4 << 20):
+                 first_bucket_bytes=4 << 20, sharded=None, overlap_gather=True):
         super().__init__(space, group, bucket_bytes, first_bucket_bytes)
-        self.ranges = owners_ranges          # [(owner_rank, start, end)]
-        self.rank = dist.get_rank()
-        # per bucket: [(owner, start, end)] pieces (bucket ∩ owner range)
-        self.pieces = []
-        for bs, be, _ in self.buckets:
-            self.pieces.append([(o, max(bs, s), min(be, e)) for o, s, e in owners_ranges
-                                if min(be, e) > max(bs, s)])
+        self.rank = dist.get_rank(group)
+        W = self.world
+        ok = all((e - s) % W == 0 for s, e, _ in self.buckets) and \
+            getattr(space, "elementwise", True)
+        self.sharded = ok if sharded is None else (sharded and ok)
+        if self.sharded:
+            self.ranges = []
+            self.pieces = []
+            for s, e, _ in self.buckets:
+                c = (e - s) // W
+                self.pieces.append([(o, s + o * c, s + (o + 1) * c) for o in range(W)])
+                self.ranges.append((self.rank, s + self.rank * c, s + (self.rank + 1) * c))
+        else:
+            self.ranges = owners_ranges          # [(owner_rank, start, end)]
+            # per bucket: [(owner, start, end)] pieces (bucket ∩ owner range)
+            self.pieces = []
+            for bs, be, _ in self.buckets:
+                self.pieces.append([(o, max(bs, s), min(be, e)) for o, s, e in owners_ranges
+                                    if min(be, e) > max(bs, s)])
+        self.overlap_gather = overlap_gather
+        self.gpending = [None] * len(self.buckets)
+        self._n_pending = 0
+        for b, (_, _, mem) in enumerate(self.buckets):
+            for i in mem:
+                space.order[i]._dtf_gbucket = b
+        self._pre_hook = None
+        if overlap_gather:
+            from torch.nn.modules.module import register_module_forward_pre_hook
+            self._pre_hook = register_module_forward_pre_hook(self._module_fence)
 
+    # -- push (during backward)
+    @comm_call
     def _launch(self, b):
         if self.launched[b]:
             return
         self.launched[b] = True
+        g = self.space.grad
+        if self.sharded:
+            s, e, _ = self.buckets[b]
+            _, cs, ce = self.pieces[b][self.rank]
+            self.works.append((dist.reduce_scatter_tensor(g[cs:ce], g[s:e], group=self.group,
+                                                          async_op=True), None, None))
+            return
         for o, s, e in self.pieces[b]:
-            self.works.append((dist.reduce(self.space.grad[s:e], dst=o, group=self.group,
+            self.works.append((dist.reduce(g[s:e], dst=o, group=self.group,
                                            async_op=True), None, None))
 
     def grad_scale(self):
         return 1.0 / self.world
 
+    # -- owner apply + pull
+    @comm_call
     def apply_remote(self, optimizer):
+        self.drain()
         for o, s, e in self.ranges:
             if o == self.rank and e > s:
                 optimizer._apply(self.grad_scale(), (s, e))
-        works = [dist.broadcast(self.space.master[s:e], src=o, group=self.group, async_op=True)
-                 for o, s, e in self.ranges if e > s]
+        m = self.space.master
+        # forward order: the non-decayed tail (BN / bias variables of every layer) first, then
+        # the decayed buckets from the first layers (last bucket) to the last layers (bucket 0)
+        n = len(self.buckets)
+        order = ([n - 1] + list(range(n - 2, -1, -1))) if self.space.decay_end < \
+            self.space.numel else list(range(n - 1, -1, -1))
+        for b in order:
+            if self.sharded:
+                s, e, _ = self.buckets[b]
+                _, cs, ce = self.pieces[b][self.rank]
+                works = [dist.all_gather_into_tensor(m[s:e], m[cs:ce], group=self.group,
+                                                     async_op=True)]
+            else:
+                works = [dist.broadcast(m[s:e], src=o, group=self.group, async_op=True)
+                         for o, s, e in self.pieces[b]]
+            self.gpending[b] = works
+            self._n_pending += 1
+        if self.overlap_gather:
+            from .. import ops
+            ops.set_param_fence(self._op_fence)
+        else:
+            self.drain()
+        return None
+
+    @comm_call
+    def _wait_gather(self, b):
+        works = self.gpending[b]
+        if works is None:
+            return
+        self.gpending[b] = None
         for w in works:
             w.wait()
-        self.space.refresh_shadow()
-        return None
+        sh = self.space.shadow
+        if sh is not None:
+            # through .data: the forward may already have saved bf16 weight views of this
+            # buffer for backward, and a tracked in-place copy would bump their shared version
+            # counter (autograd would then refuse the backward)
+            s, e, _ = self.buckets[b]
+            sh.data[s:e].copy_(self.space.master.data[s:e])
+        self._n_pending -= 1
+        if self._n_pending == 0:
+            from .. import ops
+            ops.set_param_fence(None)
+
+    def _op_fence(self, args, kw):
+        for a in args:
+            b = getattr(a, "_dtf_gbucket", None)
+            if b is not None and self.gpending[b] is not None:
+                self._wait_gather(b)
+        for a in kw.values():
+            b = getattr(a, "_dtf_gbucket", None)
+            if b is not None and self.gpending[b] is not None:
+                self._wait_gather(b)
+
+    def _module_fence(self, module, _inputs):
+        if self._n_pending:
+            for p in module._parameters.values():
+                b = getattr(p, "_dtf_gbucket", None)
+                if b is not None and self.gpending[b] is not None:
+                    self._wait_gather(b)
+
+    def drain(self):
+        if self._n_pending:
+            for b in range(len(self.buckets)):
+                self._wait_gather(b)
+
+    def begin_step(self):
+        self.drain()
+        super().begin_step()
+
+    @comm_call
+    def gather_state(self, bufs):
+        """Sharded owners keep each slot chunk only on its owner: all-gather every slot buffer
+        (collective; before a checkpoint of the slots)."""
+        self.drain()
+        for buf in bufs:
+            for b, (s, e, _) in enumerate(self.buckets):
+                if self.sharded:
+                    _, cs, ce = self.pieces[b][self.rank]
+                    dist.all_gather_into_tensor(buf[s:e], buf[cs:ce], group=self.group)
+                else:
+                    for o, ps, pe in self.pieces[b]:
+                        dist.broadcast(buf[ps:pe], src=o, group=self.group)
+
+    def close(self):
+        self.drain()
+        super().close()
+        if self._pre_hook is not None:
+            self._pre_hook.remove()
+            self._pre_hook = None
+        for v in self.space.order:
+            v._dtf_gbucket = None
 
 
 def balanced_ranges(space, num_owners, owner_ranks):
@@ -104,13 +240,17 @@ def balanced_ranges(space, num_owners, owner_ranks):
 class ParameterServerStrategy(Strategy):
     def __init__(self, cluster_resolver=None, server=None, num_ps=None, sync=None,
                  replicas_to_aggregate=None, variable_placement="balanced", device=None,
-                 data_plane=None, bucket_mb=64, first_bucket_mb=4):
+                 data_plane=None, bucket_mb=64, first_bucket_mb=4, force_reducer=None,
+                 sharded=None, overlap_gather=True):
         self.server = server
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.first_bucket_bytes = int(first_bucket_mb * (1 << 20))
         self.data_plane = data_plane
         self.variable_placement = variable_placement
         self.replicas_to_aggregate = replicas_to_aggregate
+        self.force_reducer = force_reducer_default() if force_reducer is None else force_reducer
+        self.sharded = sharded
+        self.overlap_gather = overlap_gather
         self._client = None
         if server is not None:
             # between-graph: this process is a worker of a PS cluster
@@ -131,7 +271,7 @@ class ParameterServerStrategy(Strategy):
             else:
                 device = torch.device("cpu")
             super().__init__(device)
-            if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            if int(os.environ.get("WORLD_SIZE", "1")) > 1 or self.force_reducer:
                 init_process_group_from_env()
             self.sync = True if sync is None else bool(sync)
             if not self.sync:
@@ -165,17 +305,31 @@ class ParameterServerStrategy(Strategy):
             self._client = PSClient(self.server.ps_ranks(), policy=self.variable_placement,
                                     space=space, data_plane=self.data_plane)
             return _RemotePSReducer(space, self._client)
-        if not dist.is_initialized() or dist.get_world_size() == 1:
+        if not self.collective:
             return _NullReducer(space)
         ranges = balanced_ranges(space, self.num_ps, list(range(self.num_ps)))
+        sharded = (self.num_ps == dist.get_world_size()) and self.sharded is not False
         return _ColocatedPSReducer(space, ranges, None, self.bucket_bytes,
-                                   self.first_bucket_bytes)
+                                   self.first_bucket_bytes, sharded=sharded,
+                                   overlap_gather=self.overlap_gather)
+
+    @property
+    def collective(self):
+        return self.mode == "colocated" and dist.is_initialized() and \
+            (dist.get_world_size() > 1 or self.force_reducer)
+
+    def sync_after_restore(self, optimizer, global_step=None):
+        _broadcast_training_state(self.collective, optimizer, global_step)
+
+    def cluster_changed(self):
+        if self.mode == "between_graph":
+            return self.server.cluster_changed()
+        return collective_cluster_changed()
 
     def broadcast_space(self, space):
-        if self.mode == "colocated":
-            if dist.is_initialized() and dist.get_world_size() > 1:
-                dist.broadcast(space.master, 0)
-                space.refresh_shadow()
+        if self.collective:
+            dist.broadcast(space.master, 0)
+            space.refresh_shadow()
 
     def register_with_ps(self, optimizer, global_step=0, restored_slots=False):
         """Chief: ship variables + optimizer config (+ the optimizer slots just restored from a
@@ -201,7 +355,15 @@ class ParameterServerStrategy(Strategy):
         PS joins too) and re-map the new shard's buffers.  The caller restores the checkpoint
         and calls :meth:`register_with_ps` again (chief re-initialises the PS; others wait)."""
         if self.mode != "between_graph":
-            raise RuntimeError("cluster recovery is for between-graph parameter servers")
+            # colocated owners: the same world re-formation as MirroredStrategy
+            epoch = rejoin_collective()
+            if optimizer is not None and optimizer.space is not None:
+                old = optimizer._reducer
+                if hasattr(old, "close"):
+                    old.close()
+                optimizer._reducer = self.make_gradient_reducer(optimizer.space)
+                self.broadcast_space(optimizer.space)     # mirrors the restarted rank's build
+            return epoch
         self.server.restart_group()
         from .ps_service import PSClient
         old = self._client

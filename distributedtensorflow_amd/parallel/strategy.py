@@ -21,6 +21,7 @@ replication — ``run_mnist_distributed.py:104-161``).  Design:
 from __future__ import annotations
 
 import contextlib
+import functools
 import os
 import threading
 
@@ -59,6 +60,38 @@ def has_strategy():
 
 # ----------------------------------------------------------------------------- gradient reducers
 
+class CommError(ConnectionError):
+    """A collective or parameter-server transfer failed -- a peer process died or the transport
+    broke.  Raised (from the transport's RuntimeError) only by this package's communication
+    calls, so MonitoredTrainingSession can recover from exactly these and nothing else."""
+
+
+def comm_call(fn):
+    """Decorator for communication entry points: a transport RuntimeError (gloo's "Connection
+    closed by peer", torch.distributed's DistError family) becomes :class:`CommError`; device
+    faults (``torch.AcceleratorError``) stay what they are -- they are not recoverable by
+    re-forming the cluster."""
+    @functools.wraps(fn)
+    def wrapper(*args, **kw):
+        try:
+            return fn(*args, **kw)
+        except ConnectionError:
+            raise
+        except RuntimeError as e:
+            if isinstance(e, getattr(torch, "AcceleratorError", ())):
+                raise
+            raise CommError(f"{type(e).__name__}: {e}") from e
+    return wrapper
+
+
+def force_reducer_default():
+    """``DTF_FORCE_REDUCER=1``: build the communicating gradient reducer (and the process group)
+    even when the world has ONE rank, so a ``torchrun --nproc-per-node 1`` run on the ``nccl``
+    backend executes every hook, RCCL collective and ``finish()`` of the N > 1 path with the
+    native ops' direct gradient writes (tests/test_forced_reducer_gpu.py)."""
+    return os.environ.get("DTF_FORCE_REDUCER", "0") == "1"
+
+
 class _NullReducer:
     def __init__(self, space=None):
         self.space = space
@@ -68,6 +101,13 @@ class _NullReducer:
 
     def finish(self):
         pass
+
+    def drain(self):
+        """Complete any communication still in flight that writes the variables (the colocated
+        parameter server's overlapped variable gather); a no-op for replicated strategies."""
+
+    def gather_state(self, bufs):
+        """Make flat optimizer-state buffers whole on every rank (sharded owners only)."""
 
     def grad_scale(self):
         return 1.0
@@ -184,6 +224,7 @@ class BucketedAllReduce:
                 self._launch(b)
         return hook
 
+    @comm_call
     def _launch(self, b):
         if self.launched[b]:
             return
@@ -235,6 +276,7 @@ class BucketedAllReduce:
             import time
             st._host_s += time.perf_counter() - t0
 
+    @comm_call
     def finish(self):
         st = self.stats
         early = sum(self.launched)
@@ -260,6 +302,12 @@ class BucketedAllReduce:
 
     def grad_scale(self):
         return 1.0 / self.world if self.average else 1.0
+
+    def drain(self):
+        pass
+
+    def gather_state(self, bufs):
+        pass
 
 
 # ----------------------------------------------------------------------------- strategies
@@ -327,6 +375,16 @@ class Strategy:
     def barrier(self):
         pass
 
+    @property
+    def collective(self) -> bool:
+        """True when the replicas are one synchronous collective world (every rank must enter
+        checkpoint/state synchronisation together)."""
+        return False
+
+    def sync_after_restore(self, optimizer, global_step=None):
+        """After the chief restored a checkpoint: make every replica hold the chief's variables,
+        optimizer slots, update count and global step (collective strategies only)."""
+
 
 class _DefaultStrategy(Strategy):
     def __init__(self):
@@ -356,9 +414,37 @@ def _parse_device(d):
     return torch.device(d)
 
 
+def _broadcast_training_state(active, optimizer, global_step=None, src=0):
+    """Rank ``src``'s master weights (+ compute shadow), optimizer slots, update count and global
+    step to every rank: the state a restored chief hands to the other replicas."""
+    if not active or optimizer is None or optimizer.space is None:
+        return
+    optimizer.synchronize_variables()
+    sp = optimizer.space
+    dist.broadcast(sp.master, src)
+    for t in optimizer.state_tensors():
+        dist.broadcast(t, src)
+    meta = torch.tensor([optimizer.iterations,
+                         global_step.value() if global_step is not None else 0],
+                        dtype=torch.int64, device=sp.device)
+    dist.broadcast(meta, src)
+    optimizer.iterations = int(meta[0])
+    if global_step is not None and hasattr(global_step, "assign"):
+        global_step.assign(int(meta[1]))
+    sp.refresh_shadow()
+
+
+_collective_watcher = None
+
+
 def init_process_group_from_env(backend=None, timeout_s=600):
-    """Initialise torch.distributed from torchrun-style env (RANK/WORLD_SIZE/MASTER_*)."""
+    """Initialise torch.distributed from torchrun-style env (RANK/WORLD_SIZE/MASTER_*).
+
+    Under this package's launcher (``DTF_STORE_ADDR``: the launcher hosts the rendezvous store,
+    cluster/rendezvous.py) the group is created for the current cluster EPOCH, and an epoch
+    watcher tells the training session when a failed rank was restarted."""
     import datetime
+    global _collective_watcher
     if dist.is_initialized():
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -373,8 +459,37 @@ def init_process_group_from_env(backend=None, timeout_s=600):
     kw = {}
     if backend == "nccl":
         kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    from ..cluster import rendezvous
+    if rendezvous.store_address() is not None:
+        store = rendezvous.connect(timeout_s)
+        epoch = rendezvous.current_epoch(store)
+        rendezvous.init_group(backend, rank, world, store, epoch, timeout_s, **kw)
+        if _collective_watcher is not None:
+            _collective_watcher.stop()
+        _collective_watcher = rendezvous.EpochWatcher(epoch).start()
+        _collective_watcher.backend, _collective_watcher.timeout_s = backend, timeout_s
+        _collective_watcher.store = store
+        return
     dist.init_process_group(backend, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
+
+
+def collective_cluster_changed():
+    return _collective_watcher is not None and _collective_watcher.changed
+
+
+def rejoin_collective(timeout_s=120.0):
+    """A rank of the collective world died: leave the broken group, wait until the launcher has
+    restarted it (epoch bump; bounded) and join the new epoch's group with every other rank."""
+    from ..cluster import rendezvous
+    w = _collective_watcher
+    if w is None:
+        raise RuntimeError("collective recovery needs the launcher's rendezvous store "
+                           "(DTF_STORE_ADDR)")
+    rendezvous.leave_group()
+    rendezvous.wait_for_epoch_after(w.store, w.epoch, timeout_s)
+    init_process_group_from_env(w.backend, w.timeout_s)
+    return _collective_watcher.epoch
 
 
 class MirroredStrategy(Strategy):
@@ -386,7 +501,7 @@ class MirroredStrategy(Strategy):
     """
 
     def __init__(self, devices=None, cross_device_ops=None, bucket_mb=64, first_bucket_mb=4,
-                 compress_bf16=False, backend=None, overlap=True):
+                 compress_bf16=False, backend=None, overlap=True, force_reducer=None):
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
@@ -398,9 +513,10 @@ class MirroredStrategy(Strategy):
         self.first_bucket_bytes = int(first_bucket_mb * (1 << 20))
         self.compress_bf16 = compress_bf16
         self.overlap = overlap
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        self.force_reducer = force_reducer_default() if force_reducer is None else force_reducer
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 or self.force_reducer:
             init_process_group_from_env(backend)
-        self._dist = dist.is_initialized() and dist.get_world_size() > 1
+        self._dist = dist.is_initialized() and (dist.get_world_size() > 1 or self.force_reducer)
 
     @property
     def num_replicas_in_sync(self):
@@ -425,6 +541,32 @@ class MirroredStrategy(Strategy):
         if self._dist:
             for t in tensors:
                 dist.broadcast(t, src)
+
+    @property
+    def collective(self):
+        return self._dist
+
+    def sync_after_restore(self, optimizer, global_step=None):
+        _broadcast_training_state(self._dist, optimizer, global_step)
+
+    def cluster_changed(self):
+        return collective_cluster_changed()
+
+    def recover_cluster(self, optimizer=None):
+        """A replica died and the launcher restarted it: re-form the world in the new epoch and
+        rebuild the gradient reducer on the new process group (the caller restores the latest
+        checkpoint on the chief and calls :meth:`sync_after_restore`)."""
+        epoch = rejoin_collective()
+        self._dist = dist.is_initialized() and (dist.get_world_size() > 1 or self.force_reducer)
+        if optimizer is not None and optimizer.space is not None:
+            old = optimizer._reducer
+            if hasattr(old, "close"):
+                old.close()
+            optimizer._reducer = self.make_gradient_reducer(optimizer.space)
+            # the restarted replica's Optimizer.build broadcast, mirrored (the collective
+            # sequence must be the same on every rank)
+            self.broadcast_space(optimizer.space)
+        return epoch
 
     def reduce(self, op, value, axis=None):
         value = super().reduce(op, value, axis)

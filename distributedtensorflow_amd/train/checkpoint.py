@@ -195,6 +195,8 @@ class Saver:
             prefix = save_path
         d = os.path.dirname(os.path.abspath(prefix))
         os.makedirs(d, exist_ok=True)
+        if self.optimizer is not None and getattr(self.optimizer, "space", None) is not None:
+            self.optimizer.synchronize_variables()    # overlapped parameter-server gathers
         tensors = {}
         for name, (t, layout) in self._vars().items():
             if values is not None and name in values:

@@ -127,7 +127,8 @@ class CheckpointSaverHook(SessionRunHook):
         if saver is None:
             return
         p = session.save_checkpoint(os.path.join(self.dir, self.basename), step, saver)
-        self.saved.append(p)
+        if p is not None:          # None: a non-chief replica took part in a collective save
+            self.saved.append(p)
 
 
 class StepCounterHook(SessionRunHook):

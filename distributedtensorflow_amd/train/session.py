@@ -41,13 +41,23 @@ class GPUOptions:
         self.allow_growth = bool(allow_growth)
         self.visible_device_list = str(visible_device_list or "")
 
-    def apply(self):
+    def apply(self, placed_on=None):
+        """``placed_on``: the device the session's variables already live on.  Switching the
+        current device away from it would send the native kernels to one device's stream with
+        the other device's pointers, so a ``visible_device_list`` naming a different device is
+        refused instead of applied."""
         if not torch.cuda.is_available():
             return None
         dev = torch.cuda.current_device()
         if self.visible_device_list:
             ids = [int(t) for t in self.visible_device_list.split(",") if t.strip()]
             dev = ids[0]
+            if placed_on is not None and placed_on.type == "cuda" and \
+                    (placed_on.index if placed_on.index is not None else 0) != dev:
+                raise ValueError(f"GPUOptions(visible_device_list={self.visible_device_list!r}) "
+                                 f"selects cuda:{dev}, but the variables were already created "
+                                 f"on {placed_on}; pick the device before building the model "
+                                 f"(or set HIP_VISIBLE_DEVICES)")
             torch.cuda.set_device(dev)
         if 0.0 < self.per_process_gpu_memory_fraction <= 1.0:
             torch.cuda.set_per_process_memory_fraction(self.per_process_gpu_memory_fraction, dev)
@@ -119,7 +129,7 @@ class ConfigProto:
             raise ValueError(f"device_filters {self.device_filters} hide every /job:ps task, but "
                              f"the variables live on {num_ps} parameter server(s)")
 
-    def apply(self):
+    def apply(self, placed_on=None):
         # clamp to the CPUs this process may use (utils.cpu.usable_cpus): the reference passes
         # os.cpu_count(), which on a shared many-core GPU host is far above the CPU quota
         from ..utils.cpu import usable_cpus
@@ -132,7 +142,7 @@ class ConfigProto:
             except RuntimeError:
                 pass   # can only be set once per process
         if self.gpu_options is not None:
-            self.gpu_options.apply()
+            self.gpu_options.apply(placed_on)
 
 
 def log_placement(model=None, optimizer=None, strategy=None, out=None):
@@ -191,6 +201,15 @@ class _Session:
 
     def save_checkpoint(self, path, step, saver=None):
         saver = saver or self.saver
+        opt = self.scaffold.optimizer
+        if opt is not None and opt.space is not None:
+            opt.synchronize_variables()
+            if getattr(self.strategy, "collective", False):
+                # collective: every rank is here (step-triggered saver hook on every rank); a
+                # sharded parameter server completes its slot shards on every rank first
+                opt.gather_state()
+                if not self.is_chief:
+                    return None
         values = None
         client = getattr(self.strategy, "ps_client", None)
         if client is not None and client.params is not None:
@@ -242,22 +261,46 @@ def _execute(fetches, feed_dict, session):
 
 
 def _recoverable(exc):
-    """Errors TF's _RecoverableSession would recreate the session for: injected faults, a
-    vanished peer (ConnectionError from the PS data plane, torch.distributed's DistError
-    family), and gloo transport failures surfacing as RuntimeError."""
+    """Errors TF's _RecoverableSession would recreate the session for -- matched by TYPE, never
+    by message text: injected faults (in-process checkpoint rollback), and communication
+    failures (a peer died: this package's CommError / ClusterChanged, both ConnectionErrors,
+    torch.distributed's DistError family, a data-plane TimeoutError).  Communication failures
+    are recoverable only when a launcher restarts failed tasks (``DTF_MAX_RESTARTS`` with the
+    launcher-hosted store): without one, waiting for the cluster to re-form would only hang."""
     import torch.distributed as dist
-    if isinstance(exc, (InjectedFault, ConnectionError, TimeoutError)):
+
+    from ..cluster import rendezvous
+    if isinstance(exc, InjectedFault):
         return True
-    if isinstance(exc, getattr(dist, "DistError", ())):
-        return True
-    if isinstance(exc, RuntimeError):
-        msg = str(exc).lower()
-        return any(k in msg for k in ("gloo", "connection", "peer", "broken pipe",
-                                      "parameter server"))
+    if isinstance(exc, (ConnectionError, TimeoutError, getattr(dist, "DistError", ()))):
+        return rendezvous.recovery_enabled()
     return False
 
 
+def _maybe_hard_fault(strategy, step):
+    """``DTF_FAULT_SIGKILL=<job>:<index>@<step>`` (tests, SURVEY §5.3 fault injection): this task
+    dies by SIGKILL -- no cleanup, like a preempted host -- when the global step reaches
+    ``step``, in its first incarnation only (``DTF_RESTART_COUNT`` = 0).  ``job`` is ``worker`` /
+    ``ps`` for between-graph clusters, ``rank`` for collective worlds."""
+    spec = os.environ.get("DTF_FAULT_SIGKILL", "")
+    if not spec or int(os.environ.get("DTF_RESTART_COUNT", "0") or 0):
+        return
+    who, _, at = spec.partition("@")
+    job, _, idx = who.partition(":")
+    server = getattr(strategy, "server", None)
+    if server is not None:
+        me = (server.job_name, server.task_index)
+    else:
+        me = ("rank", int(os.environ.get("RANK", "0")))
+    if me == (job, int(idx)) and step >= int(at):
+        import signal
+        print(f"[dtf] fault injection: SIGKILL {job}:{idx} at global step {step}", flush=True)
+        os.kill(os.getpid(), signal.SIGKILL)
+
+
 class MonitoredTrainingSession:
+    # the exception types _recoverable() accepts (communication ones only under a launcher
+    # that restarts failed tasks)
     RECOVERABLE = (InjectedFault, ConnectionError, TimeoutError)
 
     def __init__(self, master="", is_chief=True, checkpoint_dir=None, scaffold=None, hooks=None,
@@ -276,16 +319,23 @@ class MonitoredTrainingSession:
         self.max_recovery_attempts = max_recovery_attempts
         self.hooks = list(hooks or [])
         self._writer = None
+        collective = bool(getattr(self.strategy, "collective", False))
+        if checkpoint_dir and (save_checkpoint_secs or save_checkpoint_steps) and \
+                (is_chief or collective):
+            if collective and not save_checkpoint_steps:
+                # every replica must enter the (collective) save at the same step: a wall-clock
+                # trigger would fire at different steps on different ranks
+                save_checkpoint_steps = max(1, int(os.environ.get("DTF_COLLECTIVE_SAVE_STEPS",
+                                                                  "1000")))
+            self.hooks.append(CheckpointSaverHook(checkpoint_dir, save_checkpoint_secs
+                                                  if not save_checkpoint_steps else None,
+                                                  save_checkpoint_steps))
         if is_chief:
             self.hooks += list(chief_only_hooks or [])
             sdir = summary_dir or checkpoint_dir
             if sdir:
                 from ..summary.events import EventFileWriter
                 self._writer = EventFileWriter(sdir)
-            if checkpoint_dir and (save_checkpoint_secs or save_checkpoint_steps):
-                self.hooks.append(CheckpointSaverHook(checkpoint_dir, save_checkpoint_secs
-                                                      if not save_checkpoint_steps else None,
-                                                      save_checkpoint_steps))
             if sdir and log_step_count_steps:
                 self.hooks.append(StepCounterHook(every_n_steps=log_step_count_steps))
             if sdir and (save_summaries_steps or save_summaries_secs):
@@ -297,9 +347,18 @@ class MonitoredTrainingSession:
         self._create()
 
     # -- creation / recovery
+    def _placed_on(self):
+        opt = self.scaffold.optimizer
+        if opt is not None and getattr(opt, "space", None) is not None:
+            return opt.space.device
+        if self.scaffold.model is not None:
+            p = next(iter(self.scaffold.model.parameters()), None)
+            return p.device if p is not None else None
+        return None
+
     def _create(self):
         if self.config is not None and hasattr(self.config, "apply"):
-            self.config.apply()
+            self.config.apply(self._placed_on())
         sc = self.scaffold
         if self.config is not None and hasattr(self.config, "check_placement"):
             self.config.check_placement(self.strategy)
@@ -311,6 +370,9 @@ class MonitoredTrainingSession:
                 restored = True
         if sc.init_fn is not None and not restored:
             sc.init_fn(self)
+        if getattr(self.strategy, "collective", False) and sc.optimizer is not None:
+            # synchronous replicas: everyone continues from the chief's (restored) state
+            self.strategy.sync_after_restore(sc.optimizer, sc.global_step)
         if sc.optimizer is not None and hasattr(self.strategy, "register_with_ps"):
             self.strategy.register_with_ps(sc.optimizer, sc.global_step.value())
             client = getattr(self.strategy, "ps_client", None)
@@ -329,6 +391,26 @@ class MonitoredTrainingSession:
         self.recoveries += 1
         strat = self.strategy
         sc = self.scaffold
+        if exc is not None and not isinstance(exc, InjectedFault) and \
+                getattr(strat, "collective", False) and hasattr(strat, "recover_cluster"):
+            # a replica of the synchronous world died and was restarted: re-form the world in
+            # the new epoch, rebuild the reducer, the chief restores the latest checkpoint and
+            # every replica continues from the chief's state (the restarted one does the same
+            # from its MonitoredTrainingSession creation)
+            print(f"[dtf] recovering from {type(exc).__name__}: {exc}", flush=True)
+            epoch = strat.recover_cluster(sc.optimizer)
+            ckpt = latest_checkpoint(self.checkpoint_dir) if self.checkpoint_dir else None
+            if self.is_chief and ckpt and sc.saver is not None:
+                sc.saver.restore(None, ckpt, strict=False)
+            strat.sync_after_restore(sc.optimizer, sc.global_step)
+            # the restarted replica runs after_create_session (its initial checkpoint save is a
+            # collective under a sharded PS): the survivors mirror it
+            for h in self.hooks:
+                h.after_create_session(self._session, None)
+            print(f"[dtf] recovered: generation {epoch}, restored="
+                  f"{ckpt if self.is_chief else 'from chief'}, global step "
+                  f"{sc.global_step.value()}", flush=True)
+            return
         if exc is not None and not isinstance(exc, InjectedFault) and \
                 getattr(strat, "mode", None) == "between_graph" and \
                 hasattr(strat, "recover_cluster") and sc.optimizer is not None:
@@ -375,6 +457,11 @@ class MonitoredTrainingSession:
                 self._should_stop = True
                 return None
             try:
+                changed = getattr(self.strategy, "cluster_changed", None)
+                if changed is not None and changed():
+                    from ..cluster.rendezvous import ClusterChanged
+                    raise ClusterChanged("a task of the cluster was restarted")
+                _maybe_hard_fault(self.strategy, self.global_step.value())
                 results = _execute(fetches, feed_dict, self._session)
                 self._session.last_results = results
                 rv = SessionRunValues(results)

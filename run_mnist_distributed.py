@@ -58,6 +58,7 @@ def main():
             torch.cuda.set_device(torch.device(ps_device))
         print("Started Parameter Server ...", flush=True)
         stats = server.join()
+        Server.exit_for_rejoin(stats)       # a peer died: restart in the cluster's new epoch
         print("Close Parameter Server ...", stats, flush=True)
         if not stats.get("interrupted"):
             server.shutdown()
@@ -171,9 +172,11 @@ def parse(argv=None):
                         help="chief checkpoints every N global steps (default: every 600 s)")
     parser.add_argument("--sync_replicas", action="store_true")
     parser.add_argument("--device", choices=("auto", "cpu", "gpu"), default="auto")
-    parser.add_argument("--dtype", choices=("auto", "bf16", "fp32"), default="auto",
-                        help="compute dtype: fp32 = the reference's precision (f32 MFMA kernels); "
-                             "auto = bf16 on GPUs, fp32 on CPUs")
+    parser.add_argument("--dtype", choices=("auto", "bf16", "fp32"), default="fp32",
+                        help="compute dtype: fp32 (default) = the reference's precision "
+                             "(dataset.py:93-95, tf.layers' float32; f32 MFMA kernels on GPUs); "
+                             "bf16 = opt-in bf16 compute with fp32 masters; auto = bf16 on GPUs, "
+                             "fp32 on CPUs")
     parser.add_argument("--ps_device", choices=("auto", "cpu", "gpu"), default="auto",
                         help="where a ps task keeps its variable shard (auto: its GPU's HBM)")
     parser.add_argument("--data_plane", choices=("auto", "ipc", "shm", "gloo"), default=None,

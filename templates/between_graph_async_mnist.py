@@ -31,6 +31,7 @@ def main():
     server = Server(cluster, job_name=FLAGS.job_name, task_index=FLAGS.task_index)
     if FLAGS.job_name == "ps":
         stats = server.join()
+        server.exit_for_rejoin(stats)      # a peer died and was restarted: new cluster epoch
         if not stats.get("interrupted"):
             server.shutdown()
         return

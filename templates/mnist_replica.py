@@ -52,6 +52,7 @@ def main():
         server = Server(cluster, job_name=FLAGS.job_name, task_index=FLAGS.task_index)
     if FLAGS.job_name == "ps":
         stats = server.join()
+        server.exit_for_rejoin(stats)      # a peer died and was restarted: new cluster epoch
         if not stats.get("interrupted"):
             server.shutdown()
         return
@@ -66,6 +67,7 @@ def main():
         global_step = dtf.train.get_or_create_global_step()
         model = dtf.models.MnistMLP(FLAGS.hidden_units)
         opt = dtf.train.AdamOptimizer(FLAGS.learning_rate)
+        opt.shadow_dtype = None      # fp32 end to end, like the reference's MLP
         if FLAGS.sync_replicas:
             replicas = FLAGS.replicas_to_aggregate or num_workers
             opt = dtf.train.SyncReplicasOptimizer(opt, replicas_to_aggregate=replicas,

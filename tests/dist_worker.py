@@ -22,7 +22,10 @@ def global_batch(step, n=16):
 
 
 def make_optimizer(name):
-    from distributedtensorflow_amd.optimizers import AdamOptimizer, MomentumOptimizer
+    from distributedtensorflow_amd.optimizers import (AdamOptimizer, LAMBOptimizer,
+                                                      MomentumOptimizer)
+    if name == "lamb":
+        return LAMBOptimizer(1e-3)
     return AdamOptimizer(1e-3) if name == "adam" else MomentumOptimizer(0.05, 0.9)
 
 
@@ -60,6 +63,9 @@ def _direct_dense(x, w, b=None, relu=False):
 
 
 def main():
+    import faulthandler
+    import signal
+    faulthandler.register(signal.SIGUSR1)      # stack dump of a hung rank (tests' diagnostics)
     kind, out = sys.argv[1], sys.argv[2]
     kw = dict(a.split("=", 1) for a in sys.argv[3:])
     steps = int(kw.get("steps", 3))
@@ -70,6 +76,8 @@ def main():
                                                     ParameterServerStrategy)
     if kind == "heartbeat":
         return heartbeat_probe(out)
+    if kind == "mirrored_recovery":
+        return mirrored_recovery(out, kw, steps)
     if kind == "resnet_gpu":
         return resnet_gpu_grads(out)
     if kind == "mirrored":
@@ -79,15 +87,18 @@ def main():
                                  overlap=kw.get("overlap", "1") == "1")
     elif kind == "multiworker":
         strat = MultiWorkerMirroredStrategy()
-    elif kind == "colocated_ps":
+    elif kind in ("colocated_ps", "colocated_ckpt"):
         strat = ParameterServerStrategy(num_ps=int(kw.get("num_ps", 1)),
                                         bucket_mb=float(kw.get("bucket_mb", 64)),
-                                        first_bucket_mb=float(kw.get("bucket_mb", 4)))
+                                        first_bucket_mb=float(kw.get("bucket_mb", 4)),
+                                        overlap_gather=kw.get("overlap", "1") == "1")
     else:
         raise SystemExit(f"unknown strategy {kind}")
     rank, world = strat.replica_id, strat.num_replicas_in_sync
     if kw.get("direct", "0") == "1":
         ops.dense = _direct_dense
+    if kind == "colocated_ckpt":
+        return checkpointed_run(strat, out, kw, steps)
     torch.manual_seed(17 + 101 * rank)
     with strat.scope():
         model = MnistCNN()
@@ -108,7 +119,105 @@ def main():
         fps = dtf.distribute.check_replicas_consistent(opt)      # raises if replicas diverged
     torch.save({"state": {k: v.detach().clone() for k, v in model.state_dict().items()},
                 "global_step": gstep.value(), "world": world, "mean_loss": mean_loss,
-                "fingerprints": fps, "early_launches": early},
+                "fingerprints": fps, "early_launches": early,
+                "sharded": getattr(opt._reducer, "sharded", None),
+                "reducer": type(opt._reducer).__name__},
+               os.path.join(out, f"rank{rank}.pt"))
+    strat.barrier()
+
+
+def checkpointed_run(strat, out, kw, steps):
+    """MonitoredTrainingSession on every rank of a colocated (sharded) parameter server with a
+    step-triggered checkpoint: the save is collective (slot shards gathered from their owners),
+    the chief writes it.  A second session then restores it on the chief and must hand the
+    restored state to every rank."""
+    import distributedtensorflow_amd as dtf
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.models import MnistCNN
+    rank, world = strat.replica_id, strat.num_replicas_in_sync
+    torch.manual_seed(17 + 101 * rank)
+    ckpt = os.path.join(out, "ckpt")
+    per = 16 // world
+    with strat.scope():
+        model = MnistCNN()
+        opt = make_optimizer(kw.get("opt", "adam"))
+        gstep = dtf.train.get_or_create_global_step()
+        opt.build(list(model.parameters()))
+
+        def step_fn(step):
+            x, y = global_batch(step)
+            x, y = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
+            opt.minimize(ops.sparse_softmax_cross_entropy(model(x), y), global_step=gstep)
+
+        with dtf.train.MonitoredTrainingSession(
+                is_chief=rank == 0, checkpoint_dir=ckpt, save_checkpoint_steps=steps,
+                save_summaries_steps=None, log_step_count_steps=None, model=model,
+                optimizer=opt, global_step=gstep, strategy=strat) as sess:
+            while gstep.value() < steps:
+                s = gstep.value()
+                sess.run(lambda: step_fn(s))
+        opt.synchronize_variables()
+        # a fresh session on perturbed variables: the chief restores, everyone must follow
+        with torch.no_grad():
+            opt.space.master.add_(1.0 + rank)
+            opt.space.refresh_shadow()
+            for t in opt.state_tensors():
+                t.mul_(3.0 + rank)
+        opt.iterations = 99 + rank
+        gstep.assign(7 * (rank + 1))
+        sess2 = dtf.train.MonitoredTrainingSession(
+            is_chief=rank == 0, checkpoint_dir=ckpt, save_checkpoint_steps=None,
+            save_checkpoint_secs=None, save_summaries_steps=None, log_step_count_steps=None,
+            model=model, optimizer=opt, global_step=gstep, strategy=strat)
+        restored = {"master": opt.space.master.detach().clone(),
+                    "slots": [t.detach().clone() for t in opt.state_tensors()],
+                    "iterations": opt.iterations, "global_step": gstep.value()}
+        sess2.close()
+    torch.save({"restored": restored, "sharded": getattr(opt._reducer, "sharded", None)},
+               os.path.join(out, f"rank{rank}.pt"))
+    strat.barrier()
+
+
+def mirrored_recovery(out, kw, steps):
+    """A rank of a MirroredStrategy world under launch_collective, trained with a
+    MonitoredTrainingSession that checkpoints every ``save`` steps.  With
+    DTF_FAULT_SIGKILL=rank:1@k rank 1 dies mid-run; the launcher restarts it, rank 0 re-forms the
+    world in the new epoch, the chief's latest checkpoint is restored and broadcast, and both
+    reach ``steps`` with identical variables."""
+    import distributedtensorflow_amd as dtf
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.models import MnistCNN
+    from distributedtensorflow_amd.parallel import MirroredStrategy, ParameterServerStrategy
+    strat = (ParameterServerStrategy(num_ps=2) if kw.get("strategy") == "ps"
+             else MirroredStrategy())
+    rank, world = strat.replica_id, strat.num_replicas_in_sync
+    torch.manual_seed(17 + 101 * rank)
+    per = 16 // world
+    with strat.scope():
+        model = MnistCNN()
+        opt = make_optimizer(kw.get("opt", "momentum"))
+        gstep = dtf.train.get_or_create_global_step()
+        opt.build(list(model.parameters()))
+
+        def step_fn(step):
+            x, y = global_batch(step)
+            x, y = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
+            opt.minimize(ops.sparse_softmax_cross_entropy(model(x), y), global_step=gstep)
+
+        sess = dtf.train.MonitoredTrainingSession(
+            is_chief=rank == 0, checkpoint_dir=os.path.join(out, "ckpt"),
+            save_checkpoint_steps=int(kw.get("save", 3)), save_summaries_steps=None,
+            log_step_count_steps=None, model=model, optimizer=opt, global_step=gstep,
+            strategy=strat)
+        with sess:
+            while gstep.value() < steps:
+                s = gstep.value()
+                sess.run(lambda: step_fn(s))
+                print(f"rank {rank} step {gstep.value()}", flush=True)
+        fps = dtf.distribute.check_replicas_consistent(opt)
+    torch.save({"state": {k: v.detach().clone() for k, v in model.state_dict().items()},
+                "global_step": gstep.value(), "recoveries": sess.recoveries,
+                "fingerprints": fps, "restart": int(os.environ.get("DTF_RESTART_COUNT", "0"))},
                os.path.join(out, f"rank{rank}.pt"))
     strat.barrier()
 

@@ -81,6 +81,16 @@ def test_bench_two_ranks_colocated_ps(tmp_path):
     assert rec["value"] > 0
 
 
+def test_bench_two_ranks_sharded_ps(tmp_path):
+    """num_ps == world: reduce-scatter push / owner apply / overlapped all-gather pull."""
+    rec = _run_two_ranks(tmp_path, ["--strategy", "ps", "--num-ps", "2"])
+    cfg = rec["config"]
+    assert cfg["parallelism"] == "ps2+dp2"
+    assert cfg["comm"]["sharded_owners"] is True
+    assert cfg["comm"]["buckets"] >= 2 and cfg["comm"]["early_launches"] >= 3
+    assert rec["value"] > 0 and cfg["final_loss"] == cfg["final_loss"]
+
+
 def test_bench_two_ranks_bucket_autotune(tmp_path):
     """--bucket-mb auto: every candidate re-buckets the live reducer (hooks detached and
     re-registered), the rank-max timing picks one, and the timed steps run on it."""

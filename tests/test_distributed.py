@@ -50,7 +50,7 @@ def _launch(kind, world, tmp_path, *args, extra_env=None, timeout=240):
     return [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
 
 
-def _single_process(opt="momentum", steps=3):
+def _single_process(opt="momentum", steps=3, with_opt=False):
     from distributedtensorflow_amd import ops
     from distributedtensorflow_amd.models import MnistCNN
     from distributedtensorflow_amd.parallel import OneDeviceStrategy
@@ -65,7 +65,8 @@ def _single_process(opt="momentum", steps=3):
         for step in range(steps):
             x, y = dist_worker.global_batch(step)
             o.minimize(ops.sparse_softmax_cross_entropy(model(x), y))
-    return {k: v.detach().clone() for k, v in model.state_dict().items()}
+    state = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    return (state, o) if with_opt else state
 
 
 def _assert_replicas(results, ref, atol=2e-6, steps=3):
@@ -128,6 +129,71 @@ def test_multiworker_from_tf_config(tmp_path):
 def test_colocated_parameter_server_sync(tmp_path, num_ps):
     res = _launch("colocated_ps", 2, tmp_path, f"num_ps={num_ps}", "opt=adam")
     _assert_replicas(res, _single_process("adam"), atol=2e-5)   # Adam normalises fp noise
+
+
+def test_colocated_ps_sharded_owners_reduce_scatter(tmp_path):
+    """num_ps == world with an elementwise optimizer: every rank owns an equal chunk of every
+    bucket (reduce-scatter push from the backward hooks, all-gather pull overlapped with the
+    next forward); many buckets + the direct flat-buffer gradient writes of the native ops."""
+    res = _launch("colocated_ps", 2, tmp_path, "num_ps=2", "bucket_mb=0.05", "direct=1",
+                  "opt=momentum")
+    assert all(r["sharded"] is True for r in res)
+    _assert_replicas(res, _single_process("momentum"))
+    off = _launch("colocated_ps", 2, tmp_path, "num_ps=2", "overlap=0", "opt=momentum")
+    _assert_replicas(off, _single_process("momentum"))
+
+
+def test_colocated_ps_lamb_keeps_variable_aligned_owners(tmp_path):
+    """LAMB's per-tensor trust ratio cannot be split between owners: owner ranges stay on
+    variable boundaries (reduce / broadcast path) and still match one process."""
+    res = _launch("colocated_ps", 2, tmp_path, "num_ps=2", "opt=lamb")
+    assert all(r["sharded"] is False for r in res)
+    _assert_replicas(res, _single_process("lamb"), atol=2e-5)
+
+
+@pytest.mark.parametrize("kind,args", [("mirrored", ()), ("colocated_ps", ("num_ps=1",)),
+                                       ("colocated_ps", ("bucket_mb=0.05", "direct=1"))],
+                         ids=["mirrored", "ps", "ps_many_buckets"])
+def test_forced_reducer_one_rank_is_bit_identical(tmp_path, kind, args):
+    """DTF_FORCE_REDUCER=1: a one-rank world still builds the process group and the
+    communicating reducer (hooks, collectives, finish, owner apply, overlapped gathers); the
+    result must equal the plain single-process run bit for bit."""
+    res = _launch(kind, 1, tmp_path, *args, extra_env=lambda r: {"DTF_FORCE_REDUCER": "1"})
+    assert res[0]["reducer"] in ("BucketedAllReduce", "_ColocatedPSReducer")
+    assert all(e >= 1 for e, _ in res[0]["early_launches"])
+    plain = _launch(kind, 1, tmp_path, *args, extra_env=lambda r: {"DTF_FORCE_REDUCER": "0"})
+    assert plain[0]["reducer"] == "_NullReducer"
+    for k, v in plain[0]["state"].items():
+        assert torch.equal(res[0]["state"][k], v), k
+
+
+def test_colocated_ps_collective_checkpoint_and_restore(tmp_path):
+    """Sharded parameter server + MonitoredTrainingSession on both ranks: the step-triggered
+    save is collective (slot chunks gathered from their owners), so the chief's checkpoint holds
+    the SAME Adam slots as a one-process run; a new session restores on the chief and every
+    rank receives the restored variables, slots, update count and global step."""
+    res = _launch("colocated_ckpt", 2, tmp_path, "num_ps=2", "opt=adam")
+    assert all(r["sharded"] is True for r in res)
+    ref_state, ref_opt = _single_process("adam", with_opt=True)
+    from distributedtensorflow_amd.train.checkpoint import latest_checkpoint, load_variable
+    last = latest_checkpoint(str(tmp_path / "ckpt"))
+    assert last.endswith("model.ckpt-3"), last
+    import numpy as np
+    for name, t in ref_opt.slot_variables().items():
+        got = load_variable(last, name)
+        want = t.detach()
+        if getattr(next(p for p in ref_opt.space.order
+                        if name.startswith(p._dtf_name + "/")), "_dtf_layout", None) == "KRSC":
+            want = want.permute(1, 2, 3, 0)
+        elif want.dim() == 2:
+            want = want.t()
+        np.testing.assert_allclose(got, want.numpy(), atol=2e-6, rtol=1e-4, err_msg=name)
+    r0, r1 = res[0]["restored"], res[1]["restored"]
+    assert torch.equal(r0["master"], r1["master"])
+    for a, b in zip(r0["slots"], r1["slots"]):
+        assert torch.equal(a, b)
+    assert r0["iterations"] == r1["iterations"] == 3
+    assert r0["global_step"] == r1["global_step"] == 3
 
 
 # ----------------------------------------------------------------------------- between-graph PS
@@ -204,6 +270,69 @@ def test_allreduce_bandwidth_tool_gloo(tmp_path):
     rows = [json.loads(line) for line in open(out)]
     assert [x["size_mb"] for x in rows[:-1]] == [0.25, 0.5]
     assert all(x["busbw_GBps"] > 0 for x in rows[:-1]) and rows[-1]["bucketed_allreduce_ms"] > 0
+
+
+@pytest.mark.parametrize("victim", ["worker:1", "worker:0"], ids=["worker", "chief"])
+def test_any_task_killed_is_restarted_and_training_resumes(tmp_path, mnist_dir, victim):
+    """Recovery from ANY task's death (reference run_mnist_distributed.py:128-132,
+    146 and the Supervisor's retrying non-chiefs, templates/00_mnist_replica.py:196-211): the
+    launcher hosts the rendezvous store, so a non-chief worker OR the chief can die (SIGKILL at
+    global step 20).  The launcher bumps the cluster epoch and restarts it as a fresh process;
+    the surviving worker re-forms the cluster in the new epoch, the PS task leaves and is
+    restarted for it (its shard is re-seeded), the chief -- surviving or restarted -- restores
+    the latest checkpoint into the new PS, and training reaches max_steps with a consistent
+    global step in the final checkpoint."""
+    ckpt = tmp_path / "ckpt"
+    codes, logs = launch_local(os.path.join(ROOT, "run_mnist_distributed.py"), 1, 2,
+                               str(tmp_path),
+                               ["--max_steps=45", f"--data_dir={mnist_dir}",
+                                f"--log_dir={tmp_path}/tb", "--batch_size=32",
+                                f"--checkpoint_dir={ckpt}", "--save_checkpoint_steps=10"],
+                               env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2",
+                                    "DTF_FAULT_SIGKILL": f"{victim}@20"},
+                               timeout_s=300, max_restarts=1)
+    text = {k: open(v).read() for k, v in logs.items()}
+    assert all(c == 0 for c in codes.values()), {k: t[-3000:] for k, t in text.items()}
+    dead = "worker" + victim.split(":")[1]
+    alive = "worker1" if dead == "worker0" else "worker0"
+    assert "restarting (1/1), cluster epoch 1" in text[dead], text[dead][-2000:]
+    assert "fault injection: SIGKILL" in text[dead]
+    assert "recovered: generation 1" in text[alive], text[alive][-3000:]
+    assert "rejoining the new cluster epoch" in text["ps0"]
+    if dead == "worker0":      # the restarted chief restored the checkpoint on creation
+        assert text["worker0"].count("run main with args") == 2
+    from distributedtensorflow_amd.train.checkpoint import latest_checkpoint, load_variable
+    last = latest_checkpoint(str(ckpt))
+    assert last.endswith(f"model.ckpt-{int(load_variable(last, 'global_step'))}")
+    assert int(load_variable(last, "global_step")) >= 45
+    steps = [int(s) for s in re.findall(r"global step: (\d+)\)", text["worker0"])]
+    assert steps and steps[-1] >= 44
+
+
+@pytest.mark.parametrize("strategy", ["mirrored", "ps"])
+def test_collective_rank_killed_world_reforms_and_resumes(tmp_path, strategy):
+    """A 2-rank synchronous world (MirroredStrategy, or the sharded colocated parameter server)
+    under launch_collective: rank 1 is SIGKILLed at step 5.  The launcher restarts it alone in a
+    new epoch; rank 0's collective fails (CommError), it leaves the broken group, joins the new
+    epoch, rebuilds its reducer, restores the chief's latest checkpoint (step 3) and broadcasts
+    it; both ranks reach step 12 bit-identical."""
+    from distributedtensorflow_amd.cluster.launcher import launch_collective
+    codes, logs = launch_collective(os.path.join(HERE, "dist_worker.py"), 2, str(tmp_path),
+                                    ["mirrored_recovery", str(tmp_path), "steps=12", "save=3",
+                                     f"strategy={strategy}", "opt=adam"],
+                                    env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2",
+                                         "DTF_FAULT_SIGKILL": "rank:1@5"},
+                                    timeout_s=240, max_restarts=1)
+    text = {k: open(v).read() for k, v in logs.items()}
+    assert all(c == 0 for c in codes.values()), {k: t[-3000:] for k, t in text.items()}
+    assert "restarting (1/1), cluster epoch 1" in text["rank1"]
+    assert "recovered: generation 1" in text["rank0"], text["rank0"][-3000:]
+    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(2)]
+    assert res[0]["recoveries"] == 1 and res[1]["restart"] == 1
+    assert all(r["global_step"] == 12 for r in res)
+    assert res[0]["fingerprints"] == res[1]["fingerprints"]
+    for k in res[0]["state"]:
+        assert torch.equal(res[0]["state"][k], res[1]["state"][k]), k
 
 
 def test_ps_killed_mid_run_is_restarted_and_training_resumes(tmp_path, mnist_dir):
