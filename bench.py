@@ -60,11 +60,22 @@ def parse():
     p.add_argument("--model", choices=("resnet50", "bert_base"), default="resnet50",
                    help="resnet50: the headline metric; bert_base: BASELINE config 5 "
                         "(MLM, LAMB, MultiWorkerMirroredStrategy) in tokens/sec")
-    p.add_argument("--strategy", choices=("mirrored", "ps"), default="mirrored",
+    p.add_argument("--strategy", choices=("mirrored", "ps", "ps_async"), default="mirrored",
                    help="mirrored: MirroredStrategy (bucketed RCCL all-reduce overlapped with "
                         "backward); ps: BASELINE config 4, colocated synchronous "
-                        "ParameterServerStrategy (--num-ps owner ranks; 1 = '1 PS + N workers')")
+                        "ParameterServerStrategy (--num-ps owner ranks; 1 = '1 PS + N workers', "
+                        "= N: sharded owners, reduce-scatter / all-gather); ps_async: config 4 in "
+                        "the reference's own mode -- this process launches 1 PS task + "
+                        "--num-workers worker tasks (between-graph, Hogwild pushes applied on "
+                        "arrival; utils/ps_bench.py)")
     p.add_argument("--num-ps", type=int, default=1)
+    p.add_argument("--num-workers", type=int, default=1, help="ps_async: worker tasks")
+    p.add_argument("--timeout", type=float, default=900, help="ps_async: launcher timeout (s)")
+    # set by the ps_async launcher on its tasks (cluster/launcher.py)
+    p.add_argument("--job_name", default=None, help=argparse.SUPPRESS)
+    p.add_argument("--task_index", type=int, default=0, help=argparse.SUPPRESS)
+    p.add_argument("--config", default=None, help=argparse.SUPPRESS)
+    p.add_argument("--out-dir", default=None, help=argparse.SUPPRESS)
     p.add_argument("--seq-len", type=int, default=128)
     p.add_argument("--max-predictions", type=int, default=20)
     p.add_argument("--gemm-tuning", choices=("auto", "off", "tune"), default="auto",
@@ -268,6 +279,11 @@ def tune_buckets(args, opt, strategy, step, images, labels, sync, dev, steps=2):
 
 def main():
     args = parse()
+    if args.strategy == "ps_async":
+        from distributedtensorflow_amd.utils import ps_bench
+        if args.job_name:
+            return ps_bench.run_task(args)
+        return ps_bench.run_launcher(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -110,6 +110,20 @@ class ClusterSpec:
         ``is_chief = task_index == 0``, ``run_mnist_distributed.py:106``)."""
         return ("chief", 0) if self.num_tasks("chief") else ("worker", 0)
 
+    def hosts(self):
+        """The distinct hosts of the cluster's tasks (loopback names folded together)."""
+        out = set()
+        for job in self.jobs:
+            for addr in self.job_tasks(job):
+                h = split_host_port(addr)[0].lower()
+                out.add("localhost" if h in ("localhost", "127.0.0.1", "::1", "0.0.0.0") else h)
+        return out
+
+    def single_host(self):
+        """True when every task runs on one host: the parameter servers' device data plane
+        (hipIpc / shared memory) is only valid there; other clusters use gloo over TCP."""
+        return len(self.hosts()) <= 1
+
     def rendezvous_address(self):
         job, idx = self.chief()
         host, port = split_host_port(self.task_address(job, idx))

@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import json
 import os
+import socket
 import threading
 import time
 import uuid
@@ -52,6 +53,12 @@ def _hip():
     return native.kernels()
 
 
+# buffers this process exported: a mapping request from the SAME process (an owner and a worker
+# colocated in one process, e.g. the data-plane tests) gets the original tensor -- HIP refuses to
+# open an IPC handle in the process that created it
+_LOCAL_EXPORTS = {}
+
+
 def alloc_shared(numel, device, tag):
     """A zeroed fp32 buffer other processes of this node can map.  Returns (tensor, descriptor)."""
     device = torch.device(device)
@@ -60,6 +67,7 @@ def alloc_shared(numel, device, tag):
         from torch.utils.dlpack import from_dlpack
         cap, handle = _hip().ipc_alloc(numel, device.index or 0)
         t = from_dlpack(cap)
+        _LOCAL_EXPORTS[handle.hex()] = t
         return t, {"kind": "ipc", "handle": handle.hex(), "numel": numel}
     path = f"/dev/shm/dtf_{tag}_{os.getpid()}_{uuid.uuid4().hex[:8]}"
     with open(path, "wb") as f:
@@ -73,6 +81,9 @@ def open_shared(desc, device):
     if desc["kind"] == "ipc":
         if device.type != "cuda":
             raise RuntimeError("a CPU worker cannot map a parameter server's HBM shard")
+        local = _LOCAL_EXPORTS.get(desc["handle"])
+        if local is not None:
+            return local
         from torch.utils.dlpack import from_dlpack
         return from_dlpack(_hip().ipc_open(bytes.fromhex(desc["handle"]), int(desc["numel"]),
                                            device.index or 0))
@@ -81,6 +92,8 @@ def open_shared(desc, device):
 
 
 def release_shared(desc):
+    if desc and desc.get("kind") == "ipc":
+        _LOCAL_EXPORTS.pop(desc["handle"], None)
     if desc and desc.get("kind") == "shm":
         try:
             os.unlink(desc["path"])
@@ -204,27 +217,52 @@ def _make_optimizer(cfg, space):
 # ----------------------------------------------------------------------------- PS side
 
 class OwnerShard:
-    """A PS task's shard on the device data plane + its service thread."""
+    """A PS task's shard on the device data plane + its service thread.
+
+    Streams (GPU shard).  Every write into the shard's buffers -- the initial values, restored
+    slots, the sync accumulator, every optimizer apply -- is issued on the shard's own HIP
+    streams and the shard is synchronised before it is published to workers, so nothing the
+    default stream does can race with the service's writes.
+
+    Async (Hogwild, TF ``use_locking=False``, the reference's mode): each worker's mailbox slot
+    has its OWN stream and its own copy of the per-apply hyper-parameter buffers, so the
+    service thread launches a worker's apply the moment its post arrives, without a host lock
+    around the kernel and without waiting for other workers' applies; a completion thread
+    answers each worker when ITS apply's event has completed (so the worker's next pull sees its
+    update).  ``use_locking=True`` (spec) serialises the applies on one stream instead.
+    Sync (SyncReplicasOptimizer): gradients are summed on the shard stream; the answer to the
+    step's contributors follows the apply's event."""
 
     def __init__(self, spec, values, device, worker_ranks, ps_index):
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.names = spec["names"]
         self.shapes = [tuple(s) for s in spec["shapes"]]
         offsets = spec["owner_offsets"]
         numel = int(spec["numel"])
         self.numel = numel
         self.worker_ranks = list(worker_ranks)
-        tag = f"ps{ps_index}"
-        self.master, self.master_desc = alloc_shared(numel, self.device, tag + "m")
         nw = len(self.worker_ranks)
+        tag = f"ps{ps_index}"
+        cuda = self.device.type == "cuda"
+        self.stream = torch.cuda.Stream(self.device) if cuda else None
+        self.use_locking = bool(spec.get("use_locking", False))
+        self.streams = ([self.stream] * nw if self.use_locking else
+                        [torch.cuda.Stream(self.device) for _ in range(nw)]) if cuda else []
+        self.master, self.master_desc = alloc_shared(numel, self.device, tag + "m")
         self.mail, self.mail_desc = alloc_shared(numel * nw, self.device, tag + "g")
-        with torch.no_grad():
+        with self._on(self.stream), torch.no_grad():
             for (o, shape), v in zip(zip(offsets, self.shapes), _split(values, self.shapes)):
                 n = v.numel()
-                self.master[o:o + n].copy_(v.reshape(-1).to(self.device))
-        self.space = LayoutSpace(self.master, self.names, self.shapes, offsets, spec["decay"])
-        self.params = self.space.order
-        self.opt = _make_optimizer(spec["optimizer"], self.space)
+                self.master[o:o + n].copy_(v.reshape(-1).to(self.device, non_blocking=False))
+            self.space = LayoutSpace(self.master, self.names, self.shapes, offsets,
+                                     spec["decay"])
+            self.params = self.space.order
+            self.opt = _make_optimizer(spec["optimizer"], self.space)
+            # per-slot copies of the buffers one apply reads/writes besides the shard itself
+            self._hyper = [self._hyper_buffers() for _ in range(max(nw, 1))]
+        self._sync_device()
         self.opt.iterations = int(spec.get("iterations", spec.get("global_step", 0)))
         self.sync = bool(spec.get("sync", False))
         self.replicas_to_aggregate = int(spec.get("replicas_to_aggregate") or nw)
@@ -232,44 +270,67 @@ class OwnerShard:
         self.ctl_name = f"dtf_ps{ps_index}_{os.getpid()}_{uuid.uuid4().hex[:8]}"
         self.ctl = _native().ShmControl(self.ctl_name, True, nw)
         self.ctl.global_step = self.global_step
-        self.lock = threading.Lock()
-        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.lock = threading.Lock()           # host bookkeeping only (never held over a sync)
         self._acc = None
         self._acc_count = 0
         self._waiters = []
         self._stopped_workers = set()
-        self.stats = {"applied": 0, "dropped_stale": 0, "pushes": 0, "apply_s": 0.0}
+        self.stats = {"applied": 0, "dropped_stale": 0, "pushes": 0, "aggregated": 0,
+                      "apply_s": 0.0, "max_inflight": 0}
+        self._inflight = 0
         self._thread = None
+        self._done_thread = None
+        self._done_q = None
         self._error = None
+
+    # -- helpers
+    def _on(self, stream):
+        import contextlib
+        return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+    def _sync_device(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def _hyper_buffers(self):
+        o = self.opt
+        out = {"_lr_dev": o._lr_dev.clone(), "_nonfinite": o._nonfinite}
+        for name in ("_hyper", "_norms"):          # LAMB
+            if hasattr(o, name):
+                out[name] = getattr(o, name).clone()
+        return out
 
     # -- descriptors for the workers (WAIT_READY reply)
     def descriptor(self):
+        self._sync_device()                   # every initial write landed before publishing
         return {"plane": "ipc" if self.master_desc["kind"] == "ipc" else "shm",
                 "master": self.master_desc, "mail": self.mail_desc, "numel": self.numel,
                 "ctl": self.ctl_name, "workers": self.worker_ranks,
-                "global_step": self.global_step, "pid": os.getpid()}
+                "global_step": self.global_step, "pid": os.getpid(),
+                "host": socket.gethostname()}
 
     # -- control-plane API shared with ps_service._Shard
     def flat_values(self):
         with self.lock:
+            self._sync_device()
             return torch.cat([p.detach().reshape(-1) for p in self.params]).cpu()
 
     def set_values(self, vals, global_step):
-        with self.lock, torch.no_grad():
+        with self.lock, self._on(self.stream), torch.no_grad():
             for p, v in zip(self.params, _split(vals, self.shapes)):
                 p.copy_(v.to(p.device))
             self.global_step = int(global_step)
             self.ctl.global_step = self.global_step
-            if self.device.type == "cuda":
-                torch.cuda.synchronize(self.device)
+        self._sync_device()
 
     def load_slot(self, name, flat):
         """Restore one optimizer slot (e.g. ``Adam``) from an unpadded flat of the shard's
         variables (checkpoint restore after a PS restart)."""
         slot = next(s for s in self.opt.slots if s.name == name)
-        with self.lock, torch.no_grad():
+        with self.lock, self._on(self.stream), torch.no_grad():
             for p, v in zip(self.params, _split(flat, self.shapes)):
                 self.space.view_of(slot.buf, p).copy_(v.to(slot.buf.device))
+        self._sync_device()
 
     def worker_stopped(self, worker_rank):
         with self.lock:
@@ -280,6 +341,12 @@ class OwnerShard:
 
     # -- service thread
     def start(self):
+        import queue
+        self._sync_device()
+        self._done_q = queue.Queue()
+        self._done_thread = threading.Thread(target=self._answer, name="dtf-ps-answers",
+                                             daemon=True)
+        self._done_thread.start()
         self._thread = threading.Thread(target=self._serve, name="dtf-ps-dataplane",
                                         daemon=True)
         self._thread.start()
@@ -288,6 +355,10 @@ class OwnerShard:
         self.ctl.stop()
         if self._thread is not None:
             self._thread.join(timeout=10)
+        if self._done_q is not None:
+            self._done_q.put(None)
+            self._done_thread.join(timeout=10)
+        self._sync_device()
         release_shared(self.master_desc)
         release_shared(self.mail_desc)
         self.ctl.unlink()
@@ -304,31 +375,67 @@ class OwnerShard:
                 for w, step in got:
                     self._on_push(w, step)
         except Exception as e:   # surfaced through ParameterServerService
+            import traceback
+            traceback.print_exc()
+            self._error = e
+            self.ctl.stop()
+
+    def _answer(self):
+        """Completion thread: answer workers in launch order once their apply finished."""
+        try:
+            if self.stream is not None:
+                torch.cuda.set_device(self.device)
+            while True:
+                item = self._done_q.get()
+                if item is None:
+                    return
+                ev, t0, answers, step = item
+                if ev is not None:
+                    ev.synchronize()
+                with self.lock:
+                    self._inflight -= 1
+                    self.stats["apply_s"] += time.perf_counter() - t0
+                    if step is not None and step > int(self.ctl.global_step):
+                        self.ctl.global_step = step
+                for w, s in answers:
+                    self.ctl.done(w, s)
+        except Exception as e:
+            import traceback
+            traceback.print_exc()
             self._error = e
             self.ctl.stop()
 
     def _slot(self, w):
         return self.mail[w * self.numel:(w + 1) * self.numel]
 
-    def _run_apply(self, grad, scale):
-        """Fused TF-exact optimizer over the shard, reading the gradient in place; completes
-        before the caller answers, so the worker's next pull sees the update."""
+    def _launch_apply(self, grad, scale, w, answers, step):
+        """Fused TF-exact optimizer over the shard on worker ``w``'s stream, reading the gradient
+        in place; ``answers`` are released by the completion thread after it finished."""
         t0 = time.perf_counter()
-        sp = self.space
-        sp.grad = grad
-        try:
-            if self.stream is not None:
-                with torch.cuda.stream(self.stream):
-                    self.opt.iterations += 1
-                    self.opt._apply(scale)
-                self.stream.synchronize()
-            else:
-                self.opt.iterations += 1
-                self.opt._apply(scale)
-        finally:
-            sp.grad = None
+        stream = self.streams[w] if self.streams else None
+        sp, opt = self.space, self.opt
+        with self._on(stream):
+            if stream is not None:
+                # the mailbox was filled by the worker (host-synchronised before its post); the
+                # accumulator by the shard stream
+                stream.wait_stream(self.stream)
+            for k, v in self._hyper[w].items():
+                setattr(opt, k, v)
+            sp.grad = grad
+            try:
+                opt.iterations += 1
+                opt._apply(scale)
+            finally:
+                sp.grad = None
+            ev = None
+            if stream is not None:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                self.stream.wait_stream(stream)     # later accumulator / state writes
         self.stats["applied"] += 1
-        self.stats["apply_s"] += time.perf_counter() - t0
+        self._inflight += 1
+        self.stats["max_inflight"] = max(self.stats["max_inflight"], self._inflight)
+        self._done_q.put((ev, t0, answers, step))
 
     def _maybe_fault(self):
         """DTF_FAULT_KILL_PS_AT_STEP=n (tests): this PS task dies (SIGKILL, no cleanup, like a
@@ -342,11 +449,10 @@ class OwnerShard:
         with self.lock:
             self.stats["pushes"] += 1
             if not self.sync:
-                self._run_apply(self._slot(w), 1.0)
                 self.global_step += 1
-                self.ctl.global_step = self.global_step
                 self._maybe_fault()
-                self.ctl.done(w, self.global_step)
+                self._launch_apply(self._slot(w), 1.0, w, [(w, self.global_step)],
+                                   self.global_step)
                 return
             if step < self.global_step:                  # stale gradient: drop, release now
                 self.stats["dropped_stale"] += 1
@@ -354,15 +460,14 @@ class OwnerShard:
                 return
             slot = self._slot(w)
             if self._acc is None:
-                self._acc = torch.zeros_like(slot)
+                with self._on(self.stream):
+                    self._acc = torch.zeros_like(slot)
                 self._acc_count = 0
             if self._acc_count < self.replicas_to_aggregate:
-                if self.stream is not None:
-                    with torch.cuda.stream(self.stream):
-                        self._acc.add_(slot)
-                else:
+                with self._on(self.stream):
                     self._acc.add_(slot)
                 self._acc_count += 1
+                self.stats["aggregated"] += 1
             else:
                 self.stats["dropped_stale"] += 1
             self._waiters.append(w)
@@ -370,16 +475,19 @@ class OwnerShard:
                 self._close_step()
 
     def _close_step(self):
-        if self._acc is not None and self._acc_count > 0:
-            self._run_apply(self._acc, 1.0 / self._acc_count)
-            self.global_step += 1
-            self.ctl.global_step = self.global_step
-        if self._acc is not None:
-            self._acc.zero_()
-        self._acc_count = 0
         waiters, self._waiters = self._waiters, []
-        for w in waiters:
-            self.ctl.done(w, self.global_step)
+        if self._acc is not None and self._acc_count > 0:
+            self.global_step += 1
+            # the apply runs on the shard stream (slot 0's stream is the shard stream under
+            # use_locking; otherwise the sync apply gets its own ordering via the shard stream)
+            self._launch_apply(self._acc, 1.0 / self._acc_count, 0,
+                               [(w, self.global_step) for w in waiters], self.global_step)
+            with self._on(self.stream):
+                self._acc.zero_()                # ordered after the apply (shard stream)
+        else:
+            for w in waiters:
+                self.ctl.done(w, self.global_step)
+        self._acc_count = 0
 
 
 def _split(flat, shapes):
@@ -402,6 +510,11 @@ class PSLink:
     master buffer (and its bf16 compute shadow)."""
 
     def __init__(self, desc, plan, worker_index, device, ps_index, timeout_s=None):
+        host = desc.get("host")
+        if host is not None and host != socket.gethostname():
+            raise RuntimeError(f"parameter server {ps_index} runs on host {host!r}, this worker "
+                               f"on {socket.gethostname()!r}: its device data plane cannot be "
+                               f"mapped here (use data_plane='gloo' across hosts)")
         self.desc = desc
         self.plan = plan
         self.w = int(worker_index)

@@ -376,20 +376,32 @@ class PSClient:
     ``pull()`` copies the PS values into the local parameters, ``push()`` sends the local
     gradients and returns the new global step."""
 
-    def __init__(self, ps_ranks, group=None, policy="balanced", space=None, data_plane=None):
+    def __init__(self, ps_ranks, group=None, policy="balanced", space=None, data_plane=None,
+                 single_host=True):
         import os
         self.ps_ranks = list(ps_ranks)
         self.group = group
         self.policy = policy
         self.space = space
         # device data plane needs the flat buffers (ps_device.py); "gloo" = round-1 host path
-        self.data_plane = (data_plane or os.environ.get("DTF_PS_DATA_PLANE", "auto")) \
+        plane = (data_plane or os.environ.get("DTF_PS_DATA_PLANE", "auto")) \
             if space is not None else "gloo"
+        if not single_host and plane != "gloo":
+            # hipIpc / /dev/shm mappings only exist between processes of one host: a cluster
+            # spanning hosts (the reference's config.json lists tasks by IP) uses TCP
+            if plane != "auto":
+                raise ValueError(f"data_plane={plane!r} needs every task on one host; this "
+                                 f"cluster spans several (use 'auto' or 'gloo')")
+            plane = "gloo"
+        self.data_plane = plane
         self.params = None
         self.owner = None
         self.global_step = 0
         self.links = None
         self.plans = None
+        # host-side time per push on the device plane (bench breakdown): waiting for the local
+        # gradients + mailbox copy, waiting for the owner's answer, issuing the pull
+        self.timing = {"copy_sync_ms": [], "wait_ms": [], "pull_ms": []}
 
     def _layout(self, params):
         self.params = list(params)
@@ -483,17 +495,27 @@ class PSClient:
         ``pull`` the reply carries the updated shard values, copied into the local variables
         (push + pull in one round trip).  Returns the new global step."""
         if self.links:
+            import time
+
             from .ps_device import sync_device
+            t0 = time.perf_counter()
             for link in self.links:                  # gradients straight into the mailboxes
                 link.copy_grads(self.space)
             sync_device(self.space.device)
+            t1 = time.perf_counter()
             for link in self.links:
                 link.post(self.global_step)
             steps = [link.wait() for link in self.links]
             self.global_step = steps[0]
+            t2 = time.perf_counter()
             if pull:
                 for link in self.links:
                     link.pull(self.space)
+            t3 = time.perf_counter()
+            tm = self.timing
+            tm["copy_sync_ms"].append((t1 - t0) * 1e3)
+            tm["wait_ms"].append((t2 - t1) * 1e3)
+            tm["pull_ms"].append((t3 - t2) * 1e3)
             return self.global_step
         grads = grads or [p.grad for p in self.params]
         for k, rank in enumerate(self.ps_ranks):

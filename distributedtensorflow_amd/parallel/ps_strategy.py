@@ -303,7 +303,8 @@ class ParameterServerStrategy(Strategy):
         if self.mode == "between_graph":
             from .ps_service import PSClient
             self._client = PSClient(self.server.ps_ranks(), policy=self.variable_placement,
-                                    space=space, data_plane=self.data_plane)
+                                    space=space, data_plane=self.data_plane,
+                                    single_host=self.server.cluster.single_host())
             return _RemotePSReducer(space, self._client)
         if not self.collective:
             return _NullReducer(space)
@@ -368,7 +369,8 @@ class ParameterServerStrategy(Strategy):
         from .ps_service import PSClient
         old = self._client
         self._client = PSClient(self.server.ps_ranks(), policy=self.variable_placement,
-                                space=old.space, data_plane=self.data_plane)
+                                space=old.space, data_plane=self.data_plane,
+                                single_host=self.server.cluster.single_host())
         reducer = getattr(optimizer, "_reducer", None)
         if reducer is not None and hasattr(reducer, "client"):
             reducer.client = self._client

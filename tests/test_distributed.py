@@ -367,3 +367,22 @@ def test_ps_killed_mid_run_is_restarted_and_training_resumes(tmp_path, mnist_dir
     assert int(load_variable(last, "global_step")) >= 45
     assert abs(load_variable(last, "conv2d/kernel/Adam")).sum() > 0     # slots survived
 
+
+
+def test_bench_ps_async_flow_cpu(tmp_path):
+    """bench.py --strategy ps_async (BASELINE config 4 in the reference's async mode): the bench
+    process launches 1 PS + 2 worker tasks, every push is applied on arrival (no drops), and
+    the rank-0 style JSON line carries the aggregate and the push/wait/pull breakdown."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--strategy", "ps_async",
+                        "--num-workers", "2", "--batch", "2", "--image-size", "32", "--steps",
+                        "2", "--warmup", "1", "--timeout", "200"],
+                       env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2"),
+                       capture_output=True, text=True, timeout=260, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = rec["config"]
+    assert cfg["parallelism"] == "ps1+async2" and cfg["data_plane"] == "shm"
+    assert cfg["ps_applied"] == cfg["ps_pushes"] == 2 * (2 + 1)       # nothing dropped
+    assert cfg["final_global_step"] == 6 and rec["value"] > 0
+    assert set(cfg["worker_host_ms_per_step"]) == {"copy_sync_ms_per_step", "wait_ms_per_step",
+                                                   "pull_ms_per_step"}
