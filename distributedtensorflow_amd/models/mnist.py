@@ -22,6 +22,8 @@ IMAGE_PIXELS = 28
 
 
 class MnistCNN(Layer):
+    input_signature_shape = (None, 784)      # SavedModel serving input (flat 28x28 images)
+
     def __init__(self, num_classes=10):
         super().__init__()
         with name_scope():
@@ -42,6 +44,8 @@ class MnistCNN(Layer):
 
 
 class MnistMLP(Layer):
+    input_signature_shape = (None, 784)
+
     def __init__(self, hidden_units=100, num_classes=10):
         super().__init__()
         self.hid_w = _tag(nn.Parameter(torch.empty(IMAGE_PIXELS * IMAGE_PIXELS, hidden_units)),

@@ -105,6 +105,8 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(Layer):
+    input_signature_shape = (None, 224, 224, 3)      # SavedModel serving input, NHWC
+
     def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, in_channels=3,
                  bn_momentum=0.997, bn_eps=1e-5, zero_init_residual=False):
         super().__init__()

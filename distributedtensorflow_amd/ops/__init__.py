@@ -258,21 +258,34 @@ def set_param_fence(fn):
     _PARAM_FENCE = fn
 
 
-def _fenced(fn):
+_TRACER = None      # train/saved_model.py: records ops applied to symbolic graph tensors
+
+
+def set_tracer(tracer):
+    global _TRACER
+    _TRACER = tracer
+
+
+def _dispatch(name, fn, fenced):
     import functools
 
     @functools.wraps(fn)
     def op(*args, **kw):
-        if _PARAM_FENCE is not None:
+        if _TRACER is not None and args and isinstance(args[0], _TRACER.Tensor):
+            return _TRACER.call(name, args, kw)
+        if fenced and _PARAM_FENCE is not None:
             _PARAM_FENCE(args, kw)
         return fn(*args, **kw)
     return op
 
 
-for _name in ("conv2d", "conv2d_bias_relu", "batch_norm", "batch_norm_add_batch_norm",
-              "batch_norm_relu_max_pool", "dense", "layer_norm", "bias_dropout_add_layer_norm",
-              "embedding_layer_norm", "bias_gelu"):
-    globals()[_name] = _fenced(globals()[_name])
+_FENCED = ("conv2d", "conv2d_bias_relu", "batch_norm", "batch_norm_add_batch_norm",
+           "batch_norm_relu_max_pool", "dense", "layer_norm", "bias_dropout_add_layer_norm",
+           "embedding_layer_norm", "bias_gelu")
+for _name in _FENCED + ("relu", "max_pool2d", "global_avg_pool", "sparse_softmax_cross_entropy",
+                        "softmax_cross_entropy_clipped_sum", "gelu", "attention", "dropout",
+                        "attention_qkv", "mlm_loss"):
+    globals()[_name] = _dispatch(_name, globals()[_name], _name in _FENCED)
 del _name
 
 __all__ = [

@@ -273,25 +273,16 @@ def load_variable(ckpt, name):
 
 # ----------------------------------------------------------------------------- SavedModel
 
-def save_saved_model(export_dir, model, tags=("serve",)):
-    """SavedModel directory layout: ``saved_model.pb`` + ``variables/variables.{index,data}``."""
-    os.makedirs(os.path.join(export_dir, "variables"), exist_ok=True)
-    saver = Saver(model, write_meta_graph=False)
-    tensors = saver._vars()
-    saver.save(save_path=os.path.join(export_dir, "variables", "variables"))
-    state = os.path.join(export_dir, "variables", "checkpoint")
-    if os.path.exists(state):
-        os.remove(state)
-    meta = meta_graph_bytes(sorted(tensors))
-    meta_with_tags = meta[:0] + meta
-    # MetaGraphDef.meta_info_def.tags (field 4) are inside meta_info_def; add them there
-    info = _pb_str(1, "dtf-v1") + _pb_str(5, "1.15.0-dtf") + b"".join(_pb_str(4, t) for t in tags)
-    meta_with_tags = _pb_msg(1, info) + meta.split(_pb_msg(1, _pb_str(1, "dtf-v1") +
-                                                           _pb_str(5, "1.15.0-dtf")), 1)[1]
-    saved_model = _pb_int(1, 1) + _pb_msg(2, meta_with_tags)
-    with open(os.path.join(export_dir, "saved_model.pb"), "wb") as f:
-        f.write(saved_model)
-    return export_dir
+def save_saved_model(export_dir, model, tags=("serve",), input_shape=None):
+    """SavedModel directory: ``saved_model.pb`` (inference GraphDef traced from the model, the
+    saver subgraph and a ``serving_default`` signature; train/saved_model.py) +
+    ``variables/variables.{index,data-00000-of-00001}``.  ``input_shape`` defaults to the
+    model's ``input_signature_shape`` (``None`` = the batch dimension)."""
+    from .saved_model import export_saved_model
+    shape = input_shape or getattr(model, "input_signature_shape", None)
+    if shape is None:
+        raise ValueError("save_saved_model needs input_shape= for this model")
+    return export_saved_model(export_dir, model, tuple(shape), tags)
 
 
 def load_saved_model_variables(export_dir, model):
