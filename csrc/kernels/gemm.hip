@@ -637,6 +637,409 @@ gemm_nt_kernel(const GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent ping-pong GEMM with a register-direct epilogue (gemm_pp_kernel).
+//
+// Same 256 x 256 x 64 ping-pong main loop as SCHED 2 above, with two changes aimed at the part
+// of the step the MFMA pipe idles in -- the epilogue, ~30 % of a K = 768 BERT GEMM
+// (profiles/measurements/r2_gemm_epilogue_probes.jsonl):
+//   * the MFMA operands are swapped (D = B . A^T per 16 x 16 fragment), so each lane holds FOUR
+//     CONSECUTIVE OUTPUT COLUMNS of one row: the epilogue stores 8 B per lane straight from the
+//     accumulators (16-lane groups write 32 contiguous bytes; the four fragments of a 64-column
+//     wave strip complete whole 128-B lines back to back in L2) -- no LDS staging, no barrier;
+//   * blocks are PERSISTENT (one per CU, tiles strided by the grid) and the LDS-DMA piece stream
+//     runs ACROSS tiles: the K-loop's look-ahead issues of "step nk, nk + 1" are the NEXT tile's
+//     steps 0 / 1, so while a block stores tile t's outputs the DMA engine is already filling the
+//     ring with tile t + 1.  The ring slot parity follows the block's global step count.
+// Every lane issues the same number of stores per tile (out-of-range ones carry an offset past
+// the C descriptor and are dropped by the hardware range check), so the counted vmcnt waits of
+// the next tile's first phases know exactly how many stores sit behind the pieces they need.
+template <int CONV>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp_kernel(const GemmArgs g) {
+  using Cf = GCfg<256, 256, 64, 2, 8>;
+  constexpr int BM = 256, BN = 256, BK = 64;
+  constexpr int NSTORE = Cf::FM * Cf::FN;          // 8-B stores per lane per tile (32)
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cf::WN, wn = wave % Cf::WN;
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int ntiles = tiles_n * tiles_m;
+  const int nk = (g.K + BK - 1) / BK;              // >= 2 (host)
+  const uint32_t lds0 = lds_addr(lds);
+  const int lrow = lane / Cf::CPR, slot = lane % Cf::CPR;
+  const int frow = lane & 15, fq = lane >> 4;
+  const bool ktail = (g.K % BK) != 0;
+  const int PQc = CONV ? g.P * g.Q : 1;
+  const long img = CONV ? (long)g.H * g.W * g.Cc : 0;
+  const bool strided = CONV && (g.osh != 1 || g.osw != 1);
+
+  // piece pc (0 A-top, 1 B-left, 2 B-right, 3 A-bottom), instruction j: the 8-row group of this
+  // wave inside the tile's A / B panel (see SCHED 2)
+  auto prow = [&](int pc, int j) {
+    const int r0 = pc == 0 ? j * 128 + 8 * wave
+                 : pc == 3 ? 64 + j * 128 + 8 * wave
+                           : (2 * j + (wave >> 2)) * 64 + (pc == 2 ? 32 : 0) + (wave & 3) * 8;
+    return r0 + lrow;
+  };
+  const int pch = gswz<BK>(prow(0, 0), slot) * 8;   // the same for every piece of this wave
+  auto plds = [&](int pc, int j) {
+    const bool isA = pc == 0 || pc == 3;
+    return (uint32_t)((isA ? 0 : Cf::SA) + (prow(pc, j) - lrow) * BK) * 2u;
+  };
+
+  struct Tile { int valid, m0, n0, rows_a, rows_b, n_lo; };
+  auto tile_of = [&](int seq) {
+    Tile t{};
+    const long phys = (long)blockIdx.x + (long)seq * gridDim.x;
+    if (phys >= ntiles) return t;
+    const int bid = xcd_remap((int)phys, ntiles);
+    const int tm = bid / tiles_n, tn = bid % tiles_n;
+    t.valid = 1;
+    t.m0 = tm * BM;
+    t.n0 = tn * BN;
+    t.rows_a = min(BM, g.M - t.m0);
+    t.rows_b = min(BN, g.N - t.n0);
+    t.n_lo = CONV ? t.m0 / PQc : 0;
+    return t;
+  };
+  auto desc_a = [&](const Tile& t) {
+    return CONV ? rsrc_quad(g.A + t.n_lo * img,
+                            (uint32_t)(((t.m0 + t.rows_a - 1) / PQc - t.n_lo + 1) * img * 2))
+                : rsrc_quad(g.A + (long)t.m0 * g.lda,
+                            (uint32_t)((long)(t.rows_a - 1) * g.lda + g.K) * 2u);
+  };
+  auto desc_b = [&](const Tile& t) {
+    return rsrc_quad(g.B + (long)t.n0 * g.ldb,
+                     (uint32_t)((long)(t.rows_b - 1) * g.ldb + g.K) * 2u);
+  };
+  // per-lane source offset of a B (or dense A) piece instruction of tile t: element offset of
+  // (row, chunk) in bytes, or 2^31 (past every descriptor) for rows past the operand
+  auto boff = [&](const Tile& t, int pc, int j) {
+    const bool isA = pc == 0 || pc == 3;
+    const int row = prow(pc, j);
+    const int rows = isA ? t.rows_a : t.rows_b;
+    const int ld = isA ? g.lda : g.ldb;
+    return row < rows ? (uint32_t)(row * ld + pch) * 2u : 0x80000000u;
+  };
+  // CONV A piece instruction: the image base pixel and the packed top-left (h | w) of the
+  // receptive field of output row m0 + row (invalid rows: h far out of range)
+  auto ageom = [&](const Tile& t, int pc, int j, int& pix, int& hw) {
+    const int m = t.m0 + prow(pc, j);
+    const bool ok = m < g.M;
+    const int mm = ok ? m : t.m0;
+    const int q = mm % g.Q, tt = mm / g.Q;
+    const int p = tt % g.P, n = tt / g.P;
+    pix = (n - t.n_lo) * g.H * g.W;
+    hw = ((ok ? p * g.sh : 0x7000) << 16) | (q * g.sw);
+  };
+
+  Tile cur = tile_of(0);
+  if (!cur.valid) return;
+  int seq = 0;
+  bool nxt_valid = tile_of(1).valid;
+  i32x4_t ra = desc_a(cur), rb = desc_b(cur);
+  // CONV: the current tile's A-piece geometry (integer divisions), cached per tile
+  int apix[2][2], ahw[2][2];
+  auto cache = [&]() {
+    if constexpr (CONV) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) ageom(cur, a ? 3 : 0, j, apix[a][j], ahw[a][j]);
+    }
+  };
+  cache();
+  int gstep0 = 0;                                  // this block's steps before the current tile
+
+  auto dma_a_conv = [&](const i32x4_t& rA, int kk, bool live, int pix, int hw, uint32_t dst) {
+    const int cb = g.Cc / BK;
+    const int tap = kk / cb, c0 = (kk % cb) * BK;
+    const int h = (hw >> 16) + g.tdh[tap], w = (hw & 0xFFFF) + g.tdw[tap];
+    const bool ok = live && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+    dma16(rA, dst, ok ? (uint32_t)(((pix + h * g.W + w) * g.Cc + c0 + pch) * 2) : kGOOB);
+  };
+  auto dma_dense = [&](const i32x4_t& r, int kk, bool live, uint32_t off, uint32_t dst) {
+    const int k0 = kk * BK;
+    uint32_t o = off + (uint32_t)k0 * 2u;
+    if (!live || (ktail && k0 + pch >= g.K)) o = kGOOB;
+    dma16(r, dst, o);
+  };
+  // piece pc of step kt (relative to the current tile; kt >= nk: the next tile's step kt - nk)
+  auto issue_piece = [&](int kt, int pc) {
+    const uint32_t base = lds0 + (uint32_t)(((gstep0 + kt) & 1) * Cf::STAGE) * 2u;
+    const bool isA = pc == 0 || pc == 3;
+    if (kt < nk) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (CONV && isA)
+          dma_a_conv(ra, kt, true, apix[pc == 3][j], ahw[pc == 3][j], base + plds(pc, j));
+        else
+          dma_dense(isA ? ra : rb, kt, true, boff(cur, pc, j), base + plds(pc, j));
+      }
+      return;
+    }
+    const Tile t = nxt_valid ? tile_of(seq + 1) : cur;
+    const i32x4_t r = isA ? desc_a(t) : desc_b(t);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (CONV && isA) {
+        int pix, hw;
+        ageom(t, pc, j, pix, hw);
+        dma_a_conv(r, nxt_valid ? kt - nk : 0, nxt_valid, pix, hw, base + plds(pc, j));
+      } else {
+        dma_dense(r, nxt_valid ? kt - nk : 0, nxt_valid, boff(t, pc, j), base + plds(pc, j));
+      }
+    }
+  };
+
+  f32x4_t acc[Cf::FM][Cf::FN];
+#pragma unroll
+  for (int i = 0; i < Cf::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t fA[8], fBl[4], fBr[4];
+  auto rdA = [&](const bf16_t* sa, int half) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 128 + half * 64 + i * 16 + frow, ch = ks * 4 + fq;
+        fA[ks * 4 + i] = *reinterpret_cast<const bf16x8_t*>(sa + r * BK + gswz<BK>(r, ch) * 8);
+      }
+  };
+  auto rdB = [&](bf16x8_t* fb, const bf16_t* sa, int half) {
+    const bf16_t* sb = sa + Cf::SA;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 64 + half * 32 + j * 16 + frow, ch = ks * 4 + fq;
+        fb[ks * 2 + j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
+      }
+  };
+  auto sync = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mfma_phase = [&](const bf16x8_t* fb, int ah, int bh) {
+    sync();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ah * 4 + i][bh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              fb[ks * 2 + j], fA[ks * 4 + i], acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+  };
+
+  float* red = reinterpret_cast<float*>(lds + 2 * Cf::STAGE);   // [WM][2][BN] past the ring
+  const bool do_stats = g.stats != nullptr;
+
+  // prologue of the first tile: step 0 whole + step 1's A-top / B-left
+  issue_piece(0, 0); issue_piece(0, 1); issue_piece(0, 2); issue_piece(0, 3);
+  issue_piece(1, 0); issue_piece(1, 1);
+  DTF_WAIT_VM(8);
+  bool first = true;
+  for (;; ++seq) {
+    sync();
+    if (wm == 1) sync();                       // the one-barrier stagger
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* cur_lds = lds + ((gstep0 + kt) & 1) * Cf::STAGE;
+      rdB(fBl, cur_lds, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      rdA(cur_lds, 0);
+      issue_piece(kt + 1, 2);
+      // step 0 of every tile after the first: the previous tile's NSTORE = 32 stores were
+      // issued after the pieces this phase and the next need (younger than step 0's B-right /
+      // A-bottom: 3 pieces = 6 ops, the 32 stores, this step's 1 or 2 pieces = 2 / 4 ops -> 40)
+      if (!first && kt == 0) DTF_WAIT_VM(40); else DTF_WAIT_VM(8);
+      mfma_phase(fBl, 0, 0);                   // q0: top x left
+      rdB(fBr, cur_lds, 1);
+      issue_piece(kt + 1, 3);
+      if (!first && kt == 0) DTF_WAIT_VM(40); else DTF_WAIT_VM(8);
+      mfma_phase(fBr, 0, 1);                   // q1: top x right
+      rdA(cur_lds, 1);
+      issue_piece(kt + 2, 0);
+      DTF_WAIT_VM(8);
+      mfma_phase(fBr, 1, 1);                   // q2: bottom x right
+      issue_piece(kt + 2, 1);
+      DTF_WAIT_VM(8);
+      mfma_phase(fBl, 1, 0);                   // q3: bottom x left
+    }
+    if (wm == 0) sync();                       // re-align the barrier counts
+
+    // ---- epilogue: accumulators -> (+bias, ReLU, BN statistics, +Cin / masked acc) -> C
+    // lane (frow, fq) of fragment (i, j) holds C[m][n .. n + 3]: m = wm*128 + i*16 + frow,
+    // n = wn*64 + j*16 + fq*4
+    long cbase;
+    uint32_t cbytes;
+    if (strided) {
+      const int n_hi = (cur.m0 + cur.rows_a - 1) / PQc;
+      cbase = (long)cur.n_lo * g.Ho * g.Wo * g.ldc;
+      cbytes = (uint32_t)((long)(n_hi - cur.n_lo + 1) * g.Ho * g.Wo * g.ldc * 2);
+    } else {
+      cbase = (long)cur.m0 * g.ldc;
+      cbytes = (uint32_t)(((long)(cur.rows_a - 1) * g.ldc + g.N) * 2);
+    }
+    const __amdgpu_buffer_rsrc_t rc =
+        __builtin_amdgcn_make_buffer_rsrc(g.C + cbase, 0, (int)cbytes, 0x00020000);
+    const bool nt_store = g.nt != 0;      // non-temporal (aux bit 1)
+    long rowoff[Cf::FM];                       // element offset of row m (from cbase), -1: none
+#pragma unroll
+    for (int i = 0; i < Cf::FM; ++i) {
+      const int m = cur.m0 + wm * 128 + i * 16 + frow;
+      long o = -1;
+      if (m < g.M) {
+        if (strided) {
+          const int q = m % g.Q, t = m / g.Q;
+          const int p = t % g.P, n = t / g.P;
+          o = ((long)(n - cur.n_lo) * g.Ho + p * g.osh + g.oh0) * g.Wo + q * g.osw + g.ow0;
+          o *= g.ldc;
+        } else {
+          o = (long)(m - cur.m0) * g.ldc;
+        }
+      }
+      rowoff[i] = o;
+    }
+#pragma unroll
+    for (int j = 0; j < Cf::FN; ++j) {
+      const int ncol = cur.n0 + wn * 64 + j * 16 + fq * 4;
+      const bool col_ok = ncol < g.N;
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (g.bias && col_ok) {
+        const float4 bv = *reinterpret_cast<const float4*>(g.bias + ncol);
+        b4[0] = bv.x; b4[1] = bv.y; b4[2] = bv.z; b4[3] = bv.w;
+      }
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < Cf::FM; ++i) {
+        const bool ok = col_ok && rowoff[i] >= 0;
+        float v[4];
+        bf16_t h[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[i][j][r] + b4[r];
+          if (g.relu) v[r] = fmaxf(v[r], 0.f);
+          h[r] = f2bf(v[r]);
+          if (do_stats && ok) {
+            const float qv = bf2f(h[r]);
+            s1[r] += qv;
+            s2[r] += qv * qv;
+          }
+        }
+        const long eoff = rowoff[i] + ncol;    // element offset from cbase
+        if (ok && (g.Cin || g.acc_mask)) {
+          const bf16_t* src = g.Cin ? g.Cin + cbase + eoff : g.acc_src + cbase + eoff;
+          const uint2 sv = *reinterpret_cast<const uint2*>(src);
+          const uint32_t bits = g.Cin ? 0xFu
+                                      : (g.acc_mask[(cbase + eoff) >> 3] >> ((cbase + eoff) & 7)) & 0xFu;
+          const float s[4] = {__builtin_bit_cast(float, sv.x << 16),
+                              __builtin_bit_cast(float, sv.x & 0xffff0000u),
+                              __builtin_bit_cast(float, sv.y << 16),
+                              __builtin_bit_cast(float, sv.y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] = f2bf(bf2f(h[r]) + ((bits >> r) & 1u ? s[r] : 0.f));
+        }
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t w = {(uint32_t)h[0] | ((uint32_t)h[1] << 16),
+                           (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+        const int so = ok ? (int)(eoff * 2) : (int)kGOOB;
+        if (nt_store) __builtin_amdgcn_raw_buffer_store_b64(w, rc, so, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b64(w, rc, so, 0, 0);
+      }
+      if (do_stats) {
+        // column sums over the wave's 128 rows: the 16 lanes of a column group (frow) combine
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s1[r] += __shfl_xor(s1[r], o, 64);
+            s2[r] += __shfl_xor(s2[r], o, 64);
+          }
+        }
+        if (frow == 0) {
+          const int col = wn * 64 + j * 16 + fq * 4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            red[(wm * 2 + 0) * BN + col + r] = s1[r];
+            red[(wm * 2 + 1) * BN + col + r] = s2[r];
+          }
+        }
+      }
+    }
+    if (do_stats) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+      if (tid < BN && cur.n0 + tid < g.N) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int k = 0; k < Cf::WM; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
+        const int tm = cur.m0 / BM;
+        g.stats[((long)tm * 2 + 0) * g.N + cur.n0 + tid] = a;
+        g.stats[((long)tm * 2 + 1) * g.N + cur.n0 + tid] = b;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();                           // red is rewritten by the next tile
+    }
+    if (!nxt_valid) break;
+    // ---- next tile: its first pieces are in flight (issued by the last two K-steps)
+#pragma unroll
+    for (int i = 0; i < Cf::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < Cf::FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    gstep0 += nk;
+    cur = tile_of(seq + 1);
+    nxt_valid = tile_of(seq + 2).valid;
+    ra = desc_a(cur);
+    rb = desc_b(cur);
+    cache();
+    first = false;
+    static_assert(NSTORE == 32, "the counted waits below assume 32 stores per lane per tile");
+    // step 0's A-top / B-left landed (waited by the last tile's final phase); the stores
+    // issued since are allowed to fly
+  }
+  DTF_WAIT_VM(0);       // the trailing look-ahead DMAs still target the ring
+}
+
+template <int CONV>
+void launch_gemm_pp(const GemmArgs& g, hipStream_t st) {
+  using Cf = GCfg<256, 256, 64, 2, 8>;
+  constexpr size_t LDS = (size_t)2 * Cf::STAGE * 2 + (size_t)Cf::WM * 2 * 256 * 4;
+  static bool attr = false;
+  static int ncu = 0;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_pp_kernel<CONV>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    // scratch (spilled VGPRs) would be vector-memory traffic the counted vmcnt waits do not
+    // know about: refuse to run such a build instead of racing on the LDS ring
+    hipFuncAttributes fa{};
+    HIP_CHECK(hipFuncGetAttributes(&fa, (const void*)gemm_pp_kernel<CONV>));
+    if (fa.localSizeBytes > 0)
+      throw std::runtime_error("gemm_pp_kernel was compiled with register spills (scratch " +
+                               std::to_string(fa.localSizeBytes) + " B/lane)");
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    attr = true;
+  }
+  const long tiles = (long)((g.M + 255) / 256) * ((g.N + 255) / 256);
+  // one block per CU; a multiple of 8 (whole XCDs) so tile t, t + grid, ... stay on one XCD
+  long grid = tiles < ncu ? tiles : (ncu / 8) * 8;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((gemm_pp_kernel<CONV>), dim3((unsigned)grid), dim3(Cf::NT), LDS, st, g);
+}
+
+int g_gemm_pp = 0;         // bit 0: persistent register-epilogue kernel for gemm_nt, bit 1: convs
+
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
 int g_gemm_nt = 0;         // non-temporal C stores (ResNet-50 A/B: neutral; off keeps BERT outputs cached)
 int g_gemm_dbg = 0;        // GemmArgs::dbg for timing probes
@@ -660,6 +1063,7 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
 }  // namespace
 
 void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
+void dtf_gemm_set_pp(int v) { g_gemm_pp = v; }
 void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
 void dtf_gemm_set_dbg(int v) { g_gemm_dbg = v; }
 
@@ -690,7 +1094,10 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
     throw std::runtime_error("gemm_conv: strided outputs take no BN statistics / masked acc");
   if ((long)256 * g.ldb * 2 + 2L * g.K >= (1L << 31))
     throw std::runtime_error("gemm_conv: filter too large");
+  const bool pp_span = !(osh != 1 || osw != 1) ||
+      (256.0 / (P * Q) + 2) * Ho * Wo * (double)Kout * 2 < 2147483647.0;
   if (Kout <= 128) launch_gemm<256, 128, 64, 3, 3, 8, 1, 1>(g, st);
+  else if ((g_gemm_pp & 2) && (g.K + 63) / 64 >= 2 && pp_span) launch_gemm_pp<1>(g, st);
   else launch_gemm<256, 256, 64, 2, 2, 8, 1, 1>(g, st);
 }
 
@@ -715,8 +1122,12 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
   g.dbg = g_gemm_dbg;
   // auto: 256 x 128 tiles when N <= 128 (measured 1.02-1.07x the 256 x 256 tile on the N = 128
   // ResNet 1x1 convs, profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl)
-  const int variant = g_gemm_variant >= 0 ? g_gemm_variant : (N <= 128 ? 1 : 8);
+  const int variant = g_gemm_variant >= 0 ? g_gemm_variant
+                    : (N <= 128 ? 1 : ((g_gemm_pp & 1) && (K + 63) / 64 >= 2 ? 11 : 8));
+  if (variant == 11 && (K + 63) / 64 < 2)
+    throw std::runtime_error("gemm_nt: the persistent kernel needs K > 64");
   switch (variant) {
+    case 11: launch_gemm_pp<0>(g, st); break;
     case 1: launch_gemm<256, 128, 64, 3>(g, st); break;
     case 2: launch_gemm<256, 256, 32, 4>(g, st); break;
     case 3: launch_gemm<256, 128, 32, 4>(g, st); break;

@@ -1,0 +1,87 @@
+"""The persistent register-epilogue GEMM (csrc/kernels/gemm.hip gemm_pp_kernel, variant 11)
+against the round-2 ping-pong kernel (variant 8) and an fp32 reference.
+
+The new kernel runs the same main loop with the MFMA operands swapped (each lane then holds four
+consecutive output columns) and stores straight from the accumulators, with the LDS-DMA stream
+continuing across the tiles a persistent block walks.  Per output element the products and
+their accumulation order are unchanged, so C must be BIT-IDENTICAL to variant 8 for every
+epilogue mode (bias, ReLU, beta = 1 accumulate, masked residual accumulate); the BatchNorm
+partial sums (a different summation order) must agree to fp32 rounding.  Shapes cover edge
+tiles in M and N, a K tail, K = 128 (two steps: every look-ahead piece belongs to the next
+tile) and more tiles than CUs (several tiles per block).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(4096, 768, 768), (1000, 520, 200), (65536 // 4, 2304, 768), (777, 264, 128),
+          (300, 256, 3072), (2048, 1024, 136), (256 * 300, 512, 512)]
+
+
+def _native():
+    from distributedtensorflow_amd.ops import native
+    return native
+
+
+def _run(variant, fn):
+    n = _native()
+    n._K.gemm_set_variant(variant)
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        return out
+    finally:
+        n._K.gemm_set_variant(-1)
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_pp_matches_pingpong_bitwise(M, N, K):
+    n = _native()
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    ref8 = _run(8, lambda: n.gemm_nt(a, b))
+    out = _run(11, lambda: n.gemm_nt(a, b))
+    assert torch.equal(out, ref8)
+    exact = a.float() @ b.float().t()
+    err = ((out.float() - exact).norm() / exact.norm()).item()
+    assert err < 5e-3, err
+    r8 = _run(8, lambda: n.gemm_nt(a, b, bias=bias, relu=True))
+    r11 = _run(11, lambda: n.gemm_nt(a, b, bias=bias, relu=True))
+    assert torch.equal(r11, r8)
+    cin = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    c8 = _run(8, lambda: n.gemm_nt(a, b, cin=cin.clone()))
+    c11 = _run(11, lambda: n.gemm_nt(a, b, cin=cin.clone()))
+    assert torch.equal(c11, c8)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 768, 768), (1000, 520, 200), (256 * 300, 512, 512)])
+def test_pp_masked_accumulate_and_bn_stats(M, N, K):
+    n = _native()
+    g = torch.Generator(device="cuda").manual_seed(7)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    mask = torch.randint(0, 256, (M * N // 8,), device="cuda", dtype=torch.uint8, generator=g)
+    acc = n._MaskedGrad(dy, mask)
+    m8 = _run(8, lambda: n.gemm_nt(a, b, acc_from=acc))
+    m11 = _run(11, lambda: n.gemm_nt(a, b, acc_from=acc))
+    assert torch.equal(m11, m8)
+    tiles = n._K.gemm_tile_rows(M)
+    s8 = torch.zeros(tiles, 2, N, device="cuda")
+    s11 = torch.zeros(tiles, 2, N, device="cuda")
+    y8 = _run(8, lambda: n.gemm_nt(a, b, stats=s8))
+    y11 = _run(11, lambda: n.gemm_nt(a, b, stats=s11))
+    assert torch.equal(y11, y8)
+    torch.testing.assert_close(s11, s8, rtol=1e-5, atol=1e-3)
+    yf = y8.float()
+    torch.testing.assert_close(s11[:, 0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(s11[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-4, atol=1e-1)
