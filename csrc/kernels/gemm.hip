@@ -737,6 +737,10 @@ gemm_pp_kernel(const GemmArgs g) {
 
   Tile cur = tile_of(0);
   if (!cur.valid) return;
+  // experiment (g.dbg = d > 0): start the blocks staggered by (block % 4) * d * ~3.4 us, so the
+  // CUs' epilogues (all 256 writing their 128-KB tiles in the same few microseconds when the
+  // blocks run in lockstep) spread out in time
+  for (int i = 0; i < (int)(blockIdx.x & 3) * g.dbg; ++i) __builtin_amdgcn_s_sleep(127);
   int seq = 0;
   bool nxt_valid = tile_of(1).valid;
   i32x4_t ra = desc_a(cur), rb = desc_b(cur);

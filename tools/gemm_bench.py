@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--resnet1x1", type=int, default=0,
                     help="batch: time the ResNet-50 1x1 convs as GEMMs next to the conv kernel")
+    ap.add_argument("--dbg", default="0",
+                    help="comma list of gemm_set_dbg values to time (kernel experiments)")
     ap.add_argument("--variants", default="0",
                     help="comma list of gemm.hip pipeline variants to time (gemm_set_variant)")
     a = ap.parse_args()
@@ -104,12 +106,14 @@ def main():
         err_lib = float((ref[sub].float() - exact).norm() / exact.norm())
         t_lib = timeit(lambda: torch.nn.functional.linear(A, B), a.iters)
         fl = 2.0 * M * N * K
-        for v in [int(x) for x in a.variants.split(",")]:
+        for v, d in [(int(x), int(y)) for x in a.variants.split(",") for y in a.dbg.split(",")]:
             native._K.gemm_set_variant(v)
+            native._K.gemm_set_dbg(d)
             ours = native.gemm_nt(A, B)
             err = float((ours[sub].float() - exact).norm() / exact.norm())
             t_ours = timeit(lambda: native.gemm_nt(A, B), a.iters)
-            row = {"shape": name, "variant": v, "M": M, "N": N, "K": K,
+            native._K.gemm_set_dbg(0)
+            row = {"shape": name, "variant": v, "dbg": d, "M": M, "N": N, "K": K,
                    "ours_us": round(t_ours * 1e6, 1), "hipblaslt_us": round(t_lib * 1e6, 1),
                    "ours_tflops": round(fl / t_ours / 1e12, 1),
                    "hipblaslt_tflops": round(fl / t_lib / 1e12, 1),
