@@ -54,6 +54,10 @@ def parse():
                         "time 2 steps at each of 16/32/64/128 MB (max over ranks) and keep the "
                         "fastest for the timed steps (SURVEY.md 5.8)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--cudnn-benchmark", type=int, default=1,
+                   help="--impl torch: 1 = MIOpen exhaustive algorithm search on first use "
+                        "(slow to warm up at large batch), 0 = MIOpen immediate mode (heuristic "
+                        "/ find-db solutions, no search)")
     p.add_argument("--dump-master", default=None,
                    help="after the timed steps, save the (rank-0) fp32 master weights to this "
                         "file (tests compare the forced-reducer run bit for bit with the plain one)")
@@ -308,7 +312,7 @@ def main():
         if backend not in ("nccl", "gloo"):
             raise SystemExit(f"DTF_BENCH_BACKEND={backend!r}: expected nccl or gloo")
         init_process_group_from_env(backend)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     gemm_table = setup_gemm_tuning(args)
     native_info = {"backend": "torch (stock comparator)", "native_ext": None}
     if args.impl == "dtf":
@@ -434,6 +438,7 @@ def main():
                        "parallelism": (f"dp{world}" if args.strategy == "mirrored" else
                                        f"ps{min(args.num_ps, world)}+dp{world}"),
                        "impl": args.impl, "optimizer": "momentum0.9+wd1e-4, lr 0.1*B/256 warmup500+cosine",
+                       "cudnn_benchmark": bool(args.cudnn_benchmark) if args.impl == "torch" else None,
                        "final_loss": round(final_loss, 4),
                        "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
                        "comm": comm_info, "bucket_mb": args.bucket_mb,
