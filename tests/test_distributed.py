@@ -386,3 +386,15 @@ def test_bench_ps_async_flow_cpu(tmp_path):
     assert cfg["final_global_step"] == 6 and rec["value"] > 0
     assert set(cfg["worker_host_ms_per_step"]) == {"copy_sync_ms_per_step", "wait_ms_per_step",
                                                    "pull_ms_per_step"}
+
+
+@pytest.mark.parametrize("kind,args", [("mirrored", ("bucket_mb=0.05",)),
+                                       ("colocated_ps", ("num_ps=8", "bucket_mb=0.05"))],
+                         ids=["mirrored", "sharded_ps"])
+def test_eight_ranks_match_single_process(tmp_path, kind, args):
+    """The driver's N = 8 layout rehearsed on gloo: 8 ranks (2 images each of the 16-image
+    global batch), many buckets; the sharded parameter server splits every bucket 8 ways."""
+    res = _launch(kind, 8, tmp_path, *args, timeout=300)
+    if kind == "colocated_ps":
+        assert all(r["sharded"] is True for r in res)
+    _assert_replicas(res, _single_process(), atol=5e-6)
