@@ -253,7 +253,33 @@ static TT make_taps(const std::vector<int>& dh, const std::vector<int>& dw) {
   return t;
 }
 
+// rccl_comm.cpp: native RCCL communicator
+int dtf_rccl_load(const std::string& path);
+std::string dtf_rccl_unique_id();
+long dtf_rccl_comm_init(const std::string& uid, int nranks, int rank, int device);
+void dtf_rccl_comm_destroy(long comm, int abort);
+int dtf_rccl_async_error(long comm);
+void dtf_rccl_all_reduce(long comm, long send, long recv, long count, int dtype, int op, long stream);
+void dtf_rccl_reduce_scatter(long comm, long send, long recv, long recvcount, int dtype, int op,
+                             long stream);
+void dtf_rccl_all_gather(long comm, long send, long recv, long sendcount, int dtype, long stream);
+void dtf_rccl_broadcast(long comm, long send, long recv, long count, int dtype, int root, long stream);
+void dtf_rccl_reduce(long comm, long send, long recv, long count, int dtype, int op, int root,
+                     long stream);
+void dtf_rccl_group(int start);
+
 PYBIND11_MODULE(_dtf_hip, m) {
+  m.def("rccl_load", &dtf_rccl_load);
+  m.def("rccl_unique_id", []() { return py::bytes(dtf_rccl_unique_id()); });
+  m.def("rccl_comm_init", &dtf_rccl_comm_init);
+  m.def("rccl_comm_destroy", &dtf_rccl_comm_destroy);
+  m.def("rccl_async_error", &dtf_rccl_async_error);
+  m.def("rccl_all_reduce", &dtf_rccl_all_reduce);
+  m.def("rccl_reduce_scatter", &dtf_rccl_reduce_scatter);
+  m.def("rccl_all_gather", &dtf_rccl_all_gather);
+  m.def("rccl_broadcast", &dtf_rccl_broadcast);
+  m.def("rccl_reduce", &dtf_rccl_reduce);
+  m.def("rccl_group", &dtf_rccl_group);
   m.doc() = "distributedtensorflow_amd HIP/CDNA4 kernels (gfx950)";
 
   m.def("gemm_nt", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, int lda,

@@ -70,8 +70,8 @@ class _ColocatedPSReducer(BucketedAllReduce):
     applies_update = True
 
     def __init__(self, space, owners_ranges, group=None, bucket_bytes=64 << 20,
-                 first_bucket_bytes=4 << 20, sharded=None, overlap_gather=True):
-        super().__init__(space, group, bucket_bytes, first_bucket_bytes)
+                 first_bucket_bytes=4 << 20, sharded=None, overlap_gather=True, comm=None):
+        super().__init__(space, group, bucket_bytes, first_bucket_bytes, comm=comm)
         self.rank = dist.get_rank(group)
         W = self.world
         ok = all((e - s) % W == 0 for s, e, _ in self.buckets) and \
@@ -112,12 +112,10 @@ class _ColocatedPSReducer(BucketedAllReduce):
         if self.sharded:
             s, e, _ = self.buckets[b]
             _, cs, ce = self.pieces[b][self.rank]
-            self.works.append((dist.reduce_scatter_tensor(g[cs:ce], g[s:e], group=self.group,
-                                                          async_op=True), None, None))
+            self.works.append((self.comm.reduce_scatter(g[cs:ce], g[s:e]), None, None))
             return
         for o, s, e in self.pieces[b]:
-            self.works.append((dist.reduce(g[s:e], dst=o, group=self.group,
-                                           async_op=True), None, None))
+            self.works.append((self.comm.reduce(g[s:e], o), None, None))
 
     def grad_scale(self):
         return 1.0 / self.world
@@ -139,11 +137,9 @@ class _ColocatedPSReducer(BucketedAllReduce):
             if self.sharded:
                 s, e, _ = self.buckets[b]
                 _, cs, ce = self.pieces[b][self.rank]
-                works = [dist.all_gather_into_tensor(m[s:e], m[cs:ce], group=self.group,
-                                                     async_op=True)]
+                works = [self.comm.all_gather(m[s:e], m[cs:ce])]
             else:
-                works = [dist.broadcast(m[s:e], src=o, group=self.group, async_op=True)
-                         for o, s, e in self.pieces[b]]
+                works = [self.comm.broadcast(m[s:e], o) for o, s, e in self.pieces[b]]
             self.gpending[b] = works
             self._n_pending += 1
         if self.overlap_gather:
@@ -208,13 +204,21 @@ class _ColocatedPSReducer(BucketedAllReduce):
             for b, (s, e, _) in enumerate(self.buckets):
                 if self.sharded:
                     _, cs, ce = self.pieces[b][self.rank]
-                    dist.all_gather_into_tensor(buf[s:e], buf[cs:ce], group=self.group)
+                    self.comm.all_gather(buf[s:e], buf[cs:ce]).wait()
                 else:
                     for o, ps, pe in self.pieces[b]:
-                        dist.broadcast(buf[ps:pe], src=o, group=self.group)
+                        self.comm.broadcast(buf[ps:pe], o).wait()
 
-    def close(self):
-        self.drain()
+    def close(self, abort=False):
+        """Detach hooks and fences.  ``abort``: the process group broke (a peer died) -- drop
+        the pending variable gathers instead of waiting for them."""
+        if abort:
+            self.gpending = [None] * len(self.buckets)
+            self._n_pending = 0
+            from .. import ops
+            ops.set_param_fence(None)
+        else:
+            self.drain()
         super().close()
         if self._pre_hook is not None:
             self._pre_hook.remove()
@@ -241,7 +245,7 @@ class ParameterServerStrategy(Strategy):
     def __init__(self, cluster_resolver=None, server=None, num_ps=None, sync=None,
                  replicas_to_aggregate=None, variable_placement="balanced", device=None,
                  data_plane=None, bucket_mb=64, first_bucket_mb=4, force_reducer=None,
-                 sharded=None, overlap_gather=True):
+                 sharded=None, overlap_gather=True, comm=None):
         self.server = server
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.first_bucket_bytes = int(first_bucket_mb * (1 << 20))
@@ -251,6 +255,8 @@ class ParameterServerStrategy(Strategy):
         self.force_reducer = force_reducer_default() if force_reducer is None else force_reducer
         self.sharded = sharded
         self.overlap_gather = overlap_gather
+        self.comm_kind = comm
+        self._comm = None
         self._client = None
         if server is not None:
             # between-graph: this process is a worker of a PS cluster
@@ -310,9 +316,12 @@ class ParameterServerStrategy(Strategy):
             return _NullReducer(space)
         ranges = balanced_ranges(space, self.num_ps, list(range(self.num_ps)))
         sharded = (self.num_ps == dist.get_world_size()) and self.sharded is not False
+        if self._comm is None:
+            from .comm import make_comm
+            self._comm = make_comm(self.comm_kind, None, self.device)
         return _ColocatedPSReducer(space, ranges, None, self.bucket_bytes,
                                    self.first_bucket_bytes, sharded=sharded,
-                                   overlap_gather=self.overlap_gather)
+                                   overlap_gather=self.overlap_gather, comm=self._comm)
 
     @property
     def collective(self):
@@ -357,11 +366,17 @@ class ParameterServerStrategy(Strategy):
         and calls :meth:`register_with_ps` again (chief re-initialises the PS; others wait)."""
         if self.mode != "between_graph":
             # colocated owners: the same world re-formation as MirroredStrategy
+            if self._comm is not None:
+                try:
+                    self._comm.close(abort=True)
+                except Exception:
+                    pass
+                self._comm = None
             epoch = rejoin_collective()
             if optimizer is not None and optimizer.space is not None:
                 old = optimizer._reducer
                 if hasattr(old, "close"):
-                    old.close()
+                    old.close(abort=True)
                 optimizer._reducer = self.make_gradient_reducer(optimizer.space)
                 self.broadcast_space(optimizer.space)     # mirrors the restarted rank's build
             return epoch

@@ -161,9 +161,11 @@ class BucketedAllReduce:
     rank count), where an all-reduce run in bf16 would round at every one of the W-1 hops."""
 
     def __init__(self, space, group=None, bucket_bytes=64 << 20, first_bucket_bytes=4 << 20,
-                 average=True, compress_bf16=False, overlap=True):
+                 average=True, compress_bf16=False, overlap=True, comm=None):
+        from .comm import C10dComm
         self.space = space
         self.group = group
+        self.comm = comm if comm is not None else C10dComm(group)
         self.world = dist.get_world_size(group)
         self.average = average
         self.compress = compress_bf16
@@ -210,8 +212,9 @@ class BucketedAllReduce:
             # (caught by tests/test_distributed.py direct_grad_writes), so it is a no-op here.
             v._dtf_grad_ready = None
 
-    def close(self):
+    def close(self, abort=False):
         """Detach the backward hooks (before a re-bucketed reducer replaces this one)."""
+        self.works = []
         for h in self._hooks:
             h.remove()
         self._hooks = []
@@ -240,7 +243,7 @@ class BucketedAllReduce:
             w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
             self.works.append((w, view, (recv, c, L)))
         else:
-            self.works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+            self.works.append((self.comm.all_reduce(view), None, None))
 
     def _finish_compressed(self, view, recv, c, L):
         W = self.world
@@ -501,7 +504,7 @@ class MirroredStrategy(Strategy):
     """
 
     def __init__(self, devices=None, cross_device_ops=None, bucket_mb=64, first_bucket_mb=4,
-                 compress_bf16=False, backend=None, overlap=True, force_reducer=None):
+                 compress_bf16=False, backend=None, overlap=True, force_reducer=None, comm=None):
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
@@ -513,6 +516,8 @@ class MirroredStrategy(Strategy):
         self.first_bucket_bytes = int(first_bucket_mb * (1 << 20))
         self.compress_bf16 = compress_bf16
         self.overlap = overlap
+        self.comm_kind = comm             # "c10d" / "rccl" / None (DTF_COMM, default c10d)
+        self._comm = None
         self.force_reducer = force_reducer_default() if force_reducer is None else force_reducer
         if int(os.environ.get("WORLD_SIZE", "1")) > 1 or self.force_reducer:
             init_process_group_from_env(backend)
@@ -526,11 +531,19 @@ class MirroredStrategy(Strategy):
     def replica_id(self):
         return dist.get_rank() if self._dist else 0
 
+    def communicator(self):
+        """The gradient communicator of this world (created once; see parallel/comm.py)."""
+        if self._comm is None:
+            from .comm import make_comm
+            self._comm = make_comm(self.comm_kind, None, self.device)
+        return self._comm
+
     def make_gradient_reducer(self, space):
         if not self._dist:
             return _NullReducer(space)
         return BucketedAllReduce(space, None, self.bucket_bytes, self.first_bucket_bytes,
-                                 compress_bf16=self.compress_bf16, overlap=self.overlap)
+                                 compress_bf16=self.compress_bf16, overlap=self.overlap,
+                                 comm=None if self.compress_bf16 else self.communicator())
 
     def broadcast_space(self, space):
         if self._dist:
@@ -561,7 +574,7 @@ class MirroredStrategy(Strategy):
         if optimizer is not None and optimizer.space is not None:
             old = optimizer._reducer
             if hasattr(old, "close"):
-                old.close()
+                old.close(abort=True)
             optimizer._reducer = self.make_gradient_reducer(optimizer.space)
             # the restarted replica's Optimizer.build broadcast, mirrored (the collective
             # sequence must be the same on every rank)
