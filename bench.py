@@ -391,6 +391,8 @@ def main():
         comm_info["reducer"] = type(reducer).__name__
         if hasattr(reducer, "sharded"):
             comm_info["sharded_owners"] = bool(reducer.sharded)
+        if hasattr(reducer, "comm"):
+            comm_info["communicator"] = reducer.comm.kind
     comm_info["forced_reducer"] = force
     if args.dump_master and opt_for_stats is not None:
         opt_for_stats.synchronize_variables()

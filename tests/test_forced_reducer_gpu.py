@@ -31,11 +31,11 @@ pytestmark = pytest.mark.gpu
 ARGS = ["--gpus", "1", "--batch", "32", "--image-size", "128", "--steps", "3", "--warmup", "2"]
 
 
-def _bench(tmp_path, name, extra, forced):
+def _bench(tmp_path, name, extra, forced, comm="c10d"):
     from distributedtensorflow_amd.cluster.launcher import free_ports
     dump = tmp_path / f"{name}.pt"
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4",
-               DTF_FORCE_REDUCER="1" if forced else "0")
+               DTF_FORCE_REDUCER="1" if forced else "0", DTF_COMM=comm)
     if forced:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
                "1", "--master-addr", "127.0.0.1", "--master-port", str(free_ports(1)[0]),
@@ -52,20 +52,24 @@ def _bench(tmp_path, name, extra, forced):
     return json.loads(lines[0]), torch.load(dump, weights_only=True)
 
 
-@pytest.mark.parametrize("extra,reducer", [
-    ((), "BucketedAllReduce"),
-    (("--strategy", "ps", "--num-ps", "1"), "_ColocatedPSReducer"),
-    (("--bucket-mb", "16"), "BucketedAllReduce"),
-], ids=["mirrored", "ps_sharded", "mirrored_16mb"])
-def test_forced_reducer_on_rccl_is_bit_identical(tmp_path, extra, reducer):
-    rec, master = _bench(tmp_path, "forced", extra, True)
+@pytest.mark.parametrize("extra,reducer,comm", [
+    ((), "BucketedAllReduce", "c10d"),
+    (("--strategy", "ps", "--num-ps", "1"), "_ColocatedPSReducer", "c10d"),
+    (("--bucket-mb", "16"), "BucketedAllReduce", "c10d"),
+    ((), "BucketedAllReduce", "rccl"),
+    (("--strategy", "ps", "--num-ps", "1"), "_ColocatedPSReducer", "rccl"),
+], ids=["mirrored", "ps_sharded", "mirrored_16mb", "mirrored_native_rccl", "ps_native_rccl"])
+def test_forced_reducer_on_rccl_is_bit_identical(tmp_path, extra, reducer, comm):
+    """``comm=rccl``: the same through the native communicator (csrc/kernels/rccl_comm.cpp)."""
+    rec, master = _bench(tmp_path, "forced", extra, True, comm)
     cfg = rec["config"]
     assert cfg["comm_backend"] == "nccl", cfg
-    comm = cfg["comm"]
-    assert comm["forced_reducer"] is True and comm["reducer"] == reducer, comm
-    assert comm["buckets"] >= 2 and comm["early_launches"] >= 3 * (comm["buckets"] - 1), comm
+    cs = cfg["comm"]
+    assert cs["forced_reducer"] is True and cs["reducer"] == reducer, cs
+    assert cs["buckets"] >= 2 and cs["early_launches"] >= 3 * (cs["buckets"] - 1), cs
+    assert cs["communicator"] == comm, cs
     if reducer == "_ColocatedPSReducer":
-        assert comm["sharded_owners"] is True
+        assert cs["sharded_owners"] is True
     plain_rec, plain = _bench(tmp_path, "plain", extra, False)
     assert plain_rec["config"]["comm_backend"] is None
     assert plain_rec["config"]["comm"].get("reducer") == "_NullReducer"
