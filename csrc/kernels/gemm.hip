@@ -48,6 +48,8 @@ struct GemmArgs {
   int Ho, Wo, osh, osw, oh0, ow0;   // output rows: (n, p*osh + oh0, q*osw + ow0) of [N][Ho][Wo]
   int nt;                           // non-temporal C stores
   int dbg;                          // timing probes (tools/gemm_overhead.py): 1 = skip epilogue
+  int ncu;                          // OCC 2 kernels: compute units (the first resident round)
+  int stagger_mode, stagger;        // OCC 2: which first-round blocks start late, by how much
 };
 
 // chunk swizzle of a [rows][BK] bf16 tile: 16-row ds_read_b128 fragment reads hit 16 slots
@@ -93,9 +95,18 @@ struct GCfg {
 // SCHED 1 (BK 64, NS 2): fragments double-buffered in registers and the barrier moved between
 // the two halves -- the reads of half 1 fly under the MFMAs of half 0, the reads of the next
 // step's half 0 under the MFMAs of half 1, so no wave waits on LDS latency at a phase start.
+//
+// OCC 2 (NW 4, 256 x 128 tiles, BK 32, three 24-KB slots; opt-in variant 12): TWO blocks per
+// CU, each of four 128 x 64 wave tiles -- the same per-wave MFMA / fragment-read work and the
+// same accumulator footprint per SIMD as the 8-wave 256 x 256 kernel, as two independent blocks
+// so that one block's C staging and stores overlap the other block's MFMAs.  A set of the
+// first-round blocks starts late by about half a tile (stagger_mode / stagger) so co-resident
+// blocks do not stay in lockstep.  Bit-identical to variant 8 (same MFMA order per accumulator)
+// but 0.65-0.9x of it: the one-barrier-per-32-deep-step schedule loses more in the main loop
+// than the overlap wins (profiles/measurements/r3_gemm_occ2_and_epilogue_split.jsonl).
 template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1,
-          int CONV = 0>
-__global__ void __launch_bounds__(NW * 64, 1)
+          int CONV = 0, int OCC = 1>
+__global__ void __launch_bounds__(NW * 64, OCC == 2 ? NW * 2 / 4 : 1)
 gemm_nt_kernel(const GemmArgs g) {
   using Cf = GCfg<BM, BN, BK, NS, NW>;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
@@ -110,6 +121,15 @@ gemm_nt_kernel(const GemmArgs g) {
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (g.K + BK - 1) / BK;
+  if constexpr (OCC == 2) {
+    const int b = blockIdx.x;
+    const bool late = b < 2 * g.ncu &&
+        (g.stagger_mode == 1 ? b >= g.ncu
+         : g.stagger_mode == 2 ? ((b >> 3) & 1) != 0
+         : g.stagger_mode == 3 ? (b & 1) != 0 : false);
+    if (late)
+      for (int i = 0; i < g.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
 
   // descriptors based at this block's first row / column: 32-bit offsets span one panel only
   const int rows_a = min(BM, g.M - m0), rows_b = min(BN, g.N - n0);
@@ -1048,19 +1068,34 @@ int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
 int g_gemm_nt = 0;         // non-temporal C stores (ResNet-50 A/B: neutral; off keeps BERT outputs cached)
 int g_gemm_dbg = 0;        // GemmArgs::dbg for timing probes
 
+int g_gemm_stagger_mode = 1, g_gemm_stagger = -1;   // OCC 2 start stagger (-1: auto)
+
 template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1,
-          int CONV = 0>
-void launch_gemm(const GemmArgs& g, hipStream_t st) {
+          int CONV = 0, int OCC = 1>
+void launch_gemm(const GemmArgs& g0, hipStream_t st) {
   using Cf = GCfg<BM, BN, BK, NS, NW>;
   static bool attr = false;
+  static int ncu = 0;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute(
-        (const void*)gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO, CONV>,
+        (const void*)gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO, CONV, OCC>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cf::LDS));
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     attr = true;
   }
+  static_assert(OCC == 1 || 2 * Cf::LDS <= 160 * 1024, "OCC 2: two blocks' LDS per CU");
+  GemmArgs g = g0;
   const long tiles = (long)((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO, CONV>),
+  if (OCC == 2) {
+    g.ncu = ncu;
+    g.stagger_mode = tiles > ncu ? g_gemm_stagger_mode : 0;
+    // about half a tile: ~0.9 us per 32-deep K-step of a 256 x 128 tile with two blocks per
+    // CU; one s_sleep 127 is 8128 cycles (~3.4 us at 2.4 GHz)
+    g.stagger = g_gemm_stagger >= 0 ? g_gemm_stagger : ((g.K + BK - 1) / BK + 7) / 8;
+  }
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NS, SCHED, NW, PP_PRIO, CONV, OCC>),
                      dim3((unsigned)tiles), dim3(Cf::NT), Cf::LDS, st, g);
 }
 
@@ -1070,6 +1105,7 @@ void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
 void dtf_gemm_set_pp(int v) { g_gemm_pp = v; }
 void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
 void dtf_gemm_set_dbg(int v) { g_gemm_dbg = v; }
+void dtf_gemm_set_stagger(int mode, int iters) { g_gemm_stagger_mode = mode; g_gemm_stagger = iters; }
 
 // Implicit-GEMM convolution on the ping-pong GEMM: Y[M = N*P*Q][Kout] (+= Cin / masked acc)
 // = X (through the tap table) . Wt[Kout][Kpad]^T, Kpad = taps * C, C % 64 == 0, <= 9 taps.
@@ -1142,6 +1178,7 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
     case 8: launch_gemm<256, 256, 64, 2, 2>(g, st); break;
     case 9: launch_gemm<256, 256, 64, 2, 2, 8, 0>(g, st); break;
     case 10: launch_gemm<256, 128, 64, 3, 3>(g, st); break;
+    case 12: launch_gemm<256, 128, 32, 3, 0, 4, 1, 0, 2>(g, st); break;
     default: launch_gemm<256, 256, 64, 2>(g, st); break;
   }
 }

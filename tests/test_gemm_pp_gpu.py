@@ -1,5 +1,10 @@
-"""The persistent register-epilogue GEMM (csrc/kernels/gemm.hip gemm_pp_kernel, variant 11)
-against the round-2 ping-pong kernel (variant 8) and an fp32 reference.
+"""The persistent register-epilogue GEMM (csrc/kernels/gemm.hip gemm_pp_kernel, variant 11) and
+the two-blocks-per-CU 256 x 128 kernel (gemm_nt_kernel OCC 2, variant 12) against the round-2
+ping-pong kernel (variant 8) and an fp32 reference.
+
+Variant 12 runs 32-deep K-steps instead of 64-deep ones, but every accumulator still sees the
+same MFMA sequence (k = 0..31, 32..63, ... in order) and the same two-wave-row statistics
+combine, so it is held to the same bit-identity (and is run with its start stagger on).
 
 The new kernel runs the same main loop with the MFMA operands swapped (each lane then holds four
 consecutive output columns) and stores straight from the accumulators, with the LDS-DMA stream
@@ -41,30 +46,32 @@ def _need_gpu():
         pytest.skip("needs a GPU")
 
 
+@pytest.mark.parametrize("variant", [11, 12])
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_pp_matches_pingpong_bitwise(M, N, K):
+def test_pp_matches_pingpong_bitwise(M, N, K, variant):
     n = _native()
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
     bias = torch.randn(N, device="cuda", generator=g)
     ref8 = _run(8, lambda: n.gemm_nt(a, b))
-    out = _run(11, lambda: n.gemm_nt(a, b))
+    out = _run(variant, lambda: n.gemm_nt(a, b))
     assert torch.equal(out, ref8)
     exact = a.float() @ b.float().t()
     err = ((out.float() - exact).norm() / exact.norm()).item()
     assert err < 5e-3, err
     r8 = _run(8, lambda: n.gemm_nt(a, b, bias=bias, relu=True))
-    r11 = _run(11, lambda: n.gemm_nt(a, b, bias=bias, relu=True))
+    r11 = _run(variant, lambda: n.gemm_nt(a, b, bias=bias, relu=True))
     assert torch.equal(r11, r8)
     cin = torch.randn(M, N, device="cuda", generator=g).bfloat16()
     c8 = _run(8, lambda: n.gemm_nt(a, b, cin=cin.clone()))
-    c11 = _run(11, lambda: n.gemm_nt(a, b, cin=cin.clone()))
+    c11 = _run(variant, lambda: n.gemm_nt(a, b, cin=cin.clone()))
     assert torch.equal(c11, c8)
 
 
+@pytest.mark.parametrize("variant", [11, 12])
 @pytest.mark.parametrize("M,N,K", [(4096, 768, 768), (1000, 520, 200), (256 * 300, 512, 512)])
-def test_pp_masked_accumulate_and_bn_stats(M, N, K):
+def test_pp_masked_accumulate_and_bn_stats(M, N, K, variant):
     n = _native()
     g = torch.Generator(device="cuda").manual_seed(7)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
@@ -73,13 +80,13 @@ def test_pp_masked_accumulate_and_bn_stats(M, N, K):
     mask = torch.randint(0, 256, (M * N // 8,), device="cuda", dtype=torch.uint8, generator=g)
     acc = n._MaskedGrad(dy, mask)
     m8 = _run(8, lambda: n.gemm_nt(a, b, acc_from=acc))
-    m11 = _run(11, lambda: n.gemm_nt(a, b, acc_from=acc))
+    m11 = _run(variant, lambda: n.gemm_nt(a, b, acc_from=acc))
     assert torch.equal(m11, m8)
     tiles = n._K.gemm_tile_rows(M)
     s8 = torch.zeros(tiles, 2, N, device="cuda")
     s11 = torch.zeros(tiles, 2, N, device="cuda")
     y8 = _run(8, lambda: n.gemm_nt(a, b, stats=s8))
-    y11 = _run(11, lambda: n.gemm_nt(a, b, stats=s11))
+    y11 = _run(variant, lambda: n.gemm_nt(a, b, stats=s11))
     assert torch.equal(y11, y8)
     torch.testing.assert_close(s11, s8, rtol=1e-5, atol=1e-3)
     yf = y8.float()

@@ -57,6 +57,9 @@ def main():
                     help="comma list of gemm_set_dbg values to time (kernel experiments)")
     ap.add_argument("--variants", default="0",
                     help="comma list of gemm.hip pipeline variants to time (gemm_set_variant)")
+    ap.add_argument("--stagger", default="1:-1",
+                    help="comma list of mode:iters start staggers for the OCC-2 variant 12 "
+                         "(gemm_set_stagger; -1 iters = auto)")
     a = ap.parse_args()
     rows = []
     if a.resnet1x1:
@@ -106,14 +109,17 @@ def main():
         err_lib = float((ref[sub].float() - exact).norm() / exact.norm())
         t_lib = timeit(lambda: torch.nn.functional.linear(A, B), a.iters)
         fl = 2.0 * M * N * K
-        for v, d in [(int(x), int(y)) for x in a.variants.split(",") for y in a.dbg.split(",")]:
+        combos = [(int(x), int(y), st) for x in a.variants.split(",") for y in a.dbg.split(",")
+                  for st in (a.stagger.split(",") if int(x) == 12 else ["1:-1"])]
+        for v, d, st in combos:
             native._K.gemm_set_variant(v)
             native._K.gemm_set_dbg(d)
+            native._K.gemm_set_stagger(*[int(t) for t in st.split(":")])
             ours = native.gemm_nt(A, B)
             err = float((ours[sub].float() - exact).norm() / exact.norm())
             t_ours = timeit(lambda: native.gemm_nt(A, B), a.iters)
             native._K.gemm_set_dbg(0)
-            row = {"shape": name, "variant": v, "dbg": d, "M": M, "N": N, "K": K,
+            row = {"shape": name, "variant": v, "dbg": d, "stagger": st, "M": M, "N": N, "K": K,
                    "ours_us": round(t_ours * 1e6, 1), "hipblaslt_us": round(t_lib * 1e6, 1),
                    "ours_tflops": round(fl / t_ours / 1e12, 1),
                    "hipblaslt_tflops": round(fl / t_lib / 1e12, 1),
@@ -122,6 +128,7 @@ def main():
             rows.append(row)
             print(json.dumps(row), flush=True)
         native._K.gemm_set_variant(-1)
+        native._K.gemm_set_stagger(1, -1)
         del A, B, ours, ref
         torch.cuda.empty_cache()
     if a.out:
