@@ -129,6 +129,7 @@ void dtf_bn_set_nt(int);
 void dtf_conv_set_nt(int);
 void dtf_gemm_set_nt(int);
 void dtf_gemm_set_dbg(int);
+void dtf_gemm_set_stream(int);
 void dtf_gemm_set_stagger(int, int);
 int dtf_wgrad_get_pipe();
 void dtf_lds_probe(int, int, int*, int, hipStream_t);
@@ -666,6 +667,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("conv_set_nt", &dtf_conv_set_nt);
   m.def("gemm_set_nt", &dtf_gemm_set_nt);
   m.def("gemm_set_dbg", &dtf_gemm_set_dbg);
+  m.def("gemm_set_stream", &dtf_gemm_set_stream);
   m.def("gemm_set_stagger", &dtf_gemm_set_stagger);
   m.def("wgrad_get_pipe", &dtf_wgrad_get_pipe);
   m.def("lds_probe", [](int bytes, int blocks, uintptr_t errors, int spin, uintptr_t st) {

@@ -1063,6 +1063,7 @@ void launch_gemm_pp(const GemmArgs& g, hipStream_t st) {
 }
 
 int g_gemm_pp = 0;         // bit 0: persistent register-epilogue kernel for gemm_nt, bit 1: convs
+int g_gemm_stream = 1;     // output-heavy shapes on the row-streaming kernel (gemm_stream.hip)
 
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
 int g_gemm_nt = 0;         // non-temporal C stores (ResNet-50 A/B: neutral; off keeps BERT outputs cached)
@@ -1102,6 +1103,7 @@ void launch_gemm(const GemmArgs& g0, hipStream_t st) {
 }  // namespace
 
 void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
+void dtf_gemm_set_stream(int v) { g_gemm_stream = v; }
 void dtf_gemm_set_pp(int v) { g_gemm_pp = v; }
 void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
 void dtf_gemm_set_dbg(int v) { g_gemm_dbg = v; }
@@ -1141,6 +1143,11 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
   else launch_gemm<256, 256, 64, 2, 2, 8, 1, 1>(g, st);
 }
 
+bool dtf_gemm_stream_ok(int M, int N, int K, int lda, int ldb, int ldc);
+void dtf_gemm_stream(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda,
+                     int ldb, int ldc, const bf16_t* Cin, float* stats, const bf16_t* acc_src,
+                     const uint8_t* acc_mask, int nt, hipStream_t st);
+
 // block-tile rows of every variant (the BatchNorm statistics slab has one row per M tile)
 int dtf_gemm_tile_rows(int M) { return (M + 255) / 256; }
 
@@ -1157,6 +1164,15 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
     throw std::runtime_error("gemm_nt: BN statistics epilogue excludes bias / ReLU / accumulate");
   if (acc_mask && (!acc_src || Cin || ldc != N))
     throw std::runtime_error("gemm_nt: masked accumulation needs acc_src and a dense C");
+  // short K, output at least as wide (N >= K): the row-streaming kernel overlaps each 64-column
+  // chunk's stores with the next chunk's MFMAs (gemm_stream.hip); no bias / ReLU epilogue there
+  const bool stream_ok = !bias && !relu && (stats ? 1 : 0) + (Cin ? 1 : 0) +
+      (acc_mask ? 1 : 0) <= 1 && dtf_gemm_stream_ok(M, N, K, lda, ldb, ldc);
+  if (g_gemm_variant == 13 || (g_gemm_variant < 0 && g_gemm_stream && stream_ok && N >= K)) {
+    if (!stream_ok) throw std::runtime_error("gemm_nt: shape not supported by variant 13");
+    dtf_gemm_stream(A, B, C, M, N, K, lda, ldb, ldc, Cin, stats, acc_src, acc_mask, g_gemm_nt, st);
+    return;
+  }
   GemmArgs g{A, B, C, bias, Cin, M, N, K, lda, ldb, ldc, relu, stats, acc_src, acc_mask};
   g.nt = g_gemm_nt;
   g.dbg = g_gemm_dbg;

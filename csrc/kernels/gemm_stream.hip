@@ -1,0 +1,314 @@
+// Row-streaming GEMM for OUTPUT-HEAVY shapes (short reduction, wide output):
+//   C[M, N] = A[M, K] . B[N, K]^T   (+ BN statistics | + Cin | + acc_src * relu_bit)
+// K in {64, 128, 256}, N % 64 == 0.  In ResNet-50 these are the expanding 1x1 convs (c3: w -> 4w
+// forward) and the data gradients of the reducing ones (c1 of the identity blocks: dgrad w -> 4w):
+// per element of output they do 2K FLOPs but write 2 B, so a tile kernel alternates a short
+// K-loop with a long store phase -- and with one 256 x 256 tile per CU (gemm.hip) or 128 x 128
+// tiles whose K-loop is latency-bound (the register conv kernel) the two phases serialise: both
+// run these shapes at 2-4 TB/s (profiles/measurements/r3_gemm_occ2_and_epilogue_split.jsonl,
+// r2_conv_roofline_b1984.jsonl: 0.48-0.65 of the HBM roof).
+//
+// Design (one block of 8 waves per CU, 256 output rows per block, walking ALL of N):
+//   * each wave owns 32 rows; their A fragments for the whole K (K/4 VGPRs) are loaded ONCE,
+//     straight from HBM into MFMA operand registers -- A is never re-read;
+//   * B (the weights, L2-resident) streams through a 3-slot LDS ring in 64-column chunks by
+//     LDS-DMA (buffer_load ... lds, source-side XOR swizzle: the same conflict-free 64-deep panel
+//     layout as gemm.hip), issued two chunks ahead;
+//   * per chunk: K/32 x 8 v_mfma_f32_16x16x32_bf16 per wave, then the wave stages its 32 x 64
+//     bf16 outputs in a PRIVATE LDS area (no block barrier) and writes them as 16-B row-contiguous
+//     stores (8 rows x 128 B per wave-instruction) -- fire-and-forget: the next chunk's MFMAs
+//     start at once and the stores drain under them.  One block barrier per chunk (ring reuse).
+//   * every lane issues the same number of vector-memory ops per chunk (rows past M get buffer
+//     offsets past the descriptor, dropped by the range check), so the counted vmcnt waits are
+//     exact: the top of chunk c waits only for ITS B chunk, never for the stores of c-1 / c-2.
+//   * BN statistics: per-lane column sums of the bf16-rounded outputs + cross-lane adds; the 8
+//     waves' partials meet in LDS and are summed in fixed order into ONE slab row per block
+//     ([ceil(M / 256)][2][N], the same slab shape as gemm.hip's, so the BN finalize is shared).
+//   * accumulate modes (data gradients): Cin (beta = 1) or the identity-block residual gradient
+//     formed from (dy, ReLU bit mask); the chunk's operands are prefetched one chunk ahead.
+// Per output element the MFMA sequence (k = 0..31, 32..63, ... in order) is the one gemm.hip
+// runs, so C is bit-identical to the ping-pong GEMM (tests/test_gemm_stream_gpu.py).
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kST = 512;      // threads: 8 waves
+constexpr int kSWR = 32;      // rows per wave
+constexpr int kSBM = 256;     // rows per block
+constexpr int kSBN = 64;      // output columns per chunk
+constexpr int kSP = 72;       // staging row pitch (bf16): 144 B, conflict-free fragment writes
+constexpr uint32_t kSOOB = 0x80000000u;
+
+struct StreamArgs {
+  const bf16_t* A; const bf16_t* B; bf16_t* C;
+  const bf16_t* Cin;          // beta = 1 accumulate source ([M][ldc]) or null
+  const bf16_t* acc_src;      // C += acc_src * relu_bit ([M][N], ldc == N) or null
+  const uint8_t* acc_mask;
+  float* stats;               // [ceil(M/256)][2][N] or null
+  int M, N, lda, ldb, ldc;
+  int nt;
+};
+
+DTF_DEV int sswz(int row, int ch) { return ch ^ ((row >> 1) & 7); }   // 64-deep panel swizzle
+
+DTF_DEV __amdgpu_buffer_rsrc_t srsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (scalar branch to a literal)
+DTF_DEV void wait_vm_dyn(int n) {
+  switch (n) {
+#define DTF_VMC(k) case k: DTF_WAIT_VM(k); break;
+    DTF_VMC(0) DTF_VMC(1) DTF_VMC(2) DTF_VMC(3) DTF_VMC(4) DTF_VMC(5) DTF_VMC(6) DTF_VMC(7)
+    DTF_VMC(8) DTF_VMC(9) DTF_VMC(10) DTF_VMC(11) DTF_VMC(12) DTF_VMC(13) DTF_VMC(14)
+    DTF_VMC(15) DTF_VMC(16) DTF_VMC(17) DTF_VMC(18) DTF_VMC(19) DTF_VMC(20) DTF_VMC(21)
+    DTF_VMC(22) DTF_VMC(23) DTF_VMC(24) DTF_VMC(25) DTF_VMC(26) DTF_VMC(27) DTF_VMC(28)
+    DTF_VMC(29) DTF_VMC(30) DTF_VMC(31)
+#undef DTF_VMC
+    default: DTF_WAIT_VM(0); break;
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g) {
+  constexpr int KS = K / 32;                  // MFMA k-steps
+  constexpr int CH = kSBN * K;                // bf16 elements per ring slot
+  constexpr int D = K / 64;                   // LDS-DMA instructions per thread per chunk
+  constexpr int S = kSWR * kSBN * 2 / (64 * 16);   // 16-B stores per lane per chunk (4)
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  bf16_t* stg = lds + 3 * CH;
+  float* sred = reinterpret_cast<float*>(stg + 8 * kSWR * kSP);   // [2][8][2][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+  const long m0 = (long)blockIdx.x * kSBM;
+  const int rows_blk = (int)min((long)kSBM, (long)g.M - m0);
+  const int nch = g.N / kSBN;
+  const bool do_stats = g.stats != nullptr;
+  const int mode = g.Cin ? 1 : (g.acc_mask ? 2 : 0);
+  const int L = mode == 1 ? S : (mode == 2 ? 2 * S : 0);   // prefetch loads per chunk
+
+  // A: this wave's 32 rows x K, straight into MFMA operand registers
+  const __amdgpu_buffer_rsrc_t ra =
+      srsrc(g.A + m0 * g.lda, (uint32_t)(((long)(rows_blk - 1) * g.lda + K) * 2));
+  bf16x8_t af[2][KS];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = wave * kSWR + i * 16 + frow;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const uint32_t off = r < rows_blk ? (uint32_t)((r * g.lda + ks * 32 + fq * 8) * 2) : kSOOB;
+      af[i][ks] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+    }
+  }
+
+  // B chunk c -> ring slot c % 3: DMA instruction q = wave + 8 j fills rows (q % 8) * 8 .. + 7 of
+  // 64-deep panel q / 8; chunks past the end are issued too, out of range (constant counts)
+  const i32x4_t rb = rsrc_quad(g.B, (uint32_t)(((long)(g.N - 1) * g.ldb + K) * 2));
+  const uint32_t lds0 = lds_addr(lds);
+  const int lrow = lane >> 3, slot = lane & 7;
+  auto issue = [&](int c) {
+    const bool live = c < nch;
+    const uint32_t base = lds0 + (uint32_t)((c % 3) * CH) * 2u;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int q = wave + 8 * j, kp = q >> 3, rg = q & 7;
+      const int r = rg * 8 + lrow;
+      const uint32_t off = live ? (uint32_t)(((c * kSBN + r) * g.ldb + kp * 64 + sswz(r, slot) * 8) * 2)
+                                : 0xFFFFFFF0u;
+      dma16(rb, base + (uint32_t)(kp * 64 * 64 + rg * 8 * 64) * 2u, off);
+    }
+  };
+
+  // epilogue addressing: lane -> rows t * 8 + lane / 8 (t < 4) of the wave's 32, 16-B chunk lane % 8
+  const long ldc = g.ldc;
+  const __amdgpu_buffer_rsrc_t rc = srsrc(g.C + m0 * ldc, (uint32_t)(rows_blk * ldc * 2));
+  const __amdgpu_buffer_rsrc_t rcin =
+      srsrc(mode == 1 ? (const void*)(g.Cin + m0 * ldc) : (const void*)(g.acc_src + m0 * ldc),
+            mode ? (uint32_t)(rows_blk * ldc * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t rmask =
+      srsrc(mode == 2 ? (const void*)(g.acc_mask + m0 * ldc / 8) : (const void*)g.C,
+            mode == 2 ? (uint32_t)(rows_blk * ldc / 8) : 0u);
+  const int er = lane >> 3, ec = lane & 7;
+  auto eoff = [&](int t, int c) -> uint32_t {     // byte offset of (row, chunk) in C / Cin
+    const int rr = wave * kSWR + t * 8 + er;
+    return rr < rows_blk ? (uint32_t)((rr * ldc + c * kSBN + ec * 8) * 2) : kSOOB;
+  };
+  uint4 pre[S];
+  uint32_t pmask[S];
+  auto prefetch = [&](int c) {
+    if (mode == 0) return;
+    const int cc = c < nch ? c : 0;
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+      const uint32_t off = eoff(t, cc);
+      pre[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rcin, off, 0, 0));
+      if (mode == 2)
+        pmask[t] = __builtin_amdgcn_raw_buffer_load_b8(rmask, off == kSOOB ? kSOOB : off / 16, 0, 0);
+    }
+  };
+
+  issue(0);
+  issue(1);
+  prefetch(0);
+  bf16_t* ws = stg + wave * kSWR * kSP;
+  const int Lw = L;
+  for (int c = 0; c < nch; ++c) {
+    // this wave's DMAs of chunk c landed (everything issued after them may still fly) ...
+    wait_vm_dyn(c == 0 ? D + Lw : c == 1 ? 2 * Lw + D + S : 2 * S + 2 * Lw + D);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();      // ... every wave's; every wave finished reading chunk c - 1's slot
+    if (do_stats && c > 0 && tid < 2 * kSBN) {
+      const int which = tid >> 6, col = tid & 63;
+      const float* sr = sred + ((c - 1) & 1) * 8 * 2 * kSBN;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) t += sr[(w * 2 + which) * kSBN + col];
+      g.stats[((long)blockIdx.x * 2 + which) * g.N + (c - 1) * kSBN + col] = t;
+    }
+    issue(c + 2);
+    const bf16_t* sb = lds + (c % 3) * CH;
+    f32x4_t acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8_t bf[4];
+      const int kp = ks >> 1, ch = (ks & 1) * 4 + fq;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = j * 16 + frow;
+        bf[j] = *reinterpret_cast<const bf16x8_t*>(sb + kp * 64 * 64 + r * 64 + sswz(r, ch) * 8);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // stage the wave's 32 x 64 bf16 outputs (+ BN statistics from the rounded values)
+    float s1[4], s2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s1[j] = s2[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + fq * 4 + r;
+          const bf16_t h = f2bf(acc[i][j][r]);
+          ws[row * kSP + j * 16 + frow] = h;
+          if (do_stats && wave * kSWR + row < rows_blk) {
+            const float q = bf2f(h);
+            s1[j] += q;
+            s2[j] += q * q;
+          }
+        }
+    if (do_stats) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s1[j] += __shfl_xor(s1[j], 16, 64);
+        s1[j] += __shfl_xor(s1[j], 32, 64);
+        s2[j] += __shfl_xor(s2[j], 16, 64);
+        s2[j] += __shfl_xor(s2[j], 32, 64);
+      }
+      if (fq == 0) {
+        float* sr = sred + (c & 1) * 8 * 2 * kSBN + wave * 2 * kSBN;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sr[j * 16 + frow] = s1[j];
+          sr[kSBN + j * 16 + frow] = s2[j];
+        }
+      }
+    }
+    // the staged tile is read back by other lanes of this wave: keep the reads behind the
+    // writes (one wave's LDS instructions execute in order)
+    asm volatile("" ::: "memory");
+    if (mode) wait_vm_dyn(D);                  // this chunk's prefetched accumulate operands
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+      uint4 v = *reinterpret_cast<const uint4*>(ws + (t * 8 + er) * kSP + ec * 8);
+      if (mode) {
+        float a[8], b[8];
+        unpack8(v, a);
+        unpack8(pre[t], b);
+        if (mode == 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] += b[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] += (pmask[t] >> e) & 1u ? b[e] : 0.f;
+        }
+        v = pack8(a);
+      }
+      const uint32_t off = eoff(t, c);
+      const auto w = __builtin_bit_cast(__attribute__((ext_vector_type(4))) int, v);
+      if (g.nt) __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 2);   // nt
+      else __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 0);
+    }
+    asm volatile("" ::: "memory");            // next chunk's staging writes stay behind these reads
+    prefetch(c + 1);
+  }
+  DTF_WAIT_VM(0);       // the trailing out-of-range DMAs still target the ring
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+  if (do_stats && tid < 2 * kSBN) {
+    const int which = tid >> 6, col = tid & 63, c = nch - 1;
+    const float* sr = sred + (c & 1) * 8 * 2 * kSBN;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t += sr[(w * 2 + which) * kSBN + col];
+    g.stats[((long)blockIdx.x * 2 + which) * g.N + c * kSBN + col] = t;
+  }
+}
+
+template <int K>
+void launch_stream(const StreamArgs& g, hipStream_t st) {
+  constexpr size_t LDS = (size_t)3 * kSBN * K * 2 + (size_t)8 * kSWR * kSP * 2 +
+                         (size_t)2 * 8 * 2 * kSBN * 4;
+  static_assert(LDS <= 160 * 1024, "gemm_stream LDS");
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    attr = true;
+  }
+  const unsigned blocks = (unsigned)((g.M + kSBM - 1) / kSBM);
+  hipLaunchKernelGGL(gemm_stream_kernel<K>, dim3(blocks), dim3(kST), LDS, st, g);
+}
+
+}  // namespace
+
+// true if the row-streaming kernel takes this GEMM (see the header); statistics slab rows are
+// ceil(M / 256), the same as dtf_gemm_tile_rows
+bool dtf_gemm_stream_ok(int M, int N, int K, int lda, int ldb, int ldc) {
+  return (K == 64 || K == 128 || K == 256) && N % kSBN == 0 && N >= kSBN && M > 0 &&
+         lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 && lda >= K && ldb >= K && ldc >= N &&
+         (long)kSBM * lda * 2 < (1L << 31) && (long)kSBM * ldc * 2 < (1L << 31) &&
+         (long)N * ldb * 2 < (1L << 31);
+}
+
+void dtf_gemm_stream(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda,
+                     int ldb, int ldc, const bf16_t* Cin, float* stats, const bf16_t* acc_src,
+                     const uint8_t* acc_mask, int nt, hipStream_t st) {
+  if (!dtf_gemm_stream_ok(M, N, K, lda, ldb, ldc))
+    throw std::runtime_error("gemm_stream: K in {64,128,256}, N % 64 == 0, aligned strides");
+  if ((stats != nullptr) + (Cin != nullptr) + (acc_mask != nullptr) > 1)
+    throw std::runtime_error("gemm_stream: one epilogue mode (stats | Cin | masked acc)");
+  if (acc_mask && (!acc_src || ldc != N))
+    throw std::runtime_error("gemm_stream: masked accumulation needs acc_src and a dense C");
+  StreamArgs g{A, B, C, Cin, acc_src, acc_mask, stats, M, N, lda, ldb, ldc, nt};
+  switch (K) {
+    case 64: launch_stream<64>(g, st); break;
+    case 128: launch_stream<128>(g, st); break;
+    default: launch_stream<256>(g, st); break;
+  }
+}

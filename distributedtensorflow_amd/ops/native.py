@@ -48,6 +48,8 @@ if os.environ.get("DTF_CONV_HALO_FREG"):       # bit f: halo family f streams it
     _K.conv_set_halo_freg(int(os.environ["DTF_CONV_HALO_FREG"]))
 if os.environ.get("DTF_CONV_SMALL_K"):
     _K.conv_set_small_k(int(os.environ["DTF_CONV_SMALL_K"]))
+if os.environ.get("DTF_GEMM_STREAM"):   # row-streaming GEMM for output-heavy shapes (default on)
+    _K.gemm_set_stream(int(os.environ["DTF_GEMM_STREAM"]))
 if os.environ.get("DTF_STORE_NT"):      # non-temporal output stores: bit 0 conv, 1 GEMM, 2 BN
     _nt = int(os.environ["DTF_STORE_NT"])
     _K.conv_set_nt(_nt & 1)
@@ -1028,13 +1030,23 @@ def _gemm_1x1(C, K, R, S, stride, pads):
     output K >= 256, and within noise or slower below: shallow reductions leave the one-block-
     per-CU GEMM's prologue / epilogue exposed, where the conv kernel runs 3-4 blocks per CU
     (profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl, same-box bench A/B)."""
-    return (_CONV_GEMM and R == 1 and S == 1 and tuple(_pair(stride)) == (1, 1)
-            and not any(pads) and C % 64 == 0 and K % 8 == 0 and C >= _GEMM_1X1_MIN_C
-            and K >= 256)
+    if not (_CONV_GEMM and R == 1 and S == 1 and tuple(_pair(stride)) == (1, 1)
+            and not any(pads) and C % 64 == 0 and K % 8 == 0):
+        return False
+    # short reduction, output at least as wide (C in {64, 128, 256}, K >= C): the GEMM dispatch
+    # takes the row-streaming kernel (csrc/kernels/gemm_stream.hip), whose stores drain under
+    # the next chunk's MFMAs: 1.19-1.34x the conv kernel with the BN statistics epilogue at
+    # b1984 (profiles/measurements/r3_gemm_stream_resnet1x1_b1984.jsonl)
+    if _GEMM_STREAM and C in (64, 128, 256) and K >= C and K % 64 == 0:
+        return True
+    return C >= _GEMM_1X1_MIN_C and K >= 256
 
 
 # reduction depth from which a 1x1 conv runs on the GEMM kernel (A/B knob)
 _GEMM_1X1_MIN_C = int(os.environ.get("DTF_GEMM_1X1_MIN_C", "512"))
+# output-heavy 1x1 convs on the row-streaming GEMM (A/B knob; the C++ dispatch has its own
+# switch, gemm_set_stream, for direct gemm_nt calls)
+_GEMM_STREAM = os.environ.get("DTF_GEMM_STREAM", "1") == "1"
 
 
 class _Dense(torch.autograd.Function):

@@ -303,8 +303,10 @@ def test_any_task_killed_is_restarted_and_training_resumes(tmp_path, mnist_dir, 
         assert text["worker0"].count("run main with args") == 2
     from distributedtensorflow_amd.train.checkpoint import latest_checkpoint, load_variable
     last = latest_checkpoint(str(ckpt))
-    assert last.endswith(f"model.ckpt-{int(load_variable(last, 'global_step'))}")
-    assert int(load_variable(last, "global_step")) >= 45
+    # async training: as with TF's CheckpointSaverHook, the file is named by the global step the
+    # chief read, and the other worker may push (advance the step) before the variables are read
+    named, saved = int(last.rsplit("-", 1)[1]), int(load_variable(last, "global_step"))
+    assert named >= 45 and 0 <= saved - named <= 2, (last, saved)
     steps = [int(s) for s in re.findall(r"global step: (\d+)\)", text["worker0"])]
     assert steps and steps[-1] >= 44
 
@@ -363,8 +365,10 @@ def test_ps_killed_mid_run_is_restarted_and_training_resumes(tmp_path, mnist_dir
     assert steps[-1] >= 44           # async: the other worker may take the last step
     from distributedtensorflow_amd.train.checkpoint import latest_checkpoint, load_variable
     last = latest_checkpoint(str(ckpt))
-    assert last.endswith(f"model.ckpt-{int(load_variable(last, 'global_step'))}")
-    assert int(load_variable(last, "global_step")) >= 45
+    # async training: as with TF's CheckpointSaverHook, the file is named by the global step the
+    # chief read, and the other worker may push (advance the step) before the variables are read
+    named, saved = int(last.rsplit("-", 1)[1]), int(load_variable(last, "global_step"))
+    assert named >= 45 and 0 <= saved - named <= 2, (last, saved)
     assert abs(load_variable(last, "conv2d/kernel/Adam")).sum() > 0     # slots survived
 
 

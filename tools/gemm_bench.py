@@ -78,10 +78,21 @@ def main():
             native._CONV_GEMM = False
             t_conv_st = timeit(lambda: native.conv2d(x4, w4, 1, 0, bn_stats=True), a.iters)
             native._CONV_GEMM = True
-            print(json.dumps({"shape": f"resnet1x1_{name}_bnstats", "routed_us":
-                              round(t_route * 1e6, 1), "conv_kernel_us": round(t_conv_st * 1e6, 1),
-                              "speedup": round(t_conv_st / t_route, 3)}), flush=True)
+            rec = {"shape": f"resnet1x1_{name}_bnstats", "routed_us": round(t_route * 1e6, 1),
+                   "conv_kernel_us": round(t_conv_st * 1e6, 1),
+                   "speedup": round(t_conv_st / t_route, 3)}
+            if C in (64, 128, 256) and Kout % 64 == 0:
+                # the row-streaming GEMM with the BN statistics epilogue, forced
+                ws = torch.empty(native._K.gemm_tile_rows(M) * 2 * Kout, device="cuda")
+                native._K.gemm_set_variant(13)
+                t_s = timeit(lambda: native.gemm_nt(x, w, stats=ws), a.iters)
+                native._K.gemm_set_variant(-1)
+                rec["stream_us"] = round(t_s * 1e6, 1)
+                rec["stream_speedup"] = round(t_conv_st / t_s, 3)
+            print(json.dumps(rec), flush=True)
             for v in [int(x) for x in a.variants.split(",")]:
+                if v == 13 and not (C in (64, 128, 256) and Kout % 64 == 0):
+                    continue
                 native._K.gemm_set_variant(v)
                 t_g = timeit(lambda: native.gemm_nt(x, w), a.iters)
                 row = {"shape": f"resnet1x1_{name}", "variant": v, "M": M, "N": Kout, "K": C,
