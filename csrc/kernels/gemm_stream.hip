@@ -58,21 +58,15 @@ DTF_DEV __amdgpu_buffer_rsrc_t srsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform run-time n (scalar branch to a literal)
-DTF_DEV void wait_vm_dyn(int n) {
-  switch (n) {
-#define DTF_VMC(k) case k: DTF_WAIT_VM(k); break;
-    DTF_VMC(0) DTF_VMC(1) DTF_VMC(2) DTF_VMC(3) DTF_VMC(4) DTF_VMC(5) DTF_VMC(6) DTF_VMC(7)
-    DTF_VMC(8) DTF_VMC(9) DTF_VMC(10) DTF_VMC(11) DTF_VMC(12) DTF_VMC(13) DTF_VMC(14)
-    DTF_VMC(15) DTF_VMC(16) DTF_VMC(17) DTF_VMC(18) DTF_VMC(19) DTF_VMC(20) DTF_VMC(21)
-    DTF_VMC(22) DTF_VMC(23) DTF_VMC(24) DTF_VMC(25) DTF_VMC(26) DTF_VMC(27) DTF_VMC(28)
-    DTF_VMC(29) DTF_VMC(30) DTF_VMC(31)
-#undef DTF_VMC
-    default: DTF_WAIT_VM(0); break;
-  }
+// s_waitcnt vmcnt(N), N a compile-time count
+template <int N>
+DTF_DEV void wait_vmc() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int K>
+// MODE: 0 plain, 1 + Cin, 2 + acc_src * relu_bit; STATS: BN statistics slab
+template <int K, int MODE, bool STATS>
 __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g) {
   constexpr int KS = K / 32;                  // MFMA k-steps
   constexpr int CH = kSBN * K;                // bf16 elements per ring slot
@@ -87,9 +81,9 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   const long m0 = (long)blockIdx.x * kSBM;
   const int rows_blk = (int)min((long)kSBM, (long)g.M - m0);
   const int nch = g.N / kSBN;
-  const bool do_stats = g.stats != nullptr;
-  const int mode = g.Cin ? 1 : (g.acc_mask ? 2 : 0);
-  const int L = mode == 1 ? S : (mode == 2 ? 2 * S : 0);   // prefetch loads per chunk
+  constexpr bool do_stats = STATS;
+  constexpr int mode = MODE;
+  constexpr int L = MODE == 1 ? S : (MODE == 2 ? 2 * S : 0);   // prefetch loads per chunk
 
   // A: this wave's 32 rows x K, straight into MFMA operand registers
   const __amdgpu_buffer_rsrc_t ra =
@@ -140,13 +134,13 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   uint4 pre[S];
   uint32_t pmask[S];
   auto prefetch = [&](int c) {
-    if (mode == 0) return;
+    if constexpr (MODE == 0) return;
     const int cc = c < nch ? c : 0;
 #pragma unroll
     for (int t = 0; t < S; ++t) {
       const uint32_t off = eoff(t, cc);
       pre[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rcin, off, 0, 0));
-      if (mode == 2)
+      if constexpr (MODE == 2)
         pmask[t] = __builtin_amdgcn_raw_buffer_load_b8(rmask, off == kSOOB ? kSOOB : off / 16, 0, 0);
     }
   };
@@ -155,10 +149,11 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   issue(1);
   prefetch(0);
   bf16_t* ws = stg + wave * kSWR * kSP;
-  const int Lw = L;
   for (int c = 0; c < nch; ++c) {
     // this wave's DMAs of chunk c landed (everything issued after them may still fly) ...
-    wait_vm_dyn(c == 0 ? D + Lw : c == 1 ? 2 * Lw + D + S : 2 * S + 2 * Lw + D);
+    if (c >= 2) wait_vmc<2 * S + 2 * L + D>();
+    else if (c == 1) wait_vmc<2 * L + D + S>();
+    else wait_vmc<D + L>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();      // ... every wave's; every wave finished reading chunk c - 1's slot
     if (do_stats && c > 0 && tid < 2 * kSBN) {
@@ -232,15 +227,15 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     // the staged tile is read back by other lanes of this wave: keep the reads behind the
     // writes (one wave's LDS instructions execute in order)
     asm volatile("" ::: "memory");
-    if (mode) wait_vm_dyn(D);                  // this chunk's prefetched accumulate operands
+    if constexpr (MODE != 0) wait_vmc<D>();   // this chunk's prefetched accumulate operands
 #pragma unroll
     for (int t = 0; t < S; ++t) {
       uint4 v = *reinterpret_cast<const uint4*>(ws + (t * 8 + er) * kSP + ec * 8);
-      if (mode) {
+      if constexpr (MODE != 0) {
         float a[8], b[8];
         unpack8(v, a);
         unpack8(pre[t], b);
-        if (mode == 1) {
+        if constexpr (MODE == 1) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) a[e] += b[e];
         } else {
@@ -270,19 +265,27 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   }
 }
 
-template <int K>
+template <int K, int MODE, bool STATS>
 void launch_stream(const StreamArgs& g, hipStream_t st) {
   constexpr size_t LDS = (size_t)3 * kSBN * K * 2 + (size_t)8 * kSWR * kSP * 2 +
                          (size_t)2 * 8 * 2 * kSBN * 4;
   static_assert(LDS <= 160 * 1024, "gemm_stream LDS");
   static bool attr = false;
   if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K>,
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
     attr = true;
   }
   const unsigned blocks = (unsigned)((g.M + kSBM - 1) / kSBM);
-  hipLaunchKernelGGL(gemm_stream_kernel<K>, dim3(blocks), dim3(kST), LDS, st, g);
+  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS>), dim3(blocks), dim3(kST), LDS, st, g);
+}
+
+template <int K>
+void launch_stream_k(const StreamArgs& g, hipStream_t st) {
+  if (g.stats) launch_stream<K, 0, true>(g, st);
+  else if (g.Cin) launch_stream<K, 1, false>(g, st);
+  else if (g.acc_mask) launch_stream<K, 2, false>(g, st);
+  else launch_stream<K, 0, false>(g, st);
 }
 
 }  // namespace
@@ -307,8 +310,8 @@ void dtf_gemm_stream(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, 
     throw std::runtime_error("gemm_stream: masked accumulation needs acc_src and a dense C");
   StreamArgs g{A, B, C, Cin, acc_src, acc_mask, stats, M, N, lda, ldb, ldc, nt};
   switch (K) {
-    case 64: launch_stream<64>(g, st); break;
-    case 128: launch_stream<128>(g, st); break;
-    default: launch_stream<256>(g, st); break;
+    case 64: launch_stream_k<64>(g, st); break;
+    case 128: launch_stream_k<128>(g, st); break;
+    default: launch_stream_k<256>(g, st); break;
   }
 }

@@ -57,6 +57,8 @@ def main():
                     help="comma list of gemm_set_dbg values to time (kernel experiments)")
     ap.add_argument("--variants", default="0",
                     help="comma list of gemm.hip pipeline variants to time (gemm_set_variant)")
+    ap.add_argument("--shapes", default=None,
+                    help="extra comma list of MxNxK GEMM shapes (e.g. 388864x1024x256)")
     ap.add_argument("--stagger", default="1:-1",
                     help="comma list of mode:iters start staggers for the OCC-2 variant 12 "
                          "(gemm_set_stagger; -1 iters = auto)")
@@ -108,6 +110,8 @@ def main():
         SHAPES_RUN = []
     else:
         SHAPES_RUN = SHAPES
+    if a.shapes:
+        SHAPES_RUN = [(f"m{sh}", *[int(v) for v in sh.split("x")]) for sh in a.shapes.split(",")]
     for name, M, N, K in SHAPES_RUN:
         if a.only and name not in a.only.split(","):
             continue
