@@ -28,6 +28,9 @@ except ImportError as e:  # pragma: no cover - exercised on boxes without a buil
 
 _BF16 = torch.bfloat16
 _DENSE_IMPL = os.environ.get("DTF_DENSE", "native")     # native | library (hipBLASLt)
+# library-GEMM dense layers (BERT): weight gradients up to this many elements on our TN wgrad
+_DENSE_WGRAD_NATIVE = os.environ.get("DTF_DENSE_WGRAD_NATIVE", "1") == "1"
+_DENSE_WGRAD_NATIVE_MAX = 2304 * 768
 
 # kernel-variant switches for A/B runs on one box (defaults = the measured best)
 if os.environ.get("DTF_WGRAD_MODE"):
@@ -1083,7 +1086,18 @@ class _Dense(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             target = _direct_grad(ctx.w_param)
             S = _wgrad_splits(T, o, i) if (o * i) % 4 == 0 and dy2.dtype == x2.dtype else 1
-            if S == 1:
+            if (_DENSE_WGRAD_NATIVE and dy2.dtype == _BF16 and x2.dtype == _BF16
+                    and o % 8 == 0 and i % 8 == 0 and o * i <= _DENSE_WGRAD_NATIVE_MAX):
+                # the TN conv weight-gradient kernel, fp32 (straight into the flat buffer when
+                # there is one): 1.05-1.40x the split-K library path up to 2304 x 768 (BERT qkv
+                # / attention output / MLM transform), 0.92-0.99x above
+                # (profiles/measurements/r3_bert_dense_wgrad_native_vs_library.jsonl)
+                xw, dw4 = x2.contiguous().view(T, 1, 1, i), dy2.contiguous().view(T, 1, 1, o)
+                if target is not None:
+                    conv2d_wgrad(xw, dw4, (o, 1, 1, i), 1, 0, out=target.view(o, 1, 1, i))
+                else:
+                    dw = conv2d_wgrad(xw, dw4, (o, 1, 1, i), 1, 0).view(o, i)
+            elif S == 1:
                 if target is not None:
                     torch.addmm(target, dy2.t(), x2, out_dtype=torch.float32, out=target)
                 else:
