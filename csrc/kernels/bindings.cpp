@@ -130,6 +130,11 @@ void dtf_conv_set_nt(int);
 void dtf_gemm_set_nt(int);
 void dtf_gemm_set_dbg(int);
 void dtf_gemm_set_stream(int);
+void dtf_gemm_stream_bnb(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int,
+                         const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*,
+                         const float*, const float*, const float*, const float*, const uint8_t*,
+                         int, float*, int, hipStream_t);
+bool dtf_gemm_stream_ok(int, int, int, int, int, int);
 void dtf_gemm_set_stagger(int, int);
 int dtf_wgrad_get_pipe();
 void dtf_lds_probe(int, int, int*, int, hipStream_t);
@@ -668,6 +673,18 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("gemm_set_nt", &dtf_gemm_set_nt);
   m.def("gemm_set_dbg", &dtf_gemm_set_dbg);
   m.def("gemm_set_stream", &dtf_gemm_set_stream);
+  m.def("gemm_stream_ok", &dtf_gemm_stream_ok);
+  m.def("gemm_stream_bnb", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, int lda,
+                              int ldb, int ldc, uintptr_t cin, uintptr_t acc_src, uintptr_t acc_mask,
+                              uintptr_t bx, uintptr_t mean, uintptr_t inv, uintptr_t sc,
+                              uintptr_t sh, uintptr_t bmask, int kind, uintptr_t part,
+                              uintptr_t stream) {
+    dtf_gemm_stream_bnb(P<bf16_t>(a), P<bf16_t>(b), P<bf16_t>(c), M, N, K, lda, ldb, ldc,
+                        P<bf16_t>(cin), P<bf16_t>(acc_src), P<uint8_t>(acc_mask), P<bf16_t>(bx),
+                        P<float>(mean), P<float>(inv), P<float>(sc), P<float>(sh),
+                        P<uint8_t>(bmask), kind, P<float>(part), 0, S(stream));
+    check_launch("gemm_stream_bnb");
+  });
   m.def("gemm_set_stagger", &dtf_gemm_set_stagger);
   m.def("wgrad_get_pipe", &dtf_wgrad_get_pipe);
   m.def("lds_probe", [](int bytes, int blocks, uintptr_t errors, int spin, uintptr_t st) {

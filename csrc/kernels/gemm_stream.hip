@@ -47,9 +47,17 @@ struct StreamArgs {
   const bf16_t* Cin;          // beta = 1 accumulate source ([M][ldc]) or null
   const bf16_t* acc_src;      // C += acc_src * relu_bit ([M][N], ldc == N) or null
   const uint8_t* acc_mask;
-  float* stats;               // [ceil(M/256)][2][N] or null
+  float* stats;               // [ceil(M/256)][2][N] or null (also the BN-backward slab)
   int M, N, lda, ldb, ldc;
   int nt;
+  // BN-backward sums of the BatchNorm whose OUTPUT gradient this GEMM produces (a data gradient):
+  // sum dz, sum dz * (x - mean) * invstd per channel, dz = C * relu_bit, into `stats`
+  const bf16_t* bx;           // that BN's input x ([M][N], dense)
+  const float* bmean;
+  const float* binv;
+  const float* bsc;           // forward scale / shift (ReLU bit recomputed from x, kind 2)
+  const float* bsh;
+  const uint8_t* bmask;       // ReLU bit mask (kind 1)
 };
 
 DTF_DEV int sswz(int row, int ch) { return ch ^ ((row >> 1) & 7); }   // 64-deep panel swizzle
@@ -65,8 +73,9 @@ DTF_DEV void wait_vmc() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// MODE: 0 plain, 1 + Cin, 2 + acc_src * relu_bit; STATS: BN statistics slab
-template <int K, int MODE, bool STATS>
+// MODE: 0 plain, 1 + Cin, 2 + acc_src * relu_bit; STATS: BN statistics slab of the output;
+// BMK >= 0: BN-backward sums of the output (0 no ReLU, 1 ReLU bit mask, 2 ReLU from x)
+template <int K, int MODE, bool STATS, int BMK = -1>
 __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g) {
   constexpr int KS = K / 32;                  // MFMA k-steps
   constexpr int CH = kSBN * K;                // bf16 elements per ring slot
@@ -75,15 +84,31 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   bf16_t* stg = lds + 3 * CH;
   float* sred = reinterpret_cast<float*>(stg + 8 * kSWR * kSP);   // [2][8][2][64]
+  float* bprm = sred + 2 * 8 * 2 * kSBN;                           // BNB: [4][N] mean/inv/sc/sh
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int frow = lane & 15, fq = lane >> 4;
   const long m0 = (long)blockIdx.x * kSBM;
   const int rows_blk = (int)min((long)kSBM, (long)g.M - m0);
   const int nch = g.N / kSBN;
-  constexpr bool do_stats = STATS;
+  constexpr bool BNB = BMK >= 0;
+  static_assert(!(STATS && BNB), "one slab per launch");
+  constexpr bool do_stats = STATS || BNB;
   constexpr int mode = MODE;
-  constexpr int L = MODE == 1 ? S : (MODE == 2 ? 2 * S : 0);   // prefetch loads per chunk
+  // prefetch loads per chunk: the accumulate operands, the BN input, its mask bytes
+  constexpr int L = (MODE == 1 ? S : (MODE == 2 ? 2 * S : 0)) + (BNB ? S : 0) + (BMK == 1 ? S : 0);
+
+  // BNB: this block's copy of the per-channel parameters (one float4 per array per thread:
+  // N <= 2048), written to LDS after the first wait
+  constexpr int NPRM = BMK == 2 ? 4 : 2;
+  float4 prm[NPRM];
+  if constexpr (BNB) {
+    const float* arrs[4] = {g.bmean, g.binv, g.bsc, g.bsh};
+#pragma unroll
+    for (int a = 0; a < NPRM; ++a)
+      prm[a] = tid * 4 < g.N ? *reinterpret_cast<const float4*>(arrs[a] + tid * 4)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 
   // A: this wave's 32 rows x K, straight into MFMA operand registers
   const __amdgpu_buffer_rsrc_t ra =
@@ -131,17 +156,28 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     const int rr = wave * kSWR + t * 8 + er;
     return rr < rows_blk ? (uint32_t)((rr * ldc + c * kSBN + ec * 8) * 2) : kSOOB;
   };
-  uint4 pre[S];
-  uint32_t pmask[S];
+  uint4 pre[S], bxp[S];
+  uint32_t pmask[S], bmp[S];
+  const __amdgpu_buffer_rsrc_t rbx =
+      srsrc(BNB ? (const void*)(g.bx + m0 * ldc) : (const void*)g.C,
+            BNB ? (uint32_t)(rows_blk * ldc * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t rbm =
+      srsrc(BMK == 1 ? (const void*)(g.bmask + m0 * ldc / 8) : (const void*)g.C,
+            BMK == 1 ? (uint32_t)(rows_blk * ldc / 8) : 0u);
   auto prefetch = [&](int c) {
-    if constexpr (MODE == 0) return;
+    if constexpr (MODE == 0 && !BNB) return;
     const int cc = c < nch ? c : 0;
 #pragma unroll
     for (int t = 0; t < S; ++t) {
       const uint32_t off = eoff(t, cc);
-      pre[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rcin, off, 0, 0));
+      if constexpr (MODE != 0)
+        pre[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rcin, off, 0, 0));
       if constexpr (MODE == 2)
         pmask[t] = __builtin_amdgcn_raw_buffer_load_b8(rmask, off == kSOOB ? kSOOB : off / 16, 0, 0);
+      if constexpr (BNB)
+        bxp[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbx, off, 0, 0));
+      if constexpr (BMK == 1)
+        bmp[t] = __builtin_amdgcn_raw_buffer_load_b8(rbm, off == kSOOB ? kSOOB : off / 16, 0, 0);
     }
   };
 
@@ -154,6 +190,12 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     if (c >= 2) wait_vmc<2 * S + 2 * L + D>();
     else if (c == 1) wait_vmc<2 * L + D + S>();
     else wait_vmc<D + L>();
+    if constexpr (BNB) {
+      if (c == 0 && tid * 4 < g.N) {
+#pragma unroll
+        for (int a = 0; a < NPRM; ++a) *reinterpret_cast<float4*>(bprm + a * g.N + tid * 4) = prm[a];
+      }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();      // ... every wave's; every wave finished reading chunk c - 1's slot
     if (do_stats && c > 0 && tid < 2 * kSBN) {
@@ -201,13 +243,13 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
           const int row = i * 16 + fq * 4 + r;
           const bf16_t h = f2bf(acc[i][j][r]);
           ws[row * kSP + j * 16 + frow] = h;
-          if (do_stats && wave * kSWR + row < rows_blk) {
+          if (STATS && wave * kSWR + row < rows_blk) {
             const float q = bf2f(h);
             s1[j] += q;
             s2[j] += q * q;
           }
         }
-    if (do_stats) {
+    if constexpr (STATS) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         s1[j] += __shfl_xor(s1[j], 16, 64);
@@ -227,7 +269,19 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     // the staged tile is read back by other lanes of this wave: keep the reads behind the
     // writes (one wave's LDS instructions execute in order)
     asm volatile("" ::: "memory");
-    if constexpr (MODE != 0) wait_vmc<D>();   // this chunk's prefetched accumulate operands
+    if constexpr (L != 0) wait_vmc<D>();      // this chunk's prefetched epilogue operands
+    float b1[8], b2[8], bmu[8], bis[8], bsc[8], bsh[8];
+    if constexpr (BNB) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b1[e] = b2[e] = 0.f;
+      const int ch0 = c * kSBN + ec * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bmu[e] = bprm[ch0 + e];
+        bis[e] = bprm[g.N + ch0 + e];
+        if constexpr (BMK == 2) { bsc[e] = bprm[2 * g.N + ch0 + e]; bsh[e] = bprm[3 * g.N + ch0 + e]; }
+      }
+    }
 #pragma unroll
     for (int t = 0; t < S; ++t) {
       uint4 v = *reinterpret_cast<const uint4*>(ws + (t * 8 + er) * kSP + ec * 8);
@@ -244,12 +298,48 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
         }
         v = pack8(a);
       }
+      if constexpr (BNB) {
+        if (wave * kSWR + t * 8 + er < rows_blk) {
+          // the BatchNorm backward's reduce, on the gradient exactly as it is stored
+          float gd[8], xv[8];
+          unpack8(v, gd);
+          unpack8(bxp[t], xv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float dz = gd[e];
+            if constexpr (BMK == 1) dz = (bmp[t] >> e) & 1u ? dz : 0.f;
+            if constexpr (BMK == 2) dz = __builtin_fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? dz : 0.f;
+            b1[e] += dz;
+            b2[e] += dz * (xv[e] - bmu[e]) * bis[e];
+          }
+        }
+      }
       const uint32_t off = eoff(t, c);
       const auto w = __builtin_bit_cast(__attribute__((ext_vector_type(4))) int, v);
       if (g.nt) __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 2);   // nt
       else __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 0);
     }
     asm volatile("" ::: "memory");            // next chunk's staging writes stay behind these reads
+    if constexpr (BNB) {
+      // the 8 row lanes sharing a column chunk (lanes ec, ec + 8, ..., ec + 56) meet by
+      // cross-lane adds; lanes 0-7 hold the wave's sums of columns 8 ec .. 8 ec + 7
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        b1[e] += __shfl_xor(b1[e], 8, 64);
+        b1[e] += __shfl_xor(b1[e], 16, 64);
+        b1[e] += __shfl_xor(b1[e], 32, 64);
+        b2[e] += __shfl_xor(b2[e], 8, 64);
+        b2[e] += __shfl_xor(b2[e], 16, 64);
+        b2[e] += __shfl_xor(b2[e], 32, 64);
+      }
+      if (er == 0) {
+        float* sr = sred + (c & 1) * 8 * 2 * kSBN + wave * 2 * kSBN + ec * 8;
+        *reinterpret_cast<float4*>(sr) = make_float4(b1[0], b1[1], b1[2], b1[3]);
+        *reinterpret_cast<float4*>(sr + 4) = make_float4(b1[4], b1[5], b1[6], b1[7]);
+        *reinterpret_cast<float4*>(sr + kSBN) = make_float4(b2[0], b2[1], b2[2], b2[3]);
+        *reinterpret_cast<float4*>(sr + kSBN + 4) = make_float4(b2[4], b2[5], b2[6], b2[7]);
+      }
+    }
     prefetch(c + 1);
   }
   DTF_WAIT_VM(0);       // the trailing out-of-range DMAs still target the ring
@@ -265,24 +355,38 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   }
 }
 
-template <int K, int MODE, bool STATS>
+template <int K, int MODE, bool STATS, int BMK = -1>
 void launch_stream(const StreamArgs& g, hipStream_t st) {
-  constexpr size_t LDS = (size_t)3 * kSBN * K * 2 + (size_t)8 * kSWR * kSP * 2 +
-                         (size_t)2 * 8 * 2 * kSBN * 4;
-  static_assert(LDS <= 160 * 1024, "gemm_stream LDS");
+  constexpr size_t BASE = (size_t)3 * kSBN * K * 2 + (size_t)8 * kSWR * kSP * 2 +
+                          (size_t)2 * 8 * 2 * kSBN * 4;
+  static_assert(BASE <= 160 * 1024, "gemm_stream LDS");
+  // BNB: + the per-channel parameter arrays
+  const size_t LDS = BASE + (BMK >= 0 ? (size_t)(BMK == 2 ? 4 : 2) * g.N * 4 : 0);
+  if (LDS > 160 * 1024) throw std::runtime_error("gemm_stream: BN-backward parameters exceed LDS");
   static bool attr = false;
   if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS, BMK>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const unsigned blocks = (unsigned)((g.M + kSBM - 1) / kSBM);
-  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS>), dim3(blocks), dim3(kST), LDS, st, g);
+  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS, BMK>), dim3(blocks), dim3(kST), LDS, st, g);
+}
+
+template <int K, int MODE>
+void launch_stream_bnb(const StreamArgs& g, int bmk, hipStream_t st) {
+  if (bmk == 1) launch_stream<K, MODE, false, 1>(g, st);
+  else if (bmk == 2) launch_stream<K, MODE, false, 2>(g, st);
+  else launch_stream<K, MODE, false, 0>(g, st);
 }
 
 template <int K>
-void launch_stream_k(const StreamArgs& g, hipStream_t st) {
-  if (g.stats) launch_stream<K, 0, true>(g, st);
+void launch_stream_k(const StreamArgs& g, int bmk, hipStream_t st) {
+  if (g.bx) {
+    if (g.Cin) launch_stream_bnb<K, 1>(g, bmk, st);
+    else if (g.acc_mask) launch_stream_bnb<K, 2>(g, bmk, st);
+    else launch_stream_bnb<K, 0>(g, bmk, st);
+  } else if (g.stats) launch_stream<K, 0, true>(g, st);
   else if (g.Cin) launch_stream<K, 1, false>(g, st);
   else if (g.acc_mask) launch_stream<K, 2, false>(g, st);
   else launch_stream<K, 0, false>(g, st);
@@ -299,6 +403,14 @@ bool dtf_gemm_stream_ok(int M, int N, int K, int lda, int ldb, int ldc) {
          (long)N * ldb * 2 < (1L << 31);
 }
 
+static void run_stream(StreamArgs& g, int K, int bmk, hipStream_t st) {
+  switch (K) {
+    case 64: launch_stream_k<64>(g, bmk, st); break;
+    case 128: launch_stream_k<128>(g, bmk, st); break;
+    default: launch_stream_k<256>(g, bmk, st); break;
+  }
+}
+
 void dtf_gemm_stream(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int lda,
                      int ldb, int ldc, const bf16_t* Cin, float* stats, const bf16_t* acc_src,
                      const uint8_t* acc_mask, int nt, hipStream_t st) {
@@ -309,9 +421,25 @@ void dtf_gemm_stream(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, 
   if (acc_mask && (!acc_src || ldc != N))
     throw std::runtime_error("gemm_stream: masked accumulation needs acc_src and a dense C");
   StreamArgs g{A, B, C, Cin, acc_src, acc_mask, stats, M, N, lda, ldb, ldc, nt};
-  switch (K) {
-    case 64: launch_stream_k<64>(g, st); break;
-    case 128: launch_stream_k<128>(g, st); break;
-    default: launch_stream_k<256>(g, st); break;
-  }
+  run_stream(g, K, -1, st);
+}
+
+// A data-gradient GEMM (plain, Cin or masked accumulate) that also emits the BN-backward sums
+// of the BatchNorm whose output gradient C is: part [ceil(M/256)][2][N] (sum dz, sum dz x-hat).
+// kind: 0 no ReLU, 1 ReLU bit mask `bmask`, 2 ReLU recomputed from x with (bsc, bsh).
+void dtf_gemm_stream_bnb(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K,
+                         int lda, int ldb, int ldc, const bf16_t* Cin, const bf16_t* acc_src,
+                         const uint8_t* acc_mask, const bf16_t* bx, const float* bmean,
+                         const float* binv, const float* bsc, const float* bsh,
+                         const uint8_t* bmask, int kind, float* part, int nt, hipStream_t st) {
+  if (!dtf_gemm_stream_ok(M, N, K, lda, ldb, ldc) || ldc != N || N > 2048)
+    throw std::runtime_error("gemm_stream_bnb: stream shape, dense C, N <= 2048");
+  if (Cin && acc_mask) throw std::runtime_error("gemm_stream_bnb: Cin or masked acc, not both");
+  if (acc_mask && !acc_src) throw std::runtime_error("gemm_stream_bnb: masked acc needs acc_src");
+  if (!bx || !bmean || !binv || !part || kind < 0 || kind > 2 || (kind == 1 && !bmask) ||
+      (kind == 2 && !(bsc && bsh)))
+    throw std::runtime_error("gemm_stream_bnb: BatchNorm operands");
+  StreamArgs g{A, B, C, Cin, acc_src, acc_mask, part, M, N, lda, ldb, ldc, nt,
+               bx, bmean, binv, bsc, bsh, bmask};
+  run_stream(g, K, kind, st);
 }

@@ -222,12 +222,14 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_f
     pt, pb, pl, pr = resolve_padding(padding, h, wd, R, S, stride)
     dx = None
     wflat = w_bf16.reshape(K, R * S, C)
-    if bnb is None and _gemm_1x1(K, C, R, S, stride, (pt, pl)):
+    if _gemm_1x1(K, C, R, S, stride, (pt, pl)) and (bnb is None or _stream_bnb_ok(K, C)):
         # 1x1 stride 1: dX[M, C] = dY[M, K] . Wt[C, K]^T on the GEMM kernel, residual
         # gradients (materialised or masked) folded into its epilogue
         M = n * h * wd
         wt = _dgrad_filter(wflat).view(C, K)
         dyc = dy.contiguous().view(M, K)
+        if bnb is not None:
+            return _dgrad_1x1_bnb(dyc, wt, M, C, K, (n, h, wd, C), out, acc_from, bnb)
         if out is not None:
             o2 = out.view(M, C)
             gemm_nt(dyc, wt, out=o2, cin=o2)
@@ -291,7 +293,40 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_f
         _launch_fwd(dyc, wd_mat.reshape(C, -1), C, taps, Pc, Qc, 1, 1, dx, h, wd, sh, sw, a, b,
                     accumulate=acc, bnb=extra, acc_from=acc_from)
     if part is not None:
-        dx._dtf_bnb_part = (part, G, n * h * wd, C, tok)
+        dx._dtf_bnb_part = (part, G, n * h * wd, C, tok, dx._version)
+    return dx
+
+
+def _stream_bnb_ok(K, C):
+    """The 1x1 data gradient [M, K] x [C, K]^T runs on the row-streaming GEMM (reduction K in
+    {64, 128, 256}, output C >= K), which can also emit the consuming BatchNorm's backward sums."""
+    return _GEMM_STREAM and K in (64, 128, 256) and C >= K and C % 64 == 0 and C <= 2048
+
+
+def _dgrad_1x1_bnb(dyc, wt, M, C, K, xshape, out, acc_from, bnb):
+    """1x1 data gradient on the row-streaming GEMM whose epilogue also reduces the BN backward
+    sums (sum dz, sum dz x-hat) of the BatchNorm that produced x: its separate reduce pass over
+    (dy, x) is skipped (the sums ride on the data gradient still in registers; only x is read)."""
+    xb, stats, mask, relu, has_res, tok = bnb
+    if out is not None and acc_from is not None:
+        out.add_(acc_from.materialize())
+        acc_from = None
+    o2 = out.view(M, C) if out is not None else torch.empty(M, C, device=dyc.device, dtype=_BF16)
+    G = _K.gemm_tile_rows(M)
+    part = torch.empty(_K.bn_workspace_floats_g(G, C), device=dyc.device, dtype=torch.float32)
+    kind = (1 if has_res else 2) if relu else 0
+    _K.gemm_stream_bnb(dyc.data_ptr(), wt.data_ptr(), o2.data_ptr(), M, C, K, K, K, C,
+                       o2.data_ptr() if out is not None else 0,
+                       acc_from.dy.data_ptr() if acc_from is not None else 0,
+                       acc_from.mask.data_ptr() if acc_from is not None else 0,
+                       xb.data_ptr(), stats[0].data_ptr(), stats[1].data_ptr(),
+                       stats[2].data_ptr() if kind == 2 else 0,
+                       stats[3].data_ptr() if kind == 2 else 0,
+                       _p(mask) if kind == 1 else 0, kind, part.data_ptr(), _st())
+    dx = o2.view(xshape)
+    # valid only for this exact gradient: autograd may add another contribution IN PLACE
+    # (a residual gradient summed outside the epilogue), which bumps the version counter
+    dx._dtf_bnb_part = (part, G, M, C, tok, dx._version)
     return dx
 
 
@@ -376,7 +411,12 @@ class _Conv2d(torch.autograd.Function):
         ctx.w_param = w_master
         ctx.x_ref = x            # a residual BN may stash its residual gradient on x
         bnb = getattr(x, "_dtf_bnb", None)
-        ctx.bnb = bnb if (_FUSE_BN_BWD and bnb is not None and xb is x) else None
+        K_, R_, S_, _ = w_master.shape
+        pads = resolve_padding(padding, xb.shape[1], xb.shape[2], R_, S_, stride)
+        stream_bnb = (_FUSE_BN_BWD_STREAM and _gemm_1x1(K_, xb.shape[-1], R_, S_, stride,
+                                                        (pads[0], pads[2]))
+                      and _stream_bnb_ok(K_, xb.shape[-1]))
+        ctx.bnb = bnb if ((_FUSE_BN_BWD or stream_bnb) and bnb is not None and xb is x) else None
         if x.requires_grad and xb is x and wb.is_contiguous():
             _register_dgrad_filter(wb)
         return conv2d_forward(xb, wb, stride, padding, stats)
@@ -521,6 +561,10 @@ _SHARE_INPUT_GRAD = os.environ.get("DTF_SHARE_INPUT_GRAD", "1") == "1"
 # kernels as much time (+3.8 ms/step) as the separate reduce pass it removes (-3.9 ms/step) --
 # the 1x1 dgrads are bandwidth-bound, and the streaming reduce runs at ~5.3 TB/s.
 _FUSE_BN_BWD = os.environ.get("DTF_FUSE_BN_BWD", "0") == "1"
+# ... except where that data gradient runs on the row-streaming GEMM (identity-block c1 convs):
+# there the gradient is still in registers, the epilogue reads only x (prefetched one chunk
+# ahead, streaming), and the reduce pass's re-read of dy and the mask disappears
+_FUSE_BN_BWD_STREAM = os.environ.get("DTF_FUSE_BN_BWD_STREAM", "1") == "1"
 
 
 def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
@@ -718,7 +762,8 @@ def _bn_backward_core(ctx, dy, x, mask, g32, stats, relu=None):
     sc_ptr, sh_ptr = (stats[2].data_ptr(), stats[3].data_ptr()) if mask_x else (0, 0)
     fused = getattr(dy, "_dtf_bnb_part", None)
     tok = getattr(ctx, "bnb_token", None)
-    if fused is not None and tok is not None and fused[4] is tok and fused[2:4] == (M, C):
+    if (fused is not None and tok is not None and fused[4] is tok and fused[2:4] == (M, C)
+            and fused[5] == dy._version):
         # sums already produced by the dgrad epilogue of the conv that consumed y
         part, G = fused[0], fused[1]
     else:

@@ -122,3 +122,94 @@ def test_resnet_output_heavy_1x1_conv_route(C, K):
     dref = torch.nn.functional.conv_transpose2d(dy.float().permute(0, 3, 1, 2),
                                                 w.detach().float().permute(0, 3, 1, 2))
     torch.testing.assert_close(x.grad.float(), dref.permute(0, 2, 3, 1), rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("mode", ["plain", "cin", "masked"])
+@pytest.mark.parametrize("kind", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(1000, 256, 64), (777, 512, 128), (2048, 1024, 256)])
+def test_stream_bn_backward_sums(M, N, K, kind, mode):
+    """gemm_stream_bnb: the data gradient (bit-identical to the ping-pong GEMM with the same
+    accumulate epilogue) plus the BN-backward sums of the BatchNorm whose output it is the
+    gradient of: sum dz and sum dz * (x - mean) * invstd, dz = dx * relu_bit (kind 1: the bit
+    mask, kind 2: recomputed from x with the forward scale / shift), vs fp32 sums."""
+    n = _native()
+    a, b, g = _operands(M, N, K, 11 * K + kind)
+    x = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    mean = torch.randn(N, device="cuda", generator=g) * 0.1
+    inv = torch.rand(N, device="cuda", generator=g) + 0.5
+    sc = torch.rand(N, device="cuda", generator=g) + 0.5
+    sh = torch.randn(N, device="cuda", generator=g) * 0.2
+    bmask = torch.randint(0, 256, (M * N // 8,), device="cuda", dtype=torch.uint8, generator=g)
+    cin = torch.randn(M, N, device="cuda", generator=g).bfloat16() if mode == "cin" else None
+    acc = None
+    if mode == "masked":
+        acc = n._MaskedGrad(torch.randn(M, N, device="cuda", generator=g).bfloat16(),
+                            torch.randint(0, 256, (M * N // 8,), device="cuda", dtype=torch.uint8,
+                                          generator=g))
+    ref8 = _run(8, lambda: n.gemm_nt(a, b, cin=None if cin is None else cin.clone(), acc_from=acc))
+    out = cin.clone() if cin is not None else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    G = n._K.gemm_tile_rows(M)
+    part = torch.full((n._K.bn_workspace_floats_g(G, N),), float("nan"), device="cuda")
+    n._K.gemm_stream_bnb(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, K, K, N,
+                         out.data_ptr() if cin is not None else 0,
+                         acc.dy.data_ptr() if acc else 0, acc.mask.data_ptr() if acc else 0,
+                         x.data_ptr(), mean.data_ptr(), inv.data_ptr(),
+                         sc.data_ptr() if kind == 2 else 0, sh.data_ptr() if kind == 2 else 0,
+                         bmask.data_ptr() if kind == 1 else 0, kind, part.data_ptr(),
+                         torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref8)
+    slab = part[:G * 2 * N].view(G, 2, N)
+    assert not torch.isnan(slab).any()
+    d, xf = out.float(), x.float()
+    if kind == 1:
+        bits = ((bmask.view(-1, 1) >> torch.arange(8, device="cuda", dtype=torch.uint8)) & 1)
+        d = d * bits.view(M, N).float()
+    elif kind == 2:
+        d = d * (xf * sc + sh > 0).float()
+    xhat = (xf - mean) * inv
+    torch.testing.assert_close(slab[:, 0].sum(0), d.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(slab[:, 1].sum(0), (d * xhat).sum(0), rtol=1e-4, atol=2e-2)
+
+
+def test_resnet_block_bn_backward_sums_fused_into_streamed_dgrad():
+    """A residual+ReLU BatchNorm consumed by an identity-style 1x1 conv (w -> 4w reduction, so
+    its data gradient is streamed): the BN backward takes its sums from the dgrad epilogue
+    (spy on the entry point) and the gradients match the unfused pass."""
+    n = _native()
+    torch.manual_seed(3)
+    Nb, H, C, Kc = 4, 14, 256, 64
+    x = torch.randn(Nb, H, H, C, device="cuda").bfloat16()
+    w1 = torch.randn(C, 1, 1, C, device="cuda") / C ** 0.5
+    w2 = torch.randn(Kc, 1, 1, C, device="cuda") / C ** 0.5
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.randn(C, device="cuda") * 0.1
+    r = torch.randn(Nb, H, H, C, device="cuda").bfloat16()
+    outs, calls = [], {"n": 0}
+    orig, prev = n._K.gemm_stream_bnb, n._FUSE_BN_BWD_STREAM
+
+    def spy(*a):
+        calls["n"] += 1
+        return orig(*a)
+    try:
+        for fuse in (True, False):
+            n._FUSE_BN_BWD_STREAM = fuse
+            n._K.gemm_stream_bnb = spy
+            ps = [t.clone().requires_grad_(True) for t in (x.float(), w1, w2, gamma, beta)]
+            xi = ps[0].detach().bfloat16().requires_grad_(True)
+            y1 = n.conv2d(xi, ps[1], 1, 0, bn_stats=True)
+            z = n.batch_norm(y1, ps[3], ps[4], None, None, True, 0.9, 1e-5, relu=True, residual=r)
+            y2 = n.conv2d(z, ps[2], 1, 0)
+            g = torch.randn(y2.shape, device="cuda", generator=torch.Generator(
+                device="cuda").manual_seed(1)).bfloat16()
+            y2.backward(g)
+            outs.append((xi.grad.float(), ps[1].grad, ps[3].grad, ps[4].grad))
+            if fuse:
+                assert calls["n"] == 1, "fused BN-backward path did not run"
+    finally:
+        n._K.gemm_stream_bnb = orig
+        n._FUSE_BN_BWD_STREAM = prev
+    assert calls["n"] == 1
+    for a_, b_ in zip(*outs):
+        rel = ((a_ - b_).norm() / b_.norm()).item()
+        assert rel < 2e-2, rel

@@ -24,10 +24,13 @@ def _inputs(n=4, s=64):
 
 def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False, lazy=True):
     """Gradients of one step.  The fused BN-backward sums (summation order differs from the
-    reduce kernel) stay off unless asked for, so the other fusions can be checked bit-exactly."""
+    reduce kernel; both the register-kernel and the streamed-GEMM forms) stay off unless asked
+    for, so the other fusions can be checked bit-exactly."""
     prev, prev_r, prev_s = native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD, native._SHARE_INPUT_GRAD
     prev_b, prev_l = native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD
+    prev_bs = native._FUSE_BN_BWD_STREAM
     native._FUSE_BN_BWD = fuse_bnb
+    native._FUSE_BN_BWD_STREAM = fuse_bnb
     native._LAZY_RESIDUAL_GRAD = lazy
     native._DIRECT_GRAD = direct
     native._FUSE_RESIDUAL_GRAD = fuse_res
@@ -44,6 +47,7 @@ def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False, lazy=True):
         native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD = prev, prev_r
         native._SHARE_INPUT_GRAD = prev_s
         native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD = prev_b, prev_l
+        native._FUSE_BN_BWD_STREAM = prev_bs
 
 
 def test_direct_grad_path_bit_identical():
