@@ -58,6 +58,12 @@ struct StreamArgs {
   const float* bsc;           // forward scale / shift (ReLU bit recomputed from x, kind 2)
   const float* bsh;
   const uint8_t* bmask;       // ReLU bit mask (kind 1)
+  // PRE: A is the INPUT of a BatchNorm + ReLU (the producing conv's output); the kernel applies
+  // y = bf16(max(x * pre_sc[k] + pre_sh[k], 0)) to its A rows in registers -- exactly the BN
+  // apply pass's arithmetic -- and writes y to `pre_y` (the weight gradient's operand)
+  const float* pre_sc;
+  const float* pre_sh;
+  bf16_t* pre_y;
 };
 
 DTF_DEV int sswz(int row, int ch) { return ch ^ ((row >> 1) & 7); }   // 64-deep panel swizzle
@@ -75,7 +81,7 @@ DTF_DEV void wait_vmc() {
 
 // MODE: 0 plain, 1 + Cin, 2 + acc_src * relu_bit; STATS: BN statistics slab of the output;
 // BMK >= 0: BN-backward sums of the output (0 no ReLU, 1 ReLU bit mask, 2 ReLU from x)
-template <int K, int MODE, bool STATS, int BMK = -1>
+template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false>
 __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g) {
   constexpr int KS = K / 32;                  // MFMA k-steps
   constexpr int CH = kSBN * K;                // bf16 elements per ring slot
@@ -183,13 +189,44 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
 
   issue(0);
   issue(1);
+  constexpr int Y = PRE ? 2 * KS : 0;          // PRE: 16-B stores of the normalised A rows
+  if constexpr (PRE) {
+    // BN + ReLU of the A rows in registers (the loads above and the first chunks' DMAs are in
+    // flight; the scale / shift reads wait for the A rows, in issue order), stored once as the
+    // weight gradient's operand
+    const __amdgpu_buffer_rsrc_t ry =
+        srsrc(g.pre_y + m0 * g.lda, (uint32_t)(((long)(rows_blk - 1) * g.lda + K) * 2));
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k0 = ks * 32 + fq * 8;
+      const float4 s0 = *reinterpret_cast<const float4*>(g.pre_sc + k0);
+      const float4 s1 = *reinterpret_cast<const float4*>(g.pre_sc + k0 + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(g.pre_sh + k0);
+      const float4 h1 = *reinterpret_cast<const float4*>(g.pre_sh + k0 + 4);
+      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float v[8];
+        unpack8(__builtin_bit_cast(uint4, af[i][ks]), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(__builtin_fmaf(v[e], sc[e], sh[e]), 0.f);
+        const uint4 pk = pack8(v);
+        af[i][ks] = __builtin_bit_cast(bf16x8_t, pk);
+        const int r = wave * kSWR + i * 16 + frow;
+        const uint32_t off = r < rows_blk ? (uint32_t)((r * g.lda + k0) * 2) : kSOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) int, pk), ry, off, 0, 0);
+      }
+    }
+  }
   prefetch(0);
   bf16_t* ws = stg + wave * kSWR * kSP;
   for (int c = 0; c < nch; ++c) {
     // this wave's DMAs of chunk c landed (everything issued after them may still fly) ...
     if (c >= 2) wait_vmc<2 * S + 2 * L + D>();
-    else if (c == 1) wait_vmc<2 * L + D + S>();
-    else wait_vmc<D + L>();
+    else if (c == 1) wait_vmc<2 * L + D + S + Y>();
+    else wait_vmc<D + L + Y>();
     if constexpr (BNB) {
       if (c == 0 && tid * 4 < g.N) {
 #pragma unroll
@@ -355,7 +392,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   }
 }
 
-template <int K, int MODE, bool STATS, int BMK = -1>
+template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false>
 void launch_stream(const StreamArgs& g, hipStream_t st) {
   constexpr size_t BASE = (size_t)3 * kSBN * K * 2 + (size_t)8 * kSWR * kSP * 2 +
                           (size_t)2 * 8 * 2 * kSBN * 4;
@@ -365,12 +402,13 @@ void launch_stream(const StreamArgs& g, hipStream_t st) {
   if (LDS > 160 * 1024) throw std::runtime_error("gemm_stream: BN-backward parameters exceed LDS");
   static bool attr = false;
   if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS, BMK>,
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS, BMK, PRE>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const unsigned blocks = (unsigned)((g.M + kSBM - 1) / kSBM);
-  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS, BMK>), dim3(blocks), dim3(kST), LDS, st, g);
+  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS, BMK, PRE>), dim3(blocks), dim3(kST), LDS,
+                     st, g);
 }
 
 template <int K, int MODE>
@@ -382,7 +420,10 @@ void launch_stream_bnb(const StreamArgs& g, int bmk, hipStream_t st) {
 
 template <int K>
 void launch_stream_k(const StreamArgs& g, int bmk, hipStream_t st) {
-  if (g.bx) {
+  if (g.pre_y) {
+    if (g.stats) launch_stream<K, 0, true, -1, true>(g, st);
+    else launch_stream<K, 0, false, -1, true>(g, st);
+  } else if (g.bx) {
     if (g.Cin) launch_stream_bnb<K, 1>(g, bmk, st);
     else if (g.acc_mask) launch_stream_bnb<K, 2>(g, bmk, st);
     else launch_stream_bnb<K, 0>(g, bmk, st);
@@ -442,4 +483,20 @@ void dtf_gemm_stream_bnb(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
   StreamArgs g{A, B, C, Cin, acc_src, acc_mask, part, M, N, lda, ldb, ldc, nt,
                bx, bmean, binv, bsc, bsh, bmask};
   run_stream(g, K, kind, st);
+}
+
+// C = relu(BN(X)) . B^T with the BatchNorm + ReLU applied to the A rows in registers (scale /
+// shift per reduction channel, the BN apply pass's arithmetic) and the normalised rows written
+// to y (same layout as X) for the weight gradient; optional BN statistics of C.  The BN apply
+// pass over X and the GEMM's re-read of its output become one read of X.
+void dtf_gemm_stream_pre(const bf16_t* X, const bf16_t* B, bf16_t* C, int M, int N, int K,
+                         const float* pre_sc, const float* pre_sh, bf16_t* y, float* stats,
+                         hipStream_t st) {
+  if (!dtf_gemm_stream_ok(M, N, K, K, K, N) || !pre_sc || !pre_sh || !y)
+    throw std::runtime_error("gemm_stream_pre: stream shape and BatchNorm operands");
+  StreamArgs g{X, B, C, nullptr, nullptr, nullptr, stats, M, N, K, K, N, 0};
+  g.pre_sc = pre_sc;
+  g.pre_sh = pre_sh;
+  g.pre_y = y;
+  run_stream(g, K, -1, st);
 }

@@ -67,6 +67,9 @@ S2D_STEM = True
 FUSE_STEM_POOL = True
 # projection blocks: shortcut BN fused into the block-output BN (ops.batch_norm_add_batch_norm)
 FUSE_PROJ_BN = os.environ.get("DTF_FUSE_PROJ_BN", "1") == "1"
+# bottleneck c2's BN + ReLU inside c3's GEMM (ops.batch_norm_relu_conv1x1; falls back to the two
+# ops off the streaming route)
+FUSE_BN_CONV = os.environ.get("DTF_FUSE_BN_CONV", "1") == "1"
 
 
 class Bottleneck(nn.Module):
@@ -91,17 +94,29 @@ class Bottleneck(nn.Module):
             p, b = self.proj, self.proj.bn
             sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
                             bn_stats=b.training, grad_share=share)
-            y = self.c2(self.c1(x, grad_share=share))
+            y = self._c2_c3(self.c1(x, grad_share=share))
             c, b3 = self.c3, self.c3.bn
-            y = ops.conv2d(y, c.conv.kernel, c.conv.strides, c.conv.padding, bn_stats=b3.training)
             return ops.batch_norm_add_batch_norm(
                 y, b3.gamma, b3.beta, b3.moving_mean, b3.moving_variance, sc, b.gamma, b.beta,
                 b.moving_mean, b.moving_variance, b3.training, b3.momentum, b3.epsilon)
         sc = self.proj(x, relu=False, grad_share=share) if self.has_proj else x
-        y = self.c1(x, grad_share=share)
-        y = self.c2(y)
+        y = self._c2_c3(self.c1(x, grad_share=share))
         # identity shortcut: c1 (1x1, stride 1) also reads x, so its dgrad absorbs d(residual)
-        return self.c3(y, relu=True, residual=sc, residual_to_conv=not self.has_proj)
+        return self.c3.bn(y, relu=True, residual=sc, residual_to_conv=not self.has_proj)
+
+    def _c2_c3(self, y):
+        """c2 conv -> BN + ReLU -> c3 conv (c3's output, before its BatchNorm).  Training: the
+        BN + ReLU runs inside c3's GEMM (ops.batch_norm_relu_conv1x1) where that GEMM streams."""
+        c2, c3 = self.c2, self.c3
+        if c2.bn.training and FUSE_BN_CONV:
+            y = ops.conv2d(y, c2.conv.kernel, c2.conv.strides, c2.conv.padding, bn_stats=True)
+            b = c2.bn
+            return ops.batch_norm_relu_conv1x1(y, b.gamma, b.beta, b.moving_mean,
+                                               b.moving_variance, c3.conv.kernel, b.momentum,
+                                               b.epsilon)
+        y = c2(y)
+        return ops.conv2d(y, c3.conv.kernel, c3.conv.strides, c3.conv.padding,
+                          bn_stats=c3.bn.training)
 
 
 class ResNet(Layer):

@@ -100,6 +100,18 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
                                 momentum, eps, relu, residual)
 
 
+def batch_norm_relu_conv1x1(x, gamma, beta, running_mean, running_var, w, momentum=0.997,
+                            eps=1e-5):
+    """conv2d(relu(batch_norm(x, training=True)), w) for a 1x1 stride-1 conv.  Native path (when
+    the conv runs on the row-streaming GEMM): one fused op, the BN output is written once by the
+    GEMM instead of by a separate apply pass.  Else the two ops."""
+    if _use_native(x) and _native().bn_relu_conv1x1_ok(x, w):
+        return _native().bn_relu_conv1x1(x, gamma, beta, running_mean, running_var, w, momentum,
+                                         eps)
+    y = batch_norm(x, gamma, beta, running_mean, running_var, True, momentum, eps, relu=True)
+    return conv2d(y, w, 1, 0, bn_stats=True)
+
+
 def batch_norm_add_batch_norm(x, gamma, beta, running_mean, running_var, xp, gamma_p, beta_p,
                               running_mean_p, running_var_p, training=True, momentum=0.997,
                               eps=1e-5):
@@ -280,6 +292,7 @@ def _dispatch(name, fn, fenced):
 
 
 _FENCED = ("conv2d", "conv2d_bias_relu", "batch_norm", "batch_norm_add_batch_norm",
+           "batch_norm_relu_conv1x1",
            "batch_norm_relu_max_pool", "dense", "layer_norm", "bias_dropout_add_layer_norm",
            "embedding_layer_norm", "bias_gelu")
 for _name in _FENCED + ("relu", "max_pool2d", "global_avg_pool", "sparse_softmax_cross_entropy",
@@ -290,7 +303,7 @@ del _name
 
 __all__ = [
     "set_backend", "get_backend", "GradShare", "conv2d", "conv2d_bias_relu", "batch_norm", "relu",
-    "batch_norm_add_batch_norm",
+    "batch_norm_add_batch_norm", "batch_norm_relu_conv1x1",
     "max_pool2d", "global_avg_pool", "dense", "sparse_softmax_cross_entropy",
     "softmax_cross_entropy_clipped_sum", "layer_norm", "gelu", "attention", "dropout",
     "bias_dropout_add_layer_norm", "embedding_layer_norm", "bias_gelu", "attention_qkv",

@@ -812,6 +812,79 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
                             relu, residual, residual_to_conv)
 
 
+class _BnReluConv1x1(torch.autograd.Function):
+    """conv1x1(relu(BN(x)), w) with the BatchNorm + ReLU applied inside the row-streaming GEMM
+    (csrc/kernels/gemm_stream.hip PRE): the GEMM reads x, normalises its A rows in registers with
+    the BN apply pass's exact arithmetic and writes them once as y (the weight gradient's
+    operand) -- the separate apply pass (read x, write y) and the GEMM's read of y become one read
+    of x and one write of y.  Bit-identical to batch_norm(relu) + conv2d.  The output carries its
+    own BN statistics (``_dtf_bn_part``) for the BatchNorm that consumes it.  Backward: the conv's
+    weight / data gradients from y, then the BN backward (ReLU recomputed from x)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, w_master, momentum, eps):
+        x = x.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        stats, g32 = _bn_forward_stats(x, gamma, beta, running_mean, running_var, True,
+                                       momentum, eps)
+        wb = _bf16_weight(w_master)
+        K = wb.shape[0]
+        y = torch.empty_like(x)
+        out = torch.empty(*x.shape[:-1], K, device=x.device, dtype=_BF16)
+        G = _K.gemm_tile_rows(M)
+        part = torch.empty(_K.bn_workspace_floats_g(G, K), device=x.device, dtype=torch.float32)
+        _K.gemm_stream_pre(x.data_ptr(), wb.data_ptr(), out.data_ptr(), M, K, C,
+                           stats[2].data_ptr(), stats[3].data_ptr(), y.data_ptr(),
+                           part.data_ptr(), _st())
+        out._dtf_bn_part = (part, G, M, K)
+        if wb.is_contiguous():
+            _register_dgrad_filter(wb)
+        ctx.save_for_backward(x, y, wb, g32, stats)
+        ctx.w_param, ctx.w_dtype = w_master, w_master.dtype
+        # the BatchNorm-backward core's context
+        ctx.relu, ctx.has_res, ctx.res_ref, ctx.res_slot = True, False, None, None
+        ctx.params = (gamma, beta)
+        ctx.gdt, ctx.bdt = gamma.dtype, beta.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, y, wb, g32, stats = ctx.saved_tensors
+        dout = dout.contiguous()
+        K, _, _, C = wb.shape
+        dw = None
+        target = _direct_grad(ctx.w_param)
+        if target is not None:
+            conv2d_wgrad(y, dout, wb.shape, 1, 0, out=target)
+            _grad_ready(ctx.w_param)
+        else:
+            dw = conv2d_wgrad(y, dout, wb.shape, 1, 0).to(ctx.w_dtype)
+        dy = conv2d_dgrad(dout, wb, y.shape, 1, 0)
+        dx, dg, db, _ = _bn_backward_core(ctx, dy, x, None, g32, stats)
+        ctx.w_param = ctx.params = None
+        return dx, dg, db, None, None, dw, None, None
+
+
+def bn_relu_conv1x1_ok(x, w):
+    """The fused BN + ReLU + 1x1 conv applies: the conv is stream-routed (reduction C in
+    {64, 128, 256}, output K >= C, K % 64 == 0) on a bf16 CUDA tensor."""
+    if not (_FUSE_BN_CONV and _GEMM_STREAM and x.is_cuda and x.dtype == _BF16 and w.dim() == 4):
+        return False
+    K, R, S, C = w.shape
+    return (R == 1 and S == 1 and x.shape[-1] == C and C in (64, 128, 256) and K >= C
+            and K % 64 == 0)
+
+
+def bn_relu_conv1x1(x, gamma, beta, running_mean, running_var, w, momentum=0.997, eps=1e-5):
+    _check_cuda_bf16(x)
+    return _BnReluConv1x1.apply(x, gamma, beta, running_mean, running_var, w, momentum, eps)
+
+
+# BN + ReLU of a bottleneck's c2 output applied inside c3's streaming GEMM (A/B knob)
+_FUSE_BN_CONV = os.environ.get("DTF_FUSE_BN_CONV", "1") == "1"
+
+
 class _BatchNormAddBatchNorm(torch.autograd.Function):
     """relu(BN(x) + BN_p(xp)): a projection block's residual BatchNorm and its shortcut's
     BatchNorm as ONE op.  Forward: one apply pass normalises both conv outputs (the shortcut

@@ -213,3 +213,32 @@ def test_resnet_block_bn_backward_sums_fused_into_streamed_dgrad():
     for a_, b_ in zip(*outs):
         rel = ((a_ - b_).norm() / b_.norm()).item()
         assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 256, 64), (777, 512, 128), (2048, 1024, 256),
+                                   (37, 128, 64)])
+def test_stream_pre_bn_relu_bitwise(M, N, K):
+    """gemm_stream_pre: relu(x * sc + sh) applied to the A rows in registers == the BN apply
+    kernel's output (written back as y) and the GEMM on it, bit for bit; statistics too."""
+    n = _native()
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    sc = torch.rand(K, device="cuda", generator=g) + 0.5
+    sh = torch.randn(K, device="cuda", generator=g) * 0.3
+    y_ref = torch.empty_like(x)
+    n._K.bn_apply(x.data_ptr(), 0, y_ref.data_ptr(), sc.data_ptr(), sh.data_ptr(), M, K, 1,
+                  torch.cuda.current_stream().cuda_stream, 0)
+    G = n._K.gemm_tile_rows(M)
+    s_ref = torch.zeros(G, 2, N, device="cuda")
+    out_ref = _run(13, lambda: n.gemm_nt(y_ref, b, stats=s_ref))
+    y = torch.full_like(x, 7)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    s = torch.zeros(G, 2, N, device="cuda")
+    n._K.gemm_stream_pre(x.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, sc.data_ptr(),
+                         sh.data_ptr(), y.data_ptr(), s.data_ptr(),
+                         torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    assert torch.equal(out, out_ref)
+    assert torch.equal(s, s_ref)

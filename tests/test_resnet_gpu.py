@@ -137,6 +137,35 @@ def test_conv_epilogue_bn_stats_match_separate_pass(shape):
     torch.testing.assert_close(v1, v2, atol=1e-5, rtol=1e-4)
 
 
+def test_bn_relu_conv_fusion_bit_identical():
+    """Bottleneck c2's BN + ReLU applied inside c3's streaming GEMM (ops.batch_norm_relu_conv1x1)
+    == the separate BN apply pass + conv, for the whole ResNet-50 step (loss and every
+    gradient)."""
+    from distributedtensorflow_amd.models import resnet as R
+    torch.manual_seed(0)
+    base = resnet50().cuda()
+    calls = {"n": 0}
+    orig = native._K.gemm_stream_pre
+
+    def spy(*a):
+        calls["n"] += 1
+        return orig(*a)
+    prev = R.FUSE_BN_CONV
+    try:
+        R.FUSE_BN_CONV = True
+        native._K.gemm_stream_pre = spy
+        la, ga = _grads(copy.deepcopy(base), True)
+        native._K.gemm_stream_pre = orig
+        R.FUSE_BN_CONV = False
+        lb, gb = _grads(copy.deepcopy(base), True)
+    finally:
+        R.FUSE_BN_CONV = prev
+        native._K.gemm_stream_pre = orig
+    assert calls["n"] == 13          # c3 of every stage-1..3 bottleneck (w = 64 / 128 / 256)
+    assert la == lb
+    assert torch.equal(ga, gb)
+
+
 def test_residual_grad_fusion_bit_identical():
     """d(residual) accumulated in c1's dgrad epilogue == autograd's separate bf16 add."""
     torch.manual_seed(0)
