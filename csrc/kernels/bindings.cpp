@@ -135,6 +135,7 @@ void dtf_gemm_stream_bnb(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, i
                          const float*, const float*, const float*, const float*, const uint8_t*,
                          int, float*, int, hipStream_t);
 bool dtf_gemm_stream_ok(int, int, int, int, int, int);
+void dtf_gemm_stream_probe(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void dtf_gemm_stream_pre(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, const float*,
                          const float*, bf16_t*, float*, hipStream_t);
 void dtf_gemm_set_stagger(int, int);
@@ -676,6 +677,11 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("gemm_set_dbg", &dtf_gemm_set_dbg);
   m.def("gemm_set_stream", &dtf_gemm_set_stream);
   m.def("gemm_stream_ok", &dtf_gemm_stream_ok);
+  m.def("gemm_stream_probe", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int probe,
+                                uintptr_t stream) {
+    dtf_gemm_stream_probe(P<bf16_t>(a), P<bf16_t>(b), P<bf16_t>(c), M, N, probe, S(stream));
+    check_launch("gemm_stream_probe");
+  });
   m.def("gemm_stream_pre", [](uintptr_t x, uintptr_t b, uintptr_t c, int M, int N, int K,
                               uintptr_t sc, uintptr_t sh, uintptr_t y, uintptr_t stats,
                               uintptr_t stream) {

@@ -81,7 +81,9 @@ DTF_DEV void wait_vmc() {
 
 // MODE: 0 plain, 1 + Cin, 2 + acc_src * relu_bit; STATS: BN statistics slab of the output;
 // BMK >= 0: BN-backward sums of the output (0 no ReLU, 1 ReLU bit mask, 2 ReLU from x)
-template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false>
+// PROBE (timing experiments only, tools/gemm_bench.py --stream-probe): 1 no MFMAs, 2 no LDS
+// staging of C, 4 no chunk barrier, 8 C stores out of range
+template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false, int PROBE = 0>
 __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g) {
   constexpr int KS = K / 32;                  // MFMA k-steps
   constexpr int CH = kSBN * K;                // bf16 elements per ring slot
@@ -234,7 +236,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    raw_barrier();      // ... every wave's; every wave finished reading chunk c - 1's slot
+    if constexpr (!(PROBE & 4)) raw_barrier();   // ... every wave's; every wave finished reading chunk c - 1's slot
     if (do_stats && c > 0 && tid < 2 * kSBN) {
       const int which = tid >> 6, col = tid & 63;
       const float* sr = sred + ((c - 1) & 1) * 8 * 2 * kSBN;
@@ -264,7 +266,8 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[j], acc[i][j], 0, 0, 0);
+          if constexpr (PROBE & 1) asm volatile("" ::"v"(bf[j]), "v"(af[i][ks]));
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
     // stage the wave's 32 x 64 bf16 outputs (+ BN statistics from the rounded values)
@@ -279,7 +282,8 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
         for (int r = 0; r < 4; ++r) {
           const int row = i * 16 + fq * 4 + r;
           const bf16_t h = f2bf(acc[i][j][r]);
-          ws[row * kSP + j * 16 + frow] = h;
+          if constexpr (PROBE & 2) asm volatile("" ::"v"(h));
+          else ws[row * kSP + j * 16 + frow] = h;
           if (STATS && wave * kSWR + row < rows_blk) {
             const float q = bf2f(h);
             s1[j] += q;
@@ -321,7 +325,8 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     }
 #pragma unroll
     for (int t = 0; t < S; ++t) {
-      uint4 v = *reinterpret_cast<const uint4*>(ws + (t * 8 + er) * kSP + ec * 8);
+      uint4 v = (PROBE & 2) ? make_uint4(0u, 0u, 0u, (uint32_t)t)
+                            : *reinterpret_cast<const uint4*>(ws + (t * 8 + er) * kSP + ec * 8);
       if constexpr (MODE != 0) {
         float a[8], b[8];
         unpack8(v, a);
@@ -351,7 +356,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
           }
         }
       }
-      const uint32_t off = eoff(t, c);
+      const uint32_t off = (PROBE & 8) ? kSOOB : eoff(t, c);
       const auto w = __builtin_bit_cast(__attribute__((ext_vector_type(4))) int, v);
       if (g.nt) __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 2);   // nt
       else __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 0);
@@ -392,7 +397,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   }
 }
 
-template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false>
+template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false, int PROBE = 0>
 void launch_stream(const StreamArgs& g, hipStream_t st) {
   constexpr size_t BASE = (size_t)3 * kSBN * K * 2 + (size_t)8 * kSWR * kSP * 2 +
                           (size_t)2 * 8 * 2 * kSBN * 4;
@@ -402,13 +407,13 @@ void launch_stream(const StreamArgs& g, hipStream_t st) {
   if (LDS > 160 * 1024) throw std::runtime_error("gemm_stream: BN-backward parameters exceed LDS");
   static bool attr = false;
   if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS, BMK, PRE>,
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS, BMK, PRE, PROBE>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const unsigned blocks = (unsigned)((g.M + kSBM - 1) / kSBM);
-  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS, BMK, PRE>), dim3(blocks), dim3(kST), LDS,
-                     st, g);
+  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS, BMK, PRE, PROBE>), dim3(blocks), dim3(kST),
+                     LDS, st, g);
 }
 
 template <int K, int MODE>
@@ -499,4 +504,21 @@ void dtf_gemm_stream_pre(const bf16_t* X, const bf16_t* B, bf16_t* C, int M, int
   g.pre_sh = pre_sh;
   g.pre_y = y;
   run_stream(g, K, -1, st);
+}
+
+// timing probes of the plain K = 256 kernel (see PROBE above)
+void dtf_gemm_stream_probe(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int probe,
+                           hipStream_t st) {
+  if (!dtf_gemm_stream_ok(M, N, 256, 256, 256, N)) throw std::runtime_error("stream probe shape");
+  StreamArgs g{A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, 256, 256, N, 0};
+  switch (probe) {
+    case 1: launch_stream<256, 0, false, -1, false, 1>(g, st); break;
+    case 2: launch_stream<256, 0, false, -1, false, 2>(g, st); break;
+    case 4: launch_stream<256, 0, false, -1, false, 4>(g, st); break;
+    case 8: launch_stream<256, 0, false, -1, false, 8>(g, st); break;
+    case 10: launch_stream<256, 0, false, -1, false, 10>(g, st); break;
+    case 11: launch_stream<256, 0, false, -1, false, 11>(g, st); break;
+    case 15: launch_stream<256, 0, false, -1, false, 15>(g, st); break;
+    default: launch_stream<256, 0, false, -1, false, 0>(g, st); break;
+  }
 }
