@@ -23,10 +23,14 @@ constexpr int kThreads = 256;
 
 // rows handled by one block: big enough to amortise the partial slab, small enough to give
 // >= ~1024 blocks on ResNet-50's large layers (M = 256*112*112 = 3.2M rows).
+// target blocks of a statistics / reduce pass (512 is 1-12 % faster in isolation, -2 % in the
+// step: tools/bn_grid_probe.py)
+static int g_bn_stats_blocks = 1024;
+
 inline int stats_grid(long M, int C, int* rows_per_block) {
   const int tpr = C / 8;                        // threads per row
   const int rpi = kThreads / tpr;               // rows per block iteration
-  long target_blocks = 1024;
+  long target_blocks = g_bn_stats_blocks;
   long rpb = (M + target_blocks - 1) / target_blocks;
   rpb = ((rpb + rpi - 1) / rpi) * rpi;
   if (rpb < rpi) rpb = rpi;
@@ -478,11 +482,19 @@ inline void check_rows(long M, int C) {
     throw std::runtime_error("batch_norm: unsupported shape (C % 8, C <= 2048, M*C/8 < 2^31)");
 }
 
-// blocks for a row sweep: enough for ~2 trips of kUnroll rows per lane on the big layers
-inline int sweep_grid(long M, int C) {
+// override of the row-sweep grid caps below (0 = per-kernel defaults; tools/bn_grid_probe.py)
+static int g_bn_grid_cap = 0;
+
+// blocks for a row sweep (grid-stride): up to 8 per CU, at most `cap`.  Isolated sweeps of the
+// ResNet-50 b1984 shapes run 2-12 % faster at 1-2 blocks per CU (tools/bn_grid_probe.py), but
+// inside the training step the same caps moved the BN kernels by -4..+5 % and the step not at
+// all (profiles/measurements/r3_bn_grid_probe_b1984.jsonl), so the caps stay at 8 per CU.
+constexpr int kSweepApply = 2048, kSweepApplyRes = 2048, kSweepBwd = 2048;
+inline int sweep_grid(long M, int C, int cap) {
   const int rpi = kThreads / (C / 8);
   long g = (M + (long)rpi * kUnroll - 1) / ((long)rpi * kUnroll);
-  if (g > 256 * 8) g = 256 * 8;
+  if (g_bn_grid_cap > 0) cap = g_bn_grid_cap;
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;
 }
@@ -577,11 +589,12 @@ void dtf_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, uint8_t* mask,
                   const float* scale, const float* shift, long M, int C, int relu,
                   hipStream_t st) {
   check_rows(M, C);
+  const int cap = res ? kSweepApplyRes : kSweepApply;
   if (g_bn_nt & 1)
-    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, x,
+    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(sweep_grid(M, C, cap)), dim3(kThreads), 0, st, x,
                        res, y, mask, scale, shift, (int)M, C, relu, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(sweep_grid(M, C)), dim3(kThreads), 0, st, x,
+    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(sweep_grid(M, C, cap)), dim3(kThreads), 0, st, x,
                        res, y, mask, scale, shift, (int)M, C, relu, nullptr, nullptr);
 }
 
@@ -592,14 +605,16 @@ void dtf_bn_apply_dual(const bf16_t* x, const bf16_t* xp, bf16_t* y, uint8_t* ma
   check_rows(M, C);
   if (!xp || !pscale || !pshift) throw std::runtime_error("bn_apply_dual: missing operands");
   if (g_bn_nt & 1)
-    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(sweep_grid(M, C)), dim3(kThreads), 0, st,
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(sweep_grid(M, C, kSweepApplyRes)), dim3(kThreads), 0, st,
                        x, xp, y, mask, scale, shift, (int)M, C, relu, pscale, pshift);
   else
-    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(sweep_grid(M, C)), dim3(kThreads), 0,
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(sweep_grid(M, C, kSweepApplyRes)), dim3(kThreads), 0,
                        st, x, xp, y, mask, scale, shift, (int)M, C, relu, pscale, pshift);
 }
 
 void dtf_bn_set_nt(int v) { g_bn_nt = v; }
+void dtf_bn_set_grid_cap(int v) { g_bn_grid_cap = v; }
+void dtf_bn_set_stats_blocks(int v) { g_bn_stats_blocks = v > 0 ? v : 1024; }
 
 void dtf_bn_bwd_reduce(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16_t* x,
                        const float* mean, const float* invstd, long M, int C, int relu,
@@ -663,11 +678,11 @@ void dtf_bn_bwd_apply(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, co
   const int mk = mask_kind(relu, mask, fsc, fsh, y);
 #define DTF_BN_BWD(MK_)                                                                    \
   if (g_bn_nt & 2)                                                                         \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_, true>), dim3(sweep_grid(M, C)), dim3(kThreads), \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_, true>), dim3(sweep_grid(M, C, kSweepBwd)), dim3(kThreads), \
                        0, st, dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh,   \
                        nullptr, nullptr, nullptr, nullptr, nullptr);                        \
   else                                                                                     \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_, false>), dim3(sweep_grid(M, C)), dim3(kThreads), \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<MK_, false>), dim3(sweep_grid(M, C, kSweepBwd)), dim3(kThreads), \
                        0, st, dy, y, mask, x, cA, cB, cC, dx, dres, (int)M, C, mk, fsc, fsh,   \
                        nullptr, nullptr, nullptr, nullptr, nullptr)
   switch (mk) {
@@ -709,11 +724,11 @@ void dtf_bn_bwd_apply_dual(const bf16_t* dy, const uint8_t* mask, const bf16_t* 
   check_rows(M, C);
   if (!mask) throw std::runtime_error("bn_bwd_apply_dual: needs the forward ReLU bit mask");
   if (g_bn_nt & 2)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, true, true>), dim3(sweep_grid(M, C)), dim3(kThreads),
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, true, true>), dim3(sweep_grid(M, C, kSweepBwd)), dim3(kThreads),
                        0, st, dy, nullptr, mask, x, cA, cB, cC, dx, nullptr, (int)M, C, 1, nullptr,
                        nullptr, xp, cAp, cBp, cCp, dxp);
   else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, false, true>), dim3(sweep_grid(M, C)),
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, false, true>), dim3(sweep_grid(M, C, kSweepBwd)),
                        dim3(kThreads), 0, st, dy, nullptr, mask, x, cA, cB, cC, dx, nullptr, (int)M,
                        C, 1, nullptr, nullptr, xp, cAp, cBp, cCp, dxp);
 }

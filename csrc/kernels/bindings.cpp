@@ -126,6 +126,8 @@ void dtf_wgrad_set_pipe(int);
 void dtf_wgrad_set_pp(int);
 void dtf_conv_set_gemm(int);
 void dtf_bn_set_nt(int);
+void dtf_bn_set_grid_cap(int);
+void dtf_bn_set_stats_blocks(int);
 void dtf_conv_set_nt(int);
 void dtf_gemm_set_nt(int);
 void dtf_gemm_set_dbg(int);
@@ -672,6 +674,8 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("wgrad_set_pp", &dtf_wgrad_set_pp);
   m.def("conv_set_gemm", &dtf_conv_set_gemm);
   m.def("bn_set_nt", &dtf_bn_set_nt);
+  m.def("bn_set_grid_cap", &dtf_bn_set_grid_cap);
+  m.def("bn_set_stats_blocks", &dtf_bn_set_stats_blocks);
   m.def("conv_set_nt", &dtf_conv_set_nt);
   m.def("gemm_set_nt", &dtf_gemm_set_nt);
   m.def("gemm_set_dbg", &dtf_gemm_set_dbg);

@@ -53,6 +53,10 @@ if os.environ.get("DTF_CONV_SMALL_K"):
     _K.conv_set_small_k(int(os.environ["DTF_CONV_SMALL_K"]))
 if os.environ.get("DTF_GEMM_STREAM"):   # row-streaming GEMM for output-heavy shapes (default on)
     _K.gemm_set_stream(int(os.environ["DTF_GEMM_STREAM"]))
+if os.environ.get("DTF_BN_GRID_CAP"):     # BN row-sweep grid cap override (2048 = round-2 grids)
+    _K.bn_set_grid_cap(int(os.environ["DTF_BN_GRID_CAP"]))
+if os.environ.get("DTF_BN_STATS_BLOCKS"):  # BN reduce-pass block target (1024 = round-2)
+    _K.bn_set_stats_blocks(int(os.environ["DTF_BN_STATS_BLOCKS"]))
 if os.environ.get("DTF_STORE_NT"):      # non-temporal output stores: bit 0 conv, 1 GEMM, 2 BN
     _nt = int(os.environ["DTF_STORE_NT"])
     _K.conv_set_nt(_nt & 1)
