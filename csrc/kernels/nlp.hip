@@ -21,6 +21,8 @@
 //    regenerates the mask instead of storing it.
 //  * Embedding gather+sum+LN forward, deterministic segment-sum backward for the word table.
 //  * MLM cross-entropy over bf16 logits with per-prediction weights (loss = sum(w*nll)/sum(w)).
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -342,75 +344,91 @@ void col_sum(const float* part, long region, int nq, int P, int N, ColSumOut out
 // enough blocks (the first version used 32 slices: 64 blocks for N = 768, ~0.4 TB/s).
 constexpr int kBf16ColSplits = 256;
 
+// VEC bf16 columns per lane: 8 (16-B loads; N % 8 == 0) or 2 (4-B loads; any even N, e.g. the
+// 30522-wide MLM decoder bias)
+template <int VEC>
 __global__ void __launch_bounds__(256)
 bf16_col_sum_split_kernel(const bf16_t* __restrict__ x, int T, int N, float* __restrict__ ws, int R) {
-  __shared__ float red[4][64][9];
-  const int cv = blockIdx.x * 64 + (threadIdx.x & 63);      // 8-column vector index
+  __shared__ float red[4][64][VEC + 1];
+  const int cv = blockIdx.x * 64 + (threadIdx.x & 63);      // VEC-column vector index
   const int rg = threadIdx.x >> 6;
   const int r0 = blockIdx.y * R, r1 = min(T, r0 + R);
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (cv * 8 < N) {
-    const uint4* X4 = reinterpret_cast<const uint4*>(x) + cv;
-    const long rs = N / 8;
+  float acc[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+  typedef typename std::conditional<VEC == 8, uint4, uint32_t>::type vec_t;
+  auto add = [&](const vec_t& v) {
+    if constexpr (VEC == 8) {
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += f[e];
+    } else {
+      acc[0] += __builtin_bit_cast(float, v << 16);
+      acc[1] += __builtin_bit_cast(float, v & 0xffff0000u);
+    }
+  };
+  if (cv * VEC < N) {
+    const vec_t* X4 = reinterpret_cast<const vec_t*>(x) + cv;
+    const long rs = N / VEC;
     int r = r0 + rg;
     for (; r + 12 < r1; r += 16) {
-      uint4 v[4];
+      vec_t v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) v[u] = X4[(long)(r + 4 * u) * rs];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float f[8];
-        unpack8(v[u], f);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += f[e];
-      }
+      for (int u = 0; u < 4; ++u) add(v[u]);
     }
-    for (; r < r1; r += 4) {
-      float f[8];
-      unpack8(X4[(long)r * rs], f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += f[e];
-    }
+    for (; r < r1; r += 4) add(X4[(long)r * rs]);
   }
 #pragma unroll
-  for (int e = 0; e < 8; ++e) red[rg][threadIdx.x & 63][e] = acc[e];
+  for (int e = 0; e < VEC; ++e) red[rg][threadIdx.x & 63][e] = acc[e];
   __syncthreads();
-  if (rg == 0 && cv * 8 < N) {
+  if (rg == 0 && cv * VEC < N) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < VEC; ++e) {
       float t = red[0][threadIdx.x][e];
 #pragma unroll
       for (int k = 1; k < 4; ++k) t += red[k][threadIdx.x][e];
-      ws[(long)blockIdx.y * N + cv * 8 + e] = t;
+      ws[(long)blockIdx.y * N + cv * VEC + e] = t;
     }
   }
 }
 
-// level 2: 16 float4 columns x 16 slice groups per block, fixed-order combine (+= into out)
+// level 2: 16 column vectors (float4, or single floats when N % 4 != 0) x 16 slice groups per
+// block, fixed-order combine (+= into out)
+template <int W>
 __global__ void __launch_bounds__(256)
 bf16_col_sum_final_kernel(const float* __restrict__ ws, int S, int N, float* __restrict__ out,
                           int accumulate) {
-  __shared__ float4 red[16][16];
+  __shared__ float red[16][16][W];
   const int c4 = blockIdx.x * 16 + (threadIdx.x & 15);
   const int rg = threadIdx.x >> 4;
-  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (c4 * 4 < N)
-    for (int k = rg; k < S; k += 16) {
-      const float4 v = reinterpret_cast<const float4*>(ws + (long)k * N)[c4];
-      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-    }
-  red[rg][threadIdx.x & 15] = t;
-  __syncthreads();
-  if (rg == 0 && c4 * 4 < N) {
-    float4 u = red[0][threadIdx.x];
+  float t[W];
 #pragma unroll
-    for (int k = 1; k < 16; ++k) {
-      const float4 v = red[k][threadIdx.x];
-      u.x += v.x; u.y += v.y; u.z += v.z; u.w += v.w;
+  for (int e = 0; e < W; ++e) t[e] = 0.f;
+  if (c4 * W < N)
+    for (int k = rg; k < S; k += 16) {
+      if constexpr (W == 4) {
+        const float4 v = reinterpret_cast<const float4*>(ws + (long)k * N)[c4];
+        t[0] += v.x; t[1] += v.y; t[2] += v.z; t[3] += v.w;
+      } else {
+        t[0] += ws[(long)k * N + c4];
+      }
     }
-    float4* o = reinterpret_cast<float4*>(out) + c4;
-    if (accumulate) { const float4 v = *o; u.x += v.x; u.y += v.y; u.z += v.z; u.w += v.w; }
-    *o = u;
+#pragma unroll
+  for (int e = 0; e < W; ++e) red[rg][threadIdx.x & 15][e] = t[e];
+  __syncthreads();
+  if (rg == 0 && c4 * W < N) {
+    float u[W];
+#pragma unroll
+    for (int e = 0; e < W; ++e) {
+      u[e] = red[0][threadIdx.x][e];
+#pragma unroll
+      for (int k = 1; k < 16; ++k) u[e] += red[k][threadIdx.x][e];
+      if (accumulate) u[e] += out[c4 * W + e];
+      out[c4 * W + e] = u[e];
+    }
   }
 }
 
@@ -420,13 +438,22 @@ int dtf_bf16_col_sum_ws_floats(int N) { return kBf16ColSplits * N; }
 
 void dtf_bf16_col_sum(const bf16_t* x, int T, int N, float* ws, float* out, int accumulate,
                       hipStream_t st) {
-  if (N % 8) throw std::runtime_error("bf16_col_sum: N % 8 != 0");
+  if (N % 2) throw std::runtime_error("bf16_col_sum: N % 2 != 0");
   int S = T / 64;
   S = S < 1 ? 1 : (S > kBf16ColSplits ? kBf16ColSplits : S);
   const int R = (T + S - 1) / S;
-  hipLaunchKernelGGL(bf16_col_sum_split_kernel, dim3((N / 8 + 63) / 64, S), dim3(256), 0, st, x, T, N, ws, R);
-  hipLaunchKernelGGL(bf16_col_sum_final_kernel, dim3((N / 4 + 15) / 16), dim3(256), 0, st, ws, S,
-                     N, out, accumulate);
+  if (N % 8 == 0)
+    hipLaunchKernelGGL(bf16_col_sum_split_kernel<8>, dim3((N / 8 + 63) / 64, S), dim3(256), 0, st,
+                       x, T, N, ws, R);
+  else
+    hipLaunchKernelGGL(bf16_col_sum_split_kernel<2>, dim3((N / 2 + 63) / 64, S), dim3(256), 0, st,
+                       x, T, N, ws, R);
+  if (N % 4 == 0)
+    hipLaunchKernelGGL(bf16_col_sum_final_kernel<4>, dim3((N / 4 + 15) / 16), dim3(256), 0, st,
+                       ws, S, N, out, accumulate);
+  else
+    hipLaunchKernelGGL(bf16_col_sum_final_kernel<1>, dim3((N + 15) / 16), dim3(256), 0, st, ws, S,
+                       N, out, accumulate);
 }
 
 namespace {
@@ -675,29 +702,6 @@ attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
   if (gq == 0) lse[((long)b * H + h) * S + q] = m + log2f(l);
 }
 
-// delta[b,h,s] = sum_d O * dO  (one thread per (token, head))
-__global__ void __launch_bounds__(256)
-attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
-                  float* __restrict__ delta, int B, int S, int H) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)B * S * H) return;
-  const long tok = i / H;
-  const int h = (int)(i % H);
-  const uint4* o = (const uint4*)(O + tok * H * AD + h * AD);
-  const uint4* d = (const uint4*)(dO + tok * H * AD + h * AD);
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < AD / 8; ++k) {
-    float a[8], c[8];
-    unpack8(o[k], a);
-    unpack8(d[k], c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += a[e] * c[e];
-  }
-  const long b = tok / S, sq = tok % S;
-  delta[(b * H + h) * S + sq] = s;
-}
-
 template <bool DROP, int NW, int CH>
 __global__ void __launch_bounds__(64 * NW)
 attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
@@ -784,7 +788,8 @@ template <bool DROP, int NW, int CH>
 __global__ void __launch_bounds__(64 * NW)
 attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                    const bf16_t* __restrict__ dO, const float* __restrict__ lse,
-                   const float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom g) {
+                   float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom g,
+                   const bf16_t* __restrict__ O) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[CH * ALD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[CH * ALD];
   __shared__ float Ms[CH];
@@ -797,7 +802,27 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mas
   const bf16x8_t bq0 = *(const bf16x8_t*)(qrow + 8 * gq), bq1 = *(const bf16x8_t*)(qrow + 32 + 8 * gq);
   const bf16x8_t bo0 = *(const bf16x8_t*)(orow + 8 * gq), bo1 = *(const bf16x8_t*)(orow + 32 + 8 * gq);
   const long bh = (long)b * H + h;
-  const float lq = lse[bh * S + q], dl = delta[bh * S + q];
+  const float lq = lse[bh * S + q];
+  // delta = O . dO of this lane's query: the 4 lane groups hold 16 of its 64 columns each; the
+  // dK/dV kernel (launched after this one) reads it back
+  float dl;
+  {
+    const bf16_t* oq = O + (tok0 + q) * (long)(H * AD) + h * AD;
+    const uint4 o0 = *(const uint4*)(oq + 8 * gq), o1 = *(const uint4*)(oq + 32 + 8 * gq);
+    float fo[8], fd[8];
+    dl = 0.f;
+    unpack8(o0, fo);
+    unpack8(*(const uint4*)(orow + 8 * gq), fd);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dl += fo[e] * fd[e];
+    unpack8(o1, fo);
+    unpack8(*(const uint4*)(orow + 32 + 8 * gq), fd);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dl += fo[e] * fd[e];
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    if (gq == 0) delta[bh * S + q] = dl;
+  }
   const float c = g.scale * kLog2e;
   const uint32_t kbase = (uint32_t)((bh * S + q) * S);
   f32x4_t dq[4];
@@ -1046,20 +1071,22 @@ static void attn_fwd_launch(const bf16_t* qkv, const float* mask, bf16_t* out, f
 // dK/dV always runs the 4-wave shape: its 8-wave build needs 167 VGPRs with dropout (one block
 // per CU) and measured 8 % slower on BERT-base; dQ gains 10 % from the 8-wave shape.
 template <int NW, int CH>
-static void attn_bwd_launch(const bf16_t* qkv, const float* mask, const bf16_t* dout,
-                            const float* lse, const float* delta, bf16_t* dqkv, const AttnGeom& g,
-                            hipStream_t st) {
+static void attn_bwd_launch(const bf16_t* qkv, const float* mask, const bf16_t* out,
+                            const bf16_t* dout, const float* lse, float* delta, bf16_t* dqkv,
+                            const AttnGeom& g, hipStream_t st) {
+  // dQ first: it also forms delta = O . dO per query (the separate delta pass is gone), which
+  // the dK/dV kernel then reads
   const dim3 grid(g.S / (16 * NW), g.H, g.B), grid4(g.S / 64, g.H, g.B);
   if (g.thr) {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<true, NW, CH>), grid, dim3(64 * NW), 0, st, qkv, mask,
+                       dout, lse, delta, dqkv, g, out);
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<true, 4, 64>), grid4, dim3(256), 0, st, qkv, mask,
                        dout, lse, delta, dqkv, g);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<true, NW, CH>), grid, dim3(64 * NW), 0, st, qkv, mask,
-                       dout, lse, delta, dqkv, g);
   } else {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<false, NW, CH>), grid, dim3(64 * NW), 0, st, qkv,
+                       mask, dout, lse, delta, dqkv, g, out);
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<false, 4, 64>), grid4, dim3(256), 0, st, qkv, mask,
                        dout, lse, delta, dqkv, g);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<false, NW, CH>), grid, dim3(64 * NW), 0, st, qkv,
-                       mask, dout, lse, delta, dqkv, g);
   }
 }
 
@@ -1074,11 +1101,10 @@ void dtf_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* out, const
                   const float* lse, float* delta, bf16_t* dqkv, int B, int S, int H, float scale,
                   float p, uint32_t seed, hipStream_t st) {
   const AttnGeom g = attn_geom(B, S, H, scale, p, seed);
-  const long n = (long)B * S * H;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out,
-                     dout, delta, B, S, H);
-  if (g_attn_wide && S % 128 == 0) attn_bwd_launch<8, 128>(qkv, mask, dout, lse, delta, dqkv, g, st);
-  else attn_bwd_launch<4, 64>(qkv, mask, dout, lse, delta, dqkv, g, st);
+  if (g_attn_wide && S % 128 == 0)
+    attn_bwd_launch<8, 128>(qkv, mask, out, dout, lse, delta, dqkv, g, st);
+  else
+    attn_bwd_launch<4, 64>(qkv, mask, out, dout, lse, delta, dqkv, g, st);
 }
 
 namespace {

@@ -300,7 +300,7 @@ def test_dense_fp32_weight_grads(T, o, i, direct):
 
 
 @pytest.mark.parametrize("T,N", [(16384, 2304), (100, 1024), (7, 8), (65536, 768),
-                                 (65536, 3072), (1000, 776)])
+                                 (65536, 3072), (1000, 776), (10240, 30522), (33, 6), (5, 30)])
 def test_bf16_col_sum(T, N):
     nat = _native()
     x = torch.randn(T, N, device=dev).to(torch.bfloat16)

@@ -324,3 +324,4 @@ def test_bert_fused_grad_paths_match_autograd():
     cos = torch.nn.functional.cosine_similarity(ga.double(), gb.double(), dim=0).item()
     assert cos > 0.9999, cos              # GEMM beta=1 rounds once instead of twice
     assert (ga - gb).abs().max() <= 0.02 * gb.abs().max()
+
