@@ -66,6 +66,21 @@ class _Task:
         return f"{self.job}{self.index}"
 
 
+def _dump_stacks(tasks):
+    """Ask every live task for a Python stack dump into its log (SIGUSR1: the entry scripts
+    register faulthandler for it) before a timed-out job is torn down, so a hang is diagnosable
+    from the logs alone."""
+    import signal
+    live = [t for t in tasks if t.proc.poll() is None]
+    for t in live:
+        try:
+            os.kill(t.proc.pid, signal.SIGUSR1)
+        except OSError:
+            pass
+    if live:
+        time.sleep(1.0)
+
+
 def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script):
     """Wait for the worker tasks, restarting failed tasks meanwhile.
 
@@ -112,6 +127,7 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script):
             if not failed or used >= max_restarts or any(t.done for t in workers):
                 return
         if time.time() - t0 > timeout_s:
+            _dump_stacks(tasks)
             raise subprocess.TimeoutExpired(script, timeout_s)
         time.sleep(0.1)
 

@@ -19,7 +19,9 @@ from __future__ import annotations
 
 import argparse
 import datetime
+import faulthandler
 import os
+import signal
 import sys
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -188,5 +190,8 @@ def parse(argv=None):
 
 
 if __name__ == "__main__":
+    # `kill -USR1 <pid>` (the launcher does it before tearing down a timed-out job) writes every
+    # thread's Python stack into this task's log
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
     FLAGS = parse()
     main()
