@@ -174,6 +174,8 @@ void dtf_mlm_xent(const bf16_t*, const int64_t*, const float*, const float*, int
                   bf16_t*, hipStream_t);
 
 // ---- dense GEMM (gemm.hip)
+void dtf_gemm_nt_gelu_bwd(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int,
+                          const bf16_t*, const float*, float*, hipStream_t);
 void dtf_gemm_nt(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int,
                  const float*, const bf16_t*, int, float*, hipStream_t, const bf16_t*,
                  const uint8_t*);
@@ -305,6 +307,13 @@ PYBIND11_MODULE(_dtf_hip, m) {
      py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("bias"), py::arg("cin"),
      py::arg("relu"), py::arg("stream"), py::arg("stats") = 0, py::arg("acc_src") = 0,
      py::arg("acc_mask") = 0);
+  m.def("gemm_nt_gelu_bwd", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K,
+                               int lda, int ldb, uintptr_t gelu_a, uintptr_t gelu_b,
+                               uintptr_t colsum, uintptr_t st) {
+    dtf_gemm_nt_gelu_bwd(P<bf16_t>(a), P<bf16_t>(b), P<bf16_t>(c), M, N, K, lda, ldb,
+                         P<bf16_t>(gelu_a), P<float>(gelu_b), P<float>(colsum), S(st));
+    check_launch("gemm_nt_gelu_bwd");
+  });
   m.def("gemm_tile_rows", &dtf_gemm_tile_rows);
   m.def("gemm_set_variant", &dtf_gemm_set_variant);
   m.def("gemm_set_pp", &dtf_gemm_set_pp);

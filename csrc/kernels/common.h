@@ -106,6 +106,25 @@ DTF_DEV void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// ---- GELU (tanh approximation, BERT's "gelu") shared by the NLP kernels and the GEMM epilogue
+constexpr float kGeluK0 = 0.7978845608028654f;   // sqrt(2/pi)
+constexpr float kGeluK1 = 0.044715f;
+
+// tanh(u) = 1 - 2 / (1 + e^{2u}) on v_exp_f32 / v_rcp_f32 (libm tanhf is a long branchy
+// sequence; the absolute error here is ~1e-7, far below the bf16 output rounding)
+DTF_DEV float tanh_fast(float u) {
+  const float e = __builtin_amdgcn_exp2f(u * 2.885390081777927f);   // 2 log2(e)
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
+}
+DTF_DEV float gelu_f(float x) {
+  const float t = tanh_fast(kGeluK0 * (x + kGeluK1 * x * x * x));
+  return 0.5f * x * (1.f + t);
+}
+DTF_DEV float gelu_grad(float x) {
+  const float t = tanh_fast(kGeluK0 * (x + kGeluK1 * x * x * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluK0 * (1.f + 3.f * kGeluK1 * x * x);
+}
+
 
 #define HIP_CHECK(x)                                                               \
   do {                                                                             \

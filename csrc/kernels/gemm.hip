@@ -48,6 +48,12 @@ struct GemmArgs {
   int Ho, Wo, osh, osw, oh0, ow0;   // output rows: (n, p*osh + oh0, q*osw + ow0) of [N][Ho][Wo]
   int nt;                           // non-temporal C stores
   int dbg;                          // timing probes (tools/gemm_overhead.py): 1 = skip epilogue
+  // GELU-backward epilogue (a data gradient feeding a GELU, BERT's FFN): C = acc * gelu'(a + b)
+  // with a [M][ldc] the GELU's saved input and b [N] its bias; colsum [tiles_m][N] receives the
+  // per-tile column sums of C in fp32 (the bias gradient's first level)
+  const bf16_t* gelu_a;
+  const float* gelu_b;
+  float* colsum;
   int ncu;                          // OCC 2 kernels: compute units (the first resident round)
   int stagger_mode, stagger;        // OCC 2: which first-round blocks start late, by how much
 };
@@ -622,6 +628,12 @@ gemm_nt_kernel(const GemmArgs g) {
   constexpr int OROWS = Cf::NT / OCPR;
   const int oc = tid % OCPR;
   const bool col_ok = n0 + oc * 8 < g.N;
+  float gb[8], cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    gb[e] = (g.gelu_b && col_ok) ? g.gelu_b[n0 + oc * 8 + e] : 0.f;
+    cs[e] = 0.f;
+  }
 #pragma unroll 4
   for (int k = 0; k < BM / OROWS; ++k) {
     const int r = tid / OCPR + k * OROWS;
@@ -652,8 +664,34 @@ gemm_nt_kernel(const GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += (mb >> e) & 1u ? b[e] : 0.f;
       v = pack8(a);
+    } else if (g.gelu_a) {
+      float d[8], a[8];
+      unpack8(v, d);
+      unpack8(*reinterpret_cast<const uint4*>(g.gelu_a + off), a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        d[e] *= gelu_grad(a[e] + gb[e]);
+        cs[e] += d[e];
+      }
+      v = pack8(d);
     }
     st16(g.C + off, v, g.nt);
+  }
+  if (g.colsum) {
+    // the OROWS threads of a column chunk meet in LDS (the staged tile is dead after a barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);                 // [OROWS][BN]
+    const int rg = tid / OCPR;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[rg * BN + oc * 8 + e] = cs[e];
+    __syncthreads();
+    if (tid < BN && n0 + tid < g.N) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < OROWS; ++j) t += red[j * BN + tid];
+      g.colsum[(long)tm * g.N + n0 + tid] = t;
+    }
   }
 }
 
@@ -1141,6 +1179,25 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
   if (Kout <= 128) launch_gemm<256, 128, 64, 3, 3, 8, 1, 1>(g, st);
   else if ((g_gemm_pp & 2) && (g.K + 63) / 64 >= 2 && pp_span) launch_gemm_pp<1>(g, st);
   else launch_gemm<256, 256, 64, 2, 2, 8, 1, 1>(g, st);
+}
+
+// dX = dY . W (gemm_nt form, B = W^T rows) for a data gradient that feeds a GELU: the epilogue
+// applies gelu'(a + b) and leaves the per-tile column sums of the result (the GELU bias's
+// gradient, first level) in colsum [dtf_gemm_tile_rows(M)][N]; C and a dense [M][N].
+void dtf_gemm_nt_gelu_bwd(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K,
+                          int lda, int ldb, const bf16_t* gelu_a, const float* gelu_b,
+                          float* colsum, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0) return;
+  if (K % 8 || N % 8 || lda % 8 || ldb % 8 || lda < K || ldb < K || !gelu_a || !colsum)
+    throw std::runtime_error("gemm_nt_gelu_bwd: K, N, leading dims % 8; gelu_a and colsum needed");
+  if ((long)256 * lda * 2 + 2L * K >= (1L << 31) || (long)256 * ldb * 2 + 2L * K >= (1L << 31))
+    throw std::runtime_error("gemm_nt_gelu_bwd: leading dimension too large");
+  GemmArgs g{};
+  g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = N;
+  g.gelu_a = gelu_a; g.gelu_b = gelu_b; g.colsum = colsum;
+  g.nt = g_gemm_nt;
+  if (N <= 128) launch_gemm<256, 128, 64, 3>(g, st);
+  else launch_gemm<256, 256, 64, 2, 2>(g, st);
 }
 
 bool dtf_gemm_stream_ok(int M, int N, int K, int lda, int ldb, int ldc);

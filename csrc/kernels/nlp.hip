@@ -459,23 +459,7 @@ void dtf_bf16_col_sum(const bf16_t* x, int T, int N, float* ws, float* out, int 
 namespace {
 
 // ----------------------------------------------------------------------------- bias + GELU
-constexpr float kGeluK0 = 0.7978845608028654f;   // sqrt(2/pi)
-constexpr float kGeluK1 = 0.044715f;
-
-// tanh(u) = 1 - 2 / (1 + e^{2u}) on v_exp_f32 / v_rcp_f32 (libm tanhf is a long branchy
-// sequence; the absolute error here is ~1e-7, far below the bf16 output rounding)
-DTF_DEV float tanh_fast(float u) {
-  const float e = __builtin_amdgcn_exp2f(u * 2.885390081777927f);   // 2 log2(e)
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
-}
-DTF_DEV float gelu_f(float x) {
-  const float t = tanh_fast(kGeluK0 * (x + kGeluK1 * x * x * x));
-  return 0.5f * x * (1.f + t);
-}
-DTF_DEV float gelu_grad(float x) {
-  const float t = tanh_fast(kGeluK0 * (x + kGeluK1 * x * x * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluK0 * (1.f + 3.f * kGeluK1 * x * x);
-}
+// GELU (tanh form) and its derivative: common.h (shared with the GEMM's GELU-backward epilogue)
 
 // Row sweep (as bias_gelu_bwd_kernel): block = R rows x all columns, a thread owns column vectors
 // cv = tid + 256 j with the bias in registers and keeps 4 rows' 16-B loads in flight (the r1

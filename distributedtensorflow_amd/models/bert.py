@@ -34,6 +34,9 @@ from .layers import Layer, _tag, truncated_normal_
 # profiles/measurements/r2_gemm_vs_hipblaslt.jsonl); DTF_BERT_GEMM=native routes them through
 # csrc/kernels/gemm.hip instead.
 BERT_GEMM = os.environ.get("DTF_BERT_GEMM", "library")
+# FFN: bias + GELU + second GEMM as one op whose data gradient carries the GELU derivative in our
+# GEMM's epilogue (A/B knob)
+FUSE_GELU_DGRAD = os.environ.get("DTF_BERT_FUSE_GELU_DGRAD", "1") == "1"
 
 
 @dataclasses.dataclass
@@ -124,8 +127,13 @@ class BertLayer(nn.Module):
                                             self.attn_ln.beta, cfg.hidden_dropout_prob,
                                             self.training, cfg.layer_norm_eps,
                                             residual_to_dense=True)
-        h = ops.bias_gelu(self.inter.gemm(x), self.inter.bias)
-        o = self.out.gemm(h)
+        if FUSE_GELU_DGRAD and BERT_GEMM == "library":
+            # bias + GELU and the second FFN GEMM as one op: its backward forms d(a) in one
+            # GEMM pass with the GELU derivative in the epilogue (ops.native._BiasGeluDense)
+            o = ops.bias_gelu_dense(self.inter.gemm(x), self.inter.bias, self.out.kernel)
+        else:
+            h = ops.bias_gelu(self.inter.gemm(x), self.inter.bias)
+            o = self.out.gemm(h)
         return ops.bias_dropout_add_layer_norm(o, self.out.bias, x, self.out_ln.gamma,
                                                self.out_ln.beta, cfg.hidden_dropout_prob,
                                                self.training, cfg.layer_norm_eps,

@@ -243,6 +243,15 @@ def bias_gelu(a, bias=None):
     return reference.bias_gelu(a, bias)
 
 
+def bias_gelu_dense(a, bias, w):
+    """gelu(a + bias) @ w^T (w [out, in]): BERT's FFN after its first GEMM.  Native: the data
+    gradient of a is one GEMM pass with the GELU derivative and the bias-gradient column sums in
+    its epilogue."""
+    if _use_native(a):
+        return _native().bias_gelu_dense(a, bias, w)
+    return reference.dense(reference.bias_gelu(a, bias), w)
+
+
 def attention_qkv(qkv, mask, batch, seq_len, heads, p=0.0, training=True, scale=None):
     """Multi-head self-attention straight from the fused QKV projection output."""
     if _use_native(qkv):

@@ -1177,6 +1177,46 @@ _GEMM_1X1_MIN_C = int(os.environ.get("DTF_GEMM_1X1_MIN_C", "512"))
 _GEMM_STREAM = os.environ.get("DTF_GEMM_STREAM", "1") == "1"
 
 
+def _dense_weight_grad(w_param, x2, dy2):
+    """dW = dY^T X (fp32) of a library-GEMM dense layer: added straight into the flat gradient
+    buffer when the variable exposes one (returns None then), else returned."""
+    T, i = x2.shape
+    o = dy2.shape[1]
+    dw = None
+    target = _direct_grad(w_param)
+    S = _wgrad_splits(T, o, i) if (o * i) % 4 == 0 and dy2.dtype == x2.dtype else 1
+    if (_DENSE_WGRAD_NATIVE and dy2.dtype == _BF16 and x2.dtype == _BF16
+            and o % 8 == 0 and i % 8 == 0 and o * i <= _DENSE_WGRAD_NATIVE_MAX):
+        # the TN conv weight-gradient kernel, fp32 (straight into the flat buffer when there is
+        # one): 1.05-1.40x the split-K library path up to 2304 x 768 (BERT qkv / attention output
+        # / MLM transform), 0.97-1.00x on the FFN shapes
+        # (profiles/measurements/r3_bert_dense_wgrad_native_vs_library.jsonl)
+        xw, dw4 = x2.contiguous().view(T, 1, 1, i), dy2.contiguous().view(T, 1, 1, o)
+        if target is not None:
+            conv2d_wgrad(xw, dw4, (o, 1, 1, i), 1, 0, out=target.view(o, 1, 1, i))
+        else:
+            dw = conv2d_wgrad(xw, dw4, (o, 1, 1, i), 1, 0).view(o, i)
+    elif S == 1:
+        if target is not None:
+            torch.addmm(target, dy2.t(), x2, out_dtype=torch.float32, out=target)
+        else:
+            dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+    else:
+        part = torch.bmm(dy2.view(S, T // S, o).transpose(1, 2), x2.view(S, T // S, i),
+                         out_dtype=torch.float32)
+        out = target if target is not None else torch.empty(o, i, device=x2.device,
+                                                            dtype=torch.float32)
+        # deterministic in-order slab sum, fused with the += into the flat grad buffer
+        _K.slab_reduce(part.data_ptr(), out.data_ptr(), o * i, S, int(target is not None), _st())
+        if target is None:
+            dw = out
+    if target is not None:
+        _grad_ready(w_param)
+    elif w_param.dtype != torch.float32:
+        dw = dw.to(w_param.dtype)
+    return dw
+
+
 class _Dense(torch.autograd.Function):
     """y = x @ W^T (+ b) on hipBLASLt with the bf16 weight shadow; backward produces dW and db in
     fp32 straight into the optimizer's flat gradient buffer (no bf16 dW, no cast/add kernels)."""
@@ -1209,38 +1249,7 @@ class _Dense(torch.autograd.Function):
                 if pending is not None:
                     dx = dx + pending.view(x.shape)
         if ctx.needs_input_grad[1]:
-            target = _direct_grad(ctx.w_param)
-            S = _wgrad_splits(T, o, i) if (o * i) % 4 == 0 and dy2.dtype == x2.dtype else 1
-            if (_DENSE_WGRAD_NATIVE and dy2.dtype == _BF16 and x2.dtype == _BF16
-                    and o % 8 == 0 and i % 8 == 0 and o * i <= _DENSE_WGRAD_NATIVE_MAX):
-                # the TN conv weight-gradient kernel, fp32 (straight into the flat buffer when
-                # there is one): 1.05-1.40x the split-K library path up to 2304 x 768 (BERT qkv
-                # / attention output / MLM transform), 0.97-1.00x on the FFN shapes
-                # (profiles/measurements/r3_bert_dense_wgrad_native_vs_library.jsonl)
-                xw, dw4 = x2.contiguous().view(T, 1, 1, i), dy2.contiguous().view(T, 1, 1, o)
-                if target is not None:
-                    conv2d_wgrad(xw, dw4, (o, 1, 1, i), 1, 0, out=target.view(o, 1, 1, i))
-                else:
-                    dw = conv2d_wgrad(xw, dw4, (o, 1, 1, i), 1, 0).view(o, i)
-            elif S == 1:
-                if target is not None:
-                    torch.addmm(target, dy2.t(), x2, out_dtype=torch.float32, out=target)
-                else:
-                    dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
-            else:
-                part = torch.bmm(dy2.view(S, T // S, o).transpose(1, 2), x2.view(S, T // S, i),
-                                 out_dtype=torch.float32)
-                out = target if target is not None else torch.empty(o, i, device=x.device,
-                                                                    dtype=torch.float32)
-                # deterministic in-order slab sum, fused with the += into the flat grad buffer
-                _K.slab_reduce(part.data_ptr(), out.data_ptr(), o * i, S, int(target is not None),
-                               _st())
-                if target is None:
-                    dw = out
-            if target is not None:
-                _grad_ready(ctx.w_param)
-            elif ctx.w_param.dtype != torch.float32:
-                dw = dw.to(ctx.w_param.dtype)
+            dw = _dense_weight_grad(ctx.w_param, x2, dy2)
         if ctx.has_b and ctx.needs_input_grad[3]:
             tb = _direct_grad(ctx.b_param)
             out = tb if tb is not None else torch.empty(o, device=x.device, dtype=torch.float32)
@@ -1262,6 +1271,67 @@ class _Dense(torch.autograd.Function):
                 db = out.to(ctx.b_param.dtype)
         ctx.w_param = ctx.b_param = None
         return dx, dw, None, db
+
+
+class _BiasGeluDense(torch.autograd.Function):
+    """o = gelu(a + b1) @ W2^T -- BERT's FFN after its first GEMM (``a`` = x @ W1^T): the
+    bias + GELU runs in our fused kernel and the second GEMM on hipBLASLt as before; in backward
+    the data gradient d(a) = (do @ W2) * gelu'(a + b1) is ONE pass of our MFMA GEMM with the
+    GELU derivative and the b1 column sums in its epilogue (csrc/kernels/gemm.hip gelu_a), so the
+    d(gelu output) tensor [T, 3072] is never written or re-read (replaces hipBLASLt's data
+    gradient + the bias_gelu backward pass).  The hidden activation is internal to the op, so no
+    other consumer can add to its gradient."""
+
+    @staticmethod
+    def forward(ctx, a, b1, w_master, wb):
+        N = a.shape[-1]
+        a2 = a.reshape(-1, N).contiguous()
+        b32 = b1.detach().float().contiguous()
+        h = torch.empty_like(a2)
+        _K.bias_gelu_fwd(a2.data_ptr(), b32.data_ptr(), h.data_ptr(), a2.shape[0], N, _st())
+        o, i = wb.shape
+        if wb.is_contiguous():
+            _register_dgrad_filter(wb.view(o, 1, 1, i))
+        ctx.save_for_backward(a2, b32, h, wb)
+        ctx.params = (b1, w_master)
+        ctx.shape = a.shape
+        return torch.nn.functional.linear(h, wb).view(*a.shape[:-1], o)
+
+    @staticmethod
+    def backward(ctx, do):
+        a2, b32, h, wb = ctx.saved_tensors
+        b1, w_master = ctx.params
+        ctx.params = None
+        o, i = wb.shape
+        M = a2.shape[0]
+        do2 = do.reshape(M, o)
+        do2 = do2.contiguous() if do2.dtype == _BF16 else do2.to(_BF16).contiguous()
+        dw = da = db = None
+        if ctx.needs_input_grad[2]:
+            dw = _dense_weight_grad(w_master, h, do2)
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            wt = _transposed_bf16(wb)                                  # [i, o]
+            da = torch.empty(M, i, device=do.device, dtype=_BF16)
+            tiles = _K.gemm_tile_rows(M)
+            colsum = torch.empty(tiles, i, device=do.device, dtype=torch.float32)
+            _K.gemm_nt_gelu_bwd(do2.data_ptr(), wt.data_ptr(), da.data_ptr(), M, i, o,
+                                do2.stride(0), wt.stride(0), a2.data_ptr(), b32.data_ptr(),
+                                colsum.data_ptr(), _st())
+            if ctx.needs_input_grad[1]:
+                tb = _direct_grad(b1)
+                if tb is not None:
+                    tb.add_(colsum.sum(0))
+                    _grad_ready(b1)
+                else:
+                    db = colsum.sum(0).to(b1.dtype)
+            da = da.view(ctx.shape)
+        return da, db, dw, None
+
+
+def bias_gelu_dense(a, b1, w):
+    """gelu(a + b1) @ w^T with w [out, in] (fp32 master, bf16 shadow on the GEMM)."""
+    _check_cuda_bf16(a)
+    return _BiasGeluDense.apply(a, b1, w, _bf16_weight(w))
 
 
 def _transposed_bf16(wb):

@@ -325,3 +325,40 @@ def test_bert_fused_grad_paths_match_autograd():
     assert cos > 0.9999, cos              # GEMM beta=1 rounds once instead of twice
     assert (ga - gb).abs().max() <= 0.02 * gb.abs().max()
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,I,O", [(1024, 3072, 768), (777, 256, 96), (300, 128, 64)])
+def test_bias_gelu_dense_fused_backward(T, I, O):
+    """gelu(a + b1) @ W2^T with d(a) formed by ONE GEMM pass carrying the GELU derivative and the
+    b1 column sums in its epilogue == the unfused bias_gelu + library dense (and an fp32
+    reference)."""
+    torch.manual_seed(0)
+    a32 = torch.randn(T, I) * 2
+    b1 = torch.randn(I) * 0.5
+    w2 = torch.randn(O, I) * I ** -0.5
+    do = torch.randn(T, O)
+
+    def run(fused):
+        a = a32.cuda().bfloat16().requires_grad_(True)
+        b = b1.cuda().requires_grad_(True)
+        w = w2.cuda().requires_grad_(True)
+        if fused:
+            y = ops.bias_gelu_dense(a, b, w)
+        else:
+            y = ops.dense(ops.bias_gelu(a, b), w, None, impl="library")
+        y.backward(do.cuda().bfloat16())
+        return y.float().cpu(), a.grad.float().cpu(), b.grad.cpu(), w.grad.cpu()
+
+    fy, fa, fb, fw = run(True)
+    uy, ua, ub, uw = run(False)
+    torch.testing.assert_close(fy, uy, atol=0, rtol=0)          # same forward kernels
+    a_ = a32.bfloat16().float().requires_grad_(True)
+    b_ = b1.clone().requires_grad_(True)
+    w_ = w2.bfloat16().float().requires_grad_(True)
+    y_ = R.bias_gelu(a_, b_) @ w_.t()
+    y_.backward(do.bfloat16().float())
+    for got, unf, ref in ((fa, ua, a_.grad), (fb, ub, b_.grad), (fw, uw, w_.grad)):
+        scale = ref.abs().max()
+        assert (got - ref).abs().max() <= 2e-2 * scale, (got - ref).abs().max() / scale
+        assert (got - unf).abs().max() <= 2e-2 * scale
