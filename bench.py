@@ -3,11 +3,22 @@
 
     python bench.py --gpus N --steps K --warmup W [--batch 256] [--impl dtf|torch]
 
-For N > 1 run under ``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N``
-(one process per GPU, RCCL over xGMI).  Each rank trains on its own synthetic ImageNet-shaped
-batch (weak scaling: per-GPU batch fixed); the timed region is exactly K full training steps
-(forward, backward, overlapped bucketed all-reduce, fused SGD-momentum update) bracketed by a
-barrier + device synchronize on both sides; the MAX elapsed time over ranks is reported.
+For N > 1 the bench runs one process per GPU (RCCL over xGMI), either under
+``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` or launched by
+bench.py itself: without torchrun's ``WORLD_SIZE`` in the environment, ``--gpus N`` spawns the N
+rank processes BEFORE any GPU call, relays their output (rank 0 prints the JSON line) and exits
+with the worst rank's exit code.  It never measures fewer GPUs than asked: fewer visible devices
+than N, or a ``WORLD_SIZE`` that differs from N, is a non-zero exit with the reason.
+
+Each rank trains on its own synthetic ImageNet-shaped batch (weak scaling: per-GPU batch fixed);
+the timed region is exactly K full training steps (forward, backward, overlapped bucketed
+all-reduce, fused SGD-momentum update) bracketed by a barrier + device synchronize on both sides;
+the MAX elapsed time over ranks is reported.
+
+Hangs end loudly: the process group and the collective watchdog (parallel/watchdog.py) use
+``DTF_COMM_TIMEOUT_S`` (default 300 s), and a stack-dumping deadline (``faulthandler``) bounds
+the warm-up (``--warmup-timeout``) and every timed step (``--step-timeout``): on expiry every
+thread's stack goes to stderr and the process exits non-zero.
 
 ``--impl dtf``   (default) this framework: hand-written HIP kernels, MirroredStrategy.
 ``--impl torch`` the stock PyTorch-ROCm comparator (MIOpen convs, DDP) on the same data.
@@ -15,8 +26,11 @@ barrier + device synchronize on both sides; the MAX elapsed time over ranks is r
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
+import signal
+import subprocess
 import sys
 import time
 
@@ -87,12 +101,26 @@ def parse():
                         "auto = use this repo's tuned table for the model when present, tune = "
                         "benchmark every solution once and write the table to --gemm-tuning-out")
     p.add_argument("--gemm-tuning-out", default=None)
+    p.add_argument("--warmup-timeout", type=float, default=900,
+                   help="seconds the warm-up may take before the bench dumps every thread's "
+                        "stack and exits non-zero (0 = no deadline)")
+    p.add_argument("--step-timeout", type=float, default=120,
+                   help="seconds any timed step (and the final drain) may take before the bench "
+                        "dumps stacks and exits non-zero (0 = no deadline)")
     args = p.parse_args()
     args.bucket_auto = args.bucket_mb == "auto"
     args.bucket_mb = 64.0 if args.bucket_auto else float(args.bucket_mb)
     if args.batch is None:
         args.batch = 512 if args.model == "bert_base" else 1984
     return args
+
+
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:
+        return None
 
 
 def log(*a):
@@ -281,6 +309,95 @@ def tune_buckets(args, opt, strategy, step, images, labels, sync, dev, steps=2):
     return results
 
 
+def fail(msg, code=2):
+    print(f"bench.py: error: {msg}", file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
+def share_device():
+    """``DTF_BENCH_SHARE_DEVICE=1`` (with ``DTF_BENCH_BACKEND=gloo``): every rank on cuda:0 -- the
+    multi-rank rehearsal on a one-GPU box (RCCL refuses two ranks on one device)."""
+    return os.environ.get("DTF_BENCH_SHARE_DEVICE", "0") == "1"
+
+
+def check_devices(n):
+    """Before any GPU call (``device_count`` does not initialise the GPU): N ranks need N GPUs,
+    unless the gloo rehearsal shares one on purpose."""
+    backend = os.environ.get("DTF_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        fail(f"DTF_BENCH_BACKEND={backend!r}: expected nccl or gloo")
+    if share_device():
+        if backend != "gloo":
+            fail("DTF_BENCH_SHARE_DEVICE=1 needs DTF_BENCH_BACKEND=gloo (RCCL refuses two ranks "
+                 "on one device)")
+        if torch.cuda.device_count() < 1:
+            fail("no GPU visible")
+        return
+    ndev = torch.cuda.device_count()
+    if ndev < n:
+        fail(f"--gpus {n} but only {ndev} GPU(s) are visible: refusing to measure fewer GPUs "
+             f"than requested")
+
+
+def self_launch(args):
+    """``--gpus N`` (N > 1) without torchrun env: start the N rank processes here (one per GPU,
+    torchrun's env contract: RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_*),
+    stream their output through, and return the worst exit code.  When any rank fails, the
+    others are terminated (they would otherwise wait in a collective for the dead one)."""
+    from distributedtensorflow_amd.cluster.launcher import free_ports
+    n = args.gpus
+    check_devices(n)
+    port = free_ports(1)[0]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(0 if share_device()
+                                                                           else r),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), DTF_BENCH_LAUNCH="self")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env, cwd=ROOT, start_new_session=True))
+    codes = [None] * n
+    failed_at = None
+    try:
+        while any(c is None for c in codes):
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    codes[i] = p.poll()
+                    if codes[i] not in (None, 0) and failed_at is None:
+                        failed_at = time.time()
+                        print(f"bench.py: rank {i} exited with {codes[i]}; stopping the other "
+                              f"ranks", file=sys.stderr, flush=True)
+                        for q in procs:
+                            if q.poll() is None:
+                                os.killpg(q.pid, signal.SIGTERM)
+            if failed_at is not None and time.time() - failed_at > 20:
+                for q in procs:
+                    if q.poll() is None:
+                        os.killpg(q.pid, signal.SIGKILL)
+            time.sleep(0.1)
+    except KeyboardInterrupt:
+        for q in procs:
+            if q.poll() is None:
+                os.killpg(q.pid, signal.SIGKILL)
+        raise
+    # a signal death (negative code) is a failure too
+    return max(abs(c) for c in codes)
+
+
+class Deadline:
+    """A stack-dumping, process-ending deadline (faulthandler: a C watchdog thread that needs no
+    GIL): ``arm(s)`` restarts it, ``disarm()`` cancels."""
+
+    def arm(self, seconds, what):
+        faulthandler.cancel_dump_traceback_later()
+        if seconds and seconds > 0:
+            self.what = what
+            faulthandler.dump_traceback_later(seconds, exit=True)
+
+    def disarm(self):
+        faulthandler.cancel_dump_traceback_later()
+
+
 def main():
     args = parse()
     if args.strategy == "ps_async":
@@ -288,11 +405,18 @@ def main():
         if args.job_name:
             return ps_bench.run_task(args)
         return ps_bench.run_launcher(args)
+    if args.gpus < 1:
+        fail("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        fail(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per requested GPU")
+    if os.environ.get("DTF_BENCH_BACKEND", "nccl") == "nccl" and torch.cuda.device_count() <= local:
+        fail(f"LOCAL_RANK={local} but only {torch.cuda.device_count()} GPU(s) are visible")
+    deadline = Deadline()
     # one process per GPU: split the CPU quota between the node's ranks (torch's default pool is
     # sized by the whole machine and oversubscribes a shared host; see utils/cpu.py)
     from distributedtensorflow_amd.utils.cpu import usable_cpus
@@ -326,6 +450,16 @@ def main():
 
     # the process group that carried the gradients ("nccl" = RCCL on ROCm; None at N = 1)
     native_info["comm_backend"] = dist.get_backend() if dist.is_initialized() else None
+    native_info["launch"] = {
+        "mode": os.environ.get("DTF_BENCH_LAUNCH", "torchrun" if "WORLD_SIZE" in os.environ
+                               else "single"),
+        "env_world_size": world,
+        "dist_world_size": dist.get_world_size() if dist.is_initialized() else 1,
+        "rccl_version": _rccl_version(), "visible_gpus": torch.cuda.device_count(),
+        "comm_timeout_s": float(os.environ.get("DTF_COMM_TIMEOUT_S", "300") or 300)}
+    if native_info["launch"]["dist_world_size"] != world:
+        fail(f"process group has {native_info['launch']['dist_world_size']} ranks, expected "
+             f"{world}")
 
     strategy = None
     B, S = args.batch, args.image_size
@@ -364,6 +498,7 @@ def main():
         torch.cuda.synchronize()
 
     t0 = time.time()
+    deadline.arm(args.warmup_timeout, "warm-up")
     for i in range(args.warmup):
         loss = step(images, labels)
     sync()
@@ -380,9 +515,12 @@ def main():
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        deadline.arm(args.step_timeout, f"timed step {i}")
         loss = step(images, labels)
+    deadline.arm(2 * args.step_timeout, "final drain")
     sync()
     elapsed = time.perf_counter() - t0
+    deadline.arm(args.step_timeout, "report")
     # exposed communication: compute-stream wait for RCCL after backward (0 buckets at N=1)
     comm_info = comm.as_dict() if comm is not None else {"buckets": 0,
                                                          "exposed_ms_per_step": 0.0}
@@ -450,6 +588,7 @@ def main():
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+    deadline.disarm()
 
 
 if __name__ == "__main__":

@@ -81,7 +81,7 @@ def _dump_stacks(tasks):
         time.sleep(1.0)
 
 
-def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script):
+def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart_alone=False):
     """Wait for the worker tasks, restarting failed tasks meanwhile.
 
     A task that exits non-zero while the job runs is restarted as a FRESH process (never a
@@ -89,7 +89,9 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script):
     survivor re-forms its process group with it (cluster/rendezvous.py).  Exit code
     ``REJOIN_EXIT_CODE`` is a parameter-server task leaving voluntarily for the new epoch: it is
     restarted without counting against ``max_restarts``.  Once a worker finished cleanly the job
-    is ending and failures are no longer recovered."""
+    is ending and failures are no longer recovered.  ``restart_alone``: a collective world
+    restarts a failed rank even when no other rank is alive (a one-rank world, or every rank
+    died): the restarted ranks resume from the chief's latest checkpoint."""
     from .rendezvous import bump_epoch
     from .server import Server
     t0 = time.time()
@@ -105,7 +107,7 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script):
                 continue
             workers_alive = any(x.proc.poll() is None for x in tasks if is_worker(x))
             voluntary = rc == Server.REJOIN_EXIT_CODE
-            if ending or not (workers_alive or not is_worker(t)) or \
+            if ending or not (workers_alive or not is_worker(t) or restart_alone) or \
                     (not voluntary and used >= max_restarts):
                 continue                                  # final: reported as its exit code
             if not voluntary:
@@ -222,7 +224,8 @@ def launch_collective(script, nproc, workdir=None, extra_args=(), env=None, time
     tasks = [_Task("rank", r, spawn) for r in range(nproc)]
     rc = {}
     try:
-        _supervise(tasks, store, lambda t: True, max_restarts, timeout_s, script)
+        _supervise(tasks, store, lambda t: True, max_restarts, timeout_s, script,
+                   restart_alone=True)
         for t in tasks:
             rc[t.index] = t.proc.wait()
     finally:

@@ -300,14 +300,18 @@ def _dispatch(name, fn, fenced):
     return op
 
 
-_FENCED = ("conv2d", "conv2d_bias_relu", "batch_norm", "batch_norm_add_batch_norm",
-           "batch_norm_relu_conv1x1",
-           "batch_norm_relu_max_pool", "dense", "layer_norm", "bias_dropout_add_layer_norm",
-           "embedding_layer_norm", "bias_gelu")
-for _name in _FENCED + ("relu", "max_pool2d", "global_avg_pool", "sparse_softmax_cross_entropy",
-                        "softmax_cross_entropy_clipped_sum", "gelu", "attention", "dropout",
-                        "attention_qkv", "mlm_loss"):
-    globals()[_name] = _dispatch(_name, globals()[_name], _name in _FENCED)
+# EVERY public op entry point passes through the fence: a per-op allow-list went stale once
+# already (bias_gelu_dense read an un-gathered W2 shadow), and the fence costs one
+# global load when no gather is pending and an attribute scan of the arguments otherwise.
+_OPS = ("conv2d", "conv2d_bias_relu", "batch_norm", "batch_norm_add_batch_norm",
+        "batch_norm_relu_conv1x1", "batch_norm_relu_max_pool", "dense", "layer_norm",
+        "bias_dropout_add_layer_norm", "embedding_layer_norm", "bias_gelu", "bias_gelu_dense",
+        "relu", "max_pool2d", "global_avg_pool", "sparse_softmax_cross_entropy",
+        "softmax_cross_entropy_clipped_sum", "gelu", "attention", "dropout", "attention_qkv",
+        "mlm_loss")
+_FENCED = _OPS
+for _name in _OPS:
+    globals()[_name] = _dispatch(_name, globals()[_name], True)
 del _name
 
 __all__ = [

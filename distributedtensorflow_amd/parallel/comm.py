@@ -16,8 +16,8 @@ never the host:
 """
 from __future__ import annotations
 
-import itertools
 import os
+import threading
 
 import torch
 import torch.distributed as dist
@@ -25,7 +25,28 @@ import torch.distributed as dist
 _OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
 _DTYPES = {torch.float32: 7, torch.bfloat16: 9, torch.float16: 6, torch.int64: 4,
            torch.int32: 2, torch.uint8: 1}
-_COUNTER = itertools.count()
+# RCCL unique-id store keys: "dtf/rccl_uid/<n>" under the process group's store, which the
+# launcher scopes per cluster epoch (PrefixStore "g<epoch>").  ``n`` counts communicators created
+# in THIS world and restarts at 0 whenever a world is formed (reset_uid_index, called by
+# init_process_group_from_env): a restarted rank and the survivors then agree on the key.
+_uid_index = 0
+
+
+def reset_uid_index():
+    global _uid_index
+    _uid_index = 0
+
+
+def _next_uid_key():
+    global _uid_index
+    k = f"dtf/rccl_uid/{_uid_index}"
+    _uid_index += 1
+    return k
+
+
+def _watchdog():
+    from .watchdog import get_watchdog
+    return get_watchdog()
 
 
 class C10dComm:
@@ -35,24 +56,50 @@ class C10dComm:
 
     def __init__(self, group=None):
         self.group = group
+        self.wd = _watchdog()
+        self._nccl = dist.get_backend(group) == "nccl"
+        self._aborted = False
+        self.wd.add_abort(self.abort)
+
+    def _track(self, work, what):
+        self.wd.watch(work.is_completed, f"c10d {what}")
+        return work
 
     def all_reduce(self, t):
-        return dist.all_reduce(t, group=self.group, async_op=True)
+        self.wd.check()
+        return self._track(dist.all_reduce(t, group=self.group, async_op=True), "all_reduce")
 
     def reduce_scatter(self, out, inp):
-        return dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=True)
+        self.wd.check()
+        return self._track(dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=True),
+                           "reduce_scatter")
 
     def all_gather(self, out, inp):
-        return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
+        self.wd.check()
+        return self._track(dist.all_gather_into_tensor(out, inp, group=self.group,
+                                                       async_op=True), "all_gather")
 
     def reduce(self, t, dst):
-        return dist.reduce(t, dst=dst, group=self.group, async_op=True)
+        self.wd.check()
+        return self._track(dist.reduce(t, dst=dst, group=self.group, async_op=True), "reduce")
 
     def broadcast(self, t, src):
-        return dist.broadcast(t, src=src, group=self.group, async_op=True)
+        self.wd.check()
+        return self._track(dist.broadcast(t, src=src, group=self.group, async_op=True),
+                           "broadcast")
+
+    def abort(self):
+        """Watchdog trip: abort the RCCL communicators of the process group, so kernels blocked
+        on a dead peer exit (gloo has no device-side wait to break; its own timeout applies)."""
+        if self._aborted or not self._nccl:
+            return
+        self._aborted = True
+        abort = getattr(dist.distributed_c10d, "_abort_process_group", None)
+        if abort is not None and dist.is_initialized():
+            abort(self.group) if self.group is not None else abort()
 
     def close(self, abort=False):
-        pass
+        self.wd.remove_abort(self.abort)
 
 
 class _Done:
@@ -88,7 +135,7 @@ class RcclComm:
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
         store = store or dist.distributed_c10d._get_default_store()
-        key = f"dtf/rccl_uid/{next(_COUNTER)}"
+        key = _next_uid_key()
         if self.rank == 0:
             uid = self.K.rccl_unique_id()
             store.set(key, uid)
@@ -97,8 +144,24 @@ class RcclComm:
         self.comm = self.K.rccl_comm_init(uid, self.world, self.rank, self.device.index)
         # highest priority: the collectives should not queue behind compute kernels
         self.stream = torch.cuda.Stream(self.device, priority=-1)
+        # bounded waits: ncclCommAbort from the watchdog on a deadline / async error / epoch bump
+        self._lock = threading.Lock()
+        self.wd = _watchdog()
+        self.wd.add_abort(self.abort)
+        self.wd.add_probe(self._probe)
 
-    def _issue(self, fn, *tensors):
+    def _probe(self):
+        with self._lock:
+            if not self.comm:
+                return None
+            r = self.K.rccl_async_error(self.comm)
+        return f"rccl async error {r}" if r not in (0, 7) else None    # 7 = ncclInProgress
+
+    def _issue(self, fn, *tensors, what="collective"):
+        self.wd.check()
+        if not self.comm:
+            from .strategy import CommError
+            raise CommError("rccl communicator was aborted")
         cur = torch.cuda.current_stream(self.device)
         self.stream.wait_stream(cur)            # the producers of the operands ran before issue
         fn(self.stream.cuda_stream)
@@ -106,6 +169,7 @@ class RcclComm:
             t.record_stream(self.stream)
         ev = torch.cuda.Event()
         ev.record(self.stream)
+        self.wd.watch(ev.query, f"rccl {what}")
         return _Done(ev)
 
     @staticmethod
@@ -117,38 +181,55 @@ class RcclComm:
 
     def all_reduce(self, t, op="sum"):
         return self._issue(lambda s: self.K.rccl_all_reduce(
-            self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), _OPS[op], s), t)
+            self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), _OPS[op], s), t,
+            what="all_reduce")
 
     def reduce_scatter(self, out, inp, op="sum"):
         if inp.numel() != out.numel() * self.world:
             raise ValueError("rccl reduce_scatter: input must be world x output")
         return self._issue(lambda s: self.K.rccl_reduce_scatter(
             self.comm, inp.data_ptr(), out.data_ptr(), out.numel(), self._dt(out), _OPS[op], s),
-            out, inp)
+            out, inp, what="reduce_scatter")
 
     def all_gather(self, out, inp):
         if out.numel() != inp.numel() * self.world:
             raise ValueError("rccl all_gather: output must be world x input")
         return self._issue(lambda s: self.K.rccl_all_gather(
-            self.comm, inp.data_ptr(), out.data_ptr(), inp.numel(), self._dt(inp), s), out, inp)
+            self.comm, inp.data_ptr(), out.data_ptr(), inp.numel(), self._dt(inp), s), out, inp,
+            what="all_gather")
 
     def reduce(self, t, dst, op="sum"):
         return self._issue(lambda s: self.K.rccl_reduce(
-            self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), _OPS[op], dst, s), t)
+            self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), _OPS[op], dst, s), t,
+            what="reduce")
 
     def broadcast(self, t, src):
         return self._issue(lambda s: self.K.rccl_broadcast(
-            self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), src, s), t)
+            self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), src, s), t,
+            what="broadcast")
 
     def async_error(self):
         return self.K.rccl_async_error(self.comm)
 
+    def abort(self):
+        """ncclCommAbort (thread-safe against the probe; idempotent): RCCL kernels still spinning
+        on a dead peer see the abort flag and exit, so the comm stream drains."""
+        with self._lock:
+            c, self.comm = self.comm, 0
+        if c:
+            self.K.rccl_comm_destroy(c, 1)
+
     def close(self, abort=False):
-        if self.comm:
-            if not abort:
-                self.stream.synchronize()
-            self.K.rccl_comm_destroy(self.comm, int(abort))
-            self.comm = 0
+        self.wd.remove_abort(self.abort)
+        self.wd.remove_probe(self._probe)
+        if abort:
+            self.abort()
+            return
+        with self._lock:
+            c, self.comm = self.comm, 0
+        if c:
+            self.stream.synchronize()
+            self.K.rccl_comm_destroy(c, 0)
 
 
 def make_comm(kind=None, group=None, device=None):

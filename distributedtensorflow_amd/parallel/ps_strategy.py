@@ -328,8 +328,8 @@ class ParameterServerStrategy(Strategy):
         return self.mode == "colocated" and dist.is_initialized() and \
             (dist.get_world_size() > 1 or self.force_reducer)
 
-    def sync_after_restore(self, optimizer, global_step=None):
-        _broadcast_training_state(self.collective, optimizer, global_step)
+    def sync_after_restore(self, optimizer, global_step=None, restored=False):
+        _broadcast_training_state(self.collective, optimizer, global_step, restored=restored)
 
     def cluster_changed(self):
         if self.mode == "between_graph":

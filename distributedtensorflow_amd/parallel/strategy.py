@@ -281,6 +281,8 @@ class BucketedAllReduce:
 
     @comm_call
     def finish(self):
+        from .watchdog import check as _wd_check
+        _wd_check()
         st = self.stats
         early = sum(self.launched)
         st.steps += 1
@@ -384,7 +386,7 @@ class Strategy:
         checkpoint/state synchronisation together)."""
         return False
 
-    def sync_after_restore(self, optimizer, global_step=None):
+    def sync_after_restore(self, optimizer, global_step=None, restored=False):
         """After the chief restored a checkpoint: make every replica hold the chief's variables,
         optimizer slots, update count and global step (collective strategies only)."""
 
@@ -417,13 +419,23 @@ def _parse_device(d):
     return torch.device(d)
 
 
-def _broadcast_training_state(active, optimizer, global_step=None, src=0):
+def _broadcast_training_state(active, optimizer, global_step=None, src=0, restored=False):
     """Rank ``src``'s master weights (+ compute shadow), optimizer slots, update count and global
-    step to every rank: the state a restored chief hands to the other replicas."""
+    step to every rank: the state a restored chief hands to the other replicas.
+
+    ``restored`` (meaningful on ``src``; broadcast so every rank takes the same branch): the chief
+    holds a whole checkpoint.  When it does NOT, a parameter-server reducer's slot buffers are
+    valid only on each chunk's owner, so they are gathered from the owners first -- broadcasting
+    the chief's copy would overwrite every other owner's slots with stale values."""
     if not active or optimizer is None or optimizer.space is None:
         return
     optimizer.synchronize_variables()
     sp = optimizer.space
+    flag = torch.tensor([1 if restored else 0], dtype=torch.int64, device=sp.device)
+    dist.broadcast(flag, src)
+    reducer = getattr(optimizer, "_reducer", None)
+    if not int(flag[0]) and reducer is not None:
+        reducer.gather_state(list(optimizer.state_tensors()))
     dist.broadcast(sp.master, src)
     for t in optimizer.state_tensors():
         dist.broadcast(t, src)
@@ -440,16 +452,26 @@ def _broadcast_training_state(active, optimizer, global_step=None, src=0):
 _collective_watcher = None
 
 
-def init_process_group_from_env(backend=None, timeout_s=600):
+def init_process_group_from_env(backend=None, timeout_s=None):
     """Initialise torch.distributed from torchrun-style env (RANK/WORLD_SIZE/MASTER_*).
 
     Under this package's launcher (``DTF_STORE_ADDR``: the launcher hosts the rendezvous store,
     cluster/rendezvous.py) the group is created for the current cluster EPOCH, and an epoch
-    watcher tells the training session when a failed rank was restarted."""
+    watcher tells the training session when a failed rank was restarted.
+
+    Every world gets a fresh collective watchdog (parallel/watchdog.py): the communicators
+    register their collectives with it, and the epoch bump is one of its failure probes, so a
+    survivor blocked inside an RCCL kernel on a dead peer is released by an abort instead of
+    waiting out the process-group timeout (``timeout_s``, default ``DTF_COMM_TIMEOUT_S`` = 300)."""
     import datetime
     global _collective_watcher
     if dist.is_initialized():
         return
+    from . import comm as _comm, watchdog as _wd
+    if timeout_s is None:
+        timeout_s = _wd.default_timeout_s()
+    _comm.reset_uid_index()
+    wd = _wd.reset_watchdog()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if backend is None:
@@ -472,12 +494,20 @@ def init_process_group_from_env(backend=None, timeout_s=600):
         _collective_watcher = rendezvous.EpochWatcher(epoch).start()
         _collective_watcher.backend, _collective_watcher.timeout_s = backend, timeout_s
         _collective_watcher.store = store
+        watcher = _collective_watcher
+        wd.add_probe(lambda: (f"cluster epoch moved past {watcher.epoch}: a peer was restarted"
+                              if watcher.changed else None))
         return
     dist.init_process_group(backend, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
 
 
 def collective_cluster_changed():
+    """True once a peer was restarted (epoch bump) or the collective watchdog tripped (a
+    collective missed its deadline or the communicator reported an error)."""
+    from .watchdog import _watchdog as wd
+    if wd is not None and wd.failed is not None:
+        return True
     return _collective_watcher is not None and _collective_watcher.changed
 
 
@@ -559,8 +589,8 @@ class MirroredStrategy(Strategy):
     def collective(self):
         return self._dist
 
-    def sync_after_restore(self, optimizer, global_step=None):
-        _broadcast_training_state(self._dist, optimizer, global_step)
+    def sync_after_restore(self, optimizer, global_step=None, restored=False):
+        _broadcast_training_state(self._dist, optimizer, global_step, restored=restored)
 
     def cluster_changed(self):
         return collective_cluster_changed()
@@ -569,12 +599,20 @@ class MirroredStrategy(Strategy):
         """A replica died and the launcher restarted it: re-form the world in the new epoch and
         rebuild the gradient reducer on the new process group (the caller restores the latest
         checkpoint on the chief and calls :meth:`sync_after_restore`)."""
+        # the cached communicator belongs to the old world (it includes the dead peer): abort
+        # it BEFORE leaving, so nothing of it survives into the new epoch (the PS strategy does
+        # the same, ps_strategy.recover_cluster)
+        if optimizer is not None and hasattr(getattr(optimizer, "_reducer", None), "close"):
+            optimizer._reducer.close(abort=True)
+        if self._comm is not None:
+            try:
+                self._comm.close(abort=True)
+            except Exception:
+                pass
+            self._comm = None
         epoch = rejoin_collective()
         self._dist = dist.is_initialized() and (dist.get_world_size() > 1 or self.force_reducer)
         if optimizer is not None and optimizer.space is not None:
-            old = optimizer._reducer
-            if hasattr(old, "close"):
-                old.close(abort=True)
             optimizer._reducer = self.make_gradient_reducer(optimizer.space)
             # the restarted replica's Optimizer.build broadcast, mirrored (the collective
             # sequence must be the same on every rank)

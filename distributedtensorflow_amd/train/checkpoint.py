@@ -203,6 +203,11 @@ class Saver:
                 t = values[name]
             t = t.detach() if isinstance(t, torch.Tensor) else torch.as_tensor(t)
             tensors[name] = to_tf_layout(t.cpu(), layout).contiguous()
+        # the copies above waited for the step's collectives: if the watchdog aborted one of
+        # them (dead peer), these values are garbage -- never let them become the latest
+        # checkpoint that recovery restores
+        from ..parallel import watchdog
+        watchdog.check()
         if self.num_shards > 1:
             names = sorted(tensors)
             write_bundle(prefix, tensors, self.num_shards,

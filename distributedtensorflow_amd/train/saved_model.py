@@ -257,8 +257,9 @@ class Tracer:
                        [x.name, self.read(gamma), self.read(beta), self.read(mean),
                         self.read(var)],
                        T=a_type(DT_FLOAT), U=a_type(DT_FLOAT), epsilon=a_float(eps),
-                       exponential_avg_factor=a_float(1.0), data_format=a_str("NHWC"),
-                       is_training=a_bool(False))
+                       data_format=a_str("NHWC"), is_training=a_bool(False))
+        # (no exponential_avg_factor: that attr is TF >= 2.2, and a TF 1.15 loader -- the
+        # MetaGraph's declared version -- rejects NodeDefs with attrs its op registry lacks)
         return _Sym(self, n + ":0", x.shape)
 
     def _add(self, a, b):

@@ -298,6 +298,11 @@ def _maybe_hard_fault(strategy, step):
         os.kill(os.getpid(), signal.SIGKILL)
 
 
+def _comm_check():
+    from ..parallel import watchdog
+    watchdog.check()
+
+
 class MonitoredTrainingSession:
     # the exception types _recoverable() accepts (communication ones only under a launcher
     # that restarts failed tasks)
@@ -372,7 +377,7 @@ class MonitoredTrainingSession:
             sc.init_fn(self)
         if getattr(self.strategy, "collective", False) and sc.optimizer is not None:
             # synchronous replicas: everyone continues from the chief's (restored) state
-            self.strategy.sync_after_restore(sc.optimizer, sc.global_step)
+            self.strategy.sync_after_restore(sc.optimizer, sc.global_step, restored=restored)
         if sc.optimizer is not None and hasattr(self.strategy, "register_with_ps"):
             self.strategy.register_with_ps(sc.optimizer, sc.global_step.value())
             client = getattr(self.strategy, "ps_client", None)
@@ -400,9 +405,11 @@ class MonitoredTrainingSession:
             print(f"[dtf] recovering from {type(exc).__name__}: {exc}", flush=True)
             epoch = strat.recover_cluster(sc.optimizer)
             ckpt = latest_checkpoint(self.checkpoint_dir) if self.checkpoint_dir else None
+            restored = False
             if self.is_chief and ckpt and sc.saver is not None:
                 sc.saver.restore(None, ckpt, strict=False)
-            strat.sync_after_restore(sc.optimizer, sc.global_step)
+                restored = True
+            strat.sync_after_restore(sc.optimizer, sc.global_step, restored=restored)
             # the restarted replica runs after_create_session (its initial checkpoint save is a
             # collective under a sharded PS): the survivors mirror it
             for h in self.hooks:
@@ -463,6 +470,10 @@ class MonitoredTrainingSession:
                     raise ClusterChanged("a task of the cluster was restarted")
                 _maybe_hard_fault(self.strategy, self.global_step.value())
                 results = _execute(fetches, feed_dict, self._session)
+                # a collective of this step missed its deadline / a peer was restarted while it
+                # ran: the step's result is garbage (the watchdog aborted the communicator) --
+                # recover BEFORE any hook (a checkpoint save!) observes it
+                _comm_check()
                 self._session.last_results = results
                 rv = SessionRunValues(results)
                 for h in self.hooks:

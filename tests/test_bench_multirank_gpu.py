@@ -116,3 +116,44 @@ def test_bench_two_ranks_bert(tmp_path):
     assert cfg["comm_backend"] == "gloo" and cfg["comm"]["buckets"] >= 2
     assert cfg["comm"]["early_launches"] >= 3
     assert abs(rec["value"] - 32 * 64 * 1000.0 / rec["ms_per_step"]) / rec["value"] < 1e-3
+
+
+def test_bench_self_launches_n_ranks_without_torchrun(tmp_path):
+    """a plain ``python bench.py --gpus 2`` (no torchrun env) starts the two
+    rank processes itself -- here sharing cuda:0 over gloo, the one-GPU rehearsal -- and rank 0
+    reports the whole 2-rank job."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                        "MASTER_PORT")}
+    env.update(PYTHONPATH=ROOT, OMP_NUM_THREADS="2", DTF_BENCH_BACKEND="gloo",
+               DTF_BENCH_SHARE_DEVICE="1")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--batch", "16", "--image-size", "96", "--steps", "3", "--warmup", "2"],
+                       env=env, capture_output=True, text=True, timeout=150, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    rec = json.loads(lines[0])
+    cfg = rec["config"]
+    assert rec["n_gpus"] == 2 and cfg["parallelism"] == "dp2" and cfg["global_batch"] == 32
+    assert cfg["comm"]["buckets"] >= 2
+    assert cfg["launch"]["mode"] == "self"
+    assert cfg["launch"]["env_world_size"] == 2 and cfg["launch"]["dist_world_size"] == 2
+
+
+def test_bench_nccl_refuses_more_ranks_than_gpus():
+    """--gpus N on RCCL with fewer visible GPUs exits non-zero fast with the device-count reason
+    (never a silent 1-GPU number labelled N, never a hang)."""
+    import time
+    import torch
+    n = torch.cuda.device_count() + 1
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "DTF_BENCH_BACKEND",
+                        "DTF_BENCH_SHARE_DEVICE")}
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n),
+                        "--steps", "1", "--warmup", "1"], env=env, capture_output=True,
+                       text=True, timeout=60, cwd=ROOT)
+    assert p.returncode != 0
+    assert "refusing to measure fewer GPUs" in p.stderr, p.stderr[-2000:]
+    assert time.time() - t0 < 30

@@ -1,0 +1,162 @@
+"""Bounded collective waits (VERDICT r3 "Next round" item 2).
+
+The reference recovers from a dead task because TF1's MonitoredTrainingSession recreates its
+session on AbortedError/UnavailableError (/root/reference/run_mnist_distributed.py:128-132,146).
+A GPU collective world only gets there if a survivor blocked on a dead peer is RELEASED: these
+tests pin the watchdog that does it (parallel/watchdog.py) -- a stalled collective trips it within
+its deadline, the trip runs the communicators' abort callbacks, and every later issue / step check
+raises CommError (recoverable under the launcher, a loud failure otherwise)."""
+import json
+import os
+import subprocess
+import sys
+import threading
+import time
+
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def test_stalled_collective_trips_within_deadline_and_aborts():
+    from distributedtensorflow_amd.parallel.strategy import CommError
+    from distributedtensorflow_amd.parallel.watchdog import CommWatchdog
+    wd = CommWatchdog(timeout_s=0.4, interval_s=0.02)
+    released = threading.Event()        # the "RCCL kernel": completes only when aborted
+    wd.add_abort(released.set)
+    t0 = time.monotonic()
+    wd.watch(released.is_set, "fake all_reduce")
+    assert wd.wait_tripped(5.0)
+    dt = time.monotonic() - t0
+    assert 0.4 <= dt < 1.5, dt
+    assert released.is_set()            # abort ran: the blocked collective is released
+    assert "fake all_reduce" in wd.failed and "DTF_COMM_TIMEOUT_S" in wd.failed
+    with pytest.raises(CommError, match="watchdog"):
+        wd.check()
+    wd.stop()
+
+
+def test_completed_collectives_never_trip():
+    from distributedtensorflow_amd.parallel.watchdog import CommWatchdog
+    wd = CommWatchdog(timeout_s=0.3, interval_s=0.02)
+    aborted = []
+    wd.add_abort(lambda: aborted.append(1))
+    for _ in range(50):
+        wd.watch(lambda: True, "done")
+    time.sleep(0.6)
+    assert wd.failed is None and not aborted and wd.inflight() == 0
+    wd.check()
+    wd.stop()
+
+
+def test_probe_failure_trips_immediately_and_late_abort_runs():
+    """An epoch bump / async RCCL error trips the watchdog with nothing in flight; a communicator
+    registered after the trip is aborted at registration."""
+    from distributedtensorflow_amd.parallel.watchdog import CommWatchdog
+    wd = CommWatchdog(timeout_s=100, interval_s=0.02)
+    flag = threading.Event()
+    wd.add_probe(lambda: "cluster epoch moved" if flag.is_set() else None)
+    time.sleep(0.1)
+    assert wd.failed is None
+    flag.set()
+    assert wd.wait_tripped(2.0) and wd.failed == "cluster epoch moved"
+    late = []
+    wd.add_abort(lambda: late.append(1))
+    assert late == [1]
+    wd.stop()
+
+
+def test_errored_work_trips():
+    from distributedtensorflow_amd.parallel.watchdog import CommWatchdog
+    wd = CommWatchdog(timeout_s=100, interval_s=0.02)
+
+    def boom():
+        raise RuntimeError("NCCL error: remote process exited")
+    wd.watch(boom, "c10d all_reduce")
+    assert wd.wait_tripped(2.0) and "remote process exited" in wd.failed
+    wd.stop()
+
+
+def test_rccl_uid_key_restarts_with_each_world():
+    """a restarted rank and the survivors must agree on the unique-id store key."""
+    from distributedtensorflow_amd.parallel import comm
+    comm.reset_uid_index()
+    assert comm._next_uid_key() == "dtf/rccl_uid/0"
+    assert comm._next_uid_key() == "dtf/rccl_uid/1"
+    comm.reset_uid_index()               # what init_process_group_from_env does per world
+    assert comm._next_uid_key() == "dtf/rccl_uid/0"
+
+
+def test_session_refuses_to_continue_after_trip(monkeypatch):
+    """A step whose collective was aborted must not reach the hooks (the checkpoint saver)."""
+    from distributedtensorflow_amd.parallel import watchdog
+    from distributedtensorflow_amd.parallel.strategy import CommError
+    from distributedtensorflow_amd.train.session import MonitoredTrainingSession
+    wd = watchdog.reset_watchdog()
+    try:
+        sess = MonitoredTrainingSession(checkpoint_dir=None, save_checkpoint_secs=None,
+                                        save_summaries_steps=None, log_step_count_steps=None)
+        seen = []
+
+        def step():
+            wd.trip("injected: peer died mid-step")
+            seen.append(1)
+            return 1
+        with pytest.raises(CommError, match="peer died"):
+            sess.run(step)
+        assert seen == [1]
+    finally:
+        watchdog.reset_watchdog()
+
+
+def test_hung_peer_flagged_in_two_rank_gloo_world(tmp_path):
+    """2 ranks on gloo; rank 1 stays alive but never enters the all-reduce.  Rank 0's watchdog
+    flags the collective within DTF_COMM_TIMEOUT_S (2 s) and the next issue raises CommError."""
+    from distributedtensorflow_amd.cluster.launcher import free_ports
+    port = free_ports(1)[0]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1",
+                   PYTHONPATH=ROOT, DTF_COMM_TIMEOUT_S="2")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"),
+                                       "hung_peer", str(tmp_path)], env=env,
+                                      stdout=open(tmp_path / f"r{r}.log", "w"),
+                                      stderr=subprocess.STDOUT))
+    try:
+        for p in procs:
+            p.wait(timeout=120)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert procs[0].returncode == 0, open(tmp_path / "r0.log").read()[-3000:]
+    res = json.load(open(tmp_path / "wd.json"))
+    assert res["tripped"], res
+    assert 2.0 <= res["after_s"] < 8.0, res
+    assert res["error"] and "watchdog" in res["error"], res
+
+
+def test_bench_refuses_more_gpus_than_visible(tmp_path):
+    """bench.py never measures fewer GPUs than asked: --gpus 2 with fewer visible devices exits
+    non-zero quickly with the device-count message (here: a CPU box, 0 devices)."""
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("this box has >= 2 GPUs")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "1", "--warmup", "1"], env=env, capture_output=True,
+                       text=True, timeout=120, cwd=ROOT)
+    assert p.returncode != 0
+    assert "refusing to measure fewer GPUs" in p.stderr, p.stderr[-2000:]
+    assert time.time() - t0 < 60
+
+
+def test_bench_refuses_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "1", "--warmup", "1"], env=env, capture_output=True,
+                       text=True, timeout=120, cwd=ROOT)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr, p.stderr[-2000:]
