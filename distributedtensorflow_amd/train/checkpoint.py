@@ -278,12 +278,16 @@ def load_variable(ckpt, name):
 
 # ----------------------------------------------------------------------------- SavedModel
 
-def save_saved_model(export_dir, model, tags=("serve",), input_shape=None):
+def save_saved_model(export_dir, model, tags=("serve",), input_shape=None, seq_len=128):
     """SavedModel directory: ``saved_model.pb`` (inference GraphDef traced from the model, the
     saver subgraph and a ``serving_default`` signature; train/saved_model.py) +
     ``variables/variables.{index,data-00000-of-00001}``.  ``input_shape`` defaults to the
-    model's ``input_signature_shape`` (``None`` = the batch dimension)."""
-    from .saved_model import export_saved_model
+    model's ``input_signature_shape`` (``None`` = the batch dimension).  BERT models export
+    their own graph (token-id inputs of length ``seq_len``)."""
+    from .saved_model import export_bert_saved_model, export_saved_model
+    from ..models.bert import BertForPreTraining
+    if isinstance(model, BertForPreTraining):
+        return export_bert_saved_model(export_dir, model, seq_len, tags)
     shape = input_shape or getattr(model, "input_signature_shape", None)
     if shape is None:
         raise ValueError("save_saved_model needs input_shape= for this model")

@@ -348,8 +348,8 @@ def _saver_nodes(g, names_vals, handles):
     return prefix + ":0", "save/control_dependency:0", "save/restore_all"
 
 
-def _tensor_info(name, dims):
-    return pb.f_str(1, name) + pb.f_int(2, DT_FLOAT) + pb.f_msg(3, _shape(dims))
+def _tensor_info(name, dtype, dims):
+    return pb.f_str(1, name) + pb.f_int(2, dtype) + pb.f_msg(3, _shape(dims))
 
 
 def export_saved_model(export_dir, model, input_shape, tags=("serve",), input_name="images"):
@@ -358,13 +358,7 @@ def export_saved_model(export_dir, model, input_shape, tags=("serve",), input_na
     ``input_shape``: the model input with ``None`` for the batch dimension, e.g.
     ``(None, 784)`` for the MNIST models, ``(None, 224, 224, 3)`` for ResNet-50 (NHWC)."""
     from .. import ops
-    from .checkpoint import Saver
-    os.makedirs(os.path.join(export_dir, "variables"), exist_ok=True)
-    saver = Saver(model, write_meta_graph=False)
-    saver.save(save_path=os.path.join(export_dir, "variables", "variables"))
-    state = os.path.join(export_dir, "variables", "checkpoint")
-    if os.path.exists(state):
-        os.remove(state)
+    _write_variables(export_dir, model)
 
     tracer = Tracer(model)
     g = tracer.g
@@ -387,21 +381,214 @@ def export_saved_model(export_dir, model, input_shape, tags=("serve",), input_na
                       dtype=a_type(DT_FLOAT), shape=a_shape(val.shape))
             r = g.add("ReadVariableOp", f"{name}/Read/ReadVariableOp", [h], dtype=a_type(DT_FLOAT))
             tracer.var_nodes[name] = (h, r + ":0", val)
-    names_vals = sorted((n, v) for n, (_, _, v) in tracer.var_nodes.items())
-    fname, save_t, restore_op = _saver_nodes(g, names_vals, tracer.var_nodes)
+    out_dims = list(out.shape)
+    _write_saved_model(export_dir, g, tracer.var_nodes, tags,
+                       {input_name: (inp + ":0", DT_FLOAT, input_shape)},
+                       {"logits": (logits + ":0", DT_FLOAT, out_dims),
+                        "probabilities": (probs + ":0", DT_FLOAT, out_dims)})
+    return export_dir
 
+
+def _write_saved_model(export_dir, g, var_nodes, tags, inputs, outputs):
+    """saved_model.pb: MetaGraphDef{meta_info, graph_def (+ saver subgraph), saver_def,
+    signature_def{"serving_default": inputs -> outputs}}; ``inputs`` / ``outputs`` map a
+    signature key to (tensor name, dtype, dims)."""
+    names_vals = sorted((n, v) for n, (_, _, v) in var_nodes.items())
+    fname, save_t, restore_op = _saver_nodes(g, names_vals, var_nodes)
     meta_info = pb.f_str(1, "dtf-v1") + b"".join(pb.f_str(4, t) for t in tags) + \
         pb.f_str(5, "1.15.0") + pb.f_str(6, "distributedtensorflow_amd")
     saver_def = pb.f_str(1, fname) + pb.f_str(2, save_t) + pb.f_str(3, restore_op) + \
         pb.f_int(4, 5) + pb.f_bool(5, False) + pb.f_float(6, 10000.0) + pb.f_int(7, 2)
-    out_dims = list(out.shape)
-    sig = pb.f_map(1, {input_name: _tensor_info(inp + ":0", input_shape)},
+    sig = pb.f_map(1, {k: _tensor_info(*v) for k, v in inputs.items()},
                    lambda f, v: pb.f_msg(f, v)) + \
-        pb.f_map(2, {"logits": _tensor_info(logits + ":0", out_dims),
-                     "probabilities": _tensor_info(probs + ":0", out_dims)},
+        pb.f_map(2, {k: _tensor_info(*v) for k, v in outputs.items()},
                  lambda f, v: pb.f_msg(f, v)) + pb.f_str(3, PREDICT)
     meta = pb.f_msg(1, meta_info) + pb.f_msg(2, g.encode()) + pb.f_msg(3, saver_def) + \
         pb.f_map(5, {"serving_default": sig}, lambda f, v: pb.f_msg(f, v))
     with open(os.path.join(export_dir, "saved_model.pb"), "wb") as f:
         f.write(pb.f_int(1, 1) + pb.f_msg(2, meta))
+
+
+def _write_variables(export_dir, model):
+    from .checkpoint import Saver
+    os.makedirs(os.path.join(export_dir, "variables"), exist_ok=True)
+    Saver(model, write_meta_graph=False).save(
+        save_path=os.path.join(export_dir, "variables", "variables"))
+    state = os.path.join(export_dir, "variables", "checkpoint")
+    if os.path.exists(state):
+        os.remove(state)
+
+
+# ----------------------------------------------------------------------------- BERT
+
+class _BertGraph:
+    """Inference graph of :class:`~..models.bert.BertForPreTraining` in the op vocabulary of
+    google-research/bert's ``modeling.py`` (TF 1.15): GatherV2 embeddings, moments-style
+    LayerNorm (Mean / SquaredDifference / Rsqrt), per-head attention as Reshape + Transpose +
+    BatchMatMulV2 + Softmax with the additive -10000 key mask, tanh-GELU, and the MLM head
+    whose decoder is the word-embedding table (MatMul transpose_b).  The fused training kernels
+    (QKV in one GEMM, flash attention, bias+dropout+residual+LN) do not exist in TF: each is
+    lowered here to the stock ops computing the same function in inference mode."""
+
+    def __init__(self, model, seq_len):
+        from .checkpoint import to_tf_layout
+        self.model, self.cfg, self.S = model, model.cfg, int(seq_len)
+        if self.S > self.cfg.max_position_embeddings:
+            raise ValueError(f"seq_len {self.S} > max_position_embeddings")
+        self.g = GraphDef()
+        self.vals = {}
+        for name, t, layout in model.variables_tf():
+            self.vals[name] = to_tf_layout(t.detach().float().cpu(), layout).contiguous().numpy()
+        self.var_nodes = {}
+
+    # helpers
+    def var(self, name):
+        if name not in self.var_nodes:
+            val = self.vals[name]
+            h = self.g.add("VarHandleOp", name, container=a_str(""), shared_name=a_str(name),
+                           dtype=a_type(DT_FLOAT), shape=a_shape(val.shape))
+            r = self.g.add("ReadVariableOp", f"{name}/Read/ReadVariableOp", [h],
+                           dtype=a_type(DT_FLOAT))
+            self.var_nodes[name] = (h, r + ":0", val)
+        return self.var_nodes[name][1]
+
+    def op(self, op, name, inputs, **attrs):
+        return self.g.add(op, name, inputs, **attrs) + ":0"
+
+    def c(self, name, arr):
+        return self.g.const(name, arr) + ":0"
+
+    def f(self, op, name, *inputs, **attrs):
+        return self.op(op, name, list(inputs), T=a_type(DT_FLOAT), **attrs)
+
+    def reshape(self, x, shape, name="Reshape"):
+        return self.op("Reshape", name, [x, self.c(name + "/shape", np.array(shape, np.int32))],
+                       T=a_type(DT_FLOAT), Tshape=a_type(DT_INT32))
+
+    def transpose(self, x, perm, name="transpose"):
+        return self.op("Transpose", name, [x, self.c(name + "/perm", np.array(perm, np.int32))],
+                       T=a_type(DT_FLOAT), Tperm=a_type(DT_INT32))
+
+    def dense(self, x, scope, transpose_b=False, kernel=None, bias=None):
+        k = kernel or self.var(f"{scope}/kernel")
+        y = self.f("MatMul", f"{scope}/MatMul", x, k, transpose_a=a_bool(False),
+                   transpose_b=a_bool(transpose_b))
+        return self.f("BiasAdd", f"{scope}/BiasAdd", y, bias or self.var(f"{scope}/bias"),
+                      data_format=a_str("NHWC"))
+
+    def layer_norm(self, x, scope, eps):
+        axes = self.c(f"{scope}/moments/axes", np.array([-1], np.int32))
+        mean = self.op("Mean", f"{scope}/moments/mean", [x, axes], T=a_type(DT_FLOAT),
+                       Tidx=a_type(DT_INT32), keep_dims=a_bool(True))
+        sq = self.f("SquaredDifference", f"{scope}/moments/SquaredDifference", x, mean)
+        var = self.op("Mean", f"{scope}/moments/variance", [sq, axes], T=a_type(DT_FLOAT),
+                      Tidx=a_type(DT_INT32), keep_dims=a_bool(True))
+        ve = self.f("AddV2", f"{scope}/batchnorm/add", var,
+                    self.c(f"{scope}/batchnorm/add/y", np.array(eps, np.float32)))
+        rs = self.f("Rsqrt", f"{scope}/batchnorm/Rsqrt", ve)
+        sc = self.f("Mul", f"{scope}/batchnorm/mul", rs, self.var(f"{scope}/gamma"))
+        xs = self.f("Mul", f"{scope}/batchnorm/mul_1", x, sc)
+        ms = self.f("Mul", f"{scope}/batchnorm/mul_2", mean, sc)
+        sh = self.f("Sub", f"{scope}/batchnorm/sub", self.var(f"{scope}/beta"), ms)
+        return self.f("AddV2", f"{scope}/batchnorm/add_1", xs, sh)
+
+    def gelu(self, x, scope):
+        """0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))) -- modeling.py's gelu."""
+        x3 = self.f("Pow", f"{scope}/Pow", x, self.c(f"{scope}/Pow/y", np.array(3.0, np.float32)))
+        t = self.f("Mul", f"{scope}/mul", x3, self.c(f"{scope}/mul/x",
+                                                     np.array(0.044715, np.float32)))
+        t = self.f("AddV2", f"{scope}/add", x, t)
+        t = self.f("Mul", f"{scope}/mul_1", t, self.c(f"{scope}/mul_1/x",
+                                                      np.array(np.sqrt(2 / np.pi), np.float32)))
+        t = self.f("Tanh", f"{scope}/Tanh", t)
+        t = self.f("AddV2", f"{scope}/add_1", t, self.c(f"{scope}/add_1/x",
+                                                        np.array(1.0, np.float32)))
+        t = self.f("Mul", f"{scope}/mul_2", t, self.c(f"{scope}/mul_2/x",
+                                                      np.array(0.5, np.float32)))
+        return self.f("Mul", f"{scope}/mul_3", x, t)
+
+    def build(self):
+        cfg, S, H = self.cfg, self.S, self.cfg.hidden_size
+        nh, D = cfg.num_attention_heads, cfg.hidden_size // cfg.num_attention_heads
+        eps = cfg.layer_norm_eps
+        i32 = dict(dtype=a_type(DT_INT32), shape=a_shape([None, S]))
+        ids = self.g.add("Placeholder", "input_ids", **i32) + ":0"
+        tts = self.g.add("Placeholder", "token_type_ids", **i32) + ":0"
+        msk = self.g.add("Placeholder", "input_mask", **i32) + ":0"
+        self.inputs = {"input_ids": ids, "token_type_ids": tts, "input_mask": msk}
+        ax0 = self.c("bert/embeddings/axis", np.array(0, np.int32))
+        gather = dict(Tparams=a_type(DT_FLOAT), Tindices=a_type(DT_INT32),
+                      Taxis=a_type(DT_INT32))
+        word = self.var("bert/embeddings/word_embeddings")
+        e = self.op("GatherV2", "bert/embeddings/GatherV2", [word, ids, ax0], **gather)
+        t = self.op("GatherV2", "bert/embeddings/GatherV2_1",
+                    [self.var("bert/embeddings/token_type_embeddings"), tts, ax0], **gather)
+        pos = self.op("Slice", "bert/embeddings/Slice",
+                      [self.var("bert/embeddings/position_embeddings"),
+                       self.c("bert/embeddings/Slice/begin", np.array([0, 0], np.int32)),
+                       self.c("bert/embeddings/Slice/size", np.array([S, -1], np.int32))],
+                      T=a_type(DT_FLOAT), Index=a_type(DT_INT32))
+        e = self.f("AddV2", "bert/embeddings/add", e, t)
+        e = self.f("AddV2", "bert/embeddings/add_1", e, pos)
+        x = self.layer_norm(e, "bert/embeddings/LayerNorm", eps)
+        x = self.reshape(x, [-1, H], "bert/encoder/Reshape")
+        m = self.op("Cast", "bert/encoder/Cast", [msk], SrcT=a_type(DT_INT32),
+                    DstT=a_type(DT_FLOAT), Truncate=a_bool(False))
+        m = self.f("Sub", "bert/encoder/sub", self.c("bert/encoder/sub/x",
+                                                      np.array(1.0, np.float32)), m)
+        m = self.f("Mul", "bert/encoder/mul", m, self.c("bert/encoder/mul/y",
+                                                        np.array(-10000.0, np.float32)))
+        m = self.reshape(m, [-1, 1, 1, S], "bert/encoder/mask")
+        for li in range(cfg.num_hidden_layers):
+            pre = f"bert/encoder/layer_{li}"
+            heads = []
+            for nm in ("query", "key", "value"):
+                y = self.dense(x, f"{pre}/attention/self/{nm}")
+                y = self.reshape(y, [-1, S, nh, D], f"{pre}/attention/self/{nm}/Reshape")
+                heads.append(self.transpose(y, [0, 2, 1, 3], f"{pre}/attention/self/{nm}/T"))
+            q, k, v = heads
+            s = self.f("BatchMatMulV2", f"{pre}/attention/self/MatMul", q, k,
+                       adj_x=a_bool(False), adj_y=a_bool(True))
+            s = self.f("Mul", f"{pre}/attention/self/Mul", s,
+                       self.c(f"{pre}/attention/self/Mul/y",
+                              np.array(1.0 / np.sqrt(D), np.float32)))
+            s = self.f("AddV2", f"{pre}/attention/self/add", s, m)
+            p = self.f("Softmax", f"{pre}/attention/self/Softmax", s)
+            ctx = self.f("BatchMatMulV2", f"{pre}/attention/self/MatMul_1", p, v,
+                         adj_x=a_bool(False), adj_y=a_bool(False))
+            ctx = self.transpose(ctx, [0, 2, 1, 3], f"{pre}/attention/self/transpose_3")
+            ctx = self.reshape(ctx, [-1, H], f"{pre}/attention/self/Reshape_3")
+            a = self.dense(ctx, f"{pre}/attention/output/dense")
+            a = self.f("AddV2", f"{pre}/attention/output/add", a, x)
+            x = self.layer_norm(a, f"{pre}/attention/output/LayerNorm", eps)
+            h = self.gelu(self.dense(x, f"{pre}/intermediate/dense"), f"{pre}/intermediate/gelu")
+            o = self.dense(h, f"{pre}/output/dense")
+            o = self.f("AddV2", f"{pre}/output/add", o, x)
+            x = self.layer_norm(o, f"{pre}/output/LayerNorm", eps)
+        seq = self.reshape(x, [-1, S, H], "sequence_output")
+        tr = self.gelu(self.dense(x, "cls/predictions/transform/dense"),
+                       "cls/predictions/transform/gelu")
+        tr = self.layer_norm(tr, "cls/predictions/transform/LayerNorm", eps)
+        logits = self.dense(tr, "cls/predictions", transpose_b=True, kernel=word,
+                            bias=self.var("cls/predictions/output_bias"))
+        logits = self.reshape(logits, [-1, S, cfg.vocab_size], "mlm_logits")
+        probs = self.f("Softmax", "mlm_probabilities", logits)
+        self.outputs = {"sequence_output": (seq, [None, S, H]),
+                        "mlm_logits": (logits, [None, S, cfg.vocab_size]),
+                        "mlm_probabilities": (probs, [None, S, cfg.vocab_size])}
+        # every checkpoint variable gets a handle (restored by the saver even if unused)
+        for name in self.vals:
+            self.var(name)
+        return self
+
+
+def export_bert_saved_model(export_dir, model, seq_len=128, tags=("serve",)):
+    """SavedModel of a BERT masked-LM model: inputs ``input_ids`` / ``token_type_ids`` /
+    ``input_mask`` (int32 ``[batch, seq_len]``), outputs ``sequence_output`` and the MLM
+    ``mlm_logits`` / ``mlm_probabilities`` over every position."""
+    _write_variables(export_dir, model)
+    bg = _BertGraph(model, seq_len).build()
+    _write_saved_model(export_dir, bg.g, bg.var_nodes, tags,
+                       {k: (v, DT_INT32, [None, bg.S]) for k, v in bg.inputs.items()},
+                       {k: (t, DT_FLOAT, dims) for k, (t, dims) in bg.outputs.items()})
     return export_dir

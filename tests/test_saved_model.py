@@ -163,11 +163,40 @@ class Interpreter:
             k, s = a["ksize"][1], a["strides"][1]
             return F.max_pool2d(t(ins[0]).permute(0, 3, 1, 2), k, s).permute(0, 2, 3, 1).numpy()
         if op == "Mean":
-            return ins[0].mean(axis=tuple(int(i) for i in ins[1]))
+            return ins[0].mean(axis=tuple(int(i) for i in np.reshape(ins[1], -1)),
+                               keepdims=bool(a.get("keep_dims", False)))
         if op == "Reshape":
             return ins[0].reshape([int(s) for s in ins[1]])
         if op == "MatMul":
-            return ins[0] @ ins[1]
+            x = ins[0].T if a.get("transpose_a") else ins[0]
+            y = ins[1].T if a.get("transpose_b") else ins[1]
+            return x @ y
+        if op == "BatchMatMulV2":
+            x = np.swapaxes(ins[0], -1, -2) if a.get("adj_x") else ins[0]
+            y = np.swapaxes(ins[1], -1, -2) if a.get("adj_y") else ins[1]
+            return np.matmul(x, y)
+        if op == "GatherV2":
+            return np.take(ins[0], ins[1], axis=int(ins[2]))
+        if op == "Slice":
+            begin, size = [int(v) for v in ins[1]], [int(v) for v in ins[2]]
+            idx = tuple(slice(b, None if z == -1 else b + z) for b, z in zip(begin, size))
+            return ins[0][idx]
+        if op == "Transpose":
+            return np.transpose(ins[0], [int(v) for v in ins[1]])
+        if op == "Cast":
+            return ins[0].astype(DT[a["DstT"][1]])
+        if op == "Sub":
+            return ins[0] - ins[1]
+        if op == "Mul":
+            return ins[0] * ins[1]
+        if op == "SquaredDifference":
+            return (ins[0] - ins[1]) ** 2
+        if op == "Rsqrt":
+            return 1.0 / np.sqrt(ins[0])
+        if op == "Pow":
+            return np.power(ins[0], ins[1])
+        if op == "Tanh":
+            return np.tanh(ins[0])
         if op == "Softmax":
             e = np.exp(ins[0] - ins[0].max(-1, keepdims=True))
             return e / e.sum(-1, keepdims=True)
@@ -219,3 +248,55 @@ def test_saved_model_graph_serves_like_the_model(tmp_path, kind):
             "MatMul"} <= ops_used
     if kind == "resnet50":
         assert {"Conv2D", "FusedBatchNormV3", "MaxPool", "PadV2", "Mean", "AddV2"} <= ops_used
+
+
+def test_bert_saved_model_serves_like_the_model(tmp_path):
+    """a 2-layer BERT MLM model exported as a SavedModel (stock TF ops for the
+    fused training kernels: GatherV2 embeddings, moments LayerNorm, BatchMatMulV2 attention with
+    the -10000 key mask, tanh-GELU, tied decoder MatMul) executes in the independent
+    interpreter and reproduces the model's own inference logits at every position."""
+    from distributedtensorflow_amd.models.bert import BertConfig, BertForPreTraining
+    from distributedtensorflow_amd.train import save_saved_model
+    torch.manual_seed(0)
+    cfg = BertConfig(vocab_size=120, hidden_size=128, num_hidden_layers=2,
+                     num_attention_heads=2, intermediate_size=256, max_position_embeddings=64)
+    model = BertForPreTraining(cfg)
+    with torch.no_grad():               # non-trivial LN / bias parameters
+        for n, p in model.named_parameters():
+            if p.dim() == 1:
+                p.add_(0.1 * torch.randn_like(p))
+    model.eval()
+    B, S = 3, 16
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(0, cfg.vocab_size, (B, S), generator=g)
+    tt = torch.randint(0, 2, (B, S), generator=g)
+    mask = torch.ones(B, S, dtype=torch.int64)
+    mask[1, 11:] = 0
+    mask[2, 5:] = 0
+    with torch.no_grad():
+        want = model(ids, tt, mask).float().reshape(B, S, -1).numpy()
+    exp = save_saved_model(str(tmp_path / "bert"), model, seq_len=S)
+    graph = load_saved_model(exp)
+    it = Interpreter(graph)
+    prefix = os.path.join(exp, "variables", "variables")
+    fname, _, _ = graph["saver"]["filename"].partition(":")
+    it.run("^" + graph["saver"]["restore"], {(fname, 0): np.array([prefix], dtype=object)})
+    keys = set(BundleReader(prefix).keys()) - {""}
+    assert set(it.vars) == keys
+    sig = graph["signatures"]["serving_default"]
+    assert set(sig["inputs"]) == {"input_ids", "token_type_ids", "input_mask"}
+    feed = {(sig["inputs"][k].split(":")[0], 0): v.numpy().astype(np.int32)
+            for k, v in (("input_ids", ids), ("token_type_ids", tt), ("input_mask", mask))}
+    logits = it.run(sig["outputs"]["mlm_logits"], feed)
+    assert logits.shape == (B, S, cfg.vocab_size)
+    np.testing.assert_allclose(logits, want, rtol=2e-3, atol=2e-3)
+    seq = it.run(sig["outputs"]["sequence_output"], feed)
+    assert seq.shape == (B, S, cfg.hidden_size)
+    probs = it.run(sig["outputs"]["mlm_probabilities"], feed)
+    np.testing.assert_allclose(probs.sum(-1), 1.0, rtol=1e-5)
+    ops_used = {n["op"] for n in graph["nodes"].values()}
+    assert {"GatherV2", "BatchMatMulV2", "Softmax", "Tanh", "Rsqrt", "SquaredDifference",
+            "Transpose", "MatMul", "BiasAdd"} <= ops_used
+    # TF checkpoint names of modeling.py (query/key/value split out of the fused QKV kernel)
+    assert "bert/encoder/layer_1/attention/self/key/kernel" in keys
+    assert graph["nodes"]["cls/predictions/MatMul"]["attr"]["transpose_b"] is True
