@@ -307,7 +307,8 @@ class OwnerShard:
                 "master": self.master_desc, "mail": self.mail_desc, "numel": self.numel,
                 "ctl": self.ctl_name, "workers": self.worker_ranks,
                 "global_step": self.global_step, "pid": os.getpid(),
-                "host": socket.gethostname()}
+                "host": socket.gethostname(),
+                "device": self.device.index if self.device.type == "cuda" else None}
 
     # -- control-plane API shared with ps_service._Shard
     def flat_values(self):
@@ -520,6 +521,7 @@ class PSLink:
         self.w = int(worker_index)
         self.device = torch.device(device)
         self.ps_index = ps_index
+        check_peer_access(desc, self.device, ps_index)
         self.owner_master = open_shared(desc["master"], self.device)
         mail = open_shared(desc["mail"], self.device)
         n = int(desc["numel"])
@@ -529,8 +531,19 @@ class PSLink:
         self.timeout_ms = int(1000 * (timeout_s if timeout_s is not None else
                                       float(os.environ.get("DTF_PS_TIMEOUT_S", "600"))))
 
-    def copy_grads(self, space):
+    def _segments(self, lo=None, hi=None):
+        """This shard's (worker offset, owner offset, length) runs, clipped to the worker's flat
+        range [lo, hi) (one gradient / variable bucket)."""
         for wo, oo, n in self.plan["segments"]:
+            if lo is None:
+                yield wo, oo, n
+                continue
+            a, b = max(wo, lo), min(wo + n, hi)
+            if b > a:
+                yield a, oo + (a - wo), b - a
+
+    def copy_grads(self, space, lo=None, hi=None):
+        for wo, oo, n in self._segments(lo, hi):
             self.slot[oo:oo + n].copy_(space.grad[wo:wo + n], non_blocking=True)
 
     def post(self, step):
@@ -566,8 +579,8 @@ class PSLink:
                                       f"{self.timeout_ms / 1000:.0f} s (heartbeat "
                                       f"{self.ctl.heartbeat})")
 
-    def pull(self, space):
-        for wo, oo, n in self.plan["segments"]:
+    def pull(self, space, lo=None, hi=None):
+        for wo, oo, n in self._segments(lo, hi):
             space.master[wo:wo + n].copy_(self.owner_master[oo:oo + n], non_blocking=True)
             if space.shadow is not None:
                 space.shadow[wo:wo + n].copy_(space.master[wo:wo + n], non_blocking=True)
@@ -575,6 +588,23 @@ class PSLink:
     @property
     def global_step(self):
         return int(self.ctl.global_step)
+
+
+def check_peer_access(desc, device, ps_index=0):
+    """A worker on GPU a mapping the HBM shard of an owner on GPU b != a reads and writes it
+    over xGMI through the peer mapping ``hipIpcOpenMemHandle`` creates -- only possible when the
+    two devices are peers.  Check first (``hipDeviceCanAccessPeer``) and fail with the reason
+    instead of inside the IPC open or, worse, at the first copy."""
+    owner = desc.get("device")
+    if desc.get("master", {}).get("kind") != "ipc" or owner is None or device.type != "cuda":
+        return
+    mine = device.index if device.index is not None else torch.cuda.current_device()
+    if int(owner) == mine:
+        return
+    if not torch.cuda.can_device_access_peer(mine, int(owner)):
+        raise RuntimeError(f"parameter server {ps_index} keeps its shard on GPU {owner}, which "
+                           f"GPU {mine} cannot access as a peer (hipDeviceCanAccessPeer = 0): "
+                           f"put the PS task on a peer GPU, or use data_plane='gloo'")
 
 
 def sync_device(device):

@@ -80,23 +80,28 @@ def run_task(args):
         opt.minimize(loss)
         return loss
 
+    reducer = opt._reducer
+    timings = dict(client.timing)
+    timings.update(getattr(reducer, "timing", {}))
     for _ in range(args.warmup):
         loss = step()
+    opt.synchronize_variables()          # the pipelined push in flight completes
     sync()
-    for v in client.timing.values():
+    for v in timings.values():
         v.clear()
     import torch.distributed as dist
     dist.barrier(group=server.worker_group)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+    opt.synchronize_variables()          # inside the timed region: the last push is answered
     sync()
     elapsed = time.perf_counter() - t0
-    n = max(len(client.timing.get("wait_ms", [])), 1)
     rec = {"worker": args.task_index, "elapsed_s": elapsed, "steps": args.steps,
            "batch": args.batch, "loss": float(loss), "device": str(dev),
            "global_step": client.global_step, "data_plane": client.data_plane_in_use,
-           **{f"{k}_per_step": round(sum(v) / n, 3) for k, v in client.timing.items()}}
+           "pipelined": bool(getattr(reducer, "_pipe", False)),
+           **{f"{k}_per_step": round(sum(v) / max(len(v), 1), 3) for k, v in timings.items()}}
     with open(os.path.join(args.out_dir, f"worker{args.task_index}.json"), "w") as f:
         json.dump(rec, f)
     client.stop()
@@ -130,7 +135,8 @@ def run_launcher(args, metric_note=""):
     imgs = sum(r["steps"] * r["batch"] for r in recs)
     ips = imgs / span
     per = {k: round(sum(r.get(k, 0.0) for r in recs) / len(recs), 3)
-           for k in ("copy_sync_ms_per_step", "wait_ms_per_step", "pull_ms_per_step")}
+           for k in ("copy_sync_ms_per_step", "wait_ms_per_step", "pull_ms_per_step",
+                     "fence_ms_per_step", "answer_ms_per_step")}
     applied = max(int(ps.get("applied", 0)), 1)
     rec = {"metric": "images/sec ResNet-50 async parameter server (between-graph, 1 PS + "
                      f"{args.num_workers} workers)",
@@ -144,6 +150,7 @@ def run_launcher(args, metric_note=""):
                       "parallelism": f"ps1+async{args.num_workers}",
                       "optimizer": "momentum0.9+wd1e-4 applied on the PS (Hogwild)",
                       "data_plane": recs[0]["data_plane"],
+                      "pipelined_push_pull": all(r.get("pipelined") for r in recs),
                       "worker_devices": [r["device"] for r in recs],
                       "worker_host_ms_per_step": per,
                       "ps_apply_ms_mean": round(1e3 * float(ps.get("apply_s", 0.0)) / applied, 3),

@@ -389,7 +389,9 @@ def test_bench_ps_async_flow_cpu(tmp_path):
     assert cfg["ps_applied"] == cfg["ps_pushes"] == 2 * (2 + 1)       # nothing dropped
     assert cfg["final_global_step"] == 6 and rec["value"] > 0
     assert set(cfg["worker_host_ms_per_step"]) == {"copy_sync_ms_per_step", "wait_ms_per_step",
-                                                   "pull_ms_per_step"}
+                                                   "pull_ms_per_step", "fence_ms_per_step",
+                                                   "answer_ms_per_step"}
+    assert cfg["pipelined_push_pull"] is False         # the shm plane on CPU stays serial
 
 
 @pytest.mark.parametrize("kind,args", [("mirrored", ("bucket_mb=0.05",)),

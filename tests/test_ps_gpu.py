@@ -79,3 +79,55 @@ def test_ps_killed_on_gpu_restarts_and_resumes(tmp_path):
     m = re.search(r"Close Parameter Server \.\.\. (\{.*\})", text["ps0"])
     stats = ast.literal_eval(m.group(1))
     assert stats["data_plane"] == "ipc" and stats["global_step"] >= 60   # the restarted PS
+
+
+def test_ps_async_bench_four_workers_concurrent_applies(tmp_path):
+    """1 PS + 4 workers on the GPU data plane, pipelined push/pull (bucket
+    pushes from the backward hooks, post/answer on a comm thread, per-bucket pull fences).  The
+    owner runs applies of different workers concurrently on their own streams (Hogwild,
+    ps_max_inflight_applies >= 2), applies every push (no drops) and the final global step
+    counts every push of every worker."""
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--strategy", "ps_async",
+                        "--num-workers", "4", "--batch", "8", "--image-size", "64", "--steps",
+                        "8", "--warmup", "2", "--timeout", "150"],
+                       env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2"),
+                       capture_output=True, text=True, timeout=200, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = rec["config"]
+    assert cfg["data_plane"] == "ipc" and cfg["pipelined_push_pull"] is True
+    assert cfg["ps_applied"] == cfg["ps_pushes"] == 4 * (8 + 2)
+    assert cfg["final_global_step"] == 4 * (8 + 2)
+    assert cfg["ps_max_inflight_applies"] >= 2, cfg
+    assert rec["value"] > 0
+
+
+@pytest.mark.parametrize("pipeline", ["0", "1"])
+def test_pipelined_push_pull_matches_serial_one_worker(tmp_path, pipeline):
+    """With ONE async worker the run is deterministic: the pipelined data plane must train
+    exactly like the serial one (same pushes, same pulls, same order) -- final variables equal
+    bit for bit to the serial run's."""
+    from distributedtensorflow_amd.cluster.launcher import launch_local
+    from distributedtensorflow_amd.train.checkpoint import latest_checkpoint, load_variable
+    outs = {}
+    for mode in ("0", pipeline):
+        d = tmp_path / f"p{mode}_{len(outs)}"
+        codes, logs = launch_local(os.path.join(ROOT, "run_mnist_distributed.py"), 1, 1, str(d),
+                                   ["--max_steps=40", f"--data_dir={tmp_path}/data",
+                                    f"--log_dir={d}/tb", "--ps_device=gpu",
+                                    f"--checkpoint_dir={d}/ckpt", "--save_checkpoint_steps=1000"],
+                                   env={"PYTHONPATH": ROOT, "DTF_PS_PIPELINE": mode},
+                                   timeout_s=100, grace_s=20)
+        text = {k: open(v).read() for k, v in logs.items()}
+        assert all(c == 0 for c in codes.values()), {k: t[-2500:] for k, t in text.items()}
+        last = latest_checkpoint(str(d / "ckpt"))
+        outs[len(outs)] = {n: load_variable(last, n) for n in
+                           ("conv2d/kernel", "conv2d_1/kernel", "dense/kernel", "dense_1/bias",
+                            "global_step")}
+    a, b = outs[0], outs[1]
+    assert int(a["global_step"]) == int(b["global_step"]) >= 40
+    for k in a:
+        assert (a[k] == b[k]).all(), k
