@@ -166,6 +166,7 @@ void dtf_attn_bwd(const bf16_t*, const float*, const bf16_t*, const bf16_t*, con
                   bf16_t*, int, int, int, float, float, uint32_t, hipStream_t);
 int dtf_pos_type_grad_ws_floats(int, int, int);
 void dtf_attn_set_wide(int);
+void dtf_attn_set_fused(int);
 void dtf_pos_type_grad(const bf16_t*, const int64_t*, int, int, int, int, float*, float*, float*,
                        hipStream_t);
 void dtf_segment_sum(const int64_t*, const int64_t*, const bf16_t*, float*, int, int,
@@ -787,6 +788,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("attn_bwd");
   });
   m.def("attn_set_wide", &dtf_attn_set_wide);
+  m.def("attn_set_fused", &dtf_attn_set_fused);
   m.def("pos_type_grad_ws_floats", &dtf_pos_type_grad_ws_floats);
   m.def("pos_type_grad", [](uintptr_t ds, uintptr_t tt, int B, int S_, int H, int NT,
                             uintptr_t dpos, uintptr_t dtyp, uintptr_t ws, uintptr_t st) {

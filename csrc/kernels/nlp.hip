@@ -855,6 +855,162 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mas
   for (int dt = 0; dt < 4; ++dt) store4_scaled(dqrow + 16 * dt + 4 * gq, dq[dt], g.scale);
 }
 
+// Fused backward for S == 128 (BERT-base at seq 128): ONE 8-wave block per (b, h) holds the whole
+// sequence -- Q, K, V and dO staged once in LDS -- and forms dQ, dK and dV in two phases:
+//   1. wave w, queries 16w..16w+15 (the dQ kernel's work over all 128 keys): S = Q K^T and
+//      dP = dO V^T per 16-key group, P = exp(S - lse) (+ dropout), dS = P (dP - delta),
+//      dQ = dS K; P (dropped) and dS are kept, rounded to bf16 exactly as the split kernels'
+//      fragments round them;
+//   2. after a barrier P and dS go to LDS as [query][key] tiles (P over the dead K|V region) and
+//      wave w takes keys 16w..16w+15: dV = P^T dO, dK = dS^T Q, reading P / dS columns with the
+//      same transposing ds_read_b64_tr_b16 fragments the dK/dV kernel builds in registers.
+// Against dQ + dK/dV as two kernels this drops the second Q K^T and dO V^T (5 instead of 7
+// 128 x 128 x 64 products per (b, h)) and the second read of Q / K / V / dO; every accumulator
+// sums in the same order as before, so the gradients are bit-identical to the split kernels.
+constexpr int kFusedS = 128, kPLD = 136;   // P / dS row pitch (272 B: 8-B aligned rows)
+constexpr int kFusedLds = (4 * kFusedS * ALD + kFusedS * kPLD) * 2 + kFusedS * 4;   // 109,056 B
+
+DTF_DEV bf16x8_t lds_tr8_p(const bf16_t* base, int row0, int col0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const bf16_t* p = base + (row0 + 4 * g + (i >> 2)) * kPLD + col0 + 4 * (i & 3);
+  const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(p));
+  const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(p + 16 * kPLD));
+  return (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <bool DROP>
+__global__ void __launch_bounds__(512)
+attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                         const bf16_t* __restrict__ dO, const float* __restrict__ lse,
+                         float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom g,
+                         const bf16_t* __restrict__ O) {
+  constexpr int S = kFusedS;
+  static_assert(S * kPLD <= 2 * S * ALD, "P must fit over the K|V region");
+  extern __shared__ __attribute__((aligned(16))) bf16_t fsm[];    // kFusedLds bytes (dynamic)
+  bf16_t* Qs = fsm;
+  bf16_t* Os = Qs + S * ALD;                 // dO
+  bf16_t* KV = Os + S * ALD;                 // K | V, then P
+  bf16_t* dSs = KV + 2 * S * ALD;
+  float* Ms = reinterpret_cast<float*>(dSs + S * kPLD);
+  bf16_t* Ks = KV;
+  bf16_t* Vs = KV + S * ALD;
+  bf16_t* Ps = KV;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = lane >> 4, li = lane & 15;
+  const int h = blockIdx.x, b = blockIdx.y, H = g.H;
+  const long tok0 = (long)b * S, bh = (long)b * H + h;
+  // ---- stage Q, K, V, dO (4 x 1024 16-B chunks over 512 threads) and the key mask
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int v = tid + 512 * i;
+    const int sel = v >> 10, row = (v >> 3) & (S - 1), cc = (v & 7) * 8;
+    const bf16_t* src = sel == 3 ? dO + (tok0 + row) * (long)(H * AD) + h * AD + cc
+                                 : qkv + (tok0 + row) * g.ld + (sel * H + h) * AD + cc;
+    bf16_t* dst = (sel == 0 ? Qs : sel == 1 ? Ks : sel == 2 ? Vs : Os) + row * ALD + cc;
+    *(uint4*)dst = *(const uint4*)src;
+  }
+  if (tid < S) Ms[tid] = mask ? mask[tok0 + tid] * kLog2e : 0.f;
+  // ---- this lane's query q: lse and delta = O . dO (global reads, as the dQ kernel)
+  const int q = w * 16 + li;
+  const float lq = lse[bh * S + q];
+  float dl = 0.f;
+  {
+    const bf16_t* oq = O + (tok0 + q) * (long)(H * AD) + h * AD;
+    const bf16_t* dq_ = dO + (tok0 + q) * (long)(H * AD) + h * AD;
+    float fo[8], fd[8];
+    unpack8(*(const uint4*)(oq + 8 * gq), fo);
+    unpack8(*(const uint4*)(dq_ + 8 * gq), fd);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dl += fo[e] * fd[e];
+    unpack8(*(const uint4*)(oq + 32 + 8 * gq), fo);
+    unpack8(*(const uint4*)(dq_ + 32 + 8 * gq), fd);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dl += fo[e] * fd[e];
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    if (gq == 0) delta[bh * S + q] = dl;
+  }
+  __syncthreads();
+  // ---- phase 1: this wave's 16 queries against all 128 keys
+  const bf16x8_t bq0 = lds_row8(Qs, q, 8 * gq), bq1 = lds_row8(Qs, q, 32 + 8 * gq);
+  const bf16x8_t bo0 = lds_row8(Os, q, 8 * gq), bo1 = lds_row8(Os, q, 32 + 8 * gq);
+  const float c = g.scale * kLog2e;
+  const uint32_t kbase = (uint32_t)((bh * S + q) * S);
+  f32x4_t P[8], dS[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    f32x4_t s = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dp = s;
+    s = mfma(lds_row8(Ks, 16 * t + li, 8 * gq), bq0, s);
+    s = mfma(lds_row8(Ks, 16 * t + li, 32 + 8 * gq), bq1, s);
+    dp = mfma(lds_row8(Vs, 16 * t + li, 8 * gq), bo0, dp);
+    dp = mfma(lds_row8(Vs, 16 * t + li, 32 + 8 * gq), bo1, dp);
+    mfma_fence();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = 16 * t + 4 * gq + r;
+      const float p = exp2f(s[r] * c + Ms[key] - lq);
+      if (DROP) {
+        const bool kp = keep_elem(g.seed, kbase + key, g.thr);
+        P[t][r] = kp ? p * g.inv_keep : 0.f;
+        dS[t][r] = p * ((kp ? dp[r] * g.inv_keep : 0.f) - dl);
+      } else {
+        P[t][r] = p;
+        dS[t][r] = p * (dp[r] - dl);
+      }
+    }
+  }
+  f32x4_t acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8_t bS = pack_frag(dS[2 * ks], dS[2 * ks + 1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(lds_tr8(Ks, 32 * ks, 16 * dt, lane), bS, acc[dt]);
+  }
+  mfma_fence();
+  {
+    bf16_t* dqrow = dqkv + (tok0 + q) * g.ld + h * AD;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) store4_scaled(dqrow + 16 * dt + 4 * gq, acc[dt], g.scale);
+  }
+  __syncthreads();                 // every wave is done with K and V: P may overwrite them
+  // ---- P and dS to LDS as [query][key]: this lane's 4 consecutive keys of each group
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int off = q * kPLD + 16 * t + 4 * gq;
+    const uint2 pv = {(uint32_t)f2bf(P[t][0]) | ((uint32_t)f2bf(P[t][1]) << 16),
+                      (uint32_t)f2bf(P[t][2]) | ((uint32_t)f2bf(P[t][3]) << 16)};
+    const uint2 sv = {(uint32_t)f2bf(dS[t][0]) | ((uint32_t)f2bf(dS[t][1]) << 16),
+                      (uint32_t)f2bf(dS[t][2]) | ((uint32_t)f2bf(dS[t][3]) << 16)};
+    *(uint2*)(Ps + off) = pv;
+    *(uint2*)(dSs + off) = sv;
+  }
+  __syncthreads();
+  // ---- phase 2: this wave's 16 keys against all 128 queries
+  const int k = w * 16 + li;
+  f32x4_t dv[4], dk[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dv[dt] = dk[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8_t bP = lds_tr8_p(Ps, 32 * ks, 16 * w, lane);
+    const bf16x8_t bS = lds_tr8_p(dSs, 32 * ks, 16 * w, lane);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dv[dt] = mfma(lds_tr8(Os, 32 * ks, 16 * dt, lane), bP, dv[dt]);
+      dk[dt] = mfma(lds_tr8(Qs, 32 * ks, 16 * dt, lane), bS, dk[dt]);
+    }
+  }
+  mfma_fence();
+  bf16_t* dkrow = dqkv + (tok0 + k) * g.ld + (H + h) * AD;
+  bf16_t* dvrow = dqkv + (tok0 + k) * g.ld + (2 * H + h) * AD;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    store4_scaled(dkrow + 16 * dt + 4 * gq, dk[dt], g.scale);
+    store4_scaled(dvrow + 16 * dt + 4 * gq, dv[dt], 1.f);
+  }
+}
+
 // ----------------------------------------------------------------------------- embeddings
 // out[ids_sorted[i]] = sum over the run of equal ids of src[perm[j]]  (one wave per run start)
 __global__ void __launch_bounds__(256)
@@ -1081,10 +1237,32 @@ void dtf_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse,
   else attn_fwd_launch<4, 64>(qkv, mask, out, lse, g, st);
 }
 
+// 1 (default): S == 128 runs the fused one-block-per-(b, h) backward
+static int g_attn_fused = 1;
+void dtf_attn_set_fused(int v) { g_attn_fused = v; }
+
 void dtf_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* out, const bf16_t* dout,
                   const float* lse, float* delta, bf16_t* dqkv, int B, int S, int H, float scale,
                   float p, uint32_t seed, hipStream_t st) {
   const AttnGeom g = attn_geom(B, S, H, scale, p, seed);
+  if (g_attn_fused && S == kFusedS) {
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_fused128_kernel<true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLds));
+      HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_fused128_kernel<false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLds));
+      attr = true;
+    }
+    const dim3 grid(H, B);
+    if (g.thr)
+      hipLaunchKernelGGL(attn_bwd_fused128_kernel<true>, grid, dim3(512), kFusedLds, st, qkv,
+                         mask, dout, lse, delta, dqkv, g, out);
+    else
+      hipLaunchKernelGGL(attn_bwd_fused128_kernel<false>, grid, dim3(512), kFusedLds, st, qkv,
+                         mask, dout, lse, delta, dqkv, g, out);
+    return;
+  }
   if (g_attn_wide && S % 128 == 0)
     attn_bwd_launch<8, 128>(qkv, mask, out, dout, lse, delta, dqkv, g, st);
   else

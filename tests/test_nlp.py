@@ -252,6 +252,35 @@ def test_attention_wide_blocks_bit_identical(p):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_fused_bwd_bit_identical(p):
+    """S == 128: the fused one-block-per-(b, h) backward (dQ, dK, dV from one staging of Q / K /
+    V / dO) == the split dQ + dK/dV kernels bit for bit -- every accumulator sums in the same
+    order and P / dS are rounded to bf16 the same way -- with a padded key mask and dropout."""
+    from distributedtensorflow_amd.ops import native
+    torch.manual_seed(0)
+    B, S, H = 5, 128, 3
+    qkv = torch.randn(B * S, 3 * H * 64, device="cuda").bfloat16().requires_grad_(True)
+    mask = torch.zeros(B, S, device="cuda")
+    mask[1, S - 50:] = -10000.0
+    mask[4, 7:] = -10000.0
+    dy = torch.randn(B * S, H * 64, device="cuda").bfloat16()
+    outs = []
+    for fused in (1, 0):
+        native._K.attn_set_fused(fused)
+        try:
+            torch.manual_seed(5)
+            y = ops.attention_qkv(qkv, mask, B, S, H, p, True)
+            (g,) = torch.autograd.grad(y, [qkv], dy)
+            torch.cuda.synchronize()
+        finally:
+            native._K.attn_set_fused(1)
+        outs.append((y, g))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.gpu
 def test_mlm_loss_gpu():
     torch.manual_seed(0)
     N, V = 80, 30522
