@@ -141,6 +141,7 @@ void dtf_gemm_stream_probe(const bf16_t*, const bf16_t*, bf16_t*, int, int, int,
 void dtf_gemm_stream_pre(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, const float*,
                          const float*, bf16_t*, float*, hipStream_t);
 void dtf_gemm_set_stagger(int, int);
+void dtf_gemm_set_group(int);
 int dtf_wgrad_get_pipe();
 void dtf_lds_probe(int, int, int*, int, hipStream_t);
 int dtf_max_dynamic_lds(int);
@@ -715,6 +716,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("gemm_stream_bnb");
   });
   m.def("gemm_set_stagger", &dtf_gemm_set_stagger);
+  m.def("gemm_set_group", &dtf_gemm_set_group);
   m.def("wgrad_get_pipe", &dtf_wgrad_get_pipe);
   m.def("lds_probe", [](int bytes, int blocks, uintptr_t errors, int spin, uintptr_t st) {
     dtf_lds_probe(bytes, blocks, P<int>(errors), spin, S(st));

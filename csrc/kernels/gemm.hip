@@ -55,6 +55,7 @@ struct GemmArgs {
   const float* gelu_b;
   float* colsum;
   int ncu;                          // OCC 2 kernels: compute units (the first resident round)
+  int group_m;                      // > 0: grouped tile order (GM M-panels x all N per group)
   int stagger_mode, stagger;        // OCC 2: which first-round blocks start late, by how much
 };
 
@@ -124,7 +125,20 @@ gemm_nt_kernel(const GemmArgs g) {
   const int tiles_n = (g.N + BN - 1) / BN;
   const int tiles_m = (g.M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, tiles_n * tiles_m);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  // default order: N-tile fastest (consecutive blocks of an XCD share the A panel).  Grouped
+  // (group_m = GM): within groups of GM M-panels the M index runs fastest, so the ~32 blocks an
+  // XCD runs at once cover a GM x (32 / GM) patch of tiles -- fewer distinct A + B panels per
+  // round than 32 / tiles_n x tiles_n when B (tiles_n panels) does not fit the XCD's L2.
+  int tm, tn;
+  if (g.group_m > 0) {
+    const int per = g.group_m * tiles_n, grp = bid / per, first = grp * g.group_m;
+    const int gm = min(g.group_m, tiles_m - first), r = bid - grp * per;
+    tm = first + r % gm;
+    tn = r / gm;
+  } else {
+    tm = bid / tiles_n;
+    tn = bid % tiles_n;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (g.K + BK - 1) / BK;
   if constexpr (OCC == 2) {
@@ -1108,6 +1122,7 @@ int g_gemm_nt = 0;         // non-temporal C stores (ResNet-50 A/B: neutral; off
 int g_gemm_dbg = 0;        // GemmArgs::dbg for timing probes
 
 int g_gemm_stagger_mode = 1, g_gemm_stagger = -1;   // OCC 2 start stagger (-1: auto)
+int g_gemm_group = 0;      // grouped tile order (GemmArgs::group_m) for the non-conv GEMMs
 
 template <int BM, int BN, int BK, int NS, int SCHED = 0, int NW = 8, int PP_PRIO = 1,
           int CONV = 0, int OCC = 1>
@@ -1126,6 +1141,7 @@ void launch_gemm(const GemmArgs& g0, hipStream_t st) {
   }
   static_assert(OCC == 1 || 2 * Cf::LDS <= 160 * 1024, "OCC 2: two blocks' LDS per CU");
   GemmArgs g = g0;
+  if (!CONV) g.group_m = g_gemm_group;
   const long tiles = (long)((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   if (OCC == 2) {
     g.ncu = ncu;
@@ -1146,6 +1162,7 @@ void dtf_gemm_set_pp(int v) { g_gemm_pp = v; }
 void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
 void dtf_gemm_set_dbg(int v) { g_gemm_dbg = v; }
 void dtf_gemm_set_stagger(int mode, int iters) { g_gemm_stagger_mode = mode; g_gemm_stagger = iters; }
+void dtf_gemm_set_group(int gm) { g_gemm_group = gm < 0 ? 0 : gm; }
 
 // Implicit-GEMM convolution on the ping-pong GEMM: Y[M = N*P*Q][Kout] (+= Cin / masked acc)
 // = X (through the tap table) . Wt[Kout][Kpad]^T, Kpad = taps * C, C % 64 == 0, <= 9 taps.
