@@ -247,14 +247,31 @@ class _PushJob:
             raise self._error
 
 
+class _CommThread:
+    """One DAEMON thread running the pipelined pushes in order (a ThreadPoolExecutor's workers
+    are joined at interpreter exit: a push whose answer never comes would hang the exit)."""
+
+    def __init__(self):
+        import queue
+        self.q = queue.Queue()
+        self.t = threading.Thread(target=self._run, name="dtf-ps-push", daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            self.q.get()()
+
+    def submit(self, fn):
+        self.q.put(fn)
+
+
 _POOL = None
 
 
 def _comm_pool():
     global _POOL
     if _POOL is None:
-        from concurrent.futures import ThreadPoolExecutor
-        _POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dtf-ps-push")
+        _POOL = _CommThread()
     return _POOL
 
 

@@ -506,6 +506,9 @@ class MonitoredTrainingSession:
             self._closed = True
             client = getattr(self.strategy, "ps_client", None)
             if client is not None and client.params is not None:
+                opt = self.scaffold.optimizer
+                if opt is not None and getattr(opt, "space", None) is not None:
+                    opt.synchronize_variables()     # the pipelined push in flight is answered
                 client.stop()
             if self._writer is not None:
                 self._writer.close()
