@@ -62,7 +62,10 @@ class GraphedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         optimizer._capturing = True
         try:
-            with torch.cuda.graph(self.graph):
+            # captured on the warm-up stream: the parameters' AccumulateGrad nodes were created
+            # there, and a capture on another stream makes autograd warn that the node's stream
+            # does not match
+            with torch.cuda.graph(self.graph, stream=side):
                 self.static_out = step_fn(*self.static_inputs)
         finally:
             optimizer._capturing = False
