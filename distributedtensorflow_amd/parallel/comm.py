@@ -184,9 +184,22 @@ class RcclComm:
             self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), _OPS[op], s), t,
             what="all_reduce")
 
+    @staticmethod
+    def _overlap(a, b):
+        ea, eb = a.element_size(), b.element_size()
+        return a.data_ptr() < b.data_ptr() + b.numel() * eb and \
+            b.data_ptr() < a.data_ptr() + a.numel() * ea
+
     def reduce_scatter(self, out, inp, op="sum"):
         if inp.numel() != out.numel() * self.world:
             raise ValueError("rccl reduce_scatter: input must be world x output")
+        # NCCL's in-place rule: an output inside the input must be exactly this rank's chunk
+        # (recvbuff == sendbuff + rank * recvcount); any other overlap is undefined behaviour
+        # that a world-1 run can never show (the colocated PS reduces in place)
+        if self._overlap(out, inp) and out.data_ptr() != \
+                inp.data_ptr() + self.rank * out.numel() * out.element_size():
+            raise ValueError("rccl reduce_scatter: in-place output must be the input's chunk "
+                             f"{self.rank} (recvbuff == sendbuff + rank * count)")
         return self._issue(lambda s: self.K.rccl_reduce_scatter(
             self.comm, inp.data_ptr(), out.data_ptr(), out.numel(), self._dt(out), _OPS[op], s),
             out, inp, what="reduce_scatter")
@@ -194,6 +207,10 @@ class RcclComm:
     def all_gather(self, out, inp):
         if out.numel() != inp.numel() * self.world:
             raise ValueError("rccl all_gather: output must be world x input")
+        if self._overlap(out, inp) and inp.data_ptr() != \
+                out.data_ptr() + self.rank * inp.numel() * inp.element_size():
+            raise ValueError("rccl all_gather: in-place input must be the output's chunk "
+                             f"{self.rank} (sendbuff == recvbuff + rank * count)")
         return self._issue(lambda s: self.K.rccl_all_gather(
             self.comm, inp.data_ptr(), out.data_ptr(), inp.numel(), self._dt(inp), s), out, inp,
             what="all_gather")

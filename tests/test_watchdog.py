@@ -160,3 +160,43 @@ def test_bench_refuses_world_size_mismatch():
                         "--steps", "1", "--warmup", "1"], env=env, capture_output=True,
                        text=True, timeout=120, cwd=ROOT)
     assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr, p.stderr[-2000:]
+
+
+def _fake_rccl(rank, world):
+    """An RcclComm whose kernel calls are recorded instead of issued (no GPU / RCCL needed)."""
+    from distributedtensorflow_amd.parallel.comm import RcclComm
+    from distributedtensorflow_amd.parallel.watchdog import CommWatchdog
+
+    class K:
+        calls = []
+
+        def __getattr__(self, name):
+            return lambda *a: K.calls.append((name, a))
+    c = object.__new__(RcclComm)
+    c.K, c.rank, c.world, c.comm = K(), rank, world, 1
+    c.wd = CommWatchdog(timeout_s=100)
+    c._issue = lambda fn, *t, what="": fn(0)
+    return c, K.calls
+
+
+def test_rccl_in_place_rules_of_the_sharded_ps():
+    """The colocated PS reduce-scatters / all-gathers IN PLACE on flat-buffer views.  NCCL
+    defines in-place only for recvbuff == sendbuff + rank * count (reduce-scatter) and sendbuff ==
+    recvbuff + rank * count (all-gather); at world 1 every layout passes, so the rule is checked
+    on the host for world 8: the reducer's layout is accepted at every rank, a shifted one is
+    refused."""
+    W, c = 8, 96
+    g = torch.zeros(4 * W * c)
+    s = 64                                      # a bucket starting inside the flat buffer
+    bucket = g[s:s + W * c]
+    for r in range(W):
+        comm, calls = _fake_rccl(r, W)
+        comm.reduce_scatter(g[s + r * c:s + (r + 1) * c], bucket)
+        comm.all_gather(bucket, g[s + r * c:s + (r + 1) * c])
+        assert [n for n, _ in calls] == ["rccl_reduce_scatter", "rccl_all_gather"]
+    comm, _ = _fake_rccl(3, W)
+    with pytest.raises(ValueError, match="chunk 3"):
+        comm.reduce_scatter(g[s + 2 * c:s + 3 * c], bucket)
+    with pytest.raises(ValueError, match="chunk 3"):
+        comm.all_gather(bucket, g[s + 4 * c:s + 5 * c])
+    comm.reduce_scatter(torch.zeros(c), bucket)            # disjoint buffers: always fine

@@ -11,3 +11,6 @@ DTF_ATTN_FUSED_BWD=0 timeout -k 10 200 python bench.py --model bert_base > gpuru
 timeout -k 10 200 python bench.py > gpurun_out/r4_bench_resnet.json 2> gpurun_out/r4_bench_resnet.err && \
 timeout -k 10 500 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_recovery_gpu.py tests/test_bench_multirank_gpu.py tests/test_ps_gpu.py > gpurun_out/r4_t1.log 2>&1 && \
 timeout -k 10 300 python bench.py --strategy ps_async --num-workers 2 > gpurun_out/r4_bench_psasync2.json 2> gpurun_out/r4_bench_psasync2.err
+[ $? -eq 0 ] || exit 1
+PROF_NAME=r4_bert SKIP_TORCH=1 DTF_BENCH_ARGS="--model bert_base" bash tools/prof_bench.sh && \
+PROF_NAME=r4_resnet SKIP_TORCH=1 DTF_BENCH_ARGS="" bash tools/prof_bench.sh
