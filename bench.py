@@ -339,6 +339,15 @@ def check_devices(n):
              f"than requested")
 
 
+def _die_with_parent():
+    """Child side of the fork, before exec (no GPU touched): PR_SET_PDEATHSIG = SIGKILL."""
+    import ctypes
+    try:
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL)
+    except OSError:
+        pass
+
+
 def self_launch(args):
     """``--gpus N`` (N > 1) without torchrun env: start the N rank processes here (one per GPU,
     torchrun's env contract: RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_*),
@@ -354,8 +363,10 @@ def self_launch(args):
                                                                            else r),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), DTF_BENCH_LAUNCH="self")
+        # same process group as this launcher (a driver's group kill reaches the ranks) and a
+        # parent-death signal (a launcher killed outright takes its ranks with it)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
-                                      env=env, cwd=ROOT, start_new_session=True))
+                                      env=env, cwd=ROOT, preexec_fn=_die_with_parent))
     codes = [None] * n
     failed_at = None
     try:
@@ -369,16 +380,16 @@ def self_launch(args):
                               f"ranks", file=sys.stderr, flush=True)
                         for q in procs:
                             if q.poll() is None:
-                                os.killpg(q.pid, signal.SIGTERM)
+                                q.send_signal(signal.SIGTERM)
             if failed_at is not None and time.time() - failed_at > 20:
                 for q in procs:
                     if q.poll() is None:
-                        os.killpg(q.pid, signal.SIGKILL)
+                        q.kill()
             time.sleep(0.1)
     except KeyboardInterrupt:
         for q in procs:
             if q.poll() is None:
-                os.killpg(q.pid, signal.SIGKILL)
+                q.kill()
         raise
     # a signal death (negative code) is a failure too
     return max(abs(c) for c in codes)
