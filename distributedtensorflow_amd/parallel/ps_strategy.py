@@ -131,6 +131,11 @@ class _RemotePSReducer(_NullReducer):
         if not self.pipelined():
             params = self.space.order
             return self.client.push([p.grad for p in params], pull=True)
+        # buckets the backward hooks did not push (the first pipelined step, decided only now;
+        # variables without a gradient this step)
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._push_bucket(b)
         ev = torch.cuda.Event()
         ev.record(self.stream)
         # the next step's zero_grad (compute stream) must not overwrite the gradient buffer
