@@ -81,6 +81,25 @@ def _dump_stacks(tasks):
         time.sleep(1.0)
 
 
+def _stop_others(tasks, failed, rc, grace_s=10.0):
+    """A rank of a collective world failed for good: SIGTERM the other live ranks, SIGKILL
+    whatever is still alive after ``grace_s`` (a rank stuck in a device-side wait may ignore the
+    first signal)."""
+    live = [x for x in tasks if x is not failed and x.proc.poll() is None]
+    for x in live:
+        x.log.write(f"\n[launcher] {failed.name} failed for good (exit {rc}); stopping "
+                    f"{x.name}\n")
+        x.log.flush()
+        x.proc.terminate()
+    t0 = time.time()
+    while time.time() - t0 < grace_s and any(x.proc.poll() is None for x in live):
+        time.sleep(0.1)
+    for x in live:
+        if x.proc.poll() is None:
+            x.proc.kill()
+            x.proc.wait()
+
+
 def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart_alone=False):
     """Wait for the worker tasks, restarting failed tasks meanwhile.
 
@@ -109,7 +128,13 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart
             voluntary = rc == Server.REJOIN_EXIT_CODE
             if ending or not (workers_alive or not is_worker(t) or restart_alone) or \
                     (not voluntary and used >= max_restarts):
-                continue                                  # final: reported as its exit code
+                # final: reported as its exit code.  In a collective world the other ranks can
+                # never finish without it (they would wait in a collective until their own
+                # timeouts): end the job now, loudly, instead of waiting for the launcher's
+                if restart_alone and not ending and not getattr(t, "final", False):
+                    t.final = True
+                    _stop_others(tasks, t, rc)
+                continue
             if not voluntary:
                 used += 1
                 epoch = bump_epoch(store)

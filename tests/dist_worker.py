@@ -78,6 +78,8 @@ def main():
         return heartbeat_probe(out)
     if kind == "hung_peer":
         return hung_peer_watchdog(out)
+    if kind == "hang_mid_run":
+        return hang_mid_run(out, kw)
     if kind == "mirrored_recovery":
         return mirrored_recovery(out, kw, steps)
     if kind == "resnet_gpu":
@@ -259,6 +261,43 @@ def resnet_gpu_grads(out):
                     "order": [n for n, p in model.named_parameters()]},
                    os.path.join(out, f"rank{rank}.pt"))
     strat.barrier()
+
+
+def hang_mid_run(out, kw):
+    """A 2-rank MirroredStrategy world under launch_collective WITHOUT restarts: rank 1 hangs
+    (alive, stops stepping) at global step ``at``.  Rank 0's collective must fail within
+    DTF_COMM_TIMEOUT_S and end its process non-zero; the launcher then stops rank 1 -- the job
+    ends loudly instead of hanging."""
+    import time
+
+    import distributedtensorflow_amd as dtf
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.models import MnistCNN
+    from distributedtensorflow_amd.parallel import MirroredStrategy
+    strat = MirroredStrategy()
+    rank = strat.replica_id
+    at = int(kw.get("at", 4))
+    torch.manual_seed(3)
+    with strat.scope():
+        model = MnistCNN()
+        opt = make_optimizer("momentum")
+        gstep = dtf.train.get_or_create_global_step()
+        opt.build(list(model.parameters()))
+        sess = dtf.train.MonitoredTrainingSession(
+            is_chief=rank == 0, checkpoint_dir=None, save_checkpoint_secs=None,
+            save_summaries_steps=None, log_step_count_steps=None, model=model, optimizer=opt,
+            global_step=gstep, strategy=strat)
+        with sess:
+            while gstep.value() < 50:
+                s = gstep.value()
+                if rank == 1 and s == at:
+                    print("rank 1 hangs", flush=True)
+                    time.sleep(3600)
+                x, y = global_batch(s)
+                x, y = x[rank * 8:(rank + 1) * 8], y[rank * 8:(rank + 1) * 8]
+                sess.run(lambda: opt.minimize(ops.sparse_softmax_cross_entropy(model(x), y),
+                                              global_step=gstep))
+                print(f"rank {rank} step {gstep.value()}", flush=True)
 
 
 def hung_peer_watchdog(out):

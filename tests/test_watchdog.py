@@ -234,3 +234,22 @@ def test_ps_bucket_plan_covers_the_flat_buffer():
     assert plan[0][0] == 0 and plan[-1][1] == Space.numel
     assert all(a[1] == b[0] for a, b in zip(plan, plan[1:]))
     assert sorted(i for _, _, m in plan for i in m) == list(range(5))
+
+
+def test_hung_rank_ends_the_job_loudly(tmp_path):
+    """No restarts configured and rank 1 hangs mid-run: rank 0's collective fails within
+    DTF_COMM_TIMEOUT_S, rank 0 exits non-zero, and the launcher stops the hung rank -- the job
+    ends in well under the launcher's own timeout instead of hanging."""
+    from distributedtensorflow_amd.cluster.launcher import launch_collective
+    t0 = time.time()
+    codes, logs = launch_collective(os.path.join(HERE, "dist_worker.py"), 2, str(tmp_path),
+                                    ["hang_mid_run", str(tmp_path), "at=4"],
+                                    env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "1",
+                                         "DTF_COMM_TIMEOUT_S": "4"},
+                                    timeout_s=150, max_restarts=0)
+    took = time.time() - t0
+    text = {k: open(v).read() for k, v in logs.items()}
+    assert codes[0] != 0 and codes[1] != 0, (codes, text["rank0"][-2000:])
+    assert "rank 1 hangs" in text["rank1"]
+    assert "failed for good" in text["rank1"]
+    assert took < 90, took
