@@ -1320,12 +1320,17 @@ class _BiasGeluDense(torch.autograd.Function):
                                 do2.stride(0), wt.stride(0), a2.data_ptr(), b32.data_ptr(),
                                 colsum.data_ptr(), _st())
             if ctx.needs_input_grad[1]:
+                # the b1 gradient: the per-tile column sums' second level, in fixed order, added
+                # straight into the flat gradient buffer (was a torch reduction + add: ~21 us)
                 tb = _direct_grad(b1)
+                out = tb if tb is not None else torch.empty(i, device=do.device,
+                                                            dtype=torch.float32)
+                _K.slab_reduce(colsum.data_ptr(), out.data_ptr(), i, tiles,
+                               int(tb is not None), _st())
                 if tb is not None:
-                    tb.add_(colsum.sum(0))
                     _grad_ready(b1)
                 else:
-                    db = colsum.sum(0).to(b1.dtype)
+                    db = out.to(b1.dtype)
             da = da.view(ctx.shape)
         return da, db, dw, None
 
