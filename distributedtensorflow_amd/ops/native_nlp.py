@@ -298,11 +298,18 @@ class _MlmLoss(torch.autograd.Function):
                     grad.data_ptr(), _st())
         ctx.save_for_backward(grad)
         ctx.ldt = logits.dtype
+        # Optimizer.compute_gradients runs loss.backward() with the implicit unit gradient and
+        # says so through this flag (ctx is the output's grad_fn): the [N, vocab] gradient is
+        # then handed on as computed, without a full read + write pass multiplying it by 1
+        ctx.dtf_unit_grad_ok = True
+        ctx.dtf_unit_grad = False
         return rows.sum()
 
     @staticmethod
     def backward(ctx, g):
         (grad,) = ctx.saved_tensors
+        if ctx.dtf_unit_grad and grad.dtype == ctx.ldt:
+            return grad, None, None
         return (grad * g.to(grad.dtype)).to(ctx.ldt), None, None
 
 

@@ -161,6 +161,9 @@ class Optimizer:
         from .. import profiler
         self.space.zero_grad()
         self._reducer.begin_step()
+        fn = getattr(loss, "grad_fn", None)
+        if fn is not None and getattr(fn, "dtf_unit_grad_ok", False):
+            fn.dtf_unit_grad = True          # backward() below seeds exactly d(loss) = 1
         with profiler.maybe_phase("backward"):
             loss.backward()
         with profiler.maybe_phase("comm"):
