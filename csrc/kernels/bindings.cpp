@@ -164,7 +164,8 @@ void dtf_bias_gelu_bwd(const bf16_t*, const bf16_t*, const float*, bf16_t*, floa
 void dtf_attn_fwd(const bf16_t*, const float*, bf16_t*, float*, int, int, int, float, float,
                   uint32_t, hipStream_t);
 void dtf_attn_bwd(const bf16_t*, const float*, const bf16_t*, const bf16_t*, const float*, float*,
-                  bf16_t*, int, int, int, float, float, uint32_t, hipStream_t);
+                  bf16_t*, int, int, int, float, float, uint32_t, hipStream_t, float*);
+int dtf_attn_bwd_fused(int);
 int dtf_pos_type_grad_ws_floats(int, int, int);
 void dtf_attn_set_wide(int);
 void dtf_attn_set_fused(int);
@@ -783,12 +784,15 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("attn_bwd", [](uintptr_t qkv, uintptr_t mask, uintptr_t out, uintptr_t dout,
                        uintptr_t lse, uintptr_t delta, uintptr_t dqkv, int B, int S_, int H,
-                       float scale, float p, uint32_t seed, uintptr_t st) {
+                       float scale, float p, uint32_t seed, uintptr_t st, uintptr_t colpart) {
     dtf_attn_bwd(P<const bf16_t>(qkv), P<const float>(mask), P<const bf16_t>(out),
                  P<const bf16_t>(dout), P<const float>(lse), P<float>(delta), P<bf16_t>(dqkv), B,
-                 S_, H, scale, p, seed, S(st));
+                 S_, H, scale, p, seed, S(st), P<float>(colpart));
     check_launch("attn_bwd");
-  });
+  }, py::arg("qkv"), py::arg("mask"), py::arg("out"), py::arg("dout"), py::arg("lse"),
+     py::arg("delta"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"),
+     py::arg("scale"), py::arg("p"), py::arg("seed"), py::arg("st"), py::arg("colpart") = 0);
+  m.def("attn_bwd_fused", &dtf_attn_bwd_fused);
   m.def("attn_set_wide", &dtf_attn_set_wide);
   m.def("attn_set_fused", &dtf_attn_set_fused);
   m.def("pos_type_grad_ws_floats", &dtf_pos_type_grad_ws_floats);

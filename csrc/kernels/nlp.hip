@@ -868,7 +868,18 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mas
 // 128 x 128 x 64 products per (b, h)) and the second read of Q / K / V / dO; every accumulator
 // sums in the same order as before, so the gradients are bit-identical to the split kernels.
 constexpr int kFusedS = 128, kPLD = 136;   // P / dS row pitch (272 B: 8-B aligned rows)
-constexpr int kFusedLds = (4 * kFusedS * ALD + kFusedS * kPLD) * 2 + kFusedS * 4;   // 109,056 B
+constexpr int kFusedRed = 8 * 3 * AD;        // [wave][dq | dk | dv column] fp32 partial sums
+constexpr int kFusedLds = (4 * kFusedS * ALD + kFusedS * kPLD) * 2 + kFusedS * 4 +
+                          kFusedRed * 4;                                   // 115,200 B
+
+// sum of v over the 16 lanes of this lane's 16-lane group (the 16 queries / keys of a wave)
+DTF_DEV float sum16(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
 
 DTF_DEV bf16x8_t lds_tr8_p(const bf16_t* base, int row0, int col0, int lane) {
   const int i = lane & 15, g = lane >> 4;
@@ -883,7 +894,7 @@ __global__ void __launch_bounds__(512)
 attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                          const bf16_t* __restrict__ dO, const float* __restrict__ lse,
                          float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom g,
-                         const bf16_t* __restrict__ O) {
+                         const bf16_t* __restrict__ O, float* __restrict__ colpart) {
   constexpr int S = kFusedS;
   static_assert(S * kPLD <= 2 * S * ALD, "P must fit over the K|V region");
   extern __shared__ __attribute__((aligned(16))) bf16_t fsm[];    // kFusedLds bytes (dynamic)
@@ -892,6 +903,7 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
   bf16_t* KV = Os + S * ALD;                 // K | V, then P
   bf16_t* dSs = KV + 2 * S * ALD;
   float* Ms = reinterpret_cast<float*>(dSs + S * kPLD);
+  float* red = Ms + S;                       // [8 waves][3 * 64] column partials (colpart)
   bf16_t* Ks = KV;
   bf16_t* Vs = KV + S * ALD;
   bf16_t* Ps = KV;
@@ -972,6 +984,16 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
     bf16_t* dqrow = dqkv + (tok0 + q) * g.ld + h * AD;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) store4_scaled(dqrow + 16 * dt + 4 * gq, acc[dt], g.scale);
+    if (colpart) {
+      // column sums of the STORED (bf16-rounded) dQ over this wave's 16 queries
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = sum16(round_bf(acc[dt][r] * g.scale));
+          if (li == 0) red[w * 3 * AD + 16 * dt + 4 * gq + r] = t;
+        }
+    }
   }
   __syncthreads();                 // every wave is done with K and V: P may overwrite them
   // ---- P and dS to LDS as [query][key]: this lane's 4 consecutive keys of each group
@@ -1008,6 +1030,30 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
   for (int dt = 0; dt < 4; ++dt) {
     store4_scaled(dkrow + 16 * dt + 4 * gq, dk[dt], g.scale);
     store4_scaled(dvrow + 16 * dt + 4 * gq, dv[dt], 1.f);
+  }
+  if (colpart) {
+    // the qkv bias gradient's first level: per (b, h) column sums of dQ / dK / dV over the 128
+    // tokens (8 waves x 16, fixed order) -> colpart[b][3 * H * 64], in dqkv's column layout;
+    // the _Dense backward of the QKV projection sums the B rows instead of re-reading dqkv
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float tk = sum16(round_bf(dk[dt][r] * g.scale));
+        const float tv = sum16(round_bf(dv[dt][r]));
+        if (li == 0) {
+          red[w * 3 * AD + AD + 16 * dt + 4 * gq + r] = tk;
+          red[w * 3 * AD + 2 * AD + 16 * dt + 4 * gq + r] = tv;
+        }
+      }
+    __syncthreads();
+    if (tid < 3 * AD) {
+      float t = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) t += red[ww * 3 * AD + tid];
+      const int sec = tid / AD, col = tid % AD;
+      colpart[(long)b * g.ld + (sec * H + h) * AD + col] = t;
+    }
   }
 }
 
@@ -1241,10 +1287,16 @@ void dtf_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse,
 static int g_attn_fused = 1;
 void dtf_attn_set_fused(int v) { g_attn_fused = v; }
 
+// 1 when dtf_attn_bwd will run the fused kernel for this shape (it can then also emit the qkv
+// bias gradient's column partials)
+int dtf_attn_bwd_fused(int S) { return g_attn_fused && S == kFusedS; }
+
 void dtf_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* out, const bf16_t* dout,
                   const float* lse, float* delta, bf16_t* dqkv, int B, int S, int H, float scale,
-                  float p, uint32_t seed, hipStream_t st) {
+                  float p, uint32_t seed, hipStream_t st, float* colpart) {
   const AttnGeom g = attn_geom(B, S, H, scale, p, seed);
+  if (colpart && !(g_attn_fused && S == kFusedS))
+    throw std::runtime_error("attn_bwd: column partials need the fused S == 128 backward");
   if (g_attn_fused && S == kFusedS) {
     static bool attr = false;
     if (!attr) {
@@ -1257,10 +1309,10 @@ void dtf_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* out, const
     const dim3 grid(H, B);
     if (g.thr)
       hipLaunchKernelGGL(attn_bwd_fused128_kernel<true>, grid, dim3(512), kFusedLds, st, qkv,
-                         mask, dout, lse, delta, dqkv, g, out);
+                         mask, dout, lse, delta, dqkv, g, out, colpart);
     else
       hipLaunchKernelGGL(attn_bwd_fused128_kernel<false>, grid, dim3(512), kFusedLds, st, qkv,
-                         mask, dout, lse, delta, dqkv, g, out);
+                         mask, dout, lse, delta, dqkv, g, out, colpart);
     return;
   }
   if (g_attn_wide && S % 128 == 0)

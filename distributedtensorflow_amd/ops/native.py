@@ -1255,7 +1255,13 @@ class _Dense(torch.autograd.Function):
         if ctx.has_b and ctx.needs_input_grad[3]:
             tb = _direct_grad(ctx.b_param)
             out = tb if tb is not None else torch.empty(o, device=x.device, dtype=torch.float32)
-            if dy2.dtype == _BF16 and o % 2 == 0:
+            cp = getattr(dy, "_dtf_colsum_part", None)
+            if cp is not None and cp[2] == dy._version and cp[0].shape[1] == o and o % 4 == 0:
+                # column partials left by the producer of dy (the fused attention backward):
+                # B rows summed in fixed order instead of another pass over dy
+                _K.slab_reduce(cp[0].data_ptr(), out.data_ptr(), o, cp[1],
+                               int(tb is not None), _st())
+            elif dy2.dtype == _BF16 and o % 2 == 0:
                 # the fixed-order two-level column sum (16-B loads; 4-B loads for the 30522-wide
                 # MLM decoder bias, which torch's reduction ran at ~1.8 TB/s)
                 dyc = dy2.contiguous()

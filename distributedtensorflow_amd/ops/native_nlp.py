@@ -260,9 +260,17 @@ class _AttentionQKV(torch.autograd.Function):
         do = dout.to(_BF16).contiguous()
         dqkv = torch.empty_like(q)
         delta = torch.empty_like(lse)
+        # the fused S == 128 backward also leaves per-sequence column sums of dqkv: the QKV
+        # projection's bias gradient is then a B-row sum instead of a pass over dqkv
+        part = None
+        if _K.attn_bwd_fused(S):
+            part = torch.empty(B, 3 * heads * AD, device=q.device, dtype=torch.float32)
         _K.attn_bwd(q.data_ptr(), m.data_ptr() if has_mask else 0, out.data_ptr(), do.data_ptr(),
                     lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), B, S, heads, scale, p, seed,
-                    _st())
+                    _st(), _p(part))
+        if part is not None:
+            # valid only for this exact tensor and version (an in-place add would change it)
+            dqkv._dtf_colsum_part = (part, B, dqkv._version)
         return dqkv, None, None, None, None, None, None
 
 

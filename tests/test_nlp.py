@@ -281,6 +281,37 @@ def test_attention_fused_bwd_bit_identical(p):
 
 
 @pytest.mark.gpu
+def test_qkv_bias_grad_from_fused_attention_partials():
+    """S == 128: the fused attention backward leaves per-sequence column sums of dQKV, and the
+    QKV projection's bias gradient is their B-row sum (no pass over dQKV).  It must equal the
+    column sum of the very dQKV the kernel stored (the split path, which re-reads dQKV), up to
+    fp32 summation order, and the other gradients must not change at all."""
+    from distributedtensorflow_amd.ops import native
+    torch.manual_seed(0)
+    B, S, H, D = 6, 128, 2, 64
+    x = torch.randn(B * S, 96, device="cuda").bfloat16().requires_grad_(True)
+    w = torch.nn.Parameter(torch.randn(3 * H * D, 96, device="cuda") * 0.1)
+    b = torch.nn.Parameter(torch.randn(3 * H * D, device="cuda") * 0.1)
+    mask = torch.zeros(B, S, device="cuda")
+    mask[2, 100:] = -10000.0
+    dy = torch.randn(B * S, H * D, device="cuda").bfloat16()
+    res = []
+    for fused in (1, 0):
+        native._K.attn_set_fused(fused)
+        try:
+            torch.manual_seed(3)
+            qkv = ops.dense(x, w, b)
+            y = ops.attention_qkv(qkv, mask, B, S, H, 0.1, True)
+            gx, gw, gb = torch.autograd.grad(y, [x, w, b], dy)
+            torch.cuda.synchronize()
+        finally:
+            native._K.attn_set_fused(1)
+        res.append((gx, gw, gb))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    torch.testing.assert_close(res[0][2], res[1][2], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
 def test_mlm_loss_gpu():
     torch.manual_seed(0)
     N, V = 80, 30522
