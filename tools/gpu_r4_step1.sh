@@ -2,7 +2,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 SH=bert_qkv_fwd,bert_attnout_fwd,bert_ffn1_fwd,bert_ffn2_fwd,bert_qkv_dgrad,bert_ffn1_dgrad,bert_ffn2_dgrad
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_nlp.py -k "attention" > gpurun_out/r4_t0.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_nlp.py -k "attention or qkv_bias or mlm or gelu_dense" > gpurun_out/r4_t0.log 2>&1 || exit 1
 for gm in 0 4 8 16; do
   DTF_GEMM_GROUP_M=$gm timeout -k 10 120 python tools/gemm_bench.py --only $SH --iters 20 --variants 8 --out gpurun_out/r4_gemm_group_$gm.jsonl > gpurun_out/r4_gemm_group_$gm.log 2>&1 || exit 1
 done
