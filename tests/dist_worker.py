@@ -17,8 +17,10 @@ import torch  # noqa: E402
 
 
 def global_batch(step, n=16):
+    # explicit CPU: inside a GPU strategy's scope the default device is the GPU
     g = torch.Generator().manual_seed(1000 + step)
-    return torch.rand(n, 784, generator=g), torch.randint(0, 10, (n,), generator=g)
+    return (torch.rand(n, 784, generator=g, device="cpu"),
+            torch.randint(0, 10, (n,), generator=g, device="cpu"))
 
 
 def make_optimizer(name):

@@ -28,9 +28,10 @@ def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False, lazy=True):
     for, so the other fusions can be checked bit-exactly."""
     prev, prev_r, prev_s = native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD, native._SHARE_INPUT_GRAD
     prev_b, prev_l = native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD
-    prev_bs = native._FUSE_BN_BWD_STREAM
+    prev_bs, prev_c1 = native._FUSE_BN_BWD_STREAM, native._FUSE_C1_BWD
     native._FUSE_BN_BWD = fuse_bnb
     native._FUSE_BN_BWD_STREAM = fuse_bnb
+    native._FUSE_C1_BWD = fuse_bnb
     native._LAZY_RESIDUAL_GRAD = lazy
     native._DIRECT_GRAD = direct
     native._FUSE_RESIDUAL_GRAD = fuse_res
@@ -47,7 +48,7 @@ def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False, lazy=True):
         native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD = prev, prev_r
         native._SHARE_INPUT_GRAD = prev_s
         native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD = prev_b, prev_l
-        native._FUSE_BN_BWD_STREAM = prev_bs
+        native._FUSE_BN_BWD_STREAM, native._FUSE_C1_BWD = prev_bs, prev_c1
 
 
 def test_direct_grad_path_bit_identical():
@@ -164,6 +165,69 @@ def test_bn_relu_conv_fusion_bit_identical():
     assert calls["n"] == 13          # c3 of every stage-1..3 bottleneck (w = 64 / 128 / 256)
     assert la == lb
     assert torch.equal(ga, gb)
+
+
+def _c1_grads(x, gamma, beta, w, g, fused):
+    prev = native._FUSE_C1_BWD
+    native._FUSE_C1_BWD = fused
+    try:
+        xs = x.detach().clone().requires_grad_(True)
+        ps = [t.detach().clone().requires_grad_(True) for t in (gamma, beta, w)]
+        C = x.shape[-1]
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        out = native.bn_relu_conv1x1(xs, ps[0], ps[1], rm, rv, ps[2], 0.9, 1e-5)
+        seen = {}
+        orig = native._bn_backward_core
+
+        def spy(ctx, dy, *a, **k):
+            seen["dy"] = dy.detach().clone()
+            return orig(ctx, dy, *a, **k)
+        native._bn_backward_core = spy
+        try:
+            grads = torch.autograd.grad(out, [xs] + ps, g)
+        finally:
+            native._bn_backward_core = orig
+        torch.cuda.synchronize()
+        return seen["dy"], grads
+    finally:
+        native._FUSE_C1_BWD = prev
+
+
+@pytest.mark.parametrize("n,hw,grid", [(4, 28, 0), (4, 28, 3), (1, 8, 0), (2, 8, 1), (3, 8, 1)])
+def test_fused_c1_backward_matches_separate_passes(n, hw, grid):
+    """First-stage c3 (64 -> 256) backward as ONE pass (csrc/kernels/conv1x1_bwd.hip: data
+    gradient + weight gradient + the BN backward sums) == the separate wgrad / dgrad / BN reduce
+    passes: the data gradient bit for bit, dW / dgamma / dbeta / dx to fp32 summation order;
+    persistent-grid walks of 1, 2, 3 and 16-17 tiles per block (``grid`` forces the block count)."""
+    torch.manual_seed(0)
+    x = torch.randn(n, hw, hw, 64, device="cuda").bfloat16()
+    w = torch.randn(256, 1, 1, 64, device="cuda") / 8
+    gamma = torch.rand(64, device="cuda") + 0.5
+    beta = torch.randn(64, device="cuda") * 0.2
+    g = torch.randn(n, hw, hw, 256, device="cuda").bfloat16()
+    assert native._K.conv1x1_bwd_ok(n * hw * hw, 64, 256)
+    native._K.conv1x1_bwd_set_grid(grid)
+    try:
+        dy1, g1 = _c1_grads(x, gamma, beta, w, g, True)
+    finally:
+        native._K.conv1x1_bwd_set_grid(0)
+    dy2, g2 = _c1_grads(x, gamma, beta, w, g, False)
+    assert torch.equal(dy1, dy2)
+    for a, b, name in zip(g1, g2, ("dx", "dgamma", "dbeta", "dw")):
+        a, b = a.float(), b.float()
+        rel = ((a - b).norm() / b.norm()).item()
+        assert rel < (2e-2 if name == "dx" else 1e-4), (name, rel)
+    # and against fp32 math of the same op
+    xs = x.float().requires_grad_(True)
+    ps = [t.clone().requires_grad_(True) for t in (gamma, beta, w)]
+    mean = xs.mean((0, 1, 2))
+    var = xs.var((0, 1, 2), unbiased=False)
+    yb = torch.relu((xs - mean) / torch.sqrt(var + 1e-5) * ps[0] + ps[1])
+    ref = torch.einsum("nhwc,kc->nhwk", yb, ps[2].view(256, 64))
+    gr = torch.autograd.grad(ref, [xs] + ps, g.float())
+    for a, b, name in zip(g1, gr, ("dx", "dgamma", "dbeta", "dw")):
+        rel = ((a.float() - b).norm() / b.norm()).item()
+        assert rel < 3e-2, (name, rel)
 
 
 def test_residual_grad_fusion_bit_identical():
