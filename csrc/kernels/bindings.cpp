@@ -161,11 +161,11 @@ void dtf_bf16_col_sum(const bf16_t*, int, int, float*, float*, int, hipStream_t)
 void dtf_slab_reduce(const float*, float*, long, int, int, hipStream_t);
 // fused first-stage c3 backward (conv1x1_bwd.hip)
 bool dtf_conv1x1_bwd_ok(int, int, int);
-int dtf_conv1x1_bwd_blocks(int);
+int dtf_conv1x1_bwd_blocks(int, int);
 void dtf_conv1x1_bwd_set_grid(int);
 void dtf_conv1x1_bwd(const bf16_t*, const bf16_t*, const bf16_t*, const bf16_t*, const float*,
-                     const float*, const float*, const float*, bf16_t*, float*, float*, int,
-                     hipStream_t);
+                     const float*, const float*, const float*, bf16_t*, float*, float*, int, int,
+                     int, hipStream_t);
 void dtf_bias_gelu_bwd(const bf16_t*, const bf16_t*, const float*, bf16_t*, float*, float*, int,
                        int, hipStream_t, int);
 void dtf_attn_fwd(const bf16_t*, const float*, bf16_t*, float*, int, int, int, float, float,
@@ -776,10 +776,10 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("conv1x1_bwd_set_grid", &dtf_conv1x1_bwd_set_grid);
   m.def("conv1x1_bwd", [](uintptr_t dout, uintptr_t wt, uintptr_t y, uintptr_t x, uintptr_t mean,
                           uintptr_t inv, uintptr_t sc, uintptr_t sh, uintptr_t dy, uintptr_t wpart,
-                          uintptr_t bpart, int M, uintptr_t stream) {
+                          uintptr_t bpart, int M, int C, int K, uintptr_t stream) {
     dtf_conv1x1_bwd(P<bf16_t>(dout), P<bf16_t>(wt), P<bf16_t>(y), P<bf16_t>(x), P<float>(mean),
                     P<float>(inv), P<float>(sc), P<float>(sh), P<bf16_t>(dy), P<float>(wpart),
-                    P<float>(bpart), M, S(stream));
+                    P<float>(bpart), M, C, K, S(stream));
     check_launch("conv1x1_bwd");
   });
   m.def("slab_reduce", [](uintptr_t ws, uintptr_t out, long n, int nsplit, int accumulate,

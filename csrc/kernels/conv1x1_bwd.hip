@@ -1,30 +1,32 @@
-// Fused backward of ResNet-50's first-stage expanding 1x1 conv (c3: 64 -> 256 channels) whose
-// input is relu(BN(x)) (ops/native.py _BnReluConv1x1):
+// Fused backward of ResNet-50's expanding 1x1 convs (c3: C -> K = 4C channels) whose input is
+// relu(BN(x)) (ops/native.py _BnReluConv1x1), for the first two stages (C = 64, 128):
 //
 //   dY[m, c]   = sum_k dO[m, k] W[k, c]                  (data gradient, bf16 out)
 //   dW[k, c]  += sum_m dO[m, k] Y[m, c]                  (weight gradient, fp32 slab per block)
 //   BN sums[c] = sum_m dz, sum_m dz (x - mean) invstd,   dz = dY * [x sc + sh > 0]
 //
 // Unfused these are three passes -- the weight-gradient kernel (reads dO, Y), the data-gradient
-// GEMM (reads dO, writes dY) and the BN backward's reduce (reads dY, x): 1536 B of HBM traffic per
-// row.  Here ONE pass reads dO, Y and x and writes dY: 896 B per row; the 2 x 2 x 64 x 256 FLOPs
-// per row are ~5% of what the MFMA pipes could do in the time the bytes take, so the kernel is
-// purely a streaming problem.  (profiles/measurements/r3_conv_roofline_b1984.jsonl: the dgrad and
-// wgrad passes of this layer alone take 0.75 ms each at batch 1984.)
+// GEMM (reads dO, writes dY) and the BN backward's reduce (reads dY, x): 2K + 6C bytes of HBM
+// traffic per row (1536 at C = 64).  Here ONE pass reads dO, Y and x and writes dY: 2K + 6C - ...
+// = 896 B per row at C = 64; the 4 K C FLOPs per row are a small fraction of what the MFMA pipes
+// could do in the time the bytes take, so the kernel is a streaming problem.
+// (profiles/measurements/r3_conv_roofline_b1984.jsonl: the dgrad and wgrad passes of the C = 64
+// layer alone take 0.75 ms each at batch 1984.)
 //
-// Design (persistent: one block of 8 waves per CU, 64-row tiles walked with a grid stride):
-//   * dO (64 x 256), Y (64 x 64) and x (64 x 64) tiles stream through a 3-slot LDS ring by
-//     LDS-DMA, two tiles ahead, with source-side XOR swizzles chosen for the reads below;
-//   * data gradient with the operands swapped -- A = W^T rows (this wave's 16 channels, whole K,
-//     held in 32 VGPRs for the kernel's lifetime), B = dO rows from LDS -- so every lane ends up
+// Design (persistent: one block per CU, TM-row tiles walked with a grid stride):
+//   * dO (TM x K), Y (TM x C) and x (TM x C) tiles stream through a 3-slot LDS ring by LDS-DMA,
+//     two tiles ahead, with source-side XOR swizzles chosen for the reads below;
+//   * data gradient with the operands swapped -- A = W^T rows (the wave's channel blocks, whole
+//     K, held in VGPRs for the kernel's lifetime), B = dO rows from LDS -- so every lane ends up
 //     with 4 CONSECUTIVE channels of one row: one 8-byte store of dY, one 8-byte LDS read of x
 //     for the BN sums (computed on dY exactly as it is stored, like gemm_stream.hip's epilogue);
-//   * weight gradient: the wave owns dW rows 32 w .. 32 w + 31 x all 64 channels (8 MFMA
-//     accumulators, 32 fp32 per lane) for ALL of the block's tiles; both operands are read with
-//     the hardware transpose read ds_read_b64_tr_b16 (the reduction runs over tile rows);
-//   * at the end every block writes one fp32 dW slab [256][64] and one BN slab row [2][64]; the
-//     host reduces the slabs in fixed order (deterministic; slab_reduce / bn_bwd_finalize_g).
-// Only global memory traffic per tile per wave: 6 DMA instructions + 2 dY stores, so the counted
+//   * weight gradient: the wave owns dW rows [K/NW w, K/NW (w + 1)) x all C channels (register
+//     accumulators for ALL of the block's tiles: 32 fp32 per lane at C = 64, 128 at C = 128);
+//     both operands are read
+//     with the hardware transpose read ds_read_b64_tr_b16 (the reduction runs over tile rows);
+//   * at the end every block writes one fp32 dW slab [K][C] and one BN slab row [2][C]; the host
+//     reduces the slabs in fixed order (deterministic; slab_reduce / bn_bwd_finalize_g).
+// Only global memory traffic per tile per wave: D DMA instructions + S dY stores, so the counted
 // vmcnt waits at the top of a tile are exact (see `top`).
 #include <stdexcept>
 #include <string>
@@ -33,41 +35,58 @@
 
 namespace {
 
-constexpr int kT = 512;              // threads: 8 waves
-constexpr int kTM = 64;              // rows per tile
-constexpr int kC = 64;               // conv input channels (dY / Y / x width)
-constexpr int kK = 256;              // conv output channels (dO width)
 constexpr int kNB = 3;               // ring slots
-constexpr int kDO = kTM * kK;        // bf16 per dO tile (32 KB)
-constexpr int kYT = kTM * kC;        // bf16 per Y / x tile (8 KB)
-constexpr int kSlot = kDO + 2 * kYT; // bf16 per ring slot (48 KB)
-constexpr size_t kLds = (size_t)kNB * kSlot * 2 + 2 * 2 * kC * 4;   // + BN partials [2][2][64]
-static_assert(kLds <= 160 * 1024, "conv1x1_bwd LDS");
 
 typedef __attribute__((ext_vector_type(4))) short s4_t;
 typedef __attribute__((address_space(3))) s4_t lds_s4_t;
 
+// per-shape configuration: C in, K out, TM rows per tile, NW waves
+template <int C_, int K_, int TM_, int NW_>
+struct Cfg {
+  static constexpr int C = C_, K = K_, TM = TM_, NW = NW_;
+  static constexpr int T = NW * 64;
+  static constexpr int NCB = C / 16;                         // channel blocks
+  static constexpr int CPW = NCB >= NW ? NCB / NW : 1;       // dgrad channel blocks per wave
+  static constexpr int WPC = NW / (NCB / CPW);               // waves sharing a channel block
+  static constexpr int MBW = TM / 16 / WPC;                  // dgrad row blocks per wave
+  static constexpr int KS = K / 32;                          // dgrad MFMA k-steps
+  static constexpr int KBW = K / NW / 16;                    // wgrad dW row blocks per wave
+  static constexpr int DO = TM * K;                          // bf16 per dO tile
+  static constexpr int YT = TM * C;                          // bf16 per Y / x tile
+  static constexpr int SLOT = DO + 2 * YT;
+  static constexpr int DOI = DO * 2 / 1024;                  // 1-KB DMA instructions per dO tile
+  static constexpr int YI = YT * 2 / 1024;                   // ... per Y / x tile
+  static constexpr int D = (DOI + 2 * YI) / NW;              // DMA instructions per wave per tile
+  static constexpr int S = CPW * MBW;                        // dY stores per lane per tile
+  static constexpr size_t LDS = (size_t)kNB * SLOT * 2 + (size_t)WPC * 2 * C * 4 + 4 * C * 4;
+  static_assert(DOI % NW == 0 && (2 * YI) % NW == 0 && YI % NW == 0, "DMA split");
+  static_assert(WPC * (NCB / CPW) == NW && MBW >= 1 && TM % 32 == 0, "wave split");
+  static_assert(LDS <= 160 * 1024, "conv1x1_bwd LDS");
+};
+
 // 16-B chunk swizzles (physical chunk = logical chunk ^ swz(row)):
-//  dO, 512-B rows: the 16 rows of a dgrad B-fragment read (ds_read_b128, 16 lanes / pass) hit 16
-//    different 16-B bank slots; the 8 rows of a transpose-read half-wave keep their 32-B column
-//    pair adjacent and land on 8 different pairs
+//  dO (rows of a multiple of 256 B): the 16 rows of a dgrad B-fragment read (ds_read_b128, 16
+//    lanes / pass) hit 16 different 16-B bank slots; the 8 rows of a transpose-read half-wave keep
+//    their 32-B column pair adjacent and land on 8 different pairs
 DTF_DEV int swz_o(int r) { return 2 * (r & 7) + ((r >> 3) & 1); }
-//  Y, 128-B rows (transpose reads only): 8 rows x one 32-B pair -> 16 distinct slots
-DTF_DEV int swz_y(int r) { return 2 * ((r >> 1) & 3); }
-//  x, 128-B rows (8-B reads of 16 rows x one chunk per half-wave)
-DTF_DEV int swz_x(int r) { return (r >> 1) & 7; }
+//  Y (transpose reads only: 8 rows x one 32-B pair per half-wave -> 16 distinct slots)
+template <int C>
+DTF_DEV int swz_y(int r) { return C == 64 ? 2 * ((r >> 1) & 3) : 2 * (r & 7); }
+//  x (8-B reads of 16 rows x one 16-B chunk per half-wave)
+template <int C>
+DTF_DEV int swz_x(int r) { return C == 64 ? (r >> 1) & 7 : r & 15; }
 
 template <int RP>
 DTF_DEV int sidx(int r, int c, int s) { return r * RP + (((c >> 3) ^ s) << 3) + (c & 7); }
 
 // 8 reduction rows x one column as an MFMA operand (key permutation: j < 4 -> row0 + 4g + j,
 // j >= 4 -> row0 + 16 + 4g + j - 4; the same in both operands of a product)
-template <int RP, int W>
+template <int RP, int C, bool DOUT>
 DTF_DEV bf16x8_t tr8(const bf16_t* base, int row0, int col0, int lane) {
   const int i = lane & 15, g = lane >> 4;
   const int r = row0 + 4 * g + (i >> 2), c = col0 + 4 * (i & 3);
-  const int s0 = W == 0 ? swz_o(r) : swz_y(r);
-  const int s1 = W == 0 ? swz_o(r + 16) : swz_y(r + 16);
+  const int s0 = DOUT ? swz_o(r) : swz_y<C>(r);
+  const int s1 = DOUT ? swz_o(r + 16) : swz_y<C>(r + 16);
   const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(base + sidx<RP>(r, c, s0)));
   const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(base + sidx<RP>(r + 16, c, s1)));
   return (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -79,131 +98,174 @@ DTF_DEV f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
 
 template <int N>
 DTF_DEV void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 struct C1Args {
-  const bf16_t* dout;   // [M][256]  gradient of the conv output
-  const bf16_t* wt;     // [64][256] W^T (wt[c][k] = W[k][c])
-  const bf16_t* y;      // [M][64]   the conv input relu(BN(x))
-  const bf16_t* x;      // [M][64]   the BatchNorm input
+  const bf16_t* dout;   // [M][K]  gradient of the conv output
+  const bf16_t* wt;     // [C][K]  W^T (wt[c][k] = W[k][c])
+  const bf16_t* y;      // [M][C]  the conv input relu(BN(x))
+  const bf16_t* x;      // [M][C]  the BatchNorm input
   const float* mean;
   const float* inv;
   const float* sc;      // forward scale / shift (ReLU recomputed from x)
   const float* sh;
-  bf16_t* dy;           // [M][64]   data gradient (of y)
-  float* wpart;         // [grid][256][64]
-  float* bpart;         // [grid][2][64]
+  bf16_t* dy;           // [M][C]  data gradient (of y)
+  float* wpart;         // [grid][K][C]
+  float* bpart;         // [grid][2][C]
   int M;
 };
 
-__global__ void __launch_bounds__(kT, 1) conv1x1_bwd_kernel(const C1Args g) {
+template <class F>
+__global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
+  constexpr int C = F::C, K = F::K, TM = F::TM, NW = F::NW;
+  constexpr int CPW = F::CPW, MBW = F::MBW, KS = F::KS, KBW = F::KBW, NCB = F::NCB;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  float* sred = reinterpret_cast<float*>(lds + kNB * kSlot);
+  float* sred = reinterpret_cast<float*>(lds + kNB * F::SLOT);   // [WPC][2][C]
+  float* sprm = sred + F::WPC * 2 * C;                            // [4][C] mean / inv / sc / sh
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, gq = lane >> 4;
-  const int ntiles = g.M / kTM;
+  const int ntiles = g.M / TM;
   const int nmy = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int cb = wave & 3, mh = wave >> 2;     // data gradient: channels 16 cb.., rows 32 mh..
-  const int c0 = cb * 16 + 4 * gq;             // this lane's 4 output channels
+  // data gradient: channel blocks cg * CPW .. + CPW - 1, rows mw * MBW * 16 .. of each tile
+  const int cg = wave % (NCB / CPW), mw = wave / (NCB / CPW);
 
-  // W^T fragments: this wave's 16 channels x the whole reduction (loaded once)
-  bf16x8_t wf[8];
+  // W^T fragments: the wave's channel blocks x the whole reduction (loaded once)
+  bf16x8_t wf[CPW][KS];
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks)
-    wf[ks] = *reinterpret_cast<const bf16x8_t*>(g.wt + (cb * 16 + li) * kK + ks * 32 + gq * 8);
-  const float4 pmu = *reinterpret_cast<const float4*>(g.mean + c0);
-  const float4 pin = *reinterpret_cast<const float4*>(g.inv + c0);
-  const float4 psc = *reinterpret_cast<const float4*>(g.sc + c0);
-  const float4 psh = *reinterpret_cast<const float4*>(g.sh + c0);
-  const float mu[4] = {pmu.x, pmu.y, pmu.z, pmu.w}, is[4] = {pin.x, pin.y, pin.z, pin.w};
-  const float sc[4] = {psc.x, psc.y, psc.z, psc.w}, sh[4] = {psh.x, psh.y, psh.z, psh.w};
+  for (int j = 0; j < CPW; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      wf[j][ks] = *reinterpret_cast<const bf16x8_t*>(g.wt + ((cg * CPW + j) * 16 + li) * K +
+                                                      ks * 32 + gq * 8);
+  for (int t = tid; t < C; t += F::T) {
+    sprm[t] = g.mean[t];
+    sprm[C + t] = g.inv[t];
+    sprm[2 * C + t] = g.sc[t];
+    sprm[3 * C + t] = g.sh[t];
+  }
 
   const uint32_t lds0 = lds_addr(lds);
-  // tile i of this block -> slot i % 3: dO rows 2q, 2q + 1 per instruction (q = wave + 8 j),
-  // Y / x rows 8 wave .. 8 wave + 7
+  // tile i of this block -> slot i % 3.  dO: instruction q covers 1024 / (2K) rows; Y / x:
+  // 1024 / (2C) rows per instruction
   auto issue = [&](int i) {
-    const long m0 = ((long)blockIdx.x + (long)i * gridDim.x) * kTM;
-    const i32x4_t ro = rsrc_quad(g.dout + m0 * kK, (uint32_t)(kDO * 2));
-    const i32x4_t ry = rsrc_quad(g.y + m0 * kC, (uint32_t)(kYT * 2));
-    const i32x4_t rx = rsrc_quad(g.x + m0 * kC, (uint32_t)(kYT * 2));
-    const uint32_t base = lds0 + (uint32_t)((i % kNB) * kSlot * 2);
+    const long m0 = ((long)blockIdx.x + (long)i * gridDim.x) * TM;
+    const i32x4_t ro = rsrc_quad(g.dout + m0 * K, (uint32_t)(F::DO * 2));
+    const i32x4_t ry = rsrc_quad(g.y + m0 * C, (uint32_t)(F::YT * 2));
+    const i32x4_t rx = rsrc_quad(g.x + m0 * C, (uint32_t)(F::YT * 2));
+    const uint32_t base = lds0 + (uint32_t)((i % kNB) * F::SLOT * 2);
+    constexpr int OL = K / 8, YL = C / 8;        // 16-B chunks per row
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = wave + 8 * j, r = 2 * q + (lane >> 5), s = lane & 31;
-      dma16(ro, base + (uint32_t)q * 1024u, (uint32_t)((r * kK + ((s ^ swz_o(r)) << 3)) * 2));
+    for (int j = 0; j < F::DOI / NW; ++j) {
+      const int q = wave + NW * j, e = q * 64 + lane;     // chunk index in the tile
+      const int r = e / OL, s = e % OL;
+      dma16(ro, base + (uint32_t)q * 1024u, (uint32_t)((r * K + ((s ^ swz_o(r)) << 3)) * 2));
     }
-    const int r = 8 * wave + (lane >> 3), s = lane & 7;
-    dma16(ry, base + (uint32_t)(kDO * 2 + wave * 1024), (uint32_t)((r * kC + ((s ^ swz_y(r)) << 3)) * 2));
-    dma16(rx, base + (uint32_t)((kDO + kYT) * 2 + wave * 1024),
-          (uint32_t)((r * kC + ((s ^ swz_x(r)) << 3)) * 2));
+#pragma unroll
+    for (int j = 0; j < F::YI / NW; ++j) {
+      const int q = wave + NW * j, e = q * 64 + lane;
+      const int r = e / YL, s = e % YL;
+      dma16(ry, base + (uint32_t)(F::DO * 2 + q * 1024),
+            (uint32_t)((r * C + ((s ^ swz_y<C>(r)) << 3)) * 2));
+      dma16(rx, base + (uint32_t)((F::DO + F::YT) * 2 + q * 1024),
+            (uint32_t)((r * C + ((s ^ swz_x<C>(r)) << 3)) * 2));
+    }
   };
 
-  f32x4_t aw[2][4];
+  f32x4_t aw[KBW][NCB];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < KBW; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) aw[a][b] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < NCB; ++b) aw[a][b] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float s1[CPW][4], s2[CPW][4];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
 
   issue(0);
   if (nmy > 1) issue(1);
+  constexpr int D = F::D, S = F::S;
   for (int i = 0; i < nmy; ++i) {
     // top: this wave's DMAs of tile i landed.  Younger vector-memory ops at this point: tile
-    // i + 1's DMAs (6, if it exists) and the dY stores of tiles i - 1 and i - 2 (2 each).
+    // i + 1's DMAs (D, if it exists) and the dY stores of tiles i - 1 and i - 2 (S each).
     const bool more = i + 1 < nmy;
-    if (i == 0) { if (more) wait_vm<6>(); else wait_vm<0>(); }
-    else if (i == 1) { if (more) wait_vm<8>(); else wait_vm<2>(); }
-    else { if (more) wait_vm<10>(); else wait_vm<4>(); }
+    if (i == 0) { if (more) wait_vm<D>(); else wait_vm<0>(); }
+    else if (i == 1) { if (more) wait_vm<D + S>(); else wait_vm<S>(); }
+    else { if (more) wait_vm<D + 2 * S>(); else wait_vm<2 * S>(); }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();                  // every wave's DMAs landed; slot (i + 2) % 3 was read in i - 1
     if (i + 2 < nmy) issue(i + 2);
-    const bf16_t* sO = lds + (i % kNB) * kSlot;
-    const bf16_t* sY = sO + kDO;
-    const bf16_t* sX = sY + kYT;
+    const bf16_t* sO = lds + (i % kNB) * F::SLOT;
+    const bf16_t* sY = sO + F::DO;
+    const bf16_t* sX = sY + F::YT;
+    // the swizzled per-lane LDS addresses are recomputed every tile (a few VALU ops each) rather
+    // than hoisted out of the loop: at C = 128 the hoisted set does not fit next to the register-
+    // resident W^T fragments and dW accumulators and would be spilled
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int li = ln & 15, gq = ln >> 4;
 
-    // data gradient: rows 32 mh + 16 f + li, channels c0 .. c0 + 3 (after the MFMA's transpose)
-    f32x4_t ad[2] = {(f32x4_t){0.f, 0.f, 0.f, 0.f}, (f32x4_t){0.f, 0.f, 0.f, 0.f}};
+    // data gradient: rows mw * MBW * 16 + 16 f + li, channels of block cg * CPW + j, 4 per lane
+    f32x4_t ad[CPW][MBW];
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
+    for (int j = 0; j < CPW; ++j)
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const int m = mh * 32 + f * 16 + li;
-        const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(sO + sidx<kK>(m, ks * 32 + gq * 8, swz_o(m)));
-        ad[f] = mfma16(wf[ks], b, ad[f]);
+      for (int f = 0; f < MBW; ++f) ad[j][f] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int f = 0; f < MBW; ++f) {
+        const int m = (mw * MBW + f) * 16 + li;
+        const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(sO + sidx<K>(m, ks * 32 + gq * 8, swz_o(m)));
+#pragma unroll
+        for (int j = 0; j < CPW; ++j) ad[j][f] = mfma16(wf[j][ks], b, ad[j][f]);
       }
     }
-    // weight gradient: dW rows 32 wave + 16 kb + .., channels 16 cb2 + .., over the tile's rows
+    // weight gradient: dW rows wave * K / NW + 16 kb + .., channels 16 cb + .., over the tile
 #pragma unroll
-    for (int ms = 0; ms < 2; ++ms) {
-      bf16x8_t fa[2], fb[4];
+    for (int ms = 0; ms < TM / 32; ++ms) {
+      bf16x8_t fa[KBW];
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) fa[kb] = tr8<kK, 0>(sO, 32 * ms, wave * 32 + kb * 16, lane);
+      for (int kb = 0; kb < KBW; ++kb) fa[kb] = tr8<K, C, true>(sO, 32 * ms, wave * (K / NW) + kb * 16, ln);
 #pragma unroll
-      for (int cb2 = 0; cb2 < 4; ++cb2) fb[cb2] = tr8<kC, 1>(sY, 32 * ms, cb2 * 16, lane);
+      for (int cb = 0; cb < NCB; ++cb) {
+        const bf16x8_t fb = tr8<C, C, false>(sY, 32 * ms, cb * 16, ln);
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int cb2 = 0; cb2 < 4; ++cb2) aw[kb][cb2] = mfma16(fa[kb], fb[cb2], aw[kb][cb2]);
+        for (int kb = 0; kb < KBW; ++kb) aw[kb][cb] = mfma16(fa[kb], fb, aw[kb][cb]);
+      }
     }
     // epilogue: dY (bf16) + the BatchNorm backward sums on the stored values
-    const long m0 = ((long)blockIdx.x + (long)i * gridDim.x) * kTM;
+    const long m0 = ((long)blockIdx.x + (long)i * gridDim.x) * TM;
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const int m = mh * 32 + f * 16 + li;
-      const uint2 pk = make_uint2(pack2(ad[f][0], ad[f][1]), pack2(ad[f][2], ad[f][3]));
-      *reinterpret_cast<uint2*>(g.dy + (m0 + m) * kC + c0) = pk;
-      const uint2 xr = *reinterpret_cast<const uint2*>(sX + sidx<kC>(m, c0, swz_x(m)));
-      const float gd[4] = {__builtin_bit_cast(float, pk.x << 16), __builtin_bit_cast(float, pk.x & 0xffff0000u),
-                           __builtin_bit_cast(float, pk.y << 16), __builtin_bit_cast(float, pk.y & 0xffff0000u)};
-      const float xv[4] = {__builtin_bit_cast(float, xr.x << 16), __builtin_bit_cast(float, xr.x & 0xffff0000u),
-                           __builtin_bit_cast(float, xr.y << 16), __builtin_bit_cast(float, xr.y & 0xffff0000u)};
+    for (int j = 0; j < CPW; ++j) {
+      const int c0 = (cg * CPW + j) * 16 + 4 * gq;
+      float mu[4], is[4], sc[4], sh[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float dz = __builtin_fmaf(xv[e], sc[e], sh[e]) > 0.f ? gd[e] : 0.f;
-        s1[e] += dz;
-        s2[e] += dz * (xv[e] - mu[e]) * is[e];
+        mu[e] = sprm[c0 + e];
+        is[e] = sprm[C + c0 + e];
+        sc[e] = sprm[2 * C + c0 + e];
+        sh[e] = sprm[3 * C + c0 + e];
+      }
+#pragma unroll
+      for (int f = 0; f < MBW; ++f) {
+        const int m = (mw * MBW + f) * 16 + li;
+        const uint2 pk = make_uint2(pack2(ad[j][f][0], ad[j][f][1]), pack2(ad[j][f][2], ad[j][f][3]));
+        *reinterpret_cast<uint2*>(g.dy + (m0 + m) * C + c0) = pk;
+        const uint2 xr = *reinterpret_cast<const uint2*>(sX + sidx<C>(m, c0, swz_x<C>(m)));
+        const float gd[4] = {__builtin_bit_cast(float, pk.x << 16), __builtin_bit_cast(float, pk.x & 0xffff0000u),
+                             __builtin_bit_cast(float, pk.y << 16), __builtin_bit_cast(float, pk.y & 0xffff0000u)};
+        const float xv[4] = {__builtin_bit_cast(float, xr.x << 16), __builtin_bit_cast(float, xr.x & 0xffff0000u),
+                             __builtin_bit_cast(float, xr.y << 16), __builtin_bit_cast(float, xr.y & 0xffff0000u)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float dz = __builtin_fmaf(xv[e], sc[e], sh[e]) > 0.f ? gd[e] : 0.f;
+          s1[j][e] += dz;
+          s2[j][e] += dz * (xv[e] - mu[e]) * is[e];
+        }
       }
     }
   }
@@ -211,43 +273,55 @@ __global__ void __launch_bounds__(kT, 1) conv1x1_bwd_kernel(const C1Args g) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();
 
-  // BN partials: the 16 row lanes sharing a channel group meet by cross-lane adds, then the two
-  // waves sharing cb in fixed order
+  // BN partials: the 16 row lanes sharing a channel group meet by cross-lane adds, then the
+  // WPC waves sharing a channel block in fixed order
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      s1[e] += __shfl_xor(s1[e], o, 64);
-      s2[e] += __shfl_xor(s2[e], o, 64);
-    }
-  }
-  if (li == 0) {
+  for (int j = 0; j < CPW; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      sred[(mh * 2 + 0) * kC + c0 + e] = s1[e];
-      sred[(mh * 2 + 1) * kC + c0 + e] = s2[e];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[j][e] += __shfl_xor(s1[j][e], o, 64);
+        s2[j][e] += __shfl_xor(s2[j][e], o, 64);
+      }
     }
+  if (li == 0) {
+#pragma unroll
+    for (int j = 0; j < CPW; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = (cg * CPW + j) * 16 + 4 * gq + e;
+        sred[(mw * 2 + 0) * C + c] = s1[j][e];
+        sred[(mw * 2 + 1) * C + c] = s2[j][e];
+      }
   }
   __syncthreads();
-  if (tid < 2 * kC) {
-    const int which = tid >> 6, col = tid & 63;
-    g.bpart[((long)blockIdx.x * 2 + which) * kC + col] =
-        sred[which * kC + col] + sred[(2 + which) * kC + col];
+  for (int t = tid; t < 2 * C; t += F::T) {
+    const int which = t / C, col = t % C;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < F::WPC; ++w) v += sred[(w * 2 + which) * C + col];
+    g.bpart[((long)blockIdx.x * 2 + which) * C + col] = v;
   }
-  // dW slab: lane holds dW[32 wave + 16 kb + 4 gq + r][16 cb2 + li]
-  float* wp = g.wpart + (long)blockIdx.x * kK * kC;
+  // dW slab: lane holds dW[wave K / NW + 16 kb + 4 gq + r][16 cb + li]
+  float* wp = g.wpart + (long)blockIdx.x * K * C;
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
+  for (int kb = 0; kb < KBW; ++kb)
 #pragma unroll
-    for (int cb2 = 0; cb2 < 4; ++cb2)
+    for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        wp[(wave * 32 + kb * 16 + 4 * gq + r) * kC + cb2 * 16 + li] = aw[kb][cb2][r];
+        wp[(wave * (K / NW) + kb * 16 + 4 * gq + r) * C + cb * 16 + li] = aw[kb][cb][r];
 }
+
+typedef Cfg<64, 256, 64, 8> CfgS0;    // stage 0: 56 x 56 x 64 -> 256
+typedef Cfg<128, 512, 32, 8> CfgS1;   // stage 1: 28 x 28 x 128 -> 512
 
 int g_c1_grid = 0;   // 0 = one block per CU
 
-int c1_blocks(int M) {
+int c1_tm(int C) { return C == 64 ? CfgS0::TM : CfgS1::TM; }
+
+int c1_blocks(int M, int C) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -255,36 +329,45 @@ int c1_blocks(int M) {
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
   const int want = g_c1_grid > 0 ? g_c1_grid : cus;
-  const int ntiles = M / kTM;
+  const int ntiles = M / c1_tm(C);
   return ntiles < want ? ntiles : want;
+}
+
+template <class F>
+void launch_c1(const C1Args& g, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_bwd_kernel<F>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)F::LDS));
+    attr = true;
+  }
+  hipLaunchKernelGGL(conv1x1_bwd_kernel<F>, dim3(c1_blocks(g.M, F::C)), dim3(F::T), F::LDS, st, g);
 }
 
 }  // namespace
 
-bool dtf_conv1x1_bwd_ok(int M, int C, int K) { return C == kC && K == kK && M > 0 && M % kTM == 0; }
+bool dtf_conv1x1_bwd_ok(int M, int C, int K) {
+  return ((C == 64 && K == 256) || (C == 128 && K == 512)) && M > 0 && M % c1_tm(C) == 0;
+}
 
-// number of slab rows (blocks) the fused backward writes for M rows
-int dtf_conv1x1_bwd_blocks(int M) {
-  if (M <= 0 || M % kTM) throw std::runtime_error("conv1x1_bwd: M % 64 != 0");
-  return c1_blocks(M);
+// number of slab rows (blocks) the fused backward writes for M rows of C channels
+int dtf_conv1x1_bwd_blocks(int M, int C) {
+  if (!dtf_conv1x1_bwd_ok(M, C, 4 * C)) throw std::runtime_error("conv1x1_bwd: shape");
+  return c1_blocks(M, C);
 }
 
 void dtf_conv1x1_bwd_set_grid(int n) { g_c1_grid = n; }
 
 void dtf_conv1x1_bwd(const bf16_t* dout, const bf16_t* wt, const bf16_t* y, const bf16_t* x,
                      const float* mean, const float* inv, const float* sc, const float* sh,
-                     bf16_t* dy, float* wpart, float* bpart, int M, hipStream_t st) {
-  if (M <= 0 || M % kTM) throw std::runtime_error("conv1x1_bwd: M must be a positive multiple of 64");
+                     bf16_t* dy, float* wpart, float* bpart, int M, int C, int K, hipStream_t st) {
+  if (!dtf_conv1x1_bwd_ok(M, C, K))
+    throw std::runtime_error("conv1x1_bwd: (C, K) in {(64, 256), (128, 512)}, M % tile == 0");
   const void* ptrs[] = {dout, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart};
   for (const void* p : ptrs)
     if (!p || (reinterpret_cast<uintptr_t>(p) & 15))
       throw std::runtime_error("conv1x1_bwd: null or misaligned operand");
-  static bool attr = false;
-  if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)conv1x1_bwd_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds));
-    attr = true;
-  }
   C1Args g{dout, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart, M};
-  hipLaunchKernelGGL(conv1x1_bwd_kernel, dim3(c1_blocks(M)), dim3(kT), kLds, st, g);
+  if (C == 64) launch_c1<CfgS0>(g, st);
+  else launch_c1<CfgS1>(g, st);
 }

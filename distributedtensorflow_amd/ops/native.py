@@ -882,21 +882,21 @@ class _BnReluConv1x1(torch.autograd.Function):
 
 
 def _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K):
-    """First-stage c3 (64 -> 256) backward in ONE pass (csrc/kernels/conv1x1_bwd.hip): the
+    """Stage-0 / stage-1 c3 (64 -> 256, 128 -> 512) backward in ONE pass (csrc/kernels/conv1x1_bwd.hip): the
     data gradient dy, the weight gradient (per-block fp32 slabs, reduced here in fixed order
     into the flat gradient buffer or a fresh tensor) and the consuming BatchNorm's backward
     sums (attached to dy as ``_dtf_bnb_part`` for :func:`_bn_backward_core`).  Replaces the
     wgrad pass, the dgrad GEMM and the BN reduce pass (1536 -> 896 B of HBM traffic per row)."""
     dev = dout.device
     st = _st()
-    G = _K.conv1x1_bwd_blocks(M)
+    G = _K.conv1x1_bwd_blocks(M, C)
     wpart = torch.empty(G * K * C, device=dev, dtype=torch.float32)
     part = torch.empty(_K.bn_workspace_floats_g(G, C), device=dev, dtype=torch.float32)
     dy = torch.empty_like(y)
     wt = _dgrad_filter(wb.reshape(K, 1, C)).view(C, K)
     _K.conv1x1_bwd(dout.data_ptr(), wt.data_ptr(), y.data_ptr(), x.data_ptr(),
                    stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(),
-                   stats[3].data_ptr(), dy.data_ptr(), wpart.data_ptr(), part.data_ptr(), M, st)
+                   stats[3].data_ptr(), dy.data_ptr(), wpart.data_ptr(), part.data_ptr(), M, C, K, st)
     dw = None
     if target is not None:
         _K.slab_reduce(wpart.data_ptr(), target.data_ptr(), K * C, G, 1, st)
@@ -910,7 +910,7 @@ def _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K):
     return dy, dw
 
 
-# first-stage c3 backward as one fused pass (A/B knob; summation order of dW and the BN sums
+# stage-0 / stage-1 c3 backward as one fused pass (A/B knob; summation order of dW and the BN sums
 # differs from the separate passes)
 _FUSE_C1_BWD = os.environ.get("DTF_FUSE_C1_BWD", "1") == "1"
 

@@ -193,19 +193,23 @@ def _c1_grads(x, gamma, beta, w, g, fused):
         native._FUSE_C1_BWD = prev
 
 
-@pytest.mark.parametrize("n,hw,grid", [(4, 28, 0), (4, 28, 3), (1, 8, 0), (2, 8, 1), (3, 8, 1)])
-def test_fused_c1_backward_matches_separate_passes(n, hw, grid):
-    """First-stage c3 (64 -> 256) backward as ONE pass (csrc/kernels/conv1x1_bwd.hip: data
-    gradient + weight gradient + the BN backward sums) == the separate wgrad / dgrad / BN reduce
-    passes: the data gradient bit for bit, dW / dgamma / dbeta / dx to fp32 summation order;
-    persistent-grid walks of 1, 2, 3 and 16-17 tiles per block (``grid`` forces the block count)."""
+@pytest.mark.parametrize("c,n,hw,grid", [(64, 4, 28, 0), (64, 4, 28, 3), (64, 1, 8, 0),
+                                          (64, 2, 8, 1), (64, 3, 8, 1), (128, 4, 16, 0),
+                                          (128, 4, 16, 5), (128, 1, 8, 1), (128, 6, 4, 1)])
+def test_fused_c1_backward_matches_separate_passes(c, n, hw, grid):
+    """Stage-0 / stage-1 c3 (64 -> 256, 128 -> 512) backward as ONE pass
+    (csrc/kernels/conv1x1_bwd.hip: data gradient + weight gradient + the BN backward sums) ==
+    the separate wgrad / dgrad / BN reduce passes: the data gradient bit for bit, dW / dgamma /
+    dbeta / dx to fp32 summation order, and all of them against fp32 math of the op; persistent-
+    grid walks of 1, 2, 3 and many tiles per block (``grid`` forces the block count)."""
     torch.manual_seed(0)
-    x = torch.randn(n, hw, hw, 64, device="cuda").bfloat16()
-    w = torch.randn(256, 1, 1, 64, device="cuda") / 8
-    gamma = torch.rand(64, device="cuda") + 0.5
-    beta = torch.randn(64, device="cuda") * 0.2
-    g = torch.randn(n, hw, hw, 256, device="cuda").bfloat16()
-    assert native._K.conv1x1_bwd_ok(n * hw * hw, 64, 256)
+    k = 4 * c
+    x = torch.randn(n, hw, hw, c, device="cuda").bfloat16()
+    w = torch.randn(k, 1, 1, c, device="cuda") / c ** 0.5
+    gamma = torch.rand(c, device="cuda") + 0.5
+    beta = torch.randn(c, device="cuda") * 0.2
+    g = torch.randn(n, hw, hw, k, device="cuda").bfloat16()
+    assert native._K.conv1x1_bwd_ok(n * hw * hw, c, k)
     native._K.conv1x1_bwd_set_grid(grid)
     try:
         dy1, g1 = _c1_grads(x, gamma, beta, w, g, True)
@@ -217,13 +221,12 @@ def test_fused_c1_backward_matches_separate_passes(n, hw, grid):
         a, b = a.float(), b.float()
         rel = ((a - b).norm() / b.norm()).item()
         assert rel < (2e-2 if name == "dx" else 1e-4), (name, rel)
-    # and against fp32 math of the same op
     xs = x.float().requires_grad_(True)
     ps = [t.clone().requires_grad_(True) for t in (gamma, beta, w)]
     mean = xs.mean((0, 1, 2))
     var = xs.var((0, 1, 2), unbiased=False)
     yb = torch.relu((xs - mean) / torch.sqrt(var + 1e-5) * ps[0] + ps[1])
-    ref = torch.einsum("nhwc,kc->nhwk", yb, ps[2].view(256, 64))
+    ref = torch.einsum("nhwc,kc->nhwk", yb, ps[2].view(k, c))
     gr = torch.autograd.grad(ref, [xs] + ps, g.float())
     for a, b, name in zip(g1, gr, ("dx", "dgamma", "dbeta", "dw")):
         rel = ((a.float() - b).norm() / b.norm()).item()
