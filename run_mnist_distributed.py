@@ -43,6 +43,9 @@ def main():
     from distributedtensorflow_amd.train import (ConfigProto, MonitoredTrainingSession,
                                                  StopAtStepHook, get_or_create_global_step)
 
+    if FLAGS.seed is not None:           # default: unseeded random init, like the reference
+        torch.manual_seed(FLAGS.seed)
+
     print("run main with args =", FLAGS, flush=True)
     config = Config(FLAGS.config)
     ps_hosts, worker_hosts = config.get_ps_and_worker_hosts()
@@ -173,6 +176,9 @@ def parse(argv=None):
     parser.add_argument("--save_checkpoint_steps", type=int, default=None,
                         help="chief checkpoints every N global steps (default: every 600 s)")
     parser.add_argument("--sync_replicas", action="store_true")
+    parser.add_argument("--seed", type=int, default=None,
+                        help="seed the variable initialisers (reproducible runs; not a reference "
+                             "flag)")
     parser.add_argument("--device", choices=("auto", "cpu", "gpu"), default="auto")
     parser.add_argument("--dtype", choices=("auto", "bf16", "fp32"), default="fp32",
                         help="compute dtype: fp32 (default) = the reference's precision "

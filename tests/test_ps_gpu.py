@@ -117,7 +117,7 @@ def test_pipelined_push_pull_matches_serial_one_worker(tmp_path, pipeline):
         d = tmp_path / f"p{mode}_{len(outs)}"
         codes, logs = launch_local(os.path.join(ROOT, "run_mnist_distributed.py"), 1, 1, str(d),
                                    ["--max_steps=40", f"--data_dir={tmp_path}/data",
-                                    f"--log_dir={d}/tb", "--ps_device=gpu",
+                                    f"--log_dir={d}/tb", "--ps_device=gpu", "--seed=7",
                                     f"--checkpoint_dir={d}/ckpt", "--save_checkpoint_steps=1000"],
                                    env={"PYTHONPATH": ROOT, "DTF_PS_PIPELINE": mode},
                                    timeout_s=100, grace_s=20)
