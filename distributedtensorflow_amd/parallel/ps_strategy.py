@@ -146,7 +146,12 @@ class _RemotePSReducer(_NullReducer):
         self._fenced = 0
         from .. import ops
         ops.set_param_fence(self._op_fence)
-        return self.client.global_step
+        # the answer to this push is still in flight: report the step it will at least produce
+        # (an async push advances the PS's global step by exactly one; the previous answer
+        # arrived at this step's first fence).  Exact with one worker, a lower bound with more --
+        # the serial form's answer would also count other workers' pushes applied meanwhile.
+        # StopAtStepHook then stops at the same step as the serial data plane.
+        return self.client.global_step + 1
 
     # -- pull (next forward)
     def _issue_pulls(self):
