@@ -137,6 +137,10 @@ void dtf_gemm_stream_bnb(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, i
                          const float*, const float*, const float*, const float*, const uint8_t*,
                          int, float*, int, hipStream_t);
 bool dtf_gemm_stream_ok(int, int, int, int, int, int);
+void dtf_gemm_stream_bnb_dual(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int,
+                              const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*,
+                              const float*, const float*, const uint8_t*, float*, const bf16_t*,
+                              const float*, const float*, float*, hipStream_t);
 void dtf_gemm_stream_probe(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void dtf_gemm_stream_pre(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, const float*,
                          const float*, bf16_t*, float*, hipStream_t);
@@ -722,6 +726,18 @@ PYBIND11_MODULE(_dtf_hip, m) {
                         P<float>(mean), P<float>(inv), P<float>(sc), P<float>(sh),
                         P<uint8_t>(bmask), kind, P<float>(part), 0, S(stream));
     check_launch("gemm_stream_bnb");
+  });
+  m.def("gemm_stream_bnb_dual", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K,
+                                   int lda, int ldb, int ldc, uintptr_t cin, uintptr_t acc_src,
+                                   uintptr_t acc_mask, uintptr_t bx, uintptr_t mean, uintptr_t inv,
+                                   uintptr_t bmask, uintptr_t part, uintptr_t bxp, uintptr_t meanp,
+                                   uintptr_t invp, uintptr_t part_p, uintptr_t stream) {
+    dtf_gemm_stream_bnb_dual(P<bf16_t>(a), P<bf16_t>(b), P<bf16_t>(c), M, N, K, lda, ldb, ldc,
+                             P<bf16_t>(cin), P<bf16_t>(acc_src), P<uint8_t>(acc_mask),
+                             P<bf16_t>(bx), P<float>(mean), P<float>(inv), P<uint8_t>(bmask),
+                             P<float>(part), P<bf16_t>(bxp), P<float>(meanp), P<float>(invp),
+                             P<float>(part_p), S(stream));
+    check_launch("gemm_stream_bnb_dual");
   });
   m.def("gemm_set_stagger", &dtf_gemm_set_stagger);
   m.def("gemm_set_group", &dtf_gemm_set_group);

@@ -95,9 +95,12 @@ DTF_DEV uint32_t lds_addr(const bf16_t* p) {
 // kernel waits with explicit counted vmcnt instead.  M0 is saved and restored around it.
 DTF_DEV void dma16(const i32x4_t& r, uint32_t lds, uint32_t voff) {
   uint32_t save;
+  // the LDS base is wave-uniform by contract; readfirstlane states it where the compiler's
+  // uniformity analysis lost track (a no-op when the value already lives in an SGPR)
+  const uint32_t l = __builtin_amdgcn_readfirstlane(lds);
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
                "s_mov_b32 m0, %0"
-               : "=&s"(save) : "s"(lds), "v"(voff), "s"(r) : "memory");
+               : "=&s"(save) : "s"(l), "v"(voff), "s"(r) : "memory");
 }
 #define DTF_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 DTF_DEV void raw_barrier() {

@@ -64,6 +64,13 @@ struct StreamArgs {
   const float* pre_sc;
   const float* pre_sh;
   bf16_t* pre_y;
+  // DUAL (kind 1 only): C is also the output gradient of a second BatchNorm whose output was
+  // ADDED before the shared ReLU (a projection block's shortcut BN): its sums sum dz,
+  // sum dz * (xp - meanp) * invstdp go to `statsp` ([ceil(M/256)][2][N])
+  const bf16_t* bxp;
+  const float* bmeanp;
+  const float* binvp;
+  float* statsp;
 };
 
 DTF_DEV int sswz(int row, int ch) { return ch ^ ((row >> 1) & 7); }   // 64-deep panel swizzle
@@ -83,7 +90,8 @@ DTF_DEV void wait_vmc() {
 // BMK >= 0: BN-backward sums of the output (0 no ReLU, 1 ReLU bit mask, 2 ReLU from x)
 // PROBE (timing experiments only, tools/gemm_bench.py --stream-probe): 1 no MFMAs, 2 no LDS
 // staging of C, 4 no chunk barrier, 8 C stores out of range
-template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false, int PROBE = 0>
+template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false, int PROBE = 0,
+          bool DUAL = false>
 __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g) {
   constexpr int KS = K / 32;                  // MFMA k-steps
   constexpr int CH = kSBN * K;                // bf16 elements per ring slot
@@ -91,8 +99,10 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   constexpr int S = kSWR * kSBN * 2 / (64 * 16);   // 16-B stores per lane per chunk (4)
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   bf16_t* stg = lds + 3 * CH;
-  float* sred = reinterpret_cast<float*>(stg + 8 * kSWR * kSP);   // [2][8][2][64]
-  float* bprm = sred + 2 * 8 * 2 * kSBN;                           // BNB: [4][N] mean/inv/sc/sh
+  static_assert(!DUAL || BMK == 1, "DUAL: the residual BatchNorm's ReLU bit mask");
+  constexpr int NQ = DUAL ? 3 : 2;                                 // per-channel quantities
+  float* sred = reinterpret_cast<float*>(stg + 8 * kSWR * kSP);   // [2][8][NQ][64]
+  float* bprm = sred + 2 * 8 * NQ * kSBN;   // BNB: [4][N] mean/inv/sc/sh (DUAL: mean/inv/meanp/invp)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int frow = lane & 15, fq = lane >> 4;
@@ -104,14 +114,15 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   constexpr bool do_stats = STATS || BNB;
   constexpr int mode = MODE;
   // prefetch loads per chunk: the accumulate operands, the BN input, its mask bytes
-  constexpr int L = (MODE == 1 ? S : (MODE == 2 ? 2 * S : 0)) + (BNB ? S : 0) + (BMK == 1 ? S : 0);
+  constexpr int L = (MODE == 1 ? S : (MODE == 2 ? 2 * S : 0)) + (BNB ? S : 0) + (BMK == 1 ? S : 0) +
+                    (DUAL ? S : 0);
 
   // BNB: this block's copy of the per-channel parameters (one float4 per array per thread:
   // N <= 2048), written to LDS after the first wait
-  constexpr int NPRM = BMK == 2 ? 4 : 2;
+  constexpr int NPRM = (BMK == 2 || DUAL) ? 4 : 2;
   float4 prm[NPRM];
   if constexpr (BNB) {
-    const float* arrs[4] = {g.bmean, g.binv, g.bsc, g.bsh};
+    const float* arrs[4] = {g.bmean, g.binv, DUAL ? g.bmeanp : g.bsc, DUAL ? g.binvp : g.bsh};
 #pragma unroll
     for (int a = 0; a < NPRM; ++a)
       prm[a] = tid * 4 < g.N ? *reinterpret_cast<const float4*>(arrs[a] + tid * 4)
@@ -164,7 +175,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     const int rr = wave * kSWR + t * 8 + er;
     return rr < rows_blk ? (uint32_t)((rr * ldc + c * kSBN + ec * 8) * 2) : kSOOB;
   };
-  uint4 pre[S], bxp[S];
+  uint4 pre[S], bxp[S], bpp[S];
   uint32_t pmask[S], bmp[S];
   const __amdgpu_buffer_rsrc_t rbx =
       srsrc(BNB ? (const void*)(g.bx + m0 * ldc) : (const void*)g.C,
@@ -172,6 +183,9 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   const __amdgpu_buffer_rsrc_t rbm =
       srsrc(BMK == 1 ? (const void*)(g.bmask + m0 * ldc / 8) : (const void*)g.C,
             BMK == 1 ? (uint32_t)(rows_blk * ldc / 8) : 0u);
+  const __amdgpu_buffer_rsrc_t rbp =
+      srsrc(DUAL ? (const void*)(g.bxp + m0 * ldc) : (const void*)g.C,
+            DUAL ? (uint32_t)(rows_blk * ldc * 2) : 0u);
   auto prefetch = [&](int c) {
     if constexpr (MODE == 0 && !BNB) return;
     const int cc = c < nch ? c : 0;
@@ -186,9 +200,26 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
         bxp[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbx, off, 0, 0));
       if constexpr (BMK == 1)
         bmp[t] = __builtin_amdgcn_raw_buffer_load_b8(rbm, off == kSOOB ? kSOOB : off / 16, 0, 0);
+      if constexpr (DUAL)
+        bpp[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbp, off, 0, 0));
     }
   };
 
+  // chunk c's per-channel sums (8 waves' partials, fixed order) -> slab row blockIdx.x; DUAL: sum dz
+  // is shared, the shortcut BN's sum dz x-hat_p is quantity 2
+  auto write_slab = [&](int c) {
+    const int which = tid >> 6, col = tid & 63;
+    const float* sr = sred + (c & 1) * 8 * NQ * kSBN;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t += sr[(w * NQ + which) * kSBN + col];
+    const long o = (long)blockIdx.x * 2 * g.N + c * kSBN + col;
+    if (which < 2) g.stats[o + (long)which * g.N] = t;
+    if constexpr (DUAL) {
+      if (which == 0) g.statsp[o] = t;
+      if (which == 2) g.statsp[o + g.N] = t;
+    }
+  };
   issue(0);
   issue(1);
   constexpr int Y = PRE ? 2 * KS : 0;          // PRE: 16-B stores of the normalised A rows
@@ -237,14 +268,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (!(PROBE & 4)) raw_barrier();   // ... every wave's; every wave finished reading chunk c - 1's slot
-    if (do_stats && c > 0 && tid < 2 * kSBN) {
-      const int which = tid >> 6, col = tid & 63;
-      const float* sr = sred + ((c - 1) & 1) * 8 * 2 * kSBN;
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) t += sr[(w * 2 + which) * kSBN + col];
-      g.stats[((long)blockIdx.x * 2 + which) * g.N + (c - 1) * kSBN + col] = t;
-    }
+    if (do_stats && c > 0 && tid < NQ * kSBN) write_slab(c - 1);
     issue(c + 2);
     const bf16_t* sb = lds + (c % 3) * CH;
     f32x4_t acc[2][4];
@@ -299,7 +323,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
         s2[j] += __shfl_xor(s2[j], 32, 64);
       }
       if (fq == 0) {
-        float* sr = sred + (c & 1) * 8 * 2 * kSBN + wave * 2 * kSBN;
+        float* sr = sred + (c & 1) * 8 * NQ * kSBN + wave * NQ * kSBN;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           sr[j * 16 + frow] = s1[j];
@@ -311,16 +335,17 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     // writes (one wave's LDS instructions execute in order)
     asm volatile("" ::: "memory");
     if constexpr (L != 0) wait_vmc<D>();      // this chunk's prefetched epilogue operands
-    float b1[8], b2[8], bmu[8], bis[8], bsc[8], bsh[8];
+    float b1[8], b2[8], b3[8], bmu[8], bis[8], bsc[8], bsh[8];
     if constexpr (BNB) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) b1[e] = b2[e] = 0.f;
+      for (int e = 0; e < 8; ++e) b1[e] = b2[e] = b3[e] = 0.f;
       const int ch0 = c * kSBN + ec * 8;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         bmu[e] = bprm[ch0 + e];
         bis[e] = bprm[g.N + ch0 + e];
-        if constexpr (BMK == 2) { bsc[e] = bprm[2 * g.N + ch0 + e]; bsh[e] = bprm[3 * g.N + ch0 + e]; }
+        // BMK 2: forward scale / shift; DUAL: the shortcut BN's mean / invstd
+        if constexpr (BMK == 2 || DUAL) { bsc[e] = bprm[2 * g.N + ch0 + e]; bsh[e] = bprm[3 * g.N + ch0 + e]; }
       }
     }
 #pragma unroll
@@ -343,16 +368,18 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
       if constexpr (BNB) {
         if (wave * kSWR + t * 8 + er < rows_blk) {
           // the BatchNorm backward's reduce, on the gradient exactly as it is stored
-          float gd[8], xv[8];
+          float gd[8], xv[8], pv[8];
           unpack8(v, gd);
           unpack8(bxp[t], xv);
+          if constexpr (DUAL) unpack8(bpp[t], pv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float dz = gd[e];
             if constexpr (BMK == 1) dz = (bmp[t] >> e) & 1u ? dz : 0.f;
-            if constexpr (BMK == 2) dz = __builtin_fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? dz : 0.f;
+            if constexpr (BMK == 2 && !DUAL) dz = __builtin_fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? dz : 0.f;
             b1[e] += dz;
             b2[e] += dz * (xv[e] - bmu[e]) * bis[e];
+            if constexpr (DUAL) b3[e] += dz * (pv[e] - bsc[e]) * bsh[e];
           }
         }
       }
@@ -373,13 +400,22 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
         b2[e] += __shfl_xor(b2[e], 8, 64);
         b2[e] += __shfl_xor(b2[e], 16, 64);
         b2[e] += __shfl_xor(b2[e], 32, 64);
+        if constexpr (DUAL) {
+          b3[e] += __shfl_xor(b3[e], 8, 64);
+          b3[e] += __shfl_xor(b3[e], 16, 64);
+          b3[e] += __shfl_xor(b3[e], 32, 64);
+        }
       }
       if (er == 0) {
-        float* sr = sred + (c & 1) * 8 * 2 * kSBN + wave * 2 * kSBN + ec * 8;
+        float* sr = sred + (c & 1) * 8 * NQ * kSBN + wave * NQ * kSBN + ec * 8;
         *reinterpret_cast<float4*>(sr) = make_float4(b1[0], b1[1], b1[2], b1[3]);
         *reinterpret_cast<float4*>(sr + 4) = make_float4(b1[4], b1[5], b1[6], b1[7]);
         *reinterpret_cast<float4*>(sr + kSBN) = make_float4(b2[0], b2[1], b2[2], b2[3]);
         *reinterpret_cast<float4*>(sr + kSBN + 4) = make_float4(b2[4], b2[5], b2[6], b2[7]);
+        if constexpr (DUAL) {
+          *reinterpret_cast<float4*>(sr + 2 * kSBN) = make_float4(b3[0], b3[1], b3[2], b3[3]);
+          *reinterpret_cast<float4*>(sr + 2 * kSBN + 4) = make_float4(b3[4], b3[5], b3[6], b3[7]);
+        }
       }
     }
     prefetch(c + 1);
@@ -387,38 +423,33 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   DTF_WAIT_VM(0);       // the trailing out-of-range DMAs still target the ring
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();
-  if (do_stats && tid < 2 * kSBN) {
-    const int which = tid >> 6, col = tid & 63, c = nch - 1;
-    const float* sr = sred + (c & 1) * 8 * 2 * kSBN;
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) t += sr[(w * 2 + which) * kSBN + col];
-    g.stats[((long)blockIdx.x * 2 + which) * g.N + c * kSBN + col] = t;
-  }
+  if (do_stats && tid < NQ * kSBN) write_slab(nch - 1);
 }
 
-template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false, int PROBE = 0>
+template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false, int PROBE = 0,
+          bool DUAL = false>
 void launch_stream(const StreamArgs& g, hipStream_t st) {
   constexpr size_t BASE = (size_t)3 * kSBN * K * 2 + (size_t)8 * kSWR * kSP * 2 +
-                          (size_t)2 * 8 * 2 * kSBN * 4;
+                          (size_t)2 * 8 * (DUAL ? 3 : 2) * kSBN * 4;
   static_assert(BASE <= 160 * 1024, "gemm_stream LDS");
   // BNB: + the per-channel parameter arrays
-  const size_t LDS = BASE + (BMK >= 0 ? (size_t)(BMK == 2 ? 4 : 2) * g.N * 4 : 0);
+  const size_t LDS = BASE + (BMK >= 0 ? (size_t)((BMK == 2 || DUAL) ? 4 : 2) * g.N * 4 : 0);
   if (LDS > 160 * 1024) throw std::runtime_error("gemm_stream: BN-backward parameters exceed LDS");
   static bool attr = false;
   if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS, BMK, PRE, PROBE>,
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS, BMK, PRE, PROBE, DUAL>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const unsigned blocks = (unsigned)((g.M + kSBM - 1) / kSBM);
-  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS, BMK, PRE, PROBE>), dim3(blocks), dim3(kST),
-                     LDS, st, g);
+  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS, BMK, PRE, PROBE, DUAL>), dim3(blocks),
+                     dim3(kST), LDS, st, g);
 }
 
 template <int K, int MODE>
 void launch_stream_bnb(const StreamArgs& g, int bmk, hipStream_t st) {
-  if (bmk == 1) launch_stream<K, MODE, false, 1>(g, st);
+  if (g.bxp) launch_stream<K, MODE, false, 1, false, 0, true>(g, st);
+  else if (bmk == 1) launch_stream<K, MODE, false, 1>(g, st);
   else if (bmk == 2) launch_stream<K, MODE, false, 2>(g, st);
   else launch_stream<K, MODE, false, 0>(g, st);
 }
@@ -488,6 +519,29 @@ void dtf_gemm_stream_bnb(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
   StreamArgs g{A, B, C, Cin, acc_src, acc_mask, part, M, N, lda, ldb, ldc, nt,
                bx, bmean, binv, bsc, bsh, bmask};
   run_stream(g, K, kind, st);
+}
+
+// dtf_gemm_stream_bnb for the output gradient of relu(BN(x) + BN_p(xp)) (kind 1, bit mask): also
+// the shortcut BN's sums (sum dz, sum dz xp-hat) into part_p.  Replaces the dual reduce pass.
+void dtf_gemm_stream_bnb_dual(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K,
+                              int lda, int ldb, int ldc, const bf16_t* Cin, const bf16_t* acc_src,
+                              const uint8_t* acc_mask, const bf16_t* bx, const float* bmean,
+                              const float* binv, const uint8_t* bmask, float* part,
+                              const bf16_t* bxp, const float* bmeanp, const float* binvp,
+                              float* part_p, hipStream_t st) {
+  if (!dtf_gemm_stream_ok(M, N, K, lda, ldb, ldc) || ldc != N || N > 2048)
+    throw std::runtime_error("gemm_stream_bnb_dual: stream shape, dense C, N <= 2048");
+  if (Cin && acc_mask) throw std::runtime_error("gemm_stream_bnb_dual: Cin or masked acc, not both");
+  if (acc_mask && !acc_src) throw std::runtime_error("gemm_stream_bnb_dual: masked acc needs acc_src");
+  if (!bx || !bmean || !binv || !bmask || !part || !bxp || !bmeanp || !binvp || !part_p)
+    throw std::runtime_error("gemm_stream_bnb_dual: BatchNorm operands");
+  StreamArgs g{A, B, C, Cin, acc_src, acc_mask, part, M, N, lda, ldb, ldc, 0,
+               bx, bmean, binv, nullptr, nullptr, bmask};
+  g.bxp = bxp;
+  g.bmeanp = bmeanp;
+  g.binvp = binvp;
+  g.statsp = part_p;
+  run_stream(g, K, 1, st);
 }
 
 // C = relu(BN(X)) . B^T with the BatchNorm + ReLU applied to the A rows in registers (scale /

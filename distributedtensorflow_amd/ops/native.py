@@ -231,6 +231,9 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_f
     pt, pb, pl, pr = resolve_padding(padding, h, wd, R, S, stride)
     dx = None
     wflat = w_bf16.reshape(K, R * S, C)
+    if isinstance(bnb, _DualBnb) and not (_gemm_1x1(K, C, R, S, stride, (pt, pl)) and
+                                          _stream_bnb_ok(K, C)):
+        bnb = None       # the dual sums ride only on the streamed 1x1 data gradient
     if _gemm_1x1(K, C, R, S, stride, (pt, pl)) and (bnb is None or _stream_bnb_ok(K, C)):
         # 1x1 stride 1: dX[M, C] = dY[M, K] . Wt[C, K]^T on the GEMM kernel, residual
         # gradients (materialised or masked) folded into its epilogue
@@ -312,10 +315,23 @@ def _stream_bnb_ok(K, C):
     return _GEMM_STREAM and K in (64, 128, 256) and C >= K and C % 64 == 0 and C <= 2048
 
 
+class _DualBnb:
+    """The consuming conv's record of relu(BN(x) + BN_p(xp)) (:class:`_BatchNormAddBatchNorm`):
+    its streamed data gradient also emits both BatchNorms' backward sums."""
+    __slots__ = ("x", "stats", "mask", "xp", "stats_p", "tok")
+
+    def __init__(self, x, stats, mask, xp, stats_p, tok):
+        self.x, self.stats, self.mask, self.xp, self.stats_p, self.tok = \
+            x, stats, mask, xp, stats_p, tok
+
+
 def _dgrad_1x1_bnb(dyc, wt, M, C, K, xshape, out, acc_from, bnb):
     """1x1 data gradient on the row-streaming GEMM whose epilogue also reduces the BN backward
     sums (sum dz, sum dz x-hat) of the BatchNorm that produced x: its separate reduce pass over
-    (dy, x) is skipped (the sums ride on the data gradient still in registers; only x is read)."""
+    (dy, x) is skipped (the sums ride on the data gradient still in registers; only x is read).
+    A :class:`_DualBnb` adds the shortcut BatchNorm's sums (its dual reduce pass is skipped)."""
+    if isinstance(bnb, _DualBnb):
+        return _dgrad_1x1_bnb_dual(dyc, wt, M, C, K, xshape, out, acc_from, bnb)
     xb, stats, mask, relu, has_res, tok = bnb
     if out is not None and acc_from is not None:
         out.add_(acc_from.materialize())
@@ -336,6 +352,29 @@ def _dgrad_1x1_bnb(dyc, wt, M, C, K, xshape, out, acc_from, bnb):
     # valid only for this exact gradient: autograd may add another contribution IN PLACE
     # (a residual gradient summed outside the epilogue), which bumps the version counter
     dx._dtf_bnb_part = (part, G, M, C, tok, dx._version)
+    return dx
+
+
+def _dgrad_1x1_bnb_dual(dyc, wt, M, C, K, xshape, out, acc_from, d):
+    if out is not None and acc_from is not None:
+        out.add_(acc_from.materialize())
+        acc_from = None
+    o2 = out.view(M, C) if out is not None else torch.empty(M, C, device=dyc.device, dtype=_BF16)
+    G = _K.gemm_tile_rows(M)
+    ws = _K.bn_workspace_floats_g(G, C)
+    part = torch.empty(ws, device=dyc.device, dtype=torch.float32)
+    part_p = torch.empty(ws, device=dyc.device, dtype=torch.float32)
+    _K.gemm_stream_bnb_dual(dyc.data_ptr(), wt.data_ptr(), o2.data_ptr(), M, C, K, K, K, C,
+                            o2.data_ptr() if out is not None else 0,
+                            acc_from.dy.data_ptr() if acc_from is not None else 0,
+                            acc_from.mask.data_ptr() if acc_from is not None else 0,
+                            d.x.data_ptr(), d.stats[0].data_ptr(), d.stats[1].data_ptr(),
+                            d.mask.data_ptr(), part.data_ptr(), d.xp.data_ptr(),
+                            d.stats_p[0].data_ptr(), d.stats_p[1].data_ptr(), part_p.data_ptr(),
+                            _st())
+    dx = o2.view(xshape)
+    dx._dtf_bnb_part = (part, G, M, C, d.tok, dx._version)
+    dx._dtf_bnb_part_p = part_p
     return dx
 
 
@@ -426,6 +465,9 @@ class _Conv2d(torch.autograd.Function):
                                                         (pads[0], pads[2]))
                       and _stream_bnb_ok(K_, xb.shape[-1]))
         ctx.bnb = bnb if ((_FUSE_BN_BWD or stream_bnb) and bnb is not None and xb is x) else None
+        dual = getattr(x, "_dtf_bnb_dual", None)
+        if dual is not None and stream_bnb and ctx.bnb is None and xb is x:
+            ctx.bnb = _DualBnb(*dual)
         if x.requires_grad and xb is x and wb.is_contiguous():
             _register_dgrad_filter(wb)
         return conv2d_forward(xb, wb, stride, padding, stats)
@@ -962,6 +1004,11 @@ class _BatchNormAddBatchNorm(torch.autograd.Function):
         ctx.params = (gamma, beta)
         ctx.params_p = (gamma_p, beta_p)
         ctx.dtypes = (gamma.dtype, beta.dtype, gamma_p.dtype, beta_p.dtype)
+        ctx.bnb_token = None
+        if training and _FUSE_DUAL_BNB:
+            # a streamed 1x1 data gradient of y (the next block's c1) emits both BNs' sums
+            ctx.bnb_token = object()
+            y._dtf_bnb_dual = (x, stats, mask, xp, stats_p, ctx.bnb_token)
         return y
 
     @staticmethod
@@ -971,14 +1018,24 @@ class _BatchNormAddBatchNorm(torch.autograd.Function):
         C = x.shape[-1]
         M = x.numel() // C
         st = _st()
-        ws = _K.bn_workspace_floats(M, C)
-        part = torch.empty(ws, device=x.device, dtype=torch.float32)
-        part_p = torch.empty(ws, device=x.device, dtype=torch.float32)
-        _K.bn_bwd_reduce_dual(dy.data_ptr(), mask.data_ptr(), x.data_ptr(), stats[0].data_ptr(),
-                              stats[1].data_ptr(), xp.data_ptr(), stats_p[0].data_ptr(),
-                              stats_p[1].data_ptr(), M, C, part.data_ptr(), part_p.data_ptr(), st)
-        gb, direct = _bn_bwd_finalize_p(ctx.params, part, None, M, C, g32, stats)
-        gbp, direct_p = _bn_bwd_finalize_p(ctx.params_p, part_p, None, M, C, g32_p, stats_p)
+        fused = getattr(dy, "_dtf_bnb_part", None)
+        tok = ctx.bnb_token
+        if (fused is not None and tok is not None and fused[4] is tok and fused[2:4] == (M, C)
+                and fused[5] == dy._version and getattr(dy, "_dtf_bnb_part_p", None) is not None):
+            # both BNs' sums came from the streamed data gradient that produced dy
+            part, G = fused[0], fused[1]
+            part_p = dy._dtf_bnb_part_p
+        else:
+            ws = _K.bn_workspace_floats(M, C)
+            part = torch.empty(ws, device=x.device, dtype=torch.float32)
+            part_p = torch.empty(ws, device=x.device, dtype=torch.float32)
+            G = None
+            _K.bn_bwd_reduce_dual(dy.data_ptr(), mask.data_ptr(), x.data_ptr(),
+                                  stats[0].data_ptr(), stats[1].data_ptr(), xp.data_ptr(),
+                                  stats_p[0].data_ptr(), stats_p[1].data_ptr(), M, C,
+                                  part.data_ptr(), part_p.data_ptr(), st)
+        gb, direct = _bn_bwd_finalize_p(ctx.params, part, G, M, C, g32, stats)
+        gbp, direct_p = _bn_bwd_finalize_p(ctx.params_p, part_p, G, M, C, g32_p, stats_p)
         dx, dxp = torch.empty_like(x), torch.empty_like(xp)
         _K.bn_bwd_apply_dual(dy.data_ptr(), mask.data_ptr(), x.data_ptr(), gb[2].data_ptr(),
                              gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), xp.data_ptr(),
@@ -989,6 +1046,10 @@ class _BatchNormAddBatchNorm(torch.autograd.Function):
         dg, db = (None, None) if direct else (gb[0].to(gd), gb[1].to(bd))
         dgp, dbp = (None, None) if direct_p else (gbp[0].to(gpd), gbp[1].to(bpd))
         return dx, dg, db, None, None, dxp, dgp, dbp, None, None, None, None, None
+
+
+# the streamed c1 data gradient of the next block emits a projection block's dual BN sums
+_FUSE_DUAL_BNB = os.environ.get("DTF_FUSE_DUAL_BNB", "1") == "1"
 
 
 def batch_norm_add_batch_norm(x, gamma, beta, running_mean, running_var, xp, gamma_p, beta_p,

@@ -29,9 +29,11 @@ def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False, lazy=True):
     prev, prev_r, prev_s = native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD, native._SHARE_INPUT_GRAD
     prev_b, prev_l = native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD
     prev_bs, prev_c1 = native._FUSE_BN_BWD_STREAM, native._FUSE_C1_BWD
+    prev_d = native._FUSE_DUAL_BNB
     native._FUSE_BN_BWD = fuse_bnb
     native._FUSE_BN_BWD_STREAM = fuse_bnb
     native._FUSE_C1_BWD = fuse_bnb
+    native._FUSE_DUAL_BNB = fuse_bnb
     native._LAZY_RESIDUAL_GRAD = lazy
     native._DIRECT_GRAD = direct
     native._FUSE_RESIDUAL_GRAD = fuse_res
@@ -49,6 +51,7 @@ def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False, lazy=True):
         native._SHARE_INPUT_GRAD = prev_s
         native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD = prev_b, prev_l
         native._FUSE_BN_BWD_STREAM, native._FUSE_C1_BWD = prev_bs, prev_c1
+        native._FUSE_DUAL_BNB = prev_d
 
 
 def test_direct_grad_path_bit_identical():
@@ -373,6 +376,50 @@ def test_resnet50_grads_with_fused_bn_backward_sums():
     cos = torch.nn.functional.cosine_similarity(ga, gb, dim=0).item()
     assert cos > 0.99, cos
     n_tail = 2048 * 1000                 # the fc kernel lives first in the flat buffer
+    tail = ((ga[:n_tail] - gb[:n_tail]).norm() / gb[:n_tail].norm()).item()
+    assert tail < 1e-2, tail
+
+
+def _default_step_grads(model, dual):
+    """One step's loss and flat gradient with the default fusions, the dual-BN sums on or off."""
+    prev = native._FUSE_DUAL_BNB
+    native._FUSE_DUAL_BNB = dual
+    try:
+        with OneDeviceStrategy("cuda").scope():
+            opt = MomentumOptimizer(0.1, 0.9)
+            x, y = _inputs()
+            loss = ops.sparse_softmax_cross_entropy(model(x), y)
+            opt.compute_gradients(loss, list(model.parameters()))
+            torch.cuda.synchronize()
+            return loss.item(), opt.space.grad.clone()
+    finally:
+        native._FUSE_DUAL_BNB = prev
+
+
+def test_dual_bn_sums_from_streamed_dgrad():
+    """A projection block's relu(BN(x) + BN_p(xp)) backward takes BOTH BatchNorms' sums from the
+    next block's streamed c1 data gradient (gemm_stream DUAL epilogue) instead of its own dual
+    reduce pass: used at the three stream-shaped stages, and the step's gradients match the
+    separate-pass form to summation order."""
+    torch.manual_seed(0)
+    base = resnet50().cuda()
+    calls = {"n": 0}
+    orig = native._K.gemm_stream_bnb_dual
+
+    def spy(*a):
+        calls["n"] += 1
+        return orig(*a)
+    native._K.gemm_stream_bnb_dual = spy
+    try:
+        la, ga = _default_step_grads(copy.deepcopy(base), True)
+    finally:
+        native._K.gemm_stream_bnb_dual = orig
+    assert calls["n"] == 3, calls          # s0b1 / s1b1 / s2b1 c1 (s3: reduction 512)
+    lb, gb = _default_step_grads(copy.deepcopy(base), False)
+    assert la == lb
+    cos = torch.nn.functional.cosine_similarity(ga, gb, dim=0).item()
+    assert cos > 0.99, cos
+    n_tail = 2048 * 1000
     tail = ((ga[:n_tail] - gb[:n_tail]).norm() / gb[:n_tail].norm()).item()
     assert tail < 1e-2, tail
 
