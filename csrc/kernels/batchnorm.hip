@@ -455,13 +455,13 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                  MK, ksc, ksh);
       if (dres) stv<NT>(DR4 + v, pack8(g));
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = ka[i] * g[i] + kb[i] * xv[i] + kc[i];
+      for (int i = 0; i < 8; ++i) o[i] = bn_bwd_dx(ka[i], g[i], kb[i], xv[i], kc[i]);
       stv<NT>(DX4 + v, pack8(o));
       if (DUAL) {
         float pv[8];
         unpack8(pr[u], pv);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = pa[i] * g[i] + pb[i] * pv[i] + pc[i];
+        for (int i = 0; i < 8; ++i) o[i] = bn_bwd_dx(pa[i], g[i], pb[i], pv[i], pc[i]);
         stv<NT>(DXP4 + v, pack8(o));
       }
     }

@@ -109,6 +109,13 @@ DTF_DEV void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// ---- BatchNorm backward apply: dx = A dz + B x + C per channel, in ONE explicit operation order
+// (every kernel that forms it -- the apply passes, the pool-fused stem pass, the fused 1x1
+// backward that consumes it without storing -- must round identically)
+DTF_DEV float bn_bwd_dx(float a, float dz, float b, float x, float c) {
+  return __builtin_fmaf(a, dz, b * x) + c;
+}
+
 // ---- GELU (tanh approximation, BERT's "gelu") shared by the NLP kernels and the GEMM epilogue
 constexpr float kGeluK0 = 0.7978845608028654f;   // sqrt(2/pi)
 constexpr float kGeluK1 = 0.044715f;

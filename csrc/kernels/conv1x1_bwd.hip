@@ -40,10 +40,13 @@ constexpr int kNB = 3;               // ring slots
 typedef __attribute__((ext_vector_type(4))) short s4_t;
 typedef __attribute__((address_space(3))) s4_t lds_s4_t;
 
-// per-shape configuration: C in, K out, TM rows per tile, NW waves
-template <int C_, int K_, int TM_, int NW_>
+// per-shape configuration: C in, K out, TM rows per tile, NW waves; LZ: the conv-output gradient
+// dO is formed in the kernel from the consuming BatchNorm's (dy, x3, ReLU bit mask) and its
+// backward coefficients (see `LAZY` below) instead of being read
+template <int C_, int K_, int TM_, int NW_, bool LZ_ = false>
 struct Cfg {
   static constexpr int C = C_, K = K_, TM = TM_, NW = NW_;
+  static constexpr bool LZ = LZ_;
   static constexpr int T = NW * 64;
   static constexpr int NCB = C / 16;                         // channel blocks
   static constexpr int CPW = NCB >= NW ? NCB / NW : 1;       // dgrad channel blocks per wave
@@ -53,13 +56,19 @@ struct Cfg {
   static constexpr int KBW = K / NW / 16;                    // wgrad dW row blocks per wave
   static constexpr int DO = TM * K;                          // bf16 per dO tile
   static constexpr int YT = TM * C;                          // bf16 per Y / x tile
-  static constexpr int SLOT = DO + 2 * YT;
-  static constexpr int DOI = DO * 2 / 1024;                  // 1-KB DMA instructions per dO tile
+  static constexpr int OT = LZ ? 2 * DO : DO;               // dO tile, or dy3 + x3 tiles (LZ)
+  static constexpr int MB = LZ ? TM * K / 8 : 0;             // LZ: ReLU mask bytes per tile
+  static constexpr int MI = MB / 1024;                       // ... = 1-KB DMAs, by wave 0
+  static constexpr int SLOT = OT + 2 * YT + MB / 2;
+  static constexpr int DOI = OT * 2 / 1024;                  // 1-KB DMA instructions per dO tile(s)
   static constexpr int YI = YT * 2 / 1024;                   // ... per Y / x tile
   static constexpr int D = (DOI + 2 * YI) / NW;              // DMA instructions per wave per tile
   static constexpr int S = CPW * MBW;                        // dY stores per lane per tile
+  static constexpr int MCH = LZ ? TM * K / 8 / T : 0;       // LZ: 8-channel chunks per thread
   static constexpr size_t LDS = (size_t)kNB * SLOT * 2 + (size_t)WPC * 2 * C * 4 + 4 * C * 4;
-  static_assert(DOI % NW == 0 && (2 * YI) % NW == 0 && YI % NW == 0, "DMA split");
+  static_assert(!LZ || ((TM * K / 8) % T == 0 && T % (K / 8) == 0 && MB % 1024 == 0 && MI <= NW),
+                "LZ transform split");
+  static_assert(DOI % NW == 0 && (2 * YI) % NW == 0, "DMA split");
   static_assert(WPC * (NCB / CPW) == NW && MBW >= 1 && TM % 32 == 0, "wave split");
   static_assert(LDS <= 160 * 1024, "conv1x1_bwd LDS");
 };
@@ -115,12 +124,20 @@ struct C1Args {
   float* wpart;         // [grid][K][C]
   float* bpart;         // [grid][2][C]
   int M;
+  // LZ: dO = bn_bwd_dx(cA, dy3 * mask bit, cB, x3, cC) per element (the consuming residual
+  // BatchNorm's backward apply, never stored); `dout` then holds that BN's incoming gradient dy3
+  const bf16_t* x3;     // [M][K]  the BN's input (this conv's output)
+  const uint8_t* mask;  // [M][K / 8] ReLU bit mask of the BN's forward
+  const float* cA;
+  const float* cB;
+  const float* cC;
 };
 
 template <class F>
 __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
   constexpr int C = F::C, K = F::K, TM = F::TM, NW = F::NW;
   constexpr int CPW = F::CPW, MBW = F::MBW, KS = F::KS, KBW = F::KBW, NCB = F::NCB;
+  constexpr bool LZ = F::LZ;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   float* sred = reinterpret_cast<float*>(lds + kNB * F::SLOT);   // [WPC][2][C]
   float* sprm = sred + F::WPC * 2 * C;                            // [4][C] mean / inv / sc / sh
@@ -150,29 +167,57 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
   const uint32_t lds0 = lds_addr(lds);
   // tile i of this block -> slot i % 3.  dO: instruction q covers 1024 / (2K) rows; Y / x:
   // 1024 / (2C) rows per instruction
+  // LZ issues every tile index (past the block's last tile: out-of-range offsets, the range check
+  // drops the reads and the DMA fills a free slot with zeros) so its vmcnt counts are constant
   auto issue = [&](int i) {
-    const long m0 = ((long)blockIdx.x + (long)i * gridDim.x) * TM;
+    const bool live = !LZ || i < nmy;
+    const long m0 = ((long)blockIdx.x + (long)(live ? i : 0) * gridDim.x) * TM;
     const i32x4_t ro = rsrc_quad(g.dout + m0 * K, (uint32_t)(F::DO * 2));
+    const i32x4_t r3 = rsrc_quad(LZ ? g.x3 + m0 * K : g.dout, (uint32_t)(F::DO * 2));
     const i32x4_t ry = rsrc_quad(g.y + m0 * C, (uint32_t)(F::YT * 2));
     const i32x4_t rx = rsrc_quad(g.x + m0 * C, (uint32_t)(F::YT * 2));
     const uint32_t base = lds0 + (uint32_t)((i % kNB) * F::SLOT * 2);
     constexpr int OL = K / 8, YL = C / 8;        // 16-B chunks per row
+    constexpr int OI1 = F::DO * 2 / 1024;        // instructions per K-wide tile
 #pragma unroll
     for (int j = 0; j < F::DOI / NW; ++j) {
-      const int q = wave + NW * j, e = q * 64 + lane;     // chunk index in the tile
+      const int q = wave + NW * j;
+      const int qq = q % OI1, e = qq * 64 + lane;          // chunk index in the tile
       const int r = e / OL, s = e % OL;
-      dma16(ro, base + (uint32_t)q * 1024u, (uint32_t)((r * K + ((s ^ swz_o(r)) << 3)) * 2));
+      const uint32_t off = live ? (uint32_t)((r * K + ((s ^ swz_o(r)) << 3)) * 2) : 0xFFFFFFF0u;
+      dma16(q < OI1 ? ro : r3, base + (uint32_t)q * 1024u, off);
     }
 #pragma unroll
-    for (int j = 0; j < F::YI / NW; ++j) {
-      const int q = wave + NW * j, e = q * 64 + lane;
+    for (int j = 0; j < 2 * F::YI / NW; ++j) {      // Y instructions 0 .. YI-1, then x
+      const int q = wave + NW * j;
+      const bool isx = q >= F::YI;
+      const int qq = isx ? q - F::YI : q, e = qq * 64 + lane;
       const int r = e / YL, s = e % YL;
-      dma16(ry, base + (uint32_t)(F::DO * 2 + q * 1024),
-            (uint32_t)((r * C + ((s ^ swz_y<C>(r)) << 3)) * 2));
-      dma16(rx, base + (uint32_t)((F::DO + F::YT) * 2 + q * 1024),
-            (uint32_t)((r * C + ((s ^ swz_x<C>(r)) << 3)) * 2));
+      const int sw = isx ? swz_x<C>(r) : swz_y<C>(r);
+      const uint32_t off = live ? (uint32_t)((r * C + ((s ^ sw) << 3)) * 2) : 0xFFFFFFF0u;
+      dma16(isx ? rx : ry, base + (uint32_t)(F::OT * 2 + q * 1024), off);
+    }
+    if constexpr (LZ) {             // the tile's mask bytes (row-major, unswizzled): waves < MI
+      if (wave < F::MI) {
+        const i32x4_t rm = rsrc_quad(g.mask + m0 * (K / 8), (uint32_t)F::MB);
+        dma16(rm, base + (uint32_t)((F::OT + 2 * F::YT) * 2 + wave * 1024),
+              live ? (uint32_t)(wave * 1024 + lane * 16) : 0xFFFFFFF0u);
+      }
     }
   };
+  // LZ: this thread's 8-channel chunks of every tile (rows t / (K/8) + k T / (K/8), column chunk
+  // t % (K/8)) and the chunk's coefficients
+  constexpr int MCH = F::MCH > 0 ? F::MCH : 1;
+  float ca[8], cb[8], cc[8];
+  const int lch = tid % (K / 8), lrow = tid / (K / 8);
+  if constexpr (LZ) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ca[e] = g.cA[lch * 8 + e];
+      cb[e] = g.cB[lch * 8 + e];
+      cc[e] = g.cC[lch * 8 + e];
+    }
+  }
 
   f32x4_t aw[KBW][NCB];
 #pragma unroll
@@ -185,21 +230,66 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
 
-  issue(0);
-  if (nmy > 1) issue(1);
   constexpr int D = F::D, S = F::S;
+  if constexpr (LZ) {
+    issue(0);
+    issue(1);
+  } else {
+    issue(0);
+    if (nmy > 1) issue(1);
+  }
   for (int i = 0; i < nmy; ++i) {
-    // top: this wave's DMAs of tile i landed.  Younger vector-memory ops at this point: tile
-    // i + 1's DMAs (D, if it exists) and the dY stores of tiles i - 1 and i - 2 (S each).
-    const bool more = i + 1 < nmy;
-    if (i == 0) { if (more) wait_vm<D>(); else wait_vm<0>(); }
-    else if (i == 1) { if (more) wait_vm<D + S>(); else wait_vm<S>(); }
-    else { if (more) wait_vm<D + 2 * S>(); else wait_vm<2 * S>(); }
+    if constexpr (LZ) {
+      // top: tile i's DMAs landed.  Every tile index is issued (constant counts); younger: tile
+      // i + 1's DMAs (D, + the mask DMA on waves < MI) and the dY stores of tiles i - 1, i - 2
+      if (wave < F::MI) {
+        if (i == 0) wait_vm<D + 1>();
+        else if (i == 1) wait_vm<D + 1 + S>();
+        else wait_vm<D + 1 + 2 * S>();
+      } else {
+        if (i == 0) wait_vm<D>();
+        else if (i == 1) wait_vm<D + S>();
+        else wait_vm<D + 2 * S>();
+      }
+    } else {
+      // top: this wave's DMAs of tile i landed.  Younger vector-memory ops at this point: tile
+      // i + 1's DMAs (D, if it exists) and the dY stores of tiles i - 1 and i - 2 (S each).
+      const bool more = i + 1 < nmy;
+      if (i == 0) { if (more) wait_vm<D>(); else wait_vm<0>(); }
+      else if (i == 1) { if (more) wait_vm<D + S>(); else wait_vm<S>(); }
+      else { if (more) wait_vm<D + 2 * S>(); else wait_vm<2 * S>(); }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();                  // every wave's DMAs landed; slot (i + 2) % 3 was read in i - 1
-    if (i + 2 < nmy) issue(i + 2);
-    const bf16_t* sO = lds + (i % kNB) * F::SLOT;
-    const bf16_t* sY = sO + F::DO;
+    if constexpr (LZ) {
+      issue(i + 2);
+    } else {
+      if (i + 2 < nmy) issue(i + 2);
+    }
+    bf16_t* const slot = lds + (i % kNB) * F::SLOT;
+    if constexpr (LZ) {
+      // dO = the residual BatchNorm's backward apply, in place over the dy3 tile (bit-identical to
+      // bn_bwd_apply_kernel<1>'s stored dx: same dz, same bn_bwd_dx, same bf16 rounding)
+#pragma unroll
+      for (int k = 0; k < MCH; ++k) {
+        const int r = lrow + k * (F::T / (K / 8));
+        const int o = sidx<K>(r, lch * 8, swz_o(r));
+        float gv[8], xv[8], ov[8];
+        unpack8(*reinterpret_cast<const uint4*>(slot + o), gv);
+        unpack8(*reinterpret_cast<const uint4*>(slot + F::DO + o), xv);
+        const uint32_t mb = reinterpret_cast<const uint8_t*>(slot + F::OT + 2 * F::YT)[r * (K / 8) + lch];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dz = (mb >> e) & 1u ? gv[e] : 0.f;
+          ov[e] = bn_bwd_dx(ca[e], dz, cb[e], xv[e], cc[e]);
+        }
+        *reinterpret_cast<uint4*>(slot + o) = pack8(ov);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+    }
+    const bf16_t* sO = slot;
+    const bf16_t* sY = sO + F::OT;
     const bf16_t* sX = sY + F::YT;
     // the swizzled per-lane LDS addresses are recomputed every tile (a few VALU ops each) rather
     // than hoisted out of the loop: at C = 128 the hoisted set does not fit next to the register-
@@ -316,12 +406,13 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
 
 typedef Cfg<64, 256, 64, 8> CfgS0;    // stage 0: 56 x 56 x 64 -> 256
 typedef Cfg<128, 512, 32, 8> CfgS1;   // stage 1: 28 x 28 x 128 -> 512
+typedef Cfg<64, 256, 32, 8, true> CfgS0L;   // stage 0, dO formed from the residual BN (LZ)
 
 int g_c1_grid = 0;   // 0 = one block per CU
 
 int c1_tm(int C) { return C == 64 ? CfgS0::TM : CfgS1::TM; }
 
-int c1_blocks(int M, int C) {
+int c1_blocks_tm(int M, int TM) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -329,9 +420,10 @@ int c1_blocks(int M, int C) {
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
   const int want = g_c1_grid > 0 ? g_c1_grid : cus;
-  const int ntiles = M / c1_tm(C);
+  const int ntiles = M / TM;
   return ntiles < want ? ntiles : want;
 }
+int c1_blocks(int M, int C) { return c1_blocks_tm(M, c1_tm(C)); }
 
 template <class F>
 void launch_c1(const C1Args& g, hipStream_t st) {
@@ -341,7 +433,8 @@ void launch_c1(const C1Args& g, hipStream_t st) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)F::LDS));
     attr = true;
   }
-  hipLaunchKernelGGL(conv1x1_bwd_kernel<F>, dim3(c1_blocks(g.M, F::C)), dim3(F::T), F::LDS, st, g);
+  hipLaunchKernelGGL(conv1x1_bwd_kernel<F>, dim3(c1_blocks_tm(g.M, F::TM)), dim3(F::T), F::LDS, st,
+                     g);
 }
 
 }  // namespace
@@ -370,4 +463,30 @@ void dtf_conv1x1_bwd(const bf16_t* dout, const bf16_t* wt, const bf16_t* y, cons
   C1Args g{dout, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart, M};
   if (C == 64) launch_c1<CfgS0>(g, st);
   else launch_c1<CfgS1>(g, st);
+}
+
+// LZ form (stage 0 only): the conv-output gradient dO is never stored -- formed per tile from the
+// residual BatchNorm's incoming gradient dy3, its input x3, its forward ReLU bit mask and its
+// backward coefficients (A, B, C) -- which removes that BN's apply pass write of dO and this
+// kernel's read of it (4 B per element of the 256-channel tensor).
+bool dtf_conv1x1_bwd_lazy_ok(int M, int C, int K) {
+  return C == CfgS0L::C && K == CfgS0L::K && M > 0 && M % CfgS0L::TM == 0;
+}
+int dtf_conv1x1_bwd_lazy_blocks(int M) {
+  if (!dtf_conv1x1_bwd_lazy_ok(M, 64, 256)) throw std::runtime_error("conv1x1_bwd_lazy: shape");
+  return c1_blocks_tm(M, CfgS0L::TM);
+}
+void dtf_conv1x1_bwd_lazy(const bf16_t* dy3, const bf16_t* x3, const uint8_t* mask,
+                          const float* cA, const float* cB, const float* cC, const bf16_t* wt,
+                          const bf16_t* y, const bf16_t* x, const float* mean, const float* inv,
+                          const float* sc, const float* sh, bf16_t* dy, float* wpart,
+                          float* bpart, int M, int C, int K, hipStream_t st) {
+  if (!dtf_conv1x1_bwd_lazy_ok(M, C, K))
+    throw std::runtime_error("conv1x1_bwd_lazy: (C, K) = (64, 256), M % 32 == 0");
+  const void* ptrs[] = {dy3, x3, mask, cA, cB, cC, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart};
+  for (const void* p : ptrs)
+    if (!p || (reinterpret_cast<uintptr_t>(p) & 15))
+      throw std::runtime_error("conv1x1_bwd_lazy: null or misaligned operand");
+  C1Args g{dy3, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart, M, x3, mask, cA, cB, cC};
+  launch_c1<CfgS0L>(g, st);
 }

@@ -418,7 +418,7 @@ pool3s2_bn_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__
         if (APPLY) {
           float o[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = k0[e] * gk[e] + k1[e] * xv[e] + k2[e];
+          for (int e = 0; e < 8; ++e) o[e] = bn_bwd_dx(k0[e], gk[e], k1[e], xv[e], k2[e]);
           reinterpret_cast<uint4*>(dx)[v] = pack8(o);
         } else {
 #pragma unroll

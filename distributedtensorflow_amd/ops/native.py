@@ -669,6 +669,25 @@ class _MaskedGrad:
         return out
 
 
+class _LazyBnDx:
+    """d(x) of a residual BatchNorm + ReLU, not yet formed: dx = A (dy * mask) + B x + C per
+    channel.  A fused conv backward that consumes it forms it per tile (bit-identical to the
+    apply pass); anything else materialises it with that pass."""
+    __slots__ = ("dy", "x", "mask", "gb")
+
+    def __init__(self, dy, x, mask, gb):
+        self.dy, self.x, self.mask, self.gb = dy, x, mask, gb
+
+    def materialize(self):
+        C = self.x.shape[-1]
+        M = self.x.numel() // C
+        dx = torch.empty_like(self.x)
+        _K.bn_bwd_apply(self.dy.data_ptr(), 0, self.x.data_ptr(), self.gb[2].data_ptr(),
+                        self.gb[3].data_ptr(), self.gb[4].data_ptr(), dx.data_ptr(), 0, M, C, 1,
+                        _st(), 0, 0, self.mask.data_ptr())
+        return dx
+
+
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu,
@@ -710,6 +729,9 @@ class _BatchNorm(torch.autograd.Function):
             ctx.set_materialize_grads(False)
         ctx.res_slot = (getattr(residual, "_dtf_grad_slot", None)
                         if residual is not None and not residual_to_conv else None)
+        # a fused c3 backward that forms d(x) itself from (dy, x, mask, coefficients)
+        ctx.in_slot = (getattr(x, "_dtf_lazy_slot", None)
+                       if training and relu and residual is not None else None)
         return y
 
     @staticmethod
@@ -824,16 +846,25 @@ def _bn_backward_core(ctx, dy, x, mask, g32, stats, relu=None):
                          invstd.data_ptr(), M, C, int(relu), part.data_ptr(), st,
                          sc_ptr, sh_ptr, _p(mask))
     gb, direct = _bn_bwd_finalize(ctx, part, G, M, C, g32, stats)
-    dx = torch.empty_like(x)
+    dx = torch.empty_like(x) if getattr(ctx, "in_slot", None) is None else None
     lazy = (ctx.has_res and ctx.res_ref is not None and _LAZY_RESIDUAL_GRAD
             and mask is not None)
     res_slot = getattr(ctx, "res_slot", None)
     lazy_slot = (ctx.has_res and not lazy and res_slot is not None and _LAZY_RESIDUAL_GRAD
                  and mask is not None)
     dres = torch.empty_like(x) if ctx.has_res and not (lazy or lazy_slot) else None
-    _K.bn_bwd_apply(dy.data_ptr(), 0, x.data_ptr(), gb[2].data_ptr(),
-                    gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
-                    int(relu), st, sc_ptr, sh_ptr, _p(mask))
+    in_slot = getattr(ctx, "in_slot", None)
+    ctx.in_slot = None
+    if in_slot is not None and dres is None and mask is not None and relu:
+        # the producing conv's fused backward forms dx per tile from these and never stores it
+        in_slot.grad = _LazyBnDx(dy, x, mask, gb)
+        dx = None
+    else:
+        if dx is None:
+            dx = torch.empty_like(x)
+        _K.bn_bwd_apply(dy.data_ptr(), 0, x.data_ptr(), gb[2].data_ptr(),
+                        gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
+                        int(relu), st, sc_ptr, sh_ptr, _p(mask))
     if lazy:
         # d(residual) = dy * relu_mask is never written: the consuming dgrad forms it in its
         # epilogue from dy and the bit mask (conv geom acc mode 2)
@@ -891,6 +922,12 @@ class _BnReluConv1x1(torch.autograd.Function):
         out._dtf_bn_part = (part, G, M, K)
         if wb.is_contiguous():
             _register_dgrad_filter(wb)
+        ctx.lz_slot = None
+        if _FUSE_C1_BWD and _FUSE_C3_LAZY and _K.conv1x1_bwd_lazy_ok(M, C, K):
+            # the residual BN consuming `out` may hand its d(out) over unformed (_LazyBnDx)
+            ctx.lz_slot = _GradSlot()
+            out._dtf_lazy_slot = ctx.lz_slot
+            ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, y, wb, g32, stats)
         ctx.w_param, ctx.w_dtype = w_master, w_master.dtype
         # the BatchNorm-backward core's context
@@ -902,11 +939,26 @@ class _BnReluConv1x1(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, y, wb, g32, stats = ctx.saved_tensors
-        dout = dout.contiguous()
+        lz, ctx.lz_slot = ctx.lz_slot, None
+        rec = lz.grad if lz is not None else None
+        if lz is not None:
+            lz.grad = None
+        if dout is None and rec is None:
+            ctx.w_param = ctx.params = None
+            return (None,) * 8
+        if dout is not None and rec is not None:
+            dout = dout + rec.materialize()      # another consumer of the conv output
+            rec = None
         K, _, _, C = wb.shape
         M = y.numel() // C
         dw = None
         target = _direct_grad(ctx.w_param)
+        if rec is not None:
+            dy, dw = _conv1x1_bwd_fused(ctx, None, x, y, wb, stats, target, M, C, K, lazy=rec)
+            dx, dg, db, _ = _bn_backward_core(ctx, dy, x, None, g32, stats)
+            ctx.w_param = ctx.params = None
+            return dx, dg, db, None, None, dw, None, None
+        dout = dout.contiguous()
         if _FUSE_C1_BWD and _K.conv1x1_bwd_ok(M, C, K):
             dy, dw = _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K)
             dx, dg, db, _ = _bn_backward_core(ctx, dy, x, None, g32, stats)
@@ -923,22 +975,29 @@ class _BnReluConv1x1(torch.autograd.Function):
         return dx, dg, db, None, None, dw, None, None
 
 
-def _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K):
+def _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K, lazy=None):
     """Stage-0 / stage-1 c3 (64 -> 256, 128 -> 512) backward in ONE pass (csrc/kernels/conv1x1_bwd.hip): the
     data gradient dy, the weight gradient (per-block fp32 slabs, reduced here in fixed order
     into the flat gradient buffer or a fresh tensor) and the consuming BatchNorm's backward
     sums (attached to dy as ``_dtf_bnb_part`` for :func:`_bn_backward_core`).  Replaces the
     wgrad pass, the dgrad GEMM and the BN reduce pass (1536 -> 896 B of HBM traffic per row)."""
-    dev = dout.device
+    dev = y.device
     st = _st()
-    G = _K.conv1x1_bwd_blocks(M, C)
+    G = _K.conv1x1_bwd_lazy_blocks(M) if lazy is not None else _K.conv1x1_bwd_blocks(M, C)
     wpart = torch.empty(G * K * C, device=dev, dtype=torch.float32)
     part = torch.empty(_K.bn_workspace_floats_g(G, C), device=dev, dtype=torch.float32)
     dy = torch.empty_like(y)
     wt = _dgrad_filter(wb.reshape(K, 1, C)).view(C, K)
-    _K.conv1x1_bwd(dout.data_ptr(), wt.data_ptr(), y.data_ptr(), x.data_ptr(),
-                   stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(),
-                   stats[3].data_ptr(), dy.data_ptr(), wpart.data_ptr(), part.data_ptr(), M, C, K, st)
+    common = (wt.data_ptr(), y.data_ptr(), x.data_ptr(), stats[0].data_ptr(),
+              stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), dy.data_ptr(),
+              wpart.data_ptr(), part.data_ptr(), M, C, K, st)
+    if lazy is not None:
+        # d(conv output) formed per tile from the residual BN's (dy, x, mask, coefficients)
+        _K.conv1x1_bwd_lazy(lazy.dy.data_ptr(), lazy.x.data_ptr(), lazy.mask.data_ptr(),
+                            lazy.gb[2].data_ptr(), lazy.gb[3].data_ptr(), lazy.gb[4].data_ptr(),
+                            *common)
+    else:
+        _K.conv1x1_bwd(dout.data_ptr(), *common)
     dw = None
     if target is not None:
         _K.slab_reduce(wpart.data_ptr(), target.data_ptr(), K * C, G, 1, st)
@@ -955,6 +1014,8 @@ def _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K):
 # stage-0 / stage-1 c3 backward as one fused pass (A/B knob; summation order of dW and the BN sums
 # differs from the separate passes)
 _FUSE_C1_BWD = os.environ.get("DTF_FUSE_C1_BWD", "1") == "1"
+# ... at stage 0 also without the residual BN's apply pass writing d(conv output) (_LazyBnDx)
+_FUSE_C3_LAZY = os.environ.get("DTF_FUSE_C3_LAZY", "1") == "1"
 
 
 def bn_relu_conv1x1_ok(x, w):

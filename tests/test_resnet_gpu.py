@@ -380,6 +380,49 @@ def test_resnet50_grads_with_fused_bn_backward_sums():
     assert tail < 1e-2, tail
 
 
+def test_lazy_residual_bn_dx_formed_in_fused_c3_backward():
+    """Stage-0 identity block: the residual BN's backward hands d(c3 output) over unformed
+    (_LazyBnDx) and the fused c3 backward forms it per tile (conv1x1_bwd.hip LZ) instead of the
+    apply pass storing it: same block output, the block-input gradient and every parameter
+    gradient match the stored-dO path (c3's data gradient bit for bit, so d(block input) too up
+    to the dW / BN-sum summation order of the 32- vs 64-row tiles)."""
+    torch.manual_seed(0)
+    m = resnet50().cuda()
+    blk = m.blocks[1]                         # s0b1: 56 x 56 x 256 identity bottleneck
+    x = torch.randn(2, 16, 16, 256, device="cuda").bfloat16()
+    g = torch.randn(2, 16, 16, 256, device="cuda").bfloat16()
+    calls = {"n": 0}
+    orig = native._K.conv1x1_bwd_lazy
+
+    def spy(*a):
+        calls["n"] += 1
+        return orig(*a)
+    out = {}
+    prev = native._FUSE_C3_LAZY
+    try:
+        native._K.conv1x1_bwd_lazy = spy
+        for lz in (True, False):
+            native._FUSE_C3_LAZY = lz
+            b = copy.deepcopy(blk)
+            xi = x.clone().requires_grad_(True)
+            y = b(xi)
+            y.backward(g)
+            torch.cuda.synchronize()
+            out[lz] = (y.detach().float(), xi.grad.float(),
+                       [p.grad.float() for p in b.parameters()])
+    finally:
+        native._K.conv1x1_bwd_lazy = orig
+        native._FUSE_C3_LAZY = prev
+    assert calls["n"] == 1
+    (ya, dxa, ga), (yb, dxb, gb) = out[True], out[False]
+    assert torch.equal(ya, yb)
+    rel = ((dxa - dxb).norm() / dxb.norm()).item()
+    assert rel < 2e-2, rel
+    for i, (a, b) in enumerate(zip(ga, gb)):
+        r = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+        assert r < 2e-2, (i, r)
+
+
 def _default_step_grads(model, dual):
     """One step's loss and flat gradient with the default fusions, the dual-BN sums on or off."""
     prev = native._FUSE_DUAL_BNB
