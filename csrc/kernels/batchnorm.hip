@@ -428,6 +428,9 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
   uint4* DX4 = reinterpret_cast<uint4*>(dx);
   uint4* DR4 = reinterpret_cast<uint4*>(dres);
   const int step = gridDim.x * rpi * kUnroll;
+  // DUAL without dx: a fused conv backward forms d(x) itself (ops/native.py _LazyBnDx); only the
+  // shortcut's dxp is written and x is not read
+  const bool want_dx = !DUAL || dx != nullptr;
   for (int m = blockIdx.x * rpi * kUnroll + ro; m < M; m += step) {
     uint4 dr[kUnroll], xr[kUnroll], yr[kUnroll], pr[kUnroll];
     uint32_t mb[kUnroll];
@@ -437,7 +440,7 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
       const uint32_t v = (uint32_t)r * tpr + cg;
       if (r < M) {
         dr[u] = ldv<NT>(D4 + v);
-        xr[u] = ldv<NT>(X4 + v);
+        xr[u] = want_dx ? ldv<NT>(X4 + v) : make_uint4(0, 0, 0, 0);
         if (MK == 1) mb[u] = mask[v];
         if (MK == 3) yr[u] = Y4[v];
         if (DUAL) pr[u] = ldv<NT>(XP4 + v);
@@ -456,7 +459,7 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
       if (dres) stv<NT>(DR4 + v, pack8(g));
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = bn_bwd_dx(ka[i], g[i], kb[i], xv[i], kc[i]);
-      stv<NT>(DX4 + v, pack8(o));
+      if (want_dx) stv<NT>(DX4 + v, pack8(o));
       if (DUAL) {
         float pv[8];
         unpack8(pr[u], pv);

@@ -1065,6 +1065,8 @@ class _BatchNormAddBatchNorm(torch.autograd.Function):
         ctx.params = (gamma, beta)
         ctx.params_p = (gamma_p, beta_p)
         ctx.dtypes = (gamma.dtype, beta.dtype, gamma_p.dtype, beta_p.dtype)
+        # the projection block's c3 (a fused BN + ReLU + 1x1 conv) may form d(x) itself
+        ctx.in_slot = getattr(x, "_dtf_lazy_slot", None) if training else None
         ctx.bnb_token = None
         if training and _FUSE_DUAL_BNB:
             # a streamed 1x1 data gradient of y (the next block's c1) emits both BNs' sums
@@ -1097,11 +1099,15 @@ class _BatchNormAddBatchNorm(torch.autograd.Function):
                                   part.data_ptr(), part_p.data_ptr(), st)
         gb, direct = _bn_bwd_finalize_p(ctx.params, part, G, M, C, g32, stats)
         gbp, direct_p = _bn_bwd_finalize_p(ctx.params_p, part_p, G, M, C, g32_p, stats_p)
-        dx, dxp = torch.empty_like(x), torch.empty_like(xp)
+        in_slot, ctx.in_slot = ctx.in_slot, None
+        dx = None if in_slot is not None else torch.empty_like(x)
+        dxp = torch.empty_like(xp)
         _K.bn_bwd_apply_dual(dy.data_ptr(), mask.data_ptr(), x.data_ptr(), gb[2].data_ptr(),
-                             gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), xp.data_ptr(),
+                             gb[3].data_ptr(), gb[4].data_ptr(), _p(dx), xp.data_ptr(),
                              gbp[2].data_ptr(), gbp[3].data_ptr(), gbp[4].data_ptr(),
                              dxp.data_ptr(), M, C, st)
+        if in_slot is not None:
+            in_slot.grad = _LazyBnDx(dy, x, mask, gb)
         gd, bd, gpd, bpd = ctx.dtypes
         ctx.params = ctx.params_p = None
         dg, db = (None, None) if direct else (gb[0].to(gd), gb[1].to(bd))

@@ -380,16 +380,17 @@ def test_resnet50_grads_with_fused_bn_backward_sums():
     assert tail < 1e-2, tail
 
 
-def test_lazy_residual_bn_dx_formed_in_fused_c3_backward():
-    """Stage-0 identity block: the residual BN's backward hands d(c3 output) over unformed
-    (_LazyBnDx) and the fused c3 backward forms it per tile (conv1x1_bwd.hip LZ) instead of the
-    apply pass storing it: same block output, the block-input gradient and every parameter
-    gradient match the stored-dO path (c3's data gradient bit for bit, so d(block input) too up
-    to the dW / BN-sum summation order of the 32- vs 64-row tiles)."""
+@pytest.mark.parametrize("block", [0, 1])
+def test_lazy_residual_bn_dx_formed_in_fused_c3_backward(block):
+    """Stage-0 blocks: the residual BN's backward (the identity block's, or the projection
+    block's dual BN) hands d(c3 output) over unformed (_LazyBnDx) and the fused c3 backward forms
+    it per tile (conv1x1_bwd.hip LZ) instead of the apply pass storing it: same block output, the
+    block-input gradient and every parameter gradient match the stored-dO path (c3's data
+    gradient bit for bit; dW / BN sums to the summation order of the 32- vs 64-row tiles)."""
     torch.manual_seed(0)
     m = resnet50().cuda()
-    blk = m.blocks[1]                         # s0b1: 56 x 56 x 256 identity bottleneck
-    x = torch.randn(2, 16, 16, 256, device="cuda").bfloat16()
+    blk = m.blocks[block]                     # s0b0 projection / s0b1 identity bottleneck
+    x = torch.randn(2, 16, 16, 64 if block == 0 else 256, device="cuda").bfloat16()
     g = torch.randn(2, 16, 16, 256, device="cuda").bfloat16()
     calls = {"n": 0}
     orig = native._K.conv1x1_bwd_lazy
