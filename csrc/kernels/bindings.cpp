@@ -168,7 +168,7 @@ bool dtf_conv1x1_bwd_ok(int, int, int);
 int dtf_conv1x1_bwd_blocks(int, int);
 void dtf_conv1x1_bwd_set_grid(int);
 bool dtf_conv1x1_bwd_lazy_ok(int, int, int);
-int dtf_conv1x1_bwd_lazy_blocks(int);
+int dtf_conv1x1_bwd_lazy_blocks(int, int);
 void dtf_conv1x1_bwd_lazy(const bf16_t*, const bf16_t*, const uint8_t*, const float*, const float*,
                           const float*, const bf16_t*, const bf16_t*, const bf16_t*, const float*,
                           const float*, const float*, const float*, bf16_t*, float*, float*, int,

@@ -65,11 +65,12 @@ struct Cfg {
   static constexpr int D = (DOI + 2 * YI) / NW;              // DMA instructions per wave per tile
   static constexpr int S = CPW * MBW;                        // dY stores per lane per tile
   static constexpr int MCH = LZ ? TM * K / 8 / T : 0;       // LZ: 8-channel chunks per thread
-  static constexpr size_t LDS = (size_t)kNB * SLOT * 2 + (size_t)WPC * 2 * C * 4 + 4 * C * 4;
+  static constexpr size_t LDS = (size_t)kNB * SLOT * 2 + (size_t)WPC * 2 * C * 4 + 4 * C * 4 +
+                                (LZ ? (size_t)3 * K * 4 : 0);   // LZ: the A / B / C coefficients
   static_assert(!LZ || ((TM * K / 8) % T == 0 && T % (K / 8) == 0 && MB % 1024 == 0 && MI <= NW),
                 "LZ transform split");
   static_assert(DOI % NW == 0 && (2 * YI) % NW == 0, "DMA split");
-  static_assert(WPC * (NCB / CPW) == NW && MBW >= 1 && TM % 32 == 0, "wave split");
+  static_assert(WPC * (NCB / CPW) == NW && MBW >= 1 && (TM % 32 == 0 || TM == 16), "wave split");
   static_assert(LDS <= 160 * 1024, "conv1x1_bwd LDS");
 };
 
@@ -99,6 +100,15 @@ DTF_DEV bf16x8_t tr8(const bf16_t* base, int row0, int col0, int lane) {
   const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(base + sidx<RP>(r, c, s0)));
   const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(base + sidx<RP>(r + 16, c, s1)));
   return (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// 4 reduction rows (4g .. 4g + 3 for lane group g) x one column: the 16x16x16 operand
+template <int RP, int C, bool DOUT>
+DTF_DEV s4_t tr4(const bf16_t* base, int col0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int r = 4 * g + (i >> 2), c = col0 + 4 * (i & 3);
+  const int s0 = DOUT ? swz_o(r) : swz_y<C>(r);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(base + sidx<RP>(r, c, s0)));
 }
 
 DTF_DEV f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
@@ -141,6 +151,7 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   float* sred = reinterpret_cast<float*>(lds + kNB * F::SLOT);   // [WPC][2][C]
   float* sprm = sred + F::WPC * 2 * C;                            // [4][C] mean / inv / sc / sh
+  float* scoef = sprm + 4 * C;                                    // LZ: [3][K] A / B / C
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, gq = lane >> 4;
@@ -208,14 +219,11 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
   // LZ: this thread's 8-channel chunks of every tile (rows t / (K/8) + k T / (K/8), column chunk
   // t % (K/8)) and the chunk's coefficients
   constexpr int MCH = F::MCH > 0 ? F::MCH : 1;
-  float ca[8], cb[8], cc[8];
-  const int lch = tid % (K / 8), lrow = tid / (K / 8);
   if constexpr (LZ) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      ca[e] = g.cA[lch * 8 + e];
-      cb[e] = g.cB[lch * 8 + e];
-      cc[e] = g.cC[lch * 8 + e];
+    for (int t = tid; t < K; t += F::T) {
+      scoef[t] = g.cA[t];
+      scoef[K + t] = g.cB[t];
+      scoef[2 * K + t] = g.cC[t];
     }
   }
 
@@ -270,6 +278,9 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
     if constexpr (LZ) {
       // dO = the residual BatchNorm's backward apply, in place over the dy3 tile (bit-identical to
       // bn_bwd_apply_kernel<1>'s stored dx: same dz, same bn_bwd_dx, same bf16 rounding)
+      int tt = tid;                 // recomputed per tile (see `ln` below)
+      asm volatile("" : "+v"(tt));
+      const int lch = tt % (K / 8), lrow = tt / (K / 8);
 #pragma unroll
       for (int k = 0; k < MCH; ++k) {
         const int r = lrow + k * (F::T / (K / 8));
@@ -278,6 +289,13 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
         unpack8(*reinterpret_cast<const uint4*>(slot + o), gv);
         unpack8(*reinterpret_cast<const uint4*>(slot + F::DO + o), xv);
         const uint32_t mb = reinterpret_cast<const uint8_t*>(slot + F::OT + 2 * F::YT)[r * (K / 8) + lch];
+        float ca[8], cb[8], cc[8];
+        *reinterpret_cast<float4*>(ca) = *reinterpret_cast<const float4*>(scoef + lch * 8);
+        *reinterpret_cast<float4*>(ca + 4) = *reinterpret_cast<const float4*>(scoef + lch * 8 + 4);
+        *reinterpret_cast<float4*>(cb) = *reinterpret_cast<const float4*>(scoef + K + lch * 8);
+        *reinterpret_cast<float4*>(cb + 4) = *reinterpret_cast<const float4*>(scoef + K + lch * 8 + 4);
+        *reinterpret_cast<float4*>(cc) = *reinterpret_cast<const float4*>(scoef + 2 * K + lch * 8);
+        *reinterpret_cast<float4*>(cc + 4) = *reinterpret_cast<const float4*>(scoef + 2 * K + lch * 8 + 4);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float dz = (mb >> e) & 1u ? gv[e] : 0.f;
@@ -315,6 +333,18 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
       }
     }
     // weight gradient: dW rows wave * K / NW + 16 kb + .., channels 16 cb + .., over the tile
+    if constexpr (TM == 16) {       // 16-deep reduction: v_mfma_f32_16x16x16_bf16, one tr read each
+      s4_t fa[KBW];
+#pragma unroll
+      for (int kb = 0; kb < KBW; ++kb) fa[kb] = tr4<K, C, true>(sO, wave * (K / NW) + kb * 16, ln);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const s4_t fb = tr4<C, C, false>(sY, cb * 16, ln);
+#pragma unroll
+        for (int kb = 0; kb < KBW; ++kb)
+          aw[kb][cb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(fa[kb], fb, aw[kb][cb], 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int ms = 0; ms < TM / 32; ++ms) {
       bf16x8_t fa[KBW];
@@ -407,6 +437,7 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
 typedef Cfg<64, 256, 64, 8> CfgS0;    // stage 0: 56 x 56 x 64 -> 256
 typedef Cfg<128, 512, 32, 8> CfgS1;   // stage 1: 28 x 28 x 128 -> 512
 typedef Cfg<64, 256, 32, 8, true> CfgS0L;   // stage 0, dO formed from the residual BN (LZ)
+typedef Cfg<128, 512, 16, 8, true> CfgS1L;  // stage 1, LZ (16-row tiles: 42 KB ring slots)
 
 int g_c1_grid = 0;   // 0 = one block per CU
 
@@ -465,16 +496,19 @@ void dtf_conv1x1_bwd(const bf16_t* dout, const bf16_t* wt, const bf16_t* y, cons
   else launch_c1<CfgS1>(g, st);
 }
 
-// LZ form (stage 0 only): the conv-output gradient dO is never stored -- formed per tile from the
+// LZ form (stages 0 and 1): the conv-output gradient dO is never stored -- formed per tile from the
 // residual BatchNorm's incoming gradient dy3, its input x3, its forward ReLU bit mask and its
 // backward coefficients (A, B, C) -- which removes that BN's apply pass write of dO and this
 // kernel's read of it (4 B per element of the 256-channel tensor).
 bool dtf_conv1x1_bwd_lazy_ok(int M, int C, int K) {
-  return C == CfgS0L::C && K == CfgS0L::K && M > 0 && M % CfgS0L::TM == 0;
+  if (M <= 0) return false;
+  if (C == CfgS0L::C && K == CfgS0L::K) return M % CfgS0L::TM == 0;
+  if (C == CfgS1L::C && K == CfgS1L::K) return M % CfgS1L::TM == 0;
+  return false;
 }
-int dtf_conv1x1_bwd_lazy_blocks(int M) {
-  if (!dtf_conv1x1_bwd_lazy_ok(M, 64, 256)) throw std::runtime_error("conv1x1_bwd_lazy: shape");
-  return c1_blocks_tm(M, CfgS0L::TM);
+int dtf_conv1x1_bwd_lazy_blocks(int M, int C) {
+  if (!dtf_conv1x1_bwd_lazy_ok(M, C, 4 * C)) throw std::runtime_error("conv1x1_bwd_lazy: shape");
+  return c1_blocks_tm(M, C == 64 ? CfgS0L::TM : CfgS1L::TM);
 }
 void dtf_conv1x1_bwd_lazy(const bf16_t* dy3, const bf16_t* x3, const uint8_t* mask,
                           const float* cA, const float* cB, const float* cC, const bf16_t* wt,
@@ -482,11 +516,12 @@ void dtf_conv1x1_bwd_lazy(const bf16_t* dy3, const bf16_t* x3, const uint8_t* ma
                           const float* sc, const float* sh, bf16_t* dy, float* wpart,
                           float* bpart, int M, int C, int K, hipStream_t st) {
   if (!dtf_conv1x1_bwd_lazy_ok(M, C, K))
-    throw std::runtime_error("conv1x1_bwd_lazy: (C, K) = (64, 256), M % 32 == 0");
+    throw std::runtime_error("conv1x1_bwd_lazy: (C, K) in {(64, 256), (128, 512)}, M % tile == 0");
   const void* ptrs[] = {dy3, x3, mask, cA, cB, cC, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart};
   for (const void* p : ptrs)
     if (!p || (reinterpret_cast<uintptr_t>(p) & 15))
       throw std::runtime_error("conv1x1_bwd_lazy: null or misaligned operand");
   C1Args g{dy3, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart, M, x3, mask, cA, cB, cC};
-  launch_c1<CfgS0L>(g, st);
+  if (C == 64) launch_c1<CfgS0L>(g, st);
+  else launch_c1<CfgS1L>(g, st);
 }

@@ -983,7 +983,7 @@ def _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K, lazy=None):
     wgrad pass, the dgrad GEMM and the BN reduce pass (1536 -> 896 B of HBM traffic per row)."""
     dev = y.device
     st = _st()
-    G = _K.conv1x1_bwd_lazy_blocks(M) if lazy is not None else _K.conv1x1_bwd_blocks(M, C)
+    G = _K.conv1x1_bwd_lazy_blocks(M, C) if lazy is not None else _K.conv1x1_bwd_blocks(M, C)
     wpart = torch.empty(G * K * C, device=dev, dtype=torch.float32)
     part = torch.empty(_K.bn_workspace_floats_g(G, C), device=dev, dtype=torch.float32)
     dy = torch.empty_like(y)

@@ -380,18 +380,18 @@ def test_resnet50_grads_with_fused_bn_backward_sums():
     assert tail < 1e-2, tail
 
 
-@pytest.mark.parametrize("block", [0, 1])
-def test_lazy_residual_bn_dx_formed_in_fused_c3_backward(block):
-    """Stage-0 blocks: the residual BN's backward (the identity block's, or the projection
+@pytest.mark.parametrize("block,cin,hw", [(0, 64, 16), (1, 256, 16), (3, 256, 16), (4, 512, 8)])
+def test_lazy_residual_bn_dx_formed_in_fused_c3_backward(block, cin, hw):
+    """Stage-0/1 blocks: the residual BN's backward (the identity block's, or the projection
     block's dual BN) hands d(c3 output) over unformed (_LazyBnDx) and the fused c3 backward forms
-    it per tile (conv1x1_bwd.hip LZ) instead of the apply pass storing it: same block output, the
+    it per tile (conv1x1_bwd.hip LZ: 32-row tiles at stage 0, 16-row tiles with a 16-deep weight-
+    gradient MFMA at stage 1) instead of the apply pass storing it: same block output, the
     block-input gradient and every parameter gradient match the stored-dO path (c3's data
-    gradient bit for bit; dW / BN sums to the summation order of the 32- vs 64-row tiles)."""
+    gradient bit for bit; dW / BN sums to summation order)."""
     torch.manual_seed(0)
     m = resnet50().cuda()
-    blk = m.blocks[block]                     # s0b0 projection / s0b1 identity bottleneck
-    x = torch.randn(2, 16, 16, 64 if block == 0 else 256, device="cuda").bfloat16()
-    g = torch.randn(2, 16, 16, 256, device="cuda").bfloat16()
+    blk = m.blocks[block]                     # s0b0 / s0b1 / s1b0 / s1b1
+    x = torch.randn(2, hw, hw, cin, device="cuda").bfloat16()
     calls = {"n": 0}
     orig = native._K.conv1x1_bwd_lazy
 
@@ -400,6 +400,7 @@ def test_lazy_residual_bn_dx_formed_in_fused_c3_backward(block):
         return orig(*a)
     out = {}
     prev = native._FUSE_C3_LAZY
+    g = None
     try:
         native._K.conv1x1_bwd_lazy = spy
         for lz in (True, False):
@@ -407,6 +408,9 @@ def test_lazy_residual_bn_dx_formed_in_fused_c3_backward(block):
             b = copy.deepcopy(blk)
             xi = x.clone().requires_grad_(True)
             y = b(xi)
+            if g is None:
+                g = torch.randn(y.shape, generator=torch.Generator().manual_seed(1)).to(
+                    device="cuda", dtype=y.dtype)
             y.backward(g)
             torch.cuda.synchronize()
             out[lz] = (y.detach().float(), xi.grad.float(),
