@@ -861,16 +861,18 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mas
 //      dP = dO V^T per 16-key group, P = exp(S - lse) (+ dropout), dS = P (dP - delta),
 //      dQ = dS K; P (dropped) and dS are kept, rounded to bf16 exactly as the split kernels'
 //      fragments round them;
-//   2. after a barrier P and dS go to LDS as [query][key] tiles (P over the dead K|V region) and
-//      wave w takes keys 16w..16w+15: dV = P^T dO, dK = dS^T Q, reading P / dS columns with the
-//      same transposing ds_read_b64_tr_b16 fragments the dK/dV kernel builds in registers.
+//   2. wave w takes keys 16w..16w+15, reading [query][key] tiles in LDS with the same
+//      transposing ds_read_b64_tr_b16 fragments the dK/dV kernel builds in registers: P goes over
+//      the dead K|V region and dV = P^T dO; then dS over the same region and dK = dS^T Q.
 // Against dQ + dK/dV as two kernels this drops the second Q K^T and dO V^T (5 instead of 7
 // 128 x 128 x 64 products per (b, h)) and the second read of Q / K / V / dO; every accumulator
 // sums in the same order as before, so the gradients are bit-identical to the split kernels.
+// P and dS taking turns in one region keeps the block at 80 KB of LDS and <= 128 VGPRs: TWO
+// blocks per CU, so one block's Q/K/V/dO loads overlap the other's MFMAs (one block per CU left
+// the matrix pipe idle for the whole load phase).
 constexpr int kFusedS = 128, kPLD = 136;   // P / dS row pitch (272 B: 8-B aligned rows)
 constexpr int kFusedRed = 8 * 3 * AD;        // [wave][dq | dk | dv column] fp32 partial sums
-constexpr int kFusedLds = (4 * kFusedS * ALD + kFusedS * kPLD) * 2 + kFusedS * 4 +
-                          kFusedRed * 4;                                   // 115,200 B
+constexpr int kFusedLds = (4 * kFusedS * ALD) * 2 + kFusedS * 4 + kFusedRed * 4;   // 80,384 B
 
 // sum of v over the 16 lanes of this lane's 16-lane group (the 16 queries / keys of a wave)
 DTF_DEV float sum16(float v) {
@@ -890,19 +892,19 @@ DTF_DEV bf16x8_t lds_tr8_p(const bf16_t* base, int row0, int col0, int lane) {
 }
 
 template <bool DROP>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(512, 4)      // 4 waves per SIMD = two 8-wave blocks per CU
 attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                          const bf16_t* __restrict__ dO, const float* __restrict__ lse,
                          float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom g,
                          const bf16_t* __restrict__ O, float* __restrict__ colpart) {
   constexpr int S = kFusedS;
-  static_assert(S * kPLD <= 2 * S * ALD, "P must fit over the K|V region");
+  static_assert(S * kPLD <= 2 * S * ALD, "P / dS must fit over the K|V region");
   extern __shared__ __attribute__((aligned(16))) bf16_t fsm[];    // kFusedLds bytes (dynamic)
   bf16_t* Qs = fsm;
   bf16_t* Os = Qs + S * ALD;                 // dO
-  bf16_t* KV = Os + S * ALD;                 // K | V, then P
-  bf16_t* dSs = KV + 2 * S * ALD;
-  float* Ms = reinterpret_cast<float*>(dSs + S * kPLD);
+  bf16_t* KV = Os + S * ALD;                 // K | V, then P, then dS
+  bf16_t* dSs = KV;
+  float* Ms = reinterpret_cast<float*>(KV + 2 * S * ALD);
   float* red = Ms + S;                       // [8 waves][3 * 64] column partials (colpart)
   bf16_t* Ks = KV;
   bf16_t* Vs = KV + S * ALD;
@@ -947,10 +949,13 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
   const bf16x8_t bo0 = lds_row8(Os, q, 8 * gq), bo1 = lds_row8(Os, q, 32 + 8 * gq);
   const float c = g.scale * kLog2e;
   const uint32_t kbase = (uint32_t)((bh * S + q) * S);
-  f32x4_t P[8], dS[8];
+  // P and dS are only ever used rounded to bf16 (MFMA fragments, LDS tiles): kept packed, 4 keys
+  // per uint2 -- half the registers of fp32, same bits
+  uint2 P[8], dS[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     f32x4_t s = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dp = s;
+    float pt[4], st[4];
     s = mfma(lds_row8(Ks, 16 * t + li, 8 * gq), bq0, s);
     s = mfma(lds_row8(Ks, 16 * t + li, 32 + 8 * gq), bq1, s);
     dp = mfma(lds_row8(Vs, 16 * t + li, 8 * gq), bo0, dp);
@@ -962,20 +967,23 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
       const float p = exp2f(s[r] * c + Ms[key] - lq);
       if (DROP) {
         const bool kp = keep_elem(g.seed, kbase + key, g.thr);
-        P[t][r] = kp ? p * g.inv_keep : 0.f;
-        dS[t][r] = p * ((kp ? dp[r] * g.inv_keep : 0.f) - dl);
+        pt[r] = kp ? p * g.inv_keep : 0.f;
+        st[r] = p * ((kp ? dp[r] * g.inv_keep : 0.f) - dl);
       } else {
-        P[t][r] = p;
-        dS[t][r] = p * (dp[r] - dl);
+        pt[r] = p;
+        st[r] = p * (dp[r] - dl);
       }
     }
+    P[t] = make_uint2(pack2(pt[0], pt[1]), pack2(pt[2], pt[3]));
+    dS[t] = make_uint2(pack2(st[0], st[1]), pack2(st[2], st[3]));
   }
   f32x4_t acc[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    const bf16x8_t bS = pack_frag(dS[2 * ks], dS[2 * ks + 1]);
+    const bf16x8_t bS = __builtin_bit_cast(
+        bf16x8_t, make_uint4(dS[2 * ks].x, dS[2 * ks].y, dS[2 * ks + 1].x, dS[2 * ks + 1].y));
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(lds_tr8(Ks, 32 * ks, 16 * dt, lane), bS, acc[dt]);
   }
@@ -996,19 +1004,14 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
     }
   }
   __syncthreads();                 // every wave is done with K and V: P may overwrite them
-  // ---- P and dS to LDS as [query][key]: this lane's 4 consecutive keys of each group
+  // ---- [query][key] tiles: this lane's 4 consecutive keys of each group
+  auto put = [&](bf16_t* dst, const uint2 (&v)[8]) {
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int off = q * kPLD + 16 * t + 4 * gq;
-    const uint2 pv = {(uint32_t)f2bf(P[t][0]) | ((uint32_t)f2bf(P[t][1]) << 16),
-                      (uint32_t)f2bf(P[t][2]) | ((uint32_t)f2bf(P[t][3]) << 16)};
-    const uint2 sv = {(uint32_t)f2bf(dS[t][0]) | ((uint32_t)f2bf(dS[t][1]) << 16),
-                      (uint32_t)f2bf(dS[t][2]) | ((uint32_t)f2bf(dS[t][3]) << 16)};
-    *(uint2*)(Ps + off) = pv;
-    *(uint2*)(dSs + off) = sv;
-  }
+    for (int t = 0; t < 8; ++t) *(uint2*)(dst + q * kPLD + 16 * t + 4 * gq) = v[t];
+  };
+  put(Ps, P);
   __syncthreads();
-  // ---- phase 2: this wave's 16 keys against all 128 queries
+  // ---- phase 2: this wave's 16 keys against all 128 queries; dV from P first
   const int k = w * 16 + li;
   f32x4_t dv[4], dk[4];
 #pragma unroll
@@ -1016,21 +1019,35 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     const bf16x8_t bP = lds_tr8_p(Ps, 32 * ks, 16 * w, lane);
-    const bf16x8_t bS = lds_tr8_p(dSs, 32 * ks, 16 * w, lane);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dv[dt] = mfma(lds_tr8(Os, 32 * ks, 16 * dt, lane), bP, dv[dt]);
-      dk[dt] = mfma(lds_tr8(Qs, 32 * ks, 16 * dt, lane), bS, dk[dt]);
-    }
+    for (int dt = 0; dt < 4; ++dt) dv[dt] = mfma(lds_tr8(Os, 32 * ks, 16 * dt, lane), bP, dv[dt]);
   }
   mfma_fence();
   bf16_t* dkrow = dqkv + (tok0 + k) * g.ld + (H + h) * AD;
   bf16_t* dvrow = dqkv + (tok0 + k) * g.ld + (2 * H + h) * AD;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    store4_scaled(dkrow + 16 * dt + 4 * gq, dk[dt], g.scale);
-    store4_scaled(dvrow + 16 * dt + 4 * gq, dv[dt], 1.f);
+  for (int dt = 0; dt < 4; ++dt) store4_scaled(dvrow + 16 * dt + 4 * gq, dv[dt], 1.f);
+  if (colpart) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float tv = sum16(round_bf(dv[dt][r]));
+        if (li == 0) red[w * 3 * AD + 2 * AD + 16 * dt + 4 * gq + r] = tv;
+      }
   }
+  __syncthreads();                 // every wave is done reading P: dS takes its place
+  put(dSs, dS);
+  __syncthreads();
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8_t bS = lds_tr8_p(dSs, 32 * ks, 16 * w, lane);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dk[dt] = mfma(lds_tr8(Qs, 32 * ks, 16 * dt, lane), bS, dk[dt]);
+  }
+  mfma_fence();
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) store4_scaled(dkrow + 16 * dt + 4 * gq, dk[dt], g.scale);
   if (colpart) {
     // the qkv bias gradient's first level: per (b, h) column sums of dQ / dK / dV over the 128
     // tokens (8 waves x 16, fixed order) -> colpart[b][3 * H * 64], in dqkv's column layout;
@@ -1040,11 +1057,7 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float tk = sum16(round_bf(dk[dt][r] * g.scale));
-        const float tv = sum16(round_bf(dv[dt][r]));
-        if (li == 0) {
-          red[w * 3 * AD + AD + 16 * dt + 4 * gq + r] = tk;
-          red[w * 3 * AD + 2 * AD + 16 * dt + 4 * gq + r] = tv;
-        }
+        if (li == 0) red[w * 3 * AD + AD + 16 * dt + 4 * gq + r] = tk;
       }
     __syncthreads();
     if (tid < 3 * AD) {

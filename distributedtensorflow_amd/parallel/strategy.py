@@ -498,7 +498,17 @@ def init_process_group_from_env(backend=None, timeout_s=None):
         wd.add_probe(lambda: (f"cluster epoch moved past {watcher.epoch}: a peer was restarted"
                               if watcher.changed else None))
         return
-    dist.init_process_group(backend, rank=rank, world_size=world,
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+        # torchrun: its agent already hosts the store and ran the rendezvous
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        return
+    # the rendezvous waits for every rank's process to START (imports, device init): bound it
+    # separately from the collective deadline, which may be seconds (DTF_COMM_TIMEOUT_S)
+    rdv_s = max(float(timeout_s), float(os.environ.get("DTF_RENDEZVOUS_TIMEOUT_S", "300") or 300))
+    store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                          rank == 0, timeout=datetime.timedelta(seconds=rdv_s))
+    dist.init_process_group(backend, store=store, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
 
 
