@@ -172,7 +172,7 @@ int dtf_conv1x1_bwd_lazy_blocks(int, int);
 void dtf_conv1x1_bwd_lazy(const bf16_t*, const bf16_t*, const uint8_t*, const float*, const float*,
                           const float*, const bf16_t*, const bf16_t*, const bf16_t*, const float*,
                           const float*, const float*, const float*, bf16_t*, float*, float*, int,
-                          int, int, hipStream_t);
+                          int, int, const bf16_t*, hipStream_t);
 void dtf_conv1x1_bwd(const bf16_t*, const bf16_t*, const bf16_t*, const bf16_t*, const float*,
                      const float*, const float*, const float*, bf16_t*, float*, float*, int, int,
                      int, hipStream_t);
@@ -802,11 +802,11 @@ PYBIND11_MODULE(_dtf_hip, m) {
                                uintptr_t cB, uintptr_t cC, uintptr_t wt, uintptr_t y, uintptr_t x,
                                uintptr_t mean, uintptr_t inv, uintptr_t sc, uintptr_t sh,
                                uintptr_t dy, uintptr_t wpart, uintptr_t bpart, int M, int C, int K,
-                               uintptr_t stream) {
+                               uintptr_t w, uintptr_t stream) {
     dtf_conv1x1_bwd_lazy(P<bf16_t>(dy3), P<bf16_t>(x3), P<uint8_t>(mask), P<float>(cA),
                          P<float>(cB), P<float>(cC), P<bf16_t>(wt), P<bf16_t>(y), P<bf16_t>(x),
                          P<float>(mean), P<float>(inv), P<float>(sc), P<float>(sh), P<bf16_t>(dy),
-                         P<float>(wpart), P<float>(bpart), M, C, K, S(stream));
+                         P<float>(wpart), P<float>(bpart), M, C, K, P<bf16_t>(w), S(stream));
     check_launch("conv1x1_bwd_lazy");
   });
   m.def("conv1x1_bwd", [](uintptr_t dout, uintptr_t wt, uintptr_t y, uintptr_t x, uintptr_t mean,

@@ -43,10 +43,12 @@ typedef __attribute__((address_space(3))) s4_t lds_s4_t;
 // per-shape configuration: C in, K out, TM rows per tile, NW waves; LZ: the conv-output gradient
 // dO is formed in the kernel from the consuming BatchNorm's (dy, x3, ReLU bit mask) and its
 // backward coefficients (see `LAZY` below) instead of being read
-template <int C_, int K_, int TM_, int NW_, bool LZ_ = false>
+// RC (with LZ): x3 is not read either -- recomputed per tile from Y and W with the forward's exact
+// MFMA chain (x3 = bf16(Y W^T), ks in order), so the kernel reads neither dO nor x3
+template <int C_, int K_, int TM_, int NW_, bool LZ_ = false, bool RC_ = false>
 struct Cfg {
   static constexpr int C = C_, K = K_, TM = TM_, NW = NW_;
-  static constexpr bool LZ = LZ_;
+  static constexpr bool LZ = LZ_, RC = RC_;
   static constexpr int T = NW * 64;
   static constexpr int NCB = C / 16;                         // channel blocks
   static constexpr int CPW = NCB >= NW ? NCB / NW : 1;       // dgrad channel blocks per wave
@@ -56,7 +58,7 @@ struct Cfg {
   static constexpr int KBW = K / NW / 16;                    // wgrad dW row blocks per wave
   static constexpr int DO = TM * K;                          // bf16 per dO tile
   static constexpr int YT = TM * C;                          // bf16 per Y / x tile
-  static constexpr int OT = LZ ? 2 * DO : DO;               // dO tile, or dy3 + x3 tiles (LZ)
+  static constexpr int OT = (LZ && !RC) ? 2 * DO : DO;      // dO / dy3 tile (+ x3 tile: LZ, !RC)
   static constexpr int MB = LZ ? TM * K / 8 : 0;             // LZ: ReLU mask bytes per tile
   static constexpr int MI = MB / 1024;                       // ... = 1-KB DMAs, by wave 0
   static constexpr int SLOT = OT + 2 * YT + MB / 2;
@@ -67,8 +69,8 @@ struct Cfg {
   static constexpr int MCH = LZ ? TM * K / 8 / T : 0;       // LZ: 8-channel chunks per thread
   static constexpr size_t LDS = (size_t)kNB * SLOT * 2 + (size_t)WPC * 2 * C * 4 + 4 * C * 4 +
                                 (LZ ? (size_t)3 * K * 4 : 0);   // LZ: the A / B / C coefficients
-  static_assert(!LZ || ((TM * K / 8) % T == 0 && T % (K / 8) == 0 && MB % 1024 == 0 && MI <= NW),
-                "LZ transform split");
+  static_assert(!LZ || ((RC || ((TM * K / 8) % T == 0 && T % (K / 8) == 0)) && MB % 1024 == 0 &&
+                        MI <= NW), "LZ transform split");
   static_assert(DOI % NW == 0 && (2 * YI) % NW == 0, "DMA split");
   static_assert(WPC * (NCB / CPW) == NW && MBW >= 1 && (TM % 32 == 0 || TM == 16), "wave split");
   static_assert(LDS <= 160 * 1024, "conv1x1_bwd LDS");
@@ -121,6 +123,9 @@ DTF_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+template <class F>
+constexpr int RC_KBW() { return F::RC ? F::K / F::NW / 16 : 1; }
+
 struct C1Args {
   const bf16_t* dout;   // [M][K]  gradient of the conv output
   const bf16_t* wt;     // [C][K]  W^T (wt[c][k] = W[k][c])
@@ -141,6 +146,7 @@ struct C1Args {
   const float* cA;
   const float* cB;
   const float* cC;
+  const bf16_t* w;      // RC: the conv weight [K][C] (x3 = Y W^T)
 };
 
 template <class F>
@@ -226,6 +232,17 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
       scoef[2 * K + t] = g.cC[t];
     }
   }
+  // RC: W fragments for this wave's x3 columns k in [wave K/NW, (wave+1) K/NW), all C (A operand)
+  constexpr int KSC = C / 32;
+  bf16x8_t wr[RC_KBW<F>()][KSC];
+  if constexpr (F::RC) {
+#pragma unroll
+    for (int kb = 0; kb < RC_KBW<F>(); ++kb)
+#pragma unroll
+      for (int ks = 0; ks < KSC; ++ks)
+        wr[kb][ks] = *reinterpret_cast<const bf16x8_t*>(
+            g.w + (long)(wave * (K / NW) + kb * 16 + li) * C + ks * 32 + gq * 8);
+  }
 
   f32x4_t aw[KBW][NCB];
 #pragma unroll
@@ -275,7 +292,50 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
       if (i + 2 < nmy) issue(i + 2);
     }
     bf16_t* const slot = lds + (i % kNB) * F::SLOT;
-    if constexpr (LZ) {
+    if constexpr (LZ && F::RC) {
+      // x3 of this wave's columns recomputed from Y (the forward stream GEMM's chain with the
+      // operands swapped: the same products in the same k order, bit-identical) and dO formed in
+      // place over dy3 -- lane (li, gq): row 16 mb + li, columns k0 .. k0 + 3
+      int lx = lane;
+      asm volatile("" : "+v"(lx));
+      const int xi = lx & 15, xq = lx >> 4;
+      const uint8_t* msk = reinterpret_cast<const uint8_t*>(slot + F::OT + 2 * F::YT);
+#pragma unroll
+      for (int mb = 0; mb < TM / 16; ++mb) {
+        const int m = mb * 16 + xi;
+        bf16x8_t yb[KSC];
+#pragma unroll
+        for (int ks = 0; ks < KSC; ++ks)
+          yb[ks] = *reinterpret_cast<const bf16x8_t*>(slot + F::OT + sidx<C>(m, ks * 32 + xq * 8, swz_y<C>(m)));
+#pragma unroll
+        for (int kb = 0; kb < RC_KBW<F>(); ++kb) {
+          f32x4_t a = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < KSC; ++ks) a = mfma16(wr[kb][ks], yb[ks], a);
+          const int k0 = wave * (K / NW) + kb * 16 + 4 * xq;
+          const int o = sidx<K>(m, k0, swz_o(m));
+          const uint2 d = *reinterpret_cast<const uint2*>(slot + o);
+          const uint32_t mbits = (uint32_t)msk[m * (K / 8) + (k0 >> 3)] >> (k0 & 7);
+          const float4 A4 = *reinterpret_cast<const float4*>(scoef + k0);
+          const float4 B4 = *reinterpret_cast<const float4*>(scoef + K + k0);
+          const float4 C4 = *reinterpret_cast<const float4*>(scoef + 2 * K + k0);
+          const float ca[4] = {A4.x, A4.y, A4.z, A4.w}, cb[4] = {B4.x, B4.y, B4.z, B4.w};
+          const float cc[4] = {C4.x, C4.y, C4.z, C4.w};
+          const float gv[4] = {__builtin_bit_cast(float, d.x << 16), __builtin_bit_cast(float, d.x & 0xffff0000u),
+                               __builtin_bit_cast(float, d.y << 16), __builtin_bit_cast(float, d.y & 0xffff0000u)};
+          float ov[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float xv = bf2f(f2bf(a[r]));          // x3 exactly as the forward stored it
+            const float dz = (mbits >> r) & 1u ? gv[r] : 0.f;
+            ov[r] = bn_bwd_dx(ca[r], dz, cb[r], xv, cc[r]);
+          }
+          *reinterpret_cast<uint2*>(slot + o) = make_uint2(pack2(ov[0], ov[1]), pack2(ov[2], ov[3]));
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+    } else if constexpr (LZ) {
       // dO = the residual BatchNorm's backward apply, in place over the dy3 tile (bit-identical to
       // bn_bwd_apply_kernel<1>'s stored dx: same dz, same bn_bwd_dx, same bf16 rounding)
       int tt = tid;                 // recomputed per tile (see `ln` below)
@@ -436,7 +496,8 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
 
 typedef Cfg<64, 256, 64, 8> CfgS0;    // stage 0: 56 x 56 x 64 -> 256
 typedef Cfg<128, 512, 32, 8> CfgS1;   // stage 1: 28 x 28 x 128 -> 512
-typedef Cfg<64, 256, 32, 8, true> CfgS0L;   // stage 0, dO formed from the residual BN (LZ)
+typedef Cfg<64, 256, 64, 8, true, true> CfgS0L;   // stage 0, dO formed from the residual BN,
+                                                  // x3 recomputed (LZ + RC)
 typedef Cfg<128, 512, 16, 8, true> CfgS1L;  // stage 1, LZ (16-row tiles: 42 KB ring slots)
 
 int g_c1_grid = 0;   // 0 = one block per CU
@@ -514,14 +575,14 @@ void dtf_conv1x1_bwd_lazy(const bf16_t* dy3, const bf16_t* x3, const uint8_t* ma
                           const float* cA, const float* cB, const float* cC, const bf16_t* wt,
                           const bf16_t* y, const bf16_t* x, const float* mean, const float* inv,
                           const float* sc, const float* sh, bf16_t* dy, float* wpart,
-                          float* bpart, int M, int C, int K, hipStream_t st) {
+                          float* bpart, int M, int C, int K, const bf16_t* w, hipStream_t st) {
   if (!dtf_conv1x1_bwd_lazy_ok(M, C, K))
     throw std::runtime_error("conv1x1_bwd_lazy: (C, K) in {(64, 256), (128, 512)}, M % tile == 0");
-  const void* ptrs[] = {dy3, x3, mask, cA, cB, cC, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart};
+  const void* ptrs[] = {dy3, x3, mask, cA, cB, cC, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart, w};
   for (const void* p : ptrs)
     if (!p || (reinterpret_cast<uintptr_t>(p) & 15))
       throw std::runtime_error("conv1x1_bwd_lazy: null or misaligned operand");
-  C1Args g{dy3, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart, M, x3, mask, cA, cB, cC};
+  C1Args g{dy3, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart, M, x3, mask, cA, cB, cC, w};
   if (C == 64) launch_c1<CfgS0L>(g, st);
   else launch_c1<CfgS1L>(g, st);
 }

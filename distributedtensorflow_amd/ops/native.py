@@ -990,14 +990,15 @@ def _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K, lazy=None):
     wt = _dgrad_filter(wb.reshape(K, 1, C)).view(C, K)
     common = (wt.data_ptr(), y.data_ptr(), x.data_ptr(), stats[0].data_ptr(),
               stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), dy.data_ptr(),
-              wpart.data_ptr(), part.data_ptr(), M, C, K, st)
+              wpart.data_ptr(), part.data_ptr(), M, C, K)
     if lazy is not None:
-        # d(conv output) formed per tile from the residual BN's (dy, x, mask, coefficients)
+        # d(conv output) formed per tile from the residual BN's (dy, x, mask, coefficients); at
+        # stage 0 x (this conv's output) is recomputed from y and w instead of read
         _K.conv1x1_bwd_lazy(lazy.dy.data_ptr(), lazy.x.data_ptr(), lazy.mask.data_ptr(),
                             lazy.gb[2].data_ptr(), lazy.gb[3].data_ptr(), lazy.gb[4].data_ptr(),
-                            *common)
+                            *common, wb.data_ptr(), st)
     else:
-        _K.conv1x1_bwd(dout.data_ptr(), *common)
+        _K.conv1x1_bwd(dout.data_ptr(), *common, st)
     dw = None
     if target is not None:
         _K.slab_reduce(wpart.data_ptr(), target.data_ptr(), K * C, G, 1, st)

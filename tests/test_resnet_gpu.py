@@ -394,16 +394,26 @@ def test_lazy_residual_bn_dx_formed_in_fused_c3_backward(block, cin, hw):
     x = torch.randn(2, hw, hw, cin, device="cuda").bfloat16()
     calls = {"n": 0}
     orig = native._K.conv1x1_bwd_lazy
+    orig_core = native._bn_backward_core
+    seen = {}
 
     def spy(*a):
         calls["n"] += 1
         return orig(*a)
+
+    def core_spy(ctx, dy, *a, **k):
+        if isinstance(ctx, native._BnReluConv1x1):
+            seen.setdefault(lz_now[0], []).append(dy.detach().clone())   # c3's data gradient
+        return orig_core(ctx, dy, *a, **k)
     out = {}
     prev = native._FUSE_C3_LAZY
     g = None
+    lz_now = [None]
     try:
         native._K.conv1x1_bwd_lazy = spy
+        native._bn_backward_core = core_spy
         for lz in (True, False):
+            lz_now[0] = lz
             native._FUSE_C3_LAZY = lz
             b = copy.deepcopy(blk)
             xi = x.clone().requires_grad_(True)
@@ -417,8 +427,13 @@ def test_lazy_residual_bn_dx_formed_in_fused_c3_backward(block, cin, hw):
                        [p.grad.float() for p in b.parameters()])
     finally:
         native._K.conv1x1_bwd_lazy = orig
+        native._bn_backward_core = orig_core
         native._FUSE_C3_LAZY = prev
     assert calls["n"] == 1
+    # d(c3 output) formed in the kernel (from dy3, x3 or its recomputation, mask) is bit-identical
+    # to the apply pass's stored one, so c3's data gradient is too
+    assert len(seen[True]) == len(seen[False]) == 1
+    assert torch.equal(seen[True][0], seen[False][0])
     (ya, dxa, ga), (yb, dxb, gb) = out[True], out[False]
     assert torch.equal(ya, yb)
     rel = ((dxa - dxb).norm() / dxb.norm()).item()
