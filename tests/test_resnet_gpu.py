@@ -402,7 +402,7 @@ def test_lazy_residual_bn_dx_formed_in_fused_c3_backward(block, cin, hw):
         return orig(*a)
 
     def core_spy(ctx, dy, *a, **k):
-        if isinstance(ctx, native._BnReluConv1x1):
+        if type(ctx).__name__.startswith("_BnReluConv1x1"):
             seen.setdefault(lz_now[0], []).append(dy.detach().clone())   # c3's data gradient
         return orig_core(ctx, dy, *a, **k)
     out = {}
