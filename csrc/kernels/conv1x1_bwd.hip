@@ -235,13 +235,23 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
   // RC: W fragments for this wave's x3 columns k in [wave K/NW, (wave+1) K/NW), all C (A operand)
   constexpr int KSC = C / 32;
   bf16x8_t wr[RC_KBW<F>()][KSC];
+  float rca[RC_KBW<F>()][4], rcb[RC_KBW<F>()][4], rcc[RC_KBW<F>()][4];   // RC: this lane's A/B/C
   if constexpr (F::RC) {
 #pragma unroll
-    for (int kb = 0; kb < RC_KBW<F>(); ++kb)
+    for (int kb = 0; kb < RC_KBW<F>(); ++kb) {
 #pragma unroll
       for (int ks = 0; ks < KSC; ++ks)
         wr[kb][ks] = *reinterpret_cast<const bf16x8_t*>(
             g.w + (long)(wave * (K / NW) + kb * 16 + li) * C + ks * 32 + gq * 8);
+      // the 4 columns this lane forms in every tile are fixed: coefficients in registers
+      const int k0 = wave * (K / NW) + kb * 16 + 4 * gq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        rca[kb][r] = g.cA[k0 + r];
+        rcb[kb][r] = g.cB[k0 + r];
+        rcc[kb][r] = g.cC[k0 + r];
+      }
+    }
   }
 
   f32x4_t aw[KBW][NCB];
@@ -316,11 +326,9 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
           const int o = sidx<K>(m, k0, swz_o(m));
           const uint2 d = *reinterpret_cast<const uint2*>(slot + o);
           const uint32_t mbits = (uint32_t)msk[m * (K / 8) + (k0 >> 3)] >> (k0 & 7);
-          const float4 A4 = *reinterpret_cast<const float4*>(scoef + k0);
-          const float4 B4 = *reinterpret_cast<const float4*>(scoef + K + k0);
-          const float4 C4 = *reinterpret_cast<const float4*>(scoef + 2 * K + k0);
-          const float ca[4] = {A4.x, A4.y, A4.z, A4.w}, cb[4] = {B4.x, B4.y, B4.z, B4.w};
-          const float cc[4] = {C4.x, C4.y, C4.z, C4.w};
+          const float* ca = rca[kb];
+          const float* cb = rcb[kb];
+          const float* cc = rcc[kb];
           const float gv[4] = {__builtin_bit_cast(float, d.x << 16), __builtin_bit_cast(float, d.x & 0xffff0000u),
                                __builtin_bit_cast(float, d.y << 16), __builtin_bit_cast(float, d.y & 0xffff0000u)};
           float ov[4];
