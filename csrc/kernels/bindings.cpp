@@ -155,6 +155,7 @@ void dtf_ln_fwd(const bf16_t*, const float*, const bf16_t*, const float*, const 
                 const int64_t*, const int64_t*, const bf16_t*, const bf16_t*, const bf16_t*, int,
                 hipStream_t);
 int dtf_ln_bwd_blocks(int);
+void dtf_ln_set_wide(int);
 void dtf_ln_bwd(const bf16_t*, const bf16_t*, const float*, const float*, const float*, bf16_t*,
                 bf16_t*, float*, float*, float*, float*, int, int, float, uint32_t, float,
                 uint32_t, hipStream_t, int);
@@ -793,6 +794,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
                            uintptr_t stream) {
     dtf_bf16_col_sum(P<const bf16_t>(x), T, N, P<float>(ws), P<float>(out), accumulate, S(stream));
   });
+  m.def("ln_set_wide", &dtf_ln_set_wide);
   m.def("conv1x1_bwd_ok", &dtf_conv1x1_bwd_ok);
   m.def("conv1x1_bwd_blocks", &dtf_conv1x1_bwd_blocks);
   m.def("conv1x1_bwd_set_grid", &dtf_conv1x1_bwd_set_grid);

@@ -253,6 +253,180 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const LnBwdArgs g) {
   }
 }
 
+// 16-B variants ("wide"): a HALF wave per row, every lane moving 16-B chunks (8 elements) at
+// columns (c * 32 + lane) * 8 -- the 8-B-per-lane kernels above read / wrote ~70 % of the HBM rate
+// at BERT's H = 768.  Same per-element arithmetic and dropout indices; the row statistics are the
+// same sums in a different lane order.
+DTF_DEV float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+  return v;
+}
+DTF_DEV void load8b(const bf16_t* p, float* f) { unpack8(*reinterpret_cast<const uint4*>(p), f); }
+DTF_DEV void store8b(bf16_t* p, const float* f) { *reinterpret_cast<uint4*>(p) = pack8(f); }
+
+template <int NC>
+__global__ void __launch_bounds__(256) ln_fwd_wide_kernel(const LnArgs g) {
+  constexpr int H = NC * 256;
+  const int hl = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (row >= g.M) return;           // whole half-waves: the shuffles stay inside a half
+  const long base = (long)row * H;
+  float v[NC][8];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int col = (i * 32 + hl) * 8;
+    if (g.a) {
+      load8b(g.a + base + col, v[i]);
+      if (g.bias) {
+        const float4 b0 = *reinterpret_cast<const float4*>(g.bias + col);
+        const float4 b1 = *reinterpret_cast<const float4*>(g.bias + col + 4);
+        v[i][0] += b0.x; v[i][1] += b0.y; v[i][2] += b0.z; v[i][3] += b0.w;
+        v[i][4] += b1.x; v[i][5] += b1.y; v[i][6] += b1.z; v[i][7] += b1.w;
+      }
+      if (g.thr_pre) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[i][e] = keep_elem(g.seed_pre, (uint32_t)(base + col + e), g.thr_pre)
+                        ? v[i][e] * g.inv_keep_pre : 0.f;
+      }
+      if (g.res) {
+        float r[8];
+        load8b(g.res + base + col, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] += r[e];
+      }
+    } else {
+      float w[8], p[8], t[8];
+      load8b(g.word + g.ids[row] * (long)H + col, w);
+      load8b(g.pos + (long)(row % g.S) * H + col, p);
+      load8b(g.type + (g.tt ? g.tt[row] : 0) * (long)H + col, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = w[e] + p[e] + t[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = round_bf(v[i][e]);
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sum += v[i][e];
+  const float mean = half_sum(sum) * (1.f / H);
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[i][e] - mean;
+      sq += d * d;
+    }
+  const float rstd = rsqrtf(half_sum(sq) * (1.f / H) + g.eps);
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int col = (i * 32 + hl) * 8;
+    if (g.s) store8b(g.s + base + col, v[i]);
+    float o[8];
+    const float4 g0 = *reinterpret_cast<const float4*>(g.gamma + col);
+    const float4 g1 = *reinterpret_cast<const float4*>(g.gamma + col + 4);
+    const float4 e0 = *reinterpret_cast<const float4*>(g.beta + col);
+    const float4 e1 = *reinterpret_cast<const float4*>(g.beta + col + 4);
+    const float gm[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bt[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = (v[i][e] - mean) * rstd * gm[e] + bt[e];
+      if (g.thr_post)
+        o[e] = keep_elem(g.seed_post, (uint32_t)(base + col + e), g.thr_post)
+                   ? o[e] * g.inv_keep_post : 0.f;
+    }
+    store8b(g.y + base + col, o);
+  }
+  if (hl == 0) {
+    g.mean[row] = mean;
+    g.rstd[row] = rstd;
+  }
+}
+
+template <int NC>
+__global__ void __launch_bounds__(256) ln_bwd_wide_kernel(const LnBwdArgs g) {
+  constexpr int H = NC * 256;
+  __shared__ float red[8][H];
+  const int hl = threadIdx.x & 31, half = threadIdx.x >> 5;
+  float ag[NC][8], ab[NC][8], abias[NC][8];
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ag[i][e] = ab[i][e] = abias[i][e] = 0.f;
+  const int r0 = blockIdx.x * g.rows_per_block;
+  const int r1 = min(g.M, r0 + g.rows_per_block);
+  for (int row = r0 + half; row < r1; row += 8) {
+    const long base = (long)row * H;
+    const float mean = g.mean[row], rstd = g.rstd[row];
+    float xh[NC][8], gy[NC][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int col = (i * 32 + hl) * 8;
+      float sv[8], dy[8];
+      load8b(g.dy + base + col, dy);
+      load8b(g.s + base + col, sv);
+      const float4 g0 = *reinterpret_cast<const float4*>(g.gamma + col);
+      const float4 g1 = *reinterpret_cast<const float4*>(g.gamma + col + 4);
+      const float gm[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (g.thr_post)
+          dy[e] = keep_elem(g.seed_post, (uint32_t)(base + col + e), g.thr_post)
+                      ? dy[e] * g.inv_keep_post : 0.f;
+        xh[i][e] = (sv[e] - mean) * rstd;
+        gy[i][e] = dy[e] * gm[e];
+        ag[i][e] += dy[e] * xh[i][e];
+        ab[i][e] += dy[e];
+        s1 += gy[i][e];
+        s2 += gy[i][e] * xh[i][e];
+      }
+    }
+    s1 = half_sum(s1) * (1.f / H);
+    s2 = half_sum(s2) * (1.f / H);
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int col = (i * 32 + hl) * 8;
+      float dx[8], da[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dx[e] = rstd * (gy[i][e] - s1 - xh[i][e] * s2);
+        if (g.thr_pre)
+          da[e] = keep_elem(g.seed_pre, (uint32_t)(base + col + e), g.thr_pre)
+                      ? dx[e] * g.inv_keep_pre : 0.f;
+        else
+          da[e] = dx[e];
+        abias[i][e] += da[e];
+      }
+      store8b(g.ds + base + col, dx);
+      if (g.da) store8b(g.da + base + col, da);
+    }
+  }
+  float* outs[3] = {g.part_g, g.part_b, g.part_bias};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (!outs[k]) continue;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NC; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        red[half][(i * 32 + hl) * 8 + e] = k == 0 ? ag[i][e] : (k == 1 ? ab[i][e] : abias[i][e]);
+    __syncthreads();
+    for (int c = threadIdx.x; c < H; c += 256) {
+      float t = 0.f;
+#pragma unroll
+      for (int h2 = 0; h2 < 8; ++h2) t += red[h2][c];
+      outs[k][(long)blockIdx.x * H + c] = t;
+    }
+  }
+}
+
 // out[c] (+)= sum_p part[p, c] in fixed order
 // Deterministic two-level column sum of a [P][N] fp32 partial slab (N % 4 == 0):
 //   level 1: grid (N/256 float4-column groups, S row slices); 4 waves = 4 row groups, each lane
@@ -1175,6 +1349,11 @@ static uint32_t drop_thr(float p) {
   return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
 }
 
+// 16-B half-wave-per-row LayerNorm kernels: bit 0 forward, bit 1 backward (the backward's 72
+// per-lane column accumulators push it to ~190 VGPRs at H = 768: off unless measured faster)
+static int g_ln_wide = 1;
+void dtf_ln_set_wide(int v) { g_ln_wide = v; }
+
 void dtf_ln_fwd(const bf16_t* a, const float* bias, const bf16_t* res, const float* gamma,
                 const float* beta, bf16_t* y, bf16_t* s, float* mean, float* rstd, int M, int H,
                 float eps, float p_pre, uint32_t seed_pre, float p_post, uint32_t seed_post,
@@ -1184,6 +1363,16 @@ void dtf_ln_fwd(const bf16_t* a, const float* bias, const bf16_t* res, const flo
   LnArgs g{a, bias, res, gamma, beta, y, s, mean, rstd, ids, tt, word, pos, type, M, S, eps,
            seed_pre, drop_thr(p_pre), seed_post, drop_thr(p_post),
            p_pre > 0.f ? 1.f / (1.f - p_pre) : 1.f, p_post > 0.f ? 1.f / (1.f - p_post) : 1.f};
+  if (g_ln_wide & 1) {
+    const dim3 gw((M + 7) / 8), bw(256);
+    switch (H / 256) {
+      case 1: hipLaunchKernelGGL(ln_fwd_wide_kernel<1>, gw, bw, 0, st, g); break;
+      case 2: hipLaunchKernelGGL(ln_fwd_wide_kernel<2>, gw, bw, 0, st, g); break;
+      case 3: hipLaunchKernelGGL(ln_fwd_wide_kernel<3>, gw, bw, 0, st, g); break;
+      default: hipLaunchKernelGGL(ln_fwd_wide_kernel<4>, gw, bw, 0, st, g); break;
+    }
+    return;
+  }
   const dim3 grid((M + 3) / 4), block(256);
   switch (H / 256) {
     case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, block, 0, st, g); break;
@@ -1211,11 +1400,20 @@ void dtf_ln_bwd(const bf16_t* dy, const bf16_t* s, const float* mean, const floa
               seed_pre, drop_thr(p_pre), seed_post, drop_thr(p_post),
               p_pre > 0.f ? 1.f / (1.f - p_pre) : 1.f, p_post > 0.f ? 1.f / (1.f - p_post) : 1.f};
   const dim3 grid(nblk), block(256);
-  switch (H / 256) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, st, g); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, st, g); break;
-    case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, st, g); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, block, 0, st, g); break;
+  if (g_ln_wide & 2) {
+    switch (H / 256) {
+      case 1: hipLaunchKernelGGL(ln_bwd_wide_kernel<1>, grid, block, 0, st, g); break;
+      case 2: hipLaunchKernelGGL(ln_bwd_wide_kernel<2>, grid, block, 0, st, g); break;
+      case 3: hipLaunchKernelGGL(ln_bwd_wide_kernel<3>, grid, block, 0, st, g); break;
+      default: hipLaunchKernelGGL(ln_bwd_wide_kernel<4>, grid, block, 0, st, g); break;
+    }
+  } else {
+    switch (H / 256) {
+      case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, st, g); break;
+      case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, st, g); break;
+      case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, st, g); break;
+      default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, block, 0, st, g); break;
+    }
   }
   col_sum(part, region, dbias ? 3 : 2, nblk, H, ColSumOut{{dgamma, dbeta, dbias}}, st, accumulate);
 }

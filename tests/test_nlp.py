@@ -130,7 +130,20 @@ def _grads_of(fn, inputs, dy):
 @pytest.mark.gpu
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("H", [768, 1024])
-def test_fused_layer_norm_gpu(p, H):
+@pytest.mark.parametrize("wide", [0, 3])
+def test_fused_layer_norm_gpu(p, H, wide):
+    """bias + dropout + residual + LayerNorm forward / backward against fp32, with the 8-B and the
+    16-B half-wave-per-row kernels (``wide``: bit 0 forward, bit 1 backward; M = 300 leaves a
+    partial last block)."""
+    from distributedtensorflow_amd.ops import native
+    native.kernels().ln_set_wide(wide)
+    try:
+        _fused_layer_norm_case(p, H)
+    finally:
+        native.kernels().ln_set_wide(1)
+
+
+def _fused_layer_norm_case(p, H):
     torch.manual_seed(0)
     M = 300
     a32, r32 = torch.randn(M, H), torch.randn(M, H)
