@@ -168,6 +168,7 @@ void dtf_slab_reduce(const float*, float*, long, int, int, hipStream_t);
 bool dtf_conv1x1_bwd_ok(int, int, int);
 int dtf_conv1x1_bwd_blocks(int, int);
 void dtf_conv1x1_bwd_set_grid(int);
+void dtf_conv1x1_bwd_set_w16(int);
 bool dtf_conv1x1_bwd_lazy_ok(int, int, int);
 int dtf_conv1x1_bwd_lazy_blocks(int, int);
 void dtf_conv1x1_bwd_lazy(const bf16_t*, const bf16_t*, const uint8_t*, const float*, const float*,
@@ -798,6 +799,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("conv1x1_bwd_ok", &dtf_conv1x1_bwd_ok);
   m.def("conv1x1_bwd_blocks", &dtf_conv1x1_bwd_blocks);
   m.def("conv1x1_bwd_set_grid", &dtf_conv1x1_bwd_set_grid);
+  m.def("conv1x1_bwd_set_w16", &dtf_conv1x1_bwd_set_w16);
   m.def("conv1x1_bwd_lazy_ok", &dtf_conv1x1_bwd_lazy_ok);
   m.def("conv1x1_bwd_lazy_blocks", &dtf_conv1x1_bwd_lazy_blocks);
   m.def("conv1x1_bwd_lazy", [](uintptr_t dy3, uintptr_t x3, uintptr_t mask, uintptr_t cA,

@@ -503,12 +503,15 @@ __global__ void __launch_bounds__(F::T, 1) conv1x1_bwd_kernel(const C1Args g) {
 }
 
 typedef Cfg<64, 256, 64, 8> CfgS0;    // stage 0: 56 x 56 x 64 -> 256
+typedef Cfg<64, 256, 64, 16> CfgS0W;  // ... as 16 waves (<= 128 VGPRs: 4 waves per SIMD)
 typedef Cfg<128, 512, 32, 8> CfgS1;   // stage 1: 28 x 28 x 128 -> 512
 typedef Cfg<64, 256, 64, 8, true, true> CfgS0L;   // stage 0, dO formed from the residual BN,
                                                   // x3 recomputed (LZ + RC)
+typedef Cfg<64, 256, 64, 16, true, true> CfgS0LW; // ... as 16 waves
 typedef Cfg<128, 512, 16, 8, true> CfgS1L;  // stage 1, LZ (16-row tiles: 42 KB ring slots)
 
 int g_c1_grid = 0;   // 0 = one block per CU
+int g_c1_w16 = 1;    // stage 0 as 16-wave blocks (twice the waves per SIMD to hide latency)
 
 int c1_tm(int C) { return C == 64 ? CfgS0::TM : CfgS1::TM; }
 
@@ -550,6 +553,7 @@ int dtf_conv1x1_bwd_blocks(int M, int C) {
 }
 
 void dtf_conv1x1_bwd_set_grid(int n) { g_c1_grid = n; }
+void dtf_conv1x1_bwd_set_w16(int v) { g_c1_w16 = v; }
 
 void dtf_conv1x1_bwd(const bf16_t* dout, const bf16_t* wt, const bf16_t* y, const bf16_t* x,
                      const float* mean, const float* inv, const float* sc, const float* sh,
@@ -561,8 +565,12 @@ void dtf_conv1x1_bwd(const bf16_t* dout, const bf16_t* wt, const bf16_t* y, cons
     if (!p || (reinterpret_cast<uintptr_t>(p) & 15))
       throw std::runtime_error("conv1x1_bwd: null or misaligned operand");
   C1Args g{dout, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart, M};
-  if (C == 64) launch_c1<CfgS0>(g, st);
-  else launch_c1<CfgS1>(g, st);
+  if (C == 64) {
+    if (g_c1_w16) launch_c1<CfgS0W>(g, st);
+    else launch_c1<CfgS0>(g, st);
+  } else {
+    launch_c1<CfgS1>(g, st);
+  }
 }
 
 // LZ form (stages 0 and 1): the conv-output gradient dO is never stored -- formed per tile from the
@@ -591,6 +599,10 @@ void dtf_conv1x1_bwd_lazy(const bf16_t* dy3, const bf16_t* x3, const uint8_t* ma
     if (!p || (reinterpret_cast<uintptr_t>(p) & 15))
       throw std::runtime_error("conv1x1_bwd_lazy: null or misaligned operand");
   C1Args g{dy3, wt, y, x, mean, inv, sc, sh, dy, wpart, bpart, M, x3, mask, cA, cB, cC, w};
-  if (C == 64) launch_c1<CfgS0L>(g, st);
-  else launch_c1<CfgS1L>(g, st);
+  if (C == 64) {
+    if (g_c1_w16) launch_c1<CfgS0LW>(g, st);
+    else launch_c1<CfgS0L>(g, st);
+  } else {
+    launch_c1<CfgS1L>(g, st);
+  }
 }

@@ -50,7 +50,10 @@ def main():
         stats = torch.rand(4, C, device=dev) + 0.5
         coef = torch.rand(3, K, device=dev)
         dy = torch.empty_like(y)
-        for lazy in (False, True):
+        for lazy, w16 in ((False, 0), (False, 1), (True, 0), (True, 1)):
+            if C != 64 and w16:
+                continue
+            _K.conv1x1_bwd_set_w16(w16)
             G = (_K.conv1x1_bwd_lazy_blocks(M, C) if lazy else _K.conv1x1_bwd_blocks(M, C))
             wpart = torch.empty(G * K * C, device=dev)
             part = torch.empty(_K.bn_workspace_floats_g(G, C), device=dev)
@@ -67,7 +70,7 @@ def main():
                 fn = lambda: _K.conv1x1_bwd(dout.data_ptr(), *common, st())  # noqa: E731
                 nbytes = M * (K * 2 + C * 6)
             us = timeit(fn, a.iters)
-            print(json.dumps({"probe": "c1_bench", "C": C, "K": K, "M": M, "lazy": lazy,
+            print(json.dumps({"probe": "c1_bench", "C": C, "K": K, "M": M, "lazy": lazy, "w16": w16,
                               "blocks": G, "us": round(us, 1), "GB": round(nbytes / 1e9, 2),
                               "TBps": round(nbytes / us / 1e6, 2)}), flush=True)
 
