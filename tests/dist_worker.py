@@ -86,6 +86,8 @@ def main():
         return mirrored_recovery(out, kw, steps)
     if kind == "resnet_gpu":
         return resnet_gpu_grads(out)
+    if kind == "colocated_bert":
+        return colocated_bert(out, kw, steps)
     if kind == "mirrored":
         strat = MirroredStrategy(bucket_mb=float(kw.get("bucket_mb", 64)),
                                  first_bucket_mb=float(kw.get("bucket_mb", 4)),
@@ -129,6 +131,46 @@ def main():
                 "sharded": getattr(opt._reducer, "sharded", None),
                 "reducer": type(opt._reducer).__name__},
                os.path.join(out, f"rank{rank}.pt"))
+    strat.barrier()
+
+
+def colocated_bert(out, kw, steps):
+    """A tiny BERT (every dense layer, the fused bias + GELU + dense FFN op, LayerNorms,
+    embeddings) under the sharded colocated parameter server with many buckets: with the
+    overlapped all-gather pull, every op that reads a variable must wait for that variable's
+    bucket (ops parameter fence).  The test compares the run with overlap on to overlap off."""
+    import distributedtensorflow_amd as dtf
+    from distributedtensorflow_amd import ops
+    from distributedtensorflow_amd.models.bert import BertConfig, BertForPreTraining
+    from distributedtensorflow_amd.optimizers import MomentumOptimizer
+    from distributedtensorflow_amd.parallel import ParameterServerStrategy
+    strat = ParameterServerStrategy(num_ps=2, bucket_mb=0.02, first_bucket_mb=0.02,
+                                    overlap_gather=kw.get("overlap", "1") == "1")
+    rank, world = strat.replica_id, strat.num_replicas_in_sync
+    torch.manual_seed(31 + 7 * rank)            # rank 0's variables must win the broadcast
+    cfg = BertConfig(vocab_size=200, hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
+                     intermediate_size=256, max_position_embeddings=32, hidden_dropout_prob=0.0,
+                     attention_probs_dropout_prob=0.0)
+    with strat.scope():
+        model = BertForPreTraining(cfg)
+        opt = MomentumOptimizer(0.05, 0.9)
+        gstep = dtf.train.get_or_create_global_step()
+        opt.build(list(model.parameters()))
+        for step in range(steps):
+            g = torch.Generator().manual_seed(500 + 10 * step + rank)
+            B, S, P = 2, 16, 4
+            ids = torch.randint(0, 200, (B, S), generator=g, device="cpu")
+            tt = torch.zeros(B, S, dtype=torch.long)
+            am = torch.ones(B, S)
+            pos = torch.randint(0, S, (B, P), generator=g, device="cpu")
+            lab = torch.randint(0, 200, (B, P), generator=g, device="cpu")
+            w = torch.ones(B, P)
+            loss = model(ids, tt, am, pos, lab, w)
+            opt.minimize(loss, global_step=gstep)
+        fps = dtf.distribute.check_replicas_consistent(opt)      # raises if replicas diverged
+    torch.save({"state": {k: v.detach().clone() for k, v in model.state_dict().items()},
+                "fingerprints": fps, "sharded": getattr(opt._reducer, "sharded", None),
+                "loss": float(loss.detach())}, os.path.join(out, f"rank{rank}.pt"))
     strat.barrier()
 
 

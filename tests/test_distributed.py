@@ -143,6 +143,20 @@ def test_colocated_ps_sharded_owners_reduce_scatter(tmp_path):
     _assert_replicas(off, _single_process("momentum"))
 
 
+def test_colocated_ps_bert_fenced_against_overlapped_gathers(tmp_path):
+    """every ops entry point that reads a variable waits for its bucket's
+    overlapped all-gather.  A tiny BERT (dense, fused bias + GELU + dense, LayerNorm, embeddings)
+    on the sharded colocated PS trains identically with the gathers overlapped and serial, and
+    the replicas agree in both."""
+    on = _launch("colocated_bert", 2, tmp_path, "steps=4", "overlap=1")
+    off = _launch("colocated_bert", 2, tmp_path, "steps=4", "overlap=0")
+    assert all(r["sharded"] is True for r in on + off)
+    for k in on[0]["state"]:
+        assert torch.equal(on[0]["state"][k], off[0]["state"][k]), k
+        assert torch.equal(on[0]["state"][k], on[1]["state"][k]), k
+    assert on[0]["loss"] == off[0]["loss"]
+
+
 def test_colocated_ps_lamb_keeps_variable_aligned_owners(tmp_path):
     """LAMB's per-tensor trust ratio cannot be split between owners: owner ranges stay on
     variable boundaries (reduce / broadcast path) and still match one process."""
