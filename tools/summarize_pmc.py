@@ -17,7 +17,7 @@ def main(d):
     keyname = "Kernel_Name" if "Kernel_Name" in rows[0] else "Kernel-Name"
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in rows:
-        k = (r[keyname][:70], r.get("Grid_Size", r.get("Grid-Size", "")))
+        k = (r[keyname][:160], r.get("Grid_Size", r.get("Grid-Size", "")))
         agg[k][r.get("Counter_Name", r.get("Counter-Name"))].append(
             float(r.get("Counter_Value", r.get("Counter-Value", 0))))
     for (name, grid), counters in agg.items():
