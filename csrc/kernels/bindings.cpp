@@ -53,7 +53,8 @@ void dtf_bn_fwd_finalize_g(const float*, int, long, int, const float*, const flo
 long dtf_bn_workspace_floats_g(int, int);
 int dtf_conv_stats_rows(long, int, int, int, int);
 void dtf_conv_set_halo(int);
-int dtf_conv_tile_rows(const ConvGeom&, const TapTable&);
+int dtf_conv_tile_rows(const ConvGeom&, const TapTable&, int bnb);
+void dtf_conv_set_halo_bnb(int);
 void dtf_conv_set_dma_mode(int);
 void dtf_conv_set_small_k(int);
 void dtf_conv_set_stem_halo(int);
@@ -187,6 +188,7 @@ void dtf_attn_bwd(const bf16_t*, const float*, const bf16_t*, const bf16_t*, con
 int dtf_attn_bwd_fused(int);
 int dtf_pos_type_grad_ws_floats(int, int, int);
 void dtf_attn_set_wide(int);
+void dtf_attn_set_fwd_occ(int);
 void dtf_attn_set_fused(int);
 void dtf_pos_type_grad(const bf16_t*, const int64_t*, int, int, int, int, float*, float*, float*,
                        hipStream_t);
@@ -410,14 +412,16 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("conv_stats_rows", &dtf_conv_stats_rows, py::arg("M"), py::arg("Kout"), py::arg("C") = 0,
         py::arg("taps") = 1, py::arg("W") = 0);
   m.def("conv_set_halo", &dtf_conv_set_halo);
-  m.def("conv_tile_rows", [](std::vector<int> geom, std::vector<int> dh, std::vector<int> dw) {
+  m.def("conv_tile_rows", [](std::vector<int> geom, std::vector<int> dh, std::vector<int> dw,
+                             int bnb) {
     if (geom.size() != 16 && geom.size() != 17)
       throw std::runtime_error("conv_tile_rows: geom needs 16 (+acc) ints");
     ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
                geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15],
                geom.size() == 17 ? geom[16] : 0};
-    return dtf_conv_tile_rows(g, make_taps<TapTable>(dh, dw));
-  });
+    return dtf_conv_tile_rows(g, make_taps<TapTable>(dh, dw), bnb);
+  }, py::arg("geom"), py::arg("dh"), py::arg("dw"), py::arg("bnb") = 0);
+  m.def("conv_set_halo_bnb", &dtf_conv_set_halo_bnb);
   m.def("conv_set_dma_mode", &dtf_conv_set_dma_mode);
   m.def("filter_transpose", [](std::vector<uintptr_t> src, std::vector<uintptr_t> dst,
                                std::vector<int> K, std::vector<int> T, std::vector<int> C,
@@ -851,6 +855,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
      py::arg("scale"), py::arg("p"), py::arg("seed"), py::arg("st"), py::arg("colpart") = 0);
   m.def("attn_bwd_fused", &dtf_attn_bwd_fused);
   m.def("attn_set_wide", &dtf_attn_set_wide);
+  m.def("attn_set_fwd_occ", &dtf_attn_set_fwd_occ);
   m.def("attn_set_fused", &dtf_attn_set_fused);
   m.def("pos_type_grad_ws_floats", &dtf_pos_type_grad_ws_floats);
   m.def("pos_type_grad", [](uintptr_t ds, uintptr_t tt, int B, int S_, int H, int NT,

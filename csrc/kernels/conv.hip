@@ -836,11 +836,17 @@ DTF_DEV int halo_swz(int u) { return C == 64 ? (((u >> 1) & 3) << 1) : ((u & 7) 
 // was issued only one step earlier (~190 ns of MFMA cover against an L2 round trip several times
 // that).  LDS holds only the patch: 44-46 KB per block instead of 60-78 KB, which leaves room for
 // a third block per CU.  The MFMA order is unchanged, so the outputs are bit-identical.
-template <int C, int W, int WMW, int NT, int ST = 1, bool FREG = false>
+//
+// BNB (a data gradient whose output feeds a BatchNorm(+ReLU) backward -- the c2 data gradient of a
+// bottleneck, consumed by BN1): the epilogue also forms that BN's backward partial sums
+// (sum dz, sum dz * xhat, dz = dy masked by the forward ReLU) per output channel, one slab row
+// per block (BnbAcc, the contract of conv_igemm_kernel's BNB epilogue).  The BN input x is loaded
+// for the thread's output rows before the tile is staged, so its latency hides under the staging.
+template <int C, int W, int WMW, int NT, int ST = 1, bool FREG = false, bool BNB = false>
 __global__ void __launch_bounds__(kThreads * ST, ST == 1 ? 2 : 1)
 conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                     bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
-                    float* __restrict__ stats) {
+                    float* __restrict__ stats, const BnBwdEpi bnb) {
   using H = HaloCfg<C, W, WMW, NT>;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   const int tid = threadIdx.x & (kThreads - 1), lane = tid & 63;   // tid within the strip
@@ -998,6 +1004,24 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   DTF_WAIT_VM(0);
   __syncthreads();
   // ---- epilogue: bf16 tile [M][NT + 8] in LDS (over the patch) -> 16-B stores; BN partials
+  constexpr int OCPR = NT / 8;
+  constexpr int OROWS = kThreads / OCPR;                         // rows per store pass
+  constexpr int NR = H::M / OROWS;                               // store passes
+  static_assert(H::M % OROWS == 0, "halo epilogue rows");
+  const long ybase = ((long)n * g.H + h0) * g.W;                 // first output pixel of the tile
+  const int oc = tid % OCPR;
+  const bool col_ok = n0 + oc * 8 < g.Kout;
+  uint4 xpre[BNB ? NR : 1];
+  uint32_t mpre[BNB ? NR : 1];
+  if constexpr (BNB) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const long off = (ybase + tid / OCPR + k * OROWS) * g.Kout + n0 + oc * 8;
+      const bool ok = live && col_ok;
+      xpre[k] = ok ? *reinterpret_cast<const uint4*>(bnb.x + off) : make_uint4(0, 0, 0, 0);
+      mpre[k] = (ok && bnb.mkind == 1) ? (uint32_t)bnb.mask[off >> 3] : 0u;
+    }
+  }
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -1012,14 +1036,21 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
         st[(wm * (H::MF * 16) + 16 * i + fq * 4 + r) * LDC + wn * (H::NF * 16) + 16 * j + frow] =
             f2bf(acc[i][j][r]);
   __syncthreads();
-  const long ybase = ((long)n * g.H + h0) * g.W;                 // first output pixel of the tile
-  constexpr int OCPR = NT / 8;
-  const int oc = tid % OCPR;
-  const bool col_ok = n0 + oc * 8 < g.Kout;
-  for (int r = tid / OCPR; r < H::M; r += kThreads / OCPR) {
+  BnbAcc ba;
+  if constexpr (BNB) ba.init(bnb, n0 + oc * 8, col_ok);
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const int r = tid / OCPR + k * OROWS;
     if (!col_ok || !live) continue;
-    st16(Y + (ybase + r) * g.Kout + n0 + oc * 8,
-         *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8), g.nt);
+    const uint4 v = *reinterpret_cast<const uint4*>(st + r * LDC + oc * 8);
+    st16(Y + (ybase + r) * g.Kout + n0 + oc * 8, v, g.nt);
+    if constexpr (BNB) ba.add_pre(bnb, v, xpre[k], mpre[k]);
+  }
+  if constexpr (BNB) {
+    // dead strips (odd tail) add nothing but still write their (zero) slab row: every row of the
+    // slab the BN finalize sums is defined
+    ba.template flush<NT, kThreads>(bnb, reinterpret_cast<float*>(st + H::M * LDC), tid / OCPR,
+                                    oc, OROWS, tid, tm, n0, g.Kout);
   }
   if (stats) {   // per-channel sum / sum of squares of the rounded outputs -> slab row tm
     constexpr int GROUPS = kThreads / NT;
@@ -1230,8 +1261,26 @@ static int g_halo_freg = 0;
 void dtf_conv_set_halo_freg(int v) { g_halo_freg = v; }
 template <int C, int W, int WMW, int NT>
 static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
-                        const TapTable& taps, float* stats, int tiles, int strips, hipStream_t st) {
+                        const TapTable& taps, float* stats, const BnBwdEpi& bnb, int tiles,
+                        int strips, hipStream_t st) {
   using Hc = HaloCfg<C, W, WMW, NT>;
+  if (bnb.part) {
+    // one strip per block; the BN-backward reduction scratch [OROWS][2][NT] fp32 sits past the
+    // staged tile (in the dead filter ring, or past the patch with FREG)
+    constexpr size_t scratch = (size_t)Hc::M * Hc::LDC * 2 + (size_t)(kThreads / (NT / 8)) * 2 * NT * 4;
+    const bool freg = (g_halo_freg & (C == 64 ? 1 : 2)) != 0;
+    const size_t base = freg ? Hc::LDS_FREG : Hc::lds(1);
+    const size_t lds = base > scratch ? base : scratch;
+    if (freg)
+      hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 1, true, true>),
+                         dim3((unsigned)tiles, g.Kout / NT), dim3(kThreads), lds, st, X, Wt, Y, g,
+                         taps, stats, bnb);
+    else
+      hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 1, false, true>),
+                         dim3((unsigned)tiles, g.Kout / NT), dim3(kThreads), lds, st, X, Wt, Y, g,
+                         taps, stats, bnb);
+    return;
+  }
   if (strips == 2) {
     static bool attr = false;
     if (!attr) {
@@ -1241,14 +1290,14 @@ static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const Conv
     }
     hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 2>),
                        dim3((unsigned)((tiles + 1) / 2), g.Kout / NT), dim3(2 * kThreads), Hc::lds(2),
-                       st, X, Wt, Y, g, taps, stats);
+                       st, X, Wt, Y, g, taps, stats, bnb);
   } else if (g_halo_freg & (C == 64 ? 1 : 2)) {
     hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 1, true>),
                        dim3((unsigned)tiles, g.Kout / NT), dim3(kThreads), Hc::LDS_FREG, st, X, Wt,
-                       Y, g, taps, stats);
+                       Y, g, taps, stats, bnb);
   } else {
     hipLaunchKernelGGL((conv3x3_halo_kernel<C, W, WMW, NT, 1>), dim3((unsigned)tiles, g.Kout / NT),
-                       dim3(kThreads), Hc::lds(1), st, X, Wt, Y, g, taps, stats);
+                       dim3(kThreads), Hc::lds(1), st, X, Wt, Y, g, taps, stats, bnb);
   }
 }
 
@@ -1266,8 +1315,11 @@ static bool use_stem_halo(const ConvGeom& g, const TapTable& taps) {
   return true;
 }
 
-// M tiles of a launch WITHOUT the halo kernel (the fused-BN-backward dgrad path, which never
-// takes it); W is accepted for API symmetry and ignored
+// the halo kernels also take the fused-BN-backward (BNB) data gradients (A/B knob)
+static int g_halo_bnb = 1;
+void dtf_conv_set_halo_bnb(int v) { g_halo_bnb = v; }
+
+// M tiles of a launch WITHOUT the halo kernel; W is accepted for API symmetry and ignored
 int dtf_conv_stats_rows(long M, int Kout, int C, int taps, int W) {
   (void)W;
   const int BM = use_dma_kernel(M, Kout, C, taps, 64) ? kDmaBM : (Kout <= 64 ? 256 : 128);
@@ -1298,7 +1350,12 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
 
 // M tiles (= BN-statistics slab rows) of exactly the kernel dtf_conv_igemm will pick for this
 // forward launch (no fused BN-backward epilogue)
-int dtf_conv_tile_rows(const ConvGeom& g, const TapTable& taps) {
+int dtf_conv_tile_rows(const ConvGeom& g, const TapTable& taps, int bnb) {
+  if (bnb) {   // a fused-BN-backward data gradient (the dispatch of dtf_conv_igemm with bnb.part)
+    if (g.C % 32 == 0 && !g.bias && !g.relu && use_halo(g, taps) && g_halo_bnb)
+      return g.N * (g.H / kHaloTH);
+    return dtf_conv_stats_rows((long)g.N * g.P * g.Q, g.Kout, g.C, taps.n, 0);
+  }
   if (use_conv_gemm(g, taps)) return (int)(((long)g.N * g.P * g.Q + 255) / 256);
   if (g.C % 32 == 0 && use_halo(g, taps)) return g.N * (g.H / kHaloTH);
   if (use_stem_halo(g, taps)) return g.N * (g.P / kStemTH);
@@ -1361,11 +1418,13 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
                   g.acc == 2 ? g.acc_mask : nullptr, st);
     return;
   }
-  if (!bnb.part && !epi && use_halo(g, taps)) {
+  if (!epi && use_halo(g, taps) && (!bnb.part || (g_halo_bnb && !stats))) {
     const int fam = halo_family(g, taps);
     const int tiles = g.N * (g.H / kHaloTH);
-    if (fam == 1) launch_halo<64, 56, 2, 64>(X, Wt, Y, g, taps, stats, tiles, (g_halo_st & 1) ? 2 : 1, st);
-    else launch_halo<128, 28, 1, 128>(X, Wt, Y, g, taps, stats, tiles, (g_halo_st & 2) ? 2 : 1, st);
+    if (fam == 1)
+      launch_halo<64, 56, 2, 64>(X, Wt, Y, g, taps, stats, bnb, tiles, (g_halo_st & 1) ? 2 : 1, st);
+    else
+      launch_halo<128, 28, 1, 128>(X, Wt, Y, g, taps, stats, bnb, tiles, (g_halo_st & 2) ? 2 : 1, st);
     return;
   }
   if (!epi && use_dma_kernel((long)m, g.Kout, g.C, taps.n, bk) && g.Kpad % 64 == 0) {

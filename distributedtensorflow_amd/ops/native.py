@@ -286,8 +286,11 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_f
     part, row0 = None, 0
     if bnb is not None:
         xb, stats, mask, relu, has_res, tok = bnb
-        rows = [_K.conv_stats_rows(n * Pc * Qc, C, K, len(taps))
-                for (_, _, Pc, Qc, taps, _) in launches]
+        # slab rows of exactly the kernel each launch takes (the halo kernels: one per block)
+        rows = [_K.conv_tile_rows(_fwd_geom(dyc.shape, C, taps, Pc, Qc, 1, 1, h, wd, sh, sw, a, b,
+                                            acc),
+                                  [t[0] for t in taps], [t[1] for t in taps], 1)
+                for (a, b, Pc, Qc, taps, _) in launches]
         G = sum(rows)
         part = torch.empty(_K.bn_workspace_floats_g(G, C), device=dy.device, dtype=torch.float32)
         mkind = (1 if has_res else 2) if relu else 0
@@ -466,7 +469,15 @@ class _Conv2d(torch.autograd.Function):
         stream_bnb = (_FUSE_BN_BWD_STREAM and _gemm_1x1(K_, xb.shape[-1], R_, S_, stride,
                                                         (pads[0], pads[2]))
                       and _stream_bnb_ok(K_, xb.shape[-1]))
-        ctx.bnb = bnb if ((_FUSE_BN_BWD or stream_bnb) and bnb is not None and xb is x) else None
+        halo_bnb = (_FUSE_BN_BWD_HALO and (R_, S_) == (3, 3) and tuple(_pair(stride)) == (1, 1)
+                    and tuple(pads) == (1, 1, 1, 1)
+                    and _halo_dgrad_shape(K_, xb.shape[-1], xb.shape[1], xb.shape[2]))
+        # stride-2 3x3 data gradients (the first block of stages 2-4) run at 0.25-0.34 of the MFMA
+        # roof: the BN-sum epilogue's extra read of x fits under them (A/B knob)
+        s2_bnb = (_FUSE_BN_BWD_S2 and (R_, S_) == (3, 3) and tuple(_pair(stride)) == (2, 2)
+                  and xb.shape[-1] % 32 == 0)
+        ctx.bnb = bnb if ((_FUSE_BN_BWD or stream_bnb or halo_bnb or s2_bnb) and bnb is not None
+                          and xb is x) else None
         dual = getattr(x, "_dtf_bnb_dual", None)
         if dual is not None and stream_bnb and ctx.bnb is None and xb is x:
             ctx.bnb = _DualBnb(*dual)
@@ -618,6 +629,19 @@ _FUSE_BN_BWD = os.environ.get("DTF_FUSE_BN_BWD", "0") == "1"
 # there the gradient is still in registers, the epilogue reads only x (prefetched one chunk
 # ahead, streaming), and the reduce pass's re-read of dy and the mask disappears
 _FUSE_BN_BWD_STREAM = os.environ.get("DTF_FUSE_BN_BWD_STREAM", "1") == "1"
+
+
+# ... and where it runs on the 3x3 halo kernels (stage-1/2 c2 data gradients -> BN1): the
+# epilogue loads x under the tile staging, and the BN1 reduce pass (a re-read of dy and x) goes
+_FUSE_BN_BWD_HALO = os.environ.get("DTF_FUSE_BN_BWD_HALO", "1") == "1"
+_FUSE_BN_BWD_S2 = os.environ.get("DTF_FUSE_BN_BWD_S2", "0") == "1"
+
+
+def _halo_dgrad_shape(K, C, H, W):
+    """The data gradient of a 3x3 stride-1 'same' conv C -> K runs on a halo kernel family
+    (csrc/kernels/conv.hip halo_family: 56 x 56 x 64 or 28 x 28 x 128 input to the dgrad)."""
+    return H % 4 == 0 and ((K == 64 and W == 56 and C % 64 == 0) or
+                           (K == 128 and W == 28 and C % 128 == 0))
 
 
 def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):

@@ -29,7 +29,9 @@ def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False, lazy=True):
     prev, prev_r, prev_s = native._DIRECT_GRAD, native._FUSE_RESIDUAL_GRAD, native._SHARE_INPUT_GRAD
     prev_b, prev_l = native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD
     prev_bs, prev_c1 = native._FUSE_BN_BWD_STREAM, native._FUSE_C1_BWD
-    prev_d = native._FUSE_DUAL_BNB
+    prev_d, prev_h = native._FUSE_DUAL_BNB, native._FUSE_BN_BWD_HALO
+    prev_s2 = native._FUSE_BN_BWD_S2
+    native._FUSE_BN_BWD_HALO = native._FUSE_BN_BWD_S2 = fuse_bnb
     native._FUSE_BN_BWD = fuse_bnb
     native._FUSE_BN_BWD_STREAM = fuse_bnb
     native._FUSE_C1_BWD = fuse_bnb
@@ -51,7 +53,8 @@ def _grads(model, direct, fuse_res=True, share=True, fuse_bnb=False, lazy=True):
         native._SHARE_INPUT_GRAD = prev_s
         native._FUSE_BN_BWD, native._LAZY_RESIDUAL_GRAD = prev_b, prev_l
         native._FUSE_BN_BWD_STREAM, native._FUSE_C1_BWD = prev_bs, prev_c1
-        native._FUSE_DUAL_BNB = prev_d
+        native._FUSE_DUAL_BNB, native._FUSE_BN_BWD_HALO = prev_d, prev_h
+        native._FUSE_BN_BWD_S2 = prev_s2
 
 
 def test_direct_grad_path_bit_identical():
@@ -457,6 +460,59 @@ def _default_step_grads(model, dual):
             return loss.item(), opt.space.grad.clone()
     finally:
         native._FUSE_DUAL_BNB = prev
+
+
+@pytest.mark.parametrize("H,C,res", [(56, 64, False), (56, 64, True), (28, 128, False)])
+def test_bn_backward_sums_fused_into_halo_dgrad(H, C, res):
+    """conv -> BN(+res)(+ReLU) -> 3x3 conv on a halo-kernel shape (56 x 56 x 64, 28 x 28 x 128):
+    the halo data-gradient kernel's epilogue emits the BN backward sums (ReLU recomputed from x,
+    or the residual bit mask); every gradient matches the separate reduce pass to fp32
+    summation-order noise, the data gradient itself bit for bit, and the halo kernel took it."""
+    torch.manual_seed(0)
+    N = 2
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w1 = torch.randn(C, 3, 3, C, device="cuda") / (9 * C) ** 0.5
+    w2 = torch.randn(C, 3, 3, C, device="cuda") / (9 * C) ** 0.5
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.randn(C, device="cuda") * 0.1
+    r = torch.randn(N, H, H, C, device="cuda").bfloat16() if res else None
+    taps = [(1 - i // 3, 1 - i % 3) for i in range(9)]
+    geom = native._fwd_geom((N, H, H, C), C, taps, H, H, 1, 1, H, H)
+    assert native._K.conv_tile_rows(geom, [t[0] for t in taps], [t[1] for t in taps], 1) == \
+        N * H // 4, "the fused-sum data gradient would not run on the halo kernel"
+    outs, seen = [], {}
+    prev = native._FUSE_BN_BWD, native._FUSE_BN_BWD_HALO
+    orig = native._K.bn_bwd_finalize_g
+
+    def spy(*a):
+        seen["g"] = True
+        return orig(*a)
+    try:
+        native._FUSE_BN_BWD = False
+        for fuse in (True, False):
+            native._FUSE_BN_BWD_HALO = fuse
+            ps = [t.clone().requires_grad_(True) for t in (x.float(), w1, w2, gamma, beta)]
+            xi = ps[0].detach().bfloat16().requires_grad_(True)
+            y1 = native.conv2d(xi, ps[1], 1, 1, bn_stats=True)
+            z = native.batch_norm(y1, ps[3], ps[4], None, None, True, 0.9, 1e-5, relu=True,
+                                  residual=r)
+            z.retain_grad()
+            y2 = native.conv2d(z, ps[2], 1, 1)
+            g = torch.randn(y2.shape, device="cuda", generator=torch.Generator(
+                device="cuda").manual_seed(1)).bfloat16()
+            if fuse:
+                native._K.bn_bwd_finalize_g = spy
+            y2.backward(g)
+            native._K.bn_bwd_finalize_g = orig
+            outs.append((z.grad.float(), xi.grad.float(), ps[1].grad, ps[3].grad, ps[4].grad))
+    finally:
+        native._FUSE_BN_BWD, native._FUSE_BN_BWD_HALO = prev
+        native._K.bn_bwd_finalize_g = orig
+    assert seen.get("g"), "fused BN-backward path did not run"
+    assert torch.equal(outs[0][0], outs[1][0])          # the data gradient itself: same kernel
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        rel = ((a - b).norm() / b.norm()).item()
+        assert rel < 2e-2, rel
 
 
 def test_dual_bn_sums_from_streamed_dgrad():
