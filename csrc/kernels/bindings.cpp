@@ -188,7 +188,6 @@ void dtf_attn_bwd(const bf16_t*, const float*, const bf16_t*, const bf16_t*, con
 int dtf_attn_bwd_fused(int);
 int dtf_pos_type_grad_ws_floats(int, int, int);
 void dtf_attn_set_wide(int);
-void dtf_attn_set_fwd_occ(int);
 void dtf_attn_set_fused(int);
 void dtf_pos_type_grad(const bf16_t*, const int64_t*, int, int, int, int, float*, float*, float*,
                        hipStream_t);
@@ -855,7 +854,6 @@ PYBIND11_MODULE(_dtf_hip, m) {
      py::arg("scale"), py::arg("p"), py::arg("seed"), py::arg("st"), py::arg("colpart") = 0);
   m.def("attn_bwd_fused", &dtf_attn_bwd_fused);
   m.def("attn_set_wide", &dtf_attn_set_wide);
-  m.def("attn_set_fwd_occ", &dtf_attn_set_fwd_occ);
   m.def("attn_set_fused", &dtf_attn_set_fused);
   m.def("pos_type_grad_ws_floats", &dtf_pos_type_grad_ws_floats);
   m.def("pos_type_grad", [](uintptr_t ds, uintptr_t tt, int B, int S_, int H, int NT,

@@ -774,11 +774,8 @@ DTF_DEV void load_two_tiles(bf16_t* d0, const bf16_t* s0, long ld0, bf16_t* d1, 
 // Launch shapes: NW waves x 16 rows per block, K/V (or Q/dO) staged CH rows at a time.  <8, 128>
 // (S % 128 == 0, e.g. BERT's 128) covers a whole 128-token sequence per block, so each (b, h)
 // reads its K/V once instead of once per 64-query block and syncs once per 128 keys.
-// OCC > 0: ask for OCC waves per SIMD (the 8-wave block otherwise takes 120 VGPRs: two blocks
-// per CU, each waiting out its own K/V loads; 6 -> three blocks per CU) and keep the key-chunk loop
-// rolled so the smaller register budget holds
-template <bool DROP, int NW, int CH, int OCC = 0>
-__global__ void __launch_bounds__(64 * NW, OCC > 0 ? OCC : 1)
+template <bool DROP, int NW, int CH>
+__global__ void __launch_bounds__(64 * NW)
 attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                 bf16_t* __restrict__ out, float* __restrict__ lse, const AttnGeom g) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[CH * ALD];
@@ -804,7 +801,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                 Vs, qkv + (tok0 + kc) * g.ld + (2 * H + h) * AD, g.ld, tid);
     if (tid < CH) Ms[tid] = mask ? mask[tok0 + kc + tid] * kLog2e : 0.f;
     __syncthreads();
-#pragma unroll (OCC > 0 ? 1 : CH / 64)
+#pragma unroll
     for (int sub = 0; sub < CH; sub += 64) {
       const bf16_t* Kb = Ks + sub * ALD;
       const bf16_t* Vb = Vs + sub * ALD;
@@ -1456,27 +1453,18 @@ static AttnGeom attn_geom(int B, int S, int H, float scale, float p, uint32_t se
 static int g_attn_wide = 1;
 void dtf_attn_set_wide(int v) { g_attn_wide = v; }
 
-// forward occupancy request (attn_fwd_kernel OCC; A/B knob): 0 = compiler's choice
-static int g_attn_fwd_occ = 0;
-void dtf_attn_set_fwd_occ(int v) { g_attn_fwd_occ = v; }
-
-template <int NW, int CH, int OCC>
-static void attn_fwd_launch_occ(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse,
-                                const AttnGeom& g, hipStream_t st) {
-  const dim3 grid(g.S / (16 * NW), g.H, g.B);
-  if (g.thr)
-    hipLaunchKernelGGL((attn_fwd_kernel<true, NW, CH, OCC>), grid, dim3(64 * NW), 0, st, qkv,
-                       mask, out, lse, g);
-  else
-    hipLaunchKernelGGL((attn_fwd_kernel<false, NW, CH, OCC>), grid, dim3(64 * NW), 0, st, qkv,
-                       mask, out, lse, g);
-}
+// (the 8-wave forward takes 120 VGPRs: two blocks per CU; forcing 6 or 8 waves per SIMD spills
+// and is 13-39 % slower with dropout, profiles/measurements/r4_attention_fwd_occupancy.jsonl)
 template <int NW, int CH>
 static void attn_fwd_launch(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse,
                             const AttnGeom& g, hipStream_t st) {
-  if (g_attn_fwd_occ == 6) attn_fwd_launch_occ<NW, CH, 6>(qkv, mask, out, lse, g, st);
-  else if (g_attn_fwd_occ == 8) attn_fwd_launch_occ<NW, CH, 8>(qkv, mask, out, lse, g, st);
-  else attn_fwd_launch_occ<NW, CH, 0>(qkv, mask, out, lse, g, st);
+  const dim3 grid(g.S / (16 * NW), g.H, g.B);
+  if (g.thr)
+    hipLaunchKernelGGL((attn_fwd_kernel<true, NW, CH>), grid, dim3(64 * NW), 0, st, qkv, mask,
+                       out, lse, g);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<false, NW, CH>), grid, dim3(64 * NW), 0, st, qkv, mask,
+                       out, lse, g);
 }
 
 // dK/dV always runs the 4-wave shape: its 8-wave build needs 167 VGPRs with dropout (one block

@@ -23,8 +23,6 @@ AD = 64   # attention head dim supported by the MFMA kernels
 _RESIDUAL_TO_DENSE = os.environ.get("DTF_RESIDUAL_TO_DENSE", "1") == "1"
 if os.environ.get("DTF_ATTN_WIDE"):
     _K.attn_set_wide(int(os.environ["DTF_ATTN_WIDE"]))
-if os.environ.get("DTF_ATTN_FWD_OCC"):      # attention forward waves/SIMD request (0 / 6 / 8)
-    _K.attn_set_fwd_occ(int(os.environ["DTF_ATTN_FWD_OCC"]))
 if os.environ.get("DTF_LN_WIDE"):          # 0: the 8-B-per-lane LayerNorm kernels
     _K.ln_set_wide(int(os.environ["DTF_LN_WIDE"]))
 if os.environ.get("DTF_ATTN_FUSED_BWD"):      # 0: the split dQ + dK/dV backward at S == 128

@@ -35,10 +35,7 @@ def main():
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--heads", type=int, default=12)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--fwd-occ", type=int, default=0,
-                    help="attention forward waves/SIMD request (attn_set_fwd_occ: 0, 6, 8)")
     a = ap.parse_args()
-    _K.attn_set_fwd_occ(a.fwd_occ)
     B, S, H, D = a.batch, a.seq, a.heads, 64
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -61,8 +58,7 @@ def main():
                                   scale, p, 1234, st())
         tf = timeit(fwd, a.iters)
         tb = timeit(bwd, a.iters)
-        rec = {"probe": "attn", "B": B, "S": S, "H": H, "dropout": p, "fwd_occ": a.fwd_occ,
-               "fwd_ms": round(tf, 4),
+        rec = {"probe": "attn", "B": B, "S": S, "H": H, "dropout": p, "fwd_ms": round(tf, 4),
                "bwd_ms": round(tb, 4), "fwd_tflops": round(flops_f / tf / 1e9, 1),
                "bwd_tflops": round(2.5 * flops_f / tb / 1e9, 1)}
         if p == 0.0:
