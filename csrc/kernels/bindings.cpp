@@ -204,7 +204,6 @@ void dtf_gemm_nt(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int,
                  const uint8_t*);
 int dtf_gemm_tile_rows(int);
 void dtf_gemm_set_variant(int);
-void dtf_gemm_set_gelu_pre(int);
 void dtf_gemm_set_pp(int);
 int dtf_bias_relu_bwd_ws_floats(int);
 void dtf_gather_u8_scale(const uint8_t*, const int64_t*, void*, int, int, float, int, hipStream_t);
@@ -340,7 +339,6 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("gemm_tile_rows", &dtf_gemm_tile_rows);
   m.def("gemm_set_variant", &dtf_gemm_set_variant);
-  m.def("gemm_set_gelu_pre", &dtf_gemm_set_gelu_pre);
   m.def("gemm_set_pp", &dtf_gemm_set_pp);
   m.def("bias_relu_bwd_ws_floats", &dtf_bias_relu_bwd_ws_floats);
   m.def("gather_u8_scale", [](uintptr_t images, uintptr_t idx, uintptr_t out, int B, int D,

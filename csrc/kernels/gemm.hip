@@ -54,7 +54,6 @@ struct GemmArgs {
   const bf16_t* gelu_a;
   const float* gelu_b;
   float* colsum;
-  int gelu_pre;                     // 1: the epilogue loads its extra input rows before the stores
   int ncu;                          // OCC 2 kernels: compute units (the first resident round)
   int group_m;                      // > 0: grouped tile order (GM M-panels x all N per group)
   int stagger_mode, stagger;        // OCC 2: which first-round blocks start late, by how much
@@ -611,41 +610,6 @@ gemm_nt_kernel(const GemmArgs g) {
           s2[j] += q * q;
         }
       }
-  constexpr int OCPR = BN / 8;                 // 16-B chunks per output row
-  constexpr int OROWS = Cf::NT / OCPR;
-  constexpr int NPASS = BM / OROWS;
-  const int oc = tid % OCPR;
-  const bool col_ok = n0 + oc * 8 < g.N;
-  // The epilogue's extra input (the GELU-backward's saved input, the accumulate source, or the
-  // masked residual gradient + its mask byte) for every row of this thread, loaded now -- the
-  // accumulators are staged, their registers free -- so the loads fly under the staging barrier
-  // instead of a few at a time inside the store loop (output rows = tile rows: dense GEMMs and
-  // unit-stride convs)
-  // (the implicit-GEMM conv kernels keep their tap state through the epilogue: with these
-  // registers on top they spilled, so they keep the in-loop loads)
-#ifdef DTF_GEMM_EPI_LEGACY   // experiment builds only: the round-3 epilogue (loads in the store loop)
-  constexpr bool PRE_OK = false;
-#else
-  constexpr bool PRE_OK = !CONV;
-#endif
-  const bf16_t* const pre_src = g.gelu_a ? g.gelu_a : g.Cin ? g.Cin : g.acc_mask ? g.acc_src : nullptr;
-  const bool pre = PRE_OK && pre_src && g.gelu_pre;
-  uint4 gpre[PRE_OK ? NPASS : 1];
-  uint32_t mpre[PRE_OK ? (NPASS + 3) / 4 : 1];
-  if constexpr (PRE_OK) {
-   if (pre) {
-#pragma unroll
-    for (int k = 0; k < (NPASS + 3) / 4; ++k) mpre[k] = 0u;
-#pragma unroll
-    for (int k = 0; k < NPASS; ++k) {
-      const int r = tid / OCPR + k * OROWS;
-      const bool ok = col_ok && m0 + r < g.M;
-      const long off = (long)(m0 + r) * g.ldc + n0 + oc * 8;
-      gpre[k] = ok ? *reinterpret_cast<const uint4*>(pre_src + off) : make_uint4(0u, 0u, 0u, 0u);
-      if (ok && !g.gelu_a && !g.Cin) mpre[k >> 2] |= (uint32_t)g.acc_mask[off >> 3] << (8 * (k & 3));
-    }
-   }
-  }
   if (do_stats) {
 #pragma unroll
     for (int j = 0; j < Cf::FN; ++j) {
@@ -674,14 +638,18 @@ gemm_nt_kernel(const GemmArgs g) {
     g.stats[((long)tm * 2 + 0) * g.N + n0 + tid] = a;
     g.stats[((long)tm * 2 + 1) * g.N + n0 + tid] = b;
   }
+  constexpr int OCPR = BN / 8;                 // 16-B chunks per output row
+  constexpr int OROWS = Cf::NT / OCPR;
+  const int oc = tid % OCPR;
+  const bool col_ok = n0 + oc * 8 < g.N;
   float gb[8], cs[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     gb[e] = (g.gelu_b && col_ok) ? g.gelu_b[n0 + oc * 8 + e] : 0.f;
     cs[e] = 0.f;
   }
-#pragma unroll (PRE_OK ? NPASS : 4)
-  for (int k = 0; k < NPASS; ++k) {
+#pragma unroll 4
+  for (int k = 0; k < BM / OROWS; ++k) {
     const int r = tid / OCPR + k * OROWS;
     if (!col_ok || m0 + r >= g.M) continue;
     uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::LDC + oc * 8);
@@ -698,23 +666,22 @@ gemm_nt_kernel(const GemmArgs g) {
     if (g.Cin) {
       float a[8], b[8];
       unpack8(v, a);
-      unpack8(pre ? gpre[PRE_OK ? k : 0] : *reinterpret_cast<const uint4*>(g.Cin + off), b);
+      unpack8(*reinterpret_cast<const uint4*>(g.Cin + off), b);
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += b[e];
       v = pack8(a);
     } else if (g.acc_mask) {
       float a[8], b[8];
       unpack8(v, a);
-      unpack8(pre ? gpre[PRE_OK ? k : 0] : *reinterpret_cast<const uint4*>(g.acc_src + off), b);
-      const uint32_t mb = pre ? (mpre[PRE_OK ? k >> 2 : 0] >> (8 * (k & 3))) & 0xFFu
-                              : g.acc_mask[off >> 3];
+      unpack8(*reinterpret_cast<const uint4*>(g.acc_src + off), b);
+      const uint32_t mb = g.acc_mask[off >> 3];
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += (mb >> e) & 1u ? b[e] : 0.f;
       v = pack8(a);
     } else if (g.gelu_a) {
       float d[8], a[8];
       unpack8(v, d);
-      unpack8(pre ? gpre[PRE_OK ? k : 0] : *reinterpret_cast<const uint4*>(g.gelu_a + off), a);
+      unpack8(*reinterpret_cast<const uint4*>(g.gelu_a + off), a);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         d[e] *= gelu_grad(a[e] + gb[e]);
@@ -1192,8 +1159,6 @@ void launch_gemm(const GemmArgs& g0, hipStream_t st) {
 void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
 void dtf_gemm_set_stream(int v) { g_gemm_stream = v; }
 void dtf_gemm_set_pp(int v) { g_gemm_pp = v; }
-static int g_gemm_gelu_pre = 1;   // epilogue extra-input loads up front (A/B knob, bit 0)
-void dtf_gemm_set_gelu_pre(int v) { g_gemm_gelu_pre = v; }
 void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
 void dtf_gemm_set_dbg(int v) { g_gemm_dbg = v; }
 void dtf_gemm_set_stagger(int mode, int iters) { g_gemm_stagger_mode = mode; g_gemm_stagger = iters; }
@@ -1222,7 +1187,6 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
   for (int t = 0; t < ntaps; ++t) { g.tdh[t] = dh[t]; g.tdw[t] = dw[t]; }
   g.Ho = Ho; g.Wo = Wo; g.osh = osh; g.osw = osw; g.oh0 = oh0; g.ow0 = ow0;
   g.nt = g_gemm_nt;
-  g.gelu_pre = g_gemm_gelu_pre;
   if ((osh != 1 || osw != 1) && (stats || acc_mask))
     throw std::runtime_error("gemm_conv: strided outputs take no BN statistics / masked acc");
   if ((long)256 * g.ldb * 2 + 2L * g.K >= (1L << 31))
@@ -1248,7 +1212,6 @@ void dtf_gemm_nt_gelu_bwd(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, in
   GemmArgs g{};
   g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = N;
   g.gelu_a = gelu_a; g.gelu_b = gelu_b; g.colsum = colsum;
-  g.gelu_pre = g_gemm_gelu_pre;
   g.nt = g_gemm_nt;
   if (N <= 128) launch_gemm<256, 128, 64, 3>(g, st);
   else launch_gemm<256, 256, 64, 2, 2>(g, st);
@@ -1287,7 +1250,6 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
   GemmArgs g{A, B, C, bias, Cin, M, N, K, lda, ldb, ldc, relu, stats, acc_src, acc_mask};
   g.nt = g_gemm_nt;
   g.dbg = g_gemm_dbg;
-  g.gelu_pre = g_gemm_gelu_pre;
   // auto: 256 x 128 tiles when N <= 128 (measured 1.02-1.07x the 256 x 256 tile on the N = 128
   // ResNet 1x1 convs, profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl)
   const int variant = g_gemm_variant >= 0 ? g_gemm_variant

@@ -56,8 +56,6 @@ if os.environ.get("DTF_CONV_SMALL_K"):
     _K.conv_set_small_k(int(os.environ["DTF_CONV_SMALL_K"]))
 if os.environ.get("DTF_GEMM_STREAM"):   # row-streaming GEMM for output-heavy shapes (default on)
     _K.gemm_set_stream(int(os.environ["DTF_GEMM_STREAM"]))
-if os.environ.get("DTF_GEMM_GELU_PRE"):  # GELU-backward GEMM epilogue loads up front (default 1)
-    _K.gemm_set_gelu_pre(int(os.environ["DTF_GEMM_GELU_PRE"]))
 if os.environ.get("DTF_C1_W16"):        # stage-0 fused c3 backward as 16-wave blocks (default 0)
     _K.conv1x1_bwd_set_w16(int(os.environ["DTF_C1_W16"]))
 if os.environ.get("DTF_GEMM_GROUP_M"):  # grouped tile order of the dense GEMMs (0: N fastest)
