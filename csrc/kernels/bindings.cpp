@@ -182,9 +182,12 @@ void dtf_conv1x1_bwd(const bf16_t*, const bf16_t*, const bf16_t*, const bf16_t*,
 void dtf_bias_gelu_bwd(const bf16_t*, const bf16_t*, const float*, bf16_t*, float*, float*, int,
                        int, hipStream_t, int);
 void dtf_attn_fwd(const bf16_t*, const float*, bf16_t*, float*, int, int, int, float, float,
-                  uint32_t, hipStream_t);
+                  uint32_t, hipStream_t, uint32_t*);
+long dtf_attn_keep_words(int, int, int, float);
+void dtf_attn_set_keep(int);
 void dtf_attn_bwd(const bf16_t*, const float*, const bf16_t*, const bf16_t*, const float*, float*,
-                  bf16_t*, int, int, int, float, float, uint32_t, hipStream_t, float*);
+                  bf16_t*, int, int, int, float, float, uint32_t, hipStream_t, float*,
+                  const uint32_t*);
 int dtf_attn_bwd_fused(int);
 int dtf_pos_type_grad_ws_floats(int, int, int);
 void dtf_attn_set_wide(int);
@@ -837,21 +840,27 @@ PYBIND11_MODULE(_dtf_hip, m) {
   }, py::arg("dy"), py::arg("a"), py::arg("bias"), py::arg("da"), py::arg("part"),
      py::arg("dbias"), py::arg("M"), py::arg("N"), py::arg("stream"), py::arg("accumulate") = 0);
   m.def("attn_fwd", [](uintptr_t qkv, uintptr_t mask, uintptr_t out, uintptr_t lse, int B, int S_,
-                       int H, float scale, float p, uint32_t seed, uintptr_t st) {
+                       int H, float scale, float p, uint32_t seed, uintptr_t st, uintptr_t keep) {
     dtf_attn_fwd(P<const bf16_t>(qkv), P<const float>(mask), P<bf16_t>(out), P<float>(lse), B,
-                 S_, H, scale, p, seed, S(st));
+                 S_, H, scale, p, seed, S(st), P<uint32_t>(keep));
     check_launch("attn_fwd");
-  });
+  }, py::arg("qkv"), py::arg("mask"), py::arg("out"), py::arg("lse"), py::arg("B"), py::arg("S"),
+     py::arg("H"), py::arg("scale"), py::arg("p"), py::arg("seed"), py::arg("st"),
+     py::arg("keep") = 0);
+  m.def("attn_keep_words", &dtf_attn_keep_words);
+  m.def("attn_set_keep", &dtf_attn_set_keep);
   m.def("attn_bwd", [](uintptr_t qkv, uintptr_t mask, uintptr_t out, uintptr_t dout,
                        uintptr_t lse, uintptr_t delta, uintptr_t dqkv, int B, int S_, int H,
-                       float scale, float p, uint32_t seed, uintptr_t st, uintptr_t colpart) {
+                       float scale, float p, uint32_t seed, uintptr_t st, uintptr_t colpart,
+                       uintptr_t keep) {
     dtf_attn_bwd(P<const bf16_t>(qkv), P<const float>(mask), P<const bf16_t>(out),
                  P<const bf16_t>(dout), P<const float>(lse), P<float>(delta), P<bf16_t>(dqkv), B,
-                 S_, H, scale, p, seed, S(st), P<float>(colpart));
+                 S_, H, scale, p, seed, S(st), P<float>(colpart), P<const uint32_t>(keep));
     check_launch("attn_bwd");
   }, py::arg("qkv"), py::arg("mask"), py::arg("out"), py::arg("dout"), py::arg("lse"),
      py::arg("delta"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"),
-     py::arg("scale"), py::arg("p"), py::arg("seed"), py::arg("st"), py::arg("colpart") = 0);
+     py::arg("scale"), py::arg("p"), py::arg("seed"), py::arg("st"), py::arg("colpart") = 0,
+     py::arg("keep") = 0);
   m.def("attn_bwd_fused", &dtf_attn_bwd_fused);
   m.def("attn_set_wide", &dtf_attn_set_wide);
   m.def("attn_set_fused", &dtf_attn_set_fused);

@@ -719,6 +719,10 @@ struct AttnGeom {
   float scale;            // softmax scale (1/sqrt(64))
   uint32_t seed, thr;     // attention-probability dropout
   float inv_keep;
+  // S == 128 with dropout (8-wave forward + fused backward): the forward's keep decisions, one
+  // 32-bit word per (b, h, query, 16-lane group) -- bit 4 t + r = key 16 t + 4 group + r, the
+  // keys of exactly that lane in both kernels -- so the backward reads 4 B instead of 32 hashes
+  uint32_t* keep;
 };
 
 DTF_DEV bf16x8_t lds_row8(const bf16_t* base, int row, int col) {
@@ -791,6 +795,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
   const float c = g.scale * kLog2e;
   const uint32_t kbase = (uint32_t)((((long)b * H + h) * S + q) * S);
   float m = -INFINITY, l = 0.f;
+  uint32_t kbits = 0;                    // keep decisions (S == CH == 128: one key chunk)
   f32x4_t acc[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
@@ -834,11 +839,13 @@ attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
         for (int r = 0; r < 4; ++r) {
           const float p = exp2f(s[t][r] - mnew);
           l += p;
-          if (DROP)
-            s[t][r] = keep_elem(g.seed, kbase + kc + sub + 16 * t + 4 * gq + r, g.thr)
-                          ? p * g.inv_keep : 0.f;
-          else
+          if (DROP) {
+            const bool kp = keep_elem(g.seed, kbase + kc + sub + 16 * t + 4 * gq + r, g.thr);
+            s[t][r] = kp ? p * g.inv_keep : 0.f;
+            if constexpr (CH == 128) kbits |= (uint32_t)kp << ((sub >> 6) * 16 + 4 * t + r);
+          } else {
             s[t][r] = p;
+          }
         }
       const bf16x8_t bp0 = pack_frag(s[0], s[1]);
       const bf16x8_t bp1 = pack_frag(s[2], s[3]);
@@ -858,6 +865,8 @@ attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) store4_scaled(orow + 16 * dt + 4 * gq, acc[dt], inv);
   if (gq == 0) lse[((long)b * H + h) * S + q] = m + log2f(l);
+  if constexpr (DROP && CH == 128)
+    if (g.keep) g.keep[(((long)b * H + h) * S + q) * 4 + gq] = kbits;
 }
 
 template <bool DROP, int NW, int CH>
@@ -1123,6 +1132,7 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
   const bf16x8_t bo0 = lds_row8(Os, q, 8 * gq), bo1 = lds_row8(Os, q, 32 + 8 * gq);
   const float c = g.scale * kLog2e;
   const uint32_t kbase = (uint32_t)((bh * S + q) * S);
+  const uint32_t kw = (DROP && g.keep) ? g.keep[(bh * S + q) * 4 + gq] : 0u;
   // P and dS are only ever used rounded to bf16 (MFMA fragments, LDS tiles): kept packed, 4 keys
   // per uint2 -- half the registers of fp32, same bits
   uint2 P[8], dS[8];
@@ -1140,7 +1150,7 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
       const int key = 16 * t + 4 * gq + r;
       const float p = exp2f(s[r] * c + Ms[key] - lq);
       if (DROP) {
-        const bool kp = keep_elem(g.seed, kbase + key, g.thr);
+        const bool kp = g.keep ? ((kw >> (4 * t + r)) & 1u) != 0u : keep_elem(g.seed, kbase + key, g.thr);
         pt[r] = kp ? p * g.inv_keep : 0.f;
         st[r] = p * ((kp ? dp[r] * g.inv_keep : 0.f) - dl);
       } else {
@@ -1446,7 +1456,8 @@ static AttnGeom attn_geom(int B, int S, int H, float scale, float p, uint32_t se
   if (S % 64) throw std::runtime_error("attention: seq_len must be a multiple of 64");
   if ((long)B * H * S * S > 0xFFFFFFFFL && p > 0.f)
     throw std::runtime_error("attention dropout index space exceeds 32 bits");
-  return AttnGeom{B, S, H, 3 * H * AD, scale, seed, drop_thr(p), p > 0.f ? 1.f / (1.f - p) : 1.f};
+  return AttnGeom{B, S, H, 3 * H * AD, scale, seed, drop_thr(p), p > 0.f ? 1.f / (1.f - p) : 1.f,
+                  nullptr};
 }
 
 // 0: always the 4-wave / 64-row shape; 1 (default): 8 waves / 128 rows when S % 128 == 0
@@ -1489,15 +1500,28 @@ static void attn_bwd_launch(const bf16_t* qkv, const float* mask, const bf16_t* 
   }
 }
 
+// 1 (default): with dropout at S == 128, the forward stores its keep decisions for the fused
+// backward (dtf_attn_keep_words > 0)
+static int g_attn_keep = 1;
+void dtf_attn_set_keep(int v) { g_attn_keep = v; }
+static int g_attn_fused = 1;
+// uint32 words of the keep-decision buffer dtf_attn_fwd / dtf_attn_bwd take (0: not used)
+long dtf_attn_keep_words(int B, int S, int H, float p) {
+  return (g_attn_keep && g_attn_wide && g_attn_fused && S == 128 && p > 0.f) ? (long)B * H * S * 4
+                                                                              : 0;
+}
+
 void dtf_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int B, int S,
-                  int H, float scale, float p, uint32_t seed, hipStream_t st) {
-  const AttnGeom g = attn_geom(B, S, H, scale, p, seed);
+                  int H, float scale, float p, uint32_t seed, hipStream_t st, uint32_t* keep) {
+  AttnGeom g = attn_geom(B, S, H, scale, p, seed);
+  if (keep && !dtf_attn_keep_words(B, S, H, p))
+    throw std::runtime_error("attn_fwd: keep buffer given for a shape that does not use it");
+  g.keep = keep;
   if (g_attn_wide && S % 128 == 0) attn_fwd_launch<8, 128>(qkv, mask, out, lse, g, st);
   else attn_fwd_launch<4, 64>(qkv, mask, out, lse, g, st);
 }
 
 // 1 (default): S == 128 runs the fused one-block-per-(b, h) backward
-static int g_attn_fused = 1;
 void dtf_attn_set_fused(int v) { g_attn_fused = v; }
 
 // 1 when dtf_attn_bwd will run the fused kernel for this shape (it can then also emit the qkv
@@ -1506,10 +1530,14 @@ int dtf_attn_bwd_fused(int S) { return g_attn_fused && S == kFusedS; }
 
 void dtf_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* out, const bf16_t* dout,
                   const float* lse, float* delta, bf16_t* dqkv, int B, int S, int H, float scale,
-                  float p, uint32_t seed, hipStream_t st, float* colpart) {
-  const AttnGeom g = attn_geom(B, S, H, scale, p, seed);
+                  float p, uint32_t seed, hipStream_t st, float* colpart,
+                  const uint32_t* keep) {
+  AttnGeom g = attn_geom(B, S, H, scale, p, seed);
   if (colpart && !(g_attn_fused && S == kFusedS))
     throw std::runtime_error("attn_bwd: column partials need the fused S == 128 backward");
+  if (keep && !dtf_attn_keep_words(B, S, H, p))
+    throw std::runtime_error("attn_bwd: keep buffer given for a shape that does not use it");
+  g.keep = const_cast<uint32_t*>(keep);
   if (g_attn_fused && S == kFusedS) {
     static bool attr = false;
     if (!attr) {

@@ -23,6 +23,8 @@ AD = 64   # attention head dim supported by the MFMA kernels
 _RESIDUAL_TO_DENSE = os.environ.get("DTF_RESIDUAL_TO_DENSE", "1") == "1"
 if os.environ.get("DTF_ATTN_WIDE"):
     _K.attn_set_wide(int(os.environ["DTF_ATTN_WIDE"]))
+if os.environ.get("DTF_ATTN_KEEP"):        # 0: the fused attention backward re-hashes dropout
+    _K.attn_set_keep(int(os.environ["DTF_ATTN_KEEP"]))
 if os.environ.get("DTF_LN_WIDE"):          # 0: the 8-B-per-lane LayerNorm kernels
     _K.ln_set_wide(int(os.environ["DTF_LN_WIDE"]))
 if os.environ.get("DTF_ATTN_FUSED_BWD"):      # 0: the split dQ + dK/dV backward at S == 128
@@ -249,8 +251,13 @@ class _AttentionQKV(torch.autograd.Function):
         out = torch.empty(B * S, heads * AD, device=qkv.device, dtype=_BF16)
         lse = torch.empty(B * heads * S, device=qkv.device, dtype=torch.float32)
         seed = next_seed() if p > 0 else 0
+        # with dropout at S == 128 the forward keeps its keep decisions (1 bit per score) for
+        # the fused backward, which then skips re-hashing them
+        nk = _K.attn_keep_words(B, S, heads, float(p))
+        keep = torch.empty(nk, device=qkv.device, dtype=torch.int32) if nk else None
         _K.attn_fwd(q.data_ptr(), _p(m), out.data_ptr(), lse.data_ptr(), B, S, heads,
-                    float(scale), float(p), seed, _st())
+                    float(scale), float(p), seed, _st(), _p(keep))
+        ctx.keep = keep
         ctx.save_for_backward(q, m if m is not None else lse, out, lse)
         ctx.cfg = (B, S, heads, float(p), seed, float(scale), m is not None)
         return out
@@ -267,9 +274,12 @@ class _AttentionQKV(torch.autograd.Function):
         part = None
         if _K.attn_bwd_fused(S):
             part = torch.empty(B, 3 * heads * AD, device=q.device, dtype=torch.float32)
+        keep, ctx.keep = ctx.keep, None
+        if keep is not None and not _K.attn_keep_words(B, S, heads, float(p)):
+            keep = None          # knobs changed between forward and backward: re-hash
         _K.attn_bwd(q.data_ptr(), m.data_ptr() if has_mask else 0, out.data_ptr(), do.data_ptr(),
                     lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), B, S, heads, scale, p, seed,
-                    _st(), _p(part))
+                    _st(), _p(part), _p(keep))
         if part is not None:
             # valid only for this exact tensor and version (an in-place add would change it)
             dqkv._dtf_colsum_part = (part, B, dqkv._version)

@@ -294,6 +294,44 @@ def test_attention_fused_bwd_bit_identical(p):
 
 
 @pytest.mark.gpu
+def test_attention_keep_bits_bit_identical():
+    """S == 128 with dropout: the forward stores its keep decisions (one bit per score) and the
+    fused backward reads them instead of re-hashing: outputs and gradients bit-identical to the
+    re-hashing backward, and the buffer really holds the decisions (~keep rate of ones)."""
+    from distributedtensorflow_amd.ops import native
+    torch.manual_seed(0)
+    B, S, H, p = 3, 128, 4, 0.1
+    qkv = torch.randn(B * S, 3 * H * 64, device="cuda").bfloat16().requires_grad_(True)
+    mask = torch.zeros(B, S, device="cuda")
+    mask[2, 90:] = -10000.0
+    dy = torch.randn(B * S, H * 64, device="cuda").bfloat16()
+    assert native._K.attn_keep_words(B, S, H, p) == B * H * S * 4
+    outs = []
+    for keep in (1, 0):
+        native._K.attn_set_keep(keep)
+        try:
+            torch.manual_seed(5)
+            y = ops.attention_qkv(qkv, mask, B, S, H, p, True)
+            (g,) = torch.autograd.grad(y, [qkv], dy)
+            torch.cuda.synchronize()
+        finally:
+            native._K.attn_set_keep(1)
+        outs.append((y, g))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    # the stored words: about (1 - p) of the bits set
+    kw = torch.empty(B * H * S * 4, device="cuda", dtype=torch.int32)
+    out = torch.empty(B * S, H * 64, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device="cuda")
+    native._K.attn_fwd(qkv.detach().data_ptr(), mask.data_ptr(), out.data_ptr(), lse.data_ptr(),
+                       B, S, H, 0.125, p, 77, torch.cuda.current_stream().cuda_stream,
+                       kw.data_ptr())
+    torch.cuda.synchronize()
+    bits = torch.stack([(kw >> i) & 1 for i in range(32)]).sum().item()
+    assert abs(bits / (32 * kw.numel()) - (1 - p)) < 0.01
+
+
+@pytest.mark.gpu
 def test_qkv_bias_grad_from_fused_attention_partials():
     """S == 128: the fused attention backward leaves per-sequence column sums of dQKV, and the
     QKV projection's bias gradient is their B-row sum (no pass over dQKV).  It must equal the

@@ -50,15 +50,29 @@ def main():
     st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
     scale = D ** -0.5
     flops_f = 4.0 * B * H * S * S * D
-    for p in (0.0, 0.1):
+    # dropout runs with and without the forward's stored keep decisions (attn_keep_words)
+    for p, use_keep in ((0.0, False), (0.1, False), (0.1, True)):
+        nk = _K.attn_keep_words(B, S, H, p) if use_keep else 0
+        if use_keep and not nk:
+            continue
+        keep = torch.empty(max(nk, 1), device=dev, dtype=torch.int32)
+        kp = keep.data_ptr() if nk else 0
         fwd = lambda: _K.attn_fwd(qkv.data_ptr(), mask.data_ptr(), out.data_ptr(), lse.data_ptr(),  # noqa: E731
-                                  B, S, H, scale, p, 1234, st())
+                                  B, S, H, scale, p, 1234, st(), kp)
         bwd = lambda: _K.attn_bwd(qkv.data_ptr(), mask.data_ptr(), out.data_ptr(), do.data_ptr(),  # noqa: E731
                                   lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), B, S, H,
-                                  scale, p, 1234, st())
+                                  scale, p, 1234, st(), 0, kp)
         tf = timeit(fwd, a.iters)
         tb = timeit(bwd, a.iters)
-        rec = {"probe": "attn", "B": B, "S": S, "H": H, "dropout": p, "fwd_ms": round(tf, 4),
+        if p > 0.0:
+            # same keep decisions either way: the backward's outputs are bit-identical
+            fwd()
+            bwd()
+            torch.cuda.synchronize()
+            if not use_keep:
+                ref_dqkv = dqkv.clone()
+        rec = {"probe": "attn", "B": B, "S": S, "H": H, "dropout": p, "keep_bits": use_keep,
+               "fwd_ms": round(tf, 4),
                "bwd_ms": round(tb, 4), "fwd_tflops": round(flops_f / tf / 1e9, 1),
                "bwd_tflops": round(2.5 * flops_f / tb / 1e9, 1)}
         if p == 0.0:
@@ -76,6 +90,8 @@ def main():
                 ref = t.grad.permute(0, 2, 1, 3)
                 rec["d%s_max_rel" % "qkv"[i]] = float((dq3[:, :, i] - ref).abs().max()
                                                        / ref.abs().max())
+        if use_keep:
+            rec["dqkv_bit_identical_to_rehash"] = bool(torch.equal(dqkv, ref_dqkv))
         print(json.dumps(rec), flush=True)
 
 
