@@ -200,6 +200,8 @@ void dtf_mlm_xent(const bf16_t*, const int64_t*, const float*, const float*, int
                   bf16_t*, hipStream_t);
 
 // ---- dense GEMM (gemm.hip)
+void dtf_gemm_nt_bias_gelu(const bf16_t*, const bf16_t*, bf16_t*, bf16_t*, int, int, int, int,
+                           int, const float*, hipStream_t);
 void dtf_gemm_nt_gelu_bwd(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int,
                           const bf16_t*, const float*, float*, hipStream_t);
 void dtf_gemm_nt(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int,
@@ -333,6 +335,12 @@ PYBIND11_MODULE(_dtf_hip, m) {
      py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("bias"), py::arg("cin"),
      py::arg("relu"), py::arg("stream"), py::arg("stats") = 0, py::arg("acc_src") = 0,
      py::arg("acc_mask") = 0);
+  m.def("gemm_nt_bias_gelu", [](uintptr_t a, uintptr_t b, uintptr_t z, uintptr_t h, int M, int N,
+                                int K, int lda, int ldb, uintptr_t bias, uintptr_t st) {
+    dtf_gemm_nt_bias_gelu(P<bf16_t>(a), P<bf16_t>(b), P<bf16_t>(z), P<bf16_t>(h), M, N, K, lda,
+                          ldb, P<float>(bias), S(st));
+    check_launch("gemm_nt_bias_gelu");
+  });
   m.def("gemm_nt_gelu_bwd", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K,
                                int lda, int ldb, uintptr_t gelu_a, uintptr_t gelu_b,
                                uintptr_t colsum, uintptr_t st) {

@@ -54,6 +54,9 @@ struct GemmArgs {
   const bf16_t* gelu_a;
   const float* gelu_b;
   float* colsum;
+  // bias + GELU forward epilogue (BERT's first FFN GEMM): C = z = acc + bias (bf16) and
+  // gelu_out = gelu(z), the pre-activation for the GELU backward and the activation for FFN2
+  bf16_t* gelu_out;
   int ncu;                          // OCC 2 kernels: compute units (the first resident round)
   int group_m;                      // > 0: grouped tile order (GM M-panels x all N per group)
   int stagger_mode, stagger;        // OCC 2: which first-round blocks start late, by how much
@@ -690,6 +693,13 @@ gemm_nt_kernel(const GemmArgs g) {
       v = pack8(d);
     }
     st16(g.C + off, v, g.nt);
+    if (g.gelu_out) {
+      float z[8];
+      unpack8(v, z);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = gelu_f(z[e]);
+      st16(g.gelu_out + off, pack8(z), g.nt);
+    }
   }
   if (g.colsum) {
     // the OROWS threads of a column chunk meet in LDS (the staged tile is dead after a barrier)
@@ -1212,6 +1222,23 @@ void dtf_gemm_nt_gelu_bwd(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, in
   GemmArgs g{};
   g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = N;
   g.gelu_a = gelu_a; g.gelu_b = gelu_b; g.colsum = colsum;
+  g.nt = g_gemm_nt;
+  if (N <= 128) launch_gemm<256, 128, 64, 3>(g, st);
+  else launch_gemm<256, 256, 64, 2, 2>(g, st);
+}
+
+// Z = A . B^T + bias (bf16) and H = gelu(Z) in one pass (BERT's first FFN GEMM: replaces a
+// library GEMM + the bias_gelu_fwd pass that re-read its output)
+void dtf_gemm_nt_bias_gelu(const bf16_t* A, const bf16_t* B, bf16_t* Z, bf16_t* H, int M, int N,
+                           int K, int lda, int ldb, const float* bias, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0) return;
+  if (K % 8 || N % 8 || lda % 8 || ldb % 8 || lda < K || ldb < K || !bias || !H)
+    throw std::runtime_error("gemm_nt_bias_gelu: K, N, leading dims % 8; bias and H needed");
+  if ((long)256 * lda * 2 + 2L * K >= (1L << 31) || (long)256 * ldb * 2 + 2L * K >= (1L << 31))
+    throw std::runtime_error("gemm_nt_bias_gelu: leading dimension too large");
+  GemmArgs g{};
+  g.A = A; g.B = B; g.C = Z; g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = N;
+  g.bias = bias; g.gelu_out = H;
   g.nt = g_gemm_nt;
   if (N <= 128) launch_gemm<256, 128, 64, 3>(g, st);
   else launch_gemm<256, 256, 64, 2, 2>(g, st);

@@ -128,9 +128,10 @@ class BertLayer(nn.Module):
                                             self.training, cfg.layer_norm_eps,
                                             residual_to_dense=True)
         if FUSE_GELU_DGRAD and BERT_GEMM == "library":
-            # bias + GELU and the second FFN GEMM as one op: its backward forms d(a) in one
-            # GEMM pass with the GELU derivative in the epilogue (ops.native._BiasGeluDense)
-            o = ops.bias_gelu_dense(self.inter.gemm(x), self.inter.bias, self.out.kernel)
+            # the whole FFN as one op: the first GEMM applies bias + GELU in its epilogue (our
+            # MFMA GEMM); the backward forms d(pre-activation) in one GEMM pass with the GELU
+            # derivative in the epilogue (ops.native.dense_gelu_dense / _BiasGeluDense)
+            o = ops.dense_gelu_dense(x, self.inter.kernel, self.inter.bias, self.out.kernel)
         else:
             h = ops.bias_gelu(self.inter.gemm(x), self.inter.bias)
             o = self.out.gemm(h)

@@ -252,6 +252,14 @@ def bias_gelu_dense(a, bias, w):
     return reference.dense(reference.bias_gelu(a, bias), w)
 
 
+def dense_gelu_dense(x, w1, b1, w2):
+    """gelu(x @ w1^T + b1) @ w2^T (w [out, in]): BERT's FFN.  Native: the first GEMM carries
+    the bias + GELU in its epilogue and also writes the pre-activation for the backward."""
+    if _use_native(x):
+        return _native().dense_gelu_dense(x, w1, b1, w2)
+    return reference.dense(reference.bias_gelu(reference.dense(x, w1), b1), w2)
+
+
 def attention_qkv(qkv, mask, batch, seq_len, heads, p=0.0, training=True, scale=None):
     """Multi-head self-attention straight from the fused QKV projection output."""
     if _use_native(qkv):
@@ -306,7 +314,7 @@ def _dispatch(name, fn, fenced):
 _OPS = ("conv2d", "conv2d_bias_relu", "batch_norm", "batch_norm_add_batch_norm",
         "batch_norm_relu_conv1x1", "batch_norm_relu_max_pool", "dense", "layer_norm",
         "bias_dropout_add_layer_norm", "embedding_layer_norm", "bias_gelu", "bias_gelu_dense",
-        "relu", "max_pool2d", "global_avg_pool", "sparse_softmax_cross_entropy",
+        "dense_gelu_dense", "relu", "max_pool2d", "global_avg_pool", "sparse_softmax_cross_entropy",
         "softmax_cross_entropy_clipped_sum", "gelu", "attention", "dropout", "attention_qkv",
         "mlm_loss")
 _FENCED = _OPS
@@ -319,6 +327,6 @@ __all__ = [
     "batch_norm_add_batch_norm", "batch_norm_relu_conv1x1",
     "max_pool2d", "global_avg_pool", "dense", "sparse_softmax_cross_entropy",
     "softmax_cross_entropy_clipped_sum", "layer_norm", "gelu", "attention", "dropout",
-    "bias_dropout_add_layer_norm", "embedding_layer_norm", "bias_gelu", "attention_qkv",
-    "mlm_loss",
+    "bias_dropout_add_layer_norm", "embedding_layer_norm", "bias_gelu", "bias_gelu_dense",
+    "dense_gelu_dense", "attention_qkv", "mlm_loss",
 ]

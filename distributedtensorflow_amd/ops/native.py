@@ -1419,15 +1419,34 @@ class _Dense(torch.autograd.Function):
     fp32 straight into the optimizer's flat gradient buffer (no bf16 dW, no cast/add kernels)."""
 
     @staticmethod
-    def forward(ctx, x, w_master, wb, b):
+    def forward(ctx, x, w_master, wb, b, gelu_b=None):
         ctx.save_for_backward(x, wb)
         ctx.w_param, ctx.b_param = w_master, b
         ctx.x_ref = x     # a fused LayerNorm may leave d(x) here (residual_to_dense)
         ctx.has_b = b is not None
+        if gelu_b is not None:
+            # (z, h) = (x W^T + gelu_b, gelu(z)) from ONE pass of our MFMA GEMM with the bias +
+            # GELU epilogue (gemm.hip gelu_out).  gelu_b is not a differentiable input here: its
+            # gradient is the column sum of dz, which the consumer (_BiasGeluDense) forms.
+            o, i = wb.shape
+            x2 = x.reshape(-1, i)
+            M = x2.shape[0]
+            z = torch.empty(M, o, device=x.device, dtype=_BF16)
+            h = torch.empty_like(z)
+            _K.gemm_nt_bias_gelu(x2.data_ptr(), wb.data_ptr(), z.data_ptr(), h.data_ptr(), M, o,
+                                 i, x2.stride(0), wb.stride(0), gelu_b.data_ptr(), _st())
+            ctx.mark_non_differentiable(h)
+            # no zero-filled [T, 3072] gradient for h (0.7 ms/step of fills at BERT-base b512)
+            ctx.set_materialize_grads(False)
+            shape = (*x.shape[:-1], o)
+            return z.view(shape), h.view(shape)
         return torch.nn.functional.linear(x, wb, None if b is None else b.to(x.dtype))
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, *_unused):
+        if dy is None:      # the GELU form's pre-activation received no gradient
+            ctx.w_param = ctx.b_param = ctx.x_ref = None
+            return None, None, None, None, None
         x, wb = ctx.saved_tensors
         o, i = wb.shape
         x2, dy2 = x.reshape(-1, i), dy.reshape(-1, o)
@@ -1473,7 +1492,7 @@ class _Dense(torch.autograd.Function):
             else:
                 db = out.to(ctx.b_param.dtype)
         ctx.w_param = ctx.b_param = None
-        return dx, dw, None, db
+        return dx, dw, None, db, None
 
 
 class _BiasGeluDense(torch.autograd.Function):
@@ -1486,16 +1505,23 @@ class _BiasGeluDense(torch.autograd.Function):
     other consumer can add to its gradient."""
 
     @staticmethod
-    def forward(ctx, a, b1, w_master, wb):
+    def forward(ctx, a, b1, w_master, wb, h=None):
         N = a.shape[-1]
         a2 = a.reshape(-1, N).contiguous()
-        b32 = b1.detach().float().contiguous()
-        h = torch.empty_like(a2)
-        _K.bias_gelu_fwd(a2.data_ptr(), b32.data_ptr(), h.data_ptr(), a2.shape[0], N, _st())
+        if h is None:
+            b32 = b1.detach().float().contiguous()
+            h = torch.empty_like(a2)
+            _K.bias_gelu_fwd(a2.data_ptr(), b32.data_ptr(), h.data_ptr(), a2.shape[0], N, _st())
+        else:
+            # the producer GEMM already applied bias + GELU (dense_gelu_dense): a is the
+            # pre-activation a + b1 itself, so the backward's GELU derivative takes no bias
+            b32 = None
+            h = h.reshape(-1, N)
         o, i = wb.shape
         if wb.is_contiguous():
             _register_dgrad_filter(wb.view(o, 1, 1, i))
-        ctx.save_for_backward(a2, b32, h, wb)
+        ctx.has_b32 = b32 is not None
+        ctx.save_for_backward(a2, b32 if b32 is not None else a2, h, wb)
         ctx.params = (b1, w_master)
         ctx.shape = a.shape
         return torch.nn.functional.linear(h, wb).view(*a.shape[:-1], o)
@@ -1503,6 +1529,7 @@ class _BiasGeluDense(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         a2, b32, h, wb = ctx.saved_tensors
+        b32 = b32 if ctx.has_b32 else None
         b1, w_master = ctx.params
         ctx.params = None
         o, i = wb.shape
@@ -1518,7 +1545,7 @@ class _BiasGeluDense(torch.autograd.Function):
             tiles = _K.gemm_tile_rows(M)
             colsum = torch.empty(tiles, i, device=do.device, dtype=torch.float32)
             _K.gemm_nt_gelu_bwd(do2.data_ptr(), wt.data_ptr(), da.data_ptr(), M, i, o,
-                                do2.stride(0), wt.stride(0), a2.data_ptr(), b32.data_ptr(),
+                                do2.stride(0), wt.stride(0), a2.data_ptr(), _p(b32),
                                 colsum.data_ptr(), _st())
             if ctx.needs_input_grad[1]:
                 # the b1 gradient: the per-tile column sums' second level, in fixed order, added
@@ -1533,13 +1560,35 @@ class _BiasGeluDense(torch.autograd.Function):
                 else:
                     db = out.to(b1.dtype)
             da = da.view(ctx.shape)
-        return da, db, dw, None
+        return da, db, dw, None, None
 
 
 def bias_gelu_dense(a, b1, w):
     """gelu(a + b1) @ w^T with w [out, in] (fp32 master, bf16 shadow on the GEMM)."""
     _check_cuda_bf16(a)
     return _BiasGeluDense.apply(a, b1, w, _bf16_weight(w))
+
+
+# BERT's FFN first GEMM on our MFMA GEMM with the bias + GELU epilogue (A/B knob, off by default:
+# in the BERT-base b512 step it takes 441 us per layer against 268 us for hipBLASLt + 139 us for the
+# bias_gelu_fwd pass, profiles/measurements/r4_bert_ffn1_fused_epilogue.jsonl)
+_FFN_GEMM_GELU = os.environ.get("DTF_FFN_GEMM_GELU", "0") == "1"
+
+
+def dense_gelu_dense(x, w1, b1, w2):
+    """gelu(x @ w1^T + b1) @ w2^T -- BERT's whole FFN (w [out, in], fp32 masters, bf16 shadows).
+    The first GEMM runs on our MFMA GEMM with the bias + GELU in its epilogue, writing the
+    pre-activation (for the GELU backward) and the activation (for the second GEMM) in one pass
+    instead of a library GEMM followed by a bias + GELU pass over its output; the rest is
+    _BiasGeluDense (the GELU derivative in the data-gradient GEMM's epilogue)."""
+    _check_cuda_bf16(x)
+    wb1 = _bf16_weight(w1)
+    o, i = wb1.shape
+    if (_FFN_GEMM_GELU and w1.dtype == torch.float32 and w1.requires_grad and wb1.is_contiguous()
+            and x.is_contiguous() and o % 8 == 0 and i % 8 == 0):
+        z, h = _Dense.apply(x, w1, wb1, None, b1.detach().float().contiguous())
+        return _BiasGeluDense.apply(z, b1, w2, _bf16_weight(w2), h)
+    return bias_gelu_dense(dense(x, w1, None, impl="library"), b1, w2)
 
 
 def _transposed_bf16(wb):

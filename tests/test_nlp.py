@@ -473,3 +473,53 @@ def test_bias_gelu_dense_fused_backward(T, I, O):
         scale = ref.abs().max()
         assert (got - ref).abs().max() <= 2e-2 * scale, (got - ref).abs().max() / scale
         assert (got - unf).abs().max() <= 2e-2 * scale
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,H,I", [(4096, 768, 3072), (1000, 256, 1024), (600, 128, 96)])
+def test_dense_gelu_dense_fused_epilogue(T, H, I):
+    """BERT's FFN as one op: the first GEMM on our MFMA kernel with the bias + GELU epilogue
+    (gemm.hip gelu_out: pre-activation and activation in one pass) == the two-pass form (library
+    GEMM + bias_gelu kernel) and an fp32 reference, forward and every gradient."""
+    from distributedtensorflow_amd.ops import native
+    torch.manual_seed(0)
+    x32 = torch.randn(T, H)
+    w1 = torch.randn(I, H) * H ** -0.5
+    b1 = torch.randn(I) * 0.5
+    w2 = torch.randn(H, I) * I ** -0.5
+    do = torch.randn(T, H)
+    calls = []
+    orig = native._K.gemm_nt_bias_gelu
+
+    def spy(*a):
+        calls.append(1)
+        return orig(*a)
+
+    def run(fused):
+        prev = native._FFN_GEMM_GELU
+        native._FFN_GEMM_GELU = fused
+        native._K.gemm_nt_bias_gelu = spy
+        try:
+            x = x32.cuda().bfloat16().requires_grad_(True)
+            p = [t.cuda().requires_grad_(True) for t in (w1, b1, w2)]
+            y = ops.dense_gelu_dense(x, *p)
+            y.backward(do.cuda().bfloat16())
+            torch.cuda.synchronize()
+            return [y.float().cpu(), x.grad.float().cpu()] + [t.grad.cpu() for t in p]
+        finally:
+            native._FFN_GEMM_GELU = prev
+            native._K.gemm_nt_bias_gelu = orig
+
+    got = run(True)
+    assert calls, "the fused bias + GELU GEMM did not run"
+    unf = run(False)
+    x_ = x32.bfloat16().float().requires_grad_(True)
+    p_ = [w1.bfloat16().float().requires_grad_(True), b1.clone().requires_grad_(True),
+          w2.bfloat16().float().requires_grad_(True)]
+    y_ = R.bias_gelu(x_ @ p_[0].t(), p_[1]) @ p_[2].t()
+    y_.backward(do.bfloat16().float())
+    refs = [y_.detach(), x_.grad] + [t.grad for t in p_]
+    for name, g, u, r in zip(("y", "dx", "dw1", "db1", "dw2"), got, unf, refs):
+        scale = r.abs().max()
+        assert (g - r).abs().max() <= 2e-2 * scale, (name, ((g - r).abs().max() / scale).item())
+        assert (g - u).abs().max() <= 2e-2 * scale, (name, ((g - u).abs().max() / scale).item())

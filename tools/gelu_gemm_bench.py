@@ -47,6 +47,20 @@ def main():
         us = timeit(fn, a.iters)
         print(json.dumps({"probe": "gelu_gemm", "M": M, "N": N, "K": K, "us": round(us, 1),
                           "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}), flush=True)
+    # the forward FFN GEMM: ours with the bias + GELU epilogue vs hipBLASLt + our bias_gelu pass
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    z = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    h = torch.empty_like(z)
+    fused = timeit(lambda: _K.gemm_nt_bias_gelu(x.data_ptr(), wt.data_ptr(), z.data_ptr(),
+                                                h.data_ptr(), M, N, K, K, K, gb.data_ptr(), st()),
+                   a.iters)
+
+    def two_pass():
+        y = torch.nn.functional.linear(x, wt)
+        _K.bias_gelu_fwd(y.data_ptr(), gb.data_ptr(), h.data_ptr(), M, N, st())
+    lib2 = timeit(two_pass, a.iters)
+    print(json.dumps({"probe": "ffn1_fwd", "fused_bias_gelu_gemm_us": round(fused, 1),
+                      "hipblaslt_plus_bias_gelu_us": round(lib2, 1)}), flush=True)
     plain = timeit(lambda: native.gemm_nt(do, wt), a.iters)
     lib = timeit(lambda: torch.nn.functional.linear(do, wt), a.iters)
     print(json.dumps({"probe": "gelu_gemm", "plain_gemm_nt_us": round(plain, 1),
