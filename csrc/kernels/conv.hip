@@ -879,6 +879,27 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
       dma16(rx, lds_patch + (uint32_t)q * 1024u, off);
     }
   }
+  // ---- BNB: this thread's epilogue rows of the BN input x (and mask bytes), loaded now -- the
+  // block runs at most two waves per SIMD (LDS-bound), so the 28 registers are free, and the loads
+  // complete under the main loop instead of in front of the epilogue's stores
+  constexpr int OCPR = NT / 8;
+  constexpr int OROWS = kThreads / OCPR;                         // rows per store pass
+  constexpr int NR = H::M / OROWS;                               // store passes
+  static_assert(H::M % OROWS == 0, "halo epilogue rows");
+  const long ybase = ((long)n * g.H + h0) * g.W;                 // first output pixel of the tile
+  const int oc = tid % OCPR;
+  const bool col_ok = n0 + oc * 8 < g.Kout;
+  uint4 xpre[BNB ? NR : 1];
+  uint32_t mpre[BNB ? NR : 1];
+  if constexpr (BNB) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const long off = (ybase + tid / OCPR + k * OROWS) * g.Kout + n0 + oc * 8;
+      const bool ok = live && col_ok;
+      xpre[k] = ok ? *reinterpret_cast<const uint4*>(bnb.x + off) : make_uint4(0, 0, 0, 0);
+      mpre[k] = (ok && bnb.mkind == 1) ? (uint32_t)bnb.mask[off >> 3] : 0u;
+    }
+  }
   // ---- filter slice of step (tap t, channel slice s): NT rows x 64 channels (128-B rows)
   const int lp8 = lane >> 3, slot8 = lane & 7;
   auto issue_w = [&](int step, int stage) {
@@ -1004,24 +1025,6 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   DTF_WAIT_VM(0);
   __syncthreads();
   // ---- epilogue: bf16 tile [M][NT + 8] in LDS (over the patch) -> 16-B stores; BN partials
-  constexpr int OCPR = NT / 8;
-  constexpr int OROWS = kThreads / OCPR;                         // rows per store pass
-  constexpr int NR = H::M / OROWS;                               // store passes
-  static_assert(H::M % OROWS == 0, "halo epilogue rows");
-  const long ybase = ((long)n * g.H + h0) * g.W;                 // first output pixel of the tile
-  const int oc = tid % OCPR;
-  const bool col_ok = n0 + oc * 8 < g.Kout;
-  uint4 xpre[BNB ? NR : 1];
-  uint32_t mpre[BNB ? NR : 1];
-  if constexpr (BNB) {
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      const long off = (ybase + tid / OCPR + k * OROWS) * g.Kout + n0 + oc * 8;
-      const bool ok = live && col_ok;
-      xpre[k] = ok ? *reinterpret_cast<const uint4*>(bnb.x + off) : make_uint4(0, 0, 0, 0);
-      mpre[k] = (ok && bnb.mkind == 1) ? (uint32_t)bnb.mask[off >> 3] : 0u;
-    }
-  }
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
