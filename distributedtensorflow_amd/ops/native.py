@@ -473,9 +473,10 @@ class _Conv2d(torch.autograd.Function):
                     and tuple(pads) == (1, 1, 1, 1)
                     and _halo_dgrad_shape(K_, xb.shape[-1], xb.shape[1], xb.shape[2]))
         # stride-2 3x3 data gradients (the first block of stages 2-4) run at 0.25-0.34 of the MFMA
-        # roof: the BN-sum epilogue's extra read of x fits under them (A/B knob)
+        # roof: the BN-sum epilogue's extra read of x fits under the 128-output one
         s2_bnb = (_FUSE_BN_BWD_S2 and (R_, S_) == (3, 3) and tuple(_pair(stride)) == (2, 2)
-                  and xb.shape[-1] % 32 == 0)
+                  and xb.shape[-1] % 32 == 0
+                  and (_FUSE_BN_BWD_S2_ALL or xb.shape[-1] < 256))
         ctx.bnb = bnb if ((_FUSE_BN_BWD or stream_bnb or halo_bnb or s2_bnb) and bnb is not None
                           and xb is x) else None
         dual = getattr(x, "_dtf_bnb_dual", None)
@@ -631,10 +632,16 @@ _FUSE_BN_BWD = os.environ.get("DTF_FUSE_BN_BWD", "0") == "1"
 _FUSE_BN_BWD_STREAM = os.environ.get("DTF_FUSE_BN_BWD_STREAM", "1") == "1"
 
 
-# ... and where it runs on the 3x3 halo kernels (stage-1/2 c2 data gradients -> BN1): the
-# epilogue loads x under the tile staging, and the BN1 reduce pass (a re-read of dy and x) goes
+# ... and where it runs on the 3x3 halo kernels (stage-1/2 c2 data gradients -> BN1): the x
+# rows load under the main loop, and the BN1 reduce pass (a re-read of dy and x) goes (+0.2 %)
 _FUSE_BN_BWD_HALO = os.environ.get("DTF_FUSE_BN_BWD_HALO", "1") == "1"
-_FUSE_BN_BWD_S2 = os.environ.get("DTF_FUSE_BN_BWD_S2", "0") == "1"
+# ... and in the stride-2 3x3 data gradient of stage 2's first block (128 outputs: the register
+# implicit-GEMM kernel either way): the 3.2 GB BN1 reduce pass goes, throughput-neutral
+# (profiles/measurements/r4_stride2_dgrad_bn_sums_ab.jsonl)
+_FUSE_BN_BWD_S2 = os.environ.get("DTF_FUSE_BN_BWD_S2", "1") == "1"
+# ... also where the data gradient (C >= 256 outputs) would otherwise run on the ping-pong GEMM
+# route, which takes no BN-sum epilogue (measured -0.3 % with it)
+_FUSE_BN_BWD_S2_ALL = os.environ.get("DTF_FUSE_BN_BWD_S2_ALL", "0") == "1"
 
 
 def _halo_dgrad_shape(K, C, H, W):
