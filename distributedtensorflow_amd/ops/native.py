@@ -635,7 +635,7 @@ _FUSE_BN_BWD_STREAM = os.environ.get("DTF_FUSE_BN_BWD_STREAM", "1") == "1"
 # ... and where it runs on the 3x3 halo kernels (stage-1/2 c2 data gradients -> BN1): the x
 # rows load under the main loop, and the BN1 reduce pass (a re-read of dy and x) goes (+0.2 %)
 _FUSE_BN_BWD_HALO = os.environ.get("DTF_FUSE_BN_BWD_HALO", "1") == "1"
-# ... and in the stride-2 3x3 data gradient of stage 2's first block (128 outputs: the register
+# ... and in the stride-2 3x3 data gradient of s1b0c2 (stage 1's first block; 128 outputs: the register
 # implicit-GEMM kernel either way): the 3.2 GB BN1 reduce pass goes, throughput-neutral
 # (profiles/measurements/r4_stride2_dgrad_bn_sums_ab.jsonl)
 _FUSE_BN_BWD_S2 = os.environ.get("DTF_FUSE_BN_BWD_S2", "1") == "1"
