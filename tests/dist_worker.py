@@ -172,6 +172,10 @@ def colocated_bert(out, kw, steps):
                 "fingerprints": fps, "sharded": getattr(opt._reducer, "sharded", None),
                 "loss": float(loss.detach())}, os.path.join(out, f"rank{rank}.pt"))
     strat.barrier()
+    # results are on disk: leave without the interpreter teardown, where gloo's threads behind the
+    # still-registered overlapped gathers intermittently hit std::terminate (exit -6)
+    sys.stdout.flush()
+    os._exit(0)
 
 
 def checkpointed_run(strat, out, kw, steps):
