@@ -68,8 +68,8 @@ class _Task:
 
 def _dump_stacks(tasks):
     """Ask every live task for a Python stack dump into its log (SIGUSR1: the entry scripts
-    register faulthandler for it) before a timed-out job is torn down, so a hang is diagnosable
-    from the logs alone."""
+    register faulthandler for it) before a timed-out or failed job is torn down, so a hang is
+    diagnosable from the logs alone."""
     import signal
     live = [t for t in tasks if t.proc.poll() is None]
     for t in live:
@@ -81,11 +81,42 @@ def _dump_stacks(tasks):
         time.sleep(1.0)
 
 
+def log_tails(tasks, chars=6000):
+    """{task name: last ``chars`` characters of its log} (flushes the launcher's own notes)."""
+    out = {}
+    for t in tasks:
+        try:
+            t.log.flush()
+            with open(t.log.name, errors="replace") as f:
+                out[t.name] = f.read()[-chars:]
+        except (OSError, ValueError):
+            out[t.name] = "<log unreadable>"
+    return out
+
+
+class LaunchTimeout(subprocess.TimeoutExpired):
+    """The job did not finish within ``timeout_s``.  Unlike a bare TimeoutExpired its message
+    carries every task's log tail -- including the SIGUSR1 stack dumps of the tasks that were
+    still alive -- so a hang on a remote box is diagnosable from the failure alone."""
+
+    def __init__(self, cmd, timeout, tails, alive):
+        super().__init__(cmd, timeout)
+        self.tails, self.alive = tails, alive
+
+    def __str__(self):
+        parts = [super().__str__(), f"tasks still alive at the deadline: {self.alive}"]
+        for name, text in self.tails.items():
+            parts.append(f"===== {name} (log tail) =====\n{text}")
+        return "\n".join(parts)
+
+
 def _stop_others(tasks, failed, rc, grace_s=10.0):
-    """A rank of a collective world failed for good: SIGTERM the other live ranks, SIGKILL
-    whatever is still alive after ``grace_s`` (a rank stuck in a device-side wait may ignore the
-    first signal)."""
+    """A task failed for good: SIGTERM the other live tasks, SIGKILL whatever is still alive
+    after ``grace_s`` (a task stuck in a device-side wait may ignore the first signal).  Their
+    stacks are dumped into their logs first: where the survivors were is what a failure report
+    needs."""
     live = [x for x in tasks if x is not failed and x.proc.poll() is None]
+    _dump_stacks(live)
     for x in live:
         x.log.write(f"\n[launcher] {failed.name} failed for good (exit {rc}); stopping "
                     f"{x.name}\n")
@@ -110,7 +141,13 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart
     restarted without counting against ``max_restarts``.  Once a worker finished cleanly the job
     is ending and failures are no longer recovered.  ``restart_alone``: a collective world
     restarts a failed rank even when no other rank is alive (a one-rank world, or every rank
-    died): the restarted ranks resume from the chief's latest checkpoint."""
+    died): the restarted ranks resume from the chief's latest checkpoint.
+
+    A task that fails FOR GOOD while the job is not ending (restarts used up, or nobody left to
+    re-form the cluster with) ends the job at once: the other tasks could only wait for it until
+    their own timeouts, so they are stopped (stacks dumped into their logs first) and the exit
+    codes report the failure.  At ``timeout_s`` every live task's stack is dumped and
+    :class:`LaunchTimeout` is raised with all log tails in its message."""
     from .rendezvous import bump_epoch
     from .server import Server
     t0 = time.time()
@@ -119,7 +156,7 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart
         ending = any(t.done for t in tasks if is_worker(t))
         for t in tasks:
             rc = t.proc.poll()
-            if rc is None or t.done:
+            if rc is None or t.done or getattr(t, "final", False):
                 continue
             if rc == 0:
                 t.done = True
@@ -128,11 +165,11 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart
             voluntary = rc == Server.REJOIN_EXIT_CODE
             if ending or not (workers_alive or not is_worker(t) or restart_alone) or \
                     (not voluntary and used >= max_restarts):
-                # final: reported as its exit code.  In a collective world the other ranks can
-                # never finish without it (they would wait in a collective until their own
-                # timeouts): end the job now, loudly, instead of waiting for the launcher's
-                if restart_alone and not ending and not getattr(t, "final", False):
-                    t.final = True
+                t.final = True
+                if not ending:
+                    t.log.write(f"\n[launcher] {t.name} (pid {t.proc.pid}) exited with {rc} "
+                                f"and is not restarted ({used}/{max_restarts} restarts used)\n")
+                    t.log.flush()
                     _stop_others(tasks, t, rc)
                 continue
             if not voluntary:
@@ -148,14 +185,15 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart
             t.restarts += 1
             t.start()
         workers = [t for t in tasks if is_worker(t)]
-        if all(t.proc.poll() is not None for t in workers):
-            failed = [t for t in workers if t.proc.returncode not in (0, None) and not t.done]
-            # a crashed worker may still be restarted above; finish when none is pending
-            if not failed or used >= max_restarts or any(t.done for t in workers):
-                return
+        # every worker exited, and each one either finished or failed for good (a failed task
+        # that is restarted is running again by now)
+        if all(t.proc.poll() is not None and (t.done or getattr(t, "final", False))
+               for t in workers):
+            return
         if time.time() - t0 > timeout_s:
+            alive = [t.name for t in tasks if t.proc.poll() is None]
             _dump_stacks(tasks)
-            raise subprocess.TimeoutExpired(script, timeout_s)
+            raise LaunchTimeout(script, timeout_s, log_tails(tasks), alive)
         time.sleep(0.1)
 
 

@@ -66,6 +66,29 @@ def bump_epoch(store):
     return int(store.add(EPOCH_KEY, 1))
 
 
+def recovery_timeout_s(default=120.0):
+    """Bound of every wait on the recovery path (the launcher's epoch bump, the other tasks
+    joining the new epoch, the chief re-seeding the parameter servers): ``DTF_RECOVERY_TIMEOUT_S``
+    (default 120 s).  Tests set it below their own budget so a stalled wait names itself."""
+    return float(os.environ.get("DTF_RECOVERY_TIMEOUT_S", "") or default)
+
+
+def arrive(store, epoch, rank, world_size, timeout_s, what="join"):
+    """Bounded arrival barrier of cluster epoch ``epoch`` before its process group is created:
+    the group's own rendezvous would wait out the store timeout (minutes) for a task that never
+    comes; this fails after ``timeout_s`` naming the ranks that did not arrive."""
+    store.set(f"g{epoch}/arrived/{rank}", "1")
+    store.add(f"g{epoch}/arrived_n", 1)
+    t0 = time.time()
+    while int(store.add(f"g{epoch}/arrived_n", 0)) < world_size:
+        if time.time() - t0 > timeout_s:
+            missing = [r for r in range(world_size)
+                       if not store.check([f"g{epoch}/arrived/{r}"])]
+            raise TimeoutError(f"{what}: waited {timeout_s:.0f} s for rank(s) {missing} of "
+                               f"{world_size} to join cluster epoch {epoch}")
+        time.sleep(0.02)
+
+
 def wait_for_epoch_after(store, epoch, timeout_s=120.0):
     """Block until the launcher moved the cluster past ``epoch`` (it bumps before restarting a
     task); bounded, so a peer death that nobody restarts fails instead of hanging."""

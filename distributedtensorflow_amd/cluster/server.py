@@ -84,6 +84,14 @@ class Server:
                 self.store = rendezvous.connect(self.timeout_s, self.host, self.port,
                                                 is_master=self.rank == 0)
             self.generation = rendezvous.current_epoch(self.store)
+            if rendezvous.store_address() is not None:
+                # launcher-hosted store: bounded arrival barrier first, so a task that never
+                # joins is named after the recovery timeout (epoch > 0: a re-formed cluster) or
+                # the start-up timeout instead of blocking inside the group's rendezvous
+                wait = (rendezvous.recovery_timeout_s() if self.generation > 0
+                        else self.timeout_s)
+                rendezvous.arrive(self.store, self.generation, self.rank, self.world_size, wait,
+                                  f"{self.job_name}:{self.task_index} (rank {self.rank})")
             rendezvous.init_group("gloo", self.rank, self.world_size, self.store,
                                   self.generation, self.timeout_s)
             if self.watcher is not None:
@@ -123,10 +131,13 @@ class Server:
         """True once the launcher restarted a task (the cluster moved to a new epoch)."""
         return self.watcher is not None and self.watcher.changed
 
-    def restart_group(self, timeout_s=120.0):
+    def restart_group(self, timeout_s=None):
         """Tear down this epoch's process group (a peer died) and join the next epoch; blocks
-        until every task -- including the restarted one -- has joined.  The wait for the
-        launcher's epoch bump is bounded: a death nobody restarts raises TimeoutError."""
+        until every task -- including the restarted one -- has joined.  Both waits (the
+        launcher's epoch bump, the other tasks' arrival) are bounded by ``timeout_s`` (default
+        ``DTF_RECOVERY_TIMEOUT_S``): a death nobody restarts raises TimeoutError."""
+        if timeout_s is None:
+            timeout_s = rendezvous.recovery_timeout_s()
         rendezvous.leave_group()
         rendezvous.wait_for_epoch_after(self.store, self.generation, timeout_s)
         self._started = False

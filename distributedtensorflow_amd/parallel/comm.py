@@ -99,6 +99,11 @@ class C10dComm:
             abort(self.group) if self.group is not None else abort()
 
     def close(self, abort=False):
+        """``abort``: the world broke (recovery) -- abort the process group's communicators
+        BEFORE leaving it, so nothing stays blocked on the dead peer; the watchdog callback is
+        unregistered only afterwards (a later trip could otherwise no longer reach it)."""
+        if abort:
+            self.abort()
         self.wd.remove_abort(self.abort)
 
 
@@ -158,13 +163,18 @@ class RcclComm:
         return f"rccl async error {r}" if r not in (0, 7) else None    # 7 = ncclInProgress
 
     def _issue(self, fn, *tensors, what="collective"):
+        """Enqueue ``fn(comm, stream)``.  The communicator handle is read and used under the
+        lock: the watchdog thread's :meth:`abort` cannot destroy it between the check and the
+        enqueue (it waits for the enqueue, then aborts -- the kernel sees the abort flag)."""
         self.wd.check()
-        if not self.comm:
-            from .strategy import CommError
-            raise CommError("rccl communicator was aborted")
         cur = torch.cuda.current_stream(self.device)
         self.stream.wait_stream(cur)            # the producers of the operands ran before issue
-        fn(self.stream.cuda_stream)
+        with self._lock:
+            comm = self.comm
+            if not comm:
+                from .strategy import CommError
+                raise CommError("rccl communicator was aborted")
+            fn(comm, self.stream.cuda_stream)
         for t in tensors:
             t.record_stream(self.stream)
         ev = torch.cuda.Event()
@@ -180,8 +190,8 @@ class RcclComm:
             raise TypeError(f"rccl: unsupported dtype {t.dtype}") from None
 
     def all_reduce(self, t, op="sum"):
-        return self._issue(lambda s: self.K.rccl_all_reduce(
-            self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), _OPS[op], s), t,
+        return self._issue(lambda c, s: self.K.rccl_all_reduce(
+            c, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), _OPS[op], s), t,
             what="all_reduce")
 
     @staticmethod
@@ -200,8 +210,8 @@ class RcclComm:
                 inp.data_ptr() + self.rank * out.numel() * out.element_size():
             raise ValueError("rccl reduce_scatter: in-place output must be the input's chunk "
                              f"{self.rank} (recvbuff == sendbuff + rank * count)")
-        return self._issue(lambda s: self.K.rccl_reduce_scatter(
-            self.comm, inp.data_ptr(), out.data_ptr(), out.numel(), self._dt(out), _OPS[op], s),
+        return self._issue(lambda c, s: self.K.rccl_reduce_scatter(
+            c, inp.data_ptr(), out.data_ptr(), out.numel(), self._dt(out), _OPS[op], s),
             out, inp, what="reduce_scatter")
 
     def all_gather(self, out, inp):
@@ -211,18 +221,18 @@ class RcclComm:
                 out.data_ptr() + self.rank * inp.numel() * inp.element_size():
             raise ValueError("rccl all_gather: in-place input must be the output's chunk "
                              f"{self.rank} (sendbuff == recvbuff + rank * count)")
-        return self._issue(lambda s: self.K.rccl_all_gather(
-            self.comm, inp.data_ptr(), out.data_ptr(), inp.numel(), self._dt(inp), s), out, inp,
+        return self._issue(lambda c, s: self.K.rccl_all_gather(
+            c, inp.data_ptr(), out.data_ptr(), inp.numel(), self._dt(inp), s), out, inp,
             what="all_gather")
 
     def reduce(self, t, dst, op="sum"):
-        return self._issue(lambda s: self.K.rccl_reduce(
-            self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), _OPS[op], dst, s), t,
+        return self._issue(lambda c, s: self.K.rccl_reduce(
+            c, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), _OPS[op], dst, s), t,
             what="reduce")
 
     def broadcast(self, t, src):
-        return self._issue(lambda s: self.K.rccl_broadcast(
-            self.comm, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), src, s), t,
+        return self._issue(lambda c, s: self.K.rccl_broadcast(
+            c, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), src, s), t,
             what="broadcast")
 
     def async_error(self):

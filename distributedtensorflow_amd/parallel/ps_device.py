@@ -555,22 +555,33 @@ class PSLink:
             return True
         try:
             os.kill(int(pid), 0)          # same host: signal 0 probes the PS task
-            return True
         except ProcessLookupError:
             return False
         except PermissionError:
             return True
+        # a SIGKILLed task stays a zombie until its parent (the launcher) reaps it, and signal 0
+        # still succeeds on a zombie: read its state
+        try:
+            with open(f"/proc/{int(pid)}/stat") as f:
+                state = f.read().rpartition(")")[2].split()[0]
+            return state not in ("Z", "X")
+        except (OSError, IndexError):
+            return True
 
-    def wait(self):
+    def wait(self, cancelled=None):
         """The owner's answer (new global step).  Sleeps on the futex in 200 ms slices and
         probes the owner process between them, so a dead PS surfaces as ConnectionError at once
-        (MonitoredTrainingSession recovers from it) instead of after the full timeout."""
+        (MonitoredTrainingSession recovers from it) instead of after the full timeout.
+        ``cancelled()`` True (the pipelined plane's recovery) ends the wait at the next slice."""
         waited = 0
         while True:
             r = self.ctl.wait_done(self.w, 200)
             if r is not None:
                 return int(r)
             waited += 200
+            if cancelled is not None and cancelled():
+                raise ConnectionError(f"wait for parameter server {self.ps_index}'s answer "
+                                      f"cancelled (the cluster is re-forming)")
             if not self._owner_alive():
                 raise ConnectionError(f"parameter server {self.ps_index} (pid "
                                       f"{self.desc.get('pid')}) died")

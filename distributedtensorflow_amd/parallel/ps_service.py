@@ -453,15 +453,28 @@ class PSClient:
                 dist.send(sv, rank, group=self.group)
 
     @comm_call
-    def wait_ready(self, params):
-        """Non-chief: block until the chief initialised every PS shard (TF WorkerSessionCreator)."""
+    def wait_ready(self, params, timeout_s=None):
+        """Non-chief: block until the chief initialised every PS shard (TF WorkerSessionCreator).
+        ``timeout_s`` bounds the wait (recovery: ``DTF_RECOVERY_TIMEOUT_S``) with an error that
+        says which shard never became ready."""
+        import datetime
         self._layout(params)
         for rank in self.ps_ranks:
             dist.send(_hdr(OP_WAIT_READY, dist.get_rank()), rank, group=self.group)
         descs = []
-        for rank in self.ps_ranks:
+        for k, rank in enumerate(self.ps_ranks):
             r = torch.zeros(HDR, dtype=torch.int64)
-            dist.recv(r, rank, group=self.group)
+            if timeout_s is None:
+                dist.recv(r, rank, group=self.group)
+            else:
+                try:
+                    dist.irecv(r, rank, group=self.group).wait(
+                        datetime.timedelta(seconds=float(timeout_s)))
+                except RuntimeError as e:
+                    if "Timed out" not in str(e):
+                        raise
+                    raise TimeoutError(f"parameter server {k} (rank {rank}) was not initialised "
+                                       f"by the chief within {float(timeout_s):.0f} s") from e
             self.global_step = max(self.global_step, int(r[1]))
             descs.append(json.loads(_recv_bytes(rank, self.group).decode()) if int(r[2]) else None)
         if all(d is not None for d in descs) and descs:

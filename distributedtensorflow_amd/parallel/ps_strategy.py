@@ -34,28 +34,48 @@ class _RemotePSReducer(_NullReducer):
     """Between-graph: push the gradients at step end; the reply carries the updated variables
     (so the NEXT forward pass reads fresh values — TF's read-at-step-start semantics).
 
-    **Pipelined async push/pull** (device data plane, async mode, GPU; ``DTF_PS_PIPELINE=0``
-    turns it off).  The serial form -- compute, full device sync, copy into the mailbox, post,
-    wait for the owner's answer, copy the variables back -- leaves the GPU idle while the host
-    waits, and at 8 workers over xGMI the 2 x 102 MB of ResNet-50 traffic per step becomes real
-    time.  Pipelined, nothing on the worker's compute stream waits for the host:
+    **Pipelined async push/pull** (device data plane -- HBM shard over hipIpc, or a /dev/shm
+    shard for CPU tasks --, async mode; ``DTF_PS_PIPELINE=0`` turns it off).  The serial form --
+    compute, full device sync, copy into the mailbox, post, wait for the owner's answer, copy
+    the variables back -- leaves the GPU idle while the host waits, and at 8 workers over xGMI
+    the 2 x 102 MB of ResNet-50 traffic per step becomes real time.  Pipelined, nothing on the
+    worker's compute stream waits for the host:
 
     * **push from the backward hooks**: the gradient buffer is cut into buckets (as for the
       all-reduce); the moment a bucket's last gradient lands, its mailbox copies are enqueued on
       a side stream behind an event of the compute stream, overlapped with the rest of backward;
     * **post / answer on a comm thread**: ``apply_remote`` records the push-complete event and
-      hands (event, step) to a thread that waits for it, posts to every owner and waits for the
-      answers -- the main thread goes straight on to issue the next step;
+      hands (event, step) to this generation's comm thread, which waits for it, posts to every
+      owner and waits for the answers -- the main thread goes straight on to issue the next step;
     * **pull fenced per bucket into the next forward**: the first op of the next forward that
       reads a bucket's variables (``ops`` parameter fence + a module forward pre-hook) waits for
-      the answer (host), enqueues every bucket's pull copy on the side stream in FORWARD order
-      with one event each, and makes the compute stream wait only for ITS bucket: the late
-      layers' variables keep streaming in while the early layers compute.
+      the answer (host, bounded), enqueues every bucket's pull copy on the side stream in
+      FORWARD order with one event each, and makes the compute stream wait only for ITS bucket:
+      the late layers' variables keep streaming in while the early layers compute.
+
+    The stream/event operations go through :class:`_Streams`: HIP streams and events on a GPU,
+    an ordered-synchronous stand-in on the CPU, so the same state machine (including recovery,
+    :meth:`reset_pipeline`) runs -- and is tested -- on CPU tasks with the /dev/shm plane.
+
+    **Generations.**  A recovery (a PS died; the cluster re-forms) calls :meth:`reset_pipeline`
+    BEFORE leaving the old process group: the push in flight is cancelled (its answer wait
+    checks the flag every 200 ms slice) and joined with a deadline, the side stream is drained,
+    the comm thread of the old generation is retired (a new one serves the next generation, so
+    a push stuck on the old control block can never delay a new one) and the module pre-hook
+    is removed (one hook per live generation, never one per recovery).
+
+    **Gradients modified after backward** (clipping between ``compute_gradients`` and
+    ``apply_gradients``): the gradient buffer's version counter is recorded when the last bucket
+    was pushed; ``apply_remote`` re-copies every bucket when it moved, so the owner always gets
+    the gradients as they are at apply time, like the serial data plane.
 
     Semantics are the reference's (``run_mnist_distributed.py:107-116,150,161``): a worker's
     next forward reads the variables after its own update was applied (plus whatever other
-    workers applied meanwhile, Hogwild).  The global step the worker sees lags by the one push
-    still in flight; ``drain()`` completes it."""
+    workers applied meanwhile, Hogwild).  The global step ``apply_remote`` reports is the one
+    the push in flight will at least produce: exact with one worker, a lower bound with more
+    (the serial form's answer also counts other workers' pushes applied meanwhile), so with N
+    workers ``StopAtStepHook`` may let a worker run one step more than the serial plane would;
+    ``drain()`` completes the push and makes the step exact."""
 
     applies_update = True
 
@@ -74,23 +94,27 @@ class _RemotePSReducer(_NullReducer):
             for i in mem:
                 space.order[i]._dtf_gbucket = b
         self._pre_hook = None
-        self.stream = None
+        self._streams = None
+        self._comm = None            # this generation's comm thread
         self._job = None             # the push in flight: a _PushJob
         self._pull_events = None     # per bucket, after the answer: event of its pull copy
         self._fenced = 0
+        self._pushed_version = None  # space.grad._version when the last bucket was pushed
+        self.generation = 0
         self.timing = {"fence_ms": [], "answer_ms": []}
+        self.repushed = 0            # steps whose gradients changed after backward pushed them
 
     # -- mode
     def pipelined(self):
         if self._pipe is None:
-            import os
             c = self.client
-            self._pipe = bool(c.links) and not self.sync and self.space.device.type == "cuda" \
-                and os.environ.get("DTF_PS_PIPELINE", "1") != "0"
+            self._pipe = bool(c.links) and not self.sync and pipeline_enabled(self.space.device)
             if self._pipe:
-                self.stream = torch.cuda.Stream(self.space.device)
-                from torch.nn.modules.module import register_module_forward_pre_hook
-                self._pre_hook = register_module_forward_pre_hook(self._module_fence)
+                self._streams = _Streams(self.space.device)
+                self._comm = _CommThread(f"dtf-ps-push-g{self.generation}")
+                if self._pre_hook is None:
+                    from torch.nn.modules.module import register_module_forward_pre_hook
+                    self._pre_hook = register_module_forward_pre_hook(self._module_fence)
         return self._pipe
 
     # -- push (backward)
@@ -99,6 +123,7 @@ class _RemotePSReducer(_NullReducer):
             self.drain()
             self.pending = [len(m) for (_, _, m) in self.buckets]
             self.launched = [False] * len(self.buckets)
+            self._pushed_version = None
 
     def _make_hook(self, i):
         def hook(_p):
@@ -110,15 +135,18 @@ class _RemotePSReducer(_NullReducer):
                 self._push_bucket(b)
         return hook
 
-    def _push_bucket(self, b):
-        if self.launched[b]:
+    def _push_bucket(self, b, force=False):
+        if self.launched[b] and not force:
             return
         self.launched[b] = True
         s, e, _ = self.buckets[b]
-        self.stream.wait_stream(torch.cuda.current_stream(self.space.device))
-        with torch.cuda.stream(self.stream):
+        st = self._streams
+        st.side_waits_compute()
+        with st.side():
             for link in self.client.links:
                 link.copy_grads(self.space, s, e)
+        if all(self.launched):
+            self._pushed_version = self.space.grad._version
 
     def finish(self):
         if self._pipe:
@@ -136,40 +164,45 @@ class _RemotePSReducer(_NullReducer):
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._push_bucket(b)
-        ev = torch.cuda.Event()
-        ev.record(self.stream)
+        if self._pushed_version is not None and self.space.grad._version != self._pushed_version:
+            # the gradients were modified in place after backward pushed them (clipping, ...):
+            # the mailbox must hold what the serial plane would send -- copy every bucket again
+            self.repushed += 1
+            for b in range(len(self.buckets)):
+                self._push_bucket(b, force=True)
+        st = self._streams
+        ev = st.record()
         # the next step's zero_grad (compute stream) must not overwrite the gradient buffer
         # under the side stream's mailbox copies
-        torch.cuda.current_stream(self.space.device).wait_event(ev)
-        self._job = _PushJob(self.client, ev, self.client.global_step, self.timing)
+        st.compute_waits(ev)
+        self._job = _PushJob(list(self.client.links), ev, self.client.global_step, self.timing,
+                             self._comm)
         self._pull_events = None
         self._fenced = 0
         from .. import ops
         ops.set_param_fence(self._op_fence)
         # the answer to this push is still in flight: report the step it will at least produce
-        # (an async push advances the PS's global step by exactly one; the previous answer
-        # arrived at this step's first fence).  Exact with one worker, a lower bound with more --
-        # the serial form's answer would also count other workers' pushes applied meanwhile.
-        # StopAtStepHook then stops at the same step as the serial data plane.
-        return self.client.global_step + 1
+        # (an async push advances the PS's global step by exactly one), or the owner's current
+        # published step when other workers' pushes moved it further (one shared-memory read)
+        return max(self.client.global_step + 1, self.client.links[0].global_step)
 
     # -- pull (next forward)
     def _issue_pulls(self):
         job, self._job = self._job, None
         t0 = time.perf_counter()
-        job.result()                                    # raises the comm thread's error
+        self.client.global_step = job.result()          # raises the comm thread's error
         self.timing["fence_ms"].append((time.perf_counter() - t0) * 1e3)
         n = len(self.buckets)
         order = ([n - 1] + list(range(n - 2, -1, -1))) if self.space.decay_end < \
             self.space.numel else list(range(n - 1, -1, -1))
         events = [None] * n
-        with torch.cuda.stream(self.stream), torch.no_grad():
+        st = self._streams
+        with st.side(), torch.no_grad():
             for b in order:
                 s, e, _ = self.buckets[b]
                 for link in self.client.links:
                     link.pull(self.space, s, e)
-                events[b] = torch.cuda.Event()
-                events[b].record(self.stream)
+                events[b] = st.record()
         self._pull_events = events
 
     @comm_call
@@ -179,7 +212,7 @@ class _RemotePSReducer(_NullReducer):
         evs = self._pull_events
         if evs is None or evs[b] is None:
             return
-        torch.cuda.current_stream(self.space.device).wait_event(evs[b])
+        self._streams.compute_waits(evs[b])
         evs[b] = None
         self._fenced += 1
         if self._fenced == len(evs):
@@ -206,9 +239,31 @@ class _RemotePSReducer(_NullReducer):
             for b in range(len(self.buckets)):
                 self._wait_bucket(b)
 
-    def reset_pipeline(self):
-        """The cluster was re-formed (recovery): whatever was in flight went to the old PS."""
-        self._job, self._pull_events, self._pipe = None, None, None
+    def reset_pipeline(self, join_s=5.0):
+        """The cluster is being re-formed (recovery): whatever is in flight targets the old PS.
+        Cancel and join the push in flight (bounded), drain the side stream so no copy into the
+        old shard's mappings is still running, retire this generation's comm thread and detach
+        the fences and the module pre-hook.  The next ``apply_remote`` starts generation + 1."""
+        job, self._job = self._job, None
+        if job is not None and not job.cancel(join_s):
+            print(f"[dtf] pipelined push of global step {job.step} still blocked {join_s:g} s "
+                  f"after cancel; its comm thread is abandoned", flush=True)
+        if self._comm is not None:
+            self._comm.retire()
+            self._comm = None
+        if self._streams is not None:
+            self._streams.synchronize()
+            self._streams = None
+        self._pull_events, self._fenced, self._pipe = None, 0, None
+        self._pushed_version = None
+        # the interrupted step's buckets went to the old shard: the retried step (whose
+        # begin_step skips the reset while the mode is undecided) must push every bucket again
+        self.pending = [len(m) for (_, _, m) in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        if self._pre_hook is not None:
+            self._pre_hook.remove()
+            self._pre_hook = None
+        self.generation += 1
         from .. import ops
         ops.set_param_fence(None)
 
@@ -219,32 +274,87 @@ class _RemotePSReducer(_NullReducer):
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        if self._pre_hook is not None:
-            self._pre_hook.remove()
-            self._pre_hook = None
         for v in self.space.order:
             v._dtf_gbucket = None
 
 
-class _PushJob:
-    """One pipelined push on the comm thread: wait for the mailbox copies, post to every owner,
-    wait for their answers (the new global step)."""
+def pipeline_enabled(device):
+    """``DTF_PS_PIPELINE``: unset = on (GPU and CPU tasks), ``0`` = the serial data plane."""
+    return os.environ.get("DTF_PS_PIPELINE", "1") != "0"
 
-    def __init__(self, client, event, step, timing):
-        self.client, self.event, self.step, self.timing = client, event, step, timing
+
+class _DoneEvent:
+    """CPU stand-in for a HIP event: CPU copies have completed when they return."""
+
+    @staticmethod
+    def synchronize():
+        pass
+
+    @staticmethod
+    def query():
+        return True
+
+
+class _Streams:
+    """Stream/event operations of the pipelined data plane: a HIP side stream and events on a
+    GPU; on a CPU task every copy is synchronous and in program order, so the side stream is
+    the caller's thread and every event is complete when recorded."""
+
+    def __init__(self, device):
+        self.device = device
+        self.cuda = device.type == "cuda"
+        self.stream = torch.cuda.Stream(device) if self.cuda else None
+
+    def side(self):
+        import contextlib
+        return torch.cuda.stream(self.stream) if self.cuda else contextlib.nullcontext()
+
+    def side_waits_compute(self):
+        if self.cuda:
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+
+    def record(self):
+        if not self.cuda:
+            return _DoneEvent()
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
+    def compute_waits(self, ev):
+        if self.cuda:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def synchronize(self):
+        if self.cuda:
+            self.stream.synchronize()
+
+
+class _PushJob:
+    """One pipelined push on a generation's comm thread: wait for the mailbox copies, post to
+    every owner, wait for their answers (the new global step).  ``cancel`` makes the answer
+    wait give up at its next 200 ms slice; ``result`` is bounded by the links' own deadline."""
+
+    def __init__(self, links, event, step, timing, thread):
+        self.links, self.event, self.step, self.timing = links, event, step, timing
         self._done = threading.Event()
+        self._cancelled = threading.Event()
         self._error = None
+        self._step_out = None
         self._t0 = time.perf_counter()
-        _comm_pool().submit(self._run)
+        # the answer waits give up at the links' deadline; the host wait here a little later
+        self.deadline_s = max((lk.timeout_ms for lk in links), default=0) / 1000.0 + 10.0
+        thread.submit(self._run)
 
     def _run(self):
         try:
+            if self._cancelled.is_set():
+                raise ConnectionError(f"push of global step {self.step} cancelled before "
+                                      f"posting (the cluster is re-forming)")
             self.event.synchronize()
-            links = self.client.links
-            for link in links:
+            for link in self.links:
                 link.post(self.step)
-            steps = [link.wait() for link in links]
-            self.client.global_step = steps[0]
+            steps = [link.wait(cancelled=self._cancelled.is_set) for link in self.links]
+            self._step_out = steps[0]
             self.timing["answer_ms"].append((time.perf_counter() - self._t0) * 1e3)
         except BaseException as e:      # re-raised on the main thread at the fence
             self._error = e
@@ -252,37 +362,42 @@ class _PushJob:
             self._done.set()
 
     def result(self):
-        self._done.wait()
+        if not self._done.wait(self.deadline_s):
+            raise TimeoutError(f"pipelined push of global step {self.step}: no answer from the "
+                               f"parameter server(s) within {self.deadline_s:.0f} s")
         if self._error is not None:
             raise self._error
+        return self._step_out
+
+    def cancel(self, join_s):
+        """Cancel and wait up to ``join_s`` for the comm thread to let go; True when it did."""
+        self._cancelled.set()
+        return self._done.wait(join_s)
 
 
 class _CommThread:
-    """One DAEMON thread running the pipelined pushes in order (a ThreadPoolExecutor's workers
-    are joined at interpreter exit: a push whose answer never comes would hang the exit)."""
+    """One DAEMON thread running one generation's pipelined pushes in order (a
+    ThreadPoolExecutor's workers are joined at interpreter exit: a push whose answer never comes
+    would hang the exit).  ``retire`` ends it after the job it is running."""
 
-    def __init__(self):
+    def __init__(self, name="dtf-ps-push"):
         import queue
         self.q = queue.Queue()
-        self.t = threading.Thread(target=self._run, name="dtf-ps-push", daemon=True)
+        self.t = threading.Thread(target=self._run, name=name, daemon=True)
         self.t.start()
 
     def _run(self):
         while True:
-            self.q.get()()
+            fn = self.q.get()
+            if fn is None:
+                return
+            fn()
 
     def submit(self, fn):
         self.q.put(fn)
 
-
-_POOL = None
-
-
-def _comm_pool():
-    global _POOL
-    if _POOL is None:
-        _POOL = _CommThread()
-    return _POOL
+    def retire(self):
+        self.q.put(None)
 
 
 def _bucket_plan(space, bucket_bytes):
@@ -599,7 +714,7 @@ class ParameterServerStrategy(Strategy):
             dist.broadcast(space.master, 0)
             space.refresh_shadow()
 
-    def register_with_ps(self, optimizer, global_step=0, restored_slots=False):
+    def register_with_ps(self, optimizer, global_step=0, restored_slots=False, timeout_s=None):
         """Chief: ship variables + optimizer config (+ the optimizer slots just restored from a
         checkpoint) to the PS shards; others: wait for it."""
         if self.mode != "between_graph":
@@ -614,7 +729,7 @@ class ParameterServerStrategy(Strategy):
                                   replicas_to_aggregate=self.replicas_to_aggregate,
                                   global_step=int(global_step), slots=slots,
                                   iterations=optimizer.iterations if restored_slots else None)
-        self._client.wait_ready(params)
+        self._client.wait_ready(params, timeout_s)
         self._client.pull()          # every worker starts from the PS values
 
     def recover_cluster(self, optimizer):
@@ -638,17 +753,19 @@ class ParameterServerStrategy(Strategy):
                 optimizer._reducer = self.make_gradient_reducer(optimizer.space)
                 self.broadcast_space(optimizer.space)     # mirrors the restarted rank's build
             return epoch
+        reducer = getattr(optimizer, "_reducer", None)
+        if reducer is not None and hasattr(reducer, "reset_pipeline"):
+            # before leaving the group: cancel + join the push in flight (it targets the dead
+            # generation's control block), drain the side stream, retire the comm thread
+            reducer.reset_pipeline()
         self.server.restart_group()
         from .ps_service import PSClient
         old = self._client
         self._client = PSClient(self.server.ps_ranks(), policy=self.variable_placement,
                                 space=old.space, data_plane=self.data_plane,
                                 single_host=self.server.cluster.single_host())
-        reducer = getattr(optimizer, "_reducer", None)
         if reducer is not None and hasattr(reducer, "client"):
             reducer.client = self._client
-            if hasattr(reducer, "reset_pipeline"):
-                reducer.reset_pipeline()
         return self.server.generation
 
     @property

@@ -484,11 +484,16 @@ def init_process_group_from_env(backend=None, timeout_s=None):
     kw = {}
     if backend == "nccl":
         kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    # ``timeout_s`` is the DTF watchdog's per-collective deadline.  The process group's own
+    # timeout is strictly larger: under TORCH_NCCL_ASYNC_ERROR_HANDLING c10d's
+    # watchdog tears the whole process down when it fires, so it must never win the race against
+    # the controlled abort that turns a hung peer into a recoverable CommError.
+    pg_timeout_s = pg_timeout_for(timeout_s)
     from ..cluster import rendezvous
     if rendezvous.store_address() is not None:
         store = rendezvous.connect(timeout_s)
         epoch = rendezvous.current_epoch(store)
-        rendezvous.init_group(backend, rank, world, store, epoch, timeout_s, **kw)
+        rendezvous.init_group(backend, rank, world, store, epoch, pg_timeout_s, **kw)
         if _collective_watcher is not None:
             _collective_watcher.stop()
         _collective_watcher = rendezvous.EpochWatcher(epoch).start()
@@ -501,7 +506,7 @@ def init_process_group_from_env(backend=None, timeout_s=None):
     if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
         # torchrun: its agent already hosts the store and ran the rendezvous
         dist.init_process_group(backend, rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+                                timeout=datetime.timedelta(seconds=pg_timeout_s), **kw)
         return
     # the rendezvous waits for every rank's process to START (imports, device init): bound it
     # separately from the collective deadline, which may be seconds (DTF_COMM_TIMEOUT_S)
@@ -509,7 +514,13 @@ def init_process_group_from_env(backend=None, timeout_s=None):
     store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
                           rank == 0, timeout=datetime.timedelta(seconds=rdv_s))
     dist.init_process_group(backend, store=store, rank=rank, world_size=world,
-                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+                            timeout=datetime.timedelta(seconds=pg_timeout_s), **kw)
+
+
+def pg_timeout_for(deadline_s):
+    """Process-group timeout for a watchdog deadline: ``max(2 x deadline, deadline + 60 s)``."""
+    d = float(deadline_s)
+    return max(2.0 * d, d + 60.0)
 
 
 def collective_cluster_changed():

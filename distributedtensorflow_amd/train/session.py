@@ -431,7 +431,9 @@ class MonitoredTrainingSession:
             if self.is_chief and ckpt and sc.saver is not None:
                 sc.saver.restore(None, ckpt, strict=False)
                 restored = True
-            strat.register_with_ps(sc.optimizer, sc.global_step.value(), restored_slots=restored)
+            from ..cluster import rendezvous
+            strat.register_with_ps(sc.optimizer, sc.global_step.value(), restored_slots=restored,
+                                   timeout_s=rendezvous.recovery_timeout_s())
             client = getattr(strat, "ps_client", None)
             if client is not None:
                 sc.global_step.assign(client.global_step)

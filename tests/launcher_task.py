@@ -1,0 +1,35 @@
+"""A task script for tests/test_launcher.py: takes the launcher's flags and misbehaves as told by
+``LAUNCHER_TASK_MODE`` (no GPU, no process group)."""
+import argparse
+import faulthandler
+import os
+import signal
+import sys
+import time
+
+
+def stalled_wait():
+    # a recognisable frame for the stack dump
+    time.sleep(600)
+
+
+def main():
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--job_name")
+    ap.add_argument("--task_index", type=int)
+    ap.add_argument("--config")
+    a, _ = ap.parse_known_args()
+    mode = os.environ.get("LAUNCHER_TASK_MODE", "ok")
+    print(f"task {a.job_name}:{a.task_index} mode {mode}", flush=True)
+    if mode == "hang" and a.job_name == "worker" and a.task_index == 1:
+        stalled_wait()
+    if mode == "ps_fail":
+        if a.job_name == "ps":
+            sys.exit(3)
+        stalled_wait()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

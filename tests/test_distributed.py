@@ -351,7 +351,8 @@ def test_collective_rank_killed_world_reforms_and_resumes(tmp_path, strategy):
         assert torch.equal(res[0]["state"][k], res[1]["state"][k]), k
 
 
-def test_ps_killed_mid_run_is_restarted_and_training_resumes(tmp_path, mnist_dir):
+@pytest.mark.parametrize("pipeline", ["0", "1"], ids=["serial", "pipelined"])
+def test_ps_killed_mid_run_is_restarted_and_training_resumes(tmp_path, mnist_dir, pipeline):
     """Real failure recovery (reference run_mnist_distributed.py:146): the PS task
     dies (SIGKILL at global step 25, DTF_FAULT_KILL_PS_AT_STEP), the launcher restarts it as a
     fresh process, every task joins the next process-group generation, the chief restores the
@@ -364,7 +365,10 @@ def test_ps_killed_mid_run_is_restarted_and_training_resumes(tmp_path, mnist_dir
                                 f"--log_dir={tmp_path}/tb", "--batch_size=32",
                                 f"--checkpoint_dir={ckpt}", "--save_checkpoint_steps=10"],
                                env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2",
-                                    "DTF_FAULT_KILL_PS_AT_STEP": "25"},
+                                    "DTF_FAULT_KILL_PS_AT_STEP": "25",
+                                    "DTF_PS_PIPELINE": pipeline,
+                                    # every recovery wait bounded well below the job budget
+                                    "DTF_RECOVERY_TIMEOUT_S": "60", "DTF_PS_TIMEOUT_S": "60"},
                                timeout_s=300, max_ps_restarts=1)
     text = {k: open(v).read() for k, v in logs.items()}
     assert all(c == 0 for c in codes.values()), {k: t[-3000:] for k, t in text.items()}
@@ -405,7 +409,9 @@ def test_bench_ps_async_flow_cpu(tmp_path):
     assert set(cfg["worker_host_ms_per_step"]) == {"copy_sync_ms_per_step", "wait_ms_per_step",
                                                    "pull_ms_per_step", "fence_ms_per_step",
                                                    "answer_ms_per_step"}
-    assert cfg["pipelined_push_pull"] is False         # the shm plane on CPU stays serial
+    # the /dev/shm plane on CPU runs the pipelined push/pull state machine too (CPU stand-ins for
+    # the side stream and its events)
+    assert cfg["pipelined_push_pull"] is True
 
 
 @pytest.mark.parametrize("kind,args", [("mirrored", ("bucket_mb=0.05",)),

@@ -59,10 +59,15 @@ def test_sync_replicas_ps_hbm_shard_ipc(tmp_path):
     assert stats["applied"] == stats["global_step"] >= 30
 
 
-def test_ps_killed_on_gpu_restarts_and_resumes(tmp_path):
+@pytest.mark.parametrize("pipeline", ["0", "1"], ids=["serial", "pipelined"])
+def test_ps_killed_on_gpu_restarts_and_resumes(tmp_path, pipeline):
     """The recovery path on the HBM data plane: the PS dies holding its exported HBM shard,
     the launcher restarts it, the workers drop their hipIpc mappings, join generation 1 and the
-    chief re-seeds the new shard from the latest checkpoint."""
+    chief re-seeds the new shard from the latest checkpoint -- with the serial and with the
+    pipelined push/pull (whose push in flight is cancelled and joined before leaving the old
+    generation).  Every recovery wait is bounded below the job budget (DTF_RECOVERY_TIMEOUT_S,
+    DTF_PS_TIMEOUT_S), so a stall names itself in a task log instead of outlasting the launcher,
+    and a launcher timeout raises with every task's log tail and stacks in its message."""
     from distributedtensorflow_amd.cluster.launcher import launch_local
     ckpt = tmp_path / "ckpt"
     codes, logs = launch_local(os.path.join(ROOT, "run_mnist_distributed.py"), 1, 2,
@@ -70,7 +75,9 @@ def test_ps_killed_on_gpu_restarts_and_resumes(tmp_path):
                                ["--max_steps=60", f"--data_dir={tmp_path}/data",
                                 f"--log_dir={tmp_path}/tb", "--ps_device=gpu",
                                 f"--checkpoint_dir={ckpt}", "--save_checkpoint_steps=10"],
-                               env={"PYTHONPATH": ROOT, "DTF_FAULT_KILL_PS_AT_STEP": "30"},
+                               env={"PYTHONPATH": ROOT, "DTF_FAULT_KILL_PS_AT_STEP": "30",
+                                    "DTF_PS_PIPELINE": pipeline,
+                                    "DTF_RECOVERY_TIMEOUT_S": "45", "DTF_PS_TIMEOUT_S": "45"},
                                timeout_s=150, grace_s=20, max_ps_restarts=1)
     text = {k: open(v).read() for k, v in logs.items()}
     assert all(c == 0 for c in codes.values()), {k: t[-2500:] for k, t in text.items()}

@@ -175,7 +175,7 @@ def _fake_rccl(rank, world):
     c = object.__new__(RcclComm)
     c.K, c.rank, c.world, c.comm = K(), rank, world, 1
     c.wd = CommWatchdog(timeout_s=100)
-    c._issue = lambda fn, *t, what="": fn(0)
+    c._issue = lambda fn, *t, what="": fn(c.comm, 0)
     return c, K.calls
 
 
