@@ -123,6 +123,57 @@ def _rccl_version():
         return None
 
 
+def _rccl_debug_file():
+    """N > 1 on RCCL: have the communicator log its INIT lines to a per-rank file (unless the
+    user set NCCL_DEBUG), so the JSON can carry the channel count RCCL itself reports."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or "NCCL_DEBUG" in os.environ or \
+            os.environ.get("DTF_BENCH_BACKEND", "nccl") != "nccl":
+        return None
+    path = f"/tmp/dtf_rccl_init_{os.getpid()}.log"
+    os.environ.update({"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT",
+                       "NCCL_DEBUG_FILE": path})
+    return path
+
+
+def _rccl_channels(path):
+    """Channel count from RCCL's own INIT log: '<n> coll channels' (NCCL >= 2.12 format), else
+    the ring count of its 'Channel NN/MM' lines; None when unavailable."""
+    import re
+    if not path or not os.path.exists(path):
+        return None
+    text = open(path, errors="replace").read()
+    m = re.findall(r"(\d+) coll channels", text)
+    if m:
+        return int(m[-1])
+    m = re.findall(r"Channel \d+/(\d+)", text)
+    return int(m[-1]) if m else None
+
+
+def rank_diagnostics(elapsed, steps, comm_info, reducer, dev, rccl_log):
+    """Collective (N > 1): per-rank step time, bucket plan / issue-order hashes, exposed comm
+    time and RCCL channel count, gathered on every rank; rank 0 reports them and the order
+    check has already failed the run if the ranks disagree (verify_bucket_agreement)."""
+    from distributedtensorflow_amd.parallel.strategy import _digest
+    plan = reducer.plan() if reducer is not None and hasattr(reducer, "plan") else None
+    order = tuple(getattr(reducer, "last_order", ()))
+    ch = _rccl_channels(rccl_log)
+    mine = torch.tensor([elapsed / steps * 1e3, float(comm_info.get("exposed_ms_per_step", 0.0)),
+                         float(len(plan["buckets"]) if plan else 0),
+                         float(_digest(plan) % (1 << 52)), float(_digest(order) % (1 << 52)),
+                         float(ch if ch is not None else -1)], dtype=torch.float64, device=dev)
+    out = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, mine)
+    rows = [o.tolist() for o in out]
+    ms = [round(r[0], 3) for r in rows]
+    return {"ms_per_step_min": min(ms), "ms_per_step_max": max(ms), "ms_per_step": ms,
+            "exposed_comm_ms_per_step": [round(r[1], 3) for r in rows],
+            "buckets": [int(r[2]) for r in rows],
+            "plan_hash": [f"{int(r[3]):013x}" for r in rows],
+            "order_hash": [f"{int(r[4]):013x}" for r in rows],
+            "issue_order_rank0": list(order) if dist.get_rank() == 0 else None,
+            "rccl_channels": [int(r[5]) if r[5] >= 0 else None for r in rows]}
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -438,6 +489,7 @@ def main():
     # DTF_FORCE_REDUCER=1 (parallel/strategy.py): a one-rank torchrun run still builds the
     # process group and the communicating reducer, so every RCCL call of the N > 1 path runs
     force = os.environ.get("DTF_FORCE_REDUCER", "0") == "1"
+    rccl_log = _rccl_debug_file()
     if (world > 1 or force) and not dist.is_initialized():
         from distributedtensorflow_amd.parallel import init_process_group_from_env
         # RCCL (backend "nccl") is the measured path; DTF_BENCH_BACKEND=gloo exists only for the
@@ -515,6 +567,15 @@ def main():
     sync()
     log(f"warmup {args.warmup} steps in {time.time() - t0:.1f}s, loss={float(loss):.4f}")
 
+    # every rank must have built the same bucket plan and issued the warm-up's bucket
+    # collectives in the same order; a mismatch fails the run here (rank 0 non-zero)
+    red0 = getattr(opt_for_stats, "_reducer", None)
+    if dist.is_initialized() and dist.get_world_size() > 1 and hasattr(red0, "plan"):
+        from distributedtensorflow_amd.parallel import verify_bucket_agreement
+        try:
+            verify_bucket_agreement(red0)
+        except RuntimeError as e:
+            fail(str(e), code=3)
     bucket_tune = None
     if args.bucket_auto and dist.is_initialized() and hasattr(getattr(opt_for_stats, "_reducer", None), "close"):
         bucket_tune = tune_buckets(args, opt_for_stats, strategy, step, images, labels, sync, dev)
@@ -547,6 +608,12 @@ def main():
         opt_for_stats.synchronize_variables()
         if rank == 0:
             torch.save(opt_for_stats.space.master.detach().cpu(), args.dump_master)
+    ranks_info = None
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        ranks_info = rank_diagnostics(elapsed, args.steps, comm_info, reducer, dev, rccl_log)
+        if len(set(ranks_info["order_hash"])) > 1 or len(set(ranks_info["plan_hash"])) > 1:
+            fail(f"bucket plan / issue order differs across ranks: {ranks_info}", code=3)
+        comm_info["ranks"] = ranks_info
     if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -481,6 +481,7 @@ class _ColocatedPSReducer(BucketedAllReduce):
         if self.launched[b]:
             return
         self.launched[b] = True
+        self.launch_log.append(b)
         g = self.space.grad
         if self.sharded:
             s, e, _ = self.buckets[b]

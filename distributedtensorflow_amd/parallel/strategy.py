@@ -200,6 +200,14 @@ class BucketedAllReduce:
         self.works = []
         self.launched = [False] * len(ranges)
         self.stats = CommStats(len(ranges), [(e - s) * 4 for s, e, _ in ranges])
+        # collective issue order of the current / last completed step: every rank must issue
+        # the same buckets in the same order (verify_bucket_agreement)
+        self.launch_log = []
+        self.last_order = ()
+        # fault injection for the order check (tests): this rank defers every bucket to finish()
+        # and issues them in reverse
+        self._perturb = os.environ.get("DTF_DEBUG_PERTURB_BUCKET_ORDER", "") == \
+            str(dist.get_rank(group))
         self._hooks = []
         for i, v in enumerate(order):
             if overlap:
@@ -223,7 +231,7 @@ class BucketedAllReduce:
         def hook(_p):
             b = self.var_bucket[i]
             self.pending[b] -= 1
-            if self.pending[b] == 0:
+            if self.pending[b] == 0 and not self._perturb:
                 self._launch(b)
         return hook
 
@@ -232,6 +240,7 @@ class BucketedAllReduce:
         if self.launched[b]:
             return
         self.launched[b] = True
+        self.launch_log.append(b)
         s, e, _ = self.buckets[b]
         view = self.space.grad[s:e]
         if self.compress:
@@ -255,6 +264,13 @@ class BucketedAllReduce:
         self.pending = [len(m) for (_, _, m) in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.works = []
+        self.launch_log = []
+
+    def plan(self):
+        """The bucket plan as plain data: [(start, end, n_variables)] + the per-bucket owner
+        pieces of a parameter-server reducer (reduce-scatter / all-gather chunk offsets)."""
+        return {"buckets": [(s, e, len(m)) for s, e, m in self.buckets],
+                "pieces": [list(p) for p in getattr(self, "pieces", [])]}
 
     def _timing_begin(self):
         st = self.stats
@@ -291,9 +307,11 @@ class BucketedAllReduce:
         st.last_early = early
         t0 = self._timing_begin()
         # buckets whose variables received no gradient this step still have to be reduced
-        for b in range(len(self.buckets)):
+        for b in (range(len(self.buckets) - 1, -1, -1) if self._perturb
+                  else range(len(self.buckets))):
             if not self.launched[b]:
                 self._launch(b)
+        self.last_order = tuple(self.launch_log)
         gathers = []
         for w, view, extra in self.works:
             w.wait()
@@ -447,6 +465,32 @@ def _broadcast_training_state(active, optimizer, global_step=None, src=0, restor
     if global_step is not None and hasattr(global_step, "assign"):
         global_step.assign(int(meta[1]))
     sp.refresh_shadow()
+
+
+def _digest(obj):
+    import hashlib
+    return int.from_bytes(hashlib.sha1(repr(obj).encode()).digest()[:7], "little")
+
+
+def verify_bucket_agreement(reducer, group=None):
+    """Collective: every rank's bucket plan (bucket ranges, owner pieces) and the issue order of
+    its last step's bucket collectives must be identical -- NCCL / RCCL match collectives by
+    issue order, so a rank that issues them in another order sums the wrong buckets (or hangs).
+    Returns the per-rank record [(n_buckets, plan_hash, order_hash)]; raises RuntimeError naming
+    the ranks that disagree with rank 0."""
+    plan = reducer.plan()
+    mine = (len(plan["buckets"]), _digest(plan), _digest(tuple(reducer.last_order)))
+    world = dist.get_world_size(group)
+    dev = reducer.space.grad.device
+    t = torch.tensor(mine, dtype=torch.int64, device=dev)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t, group=group)
+    recs = [tuple(int(v) for v in o.tolist()) for o in out]
+    bad = [r for r, rec in enumerate(recs) if rec != recs[0]]
+    if bad:
+        raise RuntimeError(f"bucket plan / collective order differs from rank 0 on rank(s) {bad}: "
+                           f"(buckets, plan hash, order hash) per rank = {recs}")
+    return recs
 
 
 _collective_watcher = None

@@ -125,11 +125,20 @@ def main():
                 early.append((st.last_early, st.n_buckets))
         mean_loss = float(strat.reduce(dtf.distribute.ReduceOp.MEAN, loss.detach()))
         fps = dtf.distribute.check_replicas_consistent(opt)      # raises if replicas diverged
+        red = opt._reducer
+        agreement = None
+        if hasattr(red, "plan") and world > 1:
+            from distributedtensorflow_amd.parallel import verify_bucket_agreement
+            agreement = verify_bucket_agreement(red)      # raises on a plan / order mismatch
     torch.save({"state": {k: v.detach().clone() for k, v in model.state_dict().items()},
                 "global_step": gstep.value(), "world": world, "mean_loss": mean_loss,
                 "fingerprints": fps, "early_launches": early,
                 "sharded": getattr(opt._reducer, "sharded", None),
-                "reducer": type(opt._reducer).__name__},
+                "reducer": type(opt._reducer).__name__,
+                "plan": red.plan() if hasattr(red, "plan") else None,
+                "order": list(getattr(red, "last_order", ())),
+                "ranges": [list(r) for r in getattr(red, "ranges", [])],
+                "agreement": agreement},
                os.path.join(out, f"rank{rank}.pt"))
     strat.barrier()
 

@@ -157,3 +157,67 @@ def test_bench_nccl_refuses_more_ranks_than_gpus():
     assert p.returncode != 0
     assert "refusing to measure fewer GPUs" in p.stderr, p.stderr[-2000:]
     assert time.time() - t0 < 30
+
+
+def _run_ranks(tmp_path, n, extra, timeout=150):
+    from distributedtensorflow_amd.cluster.launcher import free_ports
+    port = free_ports(1)[0]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK="0",
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   PYTHONPATH=ROOT, OMP_NUM_THREADS="2", DTF_BENCH_BACKEND="gloo")
+        out = open(tmp_path / f"rank{r}.out", "w")
+        err = open(tmp_path / f"rank{r}.err", "w")
+        procs.append((subprocess.Popen(
+            [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--batch", "8",
+             "--image-size", "64", "--steps", "3", "--warmup", "2", *extra],
+            env=env, stdout=out, stderr=err, cwd=ROOT), out, err))
+    try:
+        for p, _, _ in procs:
+            p.wait(timeout=timeout)
+    finally:
+        for p, out, err in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+            out.close()
+            err.close()
+    return [p.returncode for p, _, _ in procs]
+
+
+@pytest.mark.parametrize("strategy", ["mirrored", "ps"])
+def test_bench_four_ranks_reports_per_rank_diagnostics(tmp_path, strategy):
+    """the N > 1 JSON carries what a first 1 -> 8 scaling run needs to be
+    read -- per-rank step time (min / max / each rank), every rank's bucket count, bucket-plan and
+    collective issue-order hashes (identical, or the run fails), exposed comm time per rank and
+    the RCCL channel count (None on this gloo rehearsal: 4 ranks sharing cuda:0)."""
+    extra = [] if strategy == "mirrored" else ["--strategy", "ps", "--num-ps", "4"]
+    codes = _run_ranks(tmp_path, 4, extra)
+    assert codes == [0] * 4, open(tmp_path / "rank0.err").read()[-3000:]
+    lines = [ln for ln in open(tmp_path / "rank0.out").read().splitlines() if ln.startswith("{")]
+    rec = json.loads(lines[-1])
+    ranks = rec["config"]["comm"]["ranks"]
+    assert rec["n_gpus"] == 4 and len(ranks["ms_per_step"]) == 4
+    assert ranks["ms_per_step_min"] <= ranks["ms_per_step_max"]
+    # the reported step time is the slowest rank's (MAX over ranks)
+    assert abs(rec["ms_per_step"] - ranks["ms_per_step_max"]) <= 0.01 * rec["ms_per_step"] + 0.01
+    assert len(set(ranks["buckets"])) == 1 and ranks["buckets"][0] >= 2
+    assert len(set(ranks["plan_hash"])) == 1 and len(set(ranks["order_hash"])) == 1
+    assert sorted(ranks["issue_order_rank0"]) == list(range(ranks["buckets"][0]))
+    assert len(ranks["exposed_comm_ms_per_step"]) == 4
+    assert ranks["rccl_channels"] == [None] * 4
+
+
+def test_bench_rank_with_another_bucket_order_fails(tmp_path):
+    """A rank issuing its bucket collectives in another order makes the bench exit non-zero
+    (order check or comm deadline), never report a number."""
+    os.environ["DTF_DEBUG_PERTURB_BUCKET_ORDER"] = "1"
+    os.environ["DTF_COMM_TIMEOUT_S"] = "10"
+    try:
+        codes = _run_ranks(tmp_path, 2, [], timeout=120)
+    finally:
+        del os.environ["DTF_DEBUG_PERTURB_BUCKET_ORDER"], os.environ["DTF_COMM_TIMEOUT_S"]
+    assert any(c != 0 for c in codes)
+    out = open(tmp_path / "rank0.out").read()
+    assert not any(ln.startswith("{") for ln in out.splitlines())

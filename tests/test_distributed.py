@@ -424,3 +424,34 @@ def test_eight_ranks_match_single_process(tmp_path, kind, args):
     if kind == "colocated_ps":
         assert all(r["sharded"] is True for r in res)
     _assert_replicas(res, _single_process(), atol=5e-6)
+    # every rank: the same bucket plan, the same collective issue order (checked collectively by
+    # verify_bucket_agreement inside the run, and here from the saved records)
+    assert all(r["plan"] == res[0]["plan"] and r["order"] == res[0]["order"] for r in res)
+    assert len(res[0]["plan"]["buckets"]) >= 4 and sorted(res[0]["order"]) == \
+        list(range(len(res[0]["plan"]["buckets"])))
+    assert all(r["agreement"] == res[0]["agreement"] for r in res)
+    if kind == "colocated_ps":
+        # reduce-scatter / all-gather chunk offsets = the sharded owner plan at every rank:
+        # rank r owns chunk r of every bucket, equal chunks that tile the bucket exactly
+        for r, rec in enumerate(res):
+            for b, (s, e, _) in enumerate(rec["plan"]["buckets"]):
+                c = (e - s) // 8
+                assert [list(p) for p in rec["plan"]["pieces"][b]] == \
+                    [[o, s + o * c, s + (o + 1) * c] for o in range(8)]
+                assert list(rec["ranges"][b]) == [r, s + r * c, s + (r + 1) * c]
+
+
+def test_forced_bucket_order_mismatch_fails_within_the_deadline(tmp_path):
+    """A rank that issues its bucket collectives in another order (DTF_DEBUG_PERTURB_BUCKET_ORDER)
+    sums the wrong buckets or blocks: the run must fail -- by the order check or by the comm
+    watchdog's deadline -- quickly and loudly, never train on silently or hang."""
+    import time
+    t0 = time.time()
+    with pytest.raises(AssertionError) as ei:
+        _launch("mirrored", 2, tmp_path, "bucket_mb=0.05", timeout=120,
+                extra_env=lambda r: {"DTF_DEBUG_PERTURB_BUCKET_ORDER": "1",
+                                     "DTF_COMM_TIMEOUT_S": "5"})
+    assert time.time() - t0 < 90
+    msg = str(ei.value)
+    assert "collective order differs" in msg or "CommError" in msg or "did not complete" in msg, \
+        msg[-3000:]
