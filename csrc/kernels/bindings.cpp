@@ -210,6 +210,7 @@ void dtf_gemm_nt(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int,
 int dtf_gemm_tile_rows(int);
 void dtf_gemm_set_variant(int);
 void dtf_gemm_set_pp(int);
+void dtf_gemm_set_pp2(int);
 int dtf_bias_relu_bwd_ws_floats(int);
 void dtf_gather_u8_scale(const uint8_t*, const int64_t*, void*, int, int, float, int, hipStream_t);
 // ---- fp32 path (f32.hip)
@@ -351,6 +352,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("gemm_tile_rows", &dtf_gemm_tile_rows);
   m.def("gemm_set_variant", &dtf_gemm_set_variant);
   m.def("gemm_set_pp", &dtf_gemm_set_pp);
+  m.def("gemm_set_pp2", &dtf_gemm_set_pp2);
   m.def("bias_relu_bwd_ws_floats", &dtf_bias_relu_bwd_ws_floats);
   m.def("gather_u8_scale", [](uintptr_t images, uintptr_t idx, uintptr_t out, int B, int D,
                               float scale, int out_bf16, uintptr_t st) {

@@ -1096,6 +1096,400 @@ gemm_pp_kernel(const GemmArgs g) {
   DTF_WAIT_VM(0);       // the trailing look-ahead DMAs still target the ring
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent ping-pong GEMM, round 5 (gemm_pp2_kernel): gemm_pp's design -- one block per CU
+// walking tiles, the LDS-DMA piece stream running ACROSS tiles so the next tile's first pieces
+// fly while this tile's outputs are stored straight from the registers -- with a main loop that
+// is instruction-for-instruction the per-tile SCHED 2 loop.  gemm_pp lost its main loop to the
+// cross-tile issue path (tile lookup, two per-tile buffer descriptors and the CONV receptive-field
+// geometry recomputed inside every look-ahead issue: SGPR spills on the ping-pong's critical
+// load sections, profiles/measurements/r2_gemm_epilogue_probes.jsonl p1/p4).  Here
+//   * the buffer descriptors span the WHOLE operands (host: < 2^31 bytes), built once;
+//   * every piece's per-lane source offset (dense) or image pixel / receptive-field corner (CONV)
+//     is computed ONCE per tile for the current AND the next tile; a look-ahead issue selects
+//     between the two sets with a wave-uniform condition (v_cndmask), nothing else;
+//   * K % 64 == 0 (no K-tail test in the issue).
+// The epilogue (bias / ReLU / BN statistics / Cin / masked acc, strided dgrad phases) and the
+// counted waits around the stores are gemm_pp's.
+// EPI bits (each instantiation carries only the epilogue operands it uses -- SGPR pressure):
+// 1 BN statistics, 2 accumulate (Cin / masked acc), 4 strided (dgrad phase) output rows
+template <int CONV, int EPI>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp2_kernel(const GemmArgs g) {
+  using Cf = GCfg<256, 256, 64, 2, 8>;
+  constexpr int BM = 256, BN = 256, BK = 64;
+  constexpr int NSTORE = Cf::FM * Cf::FN;          // 8-B stores per lane per tile (32)
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cf::WN, wn = wave % Cf::WN;
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int ntiles = tiles_n * tiles_m;
+  const int nk = g.K / BK;                         // >= 2, K % 64 == 0 (host)
+  const uint32_t lds0 = lds_addr(lds);
+  const int lrow = lane / Cf::CPR, slot = lane % Cf::CPR;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int PQc = CONV ? g.P * g.Q : 1;
+  constexpr bool strided = CONV && (EPI & 4);
+  const int cb = CONV ? g.Cc / BK : 1;
+
+  auto prow = [&](int pc, int j) {
+    const int r0 = pc == 0 ? j * 128 + 8 * wave
+                 : pc == 3 ? 64 + j * 128 + 8 * wave
+                           : (2 * j + (wave >> 2)) * 64 + (pc == 2 ? 32 : 0) + (wave & 3) * 8;
+    return r0 + lrow;
+  };
+  const int pch = gswz<BK>(prow(0, 0), slot) * 8;   // the same for every piece of this wave
+  auto plds = [&](int pc, int j) {
+    const bool isA = pc == 0 || pc == 3;
+    return (uint32_t)((isA ? 0 : Cf::SA) + (prow(pc, j) - lrow) * BK) * 2u;
+  };
+  // whole-operand descriptors (host: A / X and B below 2^31 bytes)
+  const i32x4_t ra = rsrc_quad(g.A, (uint32_t)g.ncu);          // ncu carries A's byte size here
+  const i32x4_t rb = rsrc_quad(g.B, (uint32_t)g.group_m);      // group_m carries B's byte size
+
+  auto tile_mn = [&](int seq, int& m0, int& n0) {
+    const long phys = (long)blockIdx.x + (long)seq * gridDim.x;
+    if (phys >= ntiles) { m0 = -1; n0 = 0; return false; }
+    const int bid = xcd_remap((int)phys, ntiles);
+    m0 = (bid / tiles_n) * BM;
+    n0 = (bid % tiles_n) * BN;
+    return true;
+  };
+  // per-tile piece operands: dense -> byte offset (2^31 = out of range); CONV A pieces -> ONE
+  // packed int per piece: image n (bits 20+), top-left h (bits 10-19), w (bits 0-9) of the
+  // receptive field (invalid rows: h = 1023, beyond every image; host: N < 2048, H, W < 1000)
+  auto tile_offsets = [&](bool valid, int m0, int n0, uint32_t (&o)[4][2], int (&pk)[2][2]) {
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool isA = pc == 0 || pc == 3;
+        const int row = prow(pc, j);
+        if (isA) {
+          const int m = m0 + row;
+          const bool ok = valid && m < g.M;
+          if constexpr (CONV) {
+            const int mm = ok ? m : 0;
+            const int q = mm % g.Q, t = mm / g.Q;
+            const int p = t % g.P, n = t / g.P;
+            pk[pc == 3][j] = (n << 20) | ((ok ? p * g.sh : 1023) << 10) | (q * g.sw);
+            o[pc][j] = 0x80000000u;
+          } else {
+            o[pc][j] = ok ? (uint32_t)(m * g.lda + pch) * 2u : 0x80000000u;
+          }
+        } else {
+          const int n = n0 + row;
+          const bool ok = valid && n < g.N;
+          o[pc][j] = ok ? (uint32_t)(n * g.ldb + pch) * 2u : 0x80000000u;
+        }
+      }
+  };
+
+  int seq = 0, cm0, cn0, xm0, xn0;
+  if (!tile_mn(0, cm0, cn0)) return;
+  bool nxt_valid = tile_mn(1, xm0, xn0);
+  uint32_t ocur[4][2], onxt[4][2];
+  int pcur[2][2], pnxt[2][2];
+  tile_offsets(true, cm0, cn0, ocur, pcur);
+  tile_offsets(nxt_valid, xm0, xn0, onxt, pnxt);
+  int gstep0 = 0;
+
+  // piece pc of step kt of the current tile (kt >= nk: the next tile's step kt - nk)
+  auto issue_piece = [&](int kt, int pc) {
+    const bool nx = kt >= nk;
+    const int kk = nx ? kt - nk : kt;
+    const uint32_t base = lds0 + (uint32_t)(((gstep0 + kt) & 1) * Cf::STAGE) * 2u;
+    const bool isA = pc == 0 || pc == 3;
+    if constexpr (CONV) {
+      if (isA) {
+        const int tap = kk / cb, c0 = (kk % cb) * BK;
+        const int dh = g.tdh[tap], dw = g.tdw[tap];
+        const bool live = !nx || nxt_valid;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int v = nx ? pnxt[pc == 3][j] : pcur[pc == 3][j];
+          const int h = ((v >> 10) & 1023) + dh, w = (v & 1023) + dw;
+          const bool ok = live && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          dma16(ra, base + plds(pc, j),
+                ok ? (uint32_t)((((v >> 20) * g.H + h) * g.W + w) * g.Cc + c0 + pch) * 2u : kGOOB);
+        }
+        return;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t o = nx ? onxt[pc][j] : ocur[pc][j];
+      dma16(isA ? ra : rb, base + plds(pc, j), o + (uint32_t)(kk * BK) * 2u);
+    }
+  };
+
+  f32x4_t acc[Cf::FM][Cf::FN];
+#pragma unroll
+  for (int i = 0; i < Cf::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t fA[8], fBl[4], fBr[4];
+  auto rdA = [&](const bf16_t* sa, int half) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 128 + half * 64 + i * 16 + frow, ch = ks * 4 + fq;
+        fA[ks * 4 + i] = *reinterpret_cast<const bf16x8_t*>(sa + r * BK + gswz<BK>(r, ch) * 8);
+      }
+  };
+  auto rdB = [&](bf16x8_t* fb, const bf16_t* sa, int half) {
+    const bf16_t* sb = sa + Cf::SA;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 64 + half * 32 + j * 16 + frow, ch = ks * 4 + fq;
+        fb[ks * 2 + j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
+      }
+  };
+  auto sync = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mfma_phase = [&](const bf16x8_t* fb, int ah, int bh) {
+    sync();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ah * 4 + i][bh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              fb[ks * 2 + j], fA[ks * 4 + i], acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+  };
+
+  float* red = reinterpret_cast<float*>(lds + 2 * Cf::STAGE);   // [WM][2][BN] past the ring
+  // EPI 0 (BERT's dense layers): C (+ bias) (+ ReLU) only -- the statistics / accumulate
+  // operands and their SGPRs are compiled out
+  constexpr bool do_stats = (EPI & 1) != 0;
+  constexpr bool has_acc = (EPI & 2) != 0;
+
+  issue_piece(0, 0); issue_piece(0, 1); issue_piece(0, 2); issue_piece(0, 3);
+  issue_piece(1, 0); issue_piece(1, 1);
+  DTF_WAIT_VM(8);
+  bool first = true;
+  for (;; ++seq) {
+    sync();
+    if (wm == 1) sync();                       // the one-barrier stagger
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* cur_lds = lds + ((gstep0 + kt) & 1) * Cf::STAGE;
+      rdB(fBl, cur_lds, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      rdA(cur_lds, 0);
+      issue_piece(kt + 1, 2);
+      if (!first && kt == 0) DTF_WAIT_VM(40); else DTF_WAIT_VM(8);
+      mfma_phase(fBl, 0, 0);
+      rdB(fBr, cur_lds, 1);
+      issue_piece(kt + 1, 3);
+      if (!first && kt == 0) DTF_WAIT_VM(40); else DTF_WAIT_VM(8);
+      mfma_phase(fBr, 0, 1);
+      rdA(cur_lds, 1);
+      issue_piece(kt + 2, 0);
+      DTF_WAIT_VM(8);
+      mfma_phase(fBr, 1, 1);
+      issue_piece(kt + 2, 1);
+      DTF_WAIT_VM(8);
+      mfma_phase(fBl, 1, 0);
+    }
+    if (wm == 0) sync();
+
+    // ---- epilogue (gemm_pp's): lane (frow, fq) of fragment (i, j) holds C[m][n .. n + 3]
+    const int n_lo = CONV ? cm0 / PQc : 0;
+    const int rows_a = min(BM, g.M - cm0);
+    long cbase;
+    uint32_t cbytes;
+    if (strided) {
+      const int n_hi = (cm0 + rows_a - 1) / PQc;
+      cbase = (long)n_lo * g.Ho * g.Wo * g.ldc;
+      cbytes = (uint32_t)((long)(n_hi - n_lo + 1) * g.Ho * g.Wo * g.ldc * 2);
+    } else {
+      cbase = (long)cm0 * g.ldc;
+      cbytes = (uint32_t)(((long)(rows_a - 1) * g.ldc + g.N) * 2);
+    }
+    const __amdgpu_buffer_rsrc_t rc =
+        __builtin_amdgcn_make_buffer_rsrc(g.C + cbase, 0, (int)cbytes, 0x00020000);
+    const bool nt_store = g.nt != 0;
+    // element offset of row m from cbase (within the C descriptor: < 2^30), -1: no row
+    int rowoff[Cf::FM];
+#pragma unroll
+    for (int i = 0; i < Cf::FM; ++i) {
+      const int m = cm0 + wm * 128 + i * 16 + frow;
+      int o = -1;
+      if (m < g.M) {
+        if (strided) {
+          const int q = m % g.Q, t = m / g.Q;
+          const int p = t % g.P, n = t / g.P;
+          o = (((n - n_lo) * g.Ho + p * g.osh + g.oh0) * g.Wo + q * g.osw + g.ow0) * g.ldc;
+        } else {
+          o = (m - cm0) * g.ldc;
+        }
+      }
+      rowoff[i] = o;
+    }
+#pragma unroll
+    for (int j = 0; j < Cf::FN; ++j) {
+      const int ncol = cn0 + wn * 64 + j * 16 + fq * 4;
+      const bool col_ok = ncol < g.N;
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (g.bias && col_ok) {
+        const float4 bv = *reinterpret_cast<const float4*>(g.bias + ncol);
+        b4[0] = bv.x; b4[1] = bv.y; b4[2] = bv.z; b4[3] = bv.w;
+      }
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < Cf::FM; ++i) {
+        const bool ok = col_ok && rowoff[i] >= 0;
+        float v[4];
+        bf16_t h[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[i][j][r] + b4[r];
+          if (g.relu) v[r] = fmaxf(v[r], 0.f);
+          h[r] = f2bf(v[r]);
+          if (do_stats && ok) {
+            const float qv = bf2f(h[r]);
+            s1[r] += qv;
+            s2[r] += qv * qv;
+          }
+        }
+        const int eoff = rowoff[i] + ncol;
+        if (has_acc && ok) {
+          const bf16_t* src = g.Cin ? g.Cin + cbase + eoff : g.acc_src + cbase + eoff;
+          const uint2 sv = *reinterpret_cast<const uint2*>(src);
+          const uint32_t bits = g.Cin ? 0xFu
+                                      : (g.acc_mask[(cbase + eoff) >> 3] >> ((cbase + eoff) & 7)) & 0xFu;
+          const float sf[4] = {__builtin_bit_cast(float, sv.x << 16),
+                               __builtin_bit_cast(float, sv.x & 0xffff0000u),
+                               __builtin_bit_cast(float, sv.y << 16),
+                               __builtin_bit_cast(float, sv.y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] = f2bf(bf2f(h[r]) + ((bits >> r) & 1u ? sf[r] : 0.f));
+        }
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t w = {(uint32_t)h[0] | ((uint32_t)h[1] << 16),
+                           (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+        const int so = ok ? eoff * 2 : (int)kGOOB;
+        if (nt_store) __builtin_amdgcn_raw_buffer_store_b64(w, rc, so, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b64(w, rc, so, 0, 0);
+      }
+      if (do_stats) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s1[r] += __shfl_xor(s1[r], o, 64);
+            s2[r] += __shfl_xor(s2[r], o, 64);
+          }
+        }
+        if (frow == 0) {
+          const int col = wn * 64 + j * 16 + fq * 4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            red[(wm * 2 + 0) * BN + col + r] = s1[r];
+            red[(wm * 2 + 1) * BN + col + r] = s2[r];
+          }
+        }
+      }
+    }
+    if (do_stats) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+      if (tid < BN && cn0 + tid < g.N) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int k = 0; k < Cf::WM; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
+        const int tm = cm0 / BM;
+        g.stats[((long)tm * 2 + 0) * g.N + cn0 + tid] = a;
+        g.stats[((long)tm * 2 + 1) * g.N + cn0 + tid] = b;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+    }
+    if (!nxt_valid) break;
+#pragma unroll
+    for (int i = 0; i < Cf::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < Cf::FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    gstep0 += nk;
+    cm0 = xm0;
+    cn0 = xn0;
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) ocur[pc][j] = onxt[pc][j];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) pcur[a][j] = pnxt[a][j];
+    nxt_valid = tile_mn(seq + 2, xm0, xn0);
+    tile_offsets(nxt_valid, xm0, xn0, onxt, pnxt);
+    first = false;
+    static_assert(NSTORE == 32, "the counted waits assume 32 stores per lane per tile");
+  }
+  DTF_WAIT_VM(0);       // the trailing look-ahead DMAs still target the ring
+}
+
+template <int CONV, int EPI>
+void launch_gemm_pp2_t(const GemmArgs& g0, long a_bytes, long b_bytes, hipStream_t st) {
+  using Cf = GCfg<256, 256, 64, 2, 8>;
+  constexpr size_t LDS = (size_t)2 * Cf::STAGE * 2 + (size_t)Cf::WM * 2 * 256 * 4;
+  static bool attr = false;
+  static int ncu = 0;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_pp2_kernel<CONV, EPI>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    hipFuncAttributes fa{};
+    HIP_CHECK(hipFuncGetAttributes(&fa, (const void*)gemm_pp2_kernel<CONV, EPI>));
+    if (fa.localSizeBytes > 0)
+      throw std::runtime_error("gemm_pp2_kernel was compiled with register spills (scratch " +
+                               std::to_string(fa.localSizeBytes) + " B/lane)");
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    attr = true;
+  }
+  if (a_bytes <= 0 || a_bytes >= 0x7FFFFF00L || b_bytes <= 0 || b_bytes >= 0x7FFFFF00L ||
+      g0.K % 64 || g0.K < 128)
+    throw std::runtime_error("gemm_pp2: operands below 2^31 bytes, K % 64 == 0, K >= 128");
+  GemmArgs g = g0;
+  g.ncu = (int)a_bytes;        // the whole-operand descriptor sizes ride in these two fields
+  g.group_m = (int)b_bytes;
+  const long tiles = (long)((g.M + 255) / 256) * ((g.N + 255) / 256);
+  long grid = tiles < ncu ? tiles : (ncu / 8) * 8;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((gemm_pp2_kernel<CONV, EPI>), dim3((unsigned)grid), dim3(Cf::NT), LDS,
+                     st, g);
+}
+
+template <int CONV>
+void launch_gemm_pp2(const GemmArgs& g, long a_bytes, long b_bytes, hipStream_t st) {
+  const bool stats = g.stats != nullptr, acc = g.Cin || g.acc_mask;
+  const bool strided = CONV && (g.osh != 1 || g.osw != 1);
+  if (strided) {
+    if (acc) launch_gemm_pp2_t<CONV, 6>(g, a_bytes, b_bytes, st);
+    else launch_gemm_pp2_t<CONV, 4>(g, a_bytes, b_bytes, st);
+  } else if (stats) {
+    launch_gemm_pp2_t<CONV, 1>(g, a_bytes, b_bytes, st);
+  } else if (acc) {
+    launch_gemm_pp2_t<CONV, 2>(g, a_bytes, b_bytes, st);
+  } else {
+    launch_gemm_pp2_t<CONV, 0>(g, a_bytes, b_bytes, st);
+  }
+}
+
 template <int CONV>
 void launch_gemm_pp(const GemmArgs& g, hipStream_t st) {
   using Cf = GCfg<256, 256, 64, 2, 8>;
@@ -1125,6 +1519,7 @@ void launch_gemm_pp(const GemmArgs& g, hipStream_t st) {
 }
 
 int g_gemm_pp = 0;         // bit 0: persistent register-epilogue kernel for gemm_nt, bit 1: convs
+int g_gemm_pp2 = 0;        // round-5 persistent kernel (gemm_pp2): bit 0 gemm_nt, bit 1 convs
 int g_gemm_stream = 1;     // output-heavy shapes on the row-streaming kernel (gemm_stream.hip)
 
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
@@ -1169,6 +1564,7 @@ void launch_gemm(const GemmArgs& g0, hipStream_t st) {
 void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
 void dtf_gemm_set_stream(int v) { g_gemm_stream = v; }
 void dtf_gemm_set_pp(int v) { g_gemm_pp = v; }
+void dtf_gemm_set_pp2(int v) { g_gemm_pp2 = v; }
 void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
 void dtf_gemm_set_dbg(int v) { g_gemm_dbg = v; }
 void dtf_gemm_set_stagger(int mode, int iters) { g_gemm_stagger_mode = mode; g_gemm_stagger = iters; }
@@ -1203,7 +1599,11 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
     throw std::runtime_error("gemm_conv: filter too large");
   const bool pp_span = !(osh != 1 || osw != 1) ||
       (256.0 / (P * Q) + 2) * Ho * Wo * (double)Kout * 2 < 2147483647.0;
+  const long x_bytes = (long)N * H * W * C * 2, w_bytes = (long)Kout * g.ldb * 2;
   if (Kout <= 128) launch_gemm<256, 128, 64, 3, 3, 8, 1, 1>(g, st);
+  else if ((g_gemm_pp2 & 2) && g.K >= 128 && x_bytes < 0x7FFFFF00L && w_bytes < 0x7FFFFF00L &&
+           N < 2048 && H < 1000 && W < 1000 && pp_span)
+    launch_gemm_pp2<1>(g, x_bytes, w_bytes, st);
   else if ((g_gemm_pp & 2) && (g.K + 63) / 64 >= 2 && pp_span) launch_gemm_pp<1>(g, st);
   else launch_gemm<256, 256, 64, 2, 2, 8, 1, 1>(g, st);
 }
@@ -1249,6 +1649,13 @@ void dtf_gemm_stream(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, 
                      int ldb, int ldc, const bf16_t* Cin, float* stats, const bf16_t* acc_src,
                      const uint8_t* acc_mask, int nt, hipStream_t st);
 
+// the persistent kernel gemm_pp2 takes this dense GEMM: K % 64 == 0, K >= 128, whole operands
+// addressable with 32-bit buffer offsets
+bool dtf_gemm_pp2_ok(int M, int N, int K, int lda, int ldb) {
+  return K % 64 == 0 && K >= 128 && (long)(M - 1) * lda * 2 + 2L * K < 0x7FFFFF00L &&
+         (long)(N - 1) * ldb * 2 + 2L * K < 0x7FFFFF00L;
+}
+
 // block-tile rows of every variant (the BatchNorm statistics slab has one row per M tile)
 int dtf_gemm_tile_rows(int M) { return (M + 255) / 256; }
 
@@ -1280,11 +1687,18 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
   // auto: 256 x 128 tiles when N <= 128 (measured 1.02-1.07x the 256 x 256 tile on the N = 128
   // ResNet 1x1 convs, profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl)
   const int variant = g_gemm_variant >= 0 ? g_gemm_variant
-                    : (N <= 128 ? 1 : ((g_gemm_pp & 1) && (K + 63) / 64 >= 2 ? 11 : 8));
+                    : (N <= 128 ? 1
+                       : (g_gemm_pp2 & 1) && dtf_gemm_pp2_ok(M, N, K, lda, ldb) ? 15
+                       : ((g_gemm_pp & 1) && (K + 63) / 64 >= 2 ? 11 : 8));
   if (variant == 11 && (K + 63) / 64 < 2)
     throw std::runtime_error("gemm_nt: the persistent kernel needs K > 64");
+  if (variant == 15 && !dtf_gemm_pp2_ok(M, N, K, lda, ldb))
+    throw std::runtime_error("gemm_nt: shape not supported by the persistent kernel (variant 15)");
   switch (variant) {
     case 11: launch_gemm_pp<0>(g, st); break;
+    case 15:
+      launch_gemm_pp2<0>(g, (long)(M - 1) * lda * 2 + 2L * K, (long)(N - 1) * ldb * 2 + 2L * K, st);
+      break;
     case 1: launch_gemm<256, 128, 64, 3>(g, st); break;
     case 2: launch_gemm<256, 256, 32, 4>(g, st); break;
     case 3: launch_gemm<256, 128, 32, 4>(g, st); break;

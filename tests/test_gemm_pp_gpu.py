@@ -92,3 +92,24 @@ def test_pp_masked_accumulate_and_bn_stats(M, N, K, variant):
     yf = y8.float()
     torch.testing.assert_close(s11[:, 0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(s11[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-4, atol=1e-1)
+
+
+PP2_SHAPES = [s for s in SHAPES if s[2] % 64 == 0 and s[2] >= 128] + [(65536, 768, 3072)]
+
+
+@pytest.mark.parametrize("M,N,K", PP2_SHAPES)
+def test_pp2_matches_pingpong_bitwise(M, N, K):
+    """Round 5's persistent kernel (variant 15: whole-operand descriptors, per-tile piece offsets
+    computed once for the current and the next tile) -- the same MFMA sequence per output element
+    as variant 8, so bit-identical for every epilogue mode, and the BN partial sums to rounding."""
+    test_pp_matches_pingpong_bitwise(M, N, K, 15)
+    if K in (768, 512):
+        test_pp_masked_accumulate_and_bn_stats(M, N, K, 15)
+
+
+def test_pp2_refuses_unsupported_shapes():
+    n = _native()
+    a = torch.zeros(512, 200, device="cuda").bfloat16()
+    b = torch.zeros(256, 200, device="cuda").bfloat16()
+    with pytest.raises(RuntimeError, match="variant 15"):
+        _run(15, lambda: n.gemm_nt(a, b))
