@@ -136,15 +136,17 @@ void dtf_gemm_set_stream(int);
 void dtf_gemm_stream_bnb(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int,
                          const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*,
                          const float*, const float*, const float*, const float*, const uint8_t*,
-                         int, float*, int, hipStream_t);
+                         int, float*, int, hipStream_t, const bf16_t*, const bf16_t*, int);
 bool dtf_gemm_stream_ok(int, int, int, int, int, int);
+void dtf_gemm_stream_apply(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, const bf16_t*,
+                           const float*, const float*, uint8_t*, hipStream_t);
 void dtf_gemm_stream_bnb_dual(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int,
                               const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*,
                               const float*, const float*, const uint8_t*, float*, const bf16_t*,
                               const float*, const float*, float*, hipStream_t);
 void dtf_gemm_stream_probe(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void dtf_gemm_stream_pre(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, const float*,
-                         const float*, bf16_t*, float*, hipStream_t);
+                         const float*, bf16_t*, float*, hipStream_t, int);
 void dtf_gemm_set_stagger(int, int);
 void dtf_gemm_set_group(int);
 int dtf_wgrad_get_pipe();
@@ -211,6 +213,7 @@ int dtf_gemm_tile_rows(int);
 void dtf_gemm_set_variant(int);
 void dtf_gemm_set_pp(int);
 void dtf_gemm_set_pp2(int);
+bool dtf_gemm_pp2_ok(int M, int N, int K, int lda, int ldb);
 int dtf_bias_relu_bwd_ws_floats(int);
 void dtf_gather_u8_scale(const uint8_t*, const int64_t*, void*, int, int, float, int, hipStream_t);
 // ---- fp32 path (f32.hip)
@@ -353,6 +356,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("gemm_set_variant", &dtf_gemm_set_variant);
   m.def("gemm_set_pp", &dtf_gemm_set_pp);
   m.def("gemm_set_pp2", &dtf_gemm_set_pp2);
+  m.def("gemm_pp2_ok", &dtf_gemm_pp2_ok);
   m.def("bias_relu_bwd_ws_floats", &dtf_bias_relu_bwd_ws_floats);
   m.def("gather_u8_scale", [](uintptr_t images, uintptr_t idx, uintptr_t out, int B, int D,
                               float scale, int out_bf16, uintptr_t st) {
@@ -735,22 +739,36 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("gemm_stream_pre", [](uintptr_t x, uintptr_t b, uintptr_t c, int M, int N, int K,
                               uintptr_t sc, uintptr_t sh, uintptr_t y, uintptr_t stats,
-                              uintptr_t stream) {
+                              uintptr_t stream, int nostore) {
     dtf_gemm_stream_pre(P<bf16_t>(x), P<bf16_t>(b), P<bf16_t>(c), M, N, K, P<float>(sc),
-                        P<float>(sh), P<bf16_t>(y), P<float>(stats), S(stream));
+                        P<float>(sh), P<bf16_t>(y), P<float>(stats), S(stream), nostore);
     check_launch("gemm_stream_pre");
+  }, py::arg("x"), py::arg("b"), py::arg("c"), py::arg("M"), py::arg("N"), py::arg("K"),
+     py::arg("sc"), py::arg("sh"), py::arg("y"), py::arg("stats"), py::arg("stream"),
+     py::arg("nostore") = 0);
+  m.def("gemm_stream_apply", [](uintptr_t a, uintptr_t w, uintptr_t y, int M, int N, int K,
+                                uintptr_t res, uintptr_t sc, uintptr_t sh, uintptr_t mask,
+                                uintptr_t stream) {
+    dtf_gemm_stream_apply(P<bf16_t>(a), P<bf16_t>(w), P<bf16_t>(y), M, N, K, P<bf16_t>(res),
+                          P<float>(sc), P<float>(sh), P<uint8_t>(mask), S(stream));
+    check_launch("gemm_stream_apply");
   });
   m.def("gemm_stream_bnb", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, int lda,
                               int ldb, int ldc, uintptr_t cin, uintptr_t acc_src, uintptr_t acc_mask,
                               uintptr_t bx, uintptr_t mean, uintptr_t inv, uintptr_t sc,
                               uintptr_t sh, uintptr_t bmask, int kind, uintptr_t part,
-                              uintptr_t stream) {
+                              uintptr_t stream, uintptr_t y2, uintptr_t w3, int k3) {
     dtf_gemm_stream_bnb(P<bf16_t>(a), P<bf16_t>(b), P<bf16_t>(c), M, N, K, lda, ldb, ldc,
                         P<bf16_t>(cin), P<bf16_t>(acc_src), P<uint8_t>(acc_mask), P<bf16_t>(bx),
                         P<float>(mean), P<float>(inv), P<float>(sc), P<float>(sh),
-                        P<uint8_t>(bmask), kind, P<float>(part), 0, S(stream));
+                        P<uint8_t>(bmask), kind, P<float>(part), 0, S(stream), P<bf16_t>(y2),
+                        P<bf16_t>(w3), k3);
     check_launch("gemm_stream_bnb");
-  });
+  }, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("M"), py::arg("N"), py::arg("K"),
+     py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("cin"), py::arg("acc_src"),
+     py::arg("acc_mask"), py::arg("bx"), py::arg("mean"), py::arg("inv"), py::arg("sc"),
+     py::arg("sh"), py::arg("bmask"), py::arg("kind"), py::arg("part"), py::arg("stream"),
+     py::arg("y2") = 0, py::arg("w3") = 0, py::arg("k3") = 0);
   m.def("gemm_stream_bnb_dual", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K,
                                    int lda, int ldb, int ldc, uintptr_t cin, uintptr_t acc_src,
                                    uintptr_t acc_mask, uintptr_t bx, uintptr_t mean, uintptr_t inv,

@@ -71,6 +71,18 @@ struct StreamArgs {
   const float* bmeanp;
   const float* binvp;
   float* statsp;
+  // RC (BNB with K3 > 0): the BatchNorm input x (a conv output that was never stored) is
+  // recomputed per chunk as bf16(y2 . w3^T) -- the producing stream GEMM's exact MFMA chain --
+  // from y2 [M][K3] (that conv's input) and w3 [N][K3] (its weight)
+  const bf16_t* y2;
+  const bf16_t* w3;
+  // APPLY (MODE 3): C = relu(bf16(A . B^T) * asc[n] + ash[n] + Cin) -- the residual BatchNorm's
+  // apply pass on a conv output recomputed instead of read -- and its ReLU bit mask `amask`
+  const float* asc;
+  const float* ash;
+  uint8_t* amask;
+  int k3;                     // RC recompute depth
+  int nost;                   // PRE: statistics only, C not stored
 };
 
 DTF_DEV int sswz(int row, int ch) { return ch ^ ((row >> 1) & 7); }   // 64-deep panel swizzle
@@ -90,13 +102,21 @@ DTF_DEV void wait_vmc() {
 // BMK >= 0: BN-backward sums of the output (0 no ReLU, 1 ReLU bit mask, 2 ReLU from x)
 // PROBE (timing experiments only, tools/gemm_bench.py --stream-probe): 1 no MFMAs, 2 no LDS
 // staging of C, 4 no chunk barrier, 8 C stores out of range
+// NOST: C is not stored (statistics only -- a conv output recomputed later, never written);
+// K3 > 0 (BNB): the BN input x recomputed per chunk from y2 / w3 (RC above); MODE 3: APPLY
 template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false, int PROBE = 0,
-          bool DUAL = false>
+          bool DUAL = false, bool NOST = false, int K3 = 0>
 __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g) {
   constexpr int KS = K / 32;                  // MFMA k-steps
-  constexpr int CH = kSBN * K;                // bf16 elements per ring slot
-  constexpr int D = K / 64;                   // LDS-DMA instructions per thread per chunk
+  constexpr int KS3 = K3 / 32;                // RC: recompute k-steps
+  constexpr int CHB = kSBN * K;               // bf16 elements of a ring slot's B chunk
+  constexpr int CH = CHB + kSBN * K3;         // ... + the RC w3 chunk
+  constexpr int D = K / 64 + K3 / 64;         // LDS-DMA instructions per thread per chunk
   constexpr int S = kSWR * kSBN * 2 / (64 * 16);   // 16-B stores per lane per chunk (4)
+  // vector-memory stores per lane per chunk: C (+ the APPLY mask bytes); none with NOST
+  constexpr int SST = NOST ? 0 : (MODE == 3 ? 2 * S : S);
+  static_assert(K3 == 0 || (BMK == 1 && !DUAL), "RC: the residual BatchNorm's bit-mask kind");
+  static_assert(MODE != 3 || (!STATS && BMK < 0 && !PRE), "APPLY: a plain epilogue");
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   bf16_t* stg = lds + 3 * CH;
   static_assert(!DUAL || BMK == 1, "DUAL: the residual BatchNorm's ReLU bit mask");
@@ -113,16 +133,19 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   static_assert(!(STATS && BNB), "one slab per launch");
   constexpr bool do_stats = STATS || BNB;
   constexpr int mode = MODE;
-  // prefetch loads per chunk: the accumulate operands, the BN input, its mask bytes
-  constexpr int L = (MODE == 1 ? S : (MODE == 2 ? 2 * S : 0)) + (BNB ? S : 0) + (BMK == 1 ? S : 0) +
-                    (DUAL ? S : 0);
+  // prefetch loads per chunk: the accumulate operands (APPLY: the residual), the BN input (not
+  // with RC: recomputed), its mask bytes
+  constexpr int L = (MODE == 1 || MODE == 3 ? S : (MODE == 2 ? 2 * S : 0)) +
+                    (BNB && K3 == 0 ? S : 0) + (BMK == 1 ? S : 0) + (DUAL ? S : 0);
 
   // BNB: this block's copy of the per-channel parameters (one float4 per array per thread:
   // N <= 2048), written to LDS after the first wait
   constexpr int NPRM = (BMK == 2 || DUAL) ? 4 : 2;
   float4 prm[NPRM];
-  if constexpr (BNB) {
-    const float* arrs[4] = {g.bmean, g.binv, DUAL ? g.bmeanp : g.bsc, DUAL ? g.binvp : g.bsh};
+  constexpr bool HASPRM = BNB || MODE == 3;     // per-channel parameters staged in LDS
+  if constexpr (HASPRM) {
+    const float* arrs[4] = {MODE == 3 ? g.asc : g.bmean, MODE == 3 ? g.ash : g.binv,
+                            DUAL ? g.bmeanp : g.bsc, DUAL ? g.binvp : g.bsh};
 #pragma unroll
     for (int a = 0; a < NPRM; ++a)
       prm[a] = tid * 4 < g.N ? *reinterpret_cast<const float4*>(arrs[a] + tid * 4)
@@ -143,21 +166,49 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     }
   }
 
+  // RC: this wave's 32 rows of y2 (the recompute's A operand), loaded once like A
+  constexpr int KS3R = KS3 > 0 ? KS3 : 1;
+  bf16x8_t yf[2][KS3R];
+  if constexpr (K3 > 0) {
+    const __amdgpu_buffer_rsrc_t ry2 =
+        srsrc(g.y2 + m0 * K3, (uint32_t)(((long)(rows_blk - 1) * K3 + K3) * 2));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = wave * kSWR + i * 16 + frow;
+#pragma unroll
+      for (int ks = 0; ks < KS3; ++ks) {
+        const uint32_t off = r < rows_blk ? (uint32_t)((r * K3 + ks * 32 + fq * 8) * 2) : kSOOB;
+        yf[i][ks] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(ry2, off, 0, 0));
+      }
+    }
+  }
+
   // B chunk c -> ring slot c % 3: DMA instruction q = wave + 8 j fills rows (q % 8) * 8 .. + 7 of
-  // 64-deep panel q / 8; chunks past the end are issued too, out of range (constant counts)
+  // 64-deep panel q / 8; chunks past the end are issued too, out of range (constant counts).
+  // RC: the slot's second part holds the w3 chunk (rows c * 64 .., K3 deep), same layout
   const i32x4_t rb = rsrc_quad(g.B, (uint32_t)(((long)(g.N - 1) * g.ldb + K) * 2));
+  const i32x4_t rw3 = rsrc_quad(K3 > 0 ? (const void*)g.w3 : (const void*)g.B,
+                                K3 > 0 ? (uint32_t)((long)g.N * K3 * 2) : 0u);
   const uint32_t lds0 = lds_addr(lds);
   const int lrow = lane >> 3, slot = lane & 7;
   auto issue = [&](int c) {
     const bool live = c < nch;
     const uint32_t base = lds0 + (uint32_t)((c % 3) * CH) * 2u;
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
+    for (int j = 0; j < K / 64; ++j) {
       const int q = wave + 8 * j, kp = q >> 3, rg = q & 7;
       const int r = rg * 8 + lrow;
       const uint32_t off = live ? (uint32_t)(((c * kSBN + r) * g.ldb + kp * 64 + sswz(r, slot) * 8) * 2)
                                 : 0xFFFFFFF0u;
       dma16(rb, base + (uint32_t)(kp * 64 * 64 + rg * 8 * 64) * 2u, off);
+    }
+#pragma unroll
+    for (int j = 0; j < K3 / 64; ++j) {
+      const int q = wave + 8 * j, kp = q >> 3, rg = q & 7;
+      const int r = rg * 8 + lrow;
+      const uint32_t off = live ? (uint32_t)(((c * kSBN + r) * K3 + kp * 64 + sswz(r, slot) * 8) * 2)
+                                : 0xFFFFFFF0u;
+      dma16(rw3, base + (uint32_t)(CHB + kp * 64 * 64 + rg * 8 * 64) * 2u, off);
     }
   };
 
@@ -165,8 +216,12 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   const long ldc = g.ldc;
   const __amdgpu_buffer_rsrc_t rc = srsrc(g.C + m0 * ldc, (uint32_t)(rows_blk * ldc * 2));
   const __amdgpu_buffer_rsrc_t rcin =
-      srsrc(mode == 1 ? (const void*)(g.Cin + m0 * ldc) : (const void*)(g.acc_src + m0 * ldc),
+      srsrc(mode == 1 || mode == 3 ? (const void*)(g.Cin + m0 * ldc)
+                                   : (const void*)(g.acc_src + m0 * ldc),
             mode ? (uint32_t)(rows_blk * ldc * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t ramask =
+      srsrc(mode == 3 ? (const void*)(g.amask + m0 * ldc / 8) : (const void*)g.C,
+            mode == 3 ? (uint32_t)(rows_blk * ldc / 8) : 0u);
   const __amdgpu_buffer_rsrc_t rmask =
       srsrc(mode == 2 ? (const void*)(g.acc_mask + m0 * ldc / 8) : (const void*)g.C,
             mode == 2 ? (uint32_t)(rows_blk * ldc / 8) : 0u);
@@ -178,7 +233,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   uint4 pre[S], bxp[S], bpp[S];
   uint32_t pmask[S], bmp[S];
   const __amdgpu_buffer_rsrc_t rbx =
-      srsrc(BNB ? (const void*)(g.bx + m0 * ldc) : (const void*)g.C,
+      srsrc(BNB && K3 == 0 ? (const void*)(g.bx + m0 * ldc) : (const void*)g.C,
             BNB ? (uint32_t)(rows_blk * ldc * 2) : 0u);
   const __amdgpu_buffer_rsrc_t rbm =
       srsrc(BMK == 1 ? (const void*)(g.bmask + m0 * ldc / 8) : (const void*)g.C,
@@ -187,7 +242,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
       srsrc(DUAL ? (const void*)(g.bxp + m0 * ldc) : (const void*)g.C,
             DUAL ? (uint32_t)(rows_blk * ldc * 2) : 0u);
   auto prefetch = [&](int c) {
-    if constexpr (MODE == 0 && !BNB) return;
+    if constexpr (L == 0) return;
     const int cc = c < nch ? c : 0;
 #pragma unroll
     for (int t = 0; t < S; ++t) {
@@ -196,7 +251,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
         pre[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rcin, off, 0, 0));
       if constexpr (MODE == 2)
         pmask[t] = __builtin_amdgcn_raw_buffer_load_b8(rmask, off == kSOOB ? kSOOB : off / 16, 0, 0);
-      if constexpr (BNB)
+      if constexpr (BNB && K3 == 0)
         bxp[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rbx, off, 0, 0));
       if constexpr (BMK == 1)
         bmp[t] = __builtin_amdgcn_raw_buffer_load_b8(rbm, off == kSOOB ? kSOOB : off / 16, 0, 0);
@@ -257,10 +312,10 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
   bf16_t* ws = stg + wave * kSWR * kSP;
   for (int c = 0; c < nch; ++c) {
     // this wave's DMAs of chunk c landed (everything issued after them may still fly) ...
-    if (c >= 2) wait_vmc<2 * S + 2 * L + D>();
-    else if (c == 1) wait_vmc<2 * L + D + S + Y>();
+    if (c >= 2) wait_vmc<2 * SST + 2 * L + D>();
+    else if (c == 1) wait_vmc<2 * L + D + SST + Y>();
     else wait_vmc<D + L + Y>();
-    if constexpr (BNB) {
+    if constexpr (HASPRM) {
       if (c == 0 && tid * 4 < g.N) {
 #pragma unroll
         for (int a = 0; a < NPRM; ++a) *reinterpret_cast<float4*>(bprm + a * g.N + tid * 4) = prm[a];
@@ -306,7 +361,7 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
         for (int r = 0; r < 4; ++r) {
           const int row = i * 16 + fq * 4 + r;
           const bf16_t h = f2bf(acc[i][j][r]);
-          if constexpr (PROBE & 2) asm volatile("" ::"v"(h));
+          if constexpr ((PROBE & 2) || NOST) asm volatile("" ::"v"(h));
           else ws[row * kSP + j * 16 + frow] = h;
           if (STATS && wave * kSWR + row < rows_blk) {
             const float q = bf2f(h);
@@ -334,6 +389,43 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
     // the staged tile is read back by other lanes of this wave: keep the reads behind the
     // writes (one wave's LDS instructions execute in order)
     asm volatile("" ::: "memory");
+    if constexpr (NOST) {
+      prefetch(c + 1);
+      continue;                               // statistics only: nothing is stored
+    }
+    uint4 cv[S];
+#pragma unroll
+    for (int t = 0; t < S; ++t)
+      cv[t] = (PROBE & 2) ? make_uint4(0u, 0u, 0u, (uint32_t)t)
+                          : *reinterpret_cast<const uint4*>(ws + (t * 8 + er) * kSP + ec * 8);
+    if constexpr (K3 > 0) {
+      // RC: x = bf16(y2 . w3^T) for this chunk's 64 columns (the producing GEMM's chain: the same
+      // fragments, k in order), staged over the C tile (already in cv) and read back per lane
+      asm volatile("" ::: "memory");
+      const bf16_t* sw3 = sb + CHB;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4_t a3[2] = {(f32x4_t){0.f, 0.f, 0.f, 0.f}, (f32x4_t){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ks = 0; ks < KS3; ++ks) {
+          const int kp = ks >> 1, ch = (ks & 1) * 4 + fq;
+          const int r = j * 16 + frow;
+          const bf16x8_t wfr = *reinterpret_cast<const bf16x8_t*>(sw3 + kp * 64 * 64 + r * 64 + sswz(r, ch) * 8);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            a3[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yf[i][ks], wfr, a3[i], 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ws[(i * 16 + fq * 4 + r) * kSP + j * 16 + frow] = f2bf(a3[i][r]);
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < S; ++t)
+        bxp[t] = *reinterpret_cast<const uint4*>(ws + (t * 8 + er) * kSP + ec * 8);
+    }
     if constexpr (L != 0) wait_vmc<D>();      // this chunk's prefetched epilogue operands
     float b1[8], b2[8], b3[8], bmu[8], bis[8], bsc[8], bsh[8];
     if constexpr (BNB) {
@@ -348,11 +440,39 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
         if constexpr (BMK == 2 || DUAL) { bsc[e] = bprm[2 * g.N + ch0 + e]; bsh[e] = bprm[3 * g.N + ch0 + e]; }
       }
     }
+    float asv[8], ahv[8];
+    if constexpr (MODE == 3) {
+      const int ch0 = c * kSBN + ec * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        asv[e] = bprm[ch0 + e];
+        ahv[e] = bprm[g.N + ch0 + e];
+      }
+    }
 #pragma unroll
     for (int t = 0; t < S; ++t) {
-      uint4 v = (PROBE & 2) ? make_uint4(0u, 0u, 0u, (uint32_t)t)
-                            : *reinterpret_cast<const uint4*>(ws + (t * 8 + er) * kSP + ec * 8);
-      if constexpr (MODE != 0) {
+      uint4 v = cv[t];
+      if constexpr (MODE == 3) {
+        // the residual BatchNorm's apply, bit-identical to bn_apply_kernel (x * sc + sh, + res,
+        // ReLU; the mask from the rounded output)
+        float xv[8], rv[8], o[8];
+        unpack8(v, xv);
+        unpack8(pre[t], rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[e] = __builtin_fmaf(xv[e], asv[e], ahv[e]);
+          o[e] += rv[e];
+          o[e] = fmaxf(o[e], 0.f);
+        }
+        v = pack8(o);
+        float ov[8];
+        unpack8(v, ov);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bits |= (ov[e] > 0.f ? 1u : 0u) << e;
+        const uint32_t mo = eoff(t, c);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bits, ramask, mo == kSOOB ? kSOOB : mo / 16, 0, 0);
+      } else if constexpr (MODE != 0) {
         float a[8], b[8];
         unpack8(v, a);
         unpack8(pre[t], b);
@@ -427,27 +547,38 @@ __global__ void __launch_bounds__(kST, 1) gemm_stream_kernel(const StreamArgs g)
 }
 
 template <int K, int MODE, bool STATS, int BMK = -1, bool PRE = false, int PROBE = 0,
-          bool DUAL = false>
+          bool DUAL = false, bool NOST = false, int K3 = 0>
 void launch_stream(const StreamArgs& g, hipStream_t st) {
-  constexpr size_t BASE = (size_t)3 * kSBN * K * 2 + (size_t)8 * kSWR * kSP * 2 +
+  constexpr size_t BASE = (size_t)3 * kSBN * (K + K3) * 2 + (size_t)8 * kSWR * kSP * 2 +
                           (size_t)2 * 8 * (DUAL ? 3 : 2) * kSBN * 4;
   static_assert(BASE <= 160 * 1024, "gemm_stream LDS");
-  // BNB: + the per-channel parameter arrays
-  const size_t LDS = BASE + (BMK >= 0 ? (size_t)((BMK == 2 || DUAL) ? 4 : 2) * g.N * 4 : 0);
-  if (LDS > 160 * 1024) throw std::runtime_error("gemm_stream: BN-backward parameters exceed LDS");
+  // BNB / APPLY: + the per-channel parameter arrays
+  const size_t LDS = BASE + (BMK >= 0 ? (size_t)((BMK == 2 || DUAL) ? 4 : 2) * g.N * 4
+                             : MODE == 3 ? (size_t)2 * g.N * 4 : 0);
+  if (LDS > 160 * 1024) throw std::runtime_error("gemm_stream: per-channel parameters exceed LDS");
+  auto kern = gemm_stream_kernel<K, MODE, STATS, BMK, PRE, PROBE, DUAL, NOST, K3>;
   static bool attr = false;
   if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_stream_kernel<K, MODE, STATS, BMK, PRE, PROBE, DUAL>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024));
     attr = true;
   }
   const unsigned blocks = (unsigned)((g.M + kSBM - 1) / kSBM);
-  hipLaunchKernelGGL((gemm_stream_kernel<K, MODE, STATS, BMK, PRE, PROBE, DUAL>), dim3(blocks),
-                     dim3(kST), LDS, st, g);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kST), LDS, st, g);
 }
 
 template <int K, int MODE>
 void launch_stream_bnb(const StreamArgs& g, int bmk, hipStream_t st) {
+  if (g.y2) {            // RC: the residual BN's input recomputed (kind 1, K <= 128, K3 64 / 128)
+    if constexpr (K <= 128) {
+      if (bmk != 1 || g.bxp) throw std::runtime_error("gemm_stream_bnb: RC needs kind 1, no dual");
+      if (g.k3 == 64) launch_stream<K, MODE, false, 1, false, 0, false, false, 64>(g, st);
+      else if (g.k3 == 128) launch_stream<K, MODE, false, 1, false, 0, false, false, 128>(g, st);
+      else throw std::runtime_error("gemm_stream_bnb: RC depth K3 in {64, 128}");
+      return;
+    }
+    throw std::runtime_error("gemm_stream_bnb: RC needs K <= 128");
+  }
   if (g.bxp) launch_stream<K, MODE, false, 1, false, 0, true>(g, st);
   else if (bmk == 1) launch_stream<K, MODE, false, 1>(g, st);
   else if (bmk == 2) launch_stream<K, MODE, false, 2>(g, st);
@@ -457,9 +588,14 @@ void launch_stream_bnb(const StreamArgs& g, int bmk, hipStream_t st) {
 template <int K>
 void launch_stream_k(const StreamArgs& g, int bmk, hipStream_t st) {
   if (g.pre_y) {
-    if (g.stats) launch_stream<K, 0, true, -1, true>(g, st);
+    if (g.nost) {
+      if (!g.stats) throw std::runtime_error("gemm_stream_pre: no-store form needs statistics");
+      launch_stream<K, 0, true, -1, true, 0, false, true>(g, st);
+    } else if (g.stats) launch_stream<K, 0, true, -1, true>(g, st);
     else launch_stream<K, 0, false, -1, true>(g, st);
-  } else if (g.bx) {
+  } else if (g.asc) {
+    launch_stream<K, 3, false>(g, st);
+  } else if (g.bx || g.y2) {
     if (g.Cin) launch_stream_bnb<K, 1>(g, bmk, st);
     else if (g.acc_mask) launch_stream_bnb<K, 2>(g, bmk, st);
     else launch_stream_bnb<K, 0>(g, bmk, st);
@@ -508,16 +644,21 @@ void dtf_gemm_stream_bnb(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int
                          int lda, int ldb, int ldc, const bf16_t* Cin, const bf16_t* acc_src,
                          const uint8_t* acc_mask, const bf16_t* bx, const float* bmean,
                          const float* binv, const float* bsc, const float* bsh,
-                         const uint8_t* bmask, int kind, float* part, int nt, hipStream_t st) {
+                         const uint8_t* bmask, int kind, float* part, int nt, hipStream_t st,
+                         const bf16_t* y2, const bf16_t* w3, int k3) {
   if (!dtf_gemm_stream_ok(M, N, K, lda, ldb, ldc) || ldc != N || N > 2048)
     throw std::runtime_error("gemm_stream_bnb: stream shape, dense C, N <= 2048");
   if (Cin && acc_mask) throw std::runtime_error("gemm_stream_bnb: Cin or masked acc, not both");
   if (acc_mask && !acc_src) throw std::runtime_error("gemm_stream_bnb: masked acc needs acc_src");
-  if (!bx || !bmean || !binv || !part || kind < 0 || kind > 2 || (kind == 1 && !bmask) ||
-      (kind == 2 && !(bsc && bsh)))
+  const bool rc = y2 != nullptr;
+  if ((!bx && !rc) || !bmean || !binv || !part || kind < 0 || kind > 2 || (kind == 1 && !bmask) ||
+      (kind == 2 && !(bsc && bsh)) || (rc && (!w3 || (k3 != 64 && k3 != 128) || kind != 1)))
     throw std::runtime_error("gemm_stream_bnb: BatchNorm operands");
   StreamArgs g{A, B, C, Cin, acc_src, acc_mask, part, M, N, lda, ldb, ldc, nt,
                bx, bmean, binv, bsc, bsh, bmask};
+  g.y2 = y2;
+  g.w3 = w3;
+  g.k3 = rc ? k3 : 0;
   run_stream(g, K, kind, st);
 }
 
@@ -550,13 +691,31 @@ void dtf_gemm_stream_bnb_dual(const bf16_t* A, const bf16_t* B, bf16_t* C, int M
 // pass over X and the GEMM's re-read of its output become one read of X.
 void dtf_gemm_stream_pre(const bf16_t* X, const bf16_t* B, bf16_t* C, int M, int N, int K,
                          const float* pre_sc, const float* pre_sh, bf16_t* y, float* stats,
-                         hipStream_t st) {
+                         hipStream_t st, int nostore) {
   if (!dtf_gemm_stream_ok(M, N, K, K, K, N) || !pre_sc || !pre_sh || !y)
     throw std::runtime_error("gemm_stream_pre: stream shape and BatchNorm operands");
+  if (nostore && !stats) throw std::runtime_error("gemm_stream_pre: no-store form needs stats");
   StreamArgs g{X, B, C, nullptr, nullptr, nullptr, stats, M, N, K, K, N, 0};
   g.pre_sc = pre_sc;
   g.pre_sh = pre_sh;
   g.pre_y = y;
+  g.nost = nostore ? 1 : 0;
+  run_stream(g, K, -1, st);
+}
+
+// The residual BatchNorm's apply on a conv output that was never stored (lazy x3): Y = relu(
+// bf16(A . W^T) * sc + sh + res) and its ReLU bit mask, with A = the conv's input [M][K] and the
+// GEMM the producing stream GEMM's exact chain -- bit-identical to storing the conv output and
+// running the apply pass over it.
+void dtf_gemm_stream_apply(const bf16_t* A, const bf16_t* W, bf16_t* Y, int M, int N, int K,
+                           const bf16_t* res, const float* sc, const float* sh, uint8_t* mask,
+                           hipStream_t st) {
+  if (!dtf_gemm_stream_ok(M, N, K, K, K, N) || !res || !sc || !sh || !mask || N > 4096)
+    throw std::runtime_error("gemm_stream_apply: stream shape and BatchNorm operands");
+  StreamArgs g{A, W, Y, res, nullptr, nullptr, nullptr, M, N, K, K, N, 0};
+  g.asc = sc;
+  g.ash = sh;
+  g.amask = mask;
   run_stream(g, K, -1, st);
 }
 

@@ -84,6 +84,9 @@ class Bottleneck(nn.Module):
         self.c1 = ConvBN(cin, width, 1, 1, f"{name}_1", bn_momentum, bn_eps)
         self.c2 = ConvBN(width, width, 3, stride, f"{name}_2", bn_momentum, bn_eps)
         self.c3 = ConvBN(width, cout, 1, 1, f"{name}_3", bn_momentum, bn_eps, zero_gamma)
+        # set by the network: this identity block's output feeds another identity block, whose
+        # streamed c1 data gradient can recompute our c3 output (see _c2_c3)
+        self.lazy_c3 = False
 
     def forward(self, x):
         # projection blocks: proj and c1 both read x -> one dgrad buffer, no autograd add
@@ -106,14 +109,18 @@ class Bottleneck(nn.Module):
 
     def _c2_c3(self, y):
         """c2 conv -> BN + ReLU -> c3 conv (c3's output, before its BatchNorm).  Training: the
-        BN + ReLU runs inside c3's GEMM (ops.batch_norm_relu_conv1x1) where that GEMM streams."""
+        BN + ReLU runs inside c3's GEMM (ops.batch_norm_relu_conv1x1) where that GEMM streams.
+        Identity blocks followed by an identity block: c3's output only feeds the block-output
+        BN, which recomputes it (``lazy_out``: never stored).  The last block of a stage feeds a
+        stride-2 projection whose data gradient would have to recompute it once more (measured a
+        net loss), so it stores it."""
         c2, c3 = self.c2, self.c3
         if c2.bn.training and FUSE_BN_CONV:
             y = ops.conv2d(y, c2.conv.kernel, c2.conv.strides, c2.conv.padding, bn_stats=True)
             b = c2.bn
             return ops.batch_norm_relu_conv1x1(y, b.gamma, b.beta, b.moving_mean,
                                                b.moving_variance, c3.conv.kernel, b.momentum,
-                                               b.epsilon)
+                                               b.epsilon, lazy_out=self.lazy_c3)
         y = c2(y)
         return ops.conv2d(y, c3.conv.kernel, c3.conv.strides, c3.conv.padding,
                           bn_stats=c3.bn.training)
@@ -136,6 +143,8 @@ class ResNet(Layer):
                                              bn_momentum, bn_eps, zero_init_residual))
                     cin = width * 4
             self.blocks = nn.ModuleList(blocks)
+            for cur, nxt in zip(blocks, blocks[1:]):
+                cur.lazy_c3 = not cur.has_proj and not nxt.has_proj
             self.fc = Dense(cin, num_classes, name="predictions")
             nn.init.normal_(self.fc.kernel.data, 0.0, 0.01)
 

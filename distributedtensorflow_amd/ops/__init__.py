@@ -101,13 +101,15 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
 
 
 def batch_norm_relu_conv1x1(x, gamma, beta, running_mean, running_var, w, momentum=0.997,
-                            eps=1e-5):
+                            eps=1e-5, lazy_out=False):
     """conv2d(relu(batch_norm(x, training=True)), w) for a 1x1 stride-1 conv.  Native path (when
     the conv runs on the row-streaming GEMM): one fused op, the BN output is written once by the
-    GEMM instead of by a separate apply pass.  Else the two ops."""
+    GEMM instead of by a separate apply pass.  Else the two ops.  ``lazy_out``: the caller's
+    only consumer of the result is a residual BatchNorm + ReLU (a bottleneck's c3), which may
+    recompute the conv output instead of reading it (native: never stored)."""
     if _use_native(x) and _native().bn_relu_conv1x1_ok(x, w):
         return _native().bn_relu_conv1x1(x, gamma, beta, running_mean, running_var, w, momentum,
-                                         eps)
+                                         eps, lazy_out)
     y = batch_norm(x, gamma, beta, running_mean, running_var, True, momentum, eps, relu=True)
     return conv2d(y, w, 1, 0, bn_stats=True)
 

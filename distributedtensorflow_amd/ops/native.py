@@ -13,6 +13,7 @@ Precision contract (mixed precision, TF-style "float32 variables, bf16 compute")
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -64,6 +65,10 @@ if os.environ.get("DTF_BN_GRID_CAP"):     # BN row-sweep grid cap override (2048
     _K.bn_set_grid_cap(int(os.environ["DTF_BN_GRID_CAP"]))
 if os.environ.get("DTF_BN_STATS_BLOCKS"):  # BN reduce-pass block target (1024 = round-2)
     _K.bn_set_stats_blocks(int(os.environ["DTF_BN_STATS_BLOCKS"]))
+if os.environ.get("DTF_GEMM_PP2"):      # round-5 persistent GEMM: bit 0 gemm_nt, bit 1 convs
+    _K.gemm_set_pp2(int(os.environ["DTF_GEMM_PP2"]))
+elif os.environ.get("DTF_DENSE_GEMM") == "native":
+    _K.gemm_set_pp2(1)                  # the dense layers' GEMMs go to the persistent kernel
 if os.environ.get("DTF_STORE_NT"):      # non-temporal output stores: bit 0 conv, 1 GEMM, 2 BN
     _nt = int(os.environ["DTF_STORE_NT"])
     _K.conv_set_nt(_nt & 1)
@@ -286,6 +291,7 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_f
     part, row0 = None, 0
     if bnb is not None:
         xb, stats, mask, relu, has_res, tok = bnb
+        _materialized(xb)              # a lazy c3 output: the tap kernels read it
         # slab rows of exactly the kernel each launch takes (the halo kernels: one per block)
         rows = [_K.conv_tile_rows(_fwd_geom(dyc.shape, C, taps, Pc, Qc, 1, 1, h, wd, sh, sw, a, b,
                                             acc),
@@ -345,6 +351,12 @@ def _dgrad_1x1_bnb(dyc, wt, M, C, K, xshape, out, acc_from, bnb):
     G = _K.gemm_tile_rows(M)
     part = torch.empty(_K.bn_workspace_floats_g(G, C), device=dyc.device, dtype=torch.float32)
     kind = (1 if has_res else 2) if relu else 0
+    # lazy x3 (RC): the epilogue recomputes the BN input from the producing conv's operands
+    rc = getattr(xb, "_dtf_recompute", None)
+    if rc is not None and (rc.done or kind != 1 or K > 128 or rc.k3 not in (64, 128)):
+        _materialized(xb)
+        rc = None
+    y2, w3, k3 = (rc.y.data_ptr(), rc.wb.data_ptr(), rc.k3) if rc is not None else (0, 0, 0)
     _K.gemm_stream_bnb(dyc.data_ptr(), wt.data_ptr(), o2.data_ptr(), M, C, K, K, K, C,
                        o2.data_ptr() if out is not None else 0,
                        acc_from.dy.data_ptr() if acc_from is not None else 0,
@@ -352,7 +364,7 @@ def _dgrad_1x1_bnb(dyc, wt, M, C, K, xshape, out, acc_from, bnb):
                        xb.data_ptr(), stats[0].data_ptr(), stats[1].data_ptr(),
                        stats[2].data_ptr() if kind == 2 else 0,
                        stats[3].data_ptr() if kind == 2 else 0,
-                       _p(mask) if kind == 1 else 0, kind, part.data_ptr(), _st())
+                       _p(mask) if kind == 1 else 0, kind, part.data_ptr(), _st(), y2, w3, k3)
     dx = o2.view(xshape)
     # valid only for this exact gradient: autograd may add another contribution IN PLACE
     # (a residual gradient summed outside the epilogue), which bumps the version counter
@@ -361,6 +373,8 @@ def _dgrad_1x1_bnb(dyc, wt, M, C, K, xshape, out, acc_from, bnb):
 
 
 def _dgrad_1x1_bnb_dual(dyc, wt, M, C, K, xshape, out, acc_from, d):
+    _materialized(d.x)
+    _materialized(d.xp)
     if out is not None and acc_from is not None:
         out.add_(acc_from.materialize())
         acc_from = None
@@ -715,6 +729,7 @@ class _LazyBnDx:
         C = self.x.shape[-1]
         M = self.x.numel() // C
         dx = torch.empty_like(self.x)
+        _materialized(self.x)
         _K.bn_bwd_apply(self.dy.data_ptr(), 0, self.x.data_ptr(), self.gb[2].data_ptr(),
                         self.gb[3].data_ptr(), self.gb[4].data_ptr(), dx.data_ptr(), 0, M, C, 1,
                         _st(), 0, 0, self.mask.data_ptr())
@@ -739,8 +754,19 @@ class _BatchNorm(torch.autograd.Function):
         # apply also writes it as 1 bit per element (1/16 of the bytes of y, read twice)
         mask = (torch.empty(M * C // 8, device=dev, dtype=torch.uint8)
                 if relu and residual is not None else None)
-        _K.bn_apply(x.data_ptr(), _p(res), y.data_ptr(), scale.data_ptr(), shift.data_ptr(), M, C,
-                    int(relu), st, _p(mask))
+        rc = getattr(x, "_dtf_recompute", None)
+        if rc is not None and not (relu and res is not None):
+            rc.materialize()
+            rc = None
+        if rc is not None:
+            # lazy x3: the apply recomputes the conv output in a stream GEMM whose epilogue is
+            # this apply (bit-identical to storing x3 and running the pass over it)
+            _K.gemm_stream_apply(rc.y.data_ptr(), rc.wb.data_ptr(), y.data_ptr(), M, C, rc.k3,
+                                 res.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                                 mask.data_ptr(), st)
+        else:
+            _K.bn_apply(x.data_ptr(), _p(res), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                        M, C, int(relu), st, _p(mask))
         ctx.save_for_backward(x, mask, g32, stats)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -873,6 +899,7 @@ def _bn_backward_core(ctx, dy, x, mask, g32, stats, relu=None):
         # sums already produced by the dgrad epilogue of the conv that consumed y
         part, G = fused[0], fused[1]
     else:
+        _materialized(x)                   # a lazy c3 output: recomputed for the reduce pass
         part, G = torch.empty(_K.bn_workspace_floats(M, C), device=dev,
                               dtype=torch.float32), None
         _K.bn_bwd_reduce(dy.data_ptr(), 0, x.data_ptr(), mean.data_ptr(),
@@ -895,6 +922,7 @@ def _bn_backward_core(ctx, dy, x, mask, g32, stats, relu=None):
     else:
         if dx is None:
             dx = torch.empty_like(x)
+        _materialized(x)
         _K.bn_bwd_apply(dy.data_ptr(), 0, x.data_ptr(), gb[2].data_ptr(),
                         gb[3].data_ptr(), gb[4].data_ptr(), dx.data_ptr(), _p(dres), M, C,
                         int(relu), st, sc_ptr, sh_ptr, _p(mask))
@@ -937,7 +965,8 @@ class _BnReluConv1x1(torch.autograd.Function):
     weight / data gradients from y, then the BN backward (ReLU recomputed from x)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, running_mean, running_var, w_master, momentum, eps):
+    def forward(ctx, x, gamma, beta, running_mean, running_var, w_master, momentum, eps,
+                lazy_out=False):
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -946,13 +975,18 @@ class _BnReluConv1x1(torch.autograd.Function):
         wb = _bf16_weight(w_master)
         K = wb.shape[0]
         y = torch.empty_like(x)
+        # lazy x3: the output tensor is allocated but never written -- the residual BN consuming
+        # it recomputes bf16(y . w^T) (the same MFMA chain) wherever it needs the values
+        lazy = bool(lazy_out) and _lazy_x3_ok(M, C, K)
         out = torch.empty(*x.shape[:-1], K, device=x.device, dtype=_BF16)
         G = _K.gemm_tile_rows(M)
         part = torch.empty(_K.bn_workspace_floats_g(G, K), device=x.device, dtype=torch.float32)
         _K.gemm_stream_pre(x.data_ptr(), wb.data_ptr(), out.data_ptr(), M, K, C,
                            stats[2].data_ptr(), stats[3].data_ptr(), y.data_ptr(),
-                           part.data_ptr(), _st())
+                           part.data_ptr(), _st(), int(lazy))
         out._dtf_bn_part = (part, G, M, K)
+        if lazy:
+            out._dtf_recompute = _Recompute(y, wb, out)
         if wb.is_contiguous():
             _register_dgrad_filter(wb)
         ctx.lz_slot = None
@@ -978,7 +1012,7 @@ class _BnReluConv1x1(torch.autograd.Function):
             lz.grad = None
         if dout is None and rec is None:
             ctx.w_param = ctx.params = None
-            return (None,) * 8
+            return (None,) * 9
         if dout is not None and rec is not None:
             dout = dout + rec.materialize()      # another consumer of the conv output
             rec = None
@@ -990,13 +1024,13 @@ class _BnReluConv1x1(torch.autograd.Function):
             dy, dw = _conv1x1_bwd_fused(ctx, None, x, y, wb, stats, target, M, C, K, lazy=rec)
             dx, dg, db, _ = _bn_backward_core(ctx, dy, x, None, g32, stats)
             ctx.w_param = ctx.params = None
-            return dx, dg, db, None, None, dw, None, None
+            return dx, dg, db, None, None, dw, None, None, None
         dout = dout.contiguous()
         if _FUSE_C1_BWD and _K.conv1x1_bwd_ok(M, C, K):
             dy, dw = _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K)
             dx, dg, db, _ = _bn_backward_core(ctx, dy, x, None, g32, stats)
             ctx.w_param = ctx.params = None
-            return dx, dg, db, None, None, dw, None, None
+            return dx, dg, db, None, None, dw, None, None, None
         if target is not None:
             conv2d_wgrad(y, dout, wb.shape, 1, 0, out=target)
             _grad_ready(ctx.w_param)
@@ -1005,7 +1039,7 @@ class _BnReluConv1x1(torch.autograd.Function):
         dy = conv2d_dgrad(dout, wb, y.shape, 1, 0)
         dx, dg, db, _ = _bn_backward_core(ctx, dy, x, None, g32, stats)
         ctx.w_param = ctx.params = None
-        return dx, dg, db, None, None, dw, None, None
+        return dx, dg, db, None, None, dw, None, None, None
 
 
 def _conv1x1_bwd_fused(ctx, dout, x, y, wb, stats, target, M, C, K, lazy=None):
@@ -1062,9 +1096,57 @@ def bn_relu_conv1x1_ok(x, w):
             and K % 64 == 0)
 
 
-def bn_relu_conv1x1(x, gamma, beta, running_mean, running_var, w, momentum=0.997, eps=1e-5):
+def bn_relu_conv1x1(x, gamma, beta, running_mean, running_var, w, momentum=0.997, eps=1e-5,
+                    lazy_out=False):
     _check_cuda_bf16(x)
-    return _BnReluConv1x1.apply(x, gamma, beta, running_mean, running_var, w, momentum, eps)
+    return _BnReluConv1x1.apply(x, gamma, beta, running_mean, running_var, w, momentum, eps,
+                                bool(lazy_out))
+
+
+class _Recompute:
+    """A bottleneck c3 output that was never stored (lazy x3): x3 = bf16(y . w^T) with y the
+    conv's input [M, K3] and w its bf16 weight [N, K3, ...] -- recomputed with the producing
+    stream GEMM's exact MFMA chain by the residual BN's apply (gemm_stream_apply), by the
+    consuming data gradient's BN-sum epilogue (gemm_stream_bnb RC) and by the fused c3 backward
+    (RC); :meth:`materialize` writes it into the tensor's own storage for any other reader."""
+    __slots__ = ("y", "wb", "out", "done")
+
+    def __init__(self, y, wb, out):
+        # the output holds this record: a weak reference back keeps them out of a cycle
+        self.y, self.wb, self.out, self.done = y, wb, weakref.ref(out), False
+
+    @property
+    def k3(self):
+        return self.y.shape[-1]
+
+    def materialize(self):
+        out = self.out()
+        if not self.done and out is not None:
+            N = out.shape[-1]
+            M = out.numel() // N
+            gemm_nt(self.y.view(M, self.k3), self.wb.view(N, self.k3), out=out.view(M, N))
+            self.done = True
+        return out
+
+
+def _lazy_x3_ok(M, C, K):
+    """Lazy x3 for this c3 (reduction C, output K): every reader can recompute it -- the stream
+    apply (C in {64, 128}), the consumers' RC BN-sum epilogue (K3 = C <= 128) and the fused c3
+    backward, which recomputes x3 only at stage 0 (C = 64; stage 1 reads it)."""
+    return _LAZY_X3 and C == 64 and K % 64 == 0 and K <= 2048 and \
+        _K.conv1x1_bwd_lazy_ok(M, C, K) and _FUSE_C1_BWD and _FUSE_C3_LAZY
+
+
+# never store the stage-0 identity blocks' c3 output (A/B knob)
+_LAZY_X3 = os.environ.get("DTF_LAZY_X3", "1") == "1"
+
+
+def _materialized(x):
+    """``x`` with its values: a lazy c3 output is recomputed into its own storage first."""
+    rc = getattr(x, "_dtf_recompute", None)
+    if rc is not None:
+        rc.materialize()
+    return x
 
 
 # BN + ReLU of a bottleneck's c2 output applied inside c3's streaming GEMM (A/B knob)
@@ -1421,9 +1503,24 @@ def _dense_weight_grad(w_param, x2, dy2):
     return dw
 
 
+# BERT's plain dense GEMMs (forward y = x W^T + b and the data gradient dx = dy W, beta = 1 onto a
+# pending residual gradient) on our persistent MFMA GEMM (gemm.hip gemm_pp2, variant 15) instead of
+# hipBLASLt: "native" / "library" (A/B knob; see _dense_gemm_native)
+_DENSE_GEMM = os.environ.get("DTF_DENSE_GEMM", "library")
+
+
+def _dense_gemm_native(M, N, K):
+    """Our GEMM takes this dense layer's forward / data gradient: DTF_DENSE_GEMM=native and the
+    shape is the persistent kernel's (N % 8, K % 64, K >= 128, 32-bit operand offsets)."""
+    return (_DENSE_GEMM == "native" and N % 8 == 0 and N > 128 and K % 64 == 0 and K >= 128
+            and _K.gemm_pp2_ok(M, N, K, K, K))
+
+
 class _Dense(torch.autograd.Function):
-    """y = x @ W^T (+ b) on hipBLASLt with the bf16 weight shadow; backward produces dW and db in
-    fp32 straight into the optimizer's flat gradient buffer (no bf16 dW, no cast/add kernels)."""
+    """y = x @ W^T (+ b) with the bf16 weight shadow -- on hipBLASLt, or with DTF_DENSE_GEMM=native
+    on our persistent MFMA GEMM with the bias in its epilogue (forward) and the pending residual
+    gradient accumulated with beta = 1 (data gradient); backward produces dW and db in fp32
+    straight into the optimizer's flat gradient buffer (no bf16 dW, no cast/add kernels)."""
 
     @staticmethod
     def forward(ctx, x, w_master, wb, b, gelu_b=None):
@@ -1447,6 +1544,12 @@ class _Dense(torch.autograd.Function):
             ctx.set_materialize_grads(False)
             shape = (*x.shape[:-1], o)
             return z.view(shape), h.view(shape)
+        o, i = wb.shape
+        if x.is_contiguous() and wb.is_contiguous() and _dense_gemm_native(x.numel() // i, o, i):
+            if x.requires_grad:
+                _register_dgrad_filter(wb.view(o, 1, 1, i))    # batched W^T for the backward
+            y = gemm_nt(x.view(-1, i), wb, bias=None if b is None else b.detach())
+            return y.view(*x.shape[:-1], o)
         return torch.nn.functional.linear(x, wb, None if b is None else b.to(x.dtype))
 
     @staticmethod
@@ -1464,11 +1567,19 @@ class _Dense(torch.autograd.Function):
             del ctx.x_ref._dtf_pending_grad
         ctx.x_ref = None
         if ctx.needs_input_grad[0]:
+            native = (dy2.dtype == _BF16 and _dense_gemm_native(T, i, o))
+            if native:
+                dyc = dy2 if dy2.is_contiguous() else dy2.contiguous()
+                wt = _transposed_bf16(wb)                              # [i, o]
             if pending is not None and pending.dtype == dy2.dtype and pending.is_contiguous():
                 # d(x) = d(residual) + dy @ W as one GEMM with beta = 1 on the residual gradient
-                dx = pending.view(-1, i).addmm_(dy2, wb).view(x.shape)
+                if native:
+                    pv = pending.view(-1, i)
+                    dx = gemm_nt(dyc, wt, out=pv, cin=pv).view(x.shape)
+                else:
+                    dx = pending.view(-1, i).addmm_(dy2, wb).view(x.shape)
             else:
-                dx = (dy2 @ wb).reshape(x.shape)
+                dx = (gemm_nt(dyc, wt) if native else dy2 @ wb).reshape(x.shape)
                 if pending is not None:
                     dx = dx + pending.view(x.shape)
         if ctx.needs_input_grad[1]:
@@ -1531,6 +1642,8 @@ class _BiasGeluDense(torch.autograd.Function):
         ctx.save_for_backward(a2, b32 if b32 is not None else a2, h, wb)
         ctx.params = (b1, w_master)
         ctx.shape = a.shape
+        if h.is_contiguous() and wb.is_contiguous() and _dense_gemm_native(h.shape[0], o, i):
+            return gemm_nt(h, wb).view(*a.shape[:-1], o)
         return torch.nn.functional.linear(h, wb).view(*a.shape[:-1], o)
 
     @staticmethod

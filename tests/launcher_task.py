@@ -25,8 +25,16 @@ def main():
     if mode == "hang" and a.job_name == "worker" and a.task_index == 1:
         stalled_wait()
     if mode == "ps_fail":
+        ready = os.environ.get("LAUNCHER_TASK_DIR")
         if a.job_name == "ps":
+            # fail only once both workers can dump their stacks (SIGUSR1 handler installed)
+            t0 = time.time()
+            while ready and time.time() - t0 < 30 and not all(
+                    os.path.exists(os.path.join(ready, f"ready_worker{i}")) for i in (0, 1)):
+                time.sleep(0.05)
             sys.exit(3)
+        if ready:
+            open(os.path.join(ready, f"ready_{a.job_name}{a.task_index}"), "w").close()
         stalled_wait()
     return 0
 

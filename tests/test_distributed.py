@@ -322,7 +322,9 @@ def test_any_task_killed_is_restarted_and_training_resumes(tmp_path, mnist_dir, 
     named, saved = int(last.rsplit("-", 1)[1]), int(load_variable(last, "global_step"))
     assert named >= 45 and 0 <= saved - named <= 2, (last, saved)
     steps = [int(s) for s in re.findall(r"global step: (\d+)\)", text["worker0"])]
-    assert steps and steps[-1] >= 44
+    # async: the other worker may take the last two steps while the chief is between steps, and
+    # a pipelined step reports a lower bound of the step its push became (one step in flight)
+    assert steps and steps[-1] >= 42, steps[-5:]
 
 
 @pytest.mark.parametrize("strategy", ["mirrored", "ps"])
@@ -380,7 +382,7 @@ def test_ps_killed_mid_run_is_restarted_and_training_resumes(tmp_path, mnist_dir
     m = re.search(r"restored=(\S+model\.ckpt-(\d+))", text["worker0"])
     assert m and 10 <= int(m.group(2)) <= 25, text["worker0"][-3000:]
     steps = [int(s) for s in re.findall(r"global step: (\d+)\)", text["worker0"])]
-    assert steps[-1] >= 44           # async: the other worker may take the last step
+    assert steps[-1] >= 42, steps[-5:]      # async + pipelined: see the test above
     from distributedtensorflow_amd.train.checkpoint import latest_checkpoint, load_variable
     last = latest_checkpoint(str(ckpt))
     # async training: as with TF's CheckpointSaverHook, the file is named by the global step the

@@ -30,7 +30,8 @@ def test_stalled_task_times_out_with_logs_and_stacks(tmp_path):
 
 def test_task_failing_for_good_ends_the_job_at_once(tmp_path):
     t0 = time.time()
-    codes, logs = launch_local(TASK, 1, 2, str(tmp_path), env={"LAUNCHER_TASK_MODE": "ps_fail"},
+    codes, logs = launch_local(TASK, 1, 2, str(tmp_path), env={"LAUNCHER_TASK_MODE": "ps_fail",
+                                                                "LAUNCHER_TASK_DIR": str(tmp_path)},
                                timeout_s=120, grace_s=2)
     assert time.time() - t0 < 40, "the workers must be stopped, not waited for"
     assert codes[("ps", 0)] == 3 and codes[("worker", 0)] != 0 and codes[("worker", 1)] != 0
