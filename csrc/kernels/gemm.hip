@@ -1140,6 +1140,18 @@ gemm_pp2_kernel(const GemmArgs g) {
     return r0 + lrow;
   };
   const int pch = gswz<BK>(prow(0, 0), slot) * 8;   // the same for every piece of this wave
+  // ILV (the non-strided instantiations without BN statistics): the MFMA operands in their natural order and the B
+  // rows INTERLEAVED over the wave's four 16-column fragments -- fragment jj's row f holds output
+  // column 4 f + jj of the wave's 64-column strip -- so lane (frow, fq) ends up holding
+  // C[4 fq + r][4 frow .. 4 frow + 3] of each 16-row fragment: one 8-B store per (fragment row,
+  // register) and 16 lanes cover 128 contiguous bytes of a row, i.e. every store instruction
+  // writes four WHOLE 128-B lines (the swapped layout wrote 16 rows x 32 B per instruction and
+  // completed a line only over four instructions 8 apart).  The K order per output is unchanged:
+  // bit-identical to the swapped layout.  B rows use the swizzle chunk ^ ((row >> 3) & 7), so the
+  // fragment reads (rows 4 f + jj, f = 0..15) hit the same bank pattern as consecutive rows with
+  // the A swizzle.
+  constexpr bool ILV = !strided && !(EPI & 1);   // (with BN statistics: VGPR spills)
+  auto bswz = [&](int row, int ch) { return ILV ? ch ^ ((row >> 3) & 7) : gswz<BK>(row, ch); };
   auto plds = [&](int pc, int j) {
     const bool isA = pc == 0 || pc == 3;
     return (uint32_t)((isA ? 0 : Cf::SA) + (prow(pc, j) - lrow) * BK) * 2u;
@@ -1181,7 +1193,7 @@ gemm_pp2_kernel(const GemmArgs g) {
         } else {
           const int n = n0 + row;
           const bool ok = valid && n < g.N;
-          o[pc][j] = ok ? (uint32_t)(n * g.ldb + pch) * 2u : 0x80000000u;
+          o[pc][j] = ok ? (uint32_t)(n * g.ldb + bswz(row, slot) * 8) * 2u : 0x80000000u;
         }
       }
   };
@@ -1246,8 +1258,17 @@ gemm_pp2_kernel(const GemmArgs g) {
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int r = wn * 64 + half * 32 + j * 16 + frow, ch = ks * 4 + fq;
-        fb[ks * 2 + j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
+        const int ch = ks * 4 + fq;
+        if constexpr (ILV) {
+          // rows 4 frow + jj, jj < 4: one swizzle value ((4 frow + jj) >> 3 == frow >> 1), so
+          // the four fragments' addresses differ by immediate offsets only
+          const int r = wn * 64 + 4 * frow + half * 2 + j;
+          fb[ks * 2 + j] = *reinterpret_cast<const bf16x8_t*>(
+              sb + r * BK + ((ch ^ ((frow >> 1) & 7)) << 3));
+        } else {
+          const int r = wn * 64 + half * 32 + j * 16 + frow;
+          fb[ks * 2 + j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
+        }
       }
   };
   auto sync = [&]() {
@@ -1265,8 +1286,11 @@ gemm_pp2_kernel(const GemmArgs g) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[ah * 4 + i][bh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              fb[ks * 2 + j], fA[ks * 4 + i], acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
+          acc[ah * 4 + i][bh * 2 + j] = ILV
+              ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fA[ks * 4 + i], fb[ks * 2 + j],
+                                                        acc[ah * 4 + i][bh * 2 + j], 0, 0, 0)
+              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks * 2 + j], fA[ks * 4 + i],
+                                                        acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     sync();
   };
@@ -1322,6 +1346,94 @@ gemm_pp2_kernel(const GemmArgs g) {
     const __amdgpu_buffer_rsrc_t rc =
         __builtin_amdgcn_make_buffer_rsrc(g.C + cbase, 0, (int)cbytes, 0x00020000);
     const bool nt_store = g.nt != 0;
+    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+    if constexpr (ILV) {
+      // lane (frow, fq), fragment row i, register r: C[m][ncol .. ncol + 3], m = 16 i + 4 fq + r
+      const int ncol = cn0 + wn * 64 + 4 * frow;
+      const bool col_ok = ncol < g.N;
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (g.bias && col_ok) {
+        const float4 bv = *reinterpret_cast<const float4*>(g.bias + ncol);
+        b4[0] = bv.x; b4[1] = bv.y; b4[2] = bv.z; b4[3] = bv.w;
+      }
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+      // byte offset of this lane's element run, advanced one row at a time by an opaque VALU add
+      // (as closed forms the compiler hoists 32 row offsets / row tests into SGPRs and spills).
+      // Rows past M lie past the descriptor's end; a column past N starts at 2^31 (beyond any
+      // C descriptor): the hardware range check drops those stores and zero-fills those loads.
+      int vo = col_ok ? ((wm * 128 + fq * 4) * g.ldc + ncol) * 2 : (int)0x80000000u;
+      const int ldc2 = g.ldc * 2;
+      // accumulate operands (the unused one points at C with zero size)
+      const __amdgpu_buffer_rsrc_t rcin = __builtin_amdgcn_make_buffer_rsrc(
+          has_acc ? const_cast<bf16_t*>(g.Cin ? g.Cin + cbase : g.acc_src + cbase) : g.C, 0,
+          has_acc ? (int)cbytes : 0, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rmask = __builtin_amdgcn_make_buffer_rsrc(
+          (has_acc && !g.Cin) ? const_cast<uint8_t*>(g.acc_mask + (cbase >> 3)) : (uint8_t*)g.C,
+          0, (has_acc && !g.Cin) ? (int)(cbytes / 16 + 1) : 0, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < Cf::FM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          bf16_t h[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            float v = acc[i][jj][r] + b4[jj];
+            if (g.relu) v = fmaxf(v, 0.f);
+            h[jj] = f2bf(v);
+            // rows past M / columns past N hold exact zeros (zero-filled operands, no bias with
+            // statistics: host), so they add nothing -- no per-row test (its 32 compare masks
+            // would live in SGPRs)
+            if (do_stats) {
+              const float qv = bf2f(h[jj]);
+              s1[jj] += qv;
+              s2[jj] += qv * qv;
+            }
+          }
+          if constexpr (has_acc) {
+            typedef uint32_t u32x2l_t __attribute__((ext_vector_type(2)));
+            const u32x2l_t sv = __builtin_bit_cast(
+                u32x2l_t, __builtin_amdgcn_raw_buffer_load_b64(rcin, vo, 0, 0));
+            const uint32_t bits =
+                g.Cin ? 0xFu
+                      : ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rmask, vo >> 4, 0, 0) >>
+                         ((vo >> 1) & 7)) & 0xFu;
+            const float sf[4] = {__builtin_bit_cast(float, sv.x << 16),
+                                 __builtin_bit_cast(float, sv.x & 0xffff0000u),
+                                 __builtin_bit_cast(float, sv.y << 16),
+                                 __builtin_bit_cast(float, sv.y & 0xffff0000u)};
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              h[jj] = f2bf(bf2f(h[jj]) + ((bits >> jj) & 1u ? sf[jj] : 0.f));
+          }
+          const u32x2_t w = {(uint32_t)h[0] | ((uint32_t)h[1] << 16),
+                             (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+          if (nt_store) __builtin_amdgcn_raw_buffer_store_b64(w, rc, vo, 0, 2);
+          else __builtin_amdgcn_raw_buffer_store_b64(w, rc, vo, 0, 0);
+          asm volatile("v_add_u32 %0, %0, %1" : "+v"(vo) : "s"(ldc2));
+          __builtin_amdgcn_sched_barrier(0);     // one row at a time (register pressure)
+        }
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(vo) : "s"(12 * ldc2));
+      }
+      if (do_stats) {
+        // the four lane groups of a column (lanes frow + 16 q) meet by cross-lane adds, the WM
+        // waves of a column in LDS
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          s1[jj] += __shfl_xor(s1[jj], 16, 64);
+          s1[jj] += __shfl_xor(s1[jj], 32, 64);
+          s2[jj] += __shfl_xor(s2[jj], 16, 64);
+          s2[jj] += __shfl_xor(s2[jj], 32, 64);
+        }
+        if (fq == 0) {
+          const int col = wn * 64 + 4 * frow;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            red[(wm * 2 + 0) * BN + col + jj] = s1[jj];
+            red[(wm * 2 + 1) * BN + col + jj] = s2[jj];
+          }
+        }
+      }
+    } else {
     // element offset of row m from cbase (within the C descriptor: < 2^30), -1: no row
     int rowoff[Cf::FM];
 #pragma unroll
@@ -1378,7 +1490,6 @@ gemm_pp2_kernel(const GemmArgs g) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) h[r] = f2bf(bf2f(h[r]) + ((bits >> r) & 1u ? sf[r] : 0.f));
         }
-        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
         const u32x2_t w = {(uint32_t)h[0] | ((uint32_t)h[1] << 16),
                            (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
         const int so = ok ? eoff * 2 : (int)kGOOB;
@@ -1404,6 +1515,7 @@ gemm_pp2_kernel(const GemmArgs g) {
         }
       }
     }
+    }   // swapped layout
     if (do_stats) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       raw_barrier();
@@ -1688,11 +1800,12 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
   // ResNet 1x1 convs, profiles/measurements/r2_gemm_vs_conv_resnet1x1_b1280.jsonl)
   const int variant = g_gemm_variant >= 0 ? g_gemm_variant
                     : (N <= 128 ? 1
-                       : (g_gemm_pp2 & 1) && dtf_gemm_pp2_ok(M, N, K, lda, ldb) ? 15
+                       : (g_gemm_pp2 & 1) && dtf_gemm_pp2_ok(M, N, K, lda, ldb) &&
+                                 !(stats && bias) ? 15
                        : ((g_gemm_pp & 1) && (K + 63) / 64 >= 2 ? 11 : 8));
   if (variant == 11 && (K + 63) / 64 < 2)
     throw std::runtime_error("gemm_nt: the persistent kernel needs K > 64");
-  if (variant == 15 && !dtf_gemm_pp2_ok(M, N, K, lda, ldb))
+  if (variant == 15 && (!dtf_gemm_pp2_ok(M, N, K, lda, ldb) || (stats && bias)))
     throw std::runtime_error("gemm_nt: shape not supported by the persistent kernel (variant 15)");
   switch (variant) {
     case 11: launch_gemm_pp<0>(g, st); break;

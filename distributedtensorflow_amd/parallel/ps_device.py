@@ -316,7 +316,15 @@ class OwnerShard:
             self._sync_device()
             return torch.cat([p.detach().reshape(-1) for p in self.params]).cpu()
 
+    def _join_workers(self):
+        """Order the shard stream after every worker stream's applies (async mode)."""
+        if self.stream is not None:
+            for s in self.streams:
+                if s is not self.stream:
+                    self.stream.wait_stream(s)
+
     def set_values(self, vals, global_step):
+        self._join_workers()
         with self.lock, self._on(self.stream), torch.no_grad():
             for p, v in zip(self.params, _split(vals, self.shapes)):
                 p.copy_(v.to(p.device))
@@ -328,6 +336,7 @@ class OwnerShard:
         """Restore one optimizer slot (e.g. ``Adam``) from an unpadded flat of the shard's
         variables (checkpoint restore after a PS restart)."""
         slot = next(s for s in self.opt.slots if s.name == name)
+        self._join_workers()
         with self.lock, self._on(self.stream), torch.no_grad():
             for p, v in zip(self.params, _split(flat, self.shapes)):
                 self.space.view_of(slot.buf, p).copy_(v.to(slot.buf.device))
@@ -432,7 +441,12 @@ class OwnerShard:
             if stream is not None:
                 ev = torch.cuda.Event()
                 ev.record(stream)
-                self.stream.wait_stream(stream)     # later accumulator / state writes
+                if self.sync or self.use_locking:
+                    self.stream.wait_stream(stream)  # later accumulator / state writes
+                # Hogwild (async, use_locking=False): the next worker's apply must NOT queue
+                # behind this one through the shard stream -- applies of different workers run
+                # concurrently on their own streams (TF's unlocked ApplyMomentum); shard-stream
+                # work (restore, reads) joins every worker stream first (_join_workers)
         self.stats["applied"] += 1
         self._inflight += 1
         self.stats["max_inflight"] = max(self.stats["max_inflight"], self._inflight)

@@ -113,3 +113,33 @@ def test_pp2_refuses_unsupported_shapes():
     b = torch.zeros(256, 200, device="cuda").bfloat16()
     with pytest.raises(RuntimeError, match="variant 15"):
         _run(15, lambda: n.gemm_nt(a, b))
+
+
+@pytest.mark.parametrize("n,hw,c,k,stride", [(8, 14, 256, 256, 1), (4, 28, 128, 256, 1),
+                                             (8, 14, 256, 512, 2)])
+def test_pp2_conv_matches_pingpong_bitwise(n, hw, c, k, stride):
+    """The implicit-GEMM conv on the persistent kernel (gemm_set_pp2 bit 1): forward output (the
+    interleaved register-direct epilogue), with BN statistics (the swapped-operand epilogue) and
+    the data gradient (stride 2: strided phase outputs) all equal to the ping-pong kernel's."""
+    n_ = _native()
+    g = torch.Generator(device="cuda").manual_seed(n * hw + c + k)
+    x = torch.randn(n, hw, hw, c, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(k, 3, 3, c, device="cuda", generator=g) / (9 * c) ** 0.5).bfloat16()
+    out = {}
+    for pp2 in (0, 2):
+        n_._K.gemm_set_pp2(pp2)
+        try:
+            y = n_.conv2d_forward(x, w, stride, 1)
+            P = y.shape[1]
+            st = torch.zeros(n * P * P // 64 + 1, 2, k, device="cuda")    # >= any slab count
+            ys = n_.conv2d_forward(x, w, stride, 1, stats=st)
+            dy = torch.randn(y.shape, device="cuda", generator=torch.Generator(
+                device="cuda").manual_seed(3)).bfloat16()
+            dx = n_.conv2d_dgrad(dy, w, x.shape, stride, 1)
+            torch.cuda.synchronize()
+            out[pp2] = (y, ys, st, dx)
+        finally:
+            n_._K.gemm_set_pp2(0)
+    (y0, ys0, st0, dx0), (y2, ys2, st2, dx2) = out[0], out[2]
+    assert torch.equal(y2, y0) and torch.equal(ys2, ys0) and torch.equal(dx2, dx0)
+    torch.testing.assert_close(st2.sum(0), st0.sum(0), rtol=1e-4, atol=1e-1)

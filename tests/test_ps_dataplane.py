@@ -328,3 +328,31 @@ def test_cross_host_cluster_uses_tcp_plane(plane_device):
     d = {"host": "some-other-host", "master": {}, "mail": {}}
     with pytest.raises(RuntimeError, match="cannot be"):
         ps_device.PSLink(d, {}, 0, "cpu", 0)
+
+
+def test_async_applies_of_different_workers_do_not_serialise(plane_device):
+    """a Hogwild apply must not queue behind another worker's apply.  Worker 0's
+    apply stream is held busy (a long device sleep queued on it first); worker 1's apply, launched
+    after it, completes while worker 0's is still pending -- no shard-stream edge orders them."""
+    if plane_device != "cuda":
+        pytest.skip("device streams")
+    space, _ = _space()
+    plan = ps_device.shard_plan(space, 1)[0]
+    sh = _owner(space, plan, opt={"type": "sgd", "learning_rate": 0.5, "weight_decay": 0.0})
+    try:
+        with torch.cuda.stream(sh.streams[0]):
+            torch.cuda._sleep(400_000_000)            # ~0.2 s of GPU cycles on worker 0's stream
+        with sh.lock:
+            sh._launch_apply(sh._slot(0), 1.0, 0, [], None)
+            sh._launch_apply(sh._slot(1), 1.0, 1, [], None)
+        t0 = time.time()
+        while not sh.streams[1].query() and time.time() - t0 < 5:
+            time.sleep(0.001)
+        assert sh.streams[1].query(), "worker 1's apply waited"
+        assert not sh.streams[0].query(), "worker 0's apply was expected to still run"
+        assert sh.stats["max_inflight"] >= 2
+        torch.cuda.synchronize()
+    finally:
+        err = sh._error
+        sh.stop()
+        assert err is None, repr(err)
