@@ -1140,18 +1140,15 @@ gemm_pp2_kernel(const GemmArgs g) {
     return r0 + lrow;
   };
   const int pch = gswz<BK>(prow(0, 0), slot) * 8;   // the same for every piece of this wave
-  // ILV (the non-strided instantiations without BN statistics): the MFMA operands in their natural order and the B
-  // rows INTERLEAVED over the wave's four 16-column fragments -- fragment jj's row f holds output
-  // column 4 f + jj of the wave's 64-column strip -- so lane (frow, fq) ends up holding
-  // C[4 fq + r][4 frow .. 4 frow + 3] of each 16-row fragment: one 8-B store per (fragment row,
-  // register) and 16 lanes cover 128 contiguous bytes of a row, i.e. every store instruction
-  // writes four WHOLE 128-B lines (the swapped layout wrote 16 rows x 32 B per instruction and
-  // completed a line only over four instructions 8 apart).  The K order per output is unchanged:
-  // bit-identical to the swapped layout.  B rows use the swizzle chunk ^ ((row >> 3) & 7), so the
-  // fragment reads (rows 4 f + jj, f = 0..15) hit the same bank pattern as consecutive rows with
-  // the A swizzle.
-  constexpr bool ILV = !strided && !(EPI & 1);   // (with BN statistics: VGPR spills)
-  auto bswz = [&](int row, int ch) { return ILV ? ch ^ ((row >> 3) & 7) : gswz<BK>(row, ch); };
+  // ILV (the non-strided instantiations without BN statistics): the MFMA operands in their
+  // natural order and the B rows INTERLEAVED over the wave's four 16-column fragments --
+  // fragment jj's row f holds output column 4 f + jj of the wave's 64-column strip -- so lane
+  // (frow, fq) ends up holding C[4 fq + r][4 frow .. 4 frow + 3] of each 16-row fragment: one
+  // 8-B store per (fragment row, register) and 16 lanes cover 128 contiguous bytes of a row, i.e.
+  // every store instruction writes four WHOLE 128-B lines (the swapped layout wrote 16 rows x
+  // 32 B per instruction and completed a line only over four instructions 8 apart).  The K order
+  // per output is unchanged: bit-identical to the swapped layout.
+  constexpr bool ILV = !strided && !(CONV && (EPI & 1));   // (conv + BN statistics: VGPR spills)
   auto plds = [&](int pc, int j) {
     const bool isA = pc == 0 || pc == 3;
     return (uint32_t)((isA ? 0 : Cf::SA) + (prow(pc, j) - lrow) * BK) * 2u;
@@ -1191,9 +1188,16 @@ gemm_pp2_kernel(const GemmArgs g) {
             o[pc][j] = ok ? (uint32_t)(m * g.lda + pch) * 2u : 0x80000000u;
           }
         } else {
-          const int n = n0 + row;
+          // ILV: LDS row (half 32 + j 16 + f) of a wave's 64-row strip holds output column
+          // 4 f + 2 half + j of the strip, so fragment (half, j) of the ping-pong reads covers
+          // columns 4 f + jj -- the interleave lives in the DMA source rows; the LDS layout, the
+          // swizzle and the pieces' row ranges (each phase's RAW waits) are the swapped kernel's
+          const int rho = row & 63;
+          const int nl = ILV ? (row & ~63) + 4 * (rho & 15) + 2 * (rho >> 5) + ((rho >> 4) & 1)
+                             : row;
+          const int n = n0 + nl;
           const bool ok = valid && n < g.N;
-          o[pc][j] = ok ? (uint32_t)(n * g.ldb + bswz(row, slot) * 8) * 2u : 0x80000000u;
+          o[pc][j] = ok ? (uint32_t)(n * g.ldb + pch) * 2u : 0x80000000u;
         }
       }
   };
@@ -1258,17 +1262,8 @@ gemm_pp2_kernel(const GemmArgs g) {
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int ch = ks * 4 + fq;
-        if constexpr (ILV) {
-          // rows 4 frow + jj, jj < 4: one swizzle value ((4 frow + jj) >> 3 == frow >> 1), so
-          // the four fragments' addresses differ by immediate offsets only
-          const int r = wn * 64 + 4 * frow + half * 2 + j;
-          fb[ks * 2 + j] = *reinterpret_cast<const bf16x8_t*>(
-              sb + r * BK + ((ch ^ ((frow >> 1) & 7)) << 3));
-        } else {
-          const int r = wn * 64 + half * 32 + j * 16 + frow;
-          fb[ks * 2 + j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
-        }
+        const int r = wn * 64 + half * 32 + j * 16 + frow, ch = ks * 4 + fq;
+        fb[ks * 2 + j] = *reinterpret_cast<const bf16x8_t*>(sb + r * BK + gswz<BK>(r, ch) * 8);
       }
   };
   auto sync = [&]() {
@@ -1296,6 +1291,17 @@ gemm_pp2_kernel(const GemmArgs g) {
   };
 
   float* red = reinterpret_cast<float*>(lds + 2 * Cf::STAGE);   // [WM][2][BN] past the ring
+  // EPI 8: bias + GELU forward (C = z, gelu_out = gelu(z): two stores per row); EPI 16: GELU
+  // backward (C = acc * gelu'(a + b) with the per-tile column sums into colsum)
+  constexpr bool gelu_fwd = (EPI & 8) != 0, gelu_bwd = (EPI & 16) != 0;
+  static_assert(!((gelu_fwd || gelu_bwd) && (EPI & 7)), "GELU epilogues are plain dense ones");
+  // the first phases of a tile wait for pieces issued BEFORE the previous tile's stores: allow
+  // those stores (32 per lane, 64 with the GELU output) plus the 8 younger pieces to fly
+  // (vmcnt saturates at 63: with 64 stores the wait also drains 9 of them)
+  auto wait_after_stores = [&]() {
+    if constexpr (gelu_fwd) DTF_WAIT_VM(63);
+    else DTF_WAIT_VM(40);
+  };
   // EPI 0 (BERT's dense layers): C (+ bias) (+ ReLU) only -- the statistics / accumulate
   // operands and their SGPRs are compiled out
   constexpr bool do_stats = (EPI & 1) != 0;
@@ -1314,11 +1320,11 @@ gemm_pp2_kernel(const GemmArgs g) {
       __builtin_amdgcn_sched_barrier(0);
       rdA(cur_lds, 0);
       issue_piece(kt + 1, 2);
-      if (!first && kt == 0) DTF_WAIT_VM(40); else DTF_WAIT_VM(8);
+      if (!first && kt == 0) wait_after_stores(); else DTF_WAIT_VM(8);
       mfma_phase(fBl, 0, 0);
       rdB(fBr, cur_lds, 1);
       issue_piece(kt + 1, 3);
-      if (!first && kt == 0) DTF_WAIT_VM(40); else DTF_WAIT_VM(8);
+      if (!first && kt == 0) wait_after_stores(); else DTF_WAIT_VM(8);
       mfma_phase(fBr, 0, 1);
       rdA(cur_lds, 1);
       issue_piece(kt + 2, 0);
@@ -1357,6 +1363,14 @@ gemm_pp2_kernel(const GemmArgs g) {
         b4[0] = bv.x; b4[1] = bv.y; b4[2] = bv.z; b4[3] = bv.w;
       }
       float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+      float gb4[4] = {0.f, 0.f, 0.f, 0.f};          // GELU backward: the GELU's bias
+      if (gelu_bwd && g.gelu_b && col_ok) {
+        const float4 bv = *reinterpret_cast<const float4*>(g.gelu_b + ncol);
+        gb4[0] = bv.x; gb4[1] = bv.y; gb4[2] = bv.z; gb4[3] = bv.w;
+      }
+      const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+          gelu_fwd ? (void*)(g.gelu_out + cbase) : gelu_bwd ? (void*)(g.gelu_a + cbase) : (void*)g.C,
+          0, (gelu_fwd || gelu_bwd) ? (int)cbytes : 0, 0x00020000);
       // byte offset of this lane's element run, advanced one row at a time by an opaque VALU add
       // (as closed forms the compiler hoists 32 row offsets / row tests into SGPRs and spills).
       // Rows past M lie past the descriptor's end; a column past N starts at 2^31 (beyond any
@@ -1405,14 +1419,65 @@ gemm_pp2_kernel(const GemmArgs g) {
             for (int jj = 0; jj < 4; ++jj)
               h[jj] = f2bf(bf2f(h[jj]) + ((bits >> jj) & 1u ? sf[jj] : 0.f));
           }
+          if constexpr (gelu_bwd) {
+            // d = bf16(acc) * gelu'(a + b) (the LDS-staged kernel's arithmetic: bit-identical);
+            // its fp32 value feeds the column sums (rows past M: acc and a are zero-filled ... d
+            // = 0 * gelu'(b): exact zero)
+            typedef uint32_t u32x2l_t __attribute__((ext_vector_type(2)));
+            const u32x2l_t av = __builtin_bit_cast(
+                u32x2l_t, __builtin_amdgcn_raw_buffer_load_b64(rg, vo, 0, 0));
+            const float af[4] = {__builtin_bit_cast(float, av.x << 16),
+                                 __builtin_bit_cast(float, av.x & 0xffff0000u),
+                                 __builtin_bit_cast(float, av.y << 16),
+                                 __builtin_bit_cast(float, av.y & 0xffff0000u)};
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const float d = bf2f(h[jj]) * gelu_grad(af[jj] + gb4[jj]);
+              s1[jj] += d;
+              h[jj] = f2bf(d);
+              __builtin_amdgcn_sched_barrier(0);   // one GELU derivative at a time (VGPRs)
+            }
+          }
           const u32x2_t w = {(uint32_t)h[0] | ((uint32_t)h[1] << 16),
                              (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
           if (nt_store) __builtin_amdgcn_raw_buffer_store_b64(w, rc, vo, 0, 2);
           else __builtin_amdgcn_raw_buffer_store_b64(w, rc, vo, 0, 0);
+          if constexpr (gelu_fwd) {
+            bf16_t q[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) q[jj] = f2bf(gelu_f(bf2f(h[jj])));
+            const u32x2_t wq = {(uint32_t)q[0] | ((uint32_t)q[1] << 16),
+                                (uint32_t)q[2] | ((uint32_t)q[3] << 16)};
+            if (nt_store) __builtin_amdgcn_raw_buffer_store_b64(wq, rg, vo, 0, 2);
+            else __builtin_amdgcn_raw_buffer_store_b64(wq, rg, vo, 0, 0);
+          }
           asm volatile("v_add_u32 %0, %0, %1" : "+v"(vo) : "s"(ldc2));
           __builtin_amdgcn_sched_barrier(0);     // one row at a time (register pressure)
         }
         asm volatile("v_add_u32 %0, %0, %1" : "+v"(vo) : "s"(12 * ldc2));
+      }
+      if constexpr (gelu_bwd) {
+        // per-tile column sums of d: lane groups by cross-lane adds, the two wave rows in LDS,
+        // then one fp32 row of colsum per M tile
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          s1[jj] += __shfl_xor(s1[jj], 16, 64);
+          s1[jj] += __shfl_xor(s1[jj], 32, 64);
+        }
+        if (fq == 0) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) red[wm * BN + wn * 64 + 4 * frow + jj] = s1[jj];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
+        if (tid < BN && cn0 + tid < g.N) {
+          float t = 0.f;
+#pragma unroll
+          for (int k = 0; k < Cf::WM; ++k) t += red[k * BN + tid];
+          g.colsum[(long)(cm0 / BM) * g.N + cn0 + tid] = t;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
       }
       if (do_stats) {
         // the four lane groups of a column (lanes frow + 16 q) meet by cross-lane adds, the WM
@@ -1590,6 +1655,12 @@ template <int CONV>
 void launch_gemm_pp2(const GemmArgs& g, long a_bytes, long b_bytes, hipStream_t st) {
   const bool stats = g.stats != nullptr, acc = g.Cin || g.acc_mask;
   const bool strided = CONV && (g.osh != 1 || g.osw != 1);
+  if constexpr (!CONV) {
+    if (g.gelu_out) { launch_gemm_pp2_t<0, 8>(g, a_bytes, b_bytes, st); return; }
+    // (the GELU-backward epilogue, EPI 16, compiles with ~64 VGPR spills here: it stays on the
+    // LDS-staged ping-pong kernel)
+    if (g.gelu_a) throw std::runtime_error("gemm_pp2: GELU-backward epilogue not supported");
+  }
   if (strided) {
     if (acc) launch_gemm_pp2_t<CONV, 6>(g, a_bytes, b_bytes, st);
     else launch_gemm_pp2_t<CONV, 4>(g, a_bytes, b_bytes, st);
@@ -1723,6 +1794,8 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
 // dX = dY . W (gemm_nt form, B = W^T rows) for a data gradient that feeds a GELU: the epilogue
 // applies gelu'(a + b) and leaves the per-tile column sums of the result (the GELU bias's
 // gradient, first level) in colsum [dtf_gemm_tile_rows(M)][N]; C and a dense [M][N].
+bool dtf_gemm_pp2_ok(int M, int N, int K, int lda, int ldb);
+
 void dtf_gemm_nt_gelu_bwd(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K,
                           int lda, int ldb, const bf16_t* gelu_a, const float* gelu_b,
                           float* colsum, hipStream_t st) {
@@ -1753,6 +1826,8 @@ void dtf_gemm_nt_bias_gelu(const bf16_t* A, const bf16_t* B, bf16_t* Z, bf16_t* 
   g.bias = bias; g.gelu_out = H;
   g.nt = g_gemm_nt;
   if (N <= 128) launch_gemm<256, 128, 64, 3>(g, st);
+  else if ((g_gemm_pp2 & 1) && dtf_gemm_pp2_ok(M, N, K, lda, ldb) && N % 4 == 0)
+    launch_gemm_pp2<0>(g, (long)(M - 1) * lda * 2 + 2L * K, (long)(N - 1) * ldb * 2 + 2L * K, st);
   else launch_gemm<256, 256, 64, 2, 2>(g, st);
 }
 

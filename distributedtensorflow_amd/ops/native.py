@@ -1692,7 +1692,9 @@ def bias_gelu_dense(a, b1, w):
 # BERT's FFN first GEMM on our MFMA GEMM with the bias + GELU epilogue (A/B knob, off by default:
 # in the BERT-base b512 step it takes 441 us per layer against 268 us for hipBLASLt + 139 us for the
 # bias_gelu_fwd pass, profiles/measurements/r4_bert_ffn1_fused_epilogue.jsonl)
-_FFN_GEMM_GELU = os.environ.get("DTF_FFN_GEMM_GELU", "0") == "1"
+# (on with DTF_DENSE_GEMM=native: the persistent kernel's interleaved epilogue writes z and h)
+_FFN_GEMM_GELU = os.environ.get("DTF_FFN_GEMM_GELU",
+                                "1" if _DENSE_GEMM == "native" else "0") == "1"
 
 
 def dense_gelu_dense(x, w1, b1, w2):

@@ -143,3 +143,29 @@ def test_pp2_conv_matches_pingpong_bitwise(n, hw, c, k, stride):
     (y0, ys0, st0, dx0), (y2, ys2, st2, dx2) = out[0], out[2]
     assert torch.equal(y2, y0) and torch.equal(ys2, ys0) and torch.equal(dx2, dx0)
     torch.testing.assert_close(st2.sum(0), st0.sum(0), rtol=1e-4, atol=1e-1)
+
+
+@pytest.mark.parametrize("M,N,K", [(65536 // 8, 3072, 768), (1000, 520, 256)])
+def test_pp2_bias_gelu_epilogue_matches_pingpong(M, N, K):
+    """BERT's FFN1 (z = x W^T + b, h = gelu(z)) on the persistent kernel's interleaved epilogue
+    (two stores per row): z and h bit-identical to the LDS-staged ping-pong kernel."""
+    n = _native()
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    out = {}
+    for pp2 in (0, 1):
+        n._K.gemm_set_pp2(pp2)
+        try:
+            z = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            h = torch.empty_like(z)
+            n._K.gemm_nt_bias_gelu(a.data_ptr(), b.data_ptr(), z.data_ptr(), h.data_ptr(), M, N,
+                                   K, K, K, bias.data_ptr(), n._st())
+            torch.cuda.synchronize()
+            out[pp2] = (z, h)
+        finally:
+            n._K.gemm_set_pp2(0)
+    assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
+    zf = (a.float() @ b.float().t() + bias)
+    assert ((out[1][0].float() - zf).norm() / zf.norm()).item() < 5e-3
