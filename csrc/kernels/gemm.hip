@@ -1435,7 +1435,6 @@ gemm_pp2_kernel(const GemmArgs g) {
               const float d = bf2f(h[jj]) * gelu_grad(af[jj] + gb4[jj]);
               s1[jj] += d;
               h[jj] = f2bf(d);
-              __builtin_amdgcn_sched_barrier(0);   // one GELU derivative at a time (VGPRs)
             }
           }
           const u32x2_t w = {(uint32_t)h[0] | ((uint32_t)h[1] << 16),
@@ -1657,9 +1656,7 @@ void launch_gemm_pp2(const GemmArgs& g, long a_bytes, long b_bytes, hipStream_t 
   const bool strided = CONV && (g.osh != 1 || g.osw != 1);
   if constexpr (!CONV) {
     if (g.gelu_out) { launch_gemm_pp2_t<0, 8>(g, a_bytes, b_bytes, st); return; }
-    // (the GELU-backward epilogue, EPI 16, compiles with ~64 VGPR spills here: it stays on the
-    // LDS-staged ping-pong kernel)
-    if (g.gelu_a) throw std::runtime_error("gemm_pp2: GELU-backward epilogue not supported");
+    if (g.gelu_a) { launch_gemm_pp2_t<0, 16>(g, a_bytes, b_bytes, st); return; }
   }
   if (strided) {
     if (acc) launch_gemm_pp2_t<CONV, 6>(g, a_bytes, b_bytes, st);
@@ -1702,11 +1699,16 @@ void launch_gemm_pp(const GemmArgs& g, hipStream_t st) {
 }
 
 int g_gemm_pp = 0;         // bit 0: persistent register-epilogue kernel for gemm_nt, bit 1: convs
-int g_gemm_pp2 = 0;        // round-5 persistent kernel (gemm_pp2): bit 0 gemm_nt, bit 1 convs
+// round-5 persistent kernel (gemm_pp2): bit 0 gemm_nt (default: 0.92-1.05x hipBLASLt on the BERT
+// shapes, profiles/measurements/r5_gemm_pp2_interleaved_epilogue_vs_v8.jsonl; ResNet-50 +0.6 %),
+// bit 1 the implicit-GEMM convs (measured neutral: off)
+int g_gemm_pp2 = 1;
 int g_gemm_stream = 1;     // output-heavy shapes on the row-streaming kernel (gemm_stream.hip)
 
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
-int g_gemm_nt = 0;         // non-temporal C stores (ResNet-50 A/B: neutral; off keeps BERT outputs cached)
+// non-temporal C stores: on since the persistent kernel's full-line stores (BERT-base b512 +1.1 %,
+// profiles/measurements/r5_bert_gemm_nt_stores.jsonl); ResNet-50 A/B neutral in round 2
+int g_gemm_nt = 1;
 int g_gemm_dbg = 0;        // GemmArgs::dbg for timing probes
 
 int g_gemm_stagger_mode = 1, g_gemm_stagger = -1;   // OCC 2 start stagger (-1: auto)
@@ -1809,6 +1811,8 @@ void dtf_gemm_nt_gelu_bwd(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, in
   g.gelu_a = gelu_a; g.gelu_b = gelu_b; g.colsum = colsum;
   g.nt = g_gemm_nt;
   if (N <= 128) launch_gemm<256, 128, 64, 3>(g, st);
+  else if ((g_gemm_pp2 & 1) && dtf_gemm_pp2_ok(M, N, K, lda, ldb) && N % 4 == 0)
+    launch_gemm_pp2<0>(g, (long)(M - 1) * lda * 2 + 2L * K, (long)(N - 1) * ldb * 2 + 2L * K, st);
   else launch_gemm<256, 256, 64, 2, 2>(g, st);
 }
 

@@ -65,10 +65,8 @@ if os.environ.get("DTF_BN_GRID_CAP"):     # BN row-sweep grid cap override (2048
     _K.bn_set_grid_cap(int(os.environ["DTF_BN_GRID_CAP"]))
 if os.environ.get("DTF_BN_STATS_BLOCKS"):  # BN reduce-pass block target (1024 = round-2)
     _K.bn_set_stats_blocks(int(os.environ["DTF_BN_STATS_BLOCKS"]))
-if os.environ.get("DTF_GEMM_PP2"):      # round-5 persistent GEMM: bit 0 gemm_nt, bit 1 convs
+if os.environ.get("DTF_GEMM_PP2"):      # round-5 persistent GEMM: bit 0 gemm_nt (default), 1 convs
     _K.gemm_set_pp2(int(os.environ["DTF_GEMM_PP2"]))
-elif os.environ.get("DTF_DENSE_GEMM") == "native":
-    _K.gemm_set_pp2(1)                  # the dense layers' GEMMs go to the persistent kernel
 if os.environ.get("DTF_STORE_NT"):      # non-temporal output stores: bit 0 conv, 1 GEMM, 2 BN
     _nt = int(os.environ["DTF_STORE_NT"])
     _K.conv_set_nt(_nt & 1)
@@ -1505,8 +1503,10 @@ def _dense_weight_grad(w_param, x2, dy2):
 
 # BERT's plain dense GEMMs (forward y = x W^T + b and the data gradient dx = dy W, beta = 1 onto a
 # pending residual gradient) on our persistent MFMA GEMM (gemm.hip gemm_pp2, variant 15) instead of
-# hipBLASLt: "native" / "library" (A/B knob; see _dense_gemm_native)
-_DENSE_GEMM = os.environ.get("DTF_DENSE_GEMM", "library")
+# hipBLASLt: "native" (default since its interleaved full-line epilogue: 0.92-1.05x the library
+# per GEMM, the BERT step within 0.3 %, profiles/measurements/r5_bert_dense_native_vs_library.jsonl)
+# / "library" (A/B knob; see _dense_gemm_native)
+_DENSE_GEMM = os.environ.get("DTF_DENSE_GEMM", "native")
 
 
 def _dense_gemm_native(M, N, K):

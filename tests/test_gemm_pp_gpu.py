@@ -169,3 +169,33 @@ def test_pp2_bias_gelu_epilogue_matches_pingpong(M, N, K):
     assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
     zf = (a.float() @ b.float().t() + bias)
     assert ((out[1][0].float() - zf).norm() / zf.norm()).item() < 5e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(65536 // 8, 768, 3072), (1000, 520, 256)])
+def test_pp2_gelu_backward_epilogue_matches_pingpong(M, N, K):
+    """BERT's FFN1 data gradient d(a) = (do W2) * gelu'(a + b) with the per-tile column sums on
+    the persistent kernel: d(a) bit-identical to the LDS-staged kernel, colsum to fp32 rounding
+    (summation order) and against an fp32 reference."""
+    n = _native()
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    do = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    wt = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    a = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    tiles = n._K.gemm_tile_rows(M)
+    out = {}
+    for pp2 in (0, 1):
+        n._K.gemm_set_pp2(pp2)
+        try:
+            da = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            cs = torch.empty(tiles, N, device="cuda")
+            n._K.gemm_nt_gelu_bwd(do.data_ptr(), wt.data_ptr(), da.data_ptr(), M, N, K, K, K,
+                                  a.data_ptr(), b.data_ptr(), cs.data_ptr(), n._st())
+            torch.cuda.synchronize()
+            out[pp2] = (da, cs)
+        finally:
+            n._K.gemm_set_pp2(0)
+    assert torch.equal(out[1][0], out[0][0])
+    torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-4, atol=1e-2)
+    col = out[1][0].float().sum(0)
+    torch.testing.assert_close(out[1][1].sum(0), col, rtol=2e-2, atol=1.0)

@@ -11,6 +11,7 @@
 #   prof:<name>:<bench args>   rocprofv3 kernel trace + stats -> gpurun_out/prof_<name>/summary.txt
 #   py:<script> [args]         any tools/ python probe
 #   sh:<command>               a shell command line (env-var A/B arms: "sh:DTF_X=1 python bench.py")
+#   env:<K=V>                  export K=V for every later step of this call (e.g. before a prof:)
 # Each step runs under its own time limit (STEP_TIMEOUT, default 600 s), logs to
 # gpurun_out/<TAG>/<n>_<kind>.log, and the run stops at the first failing step (no retries):
 # after a fault, abort, segfault or time limit nothing more touches the GPU in this call.
@@ -51,6 +52,7 @@ for step in "$@"; do
       (exit $rc) ;;
     py) timeout -k 10 "$T" python -u $arg > "$log" 2>&1 ;;
     sh) timeout -k 10 "$T" bash -c "$arg" > "$log" 2>&1 ;;
+    env) export "$arg"; echo "$arg" > "$log" ;;
     *) echo "unknown step kind: $kind" >&2; exit 2 ;;
   esac
   rc=$?
