@@ -1148,7 +1148,7 @@ gemm_pp2_kernel(const GemmArgs g) {
   // every store instruction writes four WHOLE 128-B lines (the swapped layout wrote 16 rows x
   // 32 B per instruction and completed a line only over four instructions 8 apart).  The K order
   // per output is unchanged: bit-identical to the swapped layout.
-  constexpr bool ILV = !strided && !(CONV && (EPI & 1));   // (conv + BN statistics: VGPR spills)
+  constexpr bool ILV = !strided;
   auto plds = [&](int pc, int j) {
     const bool isA = pc == 0 || pc == 3;
     return (uint32_t)((isA ? 0 : Cf::SA) + (prow(pc, j) - lrow) * BK) * 2u;
@@ -1358,7 +1358,8 @@ gemm_pp2_kernel(const GemmArgs g) {
       const int ncol = cn0 + wn * 64 + 4 * frow;
       const bool col_ok = ncol < g.N;
       float b4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (g.bias && col_ok) {
+      // with BN statistics the host passes no bias and no ReLU (gemm_nt / gemm_conv): compiled out
+      if (!do_stats && g.bias && col_ok) {
         const float4 bv = *reinterpret_cast<const float4*>(g.bias + ncol);
         b4[0] = bv.x; b4[1] = bv.y; b4[2] = bv.z; b4[3] = bv.w;
       }
@@ -1392,7 +1393,7 @@ gemm_pp2_kernel(const GemmArgs g) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
             float v = acc[i][jj][r] + b4[jj];
-            if (g.relu) v = fmaxf(v, 0.f);
+            if (!do_stats && g.relu) v = fmaxf(v, 0.f);
             h[jj] = f2bf(v);
             // rows past M / columns past N hold exact zeros (zero-filled operands, no bias with
             // statistics: host), so they add nothing -- no per-row test (its 32 compare masks
@@ -1880,11 +1881,11 @@ void dtf_gemm_nt(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int 
   const int variant = g_gemm_variant >= 0 ? g_gemm_variant
                     : (N <= 128 ? 1
                        : (g_gemm_pp2 & 1) && dtf_gemm_pp2_ok(M, N, K, lda, ldb) &&
-                                 !(stats && bias) ? 15
+                                 !(stats && (bias || relu)) ? 15
                        : ((g_gemm_pp & 1) && (K + 63) / 64 >= 2 ? 11 : 8));
   if (variant == 11 && (K + 63) / 64 < 2)
     throw std::runtime_error("gemm_nt: the persistent kernel needs K > 64");
-  if (variant == 15 && (!dtf_gemm_pp2_ok(M, N, K, lda, ldb) || (stats && bias)))
+  if (variant == 15 && (!dtf_gemm_pp2_ok(M, N, K, lda, ldb) || (stats && (bias || relu))))
     throw std::runtime_error("gemm_nt: shape not supported by the persistent kernel (variant 15)");
   switch (variant) {
     case 11: launch_gemm_pp<0>(g, st); break;

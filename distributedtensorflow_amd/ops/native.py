@@ -39,6 +39,8 @@ _DENSE_WGRAD_NATIVE_MAX = int(os.environ.get("DTF_DENSE_WGRAD_NATIVE_MAX", str(3
 # kernel-variant switches for A/B runs on one box (defaults = the measured best)
 if os.environ.get("DTF_WGRAD_MODE"):
     _K.wgrad_set_dma_mode(int(os.environ["DTF_WGRAD_MODE"]))
+if os.environ.get("DTF_WGRAD_PP"):       # ping-pong wgrad: 0 off, n: split-K target of n rounds
+    _K.wgrad_set_pp(int(os.environ["DTF_WGRAD_PP"]))
 if os.environ.get("DTF_WGRAD_PIPE"):
     _K.wgrad_set_pipe(int(os.environ["DTF_WGRAD_PIPE"]))
 if os.environ.get("DTF_CONV_DMA"):
