@@ -122,6 +122,7 @@ void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, con
 int dtf_conv_wgrad_splits(long, int, int, long, int);
 int dtf_conv_wgrad_halo_splits(int, int, int, int, int, int, int, int, int, const TapTableW&);
 void dtf_wgrad_set_halo(int);
+void dtf_conv_set_halo_stages(int);
 void dtf_wgrad_set_dma_mode(int);
 void dtf_wgrad_set_pipe(int);
 void dtf_wgrad_set_pp(int);
@@ -723,6 +724,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("wgrad_set_dma_mode", &dtf_wgrad_set_dma_mode);
   m.def("wgrad_set_pipe", &dtf_wgrad_set_pipe);
   m.def("wgrad_set_pp", &dtf_wgrad_set_pp);
+  m.def("conv_set_halo_stages", &dtf_conv_set_halo_stages);
   m.def("conv_set_gemm", &dtf_conv_set_gemm);
   m.def("bn_set_nt", &dtf_bn_set_nt);
   m.def("bn_set_grid_cap", &dtf_bn_set_grid_cap);

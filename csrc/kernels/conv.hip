@@ -806,7 +806,9 @@ struct HaloCfg {
   static constexpr int WST = NT * 64;                    // filter elements per stage
   static constexpr int LDC = NT + 8;
   static constexpr size_t LDS = (size_t)(PIXAL * C + 2 * WST) * 2;
-  static constexpr size_t lds(int st) { return (size_t)(st * PIXAL * C + 2 * WST) * 2; }
+  static constexpr size_t lds(int st, int nstg = 2) {
+    return (size_t)(st * PIXAL * C + nstg * WST) * 2;
+  }
   static constexpr size_t LDS_FREG = (size_t)PIXAL * C * 2;    // FREG: the patch only
   static_assert(M % (16 * WMW) == 0 && NT % (16 * WNW) == 0, "halo tiling");
   static_assert((size_t)M * LDC * 2 + (size_t)2 * NT * (kThreads / NT) * 4 <= (size_t)PIXAL * C * 2,
@@ -842,7 +844,10 @@ DTF_DEV int halo_swz(int u) { return C == 64 ? (((u >> 1) & 3) << 1) : ((u & 7) 
 // (sum dz, sum dz * xhat, dz = dy masked by the forward ReLU) per output channel, one slab row
 // per block (BnbAcc, the contract of conv_igemm_kernel's BNB epilogue).  The BN input x is loaded
 // for the thread's output rows before the tile is staged, so its latency hides under the staging.
-template <int C, int W, int WMW, int NT, int ST = 1, bool FREG = false, bool BNB = false>
+// NSTG: filter-slice ring depth (LDS stages; the slice of step s + NSTG - 1 is issued at step s,
+// so a slice has NSTG - 1 steps of MFMA work to arrive from L2; 2 = the original double buffer)
+template <int C, int W, int WMW, int NT, int ST = 1, bool FREG = false, bool BNB = false,
+          int NSTG = 2>
 __global__ void __launch_bounds__(kThreads * ST, ST == 1 ? 2 : 1)
 conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                     bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
@@ -853,7 +858,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   const int wall = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int sid = wall >> 2, wave = wall & 3;                    // strip, wave within the strip
   bf16_t* const patch = lds + sid * (H::PIXAL * C);              // [ST][PIXAL][C]
-  bf16_t* const wst = lds + ST * (H::PIXAL * C);                 // [2][NT][64]
+  bf16_t* const wst = lds + ST * (H::PIXAL * C);                 // [NSTG][NT][64]
   const int wm = wave / H::WNW, wn = wave % H::WNW;
   const int tiles_h = g.H / kHaloTH;
   const int tm = blockIdx.x * ST + sid;                          // (image, row-tile)
@@ -915,7 +920,14 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
       dma16(rw, lds_w + (uint32_t)(stage * H::WST) * 2u + (uint32_t)q * 1024u, off);
     }
   };
-  if constexpr (!FREG) issue_w(0, 0);
+  if constexpr (!FREG) {
+#pragma unroll
+    for (int s0 = 0; s0 < NSTG - 1; ++s0) issue_w(s0, s0);
+  }
+  // DMA instructions per wave per filter slice: the slices younger than the one a step reads
+  constexpr int kDPW = NT / (32 * ST);
+  constexpr int kYoung = (NSTG - 2) * kDPW;
+  static_assert(kYoung <= 4 || kYoung == 6 || kYoung == 8, "halo ring: add the wait count");
 
   // per-lane A rows: output pixel m = wm * (MF * 16) + 16 i + frow -> patch pixel of tap (0, 0)
   const int frow = lane & 15, fq = lane >> 4;
@@ -993,13 +1005,22 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   } else {
   const int nsteps = taps.n * H::KS;
   for (int step = 0; step < nsteps; ++step) {
-    DTF_WAIT_VM(0);            // patch (step 0) and this step's filter slice landed (own DMAs)...
-    __syncthreads();           // ... everyone's; everyone done reading the other filter stage
-    issue_w(step + 1, (step + 1) & 1);   // past the last step: out-of-range, no traffic
+    // patch (step 0) and this step's filter slice landed (own DMAs; the kYoung younger slice
+    // DMAs may fly) ...
+    if constexpr (kYoung == 0) DTF_WAIT_VM(0);
+    else if constexpr (kYoung == 1) DTF_WAIT_VM(1);
+    else if constexpr (kYoung == 2) DTF_WAIT_VM(2);
+    else if constexpr (kYoung == 3) DTF_WAIT_VM(3);
+    else if constexpr (kYoung == 4) DTF_WAIT_VM(4);
+    else if constexpr (kYoung == 6) DTF_WAIT_VM(6);
+    else DTF_WAIT_VM(8);
+    __syncthreads();           // ... everyone's; everyone done reading the slot restaged next
+    // past the last step: out-of-range, no traffic
+    issue_w(step + NSTG - 1, (step + NSTG - 1) % NSTG);
     const int t = step / H::KS, s = step - t * H::KS;
     const int dpix = taps.dh[t] * H::PW + taps.dw[t];            // wave-uniform
     const int dupix = taps.dh[t] * W + taps.dw[t];
-    const bf16_t* sw = wst + (step & 1) * H::WST;
+    const bf16_t* sw = wst + (step % NSTG) * H::WST;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + fq;                                // chunk within the 64-ch slice
@@ -1262,11 +1283,51 @@ void dtf_conv_set_halo_strips(int v) { g_halo_st = v; }
 // bit 1: 28 x 28 x 128); see conv3x3_halo_kernel FREG
 static int g_halo_freg = 0;
 void dtf_conv_set_halo_freg(int v) { g_halo_freg = v; }
+// filter-ring depth per halo family: nibble f - 1 of g_halo_stages (0 or 2: the double buffer;
+// 3 / 4: deeper rings; family 1 keeps two blocks per CU at 4, family 2 only with two strips)
+static int g_halo_stages = 0;
+void dtf_conv_set_halo_stages(int v) { g_halo_stages = v; }
+
+template <int C, int W, int WMW, int NT, int ST, bool BNB, int NSTG>
+static void launch_halo_ring(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
+                             const TapTable& taps, float* stats, const BnBwdEpi& bnb, int tiles,
+                             size_t lds, hipStream_t st) {
+  auto kern = conv3x3_halo_kernel<C, W, WMW, NT, ST, false, BNB, NSTG>;
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024));
+    attr = true;
+  }
+  if (lds > 160 * 1024) throw std::runtime_error("halo conv: filter ring exceeds LDS");
+  hipLaunchKernelGGL(kern, dim3((unsigned)((tiles + ST - 1) / ST), g.Kout / NT),
+                     dim3(kThreads * ST), lds, st, X, Wt, Y, g, taps, stats, bnb);
+}
+
 template <int C, int W, int WMW, int NT>
 static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
                         const TapTable& taps, float* stats, const BnBwdEpi& bnb, int tiles,
                         int strips, hipStream_t st) {
   using Hc = HaloCfg<C, W, WMW, NT>;
+  const int nstg = (g_halo_stages >> (C == 64 ? 0 : 4)) & 15;
+  const bool freg_on = (g_halo_freg & (C == 64 ? 1 : 2)) != 0;
+  if (!freg_on && (nstg == 3 || nstg == 4)) {
+    if (bnb.part) {
+      constexpr size_t scratch =
+          (size_t)Hc::M * Hc::LDC * 2 + (size_t)(kThreads / (NT / 8)) * 2 * NT * 4;
+      const size_t base = Hc::lds(1, nstg);
+      const size_t lds = base > scratch ? base : scratch;
+      if (nstg == 3) launch_halo_ring<C, W, WMW, NT, 1, true, 3>(X, Wt, Y, g, taps, stats, bnb, tiles, lds, st);
+      else launch_halo_ring<C, W, WMW, NT, 1, true, 4>(X, Wt, Y, g, taps, stats, bnb, tiles, lds, st);
+    } else if (strips == 2) {
+      if (nstg == 3) launch_halo_ring<C, W, WMW, NT, 2, false, 3>(X, Wt, Y, g, taps, stats, bnb, tiles, Hc::lds(2, 3), st);
+      else launch_halo_ring<C, W, WMW, NT, 2, false, 4>(X, Wt, Y, g, taps, stats, bnb, tiles, Hc::lds(2, 4), st);
+    } else {
+      if (nstg == 3) launch_halo_ring<C, W, WMW, NT, 1, false, 3>(X, Wt, Y, g, taps, stats, bnb, tiles, Hc::lds(1, 3), st);
+      else launch_halo_ring<C, W, WMW, NT, 1, false, 4>(X, Wt, Y, g, taps, stats, bnb, tiles, Hc::lds(1, 4), st);
+    }
+    return;
+  }
   if (bnb.part) {
     // one strip per block; the BN-backward reduction scratch [OROWS][2][NT] fp32 sits past the
     // staged tile (in the dead filter ring, or past the patch with FREG)

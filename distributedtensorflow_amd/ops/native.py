@@ -53,6 +53,8 @@ if os.environ.get("DTF_CONV_STEM_HALO"):
     _K.conv_set_stem_halo(int(os.environ["DTF_CONV_STEM_HALO"]))
 if os.environ.get("DTF_CONV_HALO_STRIPS"):     # bit f: two strips per block for halo family f
     _K.conv_set_halo_strips(int(os.environ["DTF_CONV_HALO_STRIPS"]))
+if os.environ.get("DTF_CONV_HALO_STAGES"):     # nibble f-1: filter-ring depth of halo family f
+    _K.conv_set_halo_stages(int(os.environ["DTF_CONV_HALO_STAGES"], 0))
 if os.environ.get("DTF_CONV_HALO_FREG"):       # bit f: halo family f streams its filter via VGPRs
     _K.conv_set_halo_freg(int(os.environ["DTF_CONV_HALO_FREG"]))
 if os.environ.get("DTF_CONV_SMALL_K"):

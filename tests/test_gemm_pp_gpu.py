@@ -199,3 +199,34 @@ def test_pp2_gelu_backward_epilogue_matches_pingpong(M, N, K):
     torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-4, atol=1e-2)
     col = out[1][0].float().sum(0)
     torch.testing.assert_close(out[1][1].sum(0), col, rtol=2e-2, atol=1.0)
+
+
+@pytest.mark.parametrize("stages,strips", [(0x44, 0), (0x33, 0), (0x44, 3), (0x33, 3)])
+def test_halo_conv_filter_ring_depth_bit_identical(stages, strips):
+    """The 3x3 halo convs (stage-0/1 shapes) with a 3- or 4-deep filter-slice ring, with and
+    without two strips per block: forward (+ BN statistics) and data gradient bit-identical to
+    the double-buffered kernel (same MFMA order per output)."""
+    n_ = _native()
+    out = {}
+    for cfg in ((0, 0), (stages, strips)):
+        n_._K.conv_set_halo_stages(cfg[0])
+        n_._K.conv_set_halo_strips(cfg[1])
+        try:
+            res = []
+            for (hw, c) in ((56, 64), (28, 128)):
+                g = torch.Generator(device="cuda").manual_seed(hw + c)
+                x = torch.randn(3, hw, hw, c, device="cuda", generator=g).bfloat16()
+                w = (torch.randn(c, 3, 3, c, device="cuda", generator=g) / (9 * c) ** 0.5).bfloat16()
+                y = n_.conv2d_forward(x, w, 1, 1)
+                st = torch.zeros(3 * hw * hw // 16 + 1, 2, c, device="cuda")
+                ys = n_.conv2d_forward(x, w, 1, 1, stats=st)
+                dx = n_.conv2d_dgrad(y, w, x.shape, 1, 1)
+                torch.cuda.synchronize()
+                res += [y, ys, st, dx]
+            out[cfg] = res
+        finally:
+            n_._K.conv_set_halo_stages(0)
+            n_._K.conv_set_halo_strips(0)
+    a, b = out[(0, 0)], out[(stages, strips)]
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), i
