@@ -1384,7 +1384,10 @@ gemm_pp2_kernel(const GemmArgs g) {
           has_acc ? (int)cbytes : 0, 0x00020000);
       const __amdgpu_buffer_rsrc_t rmask = __builtin_amdgcn_make_buffer_rsrc(
           (has_acc && !g.Cin) ? const_cast<uint8_t*>(g.acc_mask + (cbase >> 3)) : (uint8_t*)g.C,
-          0, (has_acc && !g.Cin) ? (int)(cbytes / 16 + 1) : 0, 0x00020000);
+          // exactly the mask bytes of the valid region (cbytes / 2 elements, 8 per byte): a
+          // row past M must fall outside it (a +1 here let row M's first lanes read one byte past
+          // the mask allocation -- a device fault when that byte was unmapped)
+          0, (has_acc && !g.Cin) ? (int)(cbytes / 16) : 0, 0x00020000);
 #pragma unroll
       for (int i = 0; i < Cf::FM; ++i) {
 #pragma unroll

@@ -70,6 +70,8 @@ FUSE_PROJ_BN = os.environ.get("DTF_FUSE_PROJ_BN", "1") == "1"
 # bottleneck c2's BN + ReLU inside c3's GEMM (ops.batch_norm_relu_conv1x1; falls back to the two
 # ops off the streaming route)
 FUSE_BN_CONV = os.environ.get("DTF_FUSE_BN_CONV", "1") == "1"
+# projection blocks: c1's backward runs after the projection's (see Bottleneck.forward; A/B knob)
+C1_LAST_BWD = os.environ.get("DTF_C1_LAST_BWD", "1") == "1"
 
 
 class Bottleneck(nn.Module):
@@ -93,17 +95,25 @@ class Bottleneck(nn.Module):
         share = ops.GradShare(2) if self.has_proj else None
         if self.has_proj and FUSE_PROJ_BN:
             # the shortcut's BN is applied inside the block-output BN (one pass forward, one
-            # reduce + one apply pass backward for both)
+            # reduce + one apply pass backward for both).  c1 is built BEFORE the projection so
+            # that autograd runs its backward LAST of the two convs sharing x: the last one's data
+            # gradient completes d(x), and c1's streamed 1x1 dgrad can also form the backward sums
+            # of the BatchNorm that produced x (the stride-2 projection's cannot; it left a 1.2 ms
+            # reduce pass at stage 1)
             p, b = self.proj, self.proj.bn
-            sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
-                            bn_stats=b.training, grad_share=share)
+            if not C1_LAST_BWD:
+                sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
+                                bn_stats=b.training, grad_share=share)
             y = self._c2_c3(self.c1(x, grad_share=share))
+            if C1_LAST_BWD:
+                sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
+                                bn_stats=b.training, grad_share=share)
             c, b3 = self.c3, self.c3.bn
             return ops.batch_norm_add_batch_norm(
                 y, b3.gamma, b3.beta, b3.moving_mean, b3.moving_variance, sc, b.gamma, b.beta,
                 b.moving_mean, b.moving_variance, b3.training, b3.momentum, b3.epsilon)
-        sc = self.proj(x, relu=False, grad_share=share) if self.has_proj else x
         y = self._c2_c3(self.c1(x, grad_share=share))
+        sc = self.proj(x, relu=False, grad_share=share) if self.has_proj else x
         # identity shortcut: c1 (1x1, stride 1) also reads x, so its dgrad absorbs d(residual)
         return self.c3.bn(y, relu=True, residual=sc, residual_to_conv=not self.has_proj)
 

@@ -230,3 +230,23 @@ def test_halo_conv_filter_ring_depth_bit_identical(stages, strips):
     a, b = out[(0, 0)], out[(stages, strips)]
     for i, (u, v) in enumerate(zip(a, b)):
         assert torch.equal(u, v), i
+
+
+def test_pp2_masked_accumulate_mask_ends_at_the_allocation():
+    """The masked-residual epilogue must not read past the bit mask: M = 16 rows (one partial
+    tile) with the mask carved from the END of a larger buffer whose next bytes are another
+    tensor's -- rows past M read nothing (a 1-byte over-read faulted on unmapped memory)."""
+    n = _native()
+    M, N, K = 16, 2048, 512
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    big = torch.randint(0, 256, (M * N // 8 + 64,), device="cuda", dtype=torch.uint8, generator=g)
+    mask = big[: M * N // 8]
+    guard = big[M * N // 8:].clone()
+    acc = n._MaskedGrad(dy, mask)
+    r8 = _run(8, lambda: n.gemm_nt(a, b, acc_from=acc))
+    r15 = _run(15, lambda: n.gemm_nt(a, b, acc_from=acc))
+    assert torch.equal(r15, r8)
+    assert torch.equal(big[M * N // 8:], guard)
