@@ -70,8 +70,11 @@ FUSE_PROJ_BN = os.environ.get("DTF_FUSE_PROJ_BN", "1") == "1"
 # bottleneck c2's BN + ReLU inside c3's GEMM (ops.batch_norm_relu_conv1x1; falls back to the two
 # ops off the streaming route)
 FUSE_BN_CONV = os.environ.get("DTF_FUSE_BN_CONV", "1") == "1"
-# projection blocks: c1's backward runs after the projection's (see Bottleneck.forward; A/B knob)
-C1_LAST_BWD = os.environ.get("DTF_C1_LAST_BWD", "1") == "1"
+# projection blocks: c1's backward after the projection's (A/B knob, off: the input BN's reduce
+# pass goes away, 1.5 ms/step, but c1's streamed dgrad then reads x and accumulates onto the
+# projection's output, +1.8 ms, and the stride-2 projection's dgrad must zero-fill 3/4 of d(x),
+# +0.8 ms -- profiles/measurements/r5_c1_last_backward_ab.jsonl)
+C1_LAST_BWD = os.environ.get("DTF_C1_LAST_BWD", "0") == "1"
 
 
 class Bottleneck(nn.Module):
@@ -95,11 +98,9 @@ class Bottleneck(nn.Module):
         share = ops.GradShare(2) if self.has_proj else None
         if self.has_proj and FUSE_PROJ_BN:
             # the shortcut's BN is applied inside the block-output BN (one pass forward, one
-            # reduce + one apply pass backward for both).  c1 is built BEFORE the projection so
-            # that autograd runs its backward LAST of the two convs sharing x: the last one's data
-            # gradient completes d(x), and c1's streamed 1x1 dgrad can also form the backward sums
-            # of the BatchNorm that produced x (the stride-2 projection's cannot; it left a 1.2 ms
-            # reduce pass at stage 1)
+            # reduce + one apply pass backward for both).  C1_LAST_BWD builds c1 before the
+            # projection so autograd runs c1's backward last: its streamed dgrad then completes
+            # d(x) and forms the input BN's backward sums (measured slower, see C1_LAST_BWD)
             p, b = self.proj, self.proj.bn
             if not C1_LAST_BWD:
                 sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
