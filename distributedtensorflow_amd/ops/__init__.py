@@ -42,6 +42,15 @@ def _native():
     return native
 
 
+def native_join_wgrad_side():
+    """Join the native ops' side stream (weight gradients written into the flat gradient buffer
+    off the compute stream) into the compute stream; a no-op when the extension is not loaded."""
+    import sys
+    m = sys.modules.get(__name__ + ".native")
+    if m is not None:
+        m.join_wgrad_side()
+
+
 def _f32(t: torch.Tensor) -> bool:
     """fp32 GPU tensors run the fp32 HIP kernels (csrc/kernels/f32.hip): the reference
     workload at the reference's precision."""

@@ -116,6 +116,49 @@ def _direct_grad(p):
     return g
 
 
+# Conv weight gradients written straight into the flat gradient buffer run on a side stream
+# (A/B knob DTF_WGRAD_SIDE_STREAM): they depend only on (x, dy) and nothing in backward reads
+# them, so they overlap the data-gradient chain -- in particular its HBM-bound BatchNorm passes,
+# which leave the MFMA / LDS units of the CUs idle.  The side stream forks from the compute
+# stream per weight gradient and joins it (1) before a gradient bucket's all-reduce is issued
+# (join_wgrad_side, called by the reducers) and (2) at the end of every backward pass (an autograd
+# final callback), so every reader of the flat buffer is ordered after the writes.
+# measured neutral at ResNet-50 b1984 (16,471 vs 16,470 img/s same box, depth 2/4/8 alike:
+# profiles/measurements/r5_wgrad_side_stream_ab.jsonl) -- off by default
+_WGRAD_SIDE = os.environ.get("DTF_WGRAD_SIDE_STREAM", "0") == "1"
+_SIDE = {}          # device index -> (side stream, compute stream it forks from)
+_side_join_queued = False
+# operands of the queued side-stream weight gradients, kept alive (instead of record_stream,
+# whose deferred frees stalled the caching allocator: 7x slower) until the compute stream has
+# joined the side stream; at most _SIDE_DEPTH layers are in flight (bounded extra memory)
+_SIDE_KEEP = []
+_SIDE_DEPTH = int(os.environ.get("DTF_WGRAD_SIDE_DEPTH", "4"))
+
+
+def _wgrad_side(dev):
+    main = torch.cuda.current_stream(dev)
+    ent = _SIDE.get(dev.index)
+    if ent is None or ent[1] != main:
+        ent = _SIDE[dev.index] = (ent[0] if ent is not None else torch.cuda.Stream(dev), main)
+    return ent[0], main
+
+
+def join_wgrad_side():
+    """Order every compute stream after the weight gradients queued on its side stream."""
+    global _side_join_queued
+    _side_join_queued = False
+    for side, main in _SIDE.values():
+        main.wait_stream(side)
+    _SIDE_KEEP.clear()          # the compute stream is ordered after every use: reusable
+
+
+def _queue_side_join():
+    global _side_join_queued
+    if not _side_join_queued:
+        _side_join_queued = True
+        torch.autograd.Variable._execution_engine.queue_callback(join_wgrad_side)
+
+
 def _grad_ready(p):
     cb = getattr(p, "_dtf_grad_ready", None)
     if cb is not None:
@@ -512,7 +555,18 @@ class _Conv2d(torch.autograd.Function):
             # weight gradient first: it only depends on dy, so the bucketed all-reduce of this
             # layer can start while dgrad still runs
             target = _direct_grad(ctx.w_param)
-            if target is not None and not padded:
+            if (target is not None and not padded and _WGRAD_SIDE
+                    and not torch.cuda.is_current_stream_capturing()):
+                if len(_SIDE_KEEP) >= _SIDE_DEPTH:
+                    join_wgrad_side()
+                side, main = _wgrad_side(dy.device)
+                side.wait_stream(main)                 # dy (and x) are ready on the compute stream
+                with torch.cuda.stream(side):
+                    conv2d_wgrad(xb, dy, wb.shape, ctx.stride, ctx.padding, out=target)
+                _SIDE_KEEP.append((xb, dy))
+                _queue_side_join()
+                _grad_ready(ctx.w_param)
+            elif target is not None and not padded:
                 conv2d_wgrad(xb, dy, wb.shape, ctx.stride, ctx.padding, out=target)
                 _grad_ready(ctx.w_param)
             else:
