@@ -1388,10 +1388,33 @@ gemm_pp2_kernel(const GemmArgs g) {
           // row past M must fall outside it (a +1 here let row M's first lanes read one byte past
           // the mask allocation -- a device fault when that byte was unmapped)
           0, (has_acc && !g.Cin) ? (int)(cbytes / 16) : 0, 0x00020000);
-#pragma unroll
-      for (int i = 0; i < Cf::FM; ++i) {
+      // the accumulate / GELU operands of fragment row i + 1 are loaded while row i is formed
+      // (one fragment row = 4 output rows per lane): their latency hides under the conversions
+      // and stores instead of stalling every row
+      constexpr bool has_ld = has_acc || gelu_bwd;
+      typedef uint32_t u32x2l_t __attribute__((ext_vector_type(2)));
+      const __amdgpu_buffer_rsrc_t rld = gelu_bwd ? rg : rcin;
+      const bool masked = has_acc && !g.Cin;
+      const int mshift = ncol & 7;                     // ldc % 8 == 0: the same for every row
+      u32x2l_t pa[4], pn[4];
+      uint32_t pm[4], pmn[4];
+      auto load_rows = [&](int vrow, u32x2l_t (&d)[4], uint32_t (&m)[4]) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          const int o = vrow + r * ldc2;
+          d[r] = __builtin_bit_cast(u32x2l_t, __builtin_amdgcn_raw_buffer_load_b64(rld, o, 0, 0));
+          m[r] = masked ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rmask, o >> 4, 0, 0) : 0u;
+        }
+      };
+      if constexpr (has_ld) load_rows(vo, pa, pm);
+#pragma unroll
+      for (int i = 0; i < Cf::FM; ++i) {
+        if constexpr (has_ld) {
+          if (i + 1 < Cf::FM) load_rows(vo + 16 * ldc2, pn, pmn);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int vr = vo + r * ldc2;
           bf16_t h[4];
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
@@ -1408,13 +1431,8 @@ gemm_pp2_kernel(const GemmArgs g) {
             }
           }
           if constexpr (has_acc) {
-            typedef uint32_t u32x2l_t __attribute__((ext_vector_type(2)));
-            const u32x2l_t sv = __builtin_bit_cast(
-                u32x2l_t, __builtin_amdgcn_raw_buffer_load_b64(rcin, vo, 0, 0));
-            const uint32_t bits =
-                g.Cin ? 0xFu
-                      : ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rmask, vo >> 4, 0, 0) >>
-                         ((vo >> 1) & 7)) & 0xFu;
+            const u32x2l_t sv = pa[r];
+            const uint32_t bits = masked ? (pm[r] >> mshift) & 0xFu : 0xFu;
             const float sf[4] = {__builtin_bit_cast(float, sv.x << 16),
                                  __builtin_bit_cast(float, sv.x & 0xffff0000u),
                                  __builtin_bit_cast(float, sv.y << 16),
@@ -1427,9 +1445,7 @@ gemm_pp2_kernel(const GemmArgs g) {
             // d = bf16(acc) * gelu'(a + b) (the LDS-staged kernel's arithmetic: bit-identical);
             // its fp32 value feeds the column sums (rows past M: acc and a are zero-filled ... d
             // = 0 * gelu'(b): exact zero)
-            typedef uint32_t u32x2l_t __attribute__((ext_vector_type(2)));
-            const u32x2l_t av = __builtin_bit_cast(
-                u32x2l_t, __builtin_amdgcn_raw_buffer_load_b64(rg, vo, 0, 0));
+            const u32x2l_t av = pa[r];
             const float af[4] = {__builtin_bit_cast(float, av.x << 16),
                                  __builtin_bit_cast(float, av.x & 0xffff0000u),
                                  __builtin_bit_cast(float, av.y << 16),
@@ -1443,21 +1459,24 @@ gemm_pp2_kernel(const GemmArgs g) {
           }
           const u32x2_t w = {(uint32_t)h[0] | ((uint32_t)h[1] << 16),
                              (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
-          if (nt_store) __builtin_amdgcn_raw_buffer_store_b64(w, rc, vo, 0, 2);
-          else __builtin_amdgcn_raw_buffer_store_b64(w, rc, vo, 0, 0);
+          if (nt_store) __builtin_amdgcn_raw_buffer_store_b64(w, rc, vr, 0, 2);
+          else __builtin_amdgcn_raw_buffer_store_b64(w, rc, vr, 0, 0);
           if constexpr (gelu_fwd) {
             bf16_t q[4];
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) q[jj] = f2bf(gelu_f(bf2f(h[jj])));
             const u32x2_t wq = {(uint32_t)q[0] | ((uint32_t)q[1] << 16),
                                 (uint32_t)q[2] | ((uint32_t)q[3] << 16)};
-            if (nt_store) __builtin_amdgcn_raw_buffer_store_b64(wq, rg, vo, 0, 2);
-            else __builtin_amdgcn_raw_buffer_store_b64(wq, rg, vo, 0, 0);
+            if (nt_store) __builtin_amdgcn_raw_buffer_store_b64(wq, rg, vr, 0, 2);
+            else __builtin_amdgcn_raw_buffer_store_b64(wq, rg, vr, 0, 0);
           }
-          asm volatile("v_add_u32 %0, %0, %1" : "+v"(vo) : "s"(ldc2));
-          __builtin_amdgcn_sched_barrier(0);     // one row at a time (register pressure)
         }
-        asm volatile("v_add_u32 %0, %0, %1" : "+v"(vo) : "s"(12 * ldc2));
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(vo) : "s"(16 * ldc2));
+        if constexpr (has_ld) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { pa[r] = pn[r]; pm[r] = pmn[r]; }
+        }
+        __builtin_amdgcn_sched_barrier(0);     // one fragment row at a time (register pressure)
       }
       if constexpr (gelu_bwd) {
         // per-tile column sums of d: lane groups by cross-lane adds, the two wave rows in LDS,
