@@ -214,6 +214,7 @@ int dtf_gemm_tile_rows(int);
 void dtf_gemm_set_variant(int);
 void dtf_gemm_set_pp(int);
 void dtf_gemm_set_pp2(int);
+int dtf_gemm_get_pp2();
 bool dtf_gemm_pp2_ok(int M, int N, int K, int lda, int ldb);
 int dtf_bias_relu_bwd_ws_floats(int);
 void dtf_gather_u8_scale(const uint8_t*, const int64_t*, void*, int, int, float, int, hipStream_t);
@@ -357,6 +358,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("gemm_set_variant", &dtf_gemm_set_variant);
   m.def("gemm_set_pp", &dtf_gemm_set_pp);
   m.def("gemm_set_pp2", &dtf_gemm_set_pp2);
+  m.def("gemm_get_pp2", &dtf_gemm_get_pp2);
   m.def("gemm_pp2_ok", &dtf_gemm_pp2_ok);
   m.def("bias_relu_bwd_ws_floats", &dtf_bias_relu_bwd_ws_floats);
   m.def("gather_u8_scale", [](uintptr_t images, uintptr_t idx, uintptr_t out, int B, int D,

@@ -1722,10 +1722,10 @@ void launch_gemm_pp(const GemmArgs& g, hipStream_t st) {
 }
 
 int g_gemm_pp = 0;         // bit 0: persistent register-epilogue kernel for gemm_nt, bit 1: convs
-// round-5 persistent kernel (gemm_pp2): bit 0 gemm_nt (default: 0.92-1.05x hipBLASLt on the BERT
-// shapes, profiles/measurements/r5_gemm_pp2_interleaved_epilogue_vs_v8.jsonl; ResNet-50 +0.6 %),
-// bit 1 the implicit-GEMM convs (measured neutral: off)
-int g_gemm_pp2 = 1;
+// round-5 persistent kernel (gemm_pp2): bit 0 gemm_nt (0.92-1.05x hipBLASLt on the BERT shapes,
+// profiles/measurements/r5_gemm_pp2_interleaved_epilogue_vs_v8.jsonl; ResNet-50 +0.6 %), bit 1 the
+// unit-stride implicit-GEMM convs (2-5 % per layer, r5_conv_pp2_per_layer_b1984.jsonl)
+int g_gemm_pp2 = 3;
 int g_gemm_stream = 1;     // output-heavy shapes on the row-streaming kernel (gemm_stream.hip)
 
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
@@ -1773,6 +1773,7 @@ void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
 void dtf_gemm_set_stream(int v) { g_gemm_stream = v; }
 void dtf_gemm_set_pp(int v) { g_gemm_pp = v; }
 void dtf_gemm_set_pp2(int v) { g_gemm_pp2 = v; }
+int dtf_gemm_get_pp2() { return g_gemm_pp2; }
 void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
 void dtf_gemm_set_dbg(int v) { g_gemm_dbg = v; }
 void dtf_gemm_set_stagger(int mode, int iters) { g_gemm_stagger_mode = mode; g_gemm_stagger = iters; }
@@ -1809,8 +1810,12 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
       (256.0 / (P * Q) + 2) * Ho * Wo * (double)Kout * 2 < 2147483647.0;
   const long x_bytes = (long)N * H * W * C * 2, w_bytes = (long)Kout * g.ldb * 2;
   if (Kout <= 128) launch_gemm<256, 128, 64, 3, 3, 8, 1, 1>(g, st);
-  else if ((g_gemm_pp2 & 2) && g.K >= 128 && x_bytes < 0x7FFFFF00L && w_bytes < 0x7FFFFF00L &&
-           N < 2048 && H < 1000 && W < 1000 && pp_span)
+  // the persistent kernel for the unit-stride output launches only: its strided (dgrad phase)
+  // epilogue is the swapped 32-B piece one -- 1.2-1.5x slower than the ping-pong's on the
+  // stride-2 data gradients, while the unit-stride convs gain 2-5 %
+  // (profiles/measurements/r5_conv_pp2_per_layer_b1984.jsonl)
+  else if ((g_gemm_pp2 & 2) && osh == 1 && osw == 1 && g.K >= 128 && x_bytes < 0x7FFFFF00L &&
+           w_bytes < 0x7FFFFF00L && N < 2048 && H < 1000 && W < 1000 && pp_span)
     launch_gemm_pp2<1>(g, x_bytes, w_bytes, st);
   else if ((g_gemm_pp & 2) && (g.K + 63) / 64 >= 2 && pp_span) launch_gemm_pp<1>(g, st);
   else launch_gemm<256, 256, 64, 2, 2, 8, 1, 1>(g, st);

@@ -126,6 +126,7 @@ def test_pp2_conv_matches_pingpong_bitwise(n, hw, c, k, stride):
     x = torch.randn(n, hw, hw, c, device="cuda", generator=g).bfloat16()
     w = (torch.randn(k, 3, 3, c, device="cuda", generator=g) / (9 * c) ** 0.5).bfloat16()
     out = {}
+    prev = n_._K.gemm_get_pp2()
     for pp2 in (0, 2):
         n_._K.gemm_set_pp2(pp2)
         try:
@@ -139,7 +140,7 @@ def test_pp2_conv_matches_pingpong_bitwise(n, hw, c, k, stride):
             torch.cuda.synchronize()
             out[pp2] = (y, ys, st, dx)
         finally:
-            n_._K.gemm_set_pp2(0)
+            n_._K.gemm_set_pp2(prev)
     (y0, ys0, st0, dx0), (y2, ys2, st2, dx2) = out[0], out[2]
     assert torch.equal(y2, y0) and torch.equal(ys2, ys0) and torch.equal(dx2, dx0)
     torch.testing.assert_close(st2.sum(0), st0.sum(0), rtol=1e-4, atol=1e-1)
@@ -155,6 +156,7 @@ def test_pp2_bias_gelu_epilogue_matches_pingpong(M, N, K):
     b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
     bias = torch.randn(N, device="cuda", generator=g)
     out = {}
+    prev = n._K.gemm_get_pp2()
     for pp2 in (0, 1):
         n._K.gemm_set_pp2(pp2)
         try:
@@ -165,7 +167,7 @@ def test_pp2_bias_gelu_epilogue_matches_pingpong(M, N, K):
             torch.cuda.synchronize()
             out[pp2] = (z, h)
         finally:
-            n._K.gemm_set_pp2(0)
+            n._K.gemm_set_pp2(prev)
     assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
     zf = (a.float() @ b.float().t() + bias)
     assert ((out[1][0].float() - zf).norm() / zf.norm()).item() < 5e-3
@@ -184,6 +186,7 @@ def test_pp2_gelu_backward_epilogue_matches_pingpong(M, N, K):
     b = torch.randn(N, device="cuda", generator=g) * 0.1
     tiles = n._K.gemm_tile_rows(M)
     out = {}
+    prev = n._K.gemm_get_pp2()
     for pp2 in (0, 1):
         n._K.gemm_set_pp2(pp2)
         try:
@@ -194,7 +197,7 @@ def test_pp2_gelu_backward_epilogue_matches_pingpong(M, N, K):
             torch.cuda.synchronize()
             out[pp2] = (da, cs)
         finally:
-            n._K.gemm_set_pp2(0)
+            n._K.gemm_set_pp2(prev)
     assert torch.equal(out[1][0], out[0][0])
     torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-4, atol=1e-2)
     col = out[1][0].float().sum(0)
