@@ -517,6 +517,10 @@ constexpr int kPpLDO = 260;                 // fp32 epilogue pitch (floats)
 constexpr size_t kPpLDS = (size_t)128 * kPpLDO * 4 > (size_t)2 * kPpStage * 2
                               ? (size_t)128 * kPpLDO * 4 : (size_t)2 * kPpStage * 2;
 
+// DENSE: a 1x1 / stride-1 / unpadded conv or a dense layer (one tap at (0, 0), P = H, Q = W):
+// pixel m IS row m of X, so the B pieces are addressed like the A pieces -- no per-step pixel
+// decode and no cross-lane shuffles (two ds_bpermute per B DMA instruction) in the main loop
+template <bool DENSE>
 __global__ void __launch_bounds__(kPpT, 1)
 conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                      float* __restrict__ dW, const WgradGeom g, const TapTableW taps,
@@ -539,7 +543,8 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
   const int PQ = g.P * g.Q;                 // split-relative descriptors (see conv_wgrad_kernel)
   const int n_lo = ms / PQ, n_hi = max(n_lo, (me - 1) / PQ);
   const long img = (long)g.H * g.W * g.C;
-  const i32x4_t rx = rsrc_quad(X + n_lo * img, (uint32_t)((n_hi - n_lo + 1) * img * 2));
+  const i32x4_t rx = DENSE ? rsrc_quad(X + (long)ms * g.C, (uint32_t)max(me - ms, 0) * g.C * 2u)
+                           : rsrc_quad(X + n_lo * img, (uint32_t)((n_hi - n_lo + 1) * img * 2));
   const i32x4_t ry = rsrc_quad(dY + (long)ms * g.Kout, (uint32_t)max(me - ms, 0) * g.Kout * 2u);
   const uint32_t lds0 = lds_addr(lds);
   int* lds_taps = reinterpret_cast<int*>(lds);
@@ -556,7 +561,10 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
     const int kc = k0 + chunk * 8;
     a_off[j] = kc < g.Kout ? kc * 2 : -1;
     const int jc = j0 + chunk * 8;
-    if (jc < TC) {
+    if (DENSE) {
+      b_dh[j] = b_dw[j] = 0;
+      b_toff[j] = jc < TC ? jc * 2 : -1;
+    } else if (jc < TC) {
       const int t = jc / g.C, c = jc - t * g.C;
       b_dh[j] = lds_taps[t];
       b_dw[j] = lds_taps[DTF_MAX_TAPS + t];
@@ -574,6 +582,7 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
   auto decode = [&](int kt) {
     const int mk = ms + kt * kPpBK;
     dec_live = me - mk;
+    if (DENSE) return;
     const int mp = mk + lane;
     int t, q, n, p;
     fdivmod(mp < me ? mp : ms, g.Q, invQ, t, q);
@@ -598,6 +607,10 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
         const uint32_t off = (R < dec_live && a_off[j] >= 0)
                                  ? (uint32_t)(mk - ms + R) * g.Kout * 2u + (uint32_t)a_off[j] : kOOB;
         dma16(ry, dst, off);
+      } else if (DENSE) {
+        const uint32_t off = (R < dec_live && b_toff[j] >= 0)
+                                 ? (uint32_t)(mk - ms + R) * g.C * 2u + (uint32_t)b_toff[j] : kOOB;
+        dma16(rx, dst, off);
       } else {
         const int hwr = __shfl(dec_hw, R, 64);
         const int pbr = __shfl(dec_pb, R, 64);
@@ -896,6 +909,9 @@ void dtf_wgrad_set_pp(int v) {
   g_wgrad_pp = v > 0;
   if (v > 0) g_wgrad_pp_rounds = v;
 }
+// ping-pong kernel: the DENSE form (no pixel decode) for one-tap unit-stride unpadded layers
+static int g_wgrad_dense = 1;
+void dtf_wgrad_set_dense(int v) { g_wgrad_dense = v; }
 static bool wgrad_pp(int Kout, int TC) { return g_wgrad_pp && Kout >= 256 && TC >= 256; }
 static int g_wgrad_pipe = 3;
 void dtf_wgrad_set_pipe(int p) { g_wgrad_pipe = p; }
@@ -1008,13 +1024,21 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   if (dma && wgrad_pp(g.Kout, TC) && g.ldw % 4 == 0) {
     static bool attr = false;
     if (!attr) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel,
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<true>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
       attr = true;
     }
     const long ptiles = (long)((g.Kout + 255) / 256) * ((TC + 255) / 256);
-    hipLaunchKernelGGL(conv_wgrad_pp_kernel, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT), kPpLDS,
-                       st, X, dY, target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+    const bool dense = g_wgrad_dense && taps.n == 1 && taps.dh[0] == 0 && taps.dw[0] == 0 &&
+                       g.sh == 1 && g.sw == 1 && g.H == g.P && g.W == g.Q;
+    if (dense)
+      hipLaunchKernelGGL(conv_wgrad_pp_kernel<true>, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT),
+                         kPpLDS, st, X, dY, target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+    else
+      hipLaunchKernelGGL(conv_wgrad_pp_kernel<false>, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT),
+                         kPpLDS, st, X, dY, target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
   } else if (dma) {
     const float iq = 1.0f / (float)g.Q, ip = 1.0f / (float)g.P;
 #define DTF_WGRAD_LAUNCH(WM_, WN_, BK_, NS_)                                                     \

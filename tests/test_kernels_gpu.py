@@ -415,6 +415,35 @@ def test_wgrad_pingpong_kernel(case):
     assert _rel(pp, old) < 1e-4, _rel(pp, old)
 
 
+WGRAD_DENSE_CASES = [
+    (4, 14, 14, 1024, 256),              # late 1x1
+    (3, 9, 11, 384, 264),                # partial Kout / T*C tiles, M not a multiple of 64
+    (4096, 1, 1, 768, 3072),             # dense layer dW
+    (40000, 1, 1, 256, 512),             # many splits, ragged last split
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_DENSE_CASES)
+def test_wgrad_pingpong_dense_form_bit_identical(case):
+    """The ping-pong wgrad kernel's DENSE form (one-tap unit-stride layers addressed as plain
+    rows, no pixel decode) is bit-identical to its general form and matches the fp32 dW."""
+    N, H, W, C, K = case
+    nat = _native()
+    torch.manual_seed(1)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    dy = torch.randn(N, H, W, K, device=dev).to(torch.bfloat16)
+    try:
+        nat._K.wgrad_set_dense(1)
+        dense = nat.conv2d_wgrad(x, dy, (K, 1, 1, C), 1, 0)
+        nat._K.wgrad_set_dense(0)
+        gen = nat.conv2d_wgrad(x, dy, (K, 1, 1, C), 1, 0)
+    finally:
+        nat._K.wgrad_set_dense(1)
+    assert torch.equal(dense, gen)
+    ref = dy.reshape(-1, K).float().t() @ x.reshape(-1, C).float()
+    assert _rel(dense.reshape(K, C), ref) < 1e-3
+
+
 CONV_GEMM_CASES = [
     (2, 28, 28, 128, 128, 3, 1, 1),      # Kout 128: the 256 x 128 ping-pong tile
     (3, 15, 13, 128, 128, 3, 2, 1),      #   strided, odd sizes
