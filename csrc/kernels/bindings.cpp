@@ -127,6 +127,7 @@ void dtf_wgrad_set_dma_mode(int);
 void dtf_wgrad_set_pipe(int);
 void dtf_wgrad_set_pp(int);
 void dtf_wgrad_set_dense(int);
+void dtf_wgrad_set_direct(int);
 void dtf_conv_set_gemm(int);
 void dtf_bn_set_nt(int);
 void dtf_bn_set_grid_cap(int);
@@ -728,6 +729,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("wgrad_set_pipe", &dtf_wgrad_set_pipe);
   m.def("wgrad_set_pp", &dtf_wgrad_set_pp);
   m.def("wgrad_set_dense", &dtf_wgrad_set_dense);
+  m.def("wgrad_set_direct", &dtf_wgrad_set_direct);
   m.def("conv_set_halo_stages", &dtf_conv_set_halo_stages);
   m.def("conv_set_gemm", &dtf_conv_set_gemm);
   m.def("bn_set_nt", &dtf_bn_set_nt);

@@ -520,11 +520,13 @@ constexpr size_t kPpLDS = (size_t)128 * kPpLDO * 4 > (size_t)2 * kPpStage * 2
 // DENSE: a 1x1 / stride-1 / unpadded conv or a dense layer (one tap at (0, 0), P = H, Q = W):
 // pixel m IS row m of X, so the B pieces are addressed like the A pieces -- no per-step pixel
 // decode and no cross-lane shuffles (two ds_bpermute per B DMA instruction) in the main loop
-template <bool DENSE>
+// FORM 0: lane-per-pixel decode shuffled to the DMA rows; 1: DENSE; 2: DIRECT per-row decode
+template <int FORM>
 __global__ void __launch_bounds__(kPpT, 1)
 conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                      float* __restrict__ dW, const WgradGeom g, const TapTableW taps,
                      float invQ, float invP) {
+  constexpr bool DENSE = FORM == 1, DIRECT = FORM == 2;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -578,11 +580,29 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
   __syncthreads();                          // the tap table is dead: slot 0 may now be filled
   const int HW = g.H * g.W;
   // pixel decode of the K-step being issued: lane l holds pixel mk + l's base offset / (h, w)
+  // (shuffled to the DMA rows), or with DIRECT each lane decodes the 4 rows it fetches itself
   int dec_pb = 0, dec_hw = 0, dec_live = 0;
+  int drow_pb[2][2], drow_hw[2][2];
   auto decode = [&](int kt) {
     const int mk = ms + kt * kPpBK;
     dec_live = me - mk;
     if (DENSE) return;
+    if (DIRECT) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int R = 32 * h + 2 * (wave + 8 * j) + (lane >> 5);
+          int t, q, n, p;
+          fdivmod(R < dec_live ? mk + R : ms, g.Q, invQ, t, q);
+          fdivmod(t, g.P, invP, n, p);
+          const int hb = R < dec_live ? p * g.sh : 0x3FFF;
+          const int wb = q * g.sw;
+          drow_pb[h][j] = (((n - n_lo) * HW + hb * g.W + wb) * g.C) * 2;
+          drow_hw[h][j] = (hb << 16) | wb;
+        }
+      return;
+    }
     const int mp = mk + lane;
     int t, q, n, p;
     fdivmod(mp < me ? mp : ms, g.Q, invQ, t, q);
@@ -612,8 +632,8 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
                                  ? (uint32_t)(mk - ms + R) * g.C * 2u + (uint32_t)b_toff[j] : kOOB;
         dma16(rx, dst, off);
       } else {
-        const int hwr = __shfl(dec_hw, R, 64);
-        const int pbr = __shfl(dec_pb, R, 64);
+        const int hwr = DIRECT ? drow_hw[h][j] : __shfl(dec_hw, R, 64);
+        const int pbr = DIRECT ? drow_pb[h][j] : __shfl(dec_pb, R, 64);
         const int hh = (hwr >> 16) + b_dh[j], ww = (hwr & 0xFFFF) + b_dw[j];
         const bool ok = (unsigned)hh < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
         dma16(rx, dst, ok ? (uint32_t)(pbr + b_toff[j]) : kOOB);
@@ -912,6 +932,12 @@ void dtf_wgrad_set_pp(int v) {
 // ping-pong kernel: the DENSE form (no pixel decode) for one-tap unit-stride unpadded layers
 static int g_wgrad_dense = 1;
 void dtf_wgrad_set_dense(int v) { g_wgrad_dense = v; }
+// multi-tap / strided layers: each lane decodes the pixel rows it fetches instead of shuffling
+// one lane-per-pixel decode (A/B knob, off: the 4 decodes per lane cost more VALU than the
+// shuffles, -0.5..+3 % on stage-3 layers, -10..-15 % on stage-4 ones;
+// profiles/measurements/r5_wgrad_direct_decode_ab.jsonl)
+static int g_wgrad_direct = 0;
+void dtf_wgrad_set_direct(int v) { g_wgrad_direct = v; }
 static bool wgrad_pp(int Kout, int TC) { return g_wgrad_pp && Kout >= 256 && TC >= 256; }
 static int g_wgrad_pipe = 3;
 void dtf_wgrad_set_pipe(int p) { g_wgrad_pipe = p; }
@@ -1024,21 +1050,21 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   if (dma && wgrad_pp(g.Kout, TC) && g.ldw % 4 == 0) {
     static bool attr = false;
     if (!attr) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<false>,
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<0>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
-      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<true>,
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<1>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<2>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
       attr = true;
     }
     const long ptiles = (long)((g.Kout + 255) / 256) * ((TC + 255) / 256);
     const bool dense = g_wgrad_dense && taps.n == 1 && taps.dh[0] == 0 && taps.dw[0] == 0 &&
                        g.sh == 1 && g.sw == 1 && g.H == g.P && g.W == g.Q;
-    if (dense)
-      hipLaunchKernelGGL(conv_wgrad_pp_kernel<true>, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT),
-                         kPpLDS, st, X, dY, target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
-    else
-      hipLaunchKernelGGL(conv_wgrad_pp_kernel<false>, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT),
-                         kPpLDS, st, X, dY, target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+    auto kern = dense ? conv_wgrad_pp_kernel<1>
+                      : g_wgrad_direct ? conv_wgrad_pp_kernel<2> : conv_wgrad_pp_kernel<0>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT), kPpLDS, st, X, dY,
+                       target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
   } else if (dma) {
     const float iq = 1.0f / (float)g.Q, ip = 1.0f / (float)g.P;
 #define DTF_WGRAD_LAUNCH(WM_, WN_, BK_, NS_)                                                     \

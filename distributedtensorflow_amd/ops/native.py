@@ -43,6 +43,8 @@ if os.environ.get("DTF_WGRAD_PP"):       # ping-pong wgrad: 0 off, n: split-K ta
     _K.wgrad_set_pp(int(os.environ["DTF_WGRAD_PP"]))
 if os.environ.get("DTF_WGRAD_DENSE"):    # ping-pong wgrad's decode-free one-tap form: 0 off
     _K.wgrad_set_dense(int(os.environ["DTF_WGRAD_DENSE"]))
+if os.environ.get("DTF_WGRAD_DIRECT"):   # ping-pong wgrad: per-row decode (1) / shuffles (0)
+    _K.wgrad_set_direct(int(os.environ["DTF_WGRAD_DIRECT"]))
 if os.environ.get("DTF_WGRAD_PIPE"):
     _K.wgrad_set_pipe(int(os.environ["DTF_WGRAD_PIPE"]))
 if os.environ.get("DTF_CONV_DMA"):

@@ -413,6 +413,13 @@ def test_wgrad_pingpong_kernel(case):
     ref.conv2d(x.float(), wr, stride, pad).backward(dy.float())
     assert _rel(pp, wr.grad) < 1e-3, _rel(pp, wr.grad)
     assert _rel(pp, old) < 1e-4, _rel(pp, old)
+    # the per-row (direct) pixel decode and the shuffled one fetch the same rows
+    try:
+        nat._K.wgrad_set_direct(1)
+        direct = nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad)
+    finally:
+        nat._K.wgrad_set_direct(0)
+    assert torch.equal(pp, direct)
 
 
 WGRAD_DENSE_CASES = [
