@@ -299,7 +299,9 @@ struct WdCfg {
   static_assert(IA >= 1 && IB >= 1 && BK % 32 == 0, "wgrad DMA plan");
 };
 
-template <int WM, int WN, int BK, int NS>
+// DENSE: one tap at (0, 0), unit stride, P = H, Q = W (see conv_wgrad_pp_kernel): X rows are
+// the pixels, no decode / shuffles
+template <int WM, int WN, int BK, int NS, bool DENSE = false>
 __global__ void __launch_bounds__(kThreads, (BK == 32 && NS == 2) ? 4 : 2)
 conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                       float* __restrict__ dW, const WgradGeom g, const TapTableW taps,
@@ -328,7 +330,8 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
   const int PQ = g.P * g.Q;                 // split-relative descriptors (see conv_wgrad_kernel)
   const int n_lo = ms / PQ, n_hi = max(n_lo, (me - 1) / PQ);
   const long img = (long)g.H * g.W * g.C;
-  const i32x4_t rx = rsrc_quad(X + n_lo * img, (uint32_t)((n_hi - n_lo + 1) * img * 2));
+  const i32x4_t rx = DENSE ? rsrc_quad(X + (long)ms * g.C, (uint32_t)max(me - ms, 0) * g.C * 2u)
+                           : rsrc_quad(X + n_lo * img, (uint32_t)((n_hi - n_lo + 1) * img * 2));
   const i32x4_t ry = rsrc_quad(dY + (long)ms * g.Kout, (uint32_t)max(me - ms, 0) * g.Kout * 2u);
   const uint32_t lds0 = lds_addr(lds);
   // tap table -> LDS (read once below, before any DMA reuses the space) so per-lane lookups
@@ -357,7 +360,10 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
     rowb[i] = r;
     const int chunk = (lane % (BNw / 8)) ^ wswz<BNw * 2>(r);
     const int jc = j0 + chunk * 8;
-    if (jc < TC) {
+    if (DENSE) {
+      b_dh[i] = b_dw[i] = 0;
+      b_toff[i] = jc < TC ? jc * 2 : -1;
+    } else if (jc < TC) {
       const int t = jc / g.C;
       const int c = jc - t * g.C;
       b_dh[i] = lds_taps[t];
@@ -378,14 +384,17 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
     const uint32_t base = lds0 + (uint32_t)(stage * Cf::STAGE) * 2u;
     const int mk = ms + kt * BK;                     // wave-uniform first pixel of the step
     const int live = me - mk;                         // rows < live are inside this split
-    const int mp = mk + lane;
-    int t, q, n, p;
-    fdivmod(mp < me ? mp : mk, g.Q, invQ, t, q);
-    fdivmod(t, g.P, invP, n, p);
-    const int hb = lane < live ? p * g.sh : 0x3FFF;   // an invalid row fails every bounds test
-    const int wb = q * g.sw;
-    const int pb = (((n - n_lo) * HW + hb * g.W + wb) * g.C) * 2;
-    const int hw = (hb << 16) | wb;
+    int pb = 0, hw = 0;
+    if (!DENSE) {
+      const int mp = mk + lane;
+      int t, q, n, p;
+      fdivmod(mp < me ? mp : mk, g.Q, invQ, t, q);
+      fdivmod(t, g.P, invP, n, p);
+      const int hb = lane < live ? p * g.sh : 0x3FFF;   // an invalid row fails every bounds test
+      const int wb = q * g.sw;
+      pb = (((n - n_lo) * HW + hb * g.W + wb) * g.C) * 2;
+      hw = (hb << 16) | wb;
+    }
     const uint32_t a_base = (uint32_t)(mk - ms) * g.Kout * 2u;
 #pragma unroll
     for (int i = 0; i < Cf::IA; ++i) {
@@ -396,6 +405,12 @@ conv_wgrad_dma_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ d
 #pragma unroll
     for (int i = 0; i < Cf::IB; ++i) {
       const int r = rowb[i];
+      if (DENSE) {
+        const uint32_t bo = (r < live && b_toff[i] >= 0)
+                                ? (uint32_t)(mk - ms + r) * g.C * 2u + (uint32_t)b_toff[i] : kOOB;
+        dma16(rx, base + (uint32_t)(BK * BMw * 2) + (uint32_t)(wave + 4 * i) * 1024u, bo);
+        continue;
+      }
       const int hwr = __shfl(hw, r, 64);
       const int pbr = __shfl(pb, r, 64);
       const int h = (hwr >> 16) + b_dh[i], w = (hwr & 0xFFFF) + b_dw[i];
@@ -1047,6 +1062,8 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   const int bm = narrow ? 64 : BM, bn = narrow ? 256 : BN;
   const long tiles = (long)((g.Kout + bm - 1) / bm) * ((TC + bn - 1) / bn);
   const dim3 grid((unsigned)(tiles * nsplit));
+  const bool dense1 = (g_wgrad_dense & 1) && taps.n == 1 && taps.dh[0] == 0 && taps.dw[0] == 0 &&
+                      g.sh == 1 && g.sw == 1 && g.H == g.P && g.W == g.Q;
   if (dma && wgrad_pp(g.Kout, TC) && g.ldw % 4 == 0) {
     static bool attr = false;
     if (!attr) {
@@ -1059,17 +1076,22 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
       attr = true;
     }
     const long ptiles = (long)((g.Kout + 255) / 256) * ((TC + 255) / 256);
-    const bool dense = g_wgrad_dense && taps.n == 1 && taps.dh[0] == 0 && taps.dw[0] == 0 &&
-                       g.sh == 1 && g.sw == 1 && g.H == g.P && g.W == g.Q;
-    auto kern = dense ? conv_wgrad_pp_kernel<1>
+    auto kern = dense1 ? conv_wgrad_pp_kernel<1>
                       : g_wgrad_direct ? conv_wgrad_pp_kernel<2> : conv_wgrad_pp_kernel<0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT), kPpLDS, st, X, dY,
                        target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
   } else if (dma) {
     const float iq = 1.0f / (float)g.Q, ip = 1.0f / (float)g.P;
 #define DTF_WGRAD_LAUNCH(WM_, WN_, BK_, NS_)                                                     \
-  hipLaunchKernelGGL((conv_wgrad_dma_kernel<WM_, WN_, BK_, NS_>), grid, dim3(kThreads),         \
-                     (WdCfg<WM_, WN_, BK_, NS_>::LDS), st, X, dY, target, g, taps, iq, ip)
+  do {                                                                                           \
+    if (dense1)                                                                                  \
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<WM_, WN_, BK_, NS_, true>), grid,               \
+                         dim3(kThreads), (WdCfg<WM_, WN_, BK_, NS_>::LDS), st, X, dY, target, g, \
+                         taps, iq, ip);                                                          \
+    else                                                                                         \
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<WM_, WN_, BK_, NS_>), grid, dim3(kThreads),     \
+                         (WdCfg<WM_, WN_, BK_, NS_>::LDS), st, X, dY, target, g, taps, iq, ip); \
+  } while (0)
     if (g_wgrad_pipe == 1) {   // 32-pixel steps, 4-stage ring (3 steps of DMA in flight)
       if (narrow) DTF_WGRAD_LAUNCH(1, 4, 32, 4);
       else DTF_WGRAD_LAUNCH(2, 2, 32, 4);

@@ -427,6 +427,8 @@ WGRAD_DENSE_CASES = [
     (3, 9, 11, 384, 264),                # partial Kout / T*C tiles, M not a multiple of 64
     (4096, 1, 1, 768, 3072),             # dense layer dW
     (40000, 1, 1, 256, 512),             # many splits, ragged last split
+    (4, 28, 28, 512, 128),               # Kout 128: the LDS-DMA kernel's dense form
+    (3, 23, 29, 64, 256),                # T*C 64: LDS-DMA kernel, ragged pixel count
 ]
 
 

@@ -14,6 +14,10 @@ SHAPES = [  # name, pixels (tokens), Kout (o), C (i)
     ("bert_attn_out", 65536, 768, 768),
     ("bert_ffn1", 65536, 3072, 768),
     ("bert_ffn2", 65536, 768, 3072),
+    ("rn50_s0_c1_b1984", 1984 * 3136, 64, 256),
+    ("rn50_s0_c3_b1984", 1984 * 3136, 256, 64),
+    ("rn50_s1_c1_b1984", 1984 * 784, 128, 512),
+    ("rn50_s1_c3_b1984", 1984 * 784, 512, 128),
     ("rn50_s2_c1_b1984", 1984 * 196, 256, 1024),
     ("rn50_s2_c3_b1984", 1984 * 196, 1024, 256),
     ("rn50_s3_c1_b1984", 1984 * 49, 512, 2048),
