@@ -128,6 +128,7 @@ void dtf_wgrad_set_pipe(int);
 void dtf_wgrad_set_pp(int);
 void dtf_wgrad_set_dense(int);
 void dtf_wgrad_set_direct(int);
+void dtf_wgrad_set_deep(int);
 void dtf_conv_set_gemm(int);
 void dtf_bn_set_nt(int);
 void dtf_bn_set_grid_cap(int);
@@ -730,6 +731,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("wgrad_set_pp", &dtf_wgrad_set_pp);
   m.def("wgrad_set_dense", &dtf_wgrad_set_dense);
   m.def("wgrad_set_direct", &dtf_wgrad_set_direct);
+  m.def("wgrad_set_deep", &dtf_wgrad_set_deep);
   m.def("conv_set_halo_stages", &dtf_conv_set_halo_stages);
   m.def("conv_set_gemm", &dtf_conv_set_gemm);
   m.def("bn_set_nt", &dtf_bn_set_nt);

@@ -531,17 +531,35 @@ constexpr int kPpStage = 2 * kPpImg;        // dY image + X image
 constexpr int kPpLDO = 260;                 // fp32 epilogue pitch (floats)
 constexpr size_t kPpLDS = (size_t)128 * kPpLDO * 4 > (size_t)2 * kPpStage * 2
                               ? (size_t)128 * kPpLDO * 4 : (size_t)2 * kPpStage * 2;
+// DEEP: 32-pixel K-steps in a 5-slot ring (32 KB per slot, the whole 160 KB), each step's two
+// pieces issued 3 steps ahead -- ~1.5x the latency cover of the 2 x 64-pixel double buffer (an
+// L2-resident probe of the latter runs 18-23 % faster, profiles/measurements/r5_wgrad_l2_probe.jsonl).
+// Per step: p0 {B + A-top reads | dY piece of step t+3 | barrier | 16 MFMAs | barrier},
+// p1 {A-bottom reads | X piece of step t+3 | vmcnt(8): step t+1 landed | barrier | 16 MFMAs |
+// barrier}.  WAR: slot (t+3) % 5 was last read in step t-2.  Same MFMA order: bit-identical.
+constexpr int kPpDeepBK = 32, kPpDeepSlots = 5;
+constexpr int kPpDeepImg = kPpDeepBK * kPpW, kPpDeepStage = 2 * kPpDeepImg;
+constexpr size_t kPpDeepLDS = (size_t)kPpDeepSlots * kPpDeepStage * 2;
+static_assert(kPpDeepLDS <= 160 * 1024 && kPpDeepLDS >= (size_t)128 * kPpLDO * 4, "deep LDS");
 
 // DENSE: a 1x1 / stride-1 / unpadded conv or a dense layer (one tap at (0, 0), P = H, Q = W):
 // pixel m IS row m of X, so the B pieces are addressed like the A pieces -- no per-step pixel
 // decode and no cross-lane shuffles (two ds_bpermute per B DMA instruction) in the main loop
 // FORM 0: lane-per-pixel decode shuffled to the DMA rows; 1: DENSE; 2: DIRECT per-row decode
-template <int FORM>
+// SCH 0: the schedule above; 1: DEEP (below); 2: EARLY -- the same 2 x 64-pixel slots with each
+// piece issued as soon as its half-slot's WAR margin (2 phases) allows: during step t,
+// q0: step t+1 X[0:32], q1: t+1 dY[32:64], q2: t+1 X[32:64], q3: t+2 dY[0:32]; the RAW waits
+// (q1: this step's second half, q3: the next step's first) then leave 3 pieces in flight
+// (vmcnt(6)), so a piece has 3-5 phases to land instead of 2-3
+template <int FORM, int SCH = 0>
 __global__ void __launch_bounds__(kPpT, 1)
 conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                      float* __restrict__ dW, const WgradGeom g, const TapTableW taps,
                      float invQ, float invP) {
-  constexpr bool DENSE = FORM == 1, DIRECT = FORM == 2;
+  // FORM 3 (timing probe only, wrong results): DENSE with every K-step re-reading the split's
+  // first 64 rows (L2-resident operands)
+  constexpr bool DENSE = FORM == 1 || FORM == 3, DIRECT = FORM == 2;
+  constexpr bool DEEP = SCH == 1, EARLY = SCH == 2;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -556,7 +574,9 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
   const int M = g.N * g.P * g.Q;
   const int ms = split * (int)g.m_per_split;
   const int me = min(ms + (int)g.m_per_split, M);
-  const int nk = (me - ms + kPpBK - 1) / kPpBK;
+  constexpr int BKS = DEEP ? kPpDeepBK : kPpBK;
+  constexpr int STG = DEEP ? kPpDeepStage : kPpStage, IMG = DEEP ? kPpDeepImg : kPpImg;
+  const int nk = (me - ms + BKS - 1) / BKS;
   const int PQ = g.P * g.Q;                 // split-relative descriptors (see conv_wgrad_kernel)
   const int n_lo = ms / PQ, n_hi = max(n_lo, (me - 1) / PQ);
   const long img = (long)g.H * g.W * g.C;
@@ -599,7 +619,7 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
   int dec_pb = 0, dec_hw = 0, dec_live = 0;
   int drow_pb[2][2], drow_hw[2][2];
   auto decode = [&](int kt) {
-    const int mk = ms + kt * kPpBK;
+    const int mk = FORM == 3 ? ms : ms + kt * BKS;
     dec_live = me - mk;
     if (DENSE) return;
     if (DIRECT) {
@@ -629,11 +649,11 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
   };
   // piece pc: 0 = dY rows 0-31, 1 = X rows 0-31, 2 = dY rows 32-63, 3 = X rows 32-63
   auto issue = [&](int kt, int pc) {
-    const int h = pc >> 1;
+    const int h = DEEP ? 0 : pc >> 1;
     const bool isB = pc & 1;
-    const int mk = ms + kt * kPpBK;
-    const uint32_t base = lds0 + (uint32_t)(((kt & 1) * kPpStage + (isB ? kPpImg : 0) +
-                                             h * 32 * kPpW) * 2);
+    const int mk = FORM == 3 ? ms : ms + kt * BKS;
+    const int slot = DEEP ? kt % kPpDeepSlots : kt & 1;
+    const uint32_t base = lds0 + (uint32_t)((slot * STG + (isB ? IMG : 0) + h * 32 * kPpW) * 2);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int R = 32 * h + 2 * (wave + 8 * j) + (lane >> 5);   // pixel row of the K-step
@@ -701,6 +721,55 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
     sync();
   };
 
+  if constexpr (DEEP) {
+#pragma unroll
+    for (int s0 = 0; s0 < 3; ++s0) { decode(s0); issue(s0, 0); issue(s0, 1); }
+    DTF_WAIT_VM(8);                         // step 0 landed (steps 1, 2 in flight)
+    sync();
+    if (wm == 1) sync();                    // the one-barrier stagger
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* sa = lds + (kt % kPpDeepSlots) * STG;
+      const bf16_t* sb = sa + IMG;
+      rdB(sb, 0);
+      rdA(sa, 0, 0);
+      decode(kt + 3);
+      issue(kt + 3, 0);
+      mfma_phase(0);
+      rdA(sa, 0, 1);
+      issue(kt + 3, 1);
+      DTF_WAIT_VM(8);                       // step kt + 1 landed (kt + 2, kt + 3 in flight)
+      mfma_phase(1);
+    }
+  } else if constexpr (EARLY) {
+    decode(0);
+    issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
+    decode(1);
+    issue(1, 0);
+    DTF_WAIT_VM(6);                         // step 0's first half landed
+    sync();
+    if (wm == 1) sync();                    // the one-barrier stagger
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16_t* sa = lds + (kt & 1) * kPpStage;
+      const bf16_t* sb = sa + kPpImg;
+      rdB(sb, 0);
+      rdA(sa, 0, 0);
+      issue(kt + 1, 1);
+      mfma_phase(0);                        // q0
+      rdA(sa, 0, 1);
+      issue(kt + 1, 2);
+      DTF_WAIT_VM(6);                       // this step's second half landed
+      mfma_phase(1);                        // q1
+      rdB(sb, 1);
+      rdA(sa, 1, 0);
+      issue(kt + 1, 3);
+      mfma_phase(0);                        // q2
+      rdA(sa, 1, 1);
+      decode(kt + 2);
+      issue(kt + 2, 0);
+      DTF_WAIT_VM(6);                       // the next step's first half landed
+      mfma_phase(1);                        // q3
+    }
+  } else {
   decode(0);
   issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
   DTF_WAIT_VM(4);                           // step 0's first half landed
@@ -726,6 +795,7 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
     issue(kt + 1, 3);
     DTF_WAIT_VM(4);                         // the next step's first half landed
     mfma_phase(1);                          // q3
+  }
   }
   if (wm == 0) sync();                      // re-align the barrier counts
   DTF_WAIT_VM(0);                           // the trailing no-op pieces still target the slots
@@ -952,6 +1022,13 @@ void dtf_wgrad_set_dense(int v) { g_wgrad_dense = v; }
 // shuffles, -0.5..+3 % on stage-3 layers, -10..-15 % on stage-4 ones;
 // profiles/measurements/r5_wgrad_direct_decode_ab.jsonl)
 static int g_wgrad_direct = 0;
+// ping-pong wgrad schedule: 0 the 2 x 64-pixel double buffer, 1 the DEEP 5-slot ring (see
+// kPpDeepSlots), 2 EARLY piece issue (conv_wgrad_pp_kernel SCH).  A/B knob, default 0: standalone
+// (operands streamed from HBM) EARLY is 9-11 % faster on BERT qkv / ffn1 and DEEP 10-30 % slower;
+// in the network (operands just written, MALL-resident) EARLY is neutral: BERT 1.430-1.433M vs
+// 1.435M tok/s, ResNet-50 +0.3 % (profiles/measurements/r5_wgrad_schedule_ab.jsonl)
+static int g_wgrad_deep = 0;
+void dtf_wgrad_set_deep(int v) { g_wgrad_deep = v; }
 void dtf_wgrad_set_direct(int v) { g_wgrad_direct = v; }
 static bool wgrad_pp(int Kout, int TC) { return g_wgrad_pp && Kout >= 256 && TC >= 256; }
 static int g_wgrad_pipe = 3;
@@ -1067,19 +1144,40 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
   if (dma && wgrad_pp(g.Kout, TC) && g.ldw % 4 == 0) {
     static bool attr = false;
     if (!attr) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<0>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
-      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<1>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
-      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_pp_kernel<2>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
+      for (const void* k : {(const void*)conv_wgrad_pp_kernel<0>,
+                            (const void*)conv_wgrad_pp_kernel<1>,
+                            (const void*)conv_wgrad_pp_kernel<2>,
+                            (const void*)conv_wgrad_pp_kernel<3>,
+                            (const void*)conv_wgrad_pp_kernel<0, 2>,
+                            (const void*)conv_wgrad_pp_kernel<1, 2>,
+                            (const void*)conv_wgrad_pp_kernel<2, 2>,
+                            (const void*)conv_wgrad_pp_kernel<3, 2>})
+        HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPpLDS));
+      for (const void* k : {(const void*)conv_wgrad_pp_kernel<0, 1>,
+                            (const void*)conv_wgrad_pp_kernel<1, 1>,
+                            (const void*)conv_wgrad_pp_kernel<2, 1>,
+                            (const void*)conv_wgrad_pp_kernel<3, 1>})
+        HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kPpDeepLDS));
       attr = true;
     }
     const long ptiles = (long)((g.Kout + 255) / 256) * ((TC + 255) / 256);
-    auto kern = dense1 ? conv_wgrad_pp_kernel<1>
-                      : g_wgrad_direct ? conv_wgrad_pp_kernel<2> : conv_wgrad_pp_kernel<0>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT), kPpLDS, st, X, dY,
-                       target, g, taps, 1.0f / (float)g.Q, 1.0f / (float)g.P);
+    const bool deep = g_wgrad_deep == 1;
+    const int form = dense1 ? (g_wgrad_dense == 3 ? 3 : 1) : g_wgrad_direct ? 2 : 0;
+    using PpKern = void (*)(const bf16_t*, const bf16_t*, float*, const WgradGeom, const TapTableW,
+                            float, float);
+    static const PpKern kerns[3][4] = {
+        {conv_wgrad_pp_kernel<0>, conv_wgrad_pp_kernel<1>, conv_wgrad_pp_kernel<2>,
+         conv_wgrad_pp_kernel<3>},
+        {conv_wgrad_pp_kernel<0, 1>, conv_wgrad_pp_kernel<1, 1>, conv_wgrad_pp_kernel<2, 1>,
+         conv_wgrad_pp_kernel<3, 1>},
+        {conv_wgrad_pp_kernel<0, 2>, conv_wgrad_pp_kernel<1, 2>, conv_wgrad_pp_kernel<2, 2>,
+         conv_wgrad_pp_kernel<3, 2>}};
+    const int sch = g_wgrad_deep >= 0 && g_wgrad_deep <= 2 ? g_wgrad_deep : 0;
+    auto kern = kerns[sch][form];
+    hipLaunchKernelGGL(kern, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT),
+                       deep ? kPpDeepLDS : kPpLDS, st, X, dY, target, g, taps,
+                       1.0f / (float)g.Q, 1.0f / (float)g.P);
   } else if (dma) {
     const float iq = 1.0f / (float)g.Q, ip = 1.0f / (float)g.P;
 #define DTF_WGRAD_LAUNCH(WM_, WN_, BK_, NS_)                                                     \

@@ -381,6 +381,8 @@ def test_halo_conv3x3_matches_implicit_gemm(N, H, C, K):
     assert _rel(outs[0][0], yr) < 1e-2
 
 
+_WGRAD_DEEP_DEFAULT = 0     # csrc/kernels/conv_wgrad.hip g_wgrad_deep
+
 WGRAD_PP_CASES = [
     (2, 14, 14, 256, 256, 3, 1, 1),      # stage-3 3x3
     (2, 7, 7, 512, 512, 3, 1, 1),        # stage-4 3x3
@@ -417,9 +419,17 @@ def test_wgrad_pingpong_kernel(case):
     try:
         nat._K.wgrad_set_direct(1)
         direct = nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad)
+        nat._K.wgrad_set_direct(0)
+        scheds = []
+        for sch in (0, 1, 2):       # double buffer / 5-slot 32-pixel ring / early piece issue
+            nat._K.wgrad_set_deep(sch)
+            scheds.append(nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad))
     finally:
         nat._K.wgrad_set_direct(0)
+        nat._K.wgrad_set_deep(_WGRAD_DEEP_DEFAULT)
     assert torch.equal(pp, direct)
+    for o in scheds:                # same MFMA order in every schedule
+        assert torch.equal(pp, o)
 
 
 WGRAD_DENSE_CASES = [
@@ -444,11 +454,19 @@ def test_wgrad_pingpong_dense_form_bit_identical(case):
     try:
         nat._K.wgrad_set_dense(1)
         dense = nat.conv2d_wgrad(x, dy, (K, 1, 1, C), 1, 0)
+        others = []
+        for sch in (0, 1, 2):
+            nat._K.wgrad_set_deep(sch)
+            others.append(nat.conv2d_wgrad(x, dy, (K, 1, 1, C), 1, 0))
+        nat._K.wgrad_set_deep(_WGRAD_DEEP_DEFAULT)
         nat._K.wgrad_set_dense(0)
         gen = nat.conv2d_wgrad(x, dy, (K, 1, 1, C), 1, 0)
     finally:
         nat._K.wgrad_set_dense(1)
+        nat._K.wgrad_set_deep(_WGRAD_DEEP_DEFAULT)
     assert torch.equal(dense, gen)
+    for o in others:
+        assert torch.equal(dense, o)
     ref = dy.reshape(-1, K).float().t() @ x.reshape(-1, C).float()
     assert _rel(dense.reshape(K, C), ref) < 1e-3
 
