@@ -1074,15 +1074,17 @@ DTF_DEV bf16x8_t lds_tr8_p(const bf16_t* base, int row0, int col0, int lane) {
   return (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// One (b, h) pair's backward from its staged LDS image (Q, K, V, dO rows at pitch ALD, the key
+// mask).  ``orow``: this lane's 16 B of O at columns 8 gq and 32 + 8 gq of its query row
+// (delta = O . dO with dO from the staged image: 2 global loads per lane fewer than re-reading
+// it, 4-8 % off the kernel).  (A persistent form -- one block per CU, the next pair's rows
+// prefetched into registers under the current pair -- measured 1.5x SLOWER: one block per CU
+// leaves the pair's dependent MFMA / exp chain exposed that two co-resident blocks interleave.)
 template <bool DROP>
-__global__ void __launch_bounds__(512, 4)      // 4 waves per SIMD = two 8-wave blocks per CU
-attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
-                         const bf16_t* __restrict__ dO, const float* __restrict__ lse,
-                         float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom g,
-                         const bf16_t* __restrict__ O, float* __restrict__ colpart) {
+DTF_DEV void attn_bwd_pair(bf16_t* fsm, int b, int h, const float* __restrict__ lse,
+                           float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom& g,
+                           const uint4 (&orow)[2], float* __restrict__ colpart) {
   constexpr int S = kFusedS;
-  static_assert(S * kPLD <= 2 * S * ALD, "P / dS must fit over the K|V region");
-  extern __shared__ __attribute__((aligned(16))) bf16_t fsm[];    // kFusedLds bytes (dynamic)
   bf16_t* Qs = fsm;
   bf16_t* Os = Qs + S * ALD;                 // dO
   bf16_t* KV = Os + S * ALD;                 // K | V, then P, then dS
@@ -1093,40 +1095,26 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
   bf16_t* Vs = KV + S * ALD;
   bf16_t* Ps = KV;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = lane >> 4, li = lane & 15;
-  const int h = blockIdx.x, b = blockIdx.y, H = g.H;
+  const int H = g.H;
   const long tok0 = (long)b * S, bh = (long)b * H + h;
-  // ---- stage Q, K, V, dO (4 x 1024 16-B chunks over 512 threads) and the key mask
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int v = tid + 512 * i;
-    const int sel = v >> 10, row = (v >> 3) & (S - 1), cc = (v & 7) * 8;
-    const bf16_t* src = sel == 3 ? dO + (tok0 + row) * (long)(H * AD) + h * AD + cc
-                                 : qkv + (tok0 + row) * g.ld + (sel * H + h) * AD + cc;
-    bf16_t* dst = (sel == 0 ? Qs : sel == 1 ? Ks : sel == 2 ? Vs : Os) + row * ALD + cc;
-    *(uint4*)dst = *(const uint4*)src;
-  }
-  if (tid < S) Ms[tid] = mask ? mask[tok0 + tid] * kLog2e : 0.f;
-  // ---- this lane's query q: lse and delta = O . dO (global reads, as the dQ kernel)
+  // ---- this lane's query q: lse and delta = O . dO (dO from the staged image: the same bits)
   const int q = w * 16 + li;
   const float lq = lse[bh * S + q];
   float dl = 0.f;
   {
-    const bf16_t* oq = O + (tok0 + q) * (long)(H * AD) + h * AD;
-    const bf16_t* dq_ = dO + (tok0 + q) * (long)(H * AD) + h * AD;
     float fo[8], fd[8];
-    unpack8(*(const uint4*)(oq + 8 * gq), fo);
-    unpack8(*(const uint4*)(dq_ + 8 * gq), fd);
+    unpack8(orow[0], fo);
+    unpack8(*(const uint4*)(Os + q * ALD + 8 * gq), fd);
 #pragma unroll
     for (int e = 0; e < 8; ++e) dl += fo[e] * fd[e];
-    unpack8(*(const uint4*)(oq + 32 + 8 * gq), fo);
-    unpack8(*(const uint4*)(dq_ + 32 + 8 * gq), fd);
+    unpack8(orow[1], fo);
+    unpack8(*(const uint4*)(Os + q * ALD + 32 + 8 * gq), fd);
 #pragma unroll
     for (int e = 0; e < 8; ++e) dl += fo[e] * fd[e];
     dl += __shfl_xor(dl, 16, 64);
     dl += __shfl_xor(dl, 32, 64);
     if (gq == 0) delta[bh * S + q] = dl;
   }
-  __syncthreads();
   // ---- phase 1: this wave's 16 queries against all 128 keys
   const bf16x8_t bq0 = lds_row8(Qs, q, 8 * gq), bq1 = lds_row8(Qs, q, 32 + 8 * gq);
   const bf16x8_t bo0 = lds_row8(Os, q, 8 * gq), bo1 = lds_row8(Os, q, 32 + 8 * gq);
@@ -1252,6 +1240,59 @@ attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict
       colpart[(long)b * g.ld + (sec * H + h) * AD + col] = t;
     }
   }
+}
+
+// the pair's Q, K, V, dO rows (4 x 1024 16-B chunks over 512 threads): global -> registers ...
+DTF_DEV void attn_bwd_pair_load(uint4 (&v)[8], float& mk, uint4 (&orow)[2], const bf16_t* qkv,
+                                const float* mask, const bf16_t* dO, const bf16_t* O,
+                                const AttnGeom& g, int b, int h) {
+  constexpr int S = kFusedS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, gq = lane >> 4, li = lane & 15;
+  const int H = g.H;
+  const long tok0 = (long)b * S;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = tid + 512 * i;
+    const int sel = c >> 10, row = (c >> 3) & (S - 1), cc = (c & 7) * 8;
+    const bf16_t* src = sel == 3 ? dO + (tok0 + row) * (long)(H * AD) + h * AD + cc
+                                 : qkv + (tok0 + row) * g.ld + (sel * H + h) * AD + cc;
+    v[i] = *(const uint4*)src;
+  }
+  mk = (tid < S && mask) ? mask[tok0 + tid] * kLog2e : 0.f;
+  const int q = w * 16 + li;
+  const bf16_t* oq = O + (tok0 + q) * (long)(H * AD) + h * AD;
+  orow[0] = *(const uint4*)(oq + 8 * gq);
+  orow[1] = *(const uint4*)(oq + 32 + 8 * gq);
+}
+// ... -> the LDS image
+DTF_DEV void attn_bwd_pair_store(bf16_t* fsm, const uint4 (&v)[8], float mk) {
+  constexpr int S = kFusedS;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = tid + 512 * i;
+    const int sel = c >> 10, row = (c >> 3) & (S - 1), cc = (c & 7) * 8;
+    const int slot = sel == 0 ? 0 : sel == 3 ? 1 : sel + 1;       // image order Q | dO | K | V
+    *(uint4*)(fsm + slot * S * ALD + row * ALD + cc) = v[i];
+  }
+  if (tid < S) reinterpret_cast<float*>(fsm + 4 * S * ALD)[tid] = mk;
+}
+
+template <bool DROP>
+__global__ void __launch_bounds__(512, 4)      // 4 waves per SIMD = two 8-wave blocks per CU
+attn_bwd_fused128_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                         const bf16_t* __restrict__ dO, const float* __restrict__ lse,
+                         float* __restrict__ delta, bf16_t* __restrict__ dqkv, const AttnGeom g,
+                         const bf16_t* __restrict__ O, float* __restrict__ colpart) {
+  static_assert(kFusedS * kPLD <= 2 * kFusedS * ALD, "P / dS must fit over the K|V region");
+  extern __shared__ __attribute__((aligned(16))) bf16_t fsm[];    // kFusedLds bytes (dynamic)
+  const int h = blockIdx.x, b = blockIdx.y;
+  uint4 v[8], orow[2];
+  float mk;
+  attn_bwd_pair_load(v, mk, orow, qkv, mask, dO, O, g, b, h);
+  attn_bwd_pair_store(fsm, v, mk);
+  __syncthreads();
+  attn_bwd_pair<DROP>(fsm, b, h, lse, delta, dqkv, g, orow, colpart);
 }
 
 // ----------------------------------------------------------------------------- embeddings
