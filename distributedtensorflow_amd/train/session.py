@@ -490,7 +490,22 @@ class MonitoredTrainingSession:
                 attempts += 1
                 if attempts > self.max_recovery_attempts:
                     raise
-                self._recover(e)
+                # a recovery that itself hits a recoverable failure (the restarted task not up
+                # yet, a peer dying mid-rejoin) is retried within the same attempt budget
+                while True:
+                    try:
+                        self._recover(e)
+                        break
+                    except Exception as e2:      # noqa: BLE001
+                        # a TimeoutError already waited out the recovery budget: not retried
+                        if isinstance(e2, TimeoutError) or not _recoverable(e2):
+                            raise
+                        attempts += 1
+                        if attempts > self.max_recovery_attempts:
+                            raise
+                        print(f"[dtf] recovery failed ({type(e2).__name__}: {e2}); retrying "
+                              f"({attempts}/{self.max_recovery_attempts})", flush=True)
+                        e = e2
         if ctx.stop_requested:
             self._should_stop = True
         return results
@@ -511,7 +526,7 @@ class MonitoredTrainingSession:
                 opt = self.scaffold.optimizer
                 if opt is not None and getattr(opt, "space", None) is not None:
                     opt.synchronize_variables()     # the pipelined push in flight is answered
-                client.stop()
+                _stop_client(client)
             if self._writer is not None:
                 self._writer.close()
 
@@ -525,8 +540,21 @@ class MonitoredTrainingSession:
         self._closed = True
         client = getattr(self.strategy, "ps_client", None)
         if client is not None and client.params is not None:
-            client.stop()
+            # best effort: the failure being propagated may be the group itself (a recovery
+            # that tore it down and could not re-form it) -- never mask it with the stop's error
+            try:
+                _stop_client(client)
+            except Exception as e:      # noqa: BLE001
+                print(f"[dtf] PS client stop after {exc_type.__name__} failed: {e!r}", flush=True)
         return False
+
+
+def _stop_client(client):
+    """Tell the parameter servers this worker is done -- only over a live process group (after
+    a failed recovery the group may be torn down; there is nobody to tell then)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        client.stop()
 
 
 class Supervisor:

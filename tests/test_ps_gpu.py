@@ -59,6 +59,20 @@ def test_sync_replicas_ps_hbm_shard_ipc(tmp_path):
     assert stats["applied"] == stats["global_step"] >= 30
 
 
+def _failure_report(codes, text):
+    """Exit codes, then per task its FIRST traceback (the primary failure: a later one may only
+    be a consequence) and its log tail -- also printed, since pytest truncates long messages."""
+    parts = [f"exit codes: {codes}"]
+    for k, t in text.items():
+        i = t.find("Traceback")
+        first = t[i:i + 3000] if i >= 0 else "(no traceback)"
+        parts.append(f"===== {k}: first traceback =====\n{first}\n===== {k}: tail =====\n"
+                     f"{t[-2000:]}")
+    rep = "\n".join(parts)
+    print(rep)
+    return rep
+
+
 @pytest.mark.parametrize("pipeline", ["0", "1"], ids=["serial", "pipelined"])
 def test_ps_killed_on_gpu_restarts_and_resumes(tmp_path, pipeline):
     """The recovery path on the HBM data plane: the PS dies holding its exported HBM shard,
@@ -80,7 +94,7 @@ def test_ps_killed_on_gpu_restarts_and_resumes(tmp_path, pipeline):
                                     "DTF_RECOVERY_TIMEOUT_S": "45", "DTF_PS_TIMEOUT_S": "45"},
                                timeout_s=150, grace_s=20, max_ps_restarts=1)
     text = {k: open(v).read() for k, v in logs.items()}
-    assert all(c == 0 for c in codes.values()), {k: t[-2500:] for k, t in text.items()}
+    assert all(c == 0 for c in codes.values()), _failure_report(codes, text)
     assert "restarting (1/1)" in text["ps0"]
     assert all("recovered: generation 1" in text[w] for w in ("worker0", "worker1"))
     m = re.search(r"Close Parameter Server \.\.\. (\{.*\})", text["ps0"])

@@ -130,6 +130,49 @@ def test_fault_injection_recovers_from_checkpoint(tmp_path):
     assert steps[:4] == [1, 2, 3, 4] and steps[4] == 5 and gstep.value() == 8
 
 
+def test_failed_recovery_is_retried_within_the_attempt_budget(tmp_path):
+    """A recovery that itself hits a recoverable failure (the restarted task not up yet) is
+    retried within max_recovery_attempts instead of escaping run()."""
+    from distributedtensorflow_amd.train.session import InjectedFault
+    ck = str(tmp_path / "ck")
+    strat, model, opt, gstep, train_op = _setup()
+    fault = FaultInjectionHook("0:5", rank=0)
+    with MonitoredTrainingSession(checkpoint_dir=ck,
+                                  hooks=[StopAtStepHook(last_step=8), fault],
+                                  save_checkpoint_steps=2, save_summaries_steps=None,
+                                  log_step_count_steps=None, model=model, optimizer=opt,
+                                  global_step=gstep, strategy=strat) as sess:
+        real, calls = sess._recover, []
+
+        def flaky(exc=None):
+            calls.append(type(exc).__name__)
+            if len(calls) == 1:
+                raise InjectedFault("recovery interrupted")
+            return real(exc)
+        sess._recover = flaky
+        while not sess.should_stop():
+            sess.run(train_op)
+    assert fault.fired and len(calls) == 2 and gstep.value() == 8
+
+
+def test_exit_never_masks_the_failure_with_the_ps_stop():
+    """__exit__ on an exception: the PS client's stop is best effort (after a failed recovery
+    the process group may be gone) -- the original exception propagates."""
+    strat, model, opt, gstep, train_op = _setup()
+
+    class _Client:
+        params = [1]
+
+        def stop(self):
+            raise ValueError("Default process group has not been initialized")
+    with pytest.raises(RuntimeError, match="primary"):
+        with MonitoredTrainingSession(model=model, optimizer=opt, global_step=gstep,
+                                      strategy=strat, save_summaries_steps=None,
+                                      log_step_count_steps=None) as sess:
+            sess.strategy.ps_client = _Client()
+            raise RuntimeError("primary failure")
+
+
 def test_nan_and_logging_hooks(tmp_path, capsys):
     strat, model, opt, gstep, train_op = _setup()
     hook = LoggingTensorHook(["loss"], every_n_iter=1)
