@@ -545,7 +545,10 @@ static_assert(kPpDeepLDS <= 160 * 1024 && kPpDeepLDS >= (size_t)128 * kPpLDO * 4
 // DENSE: a 1x1 / stride-1 / unpadded conv or a dense layer (one tap at (0, 0), P = H, Q = W):
 // pixel m IS row m of X, so the B pieces are addressed like the A pieces -- no per-step pixel
 // decode and no cross-lane shuffles (two ds_bpermute per B DMA instruction) in the main loop
-// FORM 0: lane-per-pixel decode shuffled to the DMA rows; 1: DENSE; 2: DIRECT per-row decode
+// FORM 0: lane-per-pixel decode shuffled to the DMA rows; 1: DENSE; 2: DIRECT per-row decode;
+// 4: the lane-per-pixel decode moved to the DMA rows by v_readlane (a DMA instruction's 64 lanes
+// fetch only two pixel rows, 2 (wave + 8 j) + {0, 1}: two wave-uniform reads and a select
+// instead of a ds_bpermute through the LDS pipe per value)
 // SCH 0: the schedule above; 1: DEEP (below); 2: EARLY -- the same 2 x 64-pixel slots with each
 // piece issued as soon as its half-slot's WAR margin (2 phases) allows: during step t,
 // q0: step t+1 X[0:32], q1: t+1 dY[32:64], q2: t+1 X[32:64], q3: t+2 dY[0:32]; the RAW waits
@@ -558,7 +561,7 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
                      float invQ, float invP) {
   // FORM 3 (timing probe only, wrong results): DENSE with every K-step re-reading the split's
   // first 64 rows (L2-resident operands)
-  constexpr bool DENSE = FORM == 1 || FORM == 3, DIRECT = FORM == 2;
+  constexpr bool DENSE = FORM == 1 || FORM == 3, DIRECT = FORM == 2, READL = FORM == 4;
   constexpr bool DEEP = SCH == 1, EARLY = SCH == 2;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -667,8 +670,22 @@ conv_wgrad_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY
                                  ? (uint32_t)(mk - ms + R) * g.C * 2u + (uint32_t)b_toff[j] : kOOB;
         dma16(rx, dst, off);
       } else {
-        const int hwr = DIRECT ? drow_hw[h][j] : __shfl(dec_hw, R, 64);
-        const int pbr = DIRECT ? drow_pb[h][j] : __shfl(dec_pb, R, 64);
+        int hwr, pbr;
+        if constexpr (DIRECT) {
+          hwr = drow_hw[h][j];
+          pbr = drow_pb[h][j];
+        } else if constexpr (READL) {
+          const int R0 = 32 * h + 2 * (wave + 8 * j);            // wave-uniform
+          const int hw0 = __builtin_amdgcn_readlane(dec_hw, R0);
+          const int hw1 = __builtin_amdgcn_readlane(dec_hw, R0 + 1);
+          const int pb0 = __builtin_amdgcn_readlane(dec_pb, R0);
+          const int pb1 = __builtin_amdgcn_readlane(dec_pb, R0 + 1);
+          hwr = (lane >> 5) ? hw1 : hw0;
+          pbr = (lane >> 5) ? pb1 : pb0;
+        } else {
+          hwr = __shfl(dec_hw, R, 64);
+          pbr = __shfl(dec_pb, R, 64);
+        }
         const int hh = (hwr >> 16) + b_dh[j], ww = (hwr & 0xFFFF) + b_dw[j];
         const bool ok = (unsigned)hh < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
         dma16(rx, dst, ok ? (uint32_t)(pbr + b_toff[j]) : kOOB);
@@ -1017,10 +1034,11 @@ void dtf_wgrad_set_pp(int v) {
 // ping-pong kernel: the DENSE form (no pixel decode) for one-tap unit-stride unpadded layers
 static int g_wgrad_dense = 1;
 void dtf_wgrad_set_dense(int v) { g_wgrad_dense = v; }
-// multi-tap / strided layers: each lane decodes the pixel rows it fetches instead of shuffling
-// one lane-per-pixel decode (A/B knob, off: the 4 decodes per lane cost more VALU than the
-// shuffles, -0.5..+3 % on stage-3 layers, -10..-15 % on stage-4 ones;
-// profiles/measurements/r5_wgrad_direct_decode_ab.jsonl)
+// multi-tap / strided layers' pixel decode (A/B knob): 0 lane-per-pixel decode shuffled to the
+// DMA rows; 1 each lane decodes the rows it fetches (-0.5..+3 % on stage-3 layers, -10..-15 % on
+// stage-4 ones: r5_wgrad_direct_decode_ab.jsonl); 2 the shuffles replaced by v_readlane (15 %
+// faster on the stage-3 3x3 layers standalone, -6..+2 % on stage 4, the network -0.2 %:
+// r5_wgrad_readlane_decode_ab.jsonl)
 static int g_wgrad_direct = 0;
 // ping-pong wgrad schedule: 0 the 2 x 64-pixel double buffer, 1 the DEEP 5-slot ring (see
 // kPpDeepSlots), 2 EARLY piece issue (conv_wgrad_pp_kernel SCH).  A/B knob, default 0: standalone
@@ -1148,6 +1166,7 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
                             (const void*)conv_wgrad_pp_kernel<1>,
                             (const void*)conv_wgrad_pp_kernel<2>,
                             (const void*)conv_wgrad_pp_kernel<3>,
+                            (const void*)conv_wgrad_pp_kernel<4>,
                             (const void*)conv_wgrad_pp_kernel<0, 2>,
                             (const void*)conv_wgrad_pp_kernel<1, 2>,
                             (const void*)conv_wgrad_pp_kernel<2, 2>,
@@ -1163,7 +1182,8 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
     }
     const long ptiles = (long)((g.Kout + 255) / 256) * ((TC + 255) / 256);
     const bool deep = g_wgrad_deep == 1;
-    const int form = dense1 ? (g_wgrad_dense == 3 ? 3 : 1) : g_wgrad_direct ? 2 : 0;
+    const int form = dense1 ? (g_wgrad_dense == 3 ? 3 : 1)
+                            : g_wgrad_direct == 1 ? 2 : g_wgrad_direct == 2 ? 4 : 0;
     using PpKern = void (*)(const bf16_t*, const bf16_t*, float*, const WgradGeom, const TapTableW,
                             float, float);
     static const PpKern kerns[3][4] = {
@@ -1174,7 +1194,7 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
         {conv_wgrad_pp_kernel<0, 2>, conv_wgrad_pp_kernel<1, 2>, conv_wgrad_pp_kernel<2, 2>,
          conv_wgrad_pp_kernel<3, 2>}};
     const int sch = g_wgrad_deep >= 0 && g_wgrad_deep <= 2 ? g_wgrad_deep : 0;
-    auto kern = kerns[sch][form];
+    auto kern = form == 4 ? conv_wgrad_pp_kernel<4> : kerns[sch][form];
     hipLaunchKernelGGL(kern, dim3((unsigned)(ptiles * nsplit)), dim3(kPpT),
                        deep ? kPpDeepLDS : kPpLDS, st, X, dY, target, g, taps,
                        1.0f / (float)g.Q, 1.0f / (float)g.P);

@@ -419,6 +419,8 @@ def test_wgrad_pingpong_kernel(case):
     try:
         nat._K.wgrad_set_direct(1)
         direct = nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad)
+        nat._K.wgrad_set_direct(2)        # the decode moved to the DMA rows by v_readlane
+        readl = nat.conv2d_wgrad(x, dy, (K, R, R, C), stride, pad)
         nat._K.wgrad_set_direct(0)
         scheds = []
         for sch in (0, 1, 2):       # double buffer / 5-slot 32-pixel ring / early piece issue
@@ -428,6 +430,7 @@ def test_wgrad_pingpong_kernel(case):
         nat._K.wgrad_set_direct(0)
         nat._K.wgrad_set_deep(_WGRAD_DEEP_DEFAULT)
     assert torch.equal(pp, direct)
+    assert torch.equal(pp, readl)
     for o in scheds:                # same MFMA order in every schedule
         assert torch.equal(pp, o)
 

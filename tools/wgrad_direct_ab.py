@@ -42,7 +42,7 @@ def main():
         dy = (torch.randn(B, P, Q, K, device="cuda", generator=g) / (B * P * Q) ** 0.5).bfloat16()
         dw = torch.zeros(K, R, R, C, device="cuda")
         res = {}
-        for mode in (0, 1):
+        for mode in (0, 1, 2):
             native._K.wgrad_set_direct(mode)
             res[mode] = timeit(lambda: native.conv2d_wgrad(x, dy, (K, R, R, C), st, pad, out=dw))
             res[f"w{mode}"] = native.conv2d_wgrad(x, dy, (K, R, R, C), st, pad).clone()
@@ -51,7 +51,10 @@ def main():
         rec = {"layer": name, "batch": B, "shuffle_us": round(res[0], 1),
                "direct_us": round(res[1], 1), "direct_tflops": round(fl / res[1] / 1e6, 1),
                "shuffle_tflops": round(fl / res[0] / 1e6, 1),
-               "bit_identical": bool(torch.equal(res["w0"], res["w1"]))}
+               "readlane_us": round(res[2], 1),
+               "readlane_tflops": round(fl / res[2] / 1e6, 1),
+               "bit_identical": bool(torch.equal(res["w0"], res["w1"]) and
+                                     torch.equal(res["w0"], res["w2"]))}
         print(json.dumps(rec), flush=True)
         if out:
             out.write(json.dumps(rec) + "\n")
