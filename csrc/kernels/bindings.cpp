@@ -93,6 +93,7 @@ void dtf_bn_relu_maxpool_fwd(const bf16_t*, const float*, const float*, bf16_t*,
                              int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void dtf_pool_set_blocked(int);
 int dtf_pool_bn_bwd_blocks(int, int, int, int);
+void dtf_pool_bn_bwd_set_caps(int, int);
 void dtf_pool_bn_bwd_reduce(const bf16_t*, const uint8_t*, const bf16_t*, const float*,
                             const float*, const float*, const float*, float*, int, int, int, int,
                             int, int, hipStream_t);
@@ -599,6 +600,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("pool_set_blocked", &dtf_pool_set_blocked);
   m.def("pool_bn_bwd_blocks", &dtf_pool_bn_bwd_blocks);
+  m.def("pool_bn_bwd_set_caps", &dtf_pool_bn_bwd_set_caps);
   m.def("pool_bn_bwd_reduce", [](uintptr_t dy, uintptr_t arg, uintptr_t x, uintptr_t mean,
                                  uintptr_t invstd, uintptr_t fsc, uintptr_t fsh, uintptr_t part,
                                  int N, int H, int W, int C, int P_, int Q, uintptr_t st) {

@@ -566,10 +566,18 @@ void dtf_bn_relu_maxpool_fwd(const bf16_t* x, const float* scale, const float* s
                        st, x, scale, shift, y, arg, N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw);
 }
 
+// grid caps of the stem pool + BN backward passes (reduce, apply): the reduce at 1024 blocks
+// left a third of a round (147 VGPRs: 3 blocks per CU) -- 996 -> 921 us at 4096 on the b1984 stem
+// (profiles/measurements/r5_pool_bwd_grid_probe.jsonl)
+static int g_pool_bwd_cap[2] = {4096, 4096};
+void dtf_pool_bn_bwd_set_caps(int reduce_cap, int apply_cap) {
+  if (reduce_cap > 0) g_pool_bwd_cap[0] = reduce_cap;
+  if (apply_cap > 0) g_pool_bwd_cap[1] = apply_cap;
+}
 int dtf_pool_bn_bwd_blocks(int N, int H, int W, int C) {
   const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
   long g = (total + kT - 1) / kT;
-  if (g > 1024) g = 1024;
+  if (g > g_pool_bwd_cap[0]) g = g_pool_bwd_cap[0];
   return (int)(g < 1 ? 1 : g);
 }
 
@@ -595,6 +603,8 @@ void dtf_pool_bn_bwd_apply(const bf16_t* dy, const uint8_t* arg, const bf16_t* x
                            bf16_t* dx, int N, int H, int W, int C, int P, int Q, hipStream_t st) {
   pool_bn_check(N, H, W, C, P, Q);
   const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
-  hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<true>, dim3(grid_for(total)), dim3(kT), 0, st, dy, arg,
+  long ga = (total + kT - 1) / kT;
+  if (ga > g_pool_bwd_cap[1]) ga = g_pool_bwd_cap[1];
+  hipLaunchKernelGGL(pool3s2_bn_bwd_kernel<true>, dim3((unsigned)(ga < 1 ? 1 : ga)), dim3(kT), 0, st, dy, arg,
                      x, cA, cB, cC, fsc, fsh, dx, nullptr, N, H, W, C, P, Q);
 }
