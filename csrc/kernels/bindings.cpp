@@ -26,6 +26,9 @@ struct ConvGeom {
   const float* bias;
   int relu;
   int nt;
+  const float* lsc;
+  const float* lsh;
+  bf16_t* ly;
 };
 struct BnBwdEpi {
   const bf16_t* x; const float* mean; const float* invstd; const float* fsc; const float* fsh;
@@ -54,6 +57,7 @@ long dtf_bn_workspace_floats_g(int, int);
 int dtf_conv_stats_rows(long, int, int, int, int);
 void dtf_conv_set_halo(int);
 int dtf_conv_tile_rows(const ConvGeom&, const TapTable&, int bnb);
+bool dtf_conv_bnl_ok(const ConvGeom&, const TapTable&);
 void dtf_conv_set_halo_bnb(int);
 void dtf_conv_set_dma_mode(int);
 void dtf_conv_set_small_k(int);
@@ -675,7 +679,8 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("conv_igemm", [](uintptr_t x, uintptr_t w, uintptr_t y, std::vector<int> geom,
                          std::vector<int> dh, std::vector<int> dw, int bk, uintptr_t st,
                          uintptr_t stats, std::vector<uintptr_t> bnb, uintptr_t acc_src,
-                         uintptr_t acc_mask, uintptr_t bias, int relu) {
+                         uintptr_t acc_mask, uintptr_t bias, int relu, uintptr_t bnl_sc,
+                         uintptr_t bnl_sh, uintptr_t bnl_y) {
     if (geom.size() != 16 && geom.size() != 17)
       throw std::runtime_error("conv_igemm: geom needs 16 (+acc) ints");
     ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
@@ -684,6 +689,9 @@ PYBIND11_MODULE(_dtf_hip, m) {
                P<const uint8_t>(acc_mask), P<const float>(bias), relu};
     if (g.acc == 2 && (!g.acc_src || !g.acc_mask))
       throw std::runtime_error("conv_igemm: acc 2 needs acc_src and acc_mask");
+    g.lsc = P<const float>(bnl_sc);
+    g.lsh = P<const float>(bnl_sh);
+    g.ly = P<bf16_t>(bnl_y);
     // bnb = [x, mean, invstd, fsc, fsh, mask, part, mkind, row0] (fused BN-backward sums) or []
     BnBwdEpi e{};
     if (!bnb.empty()) {
@@ -698,7 +706,16 @@ PYBIND11_MODULE(_dtf_hip, m) {
   }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("dh"), py::arg("dw"),
      py::arg("bk"), py::arg("stream"), py::arg("stats") = 0,
      py::arg("bnb") = std::vector<uintptr_t>{}, py::arg("acc_src") = 0, py::arg("acc_mask") = 0,
-     py::arg("bias") = 0, py::arg("relu") = 0);
+     py::arg("bias") = 0, py::arg("relu") = 0, py::arg("bnl_sc") = 0, py::arg("bnl_sh") = 0,
+     py::arg("bnl_y") = 0);
+  m.def("conv_bnl_ok", [](std::vector<int> geom, std::vector<int> dh, std::vector<int> dw) {
+    if (geom.size() != 16 && geom.size() != 17)
+      throw std::runtime_error("conv_bnl_ok: geom needs 16 (+acc) ints");
+    ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
+               geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15],
+               geom.size() == 17 ? geom[16] : 0};
+    return dtf_conv_bnl_ok(g, make_taps<TapTable>(dh, dw));
+  });
   m.def("bn_bwd_finalize_g", [](uintptr_t part, int G, long M, int C, uintptr_t gamma,
                                 uintptr_t mean, uintptr_t invstd, uintptr_t dg, uintptr_t db,
                                 uintptr_t a, uintptr_t b, uintptr_t c, int accumulate,

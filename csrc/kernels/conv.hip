@@ -60,6 +60,12 @@ struct ConvGeom {
   const float* bias;        // fused epilogue (register kernel only): Y = act(conv + bias[k])
   int relu;                 //   tf.layers.conv2d(activation=tf.nn.relu) -- MNIST K3/K5
   int nt;                   // non-temporal output stores (set by dtf_conv_igemm)
+  // BN + ReLU on load (halo kernels, forward): X is a BatchNorm INPUT; the kernel normalises its
+  // patch in LDS with y = bf16(max(x * lsc[c] + lsh[c], 0)) -- the apply pass's arithmetic -- and
+  // writes the rows it owns to ly (the weight gradient's operand), so the apply pass never runs
+  const float* lsc;
+  const float* lsh;
+  bf16_t* ly;
 };
 
 // Residual-gradient accumulation in the dgrad epilogue.  acc 1 reads the materialised residual
@@ -847,12 +853,13 @@ DTF_DEV int halo_swz(int u) { return C == 64 ? (((u >> 1) & 3) << 1) : ((u & 7) 
 // NSTG: filter-slice ring depth (LDS stages; the slice of step s + NSTG - 1 is issued at step s,
 // so a slice has NSTG - 1 steps of MFMA work to arrive from L2; 2 = the original double buffer)
 template <int C, int W, int WMW, int NT, int ST = 1, bool FREG = false, bool BNB = false,
-          int NSTG = 2>
+          int NSTG = 2, bool BNL = false>
 __global__ void __launch_bounds__(kThreads * ST, ST == 1 ? 2 : 1)
 conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                     bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
                     float* __restrict__ stats, const BnBwdEpi bnb) {
   using H = HaloCfg<C, W, WMW, NT>;
+  static_assert(!BNL || (!FREG && ST == 1 && !BNB), "BN on load: the forward ring kernel");
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   const int tid = threadIdx.x & (kThreads - 1), lane = tid & 63;   // tid within the strip
   const int wall = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -1015,6 +1022,36 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     else if constexpr (kYoung == 6) DTF_WAIT_VM(6);
     else DTF_WAIT_VM(8);
     __syncthreads();           // ... everyone's; everyone done reading the slot restaged next
+    if constexpr (BNL) {
+      if (step == 0) {
+        // BN + ReLU of the landed patch, in place (padding pixels stay zero); the rows this block
+        // owns (input rows h0 .. h0 + TH - 1, every pixel exactly once over the grid) go to ly
+        constexpr int CPP = H::ROWB / 16;
+        for (int idx = tid; idx < H::PIX * CPP; idx += kThreads) {
+          const int pix = idx / CPP, slot = idx - pix * CPP;
+          const int pr = pix / H::PW, pc = pix - pr * H::PW;
+          const int h = h0 - 1 + pr, w = pc - 1;
+          if (!live || (unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) continue;
+          const int lch = slot ^ halo_swz<C>(pr * W + pc);      // logical chunk in this slot
+          uint4* pp = reinterpret_cast<uint4*>(patch + pix * C + slot * 8);
+          const float4 s0 = *reinterpret_cast<const float4*>(g.lsc + lch * 8);
+          const float4 s1 = *reinterpret_cast<const float4*>(g.lsc + lch * 8 + 4);
+          const float4 t0 = *reinterpret_cast<const float4*>(g.lsh + lch * 8);
+          const float4 t1 = *reinterpret_cast<const float4*>(g.lsh + lch * 8 + 4);
+          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float sf[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+          float v[8];
+          unpack8(*pp, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(__builtin_fmaf(v[e], sc[e], sf[e]), 0.f);
+          const uint4 pk = pack8(v);
+          *pp = pk;
+          if (pr >= 1 && pr <= kHaloTH)
+            *reinterpret_cast<uint4*>(g.ly + (((long)n * g.H + h) * g.W + w) * C + lch * 8) = pk;
+        }
+        __syncthreads();
+      }
+    }
     // past the last step: out-of-range, no traffic
     issue_w(step + NSTG - 1, (step + NSTG - 1) % NSTG);
     const int t = step / H::KS, s = step - t * H::KS;
@@ -1311,6 +1348,20 @@ static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const Conv
   using Hc = HaloCfg<C, W, WMW, NT>;
   const int nstg = (g_halo_stages >> (C == 64 ? 0 : 4)) & 15;
   const bool freg_on = (g_halo_freg & (C == 64 ? 1 : 2)) != 0;
+  if (g.ly) {
+    if (bnb.part || freg_on || nstg == 3 || nstg == 4 || strips != 1)
+      throw std::runtime_error("halo conv: BN on load needs the default forward ring kernel");
+    auto kern = conv3x3_halo_kernel<C, W, WMW, NT, 1, false, false, 2, true>;
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)Hc::lds(1)));
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles, g.Kout / NT), dim3(kThreads), Hc::lds(1), st,
+                       X, Wt, Y, g, taps, stats, bnb);
+    return;
+  }
   if (!freg_on && (nstg == 3 || nstg == 4)) {
     if (bnb.part) {
       constexpr size_t scratch =
@@ -1430,6 +1481,15 @@ int dtf_conv_tile_rows(const ConvGeom& g, const TapTable& taps, int bnb) {
 static int g_conv_nt = 0;   // measured neutral on ResNet-50 b2048 (DTF_STORE_NT A/B)
 void dtf_conv_set_nt(int v) { g_conv_nt = v; }
 
+// the forward conv can take its input through a BatchNorm + ReLU on load (halo kernels, the
+// default forward ring configuration of the family)
+bool dtf_conv_bnl_ok(const ConvGeom& g, const TapTable& taps) {
+  const int fam = halo_family(g, taps);
+  if (!fam || (g_halo_freg & fam) || (g_halo_st & fam)) return false;
+  const int nstg = (g_halo_stages >> (fam == 1 ? 0 : 4)) & 15;
+  return nstg != 3 && nstg != 4;
+}
+
 void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g_in,
                     const TapTable& taps, int bk, float* stats, const BnBwdEpi& bnb,
                     hipStream_t st) {
@@ -1452,6 +1512,16 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
   const bool epi = g.bias || g.relu;       // fused bias / ReLU: register kernel only
   if (epi && (bnb.part || g.acc))
     throw std::runtime_error("conv: fused bias/ReLU epilogue excludes BN / accumulate epilogues");
+  if (g.ly) {                              // BN + ReLU on load: the halo forward kernel only
+    if (!dtf_conv_bnl_ok(g, taps) || !g.lsc || !g.lsh || bnb.part || epi)
+      throw std::runtime_error("conv: BN on load needs a halo-family forward conv");
+    const int tiles = g.N * (g.H / kHaloTH);
+    if (halo_family(g, taps) == 1)
+      launch_halo<64, 56, 2, 64>(X, Wt, Y, g, taps, stats, bnb, tiles, 1, st);
+    else
+      launch_halo<128, 28, 1, 128>(X, Wt, Y, g, taps, stats, bnb, tiles, 1, st);
+    return;
+  }
   if (!bnb.part && use_stem_halo(g, taps)) {
     using Sc = StemCfg<112>;
     static bool attr = false;

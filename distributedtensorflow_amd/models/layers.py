@@ -170,10 +170,10 @@ class BatchNormalization(Layer):
         _tag(self.moving_variance, f"{self.name}/moving_variance")
         return out
 
-    def forward(self, x, relu=False, residual=None, residual_to_conv=False):
+    def forward(self, x, relu=False, residual=None, residual_to_conv=False, defer=False):
         return ops.batch_norm(x, self.gamma, self.beta, self.moving_mean, self.moving_variance,
                               self.training, self.momentum, self.epsilon, relu, residual,
-                              residual_to_conv)
+                              residual_to_conv, defer)
 
 
 class MaxPooling2D(Layer):

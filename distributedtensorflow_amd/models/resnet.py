@@ -27,10 +27,14 @@ class ConvBN(nn.Module):
         self.bn = BatchNormalization(cout, bn_momentum, bn_eps, name=f"{name}_bn",
                                      gamma_init=0.0 if zero_gamma else 1.0)
 
-    def forward(self, x, relu=True, residual=None, residual_to_conv=False, grad_share=None):
+    def forward(self, x, relu=True, residual=None, residual_to_conv=False, grad_share=None,
+                defer_bn=False):
+        """``defer_bn``: the output only feeds a 3x3 conv that may apply this BN + ReLU on its
+        input load (ops.batch_norm(defer=True))."""
         y = ops.conv2d(x, self.conv.kernel, self.conv.strides, self.conv.padding,
                        bn_stats=self.bn.training, grad_share=grad_share)
-        return self.bn(y, relu=relu, residual=residual, residual_to_conv=residual_to_conv)
+        return self.bn(y, relu=relu, residual=residual, residual_to_conv=residual_to_conv,
+                       defer=defer_bn)
 
 
 class StemConvBN(ConvBN):
@@ -75,6 +79,10 @@ FUSE_BN_CONV = os.environ.get("DTF_FUSE_BN_CONV", "1") == "1"
 # projection's output, +1.8 ms, and the stride-2 projection's dgrad must zero-fill 3/4 of d(x),
 # +0.8 ms -- profiles/measurements/r5_c1_last_backward_ab.jsonl)
 C1_LAST_BWD = os.environ.get("DTF_C1_LAST_BWD", "0") == "1"
+# c1's BatchNorm + ReLU applied on the c2 3x3 conv's input load (ops.batch_norm(defer=True): the
+# halo kernels normalise their patch in LDS and write the BN output once; other c2 shapes fall
+# back to the apply pass); A/B knob, see also ops/native.py DTF_BN_ON_LOAD
+BN_ON_LOAD = os.environ.get("DTF_C2_BN_ON_LOAD", "1") == "1"
 
 
 class Bottleneck(nn.Module):
@@ -92,6 +100,8 @@ class Bottleneck(nn.Module):
         # set by the network: this identity block's output feeds another identity block, whose
         # streamed c1 data gradient can recompute our c3 output (see _c2_c3)
         self.lazy_c3 = False
+        # c1's BN + ReLU applied on c2's input load (the 3x3 halo kernels; stride-1 c2 only)
+        self.c2_bn_on_load = BN_ON_LOAD and stride == 1
 
     def forward(self, x):
         # projection blocks: proj and c1 both read x -> one dgrad buffer, no autograd add
@@ -105,7 +115,7 @@ class Bottleneck(nn.Module):
             if not C1_LAST_BWD:
                 sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
                                 bn_stats=b.training, grad_share=share)
-            y = self._c2_c3(self.c1(x, grad_share=share))
+            y = self._c2_c3(self.c1(x, grad_share=share, defer_bn=self.c2_bn_on_load))
             if C1_LAST_BWD:
                 sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
                                 bn_stats=b.training, grad_share=share)
@@ -113,7 +123,7 @@ class Bottleneck(nn.Module):
             return ops.batch_norm_add_batch_norm(
                 y, b3.gamma, b3.beta, b3.moving_mean, b3.moving_variance, sc, b.gamma, b.beta,
                 b.moving_mean, b.moving_variance, b3.training, b3.momentum, b3.epsilon)
-        y = self._c2_c3(self.c1(x, grad_share=share))
+        y = self._c2_c3(self.c1(x, grad_share=share, defer_bn=self.c2_bn_on_load))
         sc = self.proj(x, relu=False, grad_share=share) if self.has_proj else x
         # identity shortcut: c1 (1x1, stride 1) also reads x, so its dgrad absorbs d(residual)
         return self.c3.bn(y, relu=True, residual=sc, residual_to_conv=not self.has_proj)

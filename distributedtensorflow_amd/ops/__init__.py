@@ -99,12 +99,15 @@ def conv2d_bias_relu(x, w, bias=None, stride=1, padding=0, relu=True):
 
 
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True,
-               momentum=0.997, eps=1e-5, relu=False, residual=None, residual_to_conv=False):
+               momentum=0.997, eps=1e-5, relu=False, residual=None, residual_to_conv=False,
+               defer=False):
     """``residual_to_conv``: the residual tensor is also the input of a stride-1 conv whose
-    data-gradient kernel will add d(residual) in its epilogue (native path; identity shortcuts)."""
+    data-gradient kernel will add d(residual) in its epilogue (native path; identity shortcuts).
+    ``defer``: the result's only consumer is a 3x3 conv, which may apply this BN + ReLU on its
+    input load instead of a separate apply pass (native path)."""
     if _use_native(x):
         return _native().batch_norm(x, gamma, beta, running_mean, running_var, training,
-                                    momentum, eps, relu, residual, residual_to_conv)
+                                    momentum, eps, relu, residual, residual_to_conv, defer)
     return reference.batch_norm(x, gamma, beta, running_mean, running_var, training,
                                 momentum, eps, relu, residual)
 

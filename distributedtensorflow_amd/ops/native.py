@@ -195,7 +195,8 @@ def _fwd_geom(xshape, K, taps, P, Q, sh, sw, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
 
 
 def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0, ow0=0,
-                stats=None, accumulate=False, bnb=(), acc_from=None, bias=None, relu=False):
+                stats=None, accumulate=False, bnb=(), acc_from=None, bias=None, relu=False,
+                bnl=None):
     """wmat: [K, T*C] bf16 (rows zero-padded here to a multiple of 32 for the gather path).
     ``acc_from``: a :class:`_MaskedGrad` the epilogue adds (as dy * mask) instead of reading
     ``out`` back (geom acc mode 2)."""
@@ -216,8 +217,39 @@ def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0
         _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
                       _p(stats), list(bnb), acc_from.dy.data_ptr(), acc_from.mask.data_ptr())
         return
+    if bnl is not None:
+        # BN + ReLU on load: x is the BatchNorm INPUT, the kernel writes the normalised tensor
+        # (bnl.y) itself -- the deferred apply pass never runs
+        _K.conv_igemm(bnl.x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
+                      _p(stats), list(bnb), 0, 0, 0, 0, bnl.scale.data_ptr(),
+                      bnl.shift.data_ptr(), bnl.y.data_ptr())
+        bnl.done = True
+        return
     _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
                   _p(stats), list(bnb), 0, 0, _p(bias), int(relu))
+
+
+class _BnDeferred:
+    """A BatchNorm + ReLU output whose apply pass has not run (``batch_norm(..., defer=True)``):
+    the consuming 3x3 conv normalises its input on load and writes ``y`` itself (halo kernels,
+    csrc/kernels/conv.hip BNL); any other use materialises it first with the apply pass."""
+    __slots__ = ("x", "scale", "shift", "y", "done")
+
+    def __init__(self, x, scale, shift, y):
+        self.x, self.scale, self.shift, self.y, self.done = x, scale, shift, y, False
+
+    def materialize(self):
+        if not self.done:
+            C = self.x.shape[-1]
+            _K.bn_apply(self.x.data_ptr(), 0, self.y.data_ptr(), self.scale.data_ptr(),
+                        self.shift.data_ptr(), self.x.numel() // C, C, 1, _st(), 0)
+            self.done = True
+        return self.y
+
+
+def _bnl_pending(x):
+    rec = getattr(x, "_dtf_bnl", None)
+    return rec if rec is not None and not rec.done else None
 
 
 def conv2d_forward(x, w_bf16, stride, padding, stats=None, bias=None, relu=False):
@@ -228,12 +260,20 @@ def conv2d_forward(x, w_bf16, stride, padding, stats=None, bias=None, relu=False
     assert c == C, (x.shape, w_bf16.shape)
     if bias is None and not relu and _gemm_1x1(C, K, R, S, stride, (pt, pl)) and \
             x.is_contiguous() and w_bf16.is_contiguous():
+        if _bnl_pending(x) is not None:
+            _bnl_pending(x).materialize()
         y = gemm_nt(x.view(-1, C), w_bf16.view(K, C), stats=stats)
         return y.view(n, P, Q, K)
     taps = [(r - pt, s - pl) for r in range(R) for s in range(S)]
     y = torch.empty(n, P, Q, K, device=x.device, dtype=_BF16)
+    bnl = _bnl_pending(x)
+    if bnl is not None and (bias is not None or relu or not _K.conv_bnl_ok(
+            _fwd_geom(x.shape, K, taps, P, Q, sh, sw, P, Q), [t[0] for t in taps],
+            [t[1] for t in taps])):
+        bnl.materialize()
+        bnl = None
     _launch_fwd(x, w_bf16.reshape(K, R * S * C), K, taps, P, Q, sh, sw, y, P, Q, stats=stats,
-                bias=bias, relu=relu)
+                bias=bias, relu=relu, bnl=bnl)
     return y
 
 
@@ -757,6 +797,8 @@ def conv2d(x, w, stride=1, padding=0, bn_stats=False, grad_share=None):
 # ----------------------------------------------------------------------------- batch norm
 
 _FUSE_RESIDUAL_GRAD = os.environ.get("DTF_FUSE_RESIDUAL_GRAD", "1") == "1"
+# BN1 + ReLU applied on the c2 halo conv's input load (batch_norm(defer=True)); A/B knob
+_BN_ON_LOAD = os.environ.get("DTF_BN_ON_LOAD", "1") == "1"
 _LAZY_RESIDUAL_GRAD = os.environ.get("DTF_LAZY_RESIDUAL_GRAD", "1") == "1"
 # stem backward: pool gather fused into both BatchNorm backward passes (_BatchNormReluMaxPool)
 _FUSE_STEM_POOL_BWD = os.environ.get("DTF_FUSE_STEM_POOL_BWD", "1") == "1"
@@ -801,7 +843,7 @@ class _LazyBnDx:
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu,
-                residual, residual_to_conv=False):
+                residual, residual_to_conv=False, defer=False):
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -820,7 +862,11 @@ class _BatchNorm(torch.autograd.Function):
         if rc is not None and not (relu and res is not None):
             rc.materialize()
             rc = None
-        if rc is not None:
+        deferred = None
+        if defer and relu and res is None and training and rc is None:
+            # the consuming 3x3 conv applies this BN + ReLU on load and writes y (_BnDeferred)
+            deferred = _BnDeferred(x, scale, shift, y)
+        elif rc is not None:
             # lazy x3: the apply recomputes the conv output in a stream GEMM whose epilogue is
             # this apply (bit-identical to storing x3 and running the pass over it)
             _K.gemm_stream_apply(rc.y.data_ptr(), rc.wb.data_ptr(), y.data_ptr(), M, C, rc.k3,
@@ -829,6 +875,8 @@ class _BatchNorm(torch.autograd.Function):
         else:
             _K.bn_apply(x.data_ptr(), _p(res), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
                         M, C, int(relu), st, _p(mask))
+        if deferred is not None:
+            y._dtf_bnl = deferred
         ctx.save_for_backward(x, mask, g32, stats)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -862,13 +910,13 @@ class _BatchNorm(torch.autograd.Function):
         if dy is None:
             mg = ctx.slot.grad if ctx.slot is not None else None
             if mg is None:
-                return (None,) * 11
+                return (None,) * 12
             ctx.slot.grad = None
             # d(y) = dy_res * mask: the reduce / apply kernels apply the bit mask on load
             dy, mask, relu = mg.dy, mg.mask, True
         ctx.slot = None
         dx, dg, db, dres = _bn_backward_core(ctx, dy, x, mask, g32, stats, relu)
-        return dx, dg, db, None, None, None, None, None, None, dres, None
+        return dx, dg, db, None, None, None, None, None, None, dres, None, None
 
 
 class _GradSlot:
@@ -1006,7 +1054,10 @@ def _bn_backward_core(ctx, dy, x, mask, g32, stats, relu=None):
 
 
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True,
-               momentum=0.997, eps=1e-5, relu=False, residual=None, residual_to_conv=False):
+               momentum=0.997, eps=1e-5, relu=False, residual=None, residual_to_conv=False,
+               defer=False):
+    """``defer``: BN + ReLU whose only consumer is a 3x3 conv -- the apply pass is left to the
+    conv's input load where its kernel supports it (see :class:`_BnDeferred`)."""
     _check_cuda_bf16(x, residual)
     C = x.shape[-1]
     if C % 8 or C > 2048:
@@ -1014,7 +1065,7 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
     if residual is not None and residual.shape != x.shape:
         raise ValueError("residual shape mismatch")
     return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps,
-                            relu, residual, residual_to_conv)
+                            relu, residual, residual_to_conv, bool(defer and _BN_ON_LOAD))
 
 
 class _BnReluConv1x1(torch.autograd.Function):

@@ -807,3 +807,85 @@ def test_lazy_x3_never_stores_stage0_c3_output_bit_identical():
     assert torch.equal(dxa, dxb)
     for i, (a, b) in enumerate(zip(ga, gb)):
         assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize("C,W,K", [(64, 56, 64), (128, 28, 128)])
+def test_halo_conv_bn_relu_on_load_bit_identical(C, W, K):
+    """VERDICT r4 #5 (halo families): the 3x3 conv reads the BatchNorm INPUT and applies
+    y = bf16(max(x sc + sh, 0)) to its LDS patch (padding stays zero), writing y for the rows it
+    owns -- y, the conv output and its BN statistics slab equal the apply pass + conv bit for
+    bit."""
+    torch.manual_seed(0)
+    x = (torch.randn(3, W, W, C, device="cuda") * 2 + 0.3).bfloat16()
+    w = (torch.randn(K, 3, 3, C, device="cuda") / (9 * C) ** 0.5).bfloat16()
+    sc = torch.rand(C, device="cuda") + 0.5
+    sh = torch.randn(C, device="cuda") * 0.5
+    M = x.numel() // C
+    y_ref = torch.empty_like(x)
+    native._K.bn_apply(x.data_ptr(), 0, y_ref.data_ptr(), sc.data_ptr(), sh.data_ptr(), M, C, 1,
+                       torch.cuda.current_stream().cuda_stream, 0)
+    taps = [(r - 1, s - 1) for r in range(3) for s in range(3)]
+    geom = native._fwd_geom(x.shape, K, taps, W, W, 1, 1, W, W)
+    assert native._K.conv_bnl_ok(geom, [t[0] for t in taps], [t[1] for t in taps])
+    G = native._K.conv_tile_rows(geom, [t[0] for t in taps], [t[1] for t in taps])
+    outs = []
+    for bnl in (False, True):
+        part = torch.full((native._K.bn_workspace_floats_g(G, K),), float("nan"), device="cuda")
+        if bnl:
+            y = torch.full_like(x, float("nan"))
+            y._dtf_bnl = native._BnDeferred(x, sc, sh, y)
+        else:
+            y = y_ref
+        z = native.conv2d_forward(y, w, 1, 1, stats=part)
+        torch.cuda.synchronize()
+        if bnl:
+            assert y._dtf_bnl.done
+        outs.append((y.clone(), z, part[:G * 2 * K]))
+    assert torch.equal(outs[1][0], y_ref)
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][2], outs[1][2])
+
+
+@pytest.mark.parametrize("bi,shape", [(1, (2, 56, 56, 256)), (4, (2, 28, 28, 512))])
+def test_bottleneck_c2_bn_on_load_bit_identical(bi, shape):
+    """c1's BN + ReLU applied on the c2 halo conv's input load (ops.batch_norm(defer=True)):
+    an identity block's output, input gradient and every parameter gradient equal the apply
+    pass + conv path bit for bit, and the BN-on-load launch really ran."""
+    torch.manual_seed(0)
+    m = resnet50().cuda()
+    blk = m.blocks[bi]
+    x = torch.randn(*shape, device="cuda").bfloat16()
+    calls = {"bnl": 0}
+    orig = native._K.conv_igemm
+
+    def spy(*a, **k):
+        calls["bnl"] += int(len(a) > 16 and a[16] != 0)
+        return orig(*a, **k)
+    out, g = {}, None
+    prev = native._BN_ON_LOAD
+    try:
+        native._K.conv_igemm = spy
+        for on in (True, False):
+            native._BN_ON_LOAD = on
+            b = copy.deepcopy(blk)
+            assert b.c2_bn_on_load
+            xi = x.clone().requires_grad_(True)
+            y = b(xi)
+            if g is None:
+                g = torch.randn(y.shape, generator=torch.Generator().manual_seed(1)).to(
+                    device="cuda", dtype=y.dtype)
+            y.backward(g)
+            torch.cuda.synchronize()
+            out[on] = (y.detach().float(), xi.grad.float(),
+                       [p.grad.float() for p in b.parameters()])
+            if on:
+                seen = calls["bnl"]
+    finally:
+        native._K.conv_igemm = orig
+        native._BN_ON_LOAD = prev
+    assert seen == 1 and calls["bnl"] == 1
+    (ya, dxa, ga), (yb, dxb, gb) = out[True], out[False]
+    assert torch.equal(ya, yb)
+    assert torch.equal(dxa, dxb)
+    for i, (a, b) in enumerate(zip(ga, gb)):
+        assert torch.equal(a, b), i
