@@ -268,7 +268,7 @@ class Tracer:
 
     def op_batch_norm(self, x, gamma, beta, running_mean=None, running_var=None, training=True,
                       momentum=0.997, eps=1e-5, relu=False, residual=None,
-                      residual_to_conv=False):
+                      residual_to_conv=False, defer=False):
         y = self._bn(x, gamma, beta, running_mean, running_var, eps)
         if residual is not None:
             y = self._add(y, residual)
