@@ -866,6 +866,17 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   const int sid = wall >> 2, wave = wall & 3;                    // strip, wave within the strip
   bf16_t* const patch = lds + sid * (H::PIXAL * C);              // [ST][PIXAL][C]
   bf16_t* const wst = lds + ST * (H::PIXAL * C);                 // [NSTG][NT][64]
+  // BNL: per 8-channel chunk {scale[8], shift[8]} (16 floats), past the filter ring
+  float* const bnl_prm = reinterpret_cast<float*>(wst + NSTG * H::WST);
+  if constexpr (BNL) {
+    for (int t = tid; t < C / 4; t += kThreads) {       // float4 t: channels 4t .. 4t + 3
+      const int ch = t >> 1, half = t & 1;
+      reinterpret_cast<float4*>(bnl_prm)[ch * 4 + half] =
+          *reinterpret_cast<const float4*>(g.lsc + 4 * t);
+      reinterpret_cast<float4*>(bnl_prm)[ch * 4 + 2 + half] =
+          *reinterpret_cast<const float4*>(g.lsh + 4 * t);
+    }
+  }
   const int wm = wave / H::WNW, wn = wave % H::WNW;
   const int tiles_h = g.H / kHaloTH;
   const int tm = blockIdx.x * ST + sid;                          // (image, row-tile)
@@ -1025,19 +1036,23 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     if constexpr (BNL) {
       if (step == 0) {
         // BN + ReLU of the landed patch, in place (padding pixels stay zero); the rows this block
-        // owns (input rows h0 .. h0 + TH - 1, every pixel exactly once over the grid) go to ly
+        // owns (input rows h0 .. h0 + TH - 1, every pixel exactly once over the grid) go to ly.
+        // Fully unrolled over the thread's items (the patch reads and the per-chunk scale / shift
+        // reads from the LDS copy all issue ahead of their use)
         constexpr int CPP = H::ROWB / 16;
-        for (int idx = tid; idx < H::PIX * CPP; idx += kThreads) {
+        constexpr int ITEMS = (H::PIX * CPP + kThreads - 1) / kThreads;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+          const int idx = tid + k * kThreads;
           const int pix = idx / CPP, slot = idx - pix * CPP;
           const int pr = pix / H::PW, pc = pix - pr * H::PW;
           const int h = h0 - 1 + pr, w = pc - 1;
-          if (!live || (unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) continue;
+          if (idx >= H::PIX * CPP || (unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W)
+            continue;
           const int lch = slot ^ halo_swz<C>(pr * W + pc);      // logical chunk in this slot
           uint4* pp = reinterpret_cast<uint4*>(patch + pix * C + slot * 8);
-          const float4 s0 = *reinterpret_cast<const float4*>(g.lsc + lch * 8);
-          const float4 s1 = *reinterpret_cast<const float4*>(g.lsc + lch * 8 + 4);
-          const float4 t0 = *reinterpret_cast<const float4*>(g.lsh + lch * 8);
-          const float4 t1 = *reinterpret_cast<const float4*>(g.lsh + lch * 8 + 4);
+          const float4* sp = reinterpret_cast<const float4*>(bnl_prm + lch * 16);
+          const float4 s0 = sp[0], s1 = sp[1], t0 = sp[2], t1 = sp[3];
           const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
           const float sf[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
           float v[8];
@@ -1352,13 +1367,14 @@ static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const Conv
     if (bnb.part || freg_on || nstg == 3 || nstg == 4 || strips != 1)
       throw std::runtime_error("halo conv: BN on load needs the default forward ring kernel");
     auto kern = conv3x3_halo_kernel<C, W, WMW, NT, 1, false, false, 2, true>;
+    const size_t lds = Hc::lds(1) + (size_t)2 * C * sizeof(float);    // + the BN scale / shift
     static bool attr = false;
     if (!attr) {
       HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)Hc::lds(1)));
+                                    (int)lds));
       attr = true;
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)tiles, g.Kout / NT), dim3(kThreads), Hc::lds(1), st,
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles, g.Kout / NT), dim3(kThreads), lds, st,
                        X, Wt, Y, g, taps, stats, bnb);
     return;
   }
