@@ -1650,6 +1650,10 @@ class _Dense(torch.autograd.Function):
             o, i = wb.shape
             x2 = x.reshape(-1, i)
             M = x2.shape[0]
+            if x.requires_grad and wb.is_contiguous():
+                # W^T for the data gradient from the step's batched filter transpose (it was a
+                # separate 17 us permute copy per layer)
+                _register_dgrad_filter(wb.view(o, 1, 1, i))
             z = torch.empty(M, o, device=x.device, dtype=_BF16)
             h = torch.empty_like(z)
             _K.gemm_nt_bias_gelu(x2.data_ptr(), wb.data_ptr(), z.data_ptr(), h.data_ptr(), M, o,
