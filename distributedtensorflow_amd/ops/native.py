@@ -555,6 +555,8 @@ def _pad_c8(t):
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_master, stride, padding, stats=None, share=None):
+        if _bnl_pending(x) is not None and (not x.is_contiguous() or x.shape[-1] % 8):
+            _bnl_pending(x).materialize()        # BN on load needs the tensor itself as input
         xb = x.contiguous()
         ctx.share = share
         wb = _bf16_weight(w_master)
