@@ -852,8 +852,9 @@ DTF_DEV int halo_swz(int u) { return C == 64 ? (((u >> 1) & 3) << 1) : ((u & 7) 
 // for the thread's output rows before the tile is staged, so its latency hides under the staging.
 // NSTG: filter-slice ring depth (LDS stages; the slice of step s + NSTG - 1 is issued at step s,
 // so a slice has NSTG - 1 steps of MFMA work to arrive from L2; 2 = the original double buffer)
+// BNLP (timing probe only, y not written): the BN-on-load forward without its y stores
 template <int C, int W, int WMW, int NT, int ST = 1, bool FREG = false, bool BNB = false,
-          int NSTG = 2, bool BNL = false>
+          int NSTG = 2, bool BNL = false, int BNLP = 0>
 __global__ void __launch_bounds__(kThreads * ST, ST == 1 ? 2 : 1)
 conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                     bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
@@ -1061,7 +1062,7 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(__builtin_fmaf(v[e], sc[e], sf[e]), 0.f);
           const uint4 pk = pack8(v);
           *pp = pk;
-          if (pr >= 1 && pr <= kHaloTH)
+          if (BNLP == 0 && pr >= 1 && pr <= kHaloTH)
             *reinterpret_cast<uint4*>(g.ly + (((long)n * g.H + h) * g.W + w) * C + lch * 8) = pk;
         }
         __syncthreads();
@@ -1339,6 +1340,9 @@ void dtf_conv_set_halo_freg(int v) { g_halo_freg = v; }
 // 3 / 4: deeper rings; family 1 keeps two blocks per CU at 4, family 2 only with two strips)
 static int g_halo_stages = 0;
 void dtf_conv_set_halo_stages(int v) { g_halo_stages = v; }
+// timing probe: the BN-on-load forward without its y stores (wrong results downstream)
+static int g_bnl_probe = 0;
+void dtf_conv_set_bnl_probe(int v) { g_bnl_probe = v; }
 
 template <int C, int W, int WMW, int NT, int ST, bool BNB, int NSTG>
 static void launch_halo_ring(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
@@ -1366,13 +1370,14 @@ static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const Conv
   if (g.ly) {
     if (bnb.part || freg_on || nstg == 3 || nstg == 4 || strips != 1)
       throw std::runtime_error("halo conv: BN on load needs the default forward ring kernel");
-    auto kern = conv3x3_halo_kernel<C, W, WMW, NT, 1, false, false, 2, true>;
+    auto kern = g_bnl_probe ? conv3x3_halo_kernel<C, W, WMW, NT, 1, false, false, 2, true, 1>
+                            : conv3x3_halo_kernel<C, W, WMW, NT, 1, false, false, 2, true>;
     const size_t lds = Hc::lds(1) + (size_t)2 * C * sizeof(float);    // + the BN scale / shift
-    static bool attr = false;
-    if (!attr) {
+    static bool attr[2] = {false, false};
+    if (!attr[g_bnl_probe ? 1 : 0]) {
       HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
-      attr = true;
+      attr[g_bnl_probe ? 1 : 0] = true;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)tiles, g.Kout / NT), dim3(kThreads), lds, st,
                        X, Wt, Y, g, taps, stats, bnb);
