@@ -59,6 +59,7 @@ void dtf_conv_set_halo(int);
 int dtf_conv_tile_rows(const ConvGeom&, const TapTable&, int bnb);
 bool dtf_conv_bnl_ok(const ConvGeom&, const TapTable&);
 void dtf_conv_set_bnl_probe(int);
+void dtf_gemm_stream_set_bnb_probe(int);
 void dtf_conv_set_halo_bnb(int);
 void dtf_conv_set_dma_mode(int);
 void dtf_conv_set_small_k(int);
@@ -441,6 +442,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
         py::arg("taps") = 1, py::arg("W") = 0);
   m.def("conv_set_halo", &dtf_conv_set_halo);
   m.def("conv_set_bnl_probe", &dtf_conv_set_bnl_probe);
+  m.def("gemm_stream_set_bnb_probe", &dtf_gemm_stream_set_bnb_probe);
   m.def("conv_tile_rows", [](std::vector<int> geom, std::vector<int> dh, std::vector<int> dw,
                              int bnb) {
     if (geom.size() != 16 && geom.size() != 17)

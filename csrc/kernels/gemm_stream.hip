@@ -567,6 +567,9 @@ void launch_stream(const StreamArgs& g, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(kST), LDS, st, g);
 }
 
+// timing probe of the kind-1 BN-backward epilogue (PROBE bits 4 / 8 above; wrong results)
+static int g_stream_bnb_probe = 0;
+
 template <int K, int MODE>
 void launch_stream_bnb(const StreamArgs& g, int bmk, hipStream_t st) {
   if (g.y2) {            // RC: the residual BN's input recomputed (kind 1, K <= 128, K3 64 / 128)
@@ -580,7 +583,14 @@ void launch_stream_bnb(const StreamArgs& g, int bmk, hipStream_t st) {
     throw std::runtime_error("gemm_stream_bnb: RC needs K <= 128");
   }
   if (g.bxp) launch_stream<K, MODE, false, 1, false, 0, true>(g, st);
-  else if (bmk == 1) launch_stream<K, MODE, false, 1>(g, st);
+  else if (bmk == 1) {
+    switch (g_stream_bnb_probe) {
+      case 4: launch_stream<K, MODE, false, 1, false, 4>(g, st); break;
+      case 8: launch_stream<K, MODE, false, 1, false, 8>(g, st); break;
+      case 12: launch_stream<K, MODE, false, 1, false, 12>(g, st); break;
+      default: launch_stream<K, MODE, false, 1>(g, st); break;
+    }
+  }
   else if (bmk == 2) launch_stream<K, MODE, false, 2>(g, st);
   else launch_stream<K, MODE, false, 0>(g, st);
 }
@@ -718,6 +728,8 @@ void dtf_gemm_stream_apply(const bf16_t* A, const bf16_t* W, bf16_t* Y, int M, i
   g.amask = mask;
   run_stream(g, K, -1, st);
 }
+
+void dtf_gemm_stream_set_bnb_probe(int v) { g_stream_bnb_probe = v; }
 
 // timing probes of the plain K = 256 kernel (see PROBE above)
 void dtf_gemm_stream_probe(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int probe,

@@ -47,6 +47,8 @@ if os.environ.get("DTF_WGRAD_DIRECT"):   # ping-pong wgrad: per-row decode (1) /
     _K.wgrad_set_direct(int(os.environ["DTF_WGRAD_DIRECT"]))
 if os.environ.get("DTF_BNL_PROBE"):      # timing probe: BN-on-load forward without its y stores
     _K.conv_set_bnl_probe(int(os.environ["DTF_BNL_PROBE"]))
+if os.environ.get("DTF_STREAM_BNB_PROBE"):   # timing probe: BN-backward stream GEMM (wrong results)
+    _K.gemm_stream_set_bnb_probe(int(os.environ["DTF_STREAM_BNB_PROBE"]))
 if os.environ.get("DTF_WGRAD_DEEP"):     # ping-pong wgrad: 5-slot 32-pixel ring (1) / 2 x 64 (0)
     _K.wgrad_set_deep(int(os.environ["DTF_WGRAD_DEEP"]))
 if os.environ.get("DTF_WGRAD_PIPE"):
