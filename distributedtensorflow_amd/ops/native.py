@@ -226,7 +226,7 @@ def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0
         # (bnl.y) itself -- the deferred apply pass never runs
         _K.conv_igemm(bnl.x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
                       _p(stats), list(bnb), 0, 0, 0, 0, bnl.scale.data_ptr(),
-                      bnl.shift.data_ptr(), bnl.y.data_ptr())
+                      bnl.shift.data_ptr(), bnl.y().data_ptr())
         bnl.done = True
         return
     _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
@@ -240,15 +240,18 @@ class _BnDeferred:
     __slots__ = ("x", "scale", "shift", "y", "done")
 
     def __init__(self, x, scale, shift, y):
-        self.x, self.scale, self.shift, self.y, self.done = x, scale, shift, y, False
+        # y holds this record: a weak reference back keeps them out of a reference cycle (a
+        # cycle left every step's y to the cyclic collector: +2.9 GB of peak memory per step)
+        self.x, self.scale, self.shift, self.y, self.done = x, scale, shift, weakref.ref(y), False
 
     def materialize(self):
-        if not self.done:
+        y = self.y()
+        if not self.done and y is not None:
             C = self.x.shape[-1]
-            _K.bn_apply(self.x.data_ptr(), 0, self.y.data_ptr(), self.scale.data_ptr(),
+            _K.bn_apply(self.x.data_ptr(), 0, y.data_ptr(), self.scale.data_ptr(),
                         self.shift.data_ptr(), self.x.numel() // C, C, 1, _st(), 0)
             self.done = True
-        return self.y
+        return y
 
 
 def _bnl_pending(x):

@@ -889,3 +889,35 @@ def test_bottleneck_c2_bn_on_load_bit_identical(bi, shape):
     assert torch.equal(dxa, dxb)
     for i, (a, b) in enumerate(zip(ga, gb)):
         assert torch.equal(a, b), i
+
+
+def test_training_step_frees_its_activations_without_the_cycle_collector():
+    """A default training step (BN on load, lazy x3, fused BN backward) leaves no reference
+    cycle holding activations: with the cyclic collector disabled, allocated memory does not
+    grow over the second, third and fourth steps (the first builds per-step caches; later steps
+    move by a few hundred KB as those alternate, while a leaked set of c1 outputs is ~11 MB per
+    step at this batch).  (A y <-> deferred-BN-record cycle once
+    kept every step's c1 outputs alive until a full collection: +2.9 GB of peak per step at
+    b1984.)"""
+    import gc
+    torch.manual_seed(0)
+    m = resnet50().cuda()
+    x = torch.randn(8, 224, 224, 3, device="cuda").bfloat16()
+    lab = torch.randint(0, 1000, (8,), device="cuda")
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        after = []
+        for _ in range(4):
+            loss = torch.nn.functional.cross_entropy(m(x).float(), lab)
+            loss.backward()
+            del loss
+            for p in m.parameters():
+                p.grad = None
+            torch.cuda.synchronize()
+            after.append(torch.cuda.memory_allocated())
+    finally:
+        if was:
+            gc.enable()
+    assert max(after[1:]) - min(after[1:]) < 2 * 2**20, after
