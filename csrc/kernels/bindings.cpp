@@ -209,8 +209,8 @@ void dtf_pos_type_grad(const bf16_t*, const int64_t*, int, int, int, int, float*
                        hipStream_t);
 void dtf_segment_sum(const int64_t*, const int64_t*, const bf16_t*, float*, int, int,
                      hipStream_t);
-void dtf_mlm_xent(const bf16_t*, const int64_t*, const float*, const float*, int, int, float*,
-                  bf16_t*, hipStream_t);
+void dtf_mlm_xent(const bf16_t*, const int64_t*, const float*, const float*, int, int, int,
+                  float*, bf16_t*, hipStream_t);
 
 // ---- dense GEMM (gemm.hip)
 void dtf_gemm_nt_bias_gelu(const bf16_t*, const bf16_t*, bf16_t*, bf16_t*, int, int, int, int,
@@ -939,9 +939,9 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("segment_sum");
   });
   m.def("mlm_xent", [](uintptr_t logits, uintptr_t labels, uintptr_t weights, uintptr_t denom,
-                       int N, int V, uintptr_t loss_rows, uintptr_t grad, uintptr_t st) {
+                       int N, int V, int ld, uintptr_t loss_rows, uintptr_t grad, uintptr_t st) {
     dtf_mlm_xent(P<const bf16_t>(logits), P<const int64_t>(labels), P<const float>(weights),
-                 P<const float>(denom), N, V, P<float>(loss_rows), P<bf16_t>(grad), S(st));
+                 P<const float>(denom), N, V, ld, P<float>(loss_rows), P<bf16_t>(grad), S(st));
     check_launch("mlm_xent");
   });
 }

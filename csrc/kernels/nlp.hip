@@ -1321,21 +1321,24 @@ segment_sum_kernel(const int64_t* __restrict__ sorted_ids, const int64_t* __rest
 
 // ----------------------------------------------------------------------------- MLM loss
 // rows: loss_rows[i] = w_i * (lse - logit[label]) / denom ; grad = w_i * (softmax - onehot) / denom
-// One wave per masked position; the row (V = 30522 bf16, rows only 4-B aligned) is swept in
-// 16-B chunks from the 16-B-aligned address below its start with raw buffer loads (range-checked:
-// the chunk before row 0 / past the last row reads zeros), elements outside the row masked.
+// One wave per masked position.  Rows are `ld` elements apart (ld >= V): the tied MLM decoder runs
+// on a vocabulary padded to a multiple of 64 (30528 for BERT's 30522), whose last ld - V logits
+// are not classes -- they are left out of the softmax and their gradient is written as exact 0.
+// With ld == V (rows only 4-B aligned) the row is swept in 16-B chunks from the 16-B-aligned
+// address below its start with raw buffer loads (range-checked: the chunk before row 0 / past the
+// last row reads zeros), elements outside the row masked.
 // Online (max, sum) with one rescale per 8 elements; the gradient pass stores whole 16-B chunks
 // inside the row and single elements at its two ends.
 __global__ void __launch_bounds__(256)
 mlm_xent_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ labels,
                 const float* __restrict__ weights, const float* __restrict__ denom, int N, int V,
-                float* __restrict__ loss_rows, bf16_t* __restrict__ grad) {
+                int ld, float* __restrict__ loss_rows, bf16_t* __restrict__ grad) {
   const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (row >= N) return;
   const auto rl = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(logits), (short)0,
-                                                    (int)((uint32_t)N * V * 2u), 0x00020000);
-  const uint32_t b0 = (uint32_t)row * V * 2u;
+                                                    (int)((uint32_t)N * ld * 2u), 0x00020000);
+  const uint32_t b0 = (uint32_t)row * ld * 2u;
   const uint32_t a0 = b0 & ~15u;
   const int head = (int)(b0 - a0) >> 1;
   const int nch = (head + V + 7) >> 3;
@@ -1367,24 +1370,27 @@ mlm_xent_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ l
   }
   const float lse = mx + __logf(s);
   const int lab = (int)labels[row];
-  const bf16_t* x = logits + (long)row * V;
+  const bf16_t* x = logits + (long)row * ld;
   const float wsc = weights ? weights[row] / fmaxf(denom[0], 1e-5f) : 1.f / fmaxf(denom[0], 1e-5f);
   if (lane == 0) loss_rows[row] = wsc * (lse - bf2f(x[lab]));
   if (grad) {
+    // the whole stored row [0, ld): classes get the gradient, padding columns exact zeros
+    const int gch = (head + ld + 7) >> 3;
     bf16_t* gbase = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(grad) + a0);
-    for (int c = lane; c < nch; c += 64) {
+    for (int c = lane; c < gch; c += 64) {
       const uint4 raw = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rl, a0 + c * 16u, 0, 0));
       float f[8];
       unpack8(raw, f);
       const int e0 = c * 8 - head;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) f[k] = wsc * (__expf(f[k] - lse) - (e0 + k == lab ? 1.f : 0.f));
-      if (e0 >= 0 && e0 + 8 <= V) {
+      for (int k = 0; k < 8; ++k)
+        f[k] = e0 + k < V ? wsc * (__expf(f[k] - lse) - (e0 + k == lab ? 1.f : 0.f)) : 0.f;
+      if (e0 >= 0 && e0 + 8 <= ld) {
         reinterpret_cast<uint4*>(gbase)[c] = pack8(f);
       } else {
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-          if (e0 + k >= 0 && e0 + k < V) gbase[c * 8 + k] = f2bf(f[k]);
+          if (e0 + k >= 0 && e0 + k < ld) gbase[c * 8 + k] = f2bf(f[k]);
       }
     }
   }
@@ -1695,9 +1701,10 @@ void dtf_segment_sum(const int64_t* sorted_ids, const int64_t* perm, const bf16_
 }
 
 void dtf_mlm_xent(const bf16_t* logits, const int64_t* labels, const float* weights,
-                  const float* denom, int N, int V, float* loss_rows, bf16_t* grad,
+                  const float* denom, int N, int V, int ld, float* loss_rows, bf16_t* grad,
                   hipStream_t st) {
-  if ((double)N * V * 2.0 >= 2147483647.0) throw std::runtime_error("mlm_xent: logits too large");
+  if ((double)N * ld * 2.0 >= 2147483647.0) throw std::runtime_error("mlm_xent: logits too large");
+  if (V < 1 || ld < V) throw std::runtime_error("mlm_xent: row stride below the class count");
   hipLaunchKernelGGL(mlm_xent_kernel, dim3((N * 64 + 255) / 256), dim3(256), 0, st, logits,
-                     labels, weights, denom, N, V, loss_rows, grad);
+                     labels, weights, denom, N, V, ld, loss_rows, grad);
 }

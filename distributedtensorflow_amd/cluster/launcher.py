@@ -121,6 +121,7 @@ def _stop_others(tasks, failed, rc, grace_s=10.0):
         x.log.write(f"\n[launcher] {failed.name} failed for good (exit {rc}); stopping "
                     f"{x.name}\n")
         x.log.flush()
+        x.final = True          # stopped on purpose: never mistaken for a crash to restart
         x.proc.terminate()
     t0 = time.time()
     while time.time() - t0 < grace_s and any(x.proc.poll() is None for x in live):
@@ -131,7 +132,8 @@ def _stop_others(tasks, failed, rc, grace_s=10.0):
             x.proc.wait()
 
 
-def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart_alone=False):
+def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart_alone=False,
+               needs_all=False):
     """Wait for the worker tasks, restarting failed tasks meanwhile.
 
     A task that exits non-zero while the job runs is restarted as a FRESH process (never a
@@ -144,9 +146,13 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart
     died): the restarted ranks resume from the chief's latest checkpoint.
 
     A task that fails FOR GOOD while the job is not ending (restarts used up, or nobody left to
-    re-form the cluster with) ends the job at once: the other tasks could only wait for it until
-    their own timeouts, so they are stopped (stacks dumped into their logs first) and the exit
-    codes report the failure.  At ``timeout_s`` every live task's stack is dumped and
+    re-form the cluster with) ends the job at once when the others cannot finish without it -- a
+    parameter-server task, any rank of a collective world (``restart_alone``), any worker of a
+    synchronous job (``needs_all``): they could only wait for it until their own timeouts, so
+    they are stopped (stacks dumped into their logs first) and the exit codes report the failure.
+    A worker of an asynchronous parameter-server job is not needed by the others (between-graph
+    training: the chief and the other workers keep training, as in TF1), so its failure is
+    logged and the job goes on.  At ``timeout_s`` every live task's stack is dumped and
     :class:`LaunchTimeout` is raised with all log tails in its message."""
     from .rendezvous import bump_epoch
     from .server import Server
@@ -167,10 +173,14 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart
                     (not voluntary and used >= max_restarts):
                 t.final = True
                 if not ending:
+                    fatal = needs_all or restart_alone or not is_worker(t)
                     t.log.write(f"\n[launcher] {t.name} (pid {t.proc.pid}) exited with {rc} "
-                                f"and is not restarted ({used}/{max_restarts} restarts used)\n")
+                                f"and is not restarted ({used}/{max_restarts} restarts used)"
+                                + ("" if fatal else "; the other tasks continue (asynchronous "
+                                   "training does not need this worker)") + "\n")
                     t.log.flush()
-                    _stop_others(tasks, t, rc)
+                    if fatal:
+                        _stop_others(tasks, t, rc)
                 continue
             if not voluntary:
                 used += 1
@@ -199,8 +209,12 @@ def _supervise(tasks, store, is_worker, max_restarts, timeout_s, script, restart
 
 def launch_local(script, num_ps=1, num_workers=2, workdir=None, extra_args=(), env=None,
                  timeout_s=600, grace_s=30, gpus_per_host=None, max_ps_restarts=0,
-                 max_restarts=0):
+                 max_restarts=0, sync=False):
     """Start a PS/worker cluster of ``script`` on this host and supervise it.
+
+    ``sync``: the workers train synchronously (SyncReplicas: every step waits for all of them),
+    so a worker that fails for good ends the job; by default (asynchronous between-graph
+    training) only a failed PS task does, and the other workers carry on.
 
     The launcher hosts the cluster's rendezvous store (at the chief's ``config.json`` address),
     so any task -- the chief included -- may die: up to ``max_restarts`` failed tasks (or
@@ -240,7 +254,8 @@ def launch_local(script, num_ps=1, num_workers=2, workdir=None, extra_args=(), e
              for i in range(n)]
     rc = {}
     try:
-        _supervise(tasks, store, lambda t: t.job == "worker", max_restarts, timeout_s, script)
+        _supervise(tasks, store, lambda t: t.job == "worker", max_restarts, timeout_s, script,
+                   needs_all=sync)
         for t in tasks:
             if t.job == "worker":
                 rc[(t.job, t.index)] = t.proc.wait()
@@ -308,8 +323,10 @@ if __name__ == "__main__":
     ap.add_argument("--num_workers", type=int, default=2)
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--max_restarts", "--max_ps_restarts", type=int, default=0)
+    ap.add_argument("--sync", action="store_true",
+                    help="synchronous workers: a worker failing for good ends the job")
     a, rest = ap.parse_known_args()
     codes, logs = launch_local(a.script, a.num_ps, a.num_workers, a.workdir, rest,
-                               max_restarts=a.max_restarts)
+                               max_restarts=a.max_restarts, sync=a.sync)
     print(json.dumps({"exit_codes": {f"{k[0]}{k[1]}": v for k, v in codes.items()},
                       "logs": logs}, indent=2))

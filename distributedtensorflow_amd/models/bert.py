@@ -11,11 +11,17 @@ MI355X layout choices:
     transposes): Q/K/V come from ONE fused ``768 -> 2304`` GEMM whose output the MFMA attention
     kernel reads in place; its fp32 master ``[2304, 768]`` is exported to checkpoints as the
     three TF variables ``query|key|value`` (row slices, ``_dtf_splits``);
-  * plain GEMMs go to hipBLASLt (bias left out), and everything around them is fused into our
-    kernels: bias+GELU, bias+dropout+residual+LayerNorm, embedding gather+sum+LN+dropout,
+  * every GEMM runs on our persistent MFMA GEMM (csrc/kernels/gemm.hip gemm_pp2) and every
+    weight gradient on our TN weight-gradient kernel, and everything around them is fused into
+    our kernels: bias+GELU, bias+dropout+residual+LayerNorm, embedding gather+sum+LN+dropout,
     flash attention with in-kernel dropout, weighted MLM cross-entropy;
-  * the MLM decoder is tied to the word embeddings (one [30522, 768] fp32 master, whose bf16
-    shadow feeds both the gather and the logits GEMM).
+  * the MLM decoder is tied to the word embeddings (one fp32 master whose bf16 shadow feeds both
+    the gather and the logits GEMM).  Its vocabulary is padded to a multiple of 64 (30522 ->
+    30528 rows) so the decoder's forward, data gradient and weight gradient fit our GEMM tiles:
+    the padding rows of the table and of the output bias are zero, never gathered, get an exact
+    zero gradient (the loss leaves their logits out of the softmax), so training is exactly the
+    unpadded model; checkpoints and SavedModels carry the TF shapes ``[30522, 768]`` /
+    ``[30522]`` (row slices, ``_dtf_splits``).
 """
 from __future__ import annotations
 
@@ -29,11 +35,17 @@ from .. import ops
 from .layers import Layer, _tag, truncated_normal_
 
 
-# BERT's plain GEMMs (bias left to the fused consumer kernels) stay on hipBLASLt by default: on
-# the BERT-base shapes the library kernels run 1.1-1.3x our MFMA GEMM (tools/gemm_bench.py,
-# profiles/measurements/r2_gemm_vs_hipblaslt.jsonl); DTF_BERT_GEMM=native routes them through
-# csrc/kernels/gemm.hip instead.
+# BERT's dense layers take ops.dense(impl="library"): the bias rides in the GEMM epilogue or in
+# the fused consumer kernel, and the GEMMs run on our persistent MFMA GEMM (ops/native.py _Dense;
+# hipBLASLt only for shapes outside its tiles, none in BERT-base).  "native" selects the
+# tf.layers.dense form (bias + ReLU epilogue, separate bias-gradient pass) instead.
 BERT_GEMM = os.environ.get("DTF_BERT_GEMM", "library")
+# the tied decoder's vocabulary rows are padded to a multiple of this (GEMM tile / 16-B rows)
+VOCAB_ALIGN = 64
+
+
+def padded_vocab(v: int) -> int:
+    return -(-v // VOCAB_ALIGN) * VOCAB_ALIGN
 # FFN: bias + GELU + second GEMM as one op whose data gradient carries the GELU derivative in our
 # GEMM's epilogue (A/B knob)
 FUSE_GELU_DGRAD = os.environ.get("DTF_BERT_FUSE_GELU_DGRAD", "1") == "1"
@@ -151,7 +163,8 @@ class BertForPreTraining(Layer):
         H, std = cfg.hidden_size, cfg.initializer_range
         if H % cfg.num_attention_heads or H // cfg.num_attention_heads != 64:
             raise ValueError("attention kernels are built for head_dim 64")
-        self.word_embeddings = _param((cfg.vocab_size, H), "bert/embeddings/word_embeddings", std)
+        V, Vp = cfg.vocab_size, padded_vocab(cfg.vocab_size)
+        self.word_embeddings = _param((Vp, H), "bert/embeddings/word_embeddings", std)
         self.token_type_embeddings = _param((cfg.type_vocab_size, H),
                                             "bert/embeddings/token_type_embeddings", std)
         self.position_embeddings = _param((cfg.max_position_embeddings, H),
@@ -160,7 +173,17 @@ class BertForPreTraining(Layer):
         self.layers = nn.ModuleList(BertLayer(cfg, i) for i in range(cfg.num_hidden_layers))
         self.mlm_transform = _Dense(H, H, "cls/predictions/transform/dense", std)
         self.mlm_ln = _LayerNorm(H, "cls/predictions/transform/LayerNorm")
-        self.mlm_bias = _param((cfg.vocab_size,), "cls/predictions/output_bias", fill=0.0)
+        self.mlm_bias = _param((Vp,), "cls/predictions/output_bias", fill=0.0)
+        if Vp != V:
+            with torch.no_grad():
+                self.word_embeddings[V:].zero_()
+            # checkpoints / SavedModels carry the TF shapes (the first V rows)
+            self.word_embeddings._dtf_splits = [("bert/embeddings/word_embeddings", 0, V)]
+            self.mlm_bias._dtf_splits = [("cls/predictions/output_bias", 0, V)]
+
+    def num_params_tf(self) -> int:
+        """Parameters of the TF model (the padding rows of the tied vocabulary excluded)."""
+        return sum(t.numel() for _, t, _ in self.variables_tf())
 
     def variables_tf(self):
         for p in self.parameters():
@@ -202,10 +225,12 @@ class BertForPreTraining(Layer):
         h = ops.bias_gelu(self.mlm_transform.gemm(h), self.mlm_transform.bias)
         h = ops.bias_dropout_add_layer_norm(h, None, None, self.mlm_ln.gamma, self.mlm_ln.beta,
                                             0.0, self.training, cfg.layer_norm_eps)
-        logits = ops.dense(h, self.word_embeddings, self.mlm_bias, impl=BERT_GEMM)  # tied decoder
+        # tied decoder over the padded vocabulary [B*P, Vp]; the padding logits are exactly 0
+        logits = ops.dense(h, self.word_embeddings, self.mlm_bias, impl=BERT_GEMM)
+        V = cfg.vocab_size
         if masked_lm_ids is None:
-            return logits
-        return ops.mlm_loss(logits, masked_lm_ids, masked_lm_weights)
+            return logits if logits.shape[-1] == V else logits[:, :V]
+        return ops.mlm_loss(logits, masked_lm_ids, masked_lm_weights, vocab=V)
 
 
 def bert_base(**kw) -> BertForPreTraining:

@@ -175,7 +175,10 @@ def global_avg_pool(x):
 
 def dense(x, w, b=None, relu=False, impl=None, layout="OI"):
     """``impl`` (native path): None/"native" = the hand-written MFMA GEMM with fused bias/ReLU
-    epilogues; "library" = hipBLASLt (a plain library GEMM, used by BERT by default).
+    epilogues (tf.layers.dense); "library" = the bias-in-epilogue form BERT uses: its forward and
+    data gradient run on our persistent MFMA GEMM (gemm_pp2) for every shape that kernel takes
+    (N % 8 == 0, K % 64 == 0 -- all BERT-base layers, the tied decoder on its padded vocabulary
+    included) and fall back to hipBLASLt only for other shapes.
     ``layout``: "OI" (kernel [out, in], tf.layers / BERT) or "IO" ([in, out], the MLP template's
     ``tf.nn.xw_plus_b`` weights)."""
     if _f32(x):
@@ -281,10 +284,12 @@ def attention_qkv(qkv, mask, batch, seq_len, heads, p=0.0, training=True, scale=
     return reference.attention_qkv(qkv, mask, batch, seq_len, heads, p, training, scale)
 
 
-def mlm_loss(logits, labels, weights=None):
+def mlm_loss(logits, labels, weights=None, vocab=None):
+    """Weighted masked-LM cross-entropy.  ``vocab``: the class count when the logits rows are
+    padded past it (BERT's tied decoder runs on a vocabulary padded to a multiple of 64)."""
     if _use_native(logits):
-        return _nlp().mlm_loss(logits, labels, weights)
-    return reference.mlm_loss(logits, labels, weights)
+        return _nlp().mlm_loss(logits, labels, weights, vocab)
+    return reference.mlm_loss(logits, labels, weights, vocab)
 
 
 # ----------------------------------------------------------------------------- variable fence

@@ -29,12 +29,6 @@ except ImportError as e:  # pragma: no cover - exercised on boxes without a buil
 
 _BF16 = torch.bfloat16
 _DENSE_IMPL = os.environ.get("DTF_DENSE", "native")     # native | library (hipBLASLt)
-# library-GEMM dense layers (BERT): weight gradients up to this many elements on our TN wgrad
-# kernel -- 3072 x 768 covers every BERT-base dense layer but the tied MLM decoder; the FFN
-# shapes run at parity with hipBLASLt (0.97 / 1.00x alone, +0.2 % on the step:
-# profiles/measurements/r3_bert_dense_wgrad_native_vs_library.jsonl)
-_DENSE_WGRAD_NATIVE = os.environ.get("DTF_DENSE_WGRAD_NATIVE", "1") == "1"
-_DENSE_WGRAD_NATIVE_MAX = int(os.environ.get("DTF_DENSE_WGRAD_NATIVE_MAX", str(3072 * 768)))
 
 # kernel-variant switches for A/B runs on one box (defaults = the measured best)
 if os.environ.get("DTF_WGRAD_MODE"):
@@ -1593,12 +1587,12 @@ def _dense_weight_grad(w_param, x2, dy2):
     dw = None
     target = _direct_grad(w_param)
     S = _wgrad_splits(T, o, i) if (o * i) % 4 == 0 and dy2.dtype == x2.dtype else 1
-    if (_DENSE_WGRAD_NATIVE and dy2.dtype == _BF16 and x2.dtype == _BF16
-            and o % 8 == 0 and i % 8 == 0 and o * i <= _DENSE_WGRAD_NATIVE_MAX):
+    if dy2.dtype == _BF16 and x2.dtype == _BF16 and o % 8 == 0 and i % 8 == 0:
         # the TN conv weight-gradient kernel, fp32 (straight into the flat buffer when there is
         # one): 1.05-1.40x the split-K library path up to 2304 x 768 (BERT qkv / attention output
         # / MLM transform), 0.97-1.00x on the FFN shapes
-        # (profiles/measurements/r3_bert_dense_wgrad_native_vs_library.jsonl)
+        # (profiles/measurements/r3_bert_dense_wgrad_native_vs_library.jsonl); since the decode-
+        # free dense form (round 5) every BERT-base layer, the padded tied decoder included
         xw, dw4 = x2.contiguous().view(T, 1, 1, i), dy2.contiguous().view(T, 1, 1, o)
         if target is not None:
             conv2d_wgrad(xw, dw4, (o, 1, 1, i), 1, 0, out=target.view(o, 1, 1, i))

@@ -304,9 +304,16 @@ def attention(q, k, v, mask=None, scale=None):
 
 # ----------------------------------------------------------------------------- MLM loss
 class _MlmLoss(torch.autograd.Function):
+    """``vocab``: the class count when the logits rows are padded past it (the tied decoder's
+    vocabulary padded to a multiple of 64): padding columns are not classes and get an exact zero
+    gradient."""
+
     @staticmethod
-    def forward(ctx, logits, labels, weights):
-        N, V = logits.shape
+    def forward(ctx, logits, labels, weights, vocab=None):
+        N, ld = logits.shape
+        V = ld if vocab is None else int(vocab)
+        if not 0 < V <= ld:
+            raise ValueError(f"mlm_loss: vocab {vocab} outside the logits width {ld}")
         lg = logits.to(_BF16).contiguous()
         lab = labels.reshape(-1).long().contiguous()
         w = None if weights is None else weights.reshape(-1).float().contiguous()
@@ -314,8 +321,8 @@ class _MlmLoss(torch.autograd.Function):
         denom = denom.float().contiguous()
         rows = torch.empty(N, device=lg.device, dtype=torch.float32)
         grad = torch.empty_like(lg)
-        _K.mlm_xent(lg.data_ptr(), lab.data_ptr(), _p(w), denom.data_ptr(), N, V, rows.data_ptr(),
-                    grad.data_ptr(), _st())
+        _K.mlm_xent(lg.data_ptr(), lab.data_ptr(), _p(w), denom.data_ptr(), N, V, ld,
+                    rows.data_ptr(), grad.data_ptr(), _st())
         ctx.save_for_backward(grad)
         ctx.ldt = logits.dtype
         # Optimizer.compute_gradients runs loss.backward() with the implicit unit gradient and
@@ -329,9 +336,9 @@ class _MlmLoss(torch.autograd.Function):
     def backward(ctx, g):
         (grad,) = ctx.saved_tensors
         if ctx.dtf_unit_grad and grad.dtype == ctx.ldt:
-            return grad, None, None
-        return (grad * g.to(grad.dtype)).to(ctx.ldt), None, None
+            return grad, None, None, None
+        return (grad * g.to(grad.dtype)).to(ctx.ldt), None, None, None
 
 
-def mlm_loss(logits, labels, weights=None):
-    return _MlmLoss.apply(logits, labels, weights)
+def mlm_loss(logits, labels, weights=None, vocab=None):
+    return _MlmLoss.apply(logits, labels, weights, vocab)

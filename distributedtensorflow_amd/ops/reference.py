@@ -267,8 +267,11 @@ def attention_qkv(qkv, mask, batch, seq_len, heads, p=0.0, training=True, scale=
     return o.permute(0, 2, 1, 3).reshape(B * S, Hh * D).to(qkv.dtype)
 
 
-def mlm_loss(logits, labels, weights=None):
-    """sum_i w_i * nll_i / sum_i w_i  (google-research/bert run_pretraining.py)."""
+def mlm_loss(logits, labels, weights=None, vocab=None):
+    """sum_i w_i * nll_i / sum_i w_i  (google-research/bert run_pretraining.py).  ``vocab``: the
+    class count when the logits rows are padded past it (columns from ``vocab`` on are ignored)."""
+    if vocab is not None and vocab != logits.shape[-1]:
+        logits = logits[..., :vocab]
     nll = F.cross_entropy(logits.float(), labels.reshape(-1).long(), reduction="none")
     if weights is None:
         return nll.mean()

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -149,37 +150,65 @@ class RcclComm:
         self.comm = self.K.rccl_comm_init(uid, self.world, self.rank, self.device.index)
         # highest priority: the collectives should not queue behind compute kernels
         self.stream = torch.cuda.Stream(self.device, priority=-1)
-        # bounded waits: ncclCommAbort from the watchdog on a deadline / async error / epoch bump
+        # bounded waits: ncclCommAbort from the watchdog on a deadline / async error / epoch bump.
+        # The lock guards the handle and the in-flight enqueue count only, and is never held
+        # across a call into RCCL that can block: the communicator is a blocking one, so an
+        # enqueue may wait inside RCCL on a dead peer (lazy connection set-up), and the watchdog
+        # thread must still be able to probe it and abort it then
         self._lock = threading.Lock()
+        self._inuse = 0
         self.wd = _watchdog()
         self.wd.add_abort(self.abort)
         self.wd.add_probe(self._probe)
 
     def _probe(self):
+        # ncclCommGetAsyncError never blocks and is safe beside an in-flight enqueue; the lock
+        # only keeps abort / close from releasing the handle during the call
         with self._lock:
             if not self.comm:
                 return None
             r = self.K.rccl_async_error(self.comm)
         return f"rccl async error {r}" if r not in (0, 7) else None    # 7 = ncclInProgress
 
-    def _issue(self, fn, *tensors, what="collective"):
-        """Enqueue ``fn(comm, stream)``.  The communicator handle is read and used under the
-        lock: the watchdog thread's :meth:`abort` cannot destroy it between the check and the
-        enqueue (it waits for the enqueue, then aborts -- the kernel sees the abort flag)."""
-        self.wd.check()
-        cur = torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)            # the producers of the operands ran before issue
+    def _enqueue(self, fn, stream, what):
+        """Run ``fn(comm, stream)`` (one RCCL enqueue) with the handle pinned by the in-flight
+        count, not by the lock.  The collective's deadline is registered BEFORE the call, so an
+        enqueue that blocks inside RCCL trips the watchdog like a kernel that never completes;
+        returns the completion cell the caller fills with the collective's event."""
+        from .strategy import CommError
+        cell = []
+        self.wd.watch(lambda: bool(cell) and cell[0](), f"rccl {what}")
         with self._lock:
             comm = self.comm
             if not comm:
-                from .strategy import CommError
+                cell.append(lambda: True)
                 raise CommError("rccl communicator was aborted")
-            fn(comm, self.stream.cuda_stream)
+            self._inuse += 1
+        try:
+            fn(comm, stream)
+        except BaseException:
+            cell.append(lambda: True)        # the error is the caller's to report
+            raise
+        finally:
+            with self._lock:
+                self._inuse -= 1
+                aborted = not self.comm
+        if aborted:
+            cell.append(lambda: True)
+            raise CommError(f"rccl communicator was aborted during the {what} enqueue")
+        return cell
+
+    def _issue(self, fn, *tensors, what="collective"):
+        """Enqueue ``fn(comm, stream)`` on the comm stream, ordered after the caller's stream."""
+        self.wd.check()
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)            # the producers of the operands ran before issue
+        cell = self._enqueue(fn, self.stream.cuda_stream, what)
         for t in tensors:
             t.record_stream(self.stream)
         ev = torch.cuda.Event()
         ev.record(self.stream)
-        self.wd.watch(ev.query, f"rccl {what}")
+        cell.append(ev.query)
         return _Done(ev)
 
     @staticmethod
@@ -239,8 +268,10 @@ class RcclComm:
         return self.K.rccl_async_error(self.comm)
 
     def abort(self):
-        """ncclCommAbort (thread-safe against the probe; idempotent): RCCL kernels still spinning
-        on a dead peer see the abort flag and exit, so the comm stream drains."""
+        """ncclCommAbort (idempotent; never waits for an in-flight enqueue): RCCL kernels still
+        spinning on a dead peer see the abort flag and exit, so the comm stream drains, and an
+        enqueue blocked inside RCCL on another thread returns with an error (its caller then
+        raises CommError).  The handle is unpublished first, so no new enqueue starts on it."""
         with self._lock:
             c, self.comm = self.comm, 0
         if c:
@@ -255,8 +286,13 @@ class RcclComm:
         with self._lock:
             c, self.comm = self.comm, 0
         if c:
+            # a graceful destroy frees the communicator: let an enqueue still in RCCL on another
+            # thread leave it first (bounded; a stuck one is the watchdog's, via abort)
+            t0 = time.monotonic()
+            while self._inuse and time.monotonic() - t0 < 30:
+                time.sleep(0.001)
             self.stream.synchronize()
-            self.K.rccl_comm_destroy(c, 0)
+            self.K.rccl_comm_destroy(c, 1 if self._inuse else 0)
 
 
 def make_comm(kind=None, group=None, device=None):

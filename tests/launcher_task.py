@@ -24,6 +24,20 @@ def main():
     print(f"task {a.job_name}:{a.task_index} mode {mode}", flush=True)
     if mode == "hang" and a.job_name == "worker" and a.task_index == 1:
         stalled_wait()
+    if mode == "worker_fail":
+        # asynchronous job: worker 1 dies at once, the chief keeps training and finishes, the PS
+        # returns from join() once the chief is done
+        done = os.path.join(os.environ["LAUNCHER_TASK_DIR"], "done_worker0")
+        if a.job_name == "worker" and a.task_index == 1:
+            sys.exit(5)
+        if a.job_name == "worker":
+            time.sleep(2.0)
+            open(done, "w").close()
+            return 0
+        t0 = time.time()
+        while not os.path.exists(done) and time.time() - t0 < 30:
+            time.sleep(0.05)
+        return 0
     if mode == "ps_fail":
         ready = os.environ.get("LAUNCHER_TASK_DIR")
         if a.job_name == "ps":

@@ -41,6 +41,26 @@ def test_task_failing_for_good_ends_the_job_at_once(tmp_path):
     assert "stalled_wait" in text["worker1"]          # stack dumped before the stop
 
 
+@pytest.mark.parametrize("sync", [False, True])
+def test_worker_failing_in_async_job_leaves_the_chief_training(tmp_path, sync):
+    """in asynchronous between-graph training a worker that fails for good does not
+    end the job -- the chief trains on and finishes (TF1 semantics); a synchronous job (every step
+    needs every worker) is stopped at once instead."""
+    codes, logs = launch_local(TASK, 1, 2, str(tmp_path),
+                               env={"LAUNCHER_TASK_MODE": "worker_fail",
+                                    "LAUNCHER_TASK_DIR": str(tmp_path)},
+                               timeout_s=60, grace_s=5, sync=sync)
+    text = {k: open(v).read() for k, v in logs.items()}
+    assert codes[("worker", 1)] == 5
+    if sync:
+        assert codes[("worker", 0)] != 0
+        assert "worker1 failed for good (exit 5); stopping worker0" in text["worker0"]
+    else:
+        assert codes[("worker", 0)] == 0 and codes[("ps", 0)] == 0
+        assert "the other tasks continue" in text["worker1"]
+        assert "stopping" not in text["worker0"] and "stopping" not in text["ps0"]
+
+
 def test_epoch_arrival_barrier_names_the_missing_rank():
     import datetime
 

@@ -42,8 +42,13 @@ def test_bert_base_size_and_tf_names():
               "cls/predictions/transform/dense/kernel", "cls/predictions/output_bias"):
         assert n in names, n
     assert not any("qkv" in n for n in names)
+    shapes = {n: tuple(t.shape) for n, t, _ in collect_variables(m)}
+    assert shapes["bert/embeddings/word_embeddings"] == (30522, 768)
+    assert shapes["cls/predictions/output_bias"] == (30522,)
     total = sum(t.numel() for _, t, _ in collect_variables(m))
-    assert total == num_params(m)
+    assert total == m.num_params_tf()
+    # the tied vocabulary is stored padded to 30528 rows (table and output bias)
+    assert num_params(m) == total + 6 * (768 + 1)
 
 
 def test_bert_param_count_exact():
@@ -52,7 +57,47 @@ def test_bert_param_count_exact():
     per_layer = 4 * (H * H + H) + 2 * 2 * H + (H * I + I) + (I * H + H)
     emb = (V + 512 + 2) * H + 2 * H
     head = H * H + H + 2 * H + V
-    assert num_params(BertForPreTraining(cfg)) == emb + L * per_layer + head
+    assert BertForPreTraining(cfg).num_params_tf() == emb + L * per_layer + head
+
+
+def test_bert_padded_vocab_is_the_unpadded_model_cpu():
+    """The tied decoder's vocabulary rows are padded to a multiple of 64 (1000 -> 1024 here):
+    the padding rows start at zero, receive an exact zero gradient (the loss leaves their logits
+    out of the softmax, ids never gather them) and stay zero through LAMB updates, the loss
+    equals the unpadded model's, and checkpoints hold the TF shapes."""
+    from distributedtensorflow_amd.models.bert import padded_vocab
+    from distributedtensorflow_amd.train import Saver, list_variables
+    torch.manual_seed(0)
+    cfg = BertConfig(**TINY, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    V, Vp = cfg.vocab_size, padded_vocab(cfg.vocab_size)
+    assert Vp == 1024
+    m = BertForPreTraining(cfg)
+    assert m.word_embeddings.shape == (Vp, 256) and m.mlm_bias.shape == (Vp,)
+    assert torch.count_nonzero(m.word_embeddings[V:]) == 0
+    batch = _batch()
+    # the loss of the padded model == cross-entropy over the first V logits of an unpadded head
+    ids, tt, am, pos, lab, w = batch
+    logits = m(ids, tt, am, pos)
+    assert logits.shape == (4 * 10, V)
+    ref = R.mlm_loss(logits, lab, w)
+    with OneDeviceStrategy("cpu").scope():
+        opt = LAMBOptimizer(5e-3, weight_decay=0.01)
+        loss = m(*batch)
+        torch.testing.assert_close(loss, ref)
+        g = opt.compute_gradients(loss, list(m.parameters()))
+        grads = {id(v): gv for gv, v in g}
+        assert torch.count_nonzero(grads[id(m.word_embeddings)][V:]) == 0
+        assert torch.count_nonzero(grads[id(m.mlm_bias)][V:]) == 0
+        opt.apply_gradients(g)
+        for _ in range(3):
+            opt.minimize(m(*batch))
+    assert torch.count_nonzero(m.word_embeddings.detach()[V:]) == 0
+    assert torch.count_nonzero(m.mlm_bias.detach()[V:]) == 0
+    names = dict(list_variables(Saver(model=m, optimizer=opt).save(None, str(
+        __import__("tempfile").mkdtemp()) + "/bert.ckpt")))
+    assert names["bert/embeddings/word_embeddings"] == [V, 256]
+    assert names["cls/predictions/output_bias"] == [V]
+    assert names["bert/embeddings/word_embeddings/adam_m"] == [V, 256]
 
 
 def test_bert_tiny_trains_with_lamb_cpu():
@@ -523,3 +568,60 @@ def test_dense_gelu_dense_fused_epilogue(T, H, I):
         scale = r.abs().max()
         assert (g - r).abs().max() <= 2e-2 * scale, (name, ((g - r).abs().max() / scale).item())
         assert (g - u).abs().max() <= 2e-2 * scale, (name, ((g - u).abs().max() / scale).item())
+
+
+@pytest.mark.gpu
+def test_tied_decoder_padded_vocab_on_our_kernels(monkeypatch):
+    """BERT's tied MLM decoder on the padded vocabulary (768 -> 30528, 30522 classes): forward,
+    data gradient and weight gradient run on our GEMM / weight-gradient kernels -- the torch
+    (hipBLASLt) entry points are booby-trapped -- and match an fp32 reference over the 30522
+    classes; the 6 padding logits are exactly 0 and the padding rows of the table and the bias
+    get exactly zero gradient."""
+    from distributedtensorflow_amd.ops import native
+    torch.manual_seed(0)
+    T, H, V, Vp = 1000, 768, 30522, 30528
+    h32 = torch.randn(T, H)
+    w32 = torch.randn(Vp, H) * 0.05
+    w32[V:] = 0
+    b32 = torch.randn(Vp) * 0.1
+    b32[V:] = 0
+    lab = torch.randint(0, V, (T,))
+    lab[:2] = torch.tensor([V - 1, V - 2])         # classes next to the padding
+    wts = (torch.rand(T) > 0.2).float()
+
+    def trap(*a, **k):
+        raise AssertionError("library GEMM called on the decoder path")
+
+    for mod, name in ((torch.nn.functional, "linear"), (torch, "mm"), (torch, "bmm"),
+                      (torch, "addmm"), (torch, "matmul"), (torch.Tensor, "__matmul__"),
+                      (torch.Tensor, "addmm_")):
+        monkeypatch.setattr(mod, name, trap)
+    h = _leaf(h32)
+    w = _leaf(w32, torch.float32)
+    b = _leaf(b32, torch.float32)
+    calls = []
+    orig = native._K.conv_wgrad
+    monkeypatch.setattr(native._K, "conv_wgrad", lambda *a: (calls.append(1), orig(*a))[1])
+    logits = ops.dense(h, w, b, impl="library")
+    assert logits.shape == (T, Vp)
+    loss = ops.mlm_loss(logits, lab.cuda(), wts.cuda(), vocab=V)
+    loss.backward()
+    torch.cuda.synchronize()
+    monkeypatch.undo()
+    assert calls, "the decoder weight gradient did not run on our wgrad kernel"
+    lg = logits.detach().float().cpu()
+    assert torch.count_nonzero(lg[:, V:]) == 0
+    assert torch.count_nonzero(w.grad[V:]) == 0 and torch.count_nonzero(b.grad[V:]) == 0
+    # fp32 reference over the classes only, on the same bf16-rounded operands
+    h_ = h32.bfloat16().float().requires_grad_(True)
+    w_ = w32[:V].bfloat16().float().requires_grad_(True)
+    b_ = b32[:V].clone().requires_grad_(True)
+    lg_ = h_ @ w_.t() + b_
+    loss_ = R.mlm_loss(lg_, lab, wts)
+    loss_.backward()
+    for name, got, ref in (("logits", lg[:, :V], lg_.detach()), ("dx", h.grad.float().cpu(), h_.grad),
+                           ("dw", w.grad[:V].cpu(), w_.grad), ("db", b.grad[:V].cpu(), b_.grad)):
+        scale = ref.abs().max()
+        err = (got - ref).abs().max()
+        assert err <= 2e-2 * scale, (name, (err / scale).item())
+    torch.testing.assert_close(loss.detach().cpu(), loss_.detach(), atol=2e-3, rtol=2e-3)

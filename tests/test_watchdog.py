@@ -253,3 +253,59 @@ def test_hung_rank_ends_the_job_loudly(tmp_path):
     assert "rank 1 hangs" in text["rank1"]
     assert "failed for good" in text["rank1"]
     assert took < 90, took
+
+
+def test_watchdog_aborts_a_communicator_blocked_inside_an_enqueue():
+    """the native communicator is a blocking one, so an enqueue can wait inside RCCL
+    on a dead peer.  The watchdog must still probe it, trip on the collective's deadline (which
+    is registered before the enqueue) and call ncclCommAbort -- which releases the blocked
+    enqueue, whose caller then gets CommError -- without waiting for that enqueue."""
+    import threading
+
+    from distributedtensorflow_amd.parallel.comm import RcclComm
+    from distributedtensorflow_amd.parallel.strategy import CommError
+    from distributedtensorflow_amd.parallel.watchdog import CommWatchdog
+
+    entered, released, log = threading.Event(), threading.Event(), []
+
+    class K:
+        def rccl_async_error(self, comm):
+            log.append(("probe", comm))
+            return 0
+
+        def rccl_comm_destroy(self, comm, abort):
+            log.append(("destroy", comm, abort))
+            released.set()                       # ncclCommAbort unblocks the stuck enqueue
+
+        def rccl_all_reduce(self, comm):
+            entered.set()
+            assert released.wait(20), "enqueue never released"
+
+    c = object.__new__(RcclComm)
+    c.K, c.comm, c._lock, c._inuse = K(), 77, threading.Lock(), 0
+    c.wd = CommWatchdog(timeout_s=0.5, interval_s=0.02)
+    c.wd.add_abort(c.abort)
+    c.wd.add_probe(c._probe)
+    err = []
+
+    def issue():
+        try:
+            c._enqueue(lambda comm, st: c.K.rccl_all_reduce(comm), 0, "all_reduce")
+        except CommError as e:
+            err.append(e)
+
+    t = threading.Thread(target=issue, daemon=True)
+    t.start()
+    assert entered.wait(5)
+    n_probes = sum(1 for e in log if e[0] == "probe")
+    time.sleep(0.1)
+    # the probe keeps running while the enqueue is blocked (it never waits on the enqueue)
+    assert sum(1 for e in log if e[0] == "probe") > n_probes
+    assert c.wd.wait_tripped(10), "the blocked enqueue never tripped the deadline"
+    assert "all_reduce did not complete" in c.wd.failed
+    t.join(10)
+    assert not t.is_alive()
+    assert ("destroy", 77, 1) in log and c.comm == 0 and c._inuse == 0
+    assert err and "aborted during the all_reduce enqueue" in str(err[0])
+    with pytest.raises(CommError):
+        c._enqueue(lambda comm, st: None, 0, "broadcast")
