@@ -63,10 +63,11 @@ def parse():
     p.add_argument("--impl", choices=("dtf", "torch"), default="dtf")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--lr", type=float, default=0.1)
-    p.add_argument("--bucket-mb", default="64",
-                   help="all-reduce bucket size in MB, or 'auto': at N > 1, after the warm-up, "
-                        "time 2 steps at each of 16/32/64/128 MB (max over ranks) and keep the "
-                        "fastest for the timed steps (SURVEY.md 5.8)")
+    p.add_argument("--bucket-mb", default=None,
+                   help="all-reduce bucket size in MB, or 'auto' (the default when N > 1; 64 at "
+                        "N = 1, where nothing is reduced): after the warm-up, time 2 steps at each "
+                        "of 16/32/64/128 MB (max over ranks) and keep the fastest for the timed "
+                        "steps (SURVEY.md 5.8)")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--cudnn-benchmark", type=int, default=1,
                    help="--impl torch: 1 = MIOpen exhaustive algorithm search on first use "
@@ -87,7 +88,9 @@ def parse():
                         "--num-workers worker tasks (between-graph, Hogwild pushes applied on "
                         "arrival; utils/ps_bench.py)")
     p.add_argument("--num-ps", type=int, default=1)
-    p.add_argument("--num-workers", type=int, default=1, help="ps_async: worker tasks")
+    p.add_argument("--num-workers", type=int, default=None,
+                   help="ps_async: worker tasks (default: --gpus, one worker per GPU; more "
+                        "workers than GPUs share them round-robin)")
     p.add_argument("--timeout", type=float, default=900, help="ps_async: launcher timeout (s)")
     # set by the ps_async launcher on its tasks (cluster/launcher.py)
     p.add_argument("--job_name", default=None, help=argparse.SUPPRESS)
@@ -108,8 +111,12 @@ def parse():
                    help="seconds any timed step (and the final drain) may take before the bench "
                         "dumps stacks and exits non-zero (0 = no deadline)")
     args = p.parse_args()
+    if args.bucket_mb is None:
+        args.bucket_mb = "auto" if args.gpus > 1 else "64"
     args.bucket_auto = args.bucket_mb == "auto"
     args.bucket_mb = 64.0 if args.bucket_auto else float(args.bucket_mb)
+    if args.num_workers is None:
+        args.num_workers = max(args.gpus, 1)
     if args.batch is None:
         args.batch = 512 if args.model == "bert_base" else 1984
     return args
@@ -365,6 +372,15 @@ def fail(msg, code=2):
     sys.exit(code)
 
 
+def refuse_probes():
+    """Timing probes produce wrong results: a bench never runs with one requested, and never on
+    a probe build of the extension (csrc: -DDTF_PROBES)."""
+    bad = [k for k in os.environ if k.startswith("DTF_") and "PROBE" in k]
+    if bad:
+        fail(f"timing-probe variables set ({', '.join(sorted(bad))}): probes give wrong results "
+             "and are never benchmarked")
+
+
 def share_device():
     """``DTF_BENCH_SHARE_DEVICE=1`` (with ``DTF_BENCH_BACKEND=gloo``): every rank on cuda:0 -- the
     multi-rank rehearsal on a one-GPU box (RCCL refuses two ranks on one device)."""
@@ -462,6 +478,7 @@ class Deadline:
 
 def main():
     args = parse()
+    refuse_probes()
     if args.strategy == "ps_async":
         from distributedtensorflow_amd.utils import ps_bench
         if args.job_name:
@@ -508,8 +525,12 @@ def main():
         if ops.get_backend() == "reference":
             raise SystemExit("bench.py --impl dtf refuses DTF_OPS_BACKEND=reference: the "
                              "measured step must run this framework's HIP kernels")
+        if native.kernels().probes_built():
+            fail("the HIP extension is a probe build (-DDTF_PROBES): rebuild without it")
         native_info = {"backend": ops.get_backend(),
                        "native_ext": os.path.relpath(native.extension_path(), ROOT)}
+    from distributedtensorflow_amd.utils import dtf_env
+    native_info["dtf_env"] = dtf_env()
 
     # the process group that carried the gradients ("nccl" = RCCL on ROCm; None at N = 1)
     native_info["comm_backend"] = dist.get_backend() if dist.is_initialized() else None

@@ -441,6 +441,14 @@ PYBIND11_MODULE(_dtf_hip, m) {
   m.def("conv_stats_rows", &dtf_conv_stats_rows, py::arg("M"), py::arg("Kout"), py::arg("C") = 0,
         py::arg("taps") = 1, py::arg("W") = 0);
   m.def("conv_set_halo", &dtf_conv_set_halo);
+  // a probe build (-DDTF_PROBES) carries wrong-result timing probes: bench.py / smoke() refuse it
+  m.def("probes_built", []() {
+#ifdef DTF_PROBES
+    return true;
+#else
+    return false;
+#endif
+  });
   m.def("conv_set_bnl_probe", &dtf_conv_set_bnl_probe);
   m.def("gemm_stream_set_bnb_probe", &dtf_gemm_stream_set_bnb_probe);
   m.def("conv_tile_rows", [](std::vector<int> geom, std::vector<int> dh, std::vector<int> dw,

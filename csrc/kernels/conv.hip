@@ -1340,9 +1340,18 @@ void dtf_conv_set_halo_freg(int v) { g_halo_freg = v; }
 // 3 / 4: deeper rings; family 1 keeps two blocks per CU at 4, family 2 only with two strips)
 static int g_halo_stages = 0;
 void dtf_conv_set_halo_stages(int v) { g_halo_stages = v; }
-// timing probe: the BN-on-load forward without its y stores (wrong results downstream)
+// timing probe: the BN-on-load forward without its y stores (wrong results downstream).  Only in
+// a probe build (-DDTF_PROBES, tools only): the default build has no such kernel and refuses
+#ifdef DTF_PROBES
 static int g_bnl_probe = 0;
 void dtf_conv_set_bnl_probe(int v) { g_bnl_probe = v; }
+#else
+static constexpr int g_bnl_probe = 0;
+void dtf_conv_set_bnl_probe(int v) {
+  if (v) throw std::runtime_error("conv_set_bnl_probe: a timing probe with wrong results; build "
+                                  "with DTF_HIP_EXTRA_FLAGS=-DDTF_PROBES (tools only)");
+}
+#endif
 
 template <int C, int W, int WMW, int NT, int ST, bool BNB, int NSTG>
 static void launch_halo_ring(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom& g,
@@ -1370,8 +1379,12 @@ static void launch_halo(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const Conv
   if (g.ly) {
     if (bnb.part || freg_on || nstg == 3 || nstg == 4 || strips != 1)
       throw std::runtime_error("halo conv: BN on load needs the default forward ring kernel");
+#ifdef DTF_PROBES
     auto kern = g_bnl_probe ? conv3x3_halo_kernel<C, W, WMW, NT, 1, false, false, 2, true, 1>
                             : conv3x3_halo_kernel<C, W, WMW, NT, 1, false, false, 2, true>;
+#else
+    auto kern = conv3x3_halo_kernel<C, W, WMW, NT, 1, false, false, 2, true>;
+#endif
     const size_t lds = Hc::lds(1) + (size_t)2 * C * sizeof(float);    // + the BN scale / shift
     static bool attr[2] = {false, false};
     if (!attr[g_bnl_probe ? 1 : 0]) {

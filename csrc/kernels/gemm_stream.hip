@@ -567,8 +567,11 @@ void launch_stream(const StreamArgs& g, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(kST), LDS, st, g);
 }
 
-// timing probe of the kind-1 BN-backward epilogue (PROBE bits 4 / 8 above; wrong results)
+// timing probe of the kind-1 BN-backward epilogue (PROBE bits 4 / 8 above; wrong results): only
+// in a probe build (-DDTF_PROBES, tools only)
+#ifdef DTF_PROBES
 static int g_stream_bnb_probe = 0;
+#endif
 
 template <int K, int MODE>
 void launch_stream_bnb(const StreamArgs& g, int bmk, hipStream_t st) {
@@ -584,12 +587,16 @@ void launch_stream_bnb(const StreamArgs& g, int bmk, hipStream_t st) {
   }
   if (g.bxp) launch_stream<K, MODE, false, 1, false, 0, true>(g, st);
   else if (bmk == 1) {
+#ifdef DTF_PROBES
     switch (g_stream_bnb_probe) {
       case 4: launch_stream<K, MODE, false, 1, false, 4>(g, st); break;
       case 8: launch_stream<K, MODE, false, 1, false, 8>(g, st); break;
       case 12: launch_stream<K, MODE, false, 1, false, 12>(g, st); break;
       default: launch_stream<K, MODE, false, 1>(g, st); break;
     }
+#else
+    launch_stream<K, MODE, false, 1>(g, st);
+#endif
   }
   else if (bmk == 2) launch_stream<K, MODE, false, 2>(g, st);
   else launch_stream<K, MODE, false, 0>(g, st);
@@ -729,11 +736,22 @@ void dtf_gemm_stream_apply(const bf16_t* A, const bf16_t* W, bf16_t* Y, int M, i
   run_stream(g, K, -1, st);
 }
 
+#ifdef DTF_PROBES
 void dtf_gemm_stream_set_bnb_probe(int v) { g_stream_bnb_probe = v; }
+#else
+void dtf_gemm_stream_set_bnb_probe(int v) {
+  if (v) throw std::runtime_error("gemm_stream_set_bnb_probe: a timing probe with wrong results; "
+                                  "build with DTF_HIP_EXTRA_FLAGS=-DDTF_PROBES (tools only)");
+}
+#endif
 
 // timing probes of the plain K = 256 kernel (see PROBE above)
 void dtf_gemm_stream_probe(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int probe,
                            hipStream_t st) {
+#ifndef DTF_PROBES
+  (void)A; (void)B; (void)C; (void)M; (void)N; (void)probe; (void)st;
+  throw std::runtime_error("gemm_stream_probe: timing probes need a DTF_PROBES build (tools only)");
+#else
   if (!dtf_gemm_stream_ok(M, N, 256, 256, 256, N)) throw std::runtime_error("stream probe shape");
   StreamArgs g{A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, 256, 256, N, 0};
   switch (probe) {
@@ -746,4 +764,5 @@ void dtf_gemm_stream_probe(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, i
     case 15: launch_stream<256, 0, false, -1, false, 15>(g, st); break;
     default: launch_stream<256, 0, false, -1, false, 0>(g, st); break;
   }
+#endif
 }

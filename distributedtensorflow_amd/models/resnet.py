@@ -74,11 +74,6 @@ FUSE_PROJ_BN = os.environ.get("DTF_FUSE_PROJ_BN", "1") == "1"
 # bottleneck c2's BN + ReLU inside c3's GEMM (ops.batch_norm_relu_conv1x1; falls back to the two
 # ops off the streaming route)
 FUSE_BN_CONV = os.environ.get("DTF_FUSE_BN_CONV", "1") == "1"
-# projection blocks: c1's backward after the projection's (A/B knob, off: the input BN's reduce
-# pass goes away, 1.5 ms/step, but c1's streamed dgrad then reads x and accumulates onto the
-# projection's output, +1.8 ms, and the stride-2 projection's dgrad must zero-fill 3/4 of d(x),
-# +0.8 ms -- profiles/measurements/r5_c1_last_backward_ab.jsonl)
-C1_LAST_BWD = os.environ.get("DTF_C1_LAST_BWD", "0") == "1"
 # c1's BatchNorm + ReLU applied on the c2 3x3 conv's input load (ops.batch_norm(defer=True): the
 # halo kernels normalise their patch in LDS and write the BN output once; other c2 shapes fall
 # back to the apply pass); A/B knob, see also ops/native.py DTF_BN_ON_LOAD
@@ -108,17 +103,13 @@ class Bottleneck(nn.Module):
         share = ops.GradShare(2) if self.has_proj else None
         if self.has_proj and FUSE_PROJ_BN:
             # the shortcut's BN is applied inside the block-output BN (one pass forward, one
-            # reduce + one apply pass backward for both).  C1_LAST_BWD builds c1 before the
-            # projection so autograd runs c1's backward last: its streamed dgrad then completes
-            # d(x) and forms the input BN's backward sums (measured slower, see C1_LAST_BWD)
+            # reduce + one apply pass backward for both).  (Building c1 before the projection,
+            # so that c1's streamed dgrad completes d(x), measured 0.7 % slower:
+            # profiles/measurements/r5_c1_last_backward_ab.jsonl)
             p, b = self.proj, self.proj.bn
-            if not C1_LAST_BWD:
-                sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
-                                bn_stats=b.training, grad_share=share)
+            sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
+                            bn_stats=b.training, grad_share=share)
             y = self._c2_c3(self.c1(x, grad_share=share, defer_bn=self.c2_bn_on_load))
-            if C1_LAST_BWD:
-                sc = ops.conv2d(x, p.conv.kernel, p.conv.strides, p.conv.padding,
-                                bn_stats=b.training, grad_share=share)
             c, b3 = self.c3, self.c3.bn
             return ops.batch_norm_add_batch_norm(
                 y, b3.gamma, b3.beta, b3.moving_mean, b3.moving_variance, sc, b.gamma, b.beta,

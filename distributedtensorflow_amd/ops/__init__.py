@@ -42,13 +42,13 @@ def _native():
     return native
 
 
-def native_join_wgrad_side():
-    """Join the native ops' side stream (weight gradients written into the flat gradient buffer
-    off the compute stream) into the compute stream; a no-op when the extension is not loaded."""
+def end_step():
+    """Release the native ops' deferred-work records of the step whose backward just returned
+    (:mod:`.records`: no record outlives its step); called by ``Optimizer.compute_gradients``.
+    Returns the number released (0 when no native op ran)."""
     import sys
-    m = sys.modules.get(__name__ + ".native")
-    if m is not None:
-        m.join_wgrad_side()
+    m = sys.modules.get(__name__ + ".records")
+    return m.end_step() if m is not None else 0
 
 
 def _f32(t: torch.Tensor) -> bool:

@@ -13,10 +13,15 @@ Precision contract (mixed precision, TF-style "float32 variables, bf16 compute")
 from __future__ import annotations
 
 import os
-import weakref
 
 import torch
 
+from .records import BnDeferred as _BnDeferred  # noqa: F401  (deferred-work records)
+from .records import GradSlot as _GradSlot
+from .records import LazyBnDx as _LazyBnDx
+from .records import MaskedGrad as _MaskedGrad
+from .records import Recompute as _Recompute
+from .records import end_step as end_step  # noqa: F401
 from .reference import resolve_padding, space_to_depth_operands  # noqa: F401
 
 try:
@@ -37,14 +42,6 @@ if os.environ.get("DTF_WGRAD_PP"):       # ping-pong wgrad: 0 off, n: split-K ta
     _K.wgrad_set_pp(int(os.environ["DTF_WGRAD_PP"]))
 if os.environ.get("DTF_WGRAD_DENSE"):    # ping-pong wgrad's decode-free one-tap form: 0 off
     _K.wgrad_set_dense(int(os.environ["DTF_WGRAD_DENSE"]))
-if os.environ.get("DTF_WGRAD_DIRECT"):   # ping-pong wgrad: per-row decode (1) / shuffles (0)
-    _K.wgrad_set_direct(int(os.environ["DTF_WGRAD_DIRECT"]))
-if os.environ.get("DTF_BNL_PROBE"):      # timing probe: BN-on-load forward without its y stores
-    _K.conv_set_bnl_probe(int(os.environ["DTF_BNL_PROBE"]))
-if os.environ.get("DTF_STREAM_BNB_PROBE"):   # timing probe: BN-backward stream GEMM (wrong results)
-    _K.gemm_stream_set_bnb_probe(int(os.environ["DTF_STREAM_BNB_PROBE"]))
-if os.environ.get("DTF_WGRAD_DEEP"):     # ping-pong wgrad: 5-slot 32-pixel ring (1) / 2 x 64 (0)
-    _K.wgrad_set_deep(int(os.environ["DTF_WGRAD_DEEP"]))
 if os.environ.get("DTF_WGRAD_PIPE"):
     _K.wgrad_set_pipe(int(os.environ["DTF_WGRAD_PIPE"]))
 if os.environ.get("DTF_CONV_DMA"):
@@ -57,8 +54,6 @@ if os.environ.get("DTF_CONV_STEM_HALO"):
     _K.conv_set_stem_halo(int(os.environ["DTF_CONV_STEM_HALO"]))
 if os.environ.get("DTF_CONV_HALO_STRIPS"):     # bit f: two strips per block for halo family f
     _K.conv_set_halo_strips(int(os.environ["DTF_CONV_HALO_STRIPS"]))
-if os.environ.get("DTF_CONV_HALO_STAGES"):     # nibble f-1: filter-ring depth of halo family f
-    _K.conv_set_halo_stages(int(os.environ["DTF_CONV_HALO_STAGES"], 0))
 if os.environ.get("DTF_CONV_HALO_FREG"):       # bit f: halo family f streams its filter via VGPRs
     _K.conv_set_halo_freg(int(os.environ["DTF_CONV_HALO_FREG"]))
 if os.environ.get("DTF_CONV_SMALL_K"):
@@ -120,47 +115,19 @@ def _direct_grad(p):
     return g
 
 
-# Conv weight gradients written straight into the flat gradient buffer run on a side stream
-# (A/B knob DTF_WGRAD_SIDE_STREAM): they depend only on (x, dy) and nothing in backward reads
-# them, so they overlap the data-gradient chain -- in particular its HBM-bound BatchNorm passes,
-# which leave the MFMA / LDS units of the CUs idle.  The side stream forks from the compute
-# stream per weight gradient and joins it (1) before a gradient bucket's all-reduce is issued
-# (join_wgrad_side, called by the reducers) and (2) at the end of every backward pass (an autograd
-# final callback), so every reader of the flat buffer is ordered after the writes.
-# measured neutral at ResNet-50 b1984 (16,471 vs 16,470 img/s same box, depth 2/4/8 alike:
-# profiles/measurements/r5_wgrad_side_stream_ab.jsonl) -- off by default
-_WGRAD_SIDE = os.environ.get("DTF_WGRAD_SIDE_STREAM", "0") == "1"
-_SIDE = {}          # device index -> (side stream, compute stream it forks from)
-_side_join_queued = False
-# operands of the queued side-stream weight gradients, kept alive (instead of record_stream,
-# whose deferred frees stalled the caching allocator: 7x slower) until the compute stream has
-# joined the side stream; at most _SIDE_DEPTH layers are in flight (bounded extra memory)
-_SIDE_KEEP = []
-_SIDE_DEPTH = int(os.environ.get("DTF_WGRAD_SIDE_DEPTH", "4"))
+# Kernel variants measured neutral or slower (the wgrad DEEP / EARLY schedules, the per-row and
+# readlane pixel decodes, deeper halo filter rings) are no longer reachable from the environment:
+# their C++ setters stay for the bit-identity tests; the conv weight gradient on a side stream
+# (neutral at b1984, profiles/measurements/r5_wgrad_side_stream_ab.jsonl) was removed.
 
 
-def _wgrad_side(dev):
-    main = torch.cuda.current_stream(dev)
-    ent = _SIDE.get(dev.index)
-    if ent is None or ent[1] != main:
-        ent = _SIDE[dev.index] = (ent[0] if ent is not None else torch.cuda.Stream(dev), main)
-    return ent[0], main
-
-
-def join_wgrad_side():
-    """Order every compute stream after the weight gradients queued on its side stream."""
-    global _side_join_queued
-    _side_join_queued = False
-    for side, main in _SIDE.values():
-        main.wait_stream(side)
-    _SIDE_KEEP.clear()          # the compute stream is ordered after every use: reusable
-
-
-def _queue_side_join():
-    global _side_join_queued
-    if not _side_join_queued:
-        _side_join_queued = True
-        torch.autograd.Variable._execution_engine.queue_callback(join_wgrad_side)
+def enable_timing_probe(name, value=1):
+    """Tools only: switch on a timing probe that produces WRONG results (``"bnl"`` the BN-on-load
+    forward without its y stores, ``"stream_bnb"`` the BN-backward stream GEMM epilogue probes).
+    They exist only in a probe build (``DTF_HIP_EXTRA_FLAGS=-DDTF_PROBES``); the default build
+    raises.  Never reachable from the environment or from training code."""
+    setter = {"bnl": _K.conv_set_bnl_probe, "stream_bnb": _K.gemm_stream_set_bnb_probe}[name]
+    setter(int(value))
 
 
 def _grad_ready(p):
@@ -225,27 +192,6 @@ def _launch_fwd(x, wmat, K, taps, P, Q, sh, sw, out, Ho, Wo, osh=1, osw=1, oh0=0
         return
     _K.conv_igemm(x.data_ptr(), wmat.data_ptr(), out.data_ptr(), geom, dh, dw, 64, _st(),
                   _p(stats), list(bnb), 0, 0, _p(bias), int(relu))
-
-
-class _BnDeferred:
-    """A BatchNorm + ReLU output whose apply pass has not run (``batch_norm(..., defer=True)``):
-    the consuming 3x3 conv normalises its input on load and writes ``y`` itself (halo kernels,
-    csrc/kernels/conv.hip BNL); any other use materialises it first with the apply pass."""
-    __slots__ = ("x", "scale", "shift", "y", "done")
-
-    def __init__(self, x, scale, shift, y):
-        # y holds this record: a weak reference back keeps them out of a reference cycle (a
-        # cycle left every step's y to the cyclic collector: +2.9 GB of peak memory per step)
-        self.x, self.scale, self.shift, self.y, self.done = x, scale, shift, weakref.ref(y), False
-
-    def materialize(self):
-        y = self.y()
-        if not self.done and y is not None:
-            C = self.x.shape[-1]
-            _K.bn_apply(self.x.data_ptr(), 0, y.data_ptr(), self.scale.data_ptr(),
-                        self.shift.data_ptr(), self.x.numel() // C, C, 1, _st(), 0)
-            self.done = True
-        return y
 
 
 def _bnl_pending(x):
@@ -604,18 +550,7 @@ class _Conv2d(torch.autograd.Function):
             # weight gradient first: it only depends on dy, so the bucketed all-reduce of this
             # layer can start while dgrad still runs
             target = _direct_grad(ctx.w_param)
-            if (target is not None and not padded and _WGRAD_SIDE
-                    and not torch.cuda.is_current_stream_capturing()):
-                if len(_SIDE_KEEP) >= _SIDE_DEPTH:
-                    join_wgrad_side()
-                side, main = _wgrad_side(dy.device)
-                side.wait_stream(main)                 # dy (and x) are ready on the compute stream
-                with torch.cuda.stream(side):
-                    conv2d_wgrad(xb, dy, wb.shape, ctx.stride, ctx.padding, out=target)
-                _SIDE_KEEP.append((xb, dy))
-                _queue_side_join()
-                _grad_ready(ctx.w_param)
-            elif target is not None and not padded:
+            if target is not None and not padded:
                 conv2d_wgrad(xb, dy, wb.shape, ctx.stride, ctx.padding, out=target)
                 _grad_ready(ctx.w_param)
             else:
@@ -807,42 +742,6 @@ _LAZY_RESIDUAL_GRAD = os.environ.get("DTF_LAZY_RESIDUAL_GRAD", "1") == "1"
 _FUSE_STEM_POOL_BWD = os.environ.get("DTF_FUSE_STEM_POOL_BWD", "1") == "1"
 
 
-class _MaskedGrad:
-    """d(residual) of a residual+ReLU BatchNorm kept as (dy, forward ReLU bit mask) rather
-    than a materialised bf16 tensor; the identity-shortcut dgrad adds dy * mask in its epilogue."""
-
-    __slots__ = ("dy", "mask")
-
-    def __init__(self, dy, mask):
-        self.dy, self.mask = dy, mask
-
-    def materialize(self):
-        out = torch.empty_like(self.dy)
-        _K.relu_mask_apply(self.dy.data_ptr(), self.mask.data_ptr(), out.data_ptr(),
-                           self.dy.numel(), _st())
-        return out
-
-
-class _LazyBnDx:
-    """d(x) of a residual BatchNorm + ReLU, not yet formed: dx = A (dy * mask) + B x + C per
-    channel.  A fused conv backward that consumes it forms it per tile (bit-identical to the
-    apply pass); anything else materialises it with that pass."""
-    __slots__ = ("dy", "x", "mask", "gb")
-
-    def __init__(self, dy, x, mask, gb):
-        self.dy, self.x, self.mask, self.gb = dy, x, mask, gb
-
-    def materialize(self):
-        C = self.x.shape[-1]
-        M = self.x.numel() // C
-        dx = torch.empty_like(self.x)
-        _materialized(self.x)
-        _K.bn_bwd_apply(self.dy.data_ptr(), 0, self.x.data_ptr(), self.gb[2].data_ptr(),
-                        self.gb[3].data_ptr(), self.gb[4].data_ptr(), dx.data_ptr(), 0, M, C, 1,
-                        _st(), 0, 0, self.mask.data_ptr())
-        return dx
-
-
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu,
@@ -920,13 +819,6 @@ class _BatchNorm(torch.autograd.Function):
         ctx.slot = None
         dx, dg, db, dres = _bn_backward_core(ctx, dy, x, mask, g32, stats, relu)
         return dx, dg, db, None, None, None, None, None, None, dres, None, None
-
-
-class _GradSlot:
-    __slots__ = ("grad",)
-
-    def __init__(self):
-        self.grad = None
 
 
 def _bn_forward_stats(x, gamma, beta, running_mean, running_var, training, momentum, eps):
@@ -1217,32 +1109,6 @@ def bn_relu_conv1x1(x, gamma, beta, running_mean, running_var, w, momentum=0.997
     _check_cuda_bf16(x)
     return _BnReluConv1x1.apply(x, gamma, beta, running_mean, running_var, w, momentum, eps,
                                 bool(lazy_out))
-
-
-class _Recompute:
-    """A bottleneck c3 output that was never stored (lazy x3): x3 = bf16(y . w^T) with y the
-    conv's input [M, K3] and w its bf16 weight [N, K3, ...] -- recomputed with the producing
-    stream GEMM's exact MFMA chain by the residual BN's apply (gemm_stream_apply), by the
-    consuming data gradient's BN-sum epilogue (gemm_stream_bnb RC) and by the fused c3 backward
-    (RC); :meth:`materialize` writes it into the tensor's own storage for any other reader."""
-    __slots__ = ("y", "wb", "out", "done")
-
-    def __init__(self, y, wb, out):
-        # the output holds this record: a weak reference back keeps them out of a cycle
-        self.y, self.wb, self.out, self.done = y, wb, weakref.ref(out), False
-
-    @property
-    def k3(self):
-        return self.y.shape[-1]
-
-    def materialize(self):
-        out = self.out()
-        if not self.done and out is not None:
-            N = out.shape[-1]
-            M = out.numel() // N
-            gemm_nt(self.y.view(M, self.k3), self.wb.view(N, self.k3), out=out.view(M, N))
-            self.done = True
-        return out
 
 
 def _lazy_x3_ok(M, C, K):

@@ -166,6 +166,9 @@ class Optimizer:
             fn.dtf_unit_grad = True          # backward() below seeds exactly d(loss) = 1
         with profiler.maybe_phase("backward"):
             loss.backward()
+        # every deferred-work record of this step has been consumed (or never will be)
+        from .. import ops
+        ops.end_step()
         with profiler.maybe_phase("comm"):
             self._reducer.finish()
         return [(v.grad, v) for v in self.space.order]

@@ -31,12 +31,6 @@ from .strategy import (BucketedAllReduce, MirroredStrategy, Strategy, _broadcast
 
 
 
-def _join_wgrad_side(grad):
-    """Weight gradients still queued on the ops' side stream land before a bucket is read."""
-    if grad.is_cuda:
-        from ..ops import native_join_wgrad_side
-        native_join_wgrad_side()
-
 class _RemotePSReducer(_NullReducer):
     """Between-graph: push the gradients at step end; the reply carries the updated variables
     (so the NEXT forward pass reads fresh values — TF's read-at-step-start semantics).
@@ -148,7 +142,6 @@ class _RemotePSReducer(_NullReducer):
         self.launched[b] = True
         s, e, _ = self.buckets[b]
         st = self._streams
-        _join_wgrad_side(self.space.grad)
         st.side_waits_compute()
         with st.side():
             for link in self.client.links:
@@ -491,7 +484,6 @@ class _ColocatedPSReducer(BucketedAllReduce):
         self.launched[b] = True
         self.launch_log.append(b)
         g = self.space.grad
-        _join_wgrad_side(g)
         if self.sharded:
             s, e, _ = self.buckets[b]
             _, cs, ce = self.pieces[b][self.rank]

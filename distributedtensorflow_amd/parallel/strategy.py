@@ -243,10 +243,6 @@ class BucketedAllReduce:
         self.launch_log.append(b)
         s, e, _ = self.buckets[b]
         view = self.space.grad[s:e]
-        if view.is_cuda:
-            # weight gradients still queued on the side stream (ops/native.py) land first
-            from ..ops import native_join_wgrad_side
-            native_join_wgrad_side()
         if self.compress:
             W, L = self.world, e - s
             c = -(-L // W)

@@ -45,7 +45,8 @@ def run_task(args):
             torch.cuda.synchronize()
 
     if args.job_name == "ps":
-        dev = torch.device("cuda", args.task_index % ndev) if cuda else torch.device("cpu")
+        # the PS task is colocated with worker 0 on GPU 0 (device_plan)
+        dev = torch.device("cuda", 0) if cuda else torch.device("cpu")
         if cuda:
             torch.cuda.set_device(dev)
         server = Server(cluster, "ps", args.task_index, ps_device=str(dev))
@@ -109,21 +110,45 @@ def run_task(args):
     server.shutdown()
 
 
+def device_plan(num_workers, gpus, visible):
+    """(worker device indices, PS device index) of ``bench.py --strategy ps_async --gpus N``:
+    worker i on GPU ``i % N`` (one per GPU when W = N, round-robin when W > N), the PS task
+    colocated on GPU 0 (BASELINE config 4, "1 PS + N workers colocated on one node").  Refuses
+    (ValueError) to plan for more GPUs than are visible: a run labelled N GPUs must use N.
+    ``visible`` = 0 (a CPU-only host) plans a CPU run for N = 1: no devices."""
+    if gpus < 1 or num_workers < 1:
+        raise ValueError("ps_async needs --gpus >= 1 and --num-workers >= 1")
+    if visible == 0 and gpus == 1:
+        return [None] * num_workers, None
+    if visible < gpus:
+        raise ValueError(f"--gpus {gpus} but only {visible} GPU(s) are visible: refusing to "
+                         f"measure fewer GPUs than requested")
+    return [i % gpus for i in range(num_workers)], 0
+
+
 def run_launcher(args, metric_note=""):
     """Start 1 PS + W workers of ``bench.py`` on this node and report the aggregate."""
     import tempfile
 
     from distributedtensorflow_amd.cluster.launcher import launch_local
+    from distributedtensorflow_amd.utils import dtf_env
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    # device_count() does not initialise the GPU (the tasks are fresh processes anyway)
+    visible = torch.cuda.device_count()
+    try:
+        workers_dev, ps_dev = device_plan(args.num_workers, args.gpus, visible)
+    except ValueError as e:
+        print(f"bench.py: error: {e}", file=sys.stderr, flush=True)
+        raise SystemExit(2)
     work = tempfile.mkdtemp(prefix="dtf_ps_bench_")
     extra = ["--strategy", "ps_async", "--batch", str(args.batch), "--steps", str(args.steps),
              "--warmup", str(args.warmup), "--image-size", str(args.image_size),
-             "--lr", str(args.lr), "--out-dir", work]
-    ndev = max(torch.cuda.device_count(), 1) if torch.cuda.is_available() else None
-    # CPU-only hosts (tests): the PS keeps its shard in host memory (/dev/shm plane)
+             "--lr", str(args.lr), "--out-dir", work, "--gpus", str(args.gpus)]
+    # worker i -> LOCAL_RANK i % N (launch_local); CPU-only hosts (tests): the PS keeps its shard
+    # in host memory (/dev/shm plane)
     codes, logs = launch_local(os.path.join(root, "bench.py"), 1, args.num_workers, work, extra,
                                env={"PYTHONPATH": root}, timeout_s=args.timeout,
-                               gpus_per_host=ndev)
+                               gpus_per_host=args.gpus if ps_dev is not None else None)
     if any(c != 0 for c in codes.values()):
         for k, p in logs.items():
             sys.stderr.write(f"--- {k}\n" + open(p).read()[-3000:])
@@ -138,9 +163,12 @@ def run_launcher(args, metric_note=""):
            for k in ("copy_sync_ms_per_step", "wait_ms_per_step", "pull_ms_per_step",
                      "fence_ms_per_step", "answer_ms_per_step")}
     applied = max(int(ps.get("applied", 0)), 1)
+    used = sorted({r["device"] for r in recs if r["device"].startswith("cuda")})
+    if ps_dev is not None and used != [f"cuda:{i}" for i in sorted(set(workers_dev))]:
+        raise SystemExit(f"ps_async bench: workers ran on {used}, planned {sorted(set(workers_dev))}")
     rec = {"metric": "images/sec ResNet-50 async parameter server (between-graph, 1 PS + "
                      f"{args.num_workers} workers)",
-           "value": round(ips, 2), "unit": "images/sec", "n_gpus": ndev,
+           "value": round(ips, 2), "unit": "images/sec", "n_gpus": len(used),
            "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(span / args.steps * 1e3, 3), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
@@ -152,11 +180,13 @@ def run_launcher(args, metric_note=""):
                       "data_plane": recs[0]["data_plane"],
                       "pipelined_push_pull": all(r.get("pipelined") for r in recs),
                       "worker_devices": [r["device"] for r in recs],
+                      "ps_device": None if ps_dev is None else f"cuda:{ps_dev}",
                       "worker_host_ms_per_step": per,
                       "ps_apply_ms_mean": round(1e3 * float(ps.get("apply_s", 0.0)) / applied, 3),
                       "ps_applied": ps.get("applied"), "ps_pushes": ps.get("pushes"),
                       "ps_max_inflight_applies": ps.get("max_inflight"),
                       "final_global_step": max(r["global_step"] for r in recs),
-                      "final_loss": [round(r["loss"], 4) for r in recs], "note": metric_note}}
+                      "final_loss": [round(r["loss"], 4) for r in recs], "note": metric_note,
+                      "dtf_env": dtf_env()}}
     print(json.dumps(rec), flush=True)
     return rec

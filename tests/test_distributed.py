@@ -417,14 +417,23 @@ def test_bench_ps_async_flow_cpu(tmp_path):
 
 
 @pytest.mark.parametrize("kind,args", [("mirrored", ("bucket_mb=0.05",)),
-                                       ("colocated_ps", ("num_ps=8", "bucket_mb=0.05"))],
-                         ids=["mirrored", "sharded_ps"])
+                                       ("colocated_ps", ("num_ps=8", "bucket_mb=0.05")),
+                                       ("colocated_ps", ("num_ps=1", "bucket_mb=0.05"))],
+                         ids=["mirrored", "sharded_ps", "one_ps"])
 def test_eight_ranks_match_single_process(tmp_path, kind, args):
     """The driver's N = 8 layout rehearsed on gloo: 8 ranks (2 images each of the 16-image
-    global batch), many buckets; the sharded parameter server splits every bucket 8 ways."""
+    global batch), many buckets; the sharded parameter server splits every bucket 8 ways, and
+    BASELINE config 4's "1 PS + 8 workers" keeps every variable on rank 0 (owner plan: one
+    range, owner 0, covering the whole flat buffer)."""
     res = _launch(kind, 8, tmp_path, *args, timeout=300)
     if kind == "colocated_ps":
-        assert all(r["sharded"] is True for r in res)
+        assert all(r["sharded"] is (args[0] == "num_ps=8") for r in res)
+        if args[0] == "num_ps=1":
+            for rec in res:
+                owners = {o for o, _, _ in rec["ranges"]}
+                assert owners == {0}, rec["ranges"]
+                ends = sorted((s, e) for _, s, e in rec["ranges"])
+                assert all(a[1] == b[0] for a, b in zip(ends, ends[1:]))   # contiguous cover
     _assert_replicas(res, _single_process(), atol=5e-6)
     # every rank: the same bucket plan, the same collective issue order (checked collectively by
     # verify_bucket_agreement inside the run, and here from the saved records)
@@ -432,7 +441,7 @@ def test_eight_ranks_match_single_process(tmp_path, kind, args):
     assert len(res[0]["plan"]["buckets"]) >= 4 and sorted(res[0]["order"]) == \
         list(range(len(res[0]["plan"]["buckets"])))
     assert all(r["agreement"] == res[0]["agreement"] for r in res)
-    if kind == "colocated_ps":
+    if kind == "colocated_ps" and args[0] == "num_ps=8":
         # reduce-scatter / all-gather chunk offsets = the sharded owner plan at every rank:
         # rank r owns chunk r of every bucket, equal chunks that tile the bucket exactly
         for r, rec in enumerate(res):
@@ -457,3 +466,24 @@ def test_forced_bucket_order_mismatch_fails_within_the_deadline(tmp_path):
     msg = str(ei.value)
     assert "collective order differs" in msg or "CommError" in msg or "did not complete" in msg, \
         msg[-3000:]
+
+
+def test_bench_ps_async_eight_workers_cpu(tmp_path):
+    """BASELINE config 4's shape in the reference's own async mode, rehearsed on the CPU: 1 PS +
+    8 worker tasks launched by bench.py, every push applied (Hogwild, no drops), the global step
+    counts all 8 workers' pushes, and the JSON names every worker's device (on a GPU node the
+    plan is cuda:0..7 with the PS on cuda:0: tests/test_bench_integrity.py)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--strategy", "ps_async",
+                        "--num-workers", "8", "--batch", "2", "--image-size", "32", "--steps",
+                        "2", "--warmup", "1", "--timeout", "400"],
+                       env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1"),
+                       capture_output=True, text=True, timeout=460, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = rec["config"]
+    assert cfg["parallelism"] == "ps1+async8" and len(cfg["worker_devices"]) == 8
+    assert cfg["ps_applied"] == cfg["ps_pushes"] == 8 * (2 + 1)
+    assert cfg["final_global_step"] == 8 * 3
+    assert rec["n_gpus"] == 0 and cfg["ps_device"] is None        # CPU host: no devices used
+    assert cfg["dtf_env"] == {k: v for k, v in sorted(os.environ.items())
+                              if k.startswith("DTF_")}

@@ -921,3 +921,43 @@ def test_training_step_frees_its_activations_without_the_cycle_collector():
         if was:
             gc.enable()
     assert max(after[1:]) - min(after[1:]) < 2 * 2**20, after
+
+
+def test_no_record_outlives_its_step():
+    """the default ResNet-50 training step (BN on load, lazy x3, fused BN
+    backward, masked residual gradients) through the optimizer, with the cyclic collector OFF:
+    after every step no deferred-work record is alive (ops/records.py end_step), and the peak
+    memory of step 25 equals step 2's (a record kept past its step would hold a step's
+    activations: +2.9 GB per step at b1984 in round 5)."""
+    import gc
+
+    from distributedtensorflow_amd.ops import records
+    from distributedtensorflow_amd.optimizers import MomentumOptimizer
+    from distributedtensorflow_amd.parallel import MirroredStrategy
+    torch.manual_seed(0)
+    with MirroredStrategy().scope():
+        m = resnet50()
+        opt = MomentumOptimizer(0.01, momentum=0.9, weight_decay=1e-4)
+        opt.build(list(m.parameters()))
+    # 224 x 224: the halo 3x3 convs (BN on load) and the stage-0 lazy x3 take their real paths
+    x = torch.randn(8, 224, 224, 3, device="cuda").bfloat16()
+    lab = torch.randint(0, 1000, (8,), device="cuda")
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    peaks, made = [], []
+    try:
+        for _ in range(25):
+            torch.cuda.reset_peak_memory_stats()
+            loss = ops.sparse_softmax_cross_entropy(m(x), lab)
+            made.append(records.live_count())
+            opt.minimize(loss)
+            del loss
+            torch.cuda.synchronize()
+            assert records.live_count() == 0
+            peaks.append(torch.cuda.max_memory_allocated())
+    finally:
+        if was:
+            gc.enable()
+    assert min(made) > 0, made                       # the step does create records
+    assert peaks[24] == peaks[1], peaks
