@@ -960,4 +960,7 @@ def test_no_record_outlives_its_step():
         if was:
             gc.enable()
     assert min(made) > 0, made                       # the step does create records
-    assert peaks[24] == peaks[1], peaks
+    # the per-step caches alternate by a few MB; one leaked step's records would hold its c1
+    # outputs and more (~11 MB per step at this batch, 23 steps: > 250 MB)
+    assert max(peaks[1:]) - min(peaks[1:]) < 4 * 2**20, peaks
+    assert abs(peaks[24] - peaks[1]) < 4 * 2**20, peaks
