@@ -56,6 +56,7 @@ void dtf_bn_fwd_finalize_g(const float*, int, long, int, const float*, const flo
 long dtf_bn_workspace_floats_g(int, int);
 int dtf_conv_stats_rows(long, int, int, int, int);
 void dtf_conv_set_halo(int);
+int dtf_gemm_conv_part_images(int, int, int, int, int, int);
 int dtf_conv_tile_rows(const ConvGeom&, const TapTable&, int bnb);
 bool dtf_conv_bnl_ok(const ConvGeom&, const TapTable&);
 void dtf_conv_set_bnl_probe(int);
@@ -123,6 +124,11 @@ void dtf_sumsq(const float*, long, float*, hipStream_t);
 void dtf_cast_f32_bf16(const float*, bf16_t*, long, hipStream_t);
 void dtf_conv_igemm(const bf16_t*, const bf16_t*, bf16_t*, const ConvGeom&, const TapTable&, int,
                     float*, const BnBwdEpi&, hipStream_t);
+bool dtf_conv_igemm_grouped(const bf16_t*, bf16_t*, const ConvGeom&, int, const bf16_t* const*,
+                            const int*, const int*, const int*,
+                            const std::vector<std::vector<int>>&,
+                            const std::vector<std::vector<int>>&, const BnBwdEpi&, const int*,
+                            hipStream_t);
 void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, const TapTableW&,
                     int, int, int, hipStream_t);
 
@@ -720,6 +726,37 @@ PYBIND11_MODULE(_dtf_hip, m) {
      py::arg("bnb") = std::vector<uintptr_t>{}, py::arg("acc_src") = 0, py::arg("acc_mask") = 0,
      py::arg("bias") = 0, py::arg("relu") = 0, py::arg("bnl_sc") = 0, py::arg("bnl_sh") = 0,
      py::arg("bnl_y") = 0);
+  // the phase classes of a strided data gradient in one launch; False: not eligible, nothing
+  // launched (the caller launches the classes one by one)
+  m.def("conv_igemm_grouped", [](uintptr_t x, uintptr_t y, std::vector<int> geom,
+                                 std::vector<uintptr_t> wts, std::vector<int> oh0,
+                                 std::vector<int> ow0, std::vector<int> kpad,
+                                 std::vector<std::vector<int>> dh, std::vector<std::vector<int>> dw,
+                                 uintptr_t st, std::vector<uintptr_t> bnb, std::vector<int> row0) {
+    if (geom.size() != 17) throw std::runtime_error("conv_igemm_grouped: geom needs 17 ints");
+    const size_t n = wts.size();
+    if (oh0.size() != n || ow0.size() != n || kpad.size() != n || dh.size() != n ||
+        dw.size() != n || (!bnb.empty() && row0.size() != n))
+      throw std::runtime_error("conv_igemm_grouped: per-class lists differ in length");
+    ConvGeom g{geom[0], geom[1], geom[2],  geom[3],  geom[4],  geom[5],  geom[6],  geom[7],
+               geom[8], geom[9], geom[10], geom[11], geom[12], geom[13], geom[14], geom[15],
+               geom[16]};
+    BnBwdEpi e{};
+    if (!bnb.empty()) {
+      if (bnb.size() != 8) throw std::runtime_error("conv_igemm_grouped: bnb needs 8 entries");
+      e = BnBwdEpi{P<const bf16_t>(bnb[0]), P<const float>(bnb[1]), P<const float>(bnb[2]),
+                   P<const float>(bnb[3]), P<const float>(bnb[4]), P<const uint8_t>(bnb[5]),
+                   P<float>(bnb[6]), (int)bnb[7], 0};
+    }
+    std::vector<const bf16_t*> w(n);
+    for (size_t i = 0; i < n; ++i) w[i] = P<const bf16_t>(wts[i]);
+    const bool ok = dtf_conv_igemm_grouped(P<const bf16_t>(x), P<bf16_t>(y), g, (int)n, w.data(),
+                                           oh0.data(), ow0.data(), kpad.data(), dh, dw, e,
+                                           row0.empty() ? nullptr : row0.data(), S(st));
+    if (ok) check_launch("conv_igemm_grouped");
+    return ok;
+  });
+  m.def("gemm_conv_part_images", &dtf_gemm_conv_part_images);
   m.def("conv_bnl_ok", [](std::vector<int> geom, std::vector<int> dh, std::vector<int> dw) {
     if (geom.size() != 16 && geom.size() != 17)
       throw std::runtime_error("conv_bnl_ok: geom needs 16 (+acc) ints");

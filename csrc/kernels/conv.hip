@@ -32,8 +32,10 @@
 //   their input channels are zero-padded to 8 by the host); 1 = per-element gather (any C).
 //   The tap table arrives as a kernel argument; it is only ever read with wave-uniform indices
 //   (scalar loads) — per-lane indices go through a copy in LDS.
+#include <algorithm>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "common.h"
 
@@ -171,7 +173,10 @@ struct BnbAcc {
       red[(orow * 2 + 0) * BN + oc * 8 + i] = s0[i];
       red[(orow * 2 + 1) * BN + oc * 8 + i] = s1[i];
     }
-    __syncthreads();
+    // LDS visibility only: a __syncthreads() would also drain vmcnt, i.e. wait for the tile's
+    // output stores issued just before
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
     for (int idx = tid; idx < 2 * BN; idx += NT) {
       const int which = idx / BN, col = idx % BN;
       if (n0 + col >= Kout) continue;
@@ -204,12 +209,13 @@ DTF_DEV uint32_t bload2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 // launches can run 4 blocks per CU instead of 3
 // STATS: the launch fuses the BatchNorm statistics (stats != nullptr); a template flag so the
 // launches without them (data gradients) keep their register budget
-template <int WAVES_M, int WAVES_N, int BK, int GATHER, bool BNB, bool HI_OCC = false,
-          bool STATS = false>
-__global__ void __launch_bounds__(kThreads, HI_OCC ? 4 : 2)
-conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
-                  bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
-                  float* __restrict__ stats, const BnBwdEpi bnb) {
+// The kernel body, for tile `bid` of the launch's (tiles_m x tiles_n) grid; TT: the tap table
+// type (TapTable, or the grouped launch's per-class TapTableG)
+template <int WAVES_M, int WAVES_N, int BK, int GATHER, bool BNB, bool STATS, class TT>
+DTF_DEV __attribute__((always_inline)) void
+conv_igemm_body(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+                bf16_t* __restrict__ Y, const ConvGeom& g, const TT& taps,
+                float* __restrict__ stats, const BnBwdEpi& bnb, const int bid) {
   constexpr int BM = 64 * WAVES_M, BN = 64 * WAVES_N;
   constexpr int CPR = BK / 8;                            // chunks per row
   constexpr int A_CHUNKS = BM * CPR / kThreads;          // 16-B loads per thread for A
@@ -225,9 +231,6 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
 
   const int M = g.N * g.P * g.Q;
   const int tiles_n = (g.Kout + BN - 1) / BN;
-  const int tiles_m = (M + BM - 1) / BM;
-  const int nwg = tiles_n * tiles_m;
-  const int bid = xcd_remap(blockIdx.x, nwg);
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * BM;
   const int n0 = tn * BN;
@@ -507,6 +510,54 @@ conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
   if constexpr (BNB)
     ba.template flush<BN, kThreads>(bnb, reinterpret_cast<float*>(st + BM * LDC), tid / OCPR, oc,
                                     OROWS, tid, tm, n0, g.Kout);
+}
+
+template <int WAVES_M, int WAVES_N, int BK, int GATHER, bool BNB, bool HI_OCC = false,
+          bool STATS = false>
+__global__ void __launch_bounds__(kThreads, HI_OCC ? 4 : 2)
+conv_igemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+                  bf16_t* __restrict__ Y, const ConvGeom g, const TapTable taps,
+                  float* __restrict__ stats, const BnBwdEpi bnb) {
+  constexpr int BM = 64 * WAVES_M, BN = 64 * WAVES_N;
+  const int nwg = ((g.N * g.P * g.Q + BM - 1) / BM) * ((g.Kout + BN - 1) / BN);
+  conv_igemm_body<WAVES_M, WAVES_N, BK, GATHER, BNB, STATS>(X, Wt, Y, g, taps, stats, bnb,
+                                                            xcd_remap(blockIdx.x, nwg));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Grouped strided data gradient: the s x s output phase classes of a stride-s conv's dgrad
+// (conv2d_dgrad: one dense stride-1 sub-convolution per class, over that class's taps only --
+// no zero taps) in ONE launch instead of one per class.  Per class, only the output placement
+// (oh0, ow0), the tap list, the filter slice and the BN-backward slab rows differ; every class
+// has the same tile count (the host requires it), and blocks are interleaved class-fastest, so
+// the classes of one M-tile run side by side and share its dY rows in L2: 1.00 vs 1.15 ms for
+// the 56x56x128 stride-2 layer at b1984 (class-major in one grid: 1.26 ms; tools/conv_gap.py).
+constexpr int kGrpMax = 4;
+constexpr int kGrpTaps = 9;
+struct TapTableG {
+  int n;
+  int dh[kGrpTaps];
+  int dw[kGrpTaps];
+};
+struct ConvGroup {
+  int n;                               // classes
+  // per class: the whole geometry / epilogue record, read in place from the kernel arguments
+  // (a copy with the class's fields patched in costs registers the BN-sum epilogue needs)
+  const bf16_t* Wt[kGrpMax];           // [Kout][Kpad] per class
+  ConvGeom g[kGrpMax];
+  BnBwdEpi bnb[kGrpMax];
+  TapTableG taps[kGrpMax];
+};
+
+template <int WAVES_M, int WAVES_N, bool BNB, bool HI_OCC>
+__global__ void __launch_bounds__(kThreads, HI_OCC ? 4 : 2)
+conv_igemm_grouped_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
+                          const ConvGroup grp) {
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int cls = __builtin_amdgcn_readfirstlane(b % grp.n);      // classes interleaved per tile
+  const int tile = b / grp.n;
+  conv_igemm_body<WAVES_M, WAVES_N, 32, 0, BNB, false>(X, grp.Wt[cls], Y, grp.g[cls],
+                                                      grp.taps[cls], nullptr, grp.bnb[cls], tile);
 }
 
 template <int WM, int WN, int BK, int GEN>
@@ -1129,7 +1180,11 @@ conv3x3_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
     ba.template flush<NT, kThreads>(bnb, reinterpret_cast<float*>(st + H::M * LDC), tid / OCPR,
                                     oc, OROWS, tid, tm, n0, g.Kout);
   }
-  if (stats) {   // per-channel sum / sum of squares of the rounded outputs -> slab row tm
+  // per-channel sum / sum of squares of the rounded outputs -> slab row tm: a column pass over the
+  // staged tile.  (Summing the stored 16-B values in the store loop and folding the lanes by
+  // shuffles -- as the stem kernel below now does -- measured 10-45 us SLOWER per call here in the
+  // network, profiles/r6; register sums from the accumulators were slower in round 2.)
+  if (stats) {
     constexpr int GROUPS = kThreads / NT;
     constexpr int RPG = H::M / GROUPS;
     float* red = reinterpret_cast<float*>(st + H::M * LDC);      // [GROUPS][2][NT]
@@ -1264,29 +1319,47 @@ conv_stem_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W
   const long ybase = ((long)n * g.P + p0) * Q;
   constexpr int OCPR = kStemK / 8;
   const int oc = tid % OCPR;
-  for (int rr = tid / OCPR; rr < H::M; rr += kThreads / OCPR)
-    st16(Y + (ybase + rr) * kStemK + oc * 8, *reinterpret_cast<const uint4*>(st + rr * LDC + oc * 8),
-         g.nt);
-  if (stats) {
-    constexpr int GROUPS = kThreads / kStemK;
-    constexpr int RPG = H::M / GROUPS;
-    float* red = reinterpret_cast<float*>(st + H::M * LDC);       // [GROUPS][2][64]
-    const int col = tid % kStemK, grp = tid / kStemK;
-    float a1 = 0.f, a2 = 0.f;
-    for (int rr = grp * RPG; rr < (grp + 1) * RPG; ++rr) {
-      const float v = bf2f(st[rr * LDC + col]);
-      a1 += v;
-      a2 += v * v;
-    }
-    red[(grp * 2 + 0) * kStemK + col] = a1;
-    red[(grp * 2 + 1) * kStemK + col] = a2;
-    __syncthreads();
-    if (grp == 0) {
-      float a = 0.f, b = 0.f;
+  // BN statistics summed from the stored 16-B values as they pass (see conv3x3_halo_kernel)
+  float q1[8], q2[8];
 #pragma unroll
-      for (int k = 0; k < GROUPS; ++k) { a += red[(k * 2 + 0) * kStemK + col]; b += red[(k * 2 + 1) * kStemK + col]; }
-      stats[((long)tm * 2 + 0) * kStemK + col] = a;
-      stats[((long)tm * 2 + 1) * kStemK + col] = b;
+  for (int e = 0; e < 8; ++e) { q1[e] = 0.f; q2[e] = 0.f; }
+  static_assert(H::M % (kThreads / OCPR) == 0, "stem epilogue rows");
+#pragma unroll
+  for (int k = 0; k < H::M / (kThreads / OCPR); ++k) {
+    const int rr = tid / OCPR + k * (kThreads / OCPR);
+    const uint4 v = *reinterpret_cast<const uint4*>(st + rr * LDC + oc * 8);
+    st16(Y + (ybase + rr) * kStemK + oc * 8, v, g.nt);
+    if (stats) {
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { q1[e] += f[e]; q2[e] = __builtin_fmaf(f[e], f[e], q2[e]); }
+    }
+  }
+  if (stats) {
+#pragma unroll
+    for (int msk = OCPR; msk < 64; msk <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        q1[e] += __shfl_xor(q1[e], msk, 64);
+        q2[e] += __shfl_xor(q2[e], msk, 64);
+      }
+    float* red = reinterpret_cast<float*>(st + H::M * LDC);       // [4 waves][2][64]
+    if (lane < OCPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 2 + 0) * kStemK + oc * 8 + e] = q1[e];
+        red[(wave * 2 + 1) * kStemK + oc * 8 + e] = q2[e];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // not vmcnt: the Y stores stay in flight
+    raw_barrier();
+    if (tid < 2 * kStemK) {
+      const int which = tid / kStemK, col = tid - which * kStemK;
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) a += red[(w * 2 + which) * kStemK + col];
+      stats[((long)tm * 2 + which) * kStemK + col] = a;
     }
   }
 }
@@ -1480,6 +1553,7 @@ int dtf_conv_stats_rows(long M, int Kout, int C, int taps, int W) {
 // kernel (256 x 256 tiles, 1.2-1.3 PF on long-K GEMMs vs ~0.9 for the 256 x 128 DMA kernel)
 static int g_conv_gemm = 1;
 void dtf_conv_set_gemm(int v) { g_conv_gemm = v; }
+int dtf_gemm_conv_part_images(int N, int H, int W, int C, int P, int Q);
 static bool use_conv_gemm(const ConvGeom& g, const TapTable& taps) {
   const bool unit = g.osh == 1 && g.osw == 1 && g.oh0 == 0 && g.ow0 == 0 && g.Ho == g.P &&
                     g.Wo == g.Q;
@@ -1487,9 +1561,16 @@ static bool use_conv_gemm(const ConvGeom& g, const TapTable& taps) {
   // bit 1: also 64 < Kout <= 128 on the 256 x 128 ping-pong tile -- measured SLOWER than the
   // halo / register kernels (profiles/measurements/r2_conv_kout128_pingpong_ab.txt), off
   const bool wide = g.Kout >= 256 || ((g_conv_gemm & 2) && g.Kout > 64 && g.Kout <= 128);
+  // strided 1x1 forward (the projection shortcuts, 1 tap): on the persistent GEMM when its whole
+  // input fits one buffer descriptor (gemm.hip launch_gemm_pp2); the register kernel ran these
+  // at 2.5 TB/s / 0.42 PF (s1b0proj 977 us, s2b0proj 666 us at b1984, profiles/r6)
+  // (an input past one descriptor runs as batch parts, dtf_gemm_conv_part_images)
+  const bool proj = taps.n == 1 && (g.sh > 1 || g.sw > 1) && g.C >= 128 && g.Kout > 128 &&
+                    !g.acc && dtf_gemm_conv_part_images(g.N, g.H, g.W, g.C, g.P, g.Q) >= 0 &&
+                    g.N < 2048 && g.H < 1000 && g.W < 1000;
   return (g_conv_gemm & 1) && g.C % 64 == 0 && wide && g.Kout % 8 == 0 && taps.n <= 9 &&
-         (unit ? taps.n > 1 : g.acc != 2) && g.Kpad == taps.n * g.C && !g.bias && !g.relu &&
-         g.H < 16384 && g.W < 32768;
+         (unit ? (taps.n > 1 || proj) : g.acc != 2) && g.Kpad == taps.n * g.C && !g.bias &&
+         !g.relu && g.H < 16384 && g.W < 32768;
 }
 void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, int W, int C,
                    int P, int Q, int sh, int sw, int Kout, int ntaps, const int* dh, const int* dw,
@@ -1617,6 +1698,84 @@ void dtf_conv_igemm(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, const ConvGeom
     if (narrow) launch_cfg<4, 1, 32, 0>(X, Wt, Y, g, taps, stats, bnb, st);
     else launch_cfg<2, 2, 32, 0>(X, Wt, Y, g, taps, stats, bnb, st);
   }
+}
+
+// The phase classes of a strided data gradient in one launch (conv_igemm_grouped_kernel).  g0:
+// the shared geometry (oh0 / ow0 / Kpad are per class); dh / dw: each class's taps.  Returns
+// false -- nothing launched -- when the classes would not all take the BK-32 register kernel
+// dtf_conv_igemm picks for them, or do not have equal tile grids; the caller then launches them
+// one by one.
+bool dtf_conv_igemm_grouped(const bf16_t* X, bf16_t* Y, const ConvGeom& g0, int ncls,
+                            const bf16_t* const* wts, const int* oh0, const int* ow0,
+                            const int* kpad, const std::vector<std::vector<int>>& dh,
+                            const std::vector<std::vector<int>>& dw, const BnBwdEpi& bnb,
+                            const int* row0, hipStream_t st) {
+  if (ncls < 2 || ncls > kGrpMax || g0.C % 32 || g0.bias || g0.relu || g0.ly || g0.acc == 2 ||
+      !(g_small_k & 8) || g0.Kout % 8)
+    return false;
+  // not with the fused BN-backward sums: grouped, that epilogue ran 1.97 vs 1.78 ms split
+  // (56x56x128 stride 2, b1984; tools/conv_gap.py)
+  if (bnb.part) return false;
+  ConvGroup grp{};
+  grp.n = ncls;
+  ConvGeom g = g0;
+  g.nt = g_conv_nt;
+  const long m = (long)g.N * g.P * g.Q;
+  int max_nk = 0;
+  for (int c = 0; c < ncls; ++c) {
+    const int nt = (int)dh[c].size();
+    if (nt < 1 || nt > kGrpTaps || (int)dw[c].size() != nt || kpad[c] % 32 ||
+        kpad[c] < nt * g.C)
+      return false;
+    TapTable t{};
+    t.n = nt;
+    grp.taps[c].n = nt;
+    for (int i = 0; i < nt; ++i) {
+      t.dh[i] = grp.taps[c].dh[i] = dh[c][i];
+      t.dw[i] = grp.taps[c].dw[i] = dw[c][i];
+    }
+    ConvGeom gc = g;
+    gc.oh0 = oh0[c];
+    gc.ow0 = ow0[c];
+    gc.Kpad = kpad[c];
+    // the kernel dtf_conv_igemm would choose must be the register kernel
+    if (use_conv_gemm(gc, t) || use_halo(gc, t) ||
+        (use_dma_kernel(m, gc.Kout, gc.C, nt, 64) && gc.Kpad % 64 == 0))
+      return false;
+    const double wbytes = 2.0 * gc.Kout * gc.Kpad;
+    if (wbytes >= 2147483647.0) return false;
+    grp.Wt[c] = wts[c];
+    grp.g[c] = gc;
+    grp.bnb[c] = bnb;
+    grp.bnb[c].row0 = row0 ? row0[c] : 0;
+    max_nk = std::max(max_nk, (nt * g.C + 31) / 32);
+  }
+  const double ibytes = 2.0 * g.H * g.W * g.C;
+  const double span = (double)(255 / (g.P * g.Q) + 2);
+  if (ibytes * span >= 2147483647.0 || m >= 2147483647.0 ||
+      (double)g.N * g.Ho * g.Wo >= 2147483647.0)
+    return false;
+  const bool narrow = g.Kout <= 64;
+  const int BM = narrow ? 256 : 128, BN = narrow ? 64 : 128;
+  const long tiles = ((m + BM - 1) / BM) * ((g.Kout + BN - 1) / BN) * ncls;
+  if (tiles >= (1L << 31)) return false;
+  const size_t stage = (size_t)(BM + BN) * 32 * sizeof(bf16_t) *
+                           ((max_nk > 1 || !(g_small_k & 1)) ? 2 : 1) +
+                       2 * DTF_MAX_TAPS * sizeof(int);
+  const int OROWS = kThreads / (BN / 8);
+  const size_t scratch = bnb.part ? (size_t)OROWS * 2 * BN : (size_t)2 * kThreads;
+  const size_t epi = (size_t)BM * (BN + 8) * sizeof(bf16_t) + scratch * sizeof(float);
+  const size_t lds = stage > epi ? stage : epi;
+  const dim3 grid((unsigned)tiles), blk(kThreads);
+  const bool hi = !bnb.part && (g_small_k & 16);
+  if (narrow) {
+    if (hi) hipLaunchKernelGGL((conv_igemm_grouped_kernel<4, 1, false, true>), grid, blk, lds, st, X, Y, grp);
+    else hipLaunchKernelGGL((conv_igemm_grouped_kernel<4, 1, false, false>), grid, blk, lds, st, X, Y, grp);
+  } else {
+    if (hi) hipLaunchKernelGGL((conv_igemm_grouped_kernel<2, 2, false, true>), grid, blk, lds, st, X, Y, grp);
+    else hipLaunchKernelGGL((conv_igemm_grouped_kernel<2, 2, false, false>), grid, blk, lds, st, X, Y, grp);
+  }
+  return true;
 }
 
 // ---------------------------------------------------------------------------------------------

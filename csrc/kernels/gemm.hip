@@ -22,6 +22,7 @@
 //   * XCD-aware bijective block remap, N-tile fastest: blocks sharing an A panel share an L2.
 //   * epilogue: accumulators (+bias, ReLU) -> bf16 -> LDS -> 16-B coalesced stores (+Cin: the
 //     beta = 1 accumulation used to fold a residual gradient into a data-gradient GEMM).
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -1784,6 +1785,19 @@ void dtf_gemm_set_group(int gm) { g_gemm_group = gm < 0 ? 0 : gm; }
 // Output row m = (n, p, q) lands at pixel (n, p*osh + oh0, q*osw + ow0) of [N][Ho][Wo] (the
 // phase classes of a strided data gradient; forward convs: osh = 1, Ho = P).  BN statistics
 // slab rows = dtf_gemm_tile_rows(M).
+// images per part when a gemm-conv input exceeds one 32-bit buffer descriptor: a multiple of
+// 256 / gcd(P Q, 256) images (whole 256-row tiles) whose input stays under 2^31 bytes; 0 when no
+// split is needed, -1 when none exists
+int dtf_gemm_conv_part_images(int N, int H, int W, int C, int P, int Q) {
+  const long img = (long)H * W * C * 2;
+  if ((long)N * img < 0x7FFFFF00L) return 0;
+  long a = (long)P * Q, b = 256;
+  while (b) { const long t = a % b; a = b; b = t; }
+  const long unit = 256 / a;
+  const long per = (0x7FFFFF00L / img) / unit * unit;
+  return per >= 1 && per < N && N < 2048 && H < 1000 && W < 1000 ? (int)per : -1;
+}
+
 void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, int W, int C,
                    int P, int Q, int sh, int sw, int Kout, int ntaps, const int* dh, const int* dw,
                    int Ho, int Wo, int osh, int osw, int oh0, int ow0,
@@ -1809,6 +1823,22 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
   const bool pp_span = !(osh != 1 || osw != 1) ||
       (256.0 / (P * Q) + 2) * Ho * Wo * (double)Kout * 2 < 2147483647.0;
   const long x_bytes = (long)N * H * W * C * 2, w_bytes = (long)Kout * g.ldb * 2;
+  // an input past one 32-bit descriptor (the stage-1 projection shortcut at b1984 reads a 3.2 GB
+  // tensor) on the persistent kernel: the batch in parts of a whole number of 256-row tiles, so
+  // the BN statistics slab rows of the parts continue exactly as one launch's would
+  const int part_n = dtf_gemm_conv_part_images(N, H, W, C, P, Q);
+  if (part_n > 0 && part_n < N && Kout > 128 && osh == 1 && osw == 1 && !Cin && !acc_src &&
+      (g_gemm_pp2 & 2)) {
+    const long pq = (long)P * Q;
+    for (int n0 = 0; n0 < N; n0 += part_n) {
+      const int cnt = std::min(part_n, N - n0);
+      dtf_gemm_conv(X + (long)n0 * H * W * C, Wt, Y + (long)n0 * pq * Kout, cnt, H, W, C, P, Q, sh,
+                    sw, Kout, ntaps, dh, dw, Ho, Wo, osh, osw, oh0, ow0,
+                    stats ? stats + (long)n0 * pq / 256 * 2 * Kout : nullptr, nullptr, nullptr,
+                    nullptr, st);
+    }
+    return;
+  }
   if (Kout <= 128) launch_gemm<256, 128, 64, 3, 3, 8, 1, 1>(g, st);
   // the persistent kernel for the unit-stride output launches only: its strided (dgrad phase)
   // epilogue is the swapped 32-B piece one -- 1.2-1.5x slower than the ping-pong's on the

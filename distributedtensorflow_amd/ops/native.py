@@ -341,12 +341,30 @@ def conv2d_dgrad(dy, w_bf16, x_shape, stride, padding, out=None, bnb=None, acc_f
         fsc, fsh = (stats[2].data_ptr(), stats[3].data_ptr()) if mkind == 2 else (0, 0)
         base = [xb.data_ptr(), stats[0].data_ptr(), stats[1].data_ptr(), fsc, fsh,
                 _p(mask) if mkind == 1 else 0, part.data_ptr(), mkind]
-    for li, (a, b, Pc, Qc, taps, idx) in enumerate(launches):
+    def class_filter(idx):
         if len(idx) == R * S:
-            wd_mat = _dgrad_filter(wflat)                      # [C, T, K]
-        else:
-            sel = wflat[:, _tap_index(idx, dy.device), :]
-            wd_mat = sel.permute(2, 1, 0).contiguous()
+            return _dgrad_filter(wflat)                        # [C, T, K]
+        sel = wflat[:, _tap_index(idx, dy.device), :]
+        return sel.permute(2, 1, 0).contiguous()
+
+    if (_DGRAD_GROUPED and len(launches) > 1 and acc_from is None and part is None and
+            len({(l[2], l[3]) for l in launches}) == 1 and K % 32 == 0):
+        # every phase class in ONE launch (csrc/kernels/conv.hip conv_igemm_grouped_kernel),
+        # classes interleaved per M-tile: 1.00 vs 1.15 ms for the 56x56x128 stride-2 layer at
+        # b1984.  Not with the fused BN-backward sums: that form ran 1.97 vs 1.78 ms
+        # (tools/conv_gap.py, profiles/r6).  False: the register kernel is not the one these
+        # classes would take -- launched one by one below
+        mats = [class_filter(l[5]).reshape(C, -1) for l in launches]
+        Pc, Qc = launches[0][2], launches[0][3]
+        geom = _fwd_geom(dyc.shape, C, launches[0][4], Pc, Qc, 1, 1, h, wd, sh, sw, 0, 0, acc)
+        if _K.conv_igemm_grouped(dyc.data_ptr(), dx.data_ptr(), geom,
+                                 [m.data_ptr() for m in mats], [l[0] for l in launches],
+                                 [l[1] for l in launches], [len(l[4]) * K for l in launches],
+                                 [[t[0] for t in l[4]] for l in launches],
+                                 [[t[1] for t in l[4]] for l in launches], _st(), [], []):
+            return dx
+    for li, (a, b, Pc, Qc, taps, idx) in enumerate(launches):
+        wd_mat = class_filter(idx)
         extra = ()
         if part is not None:
             extra = base + [row0]
@@ -693,6 +711,8 @@ _FUSE_BN_BWD_HALO = os.environ.get("DTF_FUSE_BN_BWD_HALO", "1") == "1"
 # implicit-GEMM kernel either way): the 3.2 GB BN1 reduce pass goes, throughput-neutral
 # (profiles/measurements/r4_stride2_dgrad_bn_sums_ab.jsonl)
 _FUSE_BN_BWD_S2 = os.environ.get("DTF_FUSE_BN_BWD_S2", "1") == "1"
+# the phase classes of a strided data gradient in one grouped launch (conv2d_dgrad)
+_DGRAD_GROUPED = os.environ.get("DTF_DGRAD_GROUPED", "1") == "1"
 # ... also where the data gradient (C >= 256 outputs) would otherwise run on the ping-pong GEMM
 # route, which takes no BN-sum epilogue (measured -0.3 % with it)
 _FUSE_BN_BWD_S2_ALL = os.environ.get("DTF_FUSE_BN_BWD_S2_ALL", "0") == "1"
@@ -1378,7 +1398,7 @@ def _wgrad_splits(T, o, i):
     """Token-axis split count for the dW = dY^T X GEMM: hipBLASLt tiles only the small o x i
     output (36-144 tiles of 128 x 128 at BERT-base shapes) and leaves most CUs idle, so the
     reduction is split into S batched slices and their fp32 partials summed.  Measured on MI355X
-    (tools/dense_wgrad_probe.py, T = 16384): 1.6-2.1x over the single GEMM."""
+    (a round-1 probe, since removed; T = 16384): 1.6-2.1x over the single GEMM."""
     tiles = -(-o // 128) * -(-i // 128)
     best = 1
     for s in (2, 4, 8):

@@ -11,7 +11,8 @@
 #   prof:<name>:<bench args>   rocprofv3 kernel trace + stats -> gpurun_out/prof_<name>/summary.txt
 #   py:<script> [args]         any tools/ python probe
 #   sh:<command>               a shell command line (env-var A/B arms: "sh:DTF_X=1 python bench.py")
-#   env:<K=V>                  export K=V for every later step of this call (e.g. before a prof:)
+#   env:<K=V>                  export K=V for every later step of this call (e.g. before a prof:);
+#                              env:PYTEST_K=<expr> gives later pytest: steps a -k expression (spaces ok)
 # Each step runs under its own time limit (STEP_TIMEOUT, default 600 s), logs to
 # gpurun_out/<TAG>/<n>_<kind>.log, and the run stops at the first failing step (no retries):
 # after a fault, abort, segfault or time limit nothing more touches the GPU in this call.
@@ -33,7 +34,11 @@ for step in "$@"; do
   echo "[gpu_run] step $n: $step" | tee -a "$OUT/steps.txt"
   t0=$(date +%s)
   case "$kind" in
-    pytest) timeout -k 10 "$T" python -u -m pytest -x -v --timeout 200 --timeout-method thread $arg > "$log" 2>&1 ;;
+    pytest) if [ -n "$PYTEST_K" ]; then
+              timeout -k 10 "$T" python -u -m pytest -x -v --timeout 200 --timeout-method thread -k "$PYTEST_K" $arg > "$log" 2>&1
+            else
+              timeout -k 10 "$T" python -u -m pytest -x -v --timeout 200 --timeout-method thread $arg > "$log" 2>&1
+            fi ;;
     gpu-suite) timeout -k 10 "$T" python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread --durations=25 > "$log" 2>&1 ;;
     smoke) timeout -k 10 "$T" python -u __graft_entry__.py smoke > "$log" 2>&1 ;;
     bench) timeout -k 10 "$T" python -u bench.py $arg > "$log" 2>&1 ;;
