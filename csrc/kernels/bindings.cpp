@@ -57,6 +57,7 @@ long dtf_bn_workspace_floats_g(int, int);
 int dtf_conv_stats_rows(long, int, int, int, int);
 void dtf_conv_set_halo(int);
 int dtf_gemm_conv_part_images(int, int, int, int, int, int);
+void dtf_gemm_set_pp2_strided(int);
 int dtf_conv_tile_rows(const ConvGeom&, const TapTable&, int bnb);
 bool dtf_conv_bnl_ok(const ConvGeom&, const TapTable&);
 void dtf_conv_set_bnl_probe(int);
@@ -757,6 +758,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
     return ok;
   });
   m.def("gemm_conv_part_images", &dtf_gemm_conv_part_images);
+  m.def("gemm_set_pp2_strided", &dtf_gemm_set_pp2_strided);
   m.def("conv_bnl_ok", [](std::vector<int> geom, std::vector<int> dh, std::vector<int> dw) {
     if (geom.size() != 16 && geom.size() != 17)
       throw std::runtime_error("conv_bnl_ok: geom needs 16 (+acc) ints");

@@ -1149,7 +1149,9 @@ gemm_pp2_kernel(const GemmArgs g) {
   // every store instruction writes four WHOLE 128-B lines (the swapped layout wrote 16 rows x
   // 32 B per instruction and completed a line only over four instructions 8 apart).  The K order
   // per output is unchanged: bit-identical to the swapped layout.
-  constexpr bool ILV = !strided;
+  // (round 6: the strided dgrad-phase rows too -- their output rows are addressed through a
+  // per-wave LDS row table, see the epilogue -- so the swapped layout below is no longer used)
+  constexpr bool ILV = true;
   auto plds = [&](int pc, int j) {
     const bool isA = pc == 0 || pc == 3;
     return (uint32_t)((isA ? 0 : Cf::SA) + (prow(pc, j) - lrow) * BK) * 2u;
@@ -1379,6 +1381,28 @@ gemm_pp2_kernel(const GemmArgs g) {
       // C descriptor): the hardware range check drops those stores and zero-fills those loads.
       int vo = col_ok ? ((wm * 128 + fq * 4) * g.ldc + ncol) * 2 : (int)0x80000000u;
       const int ldc2 = g.ldc * 2;
+      // strided (dgrad phase) rows: not uniformly spaced -- each wave decodes its 128 rows
+      // (two per lane) into a private LDS table of byte offsets from cbase (2^31: no row), and the
+      // stores / accumulate loads read 4 rows' offsets per fragment row with one ds_read_b128
+      int* rtab = reinterpret_cast<int*>(red + Cf::WM * 2 * BN) + wave * 128;
+      const int colb = col_ok ? ncol * 2 : (int)0x80000000u;
+      if constexpr (strided) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int m = cm0 + wm * 128 + lane + 64 * t;
+          int o = (int)0x80000000u;
+          if (m < g.M) {
+            const int q = m % g.Q, tt = m / g.Q;
+            const int p = tt % g.P, n = tt / g.P;
+            o = ((((n - n_lo) * g.Ho + p * g.osh + g.oh0) * g.Wo + q * g.osw + g.ow0) * g.ldc) * 2;
+          }
+          rtab[lane + 64 * t] = o;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's own table
+      }
+      auto rows4 = [&](int i) -> i32x4_t {        // strided: fragment row i's 4 row offsets
+        return *reinterpret_cast<const i32x4_t*>(rtab + 16 * i + 4 * fq);
+      };
       // accumulate operands (the unused one points at C with zero size)
       const __amdgpu_buffer_rsrc_t rcin = __builtin_amdgcn_make_buffer_rsrc(
           has_acc ? const_cast<bf16_t*>(g.Cin ? g.Cin + cbase : g.acc_src + cbase) : g.C, 0,
@@ -1399,23 +1423,27 @@ gemm_pp2_kernel(const GemmArgs g) {
       const int mshift = ncol & 7;                     // ldc % 8 == 0: the same for every row
       u32x2l_t pa[4], pn[4];
       uint32_t pm[4], pmn[4];
-      auto load_rows = [&](int vrow, u32x2l_t (&d)[4], uint32_t (&m)[4]) {
+      auto load_rows = [&](int vrow, int fi, u32x2l_t (&d)[4], uint32_t (&m)[4]) {
+        i32x4_t t4 = {0, 0, 0, 0};
+        if constexpr (strided) t4 = rows4(fi);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int o = vrow + r * ldc2;
+          const int o = strided ? (col_ok ? t4[r] + colb : (int)0x80000000u) : vrow + r * ldc2;
           d[r] = __builtin_bit_cast(u32x2l_t, __builtin_amdgcn_raw_buffer_load_b64(rld, o, 0, 0));
           m[r] = masked ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rmask, o >> 4, 0, 0) : 0u;
         }
       };
-      if constexpr (has_ld) load_rows(vo, pa, pm);
+      if constexpr (has_ld) load_rows(vo, 0, pa, pm);
 #pragma unroll
       for (int i = 0; i < Cf::FM; ++i) {
         if constexpr (has_ld) {
-          if (i + 1 < Cf::FM) load_rows(vo + 16 * ldc2, pn, pmn);
+          if (i + 1 < Cf::FM) load_rows(vo + 16 * ldc2, i + 1, pn, pmn);
         }
+        i32x4_t t4 = {0, 0, 0, 0};
+        if constexpr (strided) t4 = rows4(i);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int vr = vo + r * ldc2;
+          const int vr = strided ? (col_ok ? t4[r] + colb : (int)0x80000000u) : vo + r * ldc2;
           bf16_t h[4];
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
@@ -1645,7 +1673,9 @@ gemm_pp2_kernel(const GemmArgs g) {
 template <int CONV, int EPI>
 void launch_gemm_pp2_t(const GemmArgs& g0, long a_bytes, long b_bytes, hipStream_t st) {
   using Cf = GCfg<256, 256, 64, 2, 8>;
-  constexpr size_t LDS = (size_t)2 * Cf::STAGE * 2 + (size_t)Cf::WM * 2 * 256 * 4;
+  // + the strided epilogue's per-wave row tables (8 waves x 128 ints)
+  constexpr size_t LDS = (size_t)2 * Cf::STAGE * 2 + (size_t)Cf::WM * 2 * 256 * 4 +
+                         ((EPI & 4) ? (size_t)8 * 128 * 4 : 0);
   static bool attr = false;
   static int ncu = 0;
   if (!attr) {
@@ -1727,6 +1757,10 @@ int g_gemm_pp = 0;         // bit 0: persistent register-epilogue kernel for gem
 // profiles/measurements/r5_gemm_pp2_interleaved_epilogue_vs_v8.jsonl; ResNet-50 +0.6 %), bit 1 the
 // unit-stride implicit-GEMM convs (2-5 % per layer, r5_conv_pp2_per_layer_b1984.jsonl)
 int g_gemm_pp2 = 3;
+// the strided data-gradient phases on gemm_pp2 too (round 6: their rows through an LDS row table
+// in the interleaved full-line epilogue; round 5's swapped 32-B epilogue ran them 1.2-1.5x slower
+// than the ping-pong kernel)
+int g_gemm_pp2_strided = 1;
 int g_gemm_stream = 1;     // output-heavy shapes on the row-streaming kernel (gemm_stream.hip)
 
 int g_gemm_variant = -1;   // -1: auto; 0..3: force (tools/gemm_bench.py A/B)
@@ -1774,6 +1808,7 @@ void dtf_gemm_set_variant(int v) { g_gemm_variant = v; }
 void dtf_gemm_set_stream(int v) { g_gemm_stream = v; }
 void dtf_gemm_set_pp(int v) { g_gemm_pp = v; }
 void dtf_gemm_set_pp2(int v) { g_gemm_pp2 = v; }
+void dtf_gemm_set_pp2_strided(int v) { g_gemm_pp2_strided = v; }
 int dtf_gemm_get_pp2() { return g_gemm_pp2; }
 void dtf_gemm_set_nt(int v) { g_gemm_nt = v; }
 void dtf_gemm_set_dbg(int v) { g_gemm_dbg = v; }
@@ -1844,8 +1879,9 @@ void dtf_gemm_conv(const bf16_t* X, const bf16_t* Wt, bf16_t* Y, int N, int H, i
   // epilogue is the swapped 32-B piece one -- 1.2-1.5x slower than the ping-pong's on the
   // stride-2 data gradients, while the unit-stride convs gain 2-5 %
   // (profiles/measurements/r5_conv_pp2_per_layer_b1984.jsonl)
-  else if ((g_gemm_pp2 & 2) && osh == 1 && osw == 1 && g.K >= 128 && x_bytes < 0x7FFFFF00L &&
-           w_bytes < 0x7FFFFF00L && N < 2048 && H < 1000 && W < 1000 && pp_span)
+  else if ((g_gemm_pp2 & 2) && (g_gemm_pp2_strided || (osh == 1 && osw == 1)) && g.K >= 128 &&
+           x_bytes < 0x7FFFFF00L && w_bytes < 0x7FFFFF00L && N < 2048 && H < 1000 && W < 1000 &&
+           pp_span)
     launch_gemm_pp2<1>(g, x_bytes, w_bytes, st);
   else if ((g_gemm_pp & 2) && (g.K + 63) / 64 >= 2 && pp_span) launch_gemm_pp<1>(g, st);
   else launch_gemm<256, 256, 64, 2, 2, 8, 1, 1>(g, st);

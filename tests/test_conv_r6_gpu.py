@@ -143,3 +143,35 @@ def test_projection_shortcut_input_past_2gib_runs_in_batch_parts():
     ref = torch.nn.functional.conv2d(x[-4:].float().permute(0, 3, 1, 2),
                                      w.float().permute(0, 3, 1, 2), stride=2).permute(0, 2, 3, 1)
     assert float((yg[-4:].float() - ref).norm() / ref.norm()) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,K,R,acc", [(2, 28, 256, 256, 3, False), (3, 14, 512, 512, 3, False),
+                                           (2, 56, 256, 512, 1, True), (3, 28, 512, 1024, 1, False),
+                                           (5, 14, 1024, 2048, 1, True)])
+def test_strided_dgrad_phases_on_the_persistent_gemm(N, H, C, K, R, acc):
+    """Stride-2 data gradients whose phase classes run on the GEMM (output channels >= 256: the
+    3x3 of stages 3-4, every projection shortcut) now take the persistent kernel, output rows
+    addressed through its per-wave LDS row table: bit-identical to the round-5 ping-pong kernel,
+    with and without the accumulate (Cin) epilogue, and against fp32 PyTorch."""
+    torch.manual_seed(0)
+    dy = torch.randn(N, H // 2, H // 2, K, device="cuda").bfloat16()
+    w = (torch.randn(K, R, R, C, device="cuda") / (R * R * C) ** 0.5).bfloat16()
+    base = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    pad = R // 2
+    outs = []
+    try:
+        for on in (1, 0):
+            native._K.gemm_set_pp2_strided(on)
+            out = base.clone() if acc else None
+            outs.append(native.conv2d_dgrad(dy, w, (N, H, H, C), 2, pad, out=out).clone())
+            torch.cuda.synchronize()
+    finally:
+        native._K.gemm_set_pp2_strided(1)
+    assert torch.equal(outs[0], outs[1])
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2),
+                                     dy.float().permute(0, 3, 1, 2), stride=2,
+                                     padding=pad).permute(0, 2, 3, 1)
+    if acc:
+        ref = ref + base.float()
+    rel = float((outs[0].float() - ref).norm() / ref.norm())
+    assert rel < 1e-2, rel

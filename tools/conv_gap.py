@@ -84,6 +84,23 @@ def main():
         print(json.dumps(rec), flush=True)
         del dy
         torch.cuda.empty_cache()
+    # strided data gradients on the GEMM (output channels >= 256): the persistent kernel with its
+    # row-table epilogue vs the round-5 ping-pong kernel
+    for name, H, C, K, R in (("s2b0c2", 28, 256, 256, 3), ("s3b0c2", 14, 512, 512, 3),
+                             ("s1b0proj", 56, 256, 512, 1), ("s2b0proj", 28, 512, 1024, 1),
+                             ("s3b0proj", 14, 1024, 2048, 1)):
+        B = a.batch
+        dy = torch.randn(B, H // 2, H // 2, K, device=dev).to(torch.bfloat16)
+        w = (torch.randn(K, R, R, C, device=dev) * 0.02).to(torch.bfloat16)
+        rec = {"layer": name + "_dgrad_gemm"}
+        for tag, on in (("pp2", 1), ("pingpong", 0)):
+            K_.gemm_set_pp2_strided(on)
+            rec[tag + "_us"] = round(timeit(
+                lambda: native.conv2d_dgrad(dy, w, (B, H, H, C), 2, R // 2), a.iters), 1)
+        K_.gemm_set_pp2_strided(1)
+        print(json.dumps(rec), flush=True)
+        del dy
+        torch.cuda.empty_cache()
     # projection shortcuts: 1x1 stride 2 forward with the BN statistics epilogue
     for name, H, C, K in (("s1b0proj", 56, 256, 512), ("s2b0proj", 28, 512, 1024),
                           ("s3b0proj", 14, 1024, 2048)):
