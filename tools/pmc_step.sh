@@ -1,0 +1,26 @@
+#!/bin/bash
+# PMC counters of every kernel of a short bench.py run (default: the ResNet-50 b1984 step), two
+# passes in their own runs (rocprofv3 --pmc only, no traces): SQ issue/wait breakdown + MFMA busy,
+# then L2 traffic (FETCH_SIZE, WRITE_SIZE) + GRBM_GUI_ACTIVE (clock).  Summaries:
+# gpurun_out/pmc_step/{sq,tcc}/summary.txt.
+#   gpurun -- bash tools/pmc_step.sh [bench.py args]
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+export PYTHONPATH="$R${PYTHONPATH:+:$PYTHONPATH}"
+ARGS=${*:-"--steps 2 --warmup 1"}
+cd /tmp || exit 1
+run_pass() {
+  local name=$1; shift
+  local out="$R/gpurun_out/pmc_step/$name"
+  mkdir -p "$out"
+  timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d "/tmp/pmc_$name" -o run -- \
+    python3 "$R/bench.py" $ARGS > "$out/run.log" 2>&1
+  local rc=$?
+  find "/tmp/pmc_$name" -name "*counter_collection*.csv" -exec cp {} "$out/" \;
+  python3 "$R/tools/summarize_pmc.py" "$out" > "$out/summary.txt" 2>&1
+  rm -rf "/tmp/pmc_$name"
+  return $rc
+}
+run_pass sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+  SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_BUSY_CYCLES &&
+run_pass tcc FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT
