@@ -1521,8 +1521,9 @@ def _dense_gemm_native(M, N, K):
 
 
 class _Dense(torch.autograd.Function):
-    """y = x @ W^T (+ b) with the bf16 weight shadow -- on hipBLASLt, or with DTF_DENSE_GEMM=native
-    on our persistent MFMA GEMM with the bias in its epilogue (forward) and the pending residual
+    """y = x @ W^T (+ b) with the bf16 weight shadow -- by default (DTF_DENSE_GEMM=native) on our
+    persistent MFMA GEMM (hipBLASLt under DTF_DENSE_GEMM=library and for shapes it does not
+    take) with the bias in its epilogue (forward) and the pending residual
     gradient accumulated with beta = 1 (data gradient); backward produces dW and db in fp32
     straight into the optimizer's flat gradient buffer (no bf16 dW, no cast/add kernels)."""
 
@@ -1829,9 +1830,12 @@ class _NativeDense(torch.autograd.Function):
 
 def dense(x, w, b=None, relu=False, impl=None):
     """Dense layer.  ``impl``: "native" (default; the hand-written MFMA GEMM with fused
-    bias / ReLU epilogues) or "library" (hipBLASLt; kept for BERT's plain GEMMs, where the
-    library kernels are still faster -- tools/gemm_bench.py -- and the task rules allow plain
-    library GEMMs).  Trainable fp32 masters get fp32 dW / db straight in the flat buffer."""
+    bias / ReLU epilogues) or "library" -- the name is historical: the bias-in-epilogue form
+    BERT uses (:class:`_Dense`), whose forward and data gradient also run on our persistent MFMA
+    GEMM for every shape it takes (``DTF_DENSE_GEMM=native``, the default; the fp32 bias is added
+    in the epilogue, so it is not bit-identical to the hipBLASLt + bf16-bias A/B arm
+    ``DTF_DENSE_GEMM=library``) and on hipBLASLt only for other shapes.  Trainable fp32 masters
+    get fp32 dW / db straight in the flat buffer."""
     impl = impl or _DENSE_IMPL
     if (impl == "native" and w.dtype == torch.float32 and x.dtype == _BF16 and x.is_cuda
             and w.dim() == 2 and x.shape[-1] % 8 == 0):

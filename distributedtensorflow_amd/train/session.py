@@ -392,8 +392,24 @@ class MonitoredTrainingSession:
         for h in self.hooks:
             h.after_create_session(self._session, None)
 
-    def _recover(self, exc=None):
-        self.recoveries += 1
+    def _rejoin(self, state):
+        """The cluster re-formation step of a recovery, done at most once per recovery: a retry
+        after a later phase failed (restore, PS registration, the post-restore sync) does not
+        leave the epoch it already joined -- ``restart_group`` would wait for an epoch after it,
+        which only comes if the launcher restarts another task -- unless the cluster moved on
+        again meanwhile (``cluster_changed``)."""
+        strat = self.strategy
+        changed = getattr(strat, "cluster_changed", None)
+        if "epoch" not in state or (changed is not None and changed()):
+            state["epoch"] = strat.recover_cluster(self.scaffold.optimizer)
+        return state["epoch"]
+
+    def _recover(self, exc=None, state=None):
+        if state is None:
+            state = {}
+        if not state.get("counted"):
+            self.recoveries += 1          # one recovery, however many retries it takes
+            state["counted"] = True
         strat = self.strategy
         sc = self.scaffold
         if exc is not None and not isinstance(exc, InjectedFault) and \
@@ -403,7 +419,7 @@ class MonitoredTrainingSession:
             # every replica continues from the chief's state (the restarted one does the same
             # from its MonitoredTrainingSession creation)
             print(f"[dtf] recovering from {type(exc).__name__}: {exc}", flush=True)
-            epoch = strat.recover_cluster(sc.optimizer)
+            epoch = self._rejoin(state)
             ckpt = latest_checkpoint(self.checkpoint_dir) if self.checkpoint_dir else None
             restored = False
             if self.is_chief and ckpt and sc.saver is not None:
@@ -425,7 +441,7 @@ class MonitoredTrainingSession:
             # chief restores the latest checkpoint and re-initialises the PS shards with it,
             # the other workers wait for that and pull
             print(f"[dtf] recovering from {type(exc).__name__}: {exc}", flush=True)
-            gen = strat.recover_cluster(sc.optimizer)
+            gen = self._rejoin(state)
             restored = False
             ckpt = latest_checkpoint(self.checkpoint_dir) if self.checkpoint_dir else None
             if self.is_chief and ckpt and sc.saver is not None:
@@ -492,9 +508,10 @@ class MonitoredTrainingSession:
                     raise
                 # a recovery that itself hits a recoverable failure (the restarted task not up
                 # yet, a peer dying mid-rejoin) is retried within the same attempt budget
+                state = {}                # what this recovery already did (see _rejoin)
                 while True:
                     try:
-                        self._recover(e)
+                        self._recover(e, state)
                         break
                     except Exception as e2:      # noqa: BLE001
                         # a TimeoutError already waited out the recovery budget: not retried

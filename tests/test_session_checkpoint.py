@@ -144,15 +144,67 @@ def test_failed_recovery_is_retried_within_the_attempt_budget(tmp_path):
                                   global_step=gstep, strategy=strat) as sess:
         real, calls = sess._recover, []
 
-        def flaky(exc=None):
+        def flaky(exc=None, state=None):
             calls.append(type(exc).__name__)
             if len(calls) == 1:
                 raise InjectedFault("recovery interrupted")
-            return real(exc)
+            return real(exc, state)
         sess._recover = flaky
         while not sess.should_stop():
             sess.run(train_op)
     assert fault.fired and len(calls) == 2 and gstep.value() == 8
+
+
+def test_recovery_retry_resumes_after_the_rejoin():
+    """A recovery whose post-rejoin phase fails (here the synchronous world's post-restore sync)
+    is retried WITHOUT re-forming the cluster again: recover_cluster would wait for an epoch
+    after the one just joined, which only comes if another task is restarted.  Only a cluster
+    that moved on meanwhile (cluster_changed) is re-joined.  One recovery is counted once."""
+    from distributedtensorflow_amd.train.session import MonitoredTrainingSession as MTS
+
+    class _Strat:
+        collective = True
+
+        def __init__(self):
+            self.rejoins, self.syncs, self.moved = 0, 0, False
+
+        def recover_cluster(self, optimizer=None):
+            self.rejoins += 1
+            self.moved = False
+            return self.rejoins
+
+        def cluster_changed(self):
+            return self.moved
+
+        def sync_after_restore(self, optimizer, global_step, restored=False):
+            self.syncs += 1
+            if self.syncs == 1:
+                raise ConnectionError("peer died mid-rejoin")
+
+    class _Scaffold:
+        optimizer = saver = None
+
+        class global_step:
+            @staticmethod
+            def value():
+                return 7
+
+    sess = MTS.__new__(MTS)
+    sess.strategy, sess.scaffold, sess.hooks = _Strat(), _Scaffold(), []
+    sess.checkpoint_dir, sess.is_chief, sess._session, sess.recoveries = None, True, None, 0
+    state = {}
+    with pytest.raises(ConnectionError):
+        sess._recover(ConnectionError("peer died"), state)
+    sess._recover(ConnectionError("peer died"), state)       # the retry
+    assert sess.strategy.rejoins == 1 and sess.strategy.syncs == 2 and sess.recoveries == 1
+    # the cluster moved to a newer epoch before the retry: that one is joined
+    state = {}
+    sess.strategy.syncs = 0
+    with pytest.raises(ConnectionError):
+        sess._recover(ConnectionError("peer died"), state)
+    sess.strategy.moved = True
+    sess._recover(ConnectionError("peer died"), state)
+    assert sess.strategy.rejoins == 3 and sess.recoveries == 2
 
 
 def test_exit_never_masks_the_failure_with_the_ps_stop():
