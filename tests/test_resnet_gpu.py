@@ -960,7 +960,12 @@ def test_no_record_outlives_its_step():
         if was:
             gc.enable()
     assert min(made) > 0, made                       # the step does create records
-    # the per-step caches alternate by a few MB; one leaked step's records would hold its c1
-    # outputs and more (~11 MB per step at this batch, 23 steps: > 250 MB)
-    assert max(peaks[1:]) - min(peaks[1:]) < 4 * 2**20, peaks
+    # one leaked step's records would hold its c1 outputs and more (~11 MB per step at this
+    # batch: > 250 MB over 23 steps), a GROWTH; without one the peak only jitters by a few MB
+    # (per-step caches alternating, and the side-stream weight-gradient launches interleaving
+    # their allocations with the main stream's differently from step to step: 1.2-3 MB on
+    # fresh boxes)
+    early, late = max(peaks[1:6]), max(peaks[-5:])
+    assert late - early < 4 * 2**20, peaks
+    assert max(peaks[1:]) - min(peaks[1:]) < 8 * 2**20, peaks
     assert abs(peaks[24] - peaks[1]) < 4 * 2**20, peaks
