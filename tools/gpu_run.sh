@@ -53,6 +53,9 @@ for step in "$@"; do
       # the ordered dispatch list of the last ~1.3 steps (layer mapping: tools/trace_dump.py)
       python3 "$R/tools/trace_dump.py" "/tmp/prof_$name" --last ${TRACE_LAST:-900} --min-us 5 \
         > "$OUT/prof_$name/trace_tail.txt" 2>&1
+      # GPU idle inside the last step (dispatches per step: GAP_LAST, ResNet-50 ~645, BERT ~816)
+      python3 "$R/tools/trace_gaps.py" "/tmp/prof_$name" --last ${GAP_LAST:-645} \
+        > "$OUT/prof_$name/gaps.txt" 2>&1
       rm -rf "/tmp/prof_$name"
       (exit $rc) ;;
     py) timeout -k 10 "$T" python -u $arg > "$log" 2>&1 ;;
