@@ -100,6 +100,7 @@ void dtf_gap_bwd(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void dtf_bn_relu_maxpool_fwd(const bf16_t*, const float*, const float*, bf16_t*, uint8_t*, int,
                              int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 void dtf_pool_set_blocked(int);
+void dtf_s2d_set_rows(int);
 int dtf_pool_bn_bwd_blocks(int, int, int, int);
 void dtf_pool_bn_bwd_set_caps(int, int);
 void dtf_pool_bn_bwd_reduce(const bf16_t*, const uint8_t*, const bf16_t*, const float*,
@@ -622,6 +623,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
     check_launch("bn_relu_maxpool_fwd");
   });
   m.def("pool_set_blocked", &dtf_pool_set_blocked);
+  m.def("s2d_set_rows", &dtf_s2d_set_rows);
   m.def("pool_bn_bwd_blocks", &dtf_pool_bn_bwd_blocks);
   m.def("pool_bn_bwd_set_caps", &dtf_pool_bn_bwd_set_caps);
   m.def("pool_bn_bwd_reduce", [](uintptr_t dy, uintptr_t arg, uintptr_t x, uintptr_t mean,

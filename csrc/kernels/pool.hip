@@ -489,6 +489,60 @@ s2d_input_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ xs, int N, i
   }
 }
 
+// Row form for images whose rows are whole 16-B chunks (the 224 x 224 x 3 ResNet input: 1344 B
+// per row): a block stages one output row's SS input rows in LDS with 16-B loads -- the pixel
+// kernel above issues 12 two-byte loads per output pixel (~3.3 TB/s at b1984) -- then every lane
+// assembles one output pixel's channels from LDS and stores them as 16-B chunks.  Same values,
+// same zero fill: bit-identical.
+constexpr int kS2dT = 128, kS2dMaxChunks = 256;   // input rows of up to 2048 bf16
+template <int SS, int CP>
+__global__ void __launch_bounds__(kS2dT)
+s2d_rows_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ xs, int N, int H, int W,
+                int C, int Ho, int Wo, int pad) {
+  constexpr int OC = SS * SS * CP;
+  static_assert(OC % 8 == 0, "s2d channels must fill 16-B chunks");
+  __shared__ uint4 rows[SS][kS2dMaxChunks];
+  const int rc = W * C / 8;                        // 16-B chunks per input row (host-checked)
+  const long nrows = (long)N * Ho;
+  const bf16_t* rb = reinterpret_cast<const bf16_t*>(&rows[0][0]);
+  for (long r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const int i = (int)(r % Ho);
+    const int n = (int)(r / Ho);
+    __syncthreads();                               // the previous row's LDS reads are done
+#pragma unroll
+    for (int a = 0; a < SS; ++a) {
+      const int h = SS * i + a - pad;
+      const bool in = h >= 0 && h < H;
+      const uint4* src = reinterpret_cast<const uint4*>(x + ((long)n * H + (in ? h : 0)) * W * C);
+      for (int k = threadIdx.x; k < rc; k += kS2dT) rows[a][k] = in ? src[k] : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < Wo; j += kS2dT) {
+      bf16_t v[OC];
+#pragma unroll
+      for (int a = 0; a < SS; ++a)
+#pragma unroll
+        for (int b = 0; b < SS; ++b) {
+          const int w = SS * j + b - pad;
+          const bool in = w >= 0 && w < W;
+          const bf16_t* src = rb + a * kS2dMaxChunks * 8 + (in ? w : 0) * C;
+#pragma unroll
+          for (int ch = 0; ch < CP; ++ch) v[(a * SS + b) * CP + ch] = (in && ch < C) ? src[ch] : (bf16_t)0;
+        }
+      uint4* dst = reinterpret_cast<uint4*>(xs + (r * Wo + j) * OC);
+#pragma unroll
+      for (int k = 0; k < OC / 8; ++k) {
+        uint4 u;
+        u.x = (uint32_t)v[8 * k + 0] | ((uint32_t)v[8 * k + 1] << 16);
+        u.y = (uint32_t)v[8 * k + 2] | ((uint32_t)v[8 * k + 3] << 16);
+        u.z = (uint32_t)v[8 * k + 4] | ((uint32_t)v[8 * k + 5] << 16);
+        u.w = (uint32_t)v[8 * k + 6] | ((uint32_t)v[8 * k + 7] << 16);
+        dst[k] = u;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 void dtf_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* arg, int N, int H, int W, int C,
@@ -533,10 +587,26 @@ void dtf_gap_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t
                      dx, N, HW, C);
 }
 
+static int g_s2d_rows = 1;   // 0: always the per-pixel kernel (tests compare both)
+void dtf_s2d_set_rows(int v) { g_s2d_rows = v; }
+
 void dtf_s2d_input(const bf16_t* x, bf16_t* xs, int N, int H, int W, int C, int Ho, int Wo,
                    int s, int cp, int pad, hipStream_t st) {
   if (s != 2 || (cp != 2 && cp != 4) || C > cp)
     throw std::runtime_error("s2d_input: stride 2 with C <= 4 channels only (image stems)");
+  // row form: whole 16-B input rows that fit the LDS image, 16-B aligned input
+  if (g_s2d_rows && (W * C) % 8 == 0 && W * C / 8 <= kS2dMaxChunks &&
+      (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const long nrows = (long)N * Ho;
+    const int gr = (int)(nrows < 16384 ? nrows : 16384);
+    if (cp == 4)
+      hipLaunchKernelGGL((s2d_rows_kernel<2, 4>), dim3(gr), dim3(kS2dT), 0, st, x, xs, N, H, W, C,
+                         Ho, Wo, pad);
+    else
+      hipLaunchKernelGGL((s2d_rows_kernel<2, 2>), dim3(gr), dim3(kS2dT), 0, st, x, xs, N, H, W, C,
+                         Ho, Wo, pad);
+    return;
+  }
   const long total = (long)N * Ho * Wo;
   long g = (total + kT - 1) / kT;
   if (g > 65536) g = 65536;

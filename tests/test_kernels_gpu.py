@@ -312,15 +312,23 @@ def test_bf16_col_sum(T, N):
                                rtol=1e-4)
 
 
-@pytest.mark.parametrize("n,h,w,c", [(2, 224, 224, 3), (3, 33, 31, 3), (1, 20, 18, 1)])
-def test_space_to_depth_input_kernel(n, h, w, c):
-    """One-pass HIP space-to-depth of the stem input == the torch pad + permute rewrite."""
+@pytest.mark.parametrize("rows", [1, 0])
+@pytest.mark.parametrize("n,h,w,c", [(2, 224, 224, 3), (3, 33, 31, 3), (1, 20, 18, 1),
+                                     (2, 24, 16, 2), (1, 19, 8, 3)])
+def test_space_to_depth_input_kernel(n, h, w, c, rows):
+    """One-pass HIP space-to-depth of the stem input == the torch pad + permute rewrite, in the
+    row-staged form (inputs whose rows are whole 16-B chunks: 224 x 3, 16 x 2, 8 x 3) and the
+    per-pixel form (every shape)."""
     from distributedtensorflow_amd.ops import reference as ref
     nat = _native()
     x = torch.randn(n, h, w, c, device=dev).to(torch.bfloat16)
     wt = torch.randn(64, 7, 7, c, device=dev)
     xs_ref, _ = ref.space_to_depth_operands(x, wt, 2, 3)
-    xs = nat.space_to_depth_input(x, 2, 3, 7, 7)
+    nat._K.s2d_set_rows(rows)
+    try:
+        xs = nat.space_to_depth_input(x, 2, 3, 7, 7)
+    finally:
+        nat._K.s2d_set_rows(1)
     assert xs.shape == xs_ref.shape
     assert torch.equal(xs, xs_ref)
 
