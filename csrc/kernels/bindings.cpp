@@ -137,6 +137,7 @@ void dtf_conv_wgrad(const bf16_t*, const bf16_t*, float*, float*, WgradGeom, con
 int dtf_conv_wgrad_splits(long, int, int, long, int);
 int dtf_conv_wgrad_halo_splits(int, int, int, int, int, int, int, int, int, const TapTableW&);
 void dtf_wgrad_set_halo(int);
+void dtf_wgrad_set_stem(int);
 void dtf_conv_set_halo_stages(int);
 void dtf_wgrad_set_dma_mode(int);
 void dtf_wgrad_set_pipe(int);
@@ -798,6 +799,7 @@ PYBIND11_MODULE(_dtf_hip, m) {
                                       geom[8], geom[6], geom[7], make_taps<TapTableW>(dh, dw));
   });
   m.def("wgrad_set_halo", &dtf_wgrad_set_halo);
+  m.def("wgrad_set_stem", &dtf_wgrad_set_stem);
   m.def("wgrad_set_dma_mode", &dtf_wgrad_set_dma_mode);
   m.def("wgrad_set_pipe", &dtf_wgrad_set_pipe);
   m.def("wgrad_set_pp", &dtf_wgrad_set_pp);

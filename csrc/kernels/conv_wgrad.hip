@@ -1016,6 +1016,146 @@ conv_wgrad_halo_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ 
       for (int r = 0; r < 4; ++r)
         out[(long)(16 * i + 4 * gq + r) * 576 + wave * 64 + 16 * j + li] = acc[i][j][r];
 }
+
+// ---------------------------------------------------------------------------------------------
+// Halo wgrad for the ResNet-50 stem on its space-to-depth image: a 4 x 4 stride-1 VALID conv,
+// X [N][115][115][16] -> dY [N][112][112][64], dW [64][4][4][16] (ops.reference
+// space_to_depth_operands).  The tiled kernel gathers each pixel's 16 taps x 32 B from L2
+// (512 B of L2 -> LDS traffic per pixel beside its 128 B of dY: 1.23 ms per step at b1984,
+// 0.38 PF on the stem's real FLOPs).  Here a block walks strips of kStTH output rows: the strip's
+// dY rows and the kStTH + 3 X rows under them -- each one contiguous span -- are LDS-DMA'd once,
+// double-buffered (the next strip streams in under this strip's MFMAs).  Wave w owns tap row
+// dh = w % 4, i.e. dW[:, dh, 0..3, :] = 64 x 64 (16 fragments), over the strip's 32-pixel chunks
+// of parity w / 4 (flipped every strip so both halves do the same number); its B fragment for
+// tap (dh, dw) is 2 x 4 consecutive output pixels' X pixels shifted by (dh, dw) -- 32-B rows at a
+// 32-B pitch, read with the same transposed ds_read_b64_tr_b16 pairs as the A (dY) fragments.
+// The two halves' partial dW meet in LDS in fixed order; each block leaves one fp32 slab
+// [64][256], summed in order by slab_reduce (deterministic).
+constexpr int kStTH = 2, kStQ = 112, kStXW = 115, kStC = 16, kStK = 64;
+constexpr int kStT = 512;                                       // 8 waves: 4 tap rows x 2 halves
+constexpr int kStDyB = kStTH * kStQ * kStK * 2;                 // dY bytes per strip (28 KB)
+constexpr int kStXB = (kStTH + 3) * kStXW * kStC * 2;           // X bytes per strip (18,400)
+constexpr int kStXI = (kStXB + 1023) / 1024;                    // its 1-KB DMA instructions
+constexpr int kStStage = kStDyB + kStXI * 1024;                 // bytes per stage
+constexpr size_t kStLDS = 2 * (size_t)kStStage;
+static_assert(kStLDS >= 4 * 64 * 64 * 4, "the halves' combine area fits the stages");
+static_assert(kStQ % 4 == 0 && (kStTH * kStQ) % 32 == 0, "4-pixel groups inside one row");
+// K order of a 32-pixel chunk: lane group g takes pixels 4g .. 4g + 3 (lo half of its operand)
+// and 16 + 4g .. 16 + 4g + 3 (hi half), the same in both operands, so the two 16-lane groups of a
+// 32-lane read pass touch 8 consecutive pixels: 256 contiguous B of the X image (32-B pixels)
+// and dY rows 8 apart under this swizzle -- both conflict-free
+DTF_DEV int st_swz(int r) { return ((r >> 1) & 3) << 1; }
+DTF_DEV int st_el(int r, int c) { return r * 64 + (((c >> 3) ^ st_swz(r)) << 3) + (c & 7); }
+
+__global__ void __launch_bounds__(kStT, 1)
+conv_wgrad_stem_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
+                       float* __restrict__ ws, int N) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int dh = wave & 3, half = wave >> 2;
+  constexpr int tiles_h = kStQ / kStTH;
+  const int nstrip = N * tiles_h;
+  const int G = gridDim.x;
+  const uint32_t lds0 = lds_addr(lds);
+  constexpr long ximg = (long)kStXW * kStXW * kStC;             // elements per image
+  constexpr long yimg = (long)kStQ * kStQ * kStK;
+
+  // per stage: dY 28 instructions (8 pixels x 128 B, chunk-swizzled like the 3x3 halo kernel),
+  // then X 18 (a flat copy of the strip's contiguous rows); descriptors based at the strip (the
+  // tensors pass 2^31 bytes), sized 0 past the last strip (no traffic)
+  auto issue = [&](int strip, int stage) {
+    const bool live = strip < nstrip;
+    const int sn = live ? strip / tiles_h : 0, p0 = live ? (strip % tiles_h) * kStTH : 0;
+    const i32x4_t ry = rsrc_quad(dY + sn * yimg + (long)p0 * kStQ * kStK, live ? kStDyB : 0);
+    const i32x4_t rx = rsrc_quad(X + sn * ximg + (long)p0 * kStXW * kStC, live ? kStXB : 0);
+    const uint32_t base = lds0 + (uint32_t)(stage * kStStage);
+    const int rloc = lane >> 3, slot = lane & 7;
+    for (int q = wave; q < kStDyB / 1024 + kStXI; q += 8) {
+      if (q < kStDyB / 1024) {
+        const int r = q * 8 + rloc;
+        const int chunk = slot ^ st_swz(r);
+        dma16(ry, base + (uint32_t)(q * 1024), (uint32_t)((r * kStK + chunk * 8) * 2));
+      } else {
+        const int qx = q - kStDyB / 1024;
+        dma16(rx, base + (uint32_t)(q * 1024), (uint32_t)(qx * 1024 + lane * 16));
+      }
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const int gq = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;
+
+  int s = blockIdx.x, it = 0;
+  issue(s, 0);
+  for (; s < nstrip; s += G, ++it) {
+    DTF_WAIT_VM(0);            // this strip's DMAs (own) landed ...
+    __syncthreads();           // ... everyone's; everyone finished reading the other stage
+    issue(s + G, (it + 1) & 1);
+    const bf16_t* sy = lds + (it & 1) * (kStStage / 2);
+    const bf16_t* sx = sy + kStDyB / 2;
+    // (measured: a 3-slot ring, a 2-chunk register double buffer and the same loop unrolled all
+    // ran this kernel 0-12 % slower -- r6x2..r6x4)
+#pragma unroll 1
+    for (int kc = (half + it) & 1; kc < kStTH * kStQ / 32; kc += 2) {
+      const int pl = 32 * kc + 4 * gq, ph = pl + 16;            // this lane group's 2 x 4 pixels
+      const int rl = pl / kStQ, rh = ph / kStQ;                 // 4 | 112: each 4 in one row
+      const int xl = (rl + dh) * kStXW + pl - rl * kStQ;        // X pixels of tap (dh, 0)
+      const int xh = (rh + dh) * kStXW + ph - rh * kStQ;
+      bf16x8_t af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c0 = 16 * i + 4 * tp;
+        const s4_t lo = tr_read(sy + st_el(pl + tq, c0));
+        const s4_t hi = tr_read(sy + st_el(ph + tq, c0));
+        af[i] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {                             // j = dw
+        const s4_t lo = tr_read(sx + (xl + tq + j) * kStC + 4 * tp);
+        const s4_t hi = tr_read(sx + (xh + tq + j) * kStC + 4 * tp);
+        bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  DTF_WAIT_VM(0);              // the trailing no-op DMAs still target the LDS
+  __syncthreads();             // every fragment read done: the stages become the combine area
+  float* red = reinterpret_cast<float*>(lds);                   // [dh][k][64 columns]
+  if (half == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          red[(dh * 64 + 16 * i + 4 * gq + r) * 64 + 16 * j + li] = acc[i][j][r];
+  }
+  __syncthreads();
+  if (half == 0) {
+    // slab of this block: ws[blockIdx.x][k][(dh * 4 + dw) * 16 + c], half 0 + half 1
+    float* out = ws + (long)blockIdx.x * (kStK * 256);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * i + 4 * gq + r;
+          out[(long)k * 256 + dh * 64 + 16 * j + li] =
+              acc[i][j][r] + red[(dh * 64 + k) * 64 + 16 * j + li];
+        }
+  }
+}
 }  // namespace
 
 // -1 / 1: LDS-DMA kernel whenever legal (default), 0: the register-staged kernel (A/B tests)
@@ -1074,6 +1214,22 @@ static bool wgrad_halo_ok(const WgradGeom& g, const TapTableW& taps) {
     if (taps.dh[t] != t / 3 - 1 || taps.dw[t] != t % 3 - 1) return false;
   return true;
 }
+// the stem route: the 4 x 4 VALID conv on the s2d image, X 115 x 115 x 16 -> 112 x 112 x 64
+static int g_wgrad_stem = 1;   // 0: the tiled kernels (A/B tests)
+void dtf_wgrad_set_stem(int v) { g_wgrad_stem = v; }
+static bool wgrad_stem_ok(const WgradGeom& g, const TapTableW& taps) {
+  if (!g_wgrad_stem || g.C != kStC || g.Kout != kStK || g.H != kStXW || g.W != kStXW ||
+      g.P != kStQ || g.Q != kStQ || g.sh != 1 || g.sw != 1 || taps.n != 16 || g.ldw != 256 ||
+      g.N <= 0)
+    return false;
+  for (int t = 0; t < 16; ++t)
+    if (taps.dh[t] != t / 4 || taps.dw[t] != t % 4) return false;
+  return true;
+}
+static int wgrad_stem_blocks(int N) {
+  const long strips = (long)N * (kStQ / kStTH);
+  return strips < 256 ? (int)strips : 256;
+}
 static int wgrad_halo_blocks(int N, int H) {
   const int strips = N * (H / kHwTH);
   return strips < 256 ? strips : 256;
@@ -1085,7 +1241,8 @@ int dtf_conv_wgrad_halo_splits(int N, int H, int W, int C, int P, int Q, int Kou
   WgradGeom g{};
   g.N = N; g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.sh = sh; g.sw = sw; g.Kout = Kout;
   g.ldw = taps.n * C;
-  return wgrad_halo_ok(g, taps) ? wgrad_halo_blocks(N, H) : 0;
+  if (wgrad_halo_ok(g, taps)) return wgrad_halo_blocks(N, H);
+  return wgrad_stem_ok(g, taps) ? wgrad_stem_blocks(N) : 0;
 }
 
 int dtf_conv_wgrad_splits(long M, int Kout, int TC, long ws_cap, int taps) {
@@ -1129,6 +1286,20 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
     hipLaunchKernelGGL(conv_wgrad_halo_kernel, dim3((unsigned)splits), dim3(kHwT), kHwLDS, st, X,
                        dY, ws, g.N, g.H);
     launch_slab_reduce(ws, dW, 64L * 576, 64L * 576, splits, accumulate, st);
+    return;
+  }
+
+  if (wgrad_stem_ok(g, taps) && splits == wgrad_stem_blocks(g.N)) {
+    if (!ws) throw std::runtime_error("wgrad stem: needs the slab workspace");
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_stem_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStLDS));
+      attr = true;
+    }
+    hipLaunchKernelGGL(conv_wgrad_stem_kernel, dim3((unsigned)splits), dim3(kStT), kStLDS, st, X,
+                       dY, ws, g.N);
+    launch_slab_reduce(ws, dW, (long)kStK * 256, (long)kStK * 256, splits, accumulate, st);
     return;
   }
 

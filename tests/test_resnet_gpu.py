@@ -743,6 +743,34 @@ def test_wgrad_halo_kernel_vs_fp32(n, acc):
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("n,acc", [(3, False), (6, True)])
+def test_wgrad_stem_kernel_vs_fp32(n, acc):
+    """The stem's weight gradient on its space-to-depth image (4x4 VALID taps over 16 channels,
+    115x115 -> 112x112x64) on the strip kernel (one tap row per wave pair, the strip's dY and X
+    rows LDS-DMA'd once, per-block fp32 slabs reduced in order) against the fp32 reference and
+    the tiled kernel; n = 6 gives the blocks two strips each (both LDS stages, both chunk-parity
+    assignments); with accumulation into an existing gradient."""
+    g = torch.Generator(device="cuda").manual_seed(n)
+    xs = torch.randn(n, 115, 115, 16, device="cuda", generator=g).bfloat16()
+    dy = torch.randn(n, 112, 112, 64, device="cuda", generator=g).bfloat16()
+    base = torch.randn(64, 4, 4, 16, device="cuda", generator=g)
+    ref = torch.nn.grad.conv2d_weight(xs.float().permute(0, 3, 1, 2), (64, 16, 4, 4),
+                                      dy.float().permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    if acc:
+        ref = ref + base
+    outs = []
+    try:
+        for stem in (1, 0):
+            native._K.wgrad_set_stem(stem)
+            out = base.clone().contiguous() if acc else None
+            outs.append(native.conv2d_wgrad(xs, dy, (64, 4, 4, 16), 1, 0, out=out))
+    finally:
+        native._K.wgrad_set_stem(1)
+    for o in outs:
+        assert float((o - ref).norm() / ref.norm()) < 1e-5, float((o - ref).norm() / ref.norm())
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-3)
+
+
 def test_lazy_x3_never_stores_stage0_c3_output_bit_identical():
     """the stage-0 identity blocks' c3 output (x3, [M, 256]) is never written --
     the c3 GEMM runs NOST (statistics only), the residual BN's apply recomputes x3 in a stream
