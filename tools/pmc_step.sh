@@ -2,7 +2,8 @@
 # PMC counters of every kernel of a short bench.py run (default: the ResNet-50 b1984 step), two
 # passes in their own runs (rocprofv3 --pmc only, no traces): SQ issue/wait breakdown + MFMA busy,
 # then L2 traffic (FETCH_SIZE, WRITE_SIZE) + GRBM_GUI_ACTIVE (clock).  Summaries:
-# gpurun_out/pmc_step/{sq,tcc}/summary.txt.
+# gpurun_out/pmc_step/{sq,tcc}/summary.txt.  PMC_MEM_ONLY=1: one memory-pipe pass instead
+# (gpurun_out/pmc_step/mem/summary.txt).
 #   gpurun -- bash tools/pmc_step.sh [bench.py args]
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -21,6 +22,13 @@ run_pass() {
   rm -rf "/tmp/pmc_$name"
   return $rc
 }
+if [ -n "$PMC_MEM_ONLY" ]; then
+  # memory-pipe pass only: address-unit busy / stalls behind the L2, vector L1 stall and request
+  # latency (TA 2, TCP 4, GRBM 1 counters: one pass)
+  run_pass mem TA_TA_BUSY TA_DATA_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES \
+    TCP_TCR_TCP_STALL_CYCLES TCP_TCC_READ_REQ_LATENCY TCP_TCC_WRITE_REQ_LATENCY GRBM_GUI_ACTIVE
+  exit $?
+fi
 run_pass sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
   SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_BUSY_CYCLES &&
 run_pass tcc FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT
