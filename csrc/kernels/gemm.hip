@@ -1113,7 +1113,9 @@ gemm_pp_kernel(const GemmArgs g) {
 // The epilogue (bias / ReLU / BN statistics / Cin / masked acc, strided dgrad phases) and the
 // counted waits around the stores are gemm_pp's.
 // EPI bits (each instantiation carries only the epilogue operands it uses -- SGPR pressure):
-// 1 BN statistics, 2 accumulate (Cin / masked acc), 4 strided (dgrad phase) output rows
+// 1 BN statistics, 2 accumulate (Cin / masked acc), 4 strided (dgrad phase) output rows,
+// 8 / 16 GELU forward / backward (below), 32 ReLU (a compile-time bit: as the runtime flag it
+// cost a v_max + v_cndmask per output element in every epilogue, ReLU or not)
 template <int CONV, int EPI>
 __global__ void __launch_bounds__(512, 1)
 gemm_pp2_kernel(const GemmArgs g) {
@@ -1309,6 +1311,8 @@ gemm_pp2_kernel(const GemmArgs g) {
   // operands and their SGPRs are compiled out
   constexpr bool do_stats = (EPI & 1) != 0;
   constexpr bool has_acc = (EPI & 2) != 0;
+  constexpr bool relu = (EPI & 32) != 0;
+  static_assert(!relu || !(EPI & (1 | 4 | 8 | 16)), "ReLU: the plain / accumulate dense epilogues");
 
   issue_piece(0, 0); issue_piece(0, 1); issue_piece(0, 2); issue_piece(0, 3);
   issue_piece(1, 0); issue_piece(1, 1);
@@ -1448,7 +1452,7 @@ gemm_pp2_kernel(const GemmArgs g) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
             float v = acc[i][jj][r] + b4[jj];
-            if (!do_stats && g.relu) v = fmaxf(v, 0.f);
+            if (relu) v = fmaxf(v, 0.f);
             h[jj] = f2bf(v);
             // rows past M / columns past N hold exact zeros (zero-filled operands, no bias with
             // statistics: host), so they add nothing -- no per-row test (its 32 compare masks
@@ -1585,7 +1589,7 @@ gemm_pp2_kernel(const GemmArgs g) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           v[r] = acc[i][j][r] + b4[r];
-          if (g.relu) v[r] = fmaxf(v[r], 0.f);
+          if (relu) v[r] = fmaxf(v[r], 0.f);
           h[r] = f2bf(v[r]);
           if (do_stats && ok) {
             const float qv = bf2f(h[r]);
@@ -1708,9 +1712,16 @@ template <int CONV>
 void launch_gemm_pp2(const GemmArgs& g, long a_bytes, long b_bytes, hipStream_t st) {
   const bool stats = g.stats != nullptr, acc = g.Cin || g.acc_mask;
   const bool strided = CONV && (g.osh != 1 || g.osw != 1);
+  if (g.relu && (CONV || stats || strided || g.gelu_out || g.gelu_a))
+    throw std::runtime_error("gemm_pp2: ReLU only on the plain / accumulate dense epilogues");
   if constexpr (!CONV) {
     if (g.gelu_out) { launch_gemm_pp2_t<0, 8>(g, a_bytes, b_bytes, st); return; }
     if (g.gelu_a) { launch_gemm_pp2_t<0, 16>(g, a_bytes, b_bytes, st); return; }
+    if (g.relu) {
+      if (acc) launch_gemm_pp2_t<0, 34>(g, a_bytes, b_bytes, st);
+      else launch_gemm_pp2_t<0, 32>(g, a_bytes, b_bytes, st);
+      return;
+    }
   }
   if (strided) {
     if (acc) launch_gemm_pp2_t<CONV, 6>(g, a_bytes, b_bytes, st);

@@ -67,6 +67,10 @@ def test_pp_matches_pingpong_bitwise(M, N, K, variant):
     c8 = _run(8, lambda: n.gemm_nt(a, b, cin=cin.clone()))
     c11 = _run(variant, lambda: n.gemm_nt(a, b, cin=cin.clone()))
     assert torch.equal(c11, c8)
+    # bias + ReLU + accumulate (the persistent kernel's compile-time ReLU on the accumulate form)
+    cr8 = _run(8, lambda: n.gemm_nt(a, b, bias=bias, relu=True, cin=cin.clone()))
+    cr = _run(variant, lambda: n.gemm_nt(a, b, bias=bias, relu=True, cin=cin.clone()))
+    assert torch.equal(cr, cr8)
 
 
 @pytest.mark.parametrize("variant", [11, 12])
