@@ -3,7 +3,9 @@
 # passes in their own runs (rocprofv3 --pmc only, no traces): SQ issue/wait breakdown + MFMA busy,
 # then L2 traffic (FETCH_SIZE, WRITE_SIZE) + GRBM_GUI_ACTIVE (clock).  Summaries:
 # gpurun_out/pmc_step/{sq,tcc}/summary.txt.  PMC_MEM_ONLY=1: one memory-pipe pass instead
-# (gpurun_out/pmc_step/mem/summary.txt).
+# (gpurun_out/pmc_step/mem/summary.txt).  PMC_INST=1: one instruction-mix pass (VALU / LDS / MFMA
+# instructions and active cycles per wave: which kernels are VALU-issue bound)
+# (gpurun_out/pmc_step/inst/summary.txt).
 #   gpurun -- bash tools/pmc_step.sh [bench.py args]
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -27,6 +29,11 @@ if [ -n "$PMC_MEM_ONLY" ]; then
   # latency (TA 2, TCP 4, GRBM 1 counters: one pass)
   run_pass mem TA_TA_BUSY TA_DATA_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES \
     TCP_TCR_TCP_STALL_CYCLES TCP_TCC_READ_REQ_LATENCY TCP_TCC_WRITE_REQ_LATENCY GRBM_GUI_ACTIVE
+  exit $?
+fi
+if [ -n "$PMC_INST" ]; then
+  run_pass inst SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
+    SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS
   exit $?
 fi
 run_pass sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \

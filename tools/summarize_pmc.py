@@ -30,6 +30,10 @@ def main(d):
             line.append(f"  wait_any/wave={vals['SQ_WAIT_ANY'] / wc:.2f} "
                         f"wait_inst/wave={vals.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} "
                         f"active/wave={vals.get('SQ_ACTIVE_INST_ANY', 0) / wc:.2f}")
+        if "SQ_ACTIVE_INST_VALU" in vals:
+            line.append(f"  valu_active/wave={vals['SQ_ACTIVE_INST_VALU'] / wc:.3f} "
+                        f"lds_active/wave={vals.get('SQ_ACTIVE_INST_LDS', 0) / wc:.3f} "
+                        f"valu_insts/mfma={vals.get('SQ_INSTS_VALU', 0) / max(vals.get('SQ_INSTS_MFMA', 0), 1):.1f}")
         if "SQ_VALU_MFMA_BUSY_CYCLES" in vals and "SQ_BUSY_CYCLES" in vals:
             line.append(f"  mfma_busy/busy={vals['SQ_VALU_MFMA_BUSY_CYCLES'] / max(vals['SQ_BUSY_CYCLES'], 1):.3f}")
         print("\n".join(line))
