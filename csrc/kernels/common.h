@@ -128,7 +128,9 @@ constexpr float kGeluK1 = 0.044715f;
 // -- 5 (forward) / 9 (derivative) plain VALU ops besides v_exp_f32 + v_rcp_f32, against 10 / 16
 // for the tanh form: these run in the GEMM epilogues of BERT's FFN (gemm.hip EPI 8 / 16), where
 // the GELU arithmetic measured ~50 us of a ~360 us call.  e^{2u} = inf -> r = 0 (gelu = x,
-// gelu' = 1); e^{2u} = 0 -> r = 1 (gelu = 0, gelu' = 0), as the tanh form gives.
+// gelu' = 1); e^{2u} = 0 -> r = 1 (gelu = 0, gelu' = 0), as the tanh form gives, for every
+// finite x.  Non-finite x: gelu(+inf) is NaN here (the tanh form gave +inf; -inf is NaN in
+// both) -- a non-finite pre-activation has already poisoned the step either way.
 constexpr float kGeluE0 = 2.f * kGeluK0 * 1.4426950408889634f;   // 2u log2(e) = x (E0 + E1 x^2)
 constexpr float kGeluE1 = kGeluE0 * kGeluK1;
 DTF_DEV float gelu_r(float x, float x2) {
