@@ -259,6 +259,26 @@ def test_bias_gelu_gpu(M, N):
 
 
 @pytest.mark.gpu
+def test_bias_gelu_gpu_large_magnitudes():
+    """The r = 1 / (1 + e^{2u}) GELU form (csrc/kernels/common.h) at pre-activations where
+    e^{2u} overflows to inf or underflows to 0: gelu -> x / 0 and gelu' -> 1 / 0 exactly as the
+    fp32 tanh form, no NaN."""
+    torch.manual_seed(0)
+    vals = torch.tensor([-3e4, -200.0, -40.0, -9.5, -4.0, -1e-3, 0.0, 1e-3, 4.0, 9.5, 40.0, 200.0,
+                         3e4])
+    a32 = vals.repeat(64, 8)[:, :96].contiguous()           # [64, 96]
+    bias = torch.zeros(96)
+    dy = torch.randn(64, 96)
+    a, b = _leaf(a32), _leaf(bias, torch.float32)
+    y, (da, db) = _grads_of(lambda: ops.bias_gelu(a, b), [a, b], dy.cuda().bfloat16())
+    a_, b_ = a32.bfloat16().float().requires_grad_(True), bias.clone().requires_grad_(True)
+    y_, (da_, db_) = _grads_of(lambda: R.bias_gelu(a_, b_), [a_, b_], dy.bfloat16().float())
+    assert torch.isfinite(y.float()).all() and torch.isfinite(da.float()).all()
+    torch.testing.assert_close(y.cpu(), y_, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(da.cpu(), da_, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("B,S,H,p,masked", [(2, 128, 2, 0.0, True), (2, 128, 3, 0.1, True),
                                             (1, 512, 2, 0.0, False), (1, 64, 1, 0.1, False),
                                             (2, 192, 2, 0.1, True)])
