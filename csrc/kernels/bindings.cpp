@@ -138,6 +138,10 @@ int dtf_conv_wgrad_splits(long, int, int, long, int);
 int dtf_conv_wgrad_halo_splits(int, int, int, int, int, int, int, int, int, const TapTableW&);
 void dtf_wgrad_set_halo(int);
 void dtf_wgrad_set_stem(int);
+int dtf_wgrad_stem_dz_splits(int);
+void dtf_conv_wgrad_stem_dz(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*,
+                            const float*, const float*, const float*, const float*, const float*,
+                            float*, float*, int, int, hipStream_t);
 void dtf_conv_set_halo_stages(int);
 void dtf_wgrad_set_dma_mode(int);
 void dtf_wgrad_set_pipe(int);
@@ -800,6 +804,17 @@ PYBIND11_MODULE(_dtf_hip, m) {
   });
   m.def("wgrad_set_halo", &dtf_wgrad_set_halo);
   m.def("wgrad_set_stem", &dtf_wgrad_set_stem);
+  m.def("wgrad_stem_dz_splits", &dtf_wgrad_stem_dz_splits);
+  m.def("conv_wgrad_stem_dz", [](uintptr_t x, uintptr_t dp, uintptr_t arg, uintptr_t xbn,
+                                 uintptr_t ca, uintptr_t cb, uintptr_t cc, uintptr_t fsc,
+                                 uintptr_t fsh, uintptr_t dw, uintptr_t ws, int N, int acc,
+                                 uintptr_t st) {
+    dtf_conv_wgrad_stem_dz(P<const bf16_t>(x), P<const bf16_t>(dp), P<const uint8_t>(arg),
+                           P<const bf16_t>(xbn), P<const float>(ca), P<const float>(cb),
+                           P<const float>(cc), P<const float>(fsc), P<const float>(fsh),
+                           P<float>(dw), P<float>(ws), N, acc, S(st));
+    check_launch("conv_wgrad_stem_dz");
+  });
   m.def("wgrad_set_dma_mode", &dtf_wgrad_set_dma_mode);
   m.def("wgrad_set_pipe", &dtf_wgrad_set_pipe);
   m.def("wgrad_set_pp", &dtf_wgrad_set_pp);

@@ -116,6 +116,46 @@ DTF_DEV float bn_bwd_dx(float a, float dz, float b, float x, float c) {
   return __builtin_fmaf(a, dz, b * x) + c;
 }
 
+// 3x3 / 2 max-pool backward (pad 1) for the 2 x 2 block of input pixels (2a + ii, 2b + jj): the
+// gradients of the <= 4 pooled outputs (a .. a + 1, b .. b + 1) whose argmax byte (window
+// position r * 3 + s) names the pixel, rounded to bf16 as a stored d(pool input) would be.
+// Shared by pool.hip (pool3s2_bn_bwd_kernel) and conv_wgrad.hip (the stem wgrad that forms its
+// dY on load): both must produce the identical bits.
+DTF_DEV void pool3s2_gather(const uint4 (&dyr)[4], const uint2 (&amr)[4], int a, int b, int P,
+                            int Q, float (&g)[4][8]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[k][e] = 0.f;
+#pragma unroll
+  for (int da = 0; da < 2; ++da) {
+    if (a + da >= P) continue;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      if (b + db >= Q) continue;
+      float gv[8];
+      unpack8(dyr[da * 2 + db], gv);
+      const uint32_t aw[2] = {amr[da * 2 + db].x, amr[da * 2 + db].y};
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int r = ii - 2 * da + 1, s = jj - 2 * db + 1;
+          if (r < 0 || r > 2 || s < 0 || s > 2) continue;
+          const uint32_t me = (uint32_t)(r * 3 + s);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (((aw[e >> 2] >> ((e & 3) * 8)) & 0xffu) == me) g[ii * 2 + jj][e] += gv[e];
+        }
+    }
+  }
+  // the unfused path stores d(BN output) as bf16: round exactly like it
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[k][e] = bf2f(f2bf(g[k][e]));
+}
+
 // ---- GELU (tanh approximation, BERT's "gelu") shared by the NLP kernels and the GEMM epilogue
 constexpr float kGeluK0 = 0.7978845608028654f;   // sqrt(2/pi)
 constexpr float kGeluK1 = 0.044715f;

@@ -1047,9 +1047,30 @@ static_assert(kStQ % 4 == 0 && (kStTH * kStQ) % 32 == 0, "4-pixel groups inside 
 DTF_DEV int st_swz(int r) { return ((r >> 1) & 3) << 1; }
 DTF_DEV int st_el(int r, int c) { return r * 64 + (((c >> 3) ^ st_swz(r)) << 3) + (c & 7); }
 
+// FZ: dY is not a tensor but formed on load -- the stem's BN + ReLU + 3x3/2 max-pool backward
+// (pool3s2_bn_bwd_kernel<true>'s arithmetic, bit for bit: pool3s2_gather, the ReLU mask from
+// fmaf(x, fsc, fsh), bn_bwd_dx, bf16 rounding) from the pooled gradient, its argmax bytes and the
+// BN input x, so that pass never writes d(conv output) (3.2 GB at b1984) nor does this kernel
+// read it back.  The strip's x rows are LDS-DMA'd into its dY image (the DMA the unfused kernel
+// spends on dY); thread t < 448 owns the 2 x 2 pixel block (column t / 8, 8-channel group t % 8)
+// of the strip's block row, whose pooled gradients / argmax bytes for strip s + G it loads into
+// registers under strip s's MFMAs, and turns x into dY in place at the top of the strip.
+struct StemDz {
+  const bf16_t* dp;           // d(pool output) [N][56][56][64]
+  const uint8_t* arg;         // its argmax bytes (window position) [N][56][56][64]
+  const bf16_t* x;            // the BN input (the stem conv output) [N][112][112][64]
+  const float* ca;            // BN backward coefficients: dx = ca dz + cb x + cc
+  const float* cb;
+  const float* cc;
+  const float* fsc;           // forward BN scale / shift (the ReLU mask)
+  const float* fsh;
+};
+constexpr int kStPq = kStQ / 2;                                  // pooled rows / columns (56)
+
+template <bool FZ>
 __global__ void __launch_bounds__(kStT, 1)
 conv_wgrad_stem_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
-                       float* __restrict__ ws, int N) {
+                       float* __restrict__ ws, int N, const StemDz z) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1067,12 +1088,15 @@ conv_wgrad_stem_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ 
   auto issue = [&](int strip, int stage) {
     const bool live = strip < nstrip;
     const int sn = live ? strip / tiles_h : 0, p0 = live ? (strip % tiles_h) * kStTH : 0;
-    const i32x4_t ry = rsrc_quad(dY + sn * yimg + (long)p0 * kStQ * kStK, live ? kStDyB : 0);
+    const i32x4_t ry = rsrc_quad((FZ ? z.x : dY) + sn * yimg + (long)p0 * kStQ * kStK,
+                                 live ? kStDyB : 0);
     const i32x4_t rx = rsrc_quad(X + sn * ximg + (long)p0 * kStXW * kStC, live ? kStXB : 0);
     const uint32_t base = lds0 + (uint32_t)(stage * kStStage);
     const int rloc = lane >> 3, slot = lane & 7;
     for (int q = wave; q < kStDyB / 1024 + kStXI; q += 8) {
       if (q < kStDyB / 1024) {
+        // FZ: the BN input x rows (the same [N][112][112][64] layout) land where dY would; the
+        // formation pass turns them into dY in place
         const int r = q * 8 + rloc;
         const int chunk = slot ^ st_swz(r);
         dma16(ry, base + (uint32_t)(q * 1024), (uint32_t)((r * kStK + chunk * 8) * 2));
@@ -1091,11 +1115,66 @@ conv_wgrad_stem_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ 
   const int gq = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
 
+  // FZ operands of this thread's pixel block (registers: loaded one strip ahead)
+  const int zb = tid >> 3, zcg = tid & 7;
+  const bool zon = FZ && tid < kStPq * 8;
+  float za[8], zbb[8], zc[8], zsc[8], zsh[8];
+  uint4 zdy[4];
+  uint2 zam[4];
+  if constexpr (FZ) {
+    auto ld8 = [&](const float* p, float* v) {
+      const float4 lo = reinterpret_cast<const float4*>(p + zcg * 8)[0];
+      const float4 hi = reinterpret_cast<const float4*>(p + zcg * 8)[1];
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z;
+      v[7] = hi.w;
+    };
+    ld8(z.ca, za); ld8(z.cb, zbb); ld8(z.cc, zc); ld8(z.fsc, zsc); ld8(z.fsh, zsh);
+  }
+  auto zload = [&](int strip) {
+    if (!zon || strip >= nstrip) return;
+    const uint32_t n = (uint32_t)(strip / tiles_h), a = (uint32_t)(strip % tiles_h);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      // pool3s2_bn_bwd_kernel's clamped addresses (P = Q = 56, H = W = 112)
+      const uint32_t p = min(a + (k >> 1), (uint32_t)kStPq - 1);
+      const uint32_t q = min((uint32_t)zb + (k & 1), (uint32_t)kStPq - 1);
+      const uint32_t o = ((n * kStPq + p) * kStPq + q) * 8 + zcg;
+      zdy[k] = reinterpret_cast<const uint4*>(z.dp)[o];
+      zam[k] = reinterpret_cast<const uint2*>(z.arg)[o];
+    }
+  };
+  auto zform = [&](int strip, bf16_t* sy) {
+    if (!zon || strip >= nstrip) return;
+    float g[4][8];
+    pool3s2_gather(zdy, zam, strip % tiles_h, zb, kStPq, kStPq, g);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int r = ii * kStQ + 2 * zb + jj;                   // pixel of the 2-row strip
+        uint4* slot = reinterpret_cast<uint4*>(sy + st_el(r, zcg * 8));
+        float xv[8], o[8];
+        unpack8(*slot, xv);                                      // x, DMA'd into the dY image
+        const float* gk = g[ii * 2 + jj];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = __builtin_fmaf(xv[e], zsc[e], zsh[e]) > 0.f ? gk[e] : 0.f;
+          o[e] = bn_bwd_dx(za[e], d, zbb[e], xv[e], zc[e]);
+        }
+        *slot = pack8(o);                                        // ... replaced by its dY
+      }
+  };
+
   int s = blockIdx.x, it = 0;
+  if constexpr (FZ) zload(s);
   issue(s, 0);
   for (; s < nstrip; s += G, ++it) {
     DTF_WAIT_VM(0);            // this strip's DMAs (own) landed ...
+    // FZ: form this strip's dY in its stage (last read two trips ago, before the previous
+    // trip's barrier)
+    if constexpr (FZ) zform(s, lds + (it & 1) * (kStStage / 2));
     __syncthreads();           // ... everyone's; everyone finished reading the other stage
+    if constexpr (FZ) zload(s + G);
     issue(s + G, (it + 1) & 1);
     const bf16_t* sy = lds + (it & 1) * (kStStage / 2);
     const bf16_t* sx = sy + kStDyB / 2;
@@ -1293,12 +1372,12 @@ void dtf_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* dW, float* ws, Wgr
     if (!ws) throw std::runtime_error("wgrad stem: needs the slab workspace");
     static bool attr = false;
     if (!attr) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_stem_kernel,
+      HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_stem_kernel<false>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStLDS));
       attr = true;
     }
-    hipLaunchKernelGGL(conv_wgrad_stem_kernel, dim3((unsigned)splits), dim3(kStT), kStLDS, st, X,
-                       dY, ws, g.N);
+    hipLaunchKernelGGL(conv_wgrad_stem_kernel<false>, dim3((unsigned)splits), dim3(kStT), kStLDS,
+                       st, X, dY, ws, g.N, StemDz{});
     launch_slab_reduce(ws, dW, (long)kStK * 256, (long)kStK * 256, splits, accumulate, st);
     return;
   }
@@ -1416,3 +1495,32 @@ void dtf_slab_reduce(const float* ws, float* out, long n, int nsplit, int accumu
   launch_slab_reduce(ws, out, n, n, nsplit, accumulate, st);
 }
 
+
+// The stem weight gradient with its dY formed on load from the BN + ReLU + max-pool backward's
+// operands (conv_wgrad_stem_kernel<true>): X the space-to-depth image [N][115][115][16], dp / arg
+// the pooled gradient and argmax bytes [N][56][56][64], xbn the BN input [N][112][112][64],
+// (ca, cb, cc) the BN backward coefficients, (fsc, fsh) the forward scale / shift.  dW [64][256]
+// fp32 (+= with accumulate), via the [wgrad_stem_blocks(N)][64][256] slab workspace ws.
+int dtf_wgrad_stem_dz_splits(int N) { return g_wgrad_stem && N > 0 ? wgrad_stem_blocks(N) : 0; }
+void dtf_conv_wgrad_stem_dz(const bf16_t* X, const bf16_t* dp, const uint8_t* arg,
+                            const bf16_t* xbn, const float* ca, const float* cb, const float* cc,
+                            const float* fsc, const float* fsh, float* dW, float* ws, int N,
+                            int accumulate, hipStream_t st) {
+  if (N <= 0 || !ws || (long)N * kStQ * kStQ * (kStK / 8) >= 2147483647L)
+    throw std::runtime_error("wgrad stem dz: bad batch / workspace");
+  const int splits = wgrad_stem_blocks(N);
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_stem_kernel<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStLDS));
+    hipFuncAttributes fa{};
+    HIP_CHECK(hipFuncGetAttributes(&fa, (const void*)conv_wgrad_stem_kernel<true>));
+    if (fa.localSizeBytes > 0)
+      throw std::runtime_error("conv_wgrad_stem_kernel<true> was compiled with register spills");
+    attr = true;
+  }
+  const StemDz z{dp, arg, xbn, ca, cb, cc, fsc, fsh};
+  hipLaunchKernelGGL(conv_wgrad_stem_kernel<true>, dim3((unsigned)splits), dim3(kStT), kStLDS, st,
+                     X, nullptr, ws, N, z);
+  launch_slab_reduce(ws, dW, (long)kStK * 256, (long)kStK * 256, splits, accumulate, st);
+}

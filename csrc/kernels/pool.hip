@@ -319,40 +319,7 @@ maxpool3s2_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__
 // g[ii * 2 + jj] = the pooled gradient of input pixel (2a + ii, 2b + jj): the sum over the up to
 // four output windows (a + da, b + db) whose argmax byte names that pixel.  dyr / amr hold the
 // windows' (clamped, preloaded) gradients and argmax words; windows past P / Q are skipped.
-DTF_DEV void pool3s2_gather(const uint4 (&dyr)[4], const uint2 (&amr)[4], int a, int b, int P,
-                            int Q, float (&g)[4][8]) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[k][e] = 0.f;
-#pragma unroll
-  for (int da = 0; da < 2; ++da) {
-    if (a + da >= P) continue;
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      if (b + db >= Q) continue;
-      float gv[8];
-      unpack8(dyr[da * 2 + db], gv);
-      const uint32_t aw[2] = {amr[da * 2 + db].x, amr[da * 2 + db].y};
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const int r = ii - 2 * da + 1, s = jj - 2 * db + 1;
-          if (r < 0 || r > 2 || s < 0 || s > 2) continue;
-          const uint32_t me = (uint32_t)(r * 3 + s);
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (((aw[e >> 2] >> ((e & 3) * 8)) & 0xffu) == me) g[ii * 2 + jj][e] += gv[e];
-        }
-    }
-  }
-  // the unfused path stores d(BN output) as bf16: round exactly like it
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[k][e] = bf2f(f2bf(g[k][e]));
-}
+// pool3s2_gather (common.h): the 2 x 2 conv pixels' gradient gathered from the 4 pooled outputs
 
 DTF_DEV void load8(const float* __restrict__ p, int cg, float* v) {
   const float4 a = reinterpret_cast<const float4*>(p + cg * 8)[0];

@@ -19,6 +19,7 @@ import torch
 from .records import BnDeferred as _BnDeferred  # noqa: F401  (deferred-work records)
 from .records import GradSlot as _GradSlot
 from .records import LazyBnDx as _LazyBnDx
+from .records import LazyStemDz as _LazyStemDz
 from .records import MaskedGrad as _MaskedGrad
 from .records import Recompute as _Recompute
 from .records import end_step as end_step  # noqa: F401
@@ -556,7 +557,16 @@ class _Conv2d(torch.autograd.Function):
             ctx.bnb = _DualBnb(*dual)
         if x.requires_grad and xb is x and wb.is_contiguous():
             _register_dgrad_filter(wb)
-        return conv2d_forward(xb, wb, stride, padding, stats)
+        out = conv2d_forward(xb, wb, stride, padding, stats)
+        ctx.stem_slot = None
+        if (_FUSE_STEM_WGRAD and not x.requires_grad and _stem_wgrad_shape(xb, wb, stride, padding)
+                and _K.wgrad_stem_dz_splits(xb.shape[0]) > 0):
+            # the fused BN + ReLU + max-pool consuming `out` may hand d(out) over unformed
+            # (_LazyStemDz): the weight gradient then forms it on load and it is never stored
+            ctx.stem_slot = _GradSlot()
+            out._dtf_stem_slot = ctx.stem_slot
+            ctx.set_materialize_grads(False)
+        return out
 
     @staticmethod
     def backward(ctx, dy):
@@ -564,6 +574,37 @@ class _Conv2d(torch.autograd.Function):
         dx = dw = None
         C = ctx.c_orig
         padded = xb.shape[-1] != C
+        slot, ctx.stem_slot = ctx.stem_slot, None
+        rec = None
+        if slot is not None:
+            rec, slot.grad = slot.grad, None
+        if dy is None and rec is None:
+            ctx.x_ref = ctx.bnb = ctx.share = None
+            return None, None, None, None, None, None
+        if rec is not None and (dy is not None or not ctx.needs_input_grad[1]):
+            m = rec.materialize()                # another consumer of the conv output
+            dy = m if dy is None else dy + m
+            rec = None
+        if rec is not None:
+            # the stem: dW with d(out) formed on load from the BN + ReLU + pool backward's operands
+            target = _direct_grad(ctx.w_param)
+            K, R, S, _ = wb.shape
+            n = xb.shape[0]
+            splits = _K.wgrad_stem_dz_splits(n)
+            dW = target if target is not None else torch.empty(K, R * S * C, device=xb.device,
+                                                                dtype=torch.float32)
+            ws = torch.empty(splits * K * R * S * C, device=xb.device, dtype=torch.float32)
+            _K.conv_wgrad_stem_dz(xb.data_ptr(), rec.dp.data_ptr(), rec.arg.data_ptr(),
+                                  rec.x.data_ptr(), rec.gb[2].data_ptr(), rec.gb[3].data_ptr(),
+                                  rec.gb[4].data_ptr(), rec.fsc.data_ptr(), rec.fsh.data_ptr(),
+                                  dW.data_ptr(), ws.data_ptr(), n, int(target is not None), _st())
+            rec.release()
+            if target is not None:
+                _grad_ready(ctx.w_param)
+            else:
+                dw = dW.reshape(K, R, S, C).to(ctx.w_dtype)
+            ctx.x_ref = ctx.bnb = ctx.share = None
+            return None, dw, None, None, None, None
         if ctx.needs_input_grad[1]:
             # weight gradient first: it only depends on dy, so the bucketed all-reduce of this
             # layer can start while dgrad still runs
@@ -760,6 +801,17 @@ _BN_ON_LOAD = os.environ.get("DTF_BN_ON_LOAD", "1") == "1"
 _LAZY_RESIDUAL_GRAD = os.environ.get("DTF_LAZY_RESIDUAL_GRAD", "1") == "1"
 # stem backward: pool gather fused into both BatchNorm backward passes (_BatchNormReluMaxPool)
 _FUSE_STEM_POOL_BWD = os.environ.get("DTF_FUSE_STEM_POOL_BWD", "1") == "1"
+# ... and its apply pass folded into the stem weight gradient (d(stem conv output) never stored:
+# conv_wgrad_stem_dz); a module switch for the A/B tests, no environment knob
+_FUSE_STEM_WGRAD = True
+
+
+def _stem_wgrad_shape(xb, wb, stride, padding):
+    """The ResNet stem on its space-to-depth image: a 4 x 4 stride-1 VALID conv, 115 x 115 x 16
+    -> 112 x 112 x 64 (the conv_wgrad_stem_kernel geometry)."""
+    return (tuple(xb.shape[1:]) == (115, 115, 16) and tuple(wb.shape) == (64, 4, 4, 16)
+            and tuple(_pair(stride)) == (1, 1) and padding in (0, "VALID", "valid", (0, 0))
+            and xb.is_contiguous())
 
 
 class _BatchNorm(torch.autograd.Function):
@@ -1277,6 +1329,7 @@ class _BatchNormReluMaxPool(torch.autograd.Function):
                                pt, pl, _st())
         ctx.save_for_backward(x, g32, stats, arg)
         ctx.geom = (n, h, w, c, P, Q, kh, kw, sh, sw, pt, pl)
+        ctx.stem_slot = getattr(x, "_dtf_stem_slot", None) if training else None
         ctx.relu, ctx.has_res, ctx.res_ref = True, False, None
         ctx.gdt, ctx.bdt = gamma.dtype, beta.dtype
         ctx.params = (gamma, beta)
@@ -1298,10 +1351,17 @@ class _BatchNormReluMaxPool(torch.autograd.Function):
                                   stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(),
                                   stats[3].data_ptr(), part.data_ptr(), n, h, w, c, P, Q, st)
             gb, direct = _bn_bwd_finalize(ctx, part, G, M, c, g32, stats)
-            dx = torch.empty_like(x)
-            _K.pool_bn_bwd_apply(dp.data_ptr(), arg.data_ptr(), x.data_ptr(), gb[2].data_ptr(),
-                                 gb[3].data_ptr(), gb[4].data_ptr(), stats[2].data_ptr(),
-                                 stats[3].data_ptr(), dx.data_ptr(), n, h, w, c, P, Q, st)
+            slot, ctx.stem_slot = ctx.stem_slot, None
+            if slot is not None and (h, w, c, P, Q) == (112, 112, 64, 56, 56):
+                # the stem conv's weight gradient forms d(x) on load; it is never stored
+                slot.grad = _LazyStemDz(dp, arg, x, gb, stats[2], stats[3], (n, h, w, c, P, Q))
+                dx = None
+            else:
+                dx = torch.empty_like(x)
+                _K.pool_bn_bwd_apply(dp.data_ptr(), arg.data_ptr(), x.data_ptr(),
+                                     gb[2].data_ptr(), gb[3].data_ptr(), gb[4].data_ptr(),
+                                     stats[2].data_ptr(), stats[3].data_ptr(), dx.data_ptr(), n,
+                                     h, w, c, P, Q, st)
             dg, db = (None, None) if direct else (gb[0].to(ctx.gdt), gb[1].to(ctx.bdt))
             return dx, dg, db, None, None, None, None, None, None, None, None
         dy = torch.empty(n, h, w, c, device=dp.device, dtype=dp.dtype)

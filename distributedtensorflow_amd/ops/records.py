@@ -10,7 +10,9 @@ Several fused paths leave work for a LATER op instead of running a pass of their
 * :class:`LazyBnDx` -- the d(x) of a residual BatchNorm not yet formed: the fused c3 backward
   forms it per tile (handed over through a :class:`GradSlot`, ``out._dtf_lazy_slot``);
 * :class:`MaskedGrad` -- a residual gradient kept as (dy, ReLU bit mask): the dgrad epilogue of
-  the conv that also reads the residual adds it (``x._dtf_pending_grad`` / a grad slot).
+  the conv that also reads the residual adds it (``x._dtf_pending_grad`` / a grad slot);
+* :class:`LazyStemDz` -- the ResNet stem conv's output gradient (BN + ReLU + max-pool backward)
+  not yet formed: the stem weight gradient forms it on load (``out._dtf_stem_slot``).
 
 These records ride on activation tensors, so their lifetime is the activations'.  Round 5 found
 what that costs when it goes wrong: a y <-> record reference cycle left every step's c1 outputs
@@ -166,6 +168,30 @@ class LazyBnDx(_Record):
         return dx
 
 
+class LazyStemDz(_Record):
+    """d(stem conv output) of the fused BN + ReLU + 3x3/2 max-pool (the pool's gather, the ReLU
+    mask recomputed from x, dx = A dz + B x + C), not yet formed: the stem weight gradient forms
+    it per strip on load (conv_wgrad_stem_dz, bit-identical to the apply pass) so it is never
+    stored; anything else materialises it with that pass."""
+    __slots__ = ("dp", "arg", "x", "gb", "fsc", "fsh", "geom")
+
+    def __init__(self, dp, arg, x, gb, fsc, fsh, geom):
+        super().__init__()
+        self.dp, self.arg, self.x, self.gb = dp, arg, x, gb
+        self.fsc, self.fsh, self.geom = fsc, fsh, geom
+
+    def materialize(self):
+        self._check()
+        n = _native()
+        N, H, W, C, P, Q = self.geom
+        dx = self.x.new_empty(self.x.shape)
+        n._K.pool_bn_bwd_apply(self.dp.data_ptr(), self.arg.data_ptr(), self.x.data_ptr(),
+                               self.gb[2].data_ptr(), self.gb[3].data_ptr(),
+                               self.gb[4].data_ptr(), self.fsc.data_ptr(), self.fsh.data_ptr(),
+                               dx.data_ptr(), N, H, W, C, P, Q, n._st())
+        return dx
+
+
 class GradSlot(_Record):
     """A mailbox between two ops' backward passes: the producer's backward leaves a gradient
     record in ``grad``, the consumer's backward takes it."""
@@ -197,5 +223,5 @@ def end_step():
     return len(recs)
 
 
-__all__ = ["BnDeferred", "Recompute", "MaskedGrad", "LazyBnDx", "GradSlot",
+__all__ = ["BnDeferred", "Recompute", "MaskedGrad", "LazyBnDx", "LazyStemDz", "GradSlot",
            "ReleasedRecordError", "live_count", "end_step"]

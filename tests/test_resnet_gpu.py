@@ -771,6 +771,50 @@ def test_wgrad_stem_kernel_vs_fp32(n, acc):
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("n", [2, 5])
+def test_stem_wgrad_forms_pool_bn_backward_on_load_bit_identical(n):
+    """The stem's BN + ReLU + max-pool backward apply folded into the stem weight gradient
+    (conv_wgrad_stem_kernel<true>: d(stem conv output) formed per strip from the pooled gradient,
+    argmax bytes and BN input, never stored) against the apply pass + the strip wgrad kernel:
+    the conv weight gradient and BN gamma / beta gradients bit for bit; n = 5 leaves the last
+    blocks' second strip past the batch.  The lazy record must be consumed (the apply pass not
+    run) on the fused arm."""
+    torch.manual_seed(0)
+    m = resnet50().cuda()
+    x = torch.randn(n, 224, 224, 3, device="cuda").bfloat16()
+    dy = torch.randn(n, 56, 56, 64, device="cuda").bfloat16()
+    calls = {"apply": 0, "dz": 0}
+    o_apply, o_dz = native._K.pool_bn_bwd_apply, native._K.conv_wgrad_stem_dz
+
+    def c_apply(*a):
+        calls["apply"] += 1
+        return o_apply(*a)
+
+    def c_dz(*a):
+        calls["dz"] += 1
+        return o_dz(*a)
+
+    grads = []
+    try:
+        native._K.pool_bn_bwd_apply, native._K.conv_wgrad_stem_dz = c_apply, c_dz
+        for fuse in (False, True):
+            native._FUSE_STEM_WGRAD = fuse
+            stem = m.stem
+            for p in stem.parameters():
+                p.grad = None
+            y = stem(x, pool=True)
+            y.backward(dy)
+            torch.cuda.synchronize()
+            grads.append([p.grad.clone() for p in stem.parameters()])
+            assert calls == ({"apply": 1, "dz": 0} if not fuse else {"apply": 1, "dz": 1}), calls
+    finally:
+        native._FUSE_STEM_WGRAD = True
+        native._K.pool_bn_bwd_apply, native._K.conv_wgrad_stem_dz = o_apply, o_dz
+    assert len(grads[0]) == len(grads[1]) >= 3
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
 def test_lazy_x3_never_stores_stage0_c3_output_bit_identical():
     """the stage-0 identity blocks' c3 output (x3, [M, 256]) is never written --
     the c3 GEMM runs NOST (statistics only), the residual BN's apply recomputes x3 in a stream
